@@ -1,0 +1,284 @@
+// TEST INFRASTRUCTURE — parity oracle, never linked into the product library.
+//
+// Flat C entry points of the oracle for ctypes (tests/ and bench.py's cpu_baseline leg only).
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+#include <atomic>
+#include "glibc_rand.h"
+#include "pnp_oracle.h"
+#include "sim3_oracle.h"
+
+using namespace rsc_oracle;
+
+extern "C" {
+
+// ---- RNG ----
+void ora_glibc_rand(uint32_t seed, int n, int32_t* out) {
+    GlibcRand g(seed);
+    for (int i = 0; i < n; ++i) out[i] = g.rand();
+}
+
+// Sample indices of `hyps` consecutive hypotheses of `min_set` swap-remove draws over N items
+// (PnPsolver.cpp:125-138 / Sim3Solver.cpp:136-149).
+void ora_sample_stream(uint32_t seed, int N, int min_set, int hyps, int32_t* out) {
+    GlibcRand g(seed);
+    std::vector<int32_t> all(N);
+    for (int i = 0; i < N; ++i) all[i] = i;
+    for (int h = 0; h < hyps; ++h) {
+        std::vector<int32_t> av = all;
+        for (int i = 0; i < min_set; ++i) {
+            int randi = g.random_int(0, (int)av.size() - 1);
+            out[h * min_set + i] = av[randi];
+            av[randi] = av.back();
+            av.pop_back();
+        }
+    }
+}
+
+// ---- PnP ----
+void* ora_pnp_create(int n, int n_points, const float* p2d, const float* p3dw, const float* sigma2,
+                     const int32_t* kp_index, float fx, float fy, float cx, float cy, uint32_t seed) {
+    return new PnPOracle(n, n_points, p2d, p3dw, sigma2, kp_index, fx, fy, cx, cy, seed);
+}
+void ora_pnp_destroy(void* h) { delete static_cast<PnPOracle*>(h); }
+void ora_pnp_set_params(void* h, double prob, int min_inliers, int max_its, int min_set, float eps, float th2) {
+    static_cast<PnPOracle*>(h)->SetRansacParameters(prob, min_inliers, max_its, min_set, eps, th2);
+}
+// Returns iterate()'s bool; *mask_len = vbInliers.size() (0 when the reference clears it).
+int ora_pnp_iterate(void* h, int n_its, int* no_more, uint8_t* inliers, int* mask_len, int* n_inliers, float* T) {
+    std::vector<uint8_t> v;
+    bool nm = false;
+    int ni = 0;
+    bool ok = static_cast<PnPOracle*>(h)->iterate(n_its, nm, v, ni, T);
+    *no_more = nm;
+    *n_inliers = ni;
+    *mask_len = (int)v.size();
+    if (!v.empty()) std::memcpy(inliers, v.data(), v.size());
+    return ok;
+}
+void ora_pnp_info(void* h, int* out) {
+    auto* s = static_cast<PnPOracle*>(h);
+    out[0] = s->iterations();
+    out[1] = s->max_iterations();
+    out[2] = s->min_inliers();
+    out[3] = s->best_inliers();
+    out[4] = s->max_rows();
+}
+void ora_pnp_max_error(void* h, float* out) {
+    auto* s = static_cast<PnPOracle*>(h);
+    std::memcpy(out, s->max_error().data(), s->max_error().size() * sizeof(float));
+}
+double ora_pnp_compute_pose(void* h, const int* idx, int n, float* R, float* t) {
+    return static_cast<PnPOracle*>(h)->compute_pose_public(idx, n, R, t);
+}
+int ora_pnp_check_inliers(void* h, const float* R, const float* t, uint8_t* inl) {
+    std::vector<uint8_t> v;
+    int c = 0;
+    static_cast<PnPOracle*>(h)->check_inliers_public(R, t, v, c);
+    std::memcpy(inl, v.data(), v.size());
+    return c;
+}
+// Trace: per hypothesis {sample[8], n_inliers, refine_called, refine_inliers, refine_ok} ints and
+// {R[9], t[3]} floats.  Call with enable=1 before iterate; fetch with ora_pnp_trace_get.
+void ora_pnp_trace_enable(void* h) {
+    auto* s = static_cast<PnPOracle*>(h);
+    if (!s->trace) s->trace = new std::vector<PnPTrace>();
+}
+int ora_pnp_trace_get(void* h, int cap, int32_t* ints, float* floats) {
+    auto* s = static_cast<PnPOracle*>(h);
+    if (!s->trace) return 0;
+    int n = (int)s->trace->size();
+    for (int i = 0; i < n && i < cap; ++i) {
+        const PnPTrace& t = (*s->trace)[i];
+        for (int k = 0; k < 8; ++k) ints[12 * i + k] = t.sample[k];
+        ints[12 * i + 8] = t.n_inliers;
+        ints[12 * i + 9] = t.refine_called;
+        ints[12 * i + 10] = t.refine_inliers;
+        ints[12 * i + 11] = t.refine_ok;
+        for (int k = 0; k < 9; ++k) floats[12 * i + k] = t.R[k];
+        for (int k = 0; k < 3; ++k) floats[12 * i + 9 + k] = t.t[k];
+    }
+    return n;
+}
+
+// CPU baseline / batch reference: C independent problems, problem c = rows [off[c], off[c]+n[c]) of
+// the packed arrays; each builds a PnPsolver, SetRansacParameters(params), then iterate(n_its)
+// once, on `nthreads` host threads (candidates are independent, Tracking.cpp:1239-1334 runs them
+// sequentially on one thread).  Results per problem: ok, no_more, n_inliers, iterations, T[16].
+void ora_pnp_run_batch(int C, const int32_t* n, const int64_t* off, const float* p2d, const float* p3dw,
+                       const float* sigma2, float fx, float fy, float cx, float cy, const uint32_t* seeds,
+                       double prob, int min_inliers, int max_its, int min_set, float eps, float th2, int n_its,
+                       int nthreads, int32_t* out_i4, float* out_T, uint8_t* out_mask /* nullable, sum n */) {
+    std::atomic<int> next(0);
+    auto worker = [&]() {
+        for (;;) {
+            int c = next.fetch_add(1);
+            if (c >= C) break;
+            const int64_t o = off[c];
+            std::vector<int32_t> kp(n[c]);
+            for (int i = 0; i < n[c]; ++i) kp[i] = i;
+            PnPOracle s(n[c], n[c], p2d + 2 * o, p3dw + 3 * o, sigma2 + o, kp.data(), fx, fy, cx, cy, seeds[c]);
+            s.SetRansacParameters(prob, min_inliers, max_its, min_set, eps, th2);
+            std::vector<uint8_t> v;
+            bool nm = false;
+            int ni = 0;
+            float T[16];
+            for (int k = 0; k < 16; ++k) T[k] = 0.f;
+            bool ok = s.iterate(n_its, nm, v, ni, T);
+            out_i4[4 * c + 0] = ok;
+            out_i4[4 * c + 1] = nm;
+            out_i4[4 * c + 2] = ni;
+            out_i4[4 * c + 3] = s.iterations();
+            std::memcpy(out_T + 16 * c, T, sizeof(T));
+            if (out_mask) {
+                if (v.empty()) std::memset(out_mask + o, 0, n[c]);
+                else std::memcpy(out_mask + o, v.data(), n[c]);
+            }
+        }
+    };
+    if (nthreads <= 1) {
+        worker();
+    } else {
+        std::vector<std::thread> th;
+        for (int i = 0; i < nthreads; ++i) th.emplace_back(worker);
+        for (auto& t : th) t.join();
+    }
+}
+
+// ---- Sim3 ----
+void* ora_sim3_create(int n1, const uint8_t* valid, const float* Xw1, const float* Xw2, const float* s1,
+                      const float* s2, const float* R1, const float* t1, const float* R2, const float* t2,
+                      const float* K1, const float* K2, uint32_t seed) {
+    Sim3Input in;
+    in.n1 = n1; in.valid = valid; in.Xw1 = Xw1; in.Xw2 = Xw2; in.sigma2_1 = s1; in.sigma2_2 = s2;
+    std::memcpy(in.R1, R1, 9 * 4); std::memcpy(in.t1, t1, 12);
+    std::memcpy(in.R2, R2, 9 * 4); std::memcpy(in.t2, t2, 12);
+    std::memcpy(in.K1, K1, 16); std::memcpy(in.K2, K2, 16);
+    return new Sim3Oracle(in, seed);
+}
+void ora_sim3_destroy(void* h) { delete static_cast<Sim3Oracle*>(h); }
+void ora_sim3_set_params(void* h, double prob, int min_inliers, int max_its) {
+    static_cast<Sim3Oracle*>(h)->SetRansacParameters(prob, min_inliers, max_its);
+}
+int ora_sim3_n(void* h) { return static_cast<Sim3Oracle*>(h)->N; }
+// Prepared arrays: X1c[N][3], X2c[N][3], P1im1[N][2], P2im2[N][2], maxErr1/2 (as uint64), indices.
+void ora_sim3_prepared(void* h, float* X1c, float* X2c, float* P1, float* P2, uint64_t* e1, uint64_t* e2,
+                       int32_t* idx) {
+    auto* s = static_cast<Sim3Oracle*>(h);
+    const int N = s->N;
+    std::memcpy(X1c, s->mvX3Dc1.data(), 12 * N);
+    std::memcpy(X2c, s->mvX3Dc2.data(), 12 * N);
+    std::memcpy(P1, s->mvP1im1.data(), 8 * N);
+    std::memcpy(P2, s->mvP2im2.data(), 8 * N);
+    std::memcpy(e1, s->mvnMaxError1.data(), 8 * N);
+    std::memcpy(e2, s->mvnMaxError2.data(), 8 * N);
+    std::memcpy(idx, s->mvnIndices1.data(), 4 * N);
+}
+int ora_sim3_iterate(void* h, int n_its, int* no_more, uint8_t* inliers, int* n_inliers) {
+    std::vector<uint8_t> v;
+    bool nm = false;
+    int ni = 0;
+    auto* s = static_cast<Sim3Oracle*>(h);
+    bool ok = s->iterate(n_its, nm, v, ni);
+    *no_more = nm;
+    *n_inliers = ni;
+    std::memcpy(inliers, v.data(), v.size());
+    return ok;
+}
+void ora_sim3_estimate(void* h, float* R, float* t) {
+    auto* s = static_cast<Sim3Oracle*>(h);
+    s->GetEstimatedRotation(R);
+    s->GetEstimatedTranslation(t);
+}
+void ora_sim3_info(void* h, int* out) {
+    auto* s = static_cast<Sim3Oracle*>(h);
+    out[0] = s->iterations();
+    out[1] = s->max_iterations();
+    out[2] = s->N;
+}
+void ora_sim3_compute(void* h, const int* idx, float* R, float* t) {
+    static_cast<Sim3Oracle*>(h)->compute_sim3_public(idx, R, t);
+}
+int ora_sim3_check_inliers(void* h, const float* R, const float* t, uint8_t* inl) {
+    std::vector<uint8_t> v;
+    int c = static_cast<Sim3Oracle*>(h)->check_inliers_public(R, t, v);
+    std::memcpy(inl, v.data(), v.size());
+    return c;
+}
+void ora_sim3_trace_enable(void* h) {
+    auto* s = static_cast<Sim3Oracle*>(h);
+    if (!s->trace) s->trace = new std::vector<Sim3Trace>();
+}
+int ora_sim3_trace_get(void* h, int cap, int32_t* ints, float* floats) {
+    auto* s = static_cast<Sim3Oracle*>(h);
+    if (!s->trace) return 0;
+    int n = (int)s->trace->size();
+    for (int i = 0; i < n && i < cap; ++i) {
+        const Sim3Trace& t = (*s->trace)[i];
+        for (int k = 0; k < 3; ++k) ints[4 * i + k] = t.sample[k];
+        ints[4 * i + 3] = t.n_inliers;
+        for (int k = 0; k < 9; ++k) floats[12 * i + k] = t.R[k];
+        for (int k = 0; k < 3; ++k) floats[12 * i + 9 + k] = t.t[k];
+    }
+    return n;
+}
+
+// CPU baseline for Sim3 on prepared arrays (the per-pair solver after construction):
+// each problem runs SetRansacParameters(prob,minInl,maxIts) + iterate(n_its).
+void ora_sim3_run_prepared_batch(int C, const int32_t* n, const int64_t* off, const float* X1c,
+                                 const float* X2c, const float* P1, const float* P2, const uint64_t* e1,
+                                 const uint64_t* e2, const float* K1, const float* K2, const uint32_t* seeds,
+                                 double prob, int min_inliers, int max_its, int n_its, int nthreads,
+                                 int32_t* out_i4, float* out_Rt) {
+    std::atomic<int> next(0);
+    auto worker = [&]() {
+        for (;;) {
+            int c = next.fetch_add(1);
+            if (c >= C) break;
+            const int64_t o = off[c];
+            const int nc = n[c];
+            // Rebuild a solver whose ctor output equals the prepared arrays: identity poses and
+            // camera-frame points as "world" points reproduce X3Dc exactly (R*X + 0 with R = I is
+            // exact in float), thresholds are fed back through sigma^2 such that size_t(9.210*s2)
+            // would differ, so they are installed directly below.
+            std::vector<uint8_t> valid(nc, 1);
+            std::vector<float> s2(nc, 1.f);
+            Sim3Input in;
+            in.n1 = nc; in.valid = valid.data(); in.Xw1 = X1c + 3 * o; in.Xw2 = X2c + 3 * o;
+            in.sigma2_1 = s2.data(); in.sigma2_2 = s2.data();
+            const float I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, z[3] = {0, 0, 0};
+            std::memcpy(in.R1, I, 36); std::memcpy(in.R2, I, 36);
+            std::memcpy(in.t1, z, 12); std::memcpy(in.t2, z, 12);
+            std::memcpy(in.K1, K1, 16); std::memcpy(in.K2, K2, 16);
+            Sim3Oracle s(in, seeds[c]);
+            for (int i = 0; i < nc; ++i) { s.mvnMaxError1[i] = e1[o + i]; s.mvnMaxError2[i] = e2[o + i]; }
+            std::memcpy(s.mvP1im1.data(), P1 + 2 * o, 8 * nc);
+            std::memcpy(s.mvP2im2.data(), P2 + 2 * o, 8 * nc);
+            s.SetRansacParameters(prob, min_inliers, max_its);
+            std::vector<uint8_t> v;
+            bool nm = false;
+            int ni = 0;
+            bool ok = s.iterate(n_its, nm, v, ni);
+            out_i4[4 * c + 0] = ok;
+            out_i4[4 * c + 1] = nm;
+            out_i4[4 * c + 2] = ni;
+            out_i4[4 * c + 3] = s.iterations();
+            float R[9], t[3];
+            s.GetEstimatedRotation(R);
+            s.GetEstimatedTranslation(t);
+            std::memcpy(out_Rt + 12 * c, R, 36);
+            std::memcpy(out_Rt + 12 * c + 9, t, 12);
+        }
+    };
+    if (nthreads <= 1) {
+        worker();
+    } else {
+        std::vector<std::thread> th;
+        for (int i = 0; i < nthreads; ++i) th.emplace_back(worker);
+        for (auto& t : th) t.join();
+    }
+}
+
+}  // extern "C"

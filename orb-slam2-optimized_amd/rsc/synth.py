@@ -1,0 +1,175 @@
+"""Synthetic relocalization / loop-closure scenes shaped like the reference's EuRoC runs.
+
+No dataset is fetched (there is no network): every scene is generated from a seeded
+``numpy.random.Generator`` (SURVEY.md §8(d) "Synthetic inputs").
+
+Constants follow the reference's configuration:
+  * EuRoC intrinsics fx=fy=435.2046959714599, cx=367.4517211914062, cy=252.2008514404297,
+    image 752x480 (Examples/Stereo/EuRoC.yaml:8-11,18-19).  ``Frame::fx`` etc. are *static float*
+    members (include/Frame.hpp:102-105), so the values are rounded to float32 before the solvers
+    widen them to double (PnPsolver.hpp:71).
+  * ORB pyramid: 8 levels, scale factor 1.2f, sigma^2(L) = scale(L)^2 computed in float
+    (src/ORBextractor.cpp:353-360); keypoints per level follow the geometric per-level budget
+    (src/ORBextractor.cpp:372-383).
+"""
+from __future__ import annotations
+
+import dataclasses
+import numpy as np
+
+FX = np.float32(435.2046959714599)
+FY = np.float32(435.2046959714599)
+CX = np.float32(367.4517211914062)
+CY = np.float32(252.2008514404297)
+WIDTH, HEIGHT = 752, 480
+N_LEVELS = 8
+SCALE_FACTOR = np.float32(1.2)
+
+
+def level_sigma2() -> np.ndarray:
+    """mvLevelSigma2 exactly as ORBextractor computes it (float32 products)."""
+    sf = [np.float32(1.0)]
+    for _ in range(1, N_LEVELS):
+        sf.append(np.float32(sf[-1] * SCALE_FACTOR))
+    return np.array([np.float32(s * s) for s in sf], dtype=np.float32)
+
+
+def level_probabilities(nfeatures: int = 1200) -> np.ndarray:
+    factor = 1.0 / float(SCALE_FACTOR)
+    n_desired = nfeatures * (1 - factor) / (1 - factor ** N_LEVELS)
+    per = []
+    for _ in range(N_LEVELS - 1):
+        per.append(round(n_desired))
+        n_desired *= factor
+    per.append(max(nfeatures - sum(per), 0))
+    p = np.array(per, dtype=np.float64)
+    return p / p.sum()
+
+
+def random_rotation(rng: np.random.Generator, max_angle: float = np.pi) -> np.ndarray:
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    ang = rng.uniform(-max_angle, max_angle)
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * (K @ K)
+
+
+@dataclasses.dataclass
+class PnPScene:
+    """Compacted PnPsolver inputs (PnPsolver.cpp:22-44) for one relocalization candidate."""
+    p2d: np.ndarray      # float32 [n,2]  mvKeysUn[i].pt
+    p3dw: np.ndarray     # float32 [n,3]  MapPoint::GetWorldPos()
+    sigma2: np.ndarray   # float32 [n]    mvLevelSigma2[octave]
+    kp_index: np.ndarray  # int32 [n]     index of the keypoint in the Frame
+    n_points: int        # F.N (size of the output inlier vector)
+    R_true: np.ndarray   # float64 [3,3] Tcw rotation
+    t_true: np.ndarray   # float64 [3]
+    inlier_true: np.ndarray  # bool [n]
+    fx: np.float32 = FX
+    fy: np.float32 = FY
+    cx: np.float32 = CX
+    cy: np.float32 = CY
+
+    @property
+    def n(self) -> int:
+        return int(self.p2d.shape[0])
+
+
+def make_pnp_scene(rng: np.random.Generator, n: int, inlier_ratio: float, noise: bool = True,
+                   n_points: int | None = None, depth=(0.5, 8.0)) -> PnPScene:
+    """Random Tcw, inliers = noisy projections of frustum points, outliers = uniform pixels."""
+    R = random_rotation(rng)
+    t = rng.uniform(-2.0, 2.0, size=3)
+    u = rng.uniform(0, WIDTH, size=n)
+    v = rng.uniform(0, HEIGHT, size=n)
+    d = rng.uniform(depth[0], depth[1], size=n)
+    fx, fy, cx, cy = float(FX), float(FY), float(CX), float(CY)
+    Xc = np.stack([(u - cx) / fx * d, (v - cy) / fy * d, d], axis=1)
+    Xw = (Xc - t) @ R  # R^T (Xc - t)
+    levels = rng.choice(N_LEVELS, size=n, p=level_probabilities())
+    s2 = level_sigma2()[levels]
+    n_in = int(round(inlier_ratio * n))
+    inl = np.zeros(n, dtype=bool)
+    inl[rng.permutation(n)[:n_in]] = True
+    obs_u = u.copy()
+    obs_v = v.copy()
+    if noise:
+        sig = np.sqrt(s2.astype(np.float64))
+        obs_u[inl] += rng.normal(size=n_in) * sig[inl]
+        obs_v[inl] += rng.normal(size=n_in) * sig[inl]
+    n_out = n - n_in
+    obs_u[~inl] = rng.uniform(0, WIDTH, size=n_out)
+    obs_v[~inl] = rng.uniform(0, HEIGHT, size=n_out)
+    if n_points is None:
+        n_points = n
+    kp = np.sort(rng.choice(n_points, size=n, replace=False)).astype(np.int32) if n_points > n \
+        else np.arange(n, dtype=np.int32)
+    return PnPScene(p2d=np.stack([obs_u, obs_v], 1).astype(np.float32),
+                    p3dw=Xw.astype(np.float32), sigma2=s2.astype(np.float32), kp_index=kp,
+                    n_points=int(n_points), R_true=R, t_true=t, inlier_true=inl)
+
+
+@dataclasses.dataclass
+class Sim3Pair:
+    """Raw Sim3Solver constructor inputs (Sim3Solver.cpp:6-85) for one keyframe pair."""
+    valid: np.ndarray    # uint8 [n1]
+    Xw1: np.ndarray      # float32 [n1,3]  pMP1->GetWorldPos()
+    Xw2: np.ndarray      # float32 [n1,3]  pMP2->GetWorldPos()
+    sigma2_1: np.ndarray  # float32 [n1]
+    sigma2_2: np.ndarray  # float32 [n1]
+    R1: np.ndarray       # float32 [3,3]  KF1 Rcw
+    t1: np.ndarray       # float32 [3]
+    R2: np.ndarray
+    t2: np.ndarray
+    K1: np.ndarray       # float32 [4] fx, fy, cx, cy
+    K2: np.ndarray
+    inlier_true: np.ndarray  # bool [n1]
+
+    @property
+    def n1(self) -> int:
+        return int(self.valid.shape[0])
+
+
+def make_sim3_pair(rng: np.random.Generator, n1: int, n_inliers: int, invalid_frac: float = 0.0,
+                   noise3d: float = 0.01) -> Sim3Pair:
+    """Two keyframes seeing the same points; map 2 carries a rigid loop drift (Rd, td).
+
+    Physical point P: Xw1 = P (+noise), Xw2 = Rd P + td (+noise).  KF1: Xc1 = R1 P + t1.
+    KF2 is displaced by (Rrel, trel) from KF1, expressed in map-2 coordinates, so that
+    Xc2 = Rrel Xc1 + trel for inliers.  Outliers of map 2 are unrelated points in front of KF2.
+    """
+    R1 = random_rotation(rng, 0.3)
+    t1 = rng.uniform(-1, 1, size=3)
+    Rd = random_rotation(rng, 0.2)
+    td = rng.uniform(-0.5, 0.5, size=3)
+    Rrel = random_rotation(rng, 0.15)
+    trel = rng.uniform(-0.3, 0.3, size=3)
+    R2 = Rrel @ R1 @ Rd.T
+    t2 = Rrel @ (t1 - R1 @ Rd.T @ td) + trel
+    fx, fy, cx, cy = float(FX), float(FY), float(CX), float(CY)
+    u = rng.uniform(0, WIDTH, size=n1)
+    v = rng.uniform(0, HEIGHT, size=n1)
+    d = rng.uniform(1.0, 8.0, size=n1)
+    Xc1 = np.stack([(u - cx) / fx * d, (v - cy) / fy * d, d], axis=1)
+    P = (Xc1 - t1) @ R1
+    Xw1 = P + rng.normal(size=P.shape) * noise3d
+    Xw2 = P @ Rd.T + td + rng.normal(size=P.shape) * noise3d
+    inl = np.zeros(n1, dtype=bool)
+    inl[rng.permutation(n1)[:n_inliers]] = True
+    nout = int((~inl).sum())
+    uo = rng.uniform(0, WIDTH, size=nout)
+    vo = rng.uniform(0, HEIGHT, size=nout)
+    do = rng.uniform(1.0, 8.0, size=nout)
+    Xc2o = np.stack([(uo - cx) / fx * do, (vo - cy) / fy * do, do], axis=1)
+    Xw2[~inl] = (Xc2o - t2) @ R2
+    levels1 = rng.choice(N_LEVELS, size=n1, p=level_probabilities())
+    levels2 = rng.choice(N_LEVELS, size=n1, p=level_probabilities())
+    s2 = level_sigma2()
+    valid = np.ones(n1, dtype=np.uint8)
+    if invalid_frac > 0:
+        valid[rng.random(n1) < invalid_frac] = 0
+    K = np.array([FX, FY, CX, CY], dtype=np.float32)
+    return Sim3Pair(valid=valid, Xw1=Xw1.astype(np.float32), Xw2=Xw2.astype(np.float32),
+                    sigma2_1=s2[levels1].astype(np.float32), sigma2_2=s2[levels2].astype(np.float32),
+                    R1=R1.astype(np.float32), t1=t1.astype(np.float32), R2=R2.astype(np.float32),
+                    t2=t2.astype(np.float32), K1=K, K2=K.copy(), inlier_true=inl)

@@ -1,0 +1,216 @@
+"""ctypes binding of the parity oracle (oracle/build/librsc_oracle.so).
+
+TEST INFRASTRUCTURE: imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg.  The oracle is the checker, never the thing measured or shipped.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "build", "librsc_oracle.so")
+
+_lib = None
+
+f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+
+
+def build_oracle() -> str:
+    if not os.path.exists(LIB_PATH) or _stale():
+        import subprocess
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    return LIB_PATH
+
+
+def _stale() -> bool:
+    src_dir = os.path.join(ROOT, "oracle")
+    t = os.path.getmtime(LIB_PATH)
+    for f in os.listdir(src_dir):
+        if f.endswith((".cpp", ".h")) and os.path.getmtime(os.path.join(src_dir, f)) > t:
+            return True
+    return False
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build_oracle()
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    L.ora_glibc_rand.argtypes = [C.c_uint32, C.c_int, i32p]
+    L.ora_sample_stream.argtypes = [C.c_uint32, C.c_int, C.c_int, C.c_int, i32p]
+    L.ora_pnp_create.restype = vp
+    L.ora_pnp_create.argtypes = [C.c_int, C.c_int, f32p, f32p, f32p, i32p, C.c_float, C.c_float, C.c_float,
+                                 C.c_float, C.c_uint32]
+    L.ora_pnp_destroy.argtypes = [vp]
+    L.ora_pnp_set_params.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
+    L.ora_pnp_iterate.argtypes = [vp, C.c_int, C.POINTER(C.c_int), u8p, C.POINTER(C.c_int), C.POINTER(C.c_int), f32p]
+    L.ora_pnp_info.argtypes = [vp, i32p]
+    L.ora_pnp_max_error.argtypes = [vp, f32p]
+    L.ora_pnp_compute_pose.restype = C.c_double
+    L.ora_pnp_compute_pose.argtypes = [vp, i32p, C.c_int, f32p, f32p]
+    L.ora_pnp_check_inliers.argtypes = [vp, f32p, f32p, u8p]
+    L.ora_pnp_trace_enable.argtypes = [vp]
+    L.ora_pnp_trace_get.argtypes = [vp, C.c_int, i32p, f32p]
+    L.ora_pnp_run_batch.argtypes = [C.c_int, i32p, i64p, f32p, f32p, f32p, C.c_float, C.c_float, C.c_float,
+                                    C.c_float, u32p, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
+                                    C.c_int, C.c_int, i32p, f32p, C.c_void_p]
+    L.ora_sim3_create.restype = vp
+    L.ora_sim3_create.argtypes = [C.c_int, u8p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p,
+                                  C.c_uint32]
+    L.ora_sim3_destroy.argtypes = [vp]
+    L.ora_sim3_set_params.argtypes = [vp, C.c_double, C.c_int, C.c_int]
+    L.ora_sim3_n.argtypes = [vp]
+    L.ora_sim3_prepared.argtypes = [vp, f32p, f32p, f32p, f32p, u64p, u64p, i32p]
+    L.ora_sim3_iterate.argtypes = [vp, C.c_int, C.POINTER(C.c_int), u8p, C.POINTER(C.c_int)]
+    L.ora_sim3_estimate.argtypes = [vp, f32p, f32p]
+    L.ora_sim3_info.argtypes = [vp, i32p]
+    L.ora_sim3_compute.argtypes = [vp, i32p, f32p, f32p]
+    L.ora_sim3_check_inliers.argtypes = [vp, f32p, f32p, u8p]
+    L.ora_sim3_trace_enable.argtypes = [vp]
+    L.ora_sim3_trace_get.argtypes = [vp, C.c_int, i32p, f32p]
+    L.ora_sim3_run_prepared_batch.argtypes = [C.c_int, i32p, i64p, f32p, f32p, f32p, f32p, u64p, u64p, f32p, f32p,
+                                              u32p, C.c_double, C.c_int, C.c_int, C.c_int, C.c_int, i32p, f32p]
+    _lib = L
+    return L
+
+
+def glibc_rand(seed: int, n: int) -> np.ndarray:
+    out = np.zeros(n, dtype=np.int32)
+    lib().ora_glibc_rand(seed, n, out)
+    return out
+
+
+def sample_stream(seed: int, N: int, min_set: int, hyps: int) -> np.ndarray:
+    out = np.zeros(hyps * min_set, dtype=np.int32)
+    lib().ora_sample_stream(seed, N, min_set, hyps, out)
+    return out.reshape(hyps, min_set)
+
+
+class OraclePnP:
+    """PnPsolver restatement: same ctor/SetRansacParameters/iterate/find semantics."""
+
+    def __init__(self, scene, seed: int = 1):
+        self._keep = (np.ascontiguousarray(scene.p2d, np.float32), np.ascontiguousarray(scene.p3dw, np.float32),
+                      np.ascontiguousarray(scene.sigma2, np.float32), np.ascontiguousarray(scene.kp_index, np.int32))
+        self.n_points = int(scene.n_points)
+        self.h = lib().ora_pnp_create(scene.n, self.n_points, *self._keep, scene.fx, scene.fy, scene.cx,
+                                      scene.cy, seed)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ora_pnp_destroy(self.h)
+            self.h = None
+
+    def set_ransac_parameters(self, probability=0.99, min_inliers=8, max_iterations=300, min_set=4,
+                              epsilon=0.4, th2=5.991):
+        lib().ora_pnp_set_params(self.h, probability, min_inliers, max_iterations, min_set, epsilon, th2)
+
+    def iterate(self, n_iterations: int):
+        nm, ml, ni = C.c_int(), C.c_int(), C.c_int()
+        mask = np.zeros(max(self.n_points, 1), dtype=np.uint8)
+        T = np.zeros(16, dtype=np.float32)
+        ok = lib().ora_pnp_iterate(self.h, n_iterations, C.byref(nm), mask, C.byref(ml), C.byref(ni), T)
+        return dict(ok=bool(ok), no_more=bool(nm.value), n_inliers=ni.value,
+                    inliers=mask[:ml.value].astype(bool), T=T.reshape(4, 4))
+
+    def info(self):
+        out = np.zeros(5, dtype=np.int32)
+        lib().ora_pnp_info(self.h, out)
+        return dict(iterations=int(out[0]), max_iterations=int(out[1]), min_inliers=int(out[2]),
+                    best_inliers=int(out[3]), max_rows=int(out[4]))
+
+    def max_error(self, n):
+        out = np.zeros(n, dtype=np.float32)
+        lib().ora_pnp_max_error(self.h, out)
+        return out
+
+    def compute_pose(self, idx):
+        idx = np.ascontiguousarray(idx, np.int32)
+        R = np.zeros(9, np.float32)
+        t = np.zeros(3, np.float32)
+        e = lib().ora_pnp_compute_pose(self.h, idx, len(idx), R, t)
+        return R.reshape(3, 3), t, e
+
+    def check_inliers(self, R, t, n):
+        inl = np.zeros(n, np.uint8)
+        c = lib().ora_pnp_check_inliers(self.h, np.ascontiguousarray(R, np.float32).ravel(),
+                                        np.ascontiguousarray(t, np.float32), inl)
+        return c, inl.astype(bool)
+
+    def enable_trace(self):
+        lib().ora_pnp_trace_enable(self.h)
+
+    def trace(self, cap=100000):
+        ints = np.zeros((cap, 12), np.int32)
+        fl = np.zeros((cap, 12), np.float32)
+        n = lib().ora_pnp_trace_get(self.h, cap, ints, fl)
+        return ints[:n], fl[:n]
+
+
+class OracleSim3:
+    def __init__(self, pair, seed: int = 1):
+        self._keep = [np.ascontiguousarray(a) for a in (
+            pair.valid.astype(np.uint8), pair.Xw1.astype(np.float32), pair.Xw2.astype(np.float32),
+            pair.sigma2_1.astype(np.float32), pair.sigma2_2.astype(np.float32),
+            pair.R1.astype(np.float32).ravel(), pair.t1.astype(np.float32), pair.R2.astype(np.float32).ravel(),
+            pair.t2.astype(np.float32), pair.K1.astype(np.float32), pair.K2.astype(np.float32))]
+        self.n1 = pair.n1
+        self.h = lib().ora_sim3_create(self.n1, *self._keep, seed)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ora_sim3_destroy(self.h)
+            self.h = None
+
+    @property
+    def N(self):
+        return lib().ora_sim3_n(self.h)
+
+    def prepared(self):
+        N = self.N
+        X1 = np.zeros((N, 3), np.float32); X2 = np.zeros((N, 3), np.float32)
+        P1 = np.zeros((N, 2), np.float32); P2 = np.zeros((N, 2), np.float32)
+        e1 = np.zeros(N, np.uint64); e2 = np.zeros(N, np.uint64); idx = np.zeros(N, np.int32)
+        lib().ora_sim3_prepared(self.h, X1, X2, P1, P2, e1, e2, idx)
+        return dict(X1c=X1, X2c=X2, P1im1=P1, P2im2=P2, maxerr1=e1, maxerr2=e2, indices=idx)
+
+    def set_ransac_parameters(self, probability=0.99, min_inliers=6, max_iterations=300):
+        lib().ora_sim3_set_params(self.h, probability, min_inliers, max_iterations)
+
+    def iterate(self, n_iterations: int):
+        nm, ni = C.c_int(), C.c_int()
+        mask = np.zeros(max(self.n1, 1), np.uint8)
+        ok = lib().ora_sim3_iterate(self.h, n_iterations, C.byref(nm), mask, C.byref(ni))
+        R = np.zeros(9, np.float32); t = np.zeros(3, np.float32)
+        lib().ora_sim3_estimate(self.h, R, t)
+        return dict(ok=bool(ok), no_more=bool(nm.value), n_inliers=ni.value, inliers=mask[:self.n1].astype(bool),
+                    R=R.reshape(3, 3), t=t)
+
+    def info(self):
+        out = np.zeros(3, np.int32)
+        lib().ora_sim3_info(self.h, out)
+        return dict(iterations=int(out[0]), max_iterations=int(out[1]), N=int(out[2]))
+
+    def compute(self, idx):
+        R = np.zeros(9, np.float32); t = np.zeros(3, np.float32)
+        lib().ora_sim3_compute(self.h, np.ascontiguousarray(idx, np.int32), R, t)
+        return R.reshape(3, 3), t
+
+    def enable_trace(self):
+        lib().ora_sim3_trace_enable(self.h)
+
+    def trace(self, cap=100000):
+        ints = np.zeros((cap, 4), np.int32)
+        fl = np.zeros((cap, 12), np.float32)
+        n = lib().ora_sim3_trace_get(self.h, cap, ints, fl)
+        return ints[:n], fl[:n]
