@@ -1,0 +1,39 @@
+# Build of the MI355X RANSAC pose engine (gfx950).  `make` builds librsc.so (HIP kernels + C ABI),
+# the oracle (test infrastructure) and the host-emulation test library.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG = orb-slam2-optimized_amd
+CSRC = $(PKG)/csrc
+LIBDIR = $(PKG)/lib
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+           -fno-gpu-flush-denormals-to-zero -Wall -Wno-unused-function -Wno-unused-variable
+HDRS = include/rsc.h $(wildcard $(CSRC)/*.h)
+
+all: $(LIBDIR)/librsc.so oracle hostemu facade_test
+
+$(LIBDIR)/kernels.o: $(CSRC)/kernels.hip $(HDRS)
+	mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/rsc_api.o: $(CSRC)/rsc_api.cpp $(HDRS)
+	mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIBDIR)/librsc.so: $(LIBDIR)/kernels.o $(LIBDIR)/rsc_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
+
+facade_test: $(LIBDIR)/facade_test
+
+$(LIBDIR)/facade_test: tests/cpp/facade_test.cpp $(CSRC)/facade/*.hpp $(LIBDIR)/librsc.so
+	g++ -O2 -std=c++17 -Iinclude -I$(CSRC)/facade -o $@ tests/cpp/facade_test.cpp -L$(LIBDIR) -lrsc -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -s -C oracle
+
+hostemu:
+	$(MAKE) -s -C tests/hostemu
+
+clean:
+	rm -rf $(LIBDIR) oracle/build tests/hostemu/build
+
+.PHONY: all oracle hostemu facade_test clean

@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""Headline benchmark: RANSAC hypotheses/s (+ poses/s) of the relocalization EPnP batch.
+
+Workload (BASELINE.json configs[1]): per GPU, 64 relocalization
+candidates x 2000 correspondences, SetRansacParameters(0.99,10,300,4,0.5,5.991) (Tracking.cpp:1226)
+then iterate(300) on every candidate — 300 hypotheses each (Q1: '||' loop) in exhaustive mode
+(40% inliers, minInliers=1000 unreachable), i.e. 19,200 hypotheses per step, all candidates in one
+rsc_pnp_iterate_many call.  A "step" = reset every solver with a fresh rand() seed + the call above
+(sampling, EPnP solves, inlier scans, selection replay, result records).  With N GPUs (one process
+per GPU, torchrun) every rank runs its own 64-candidate batch (weak scaling) and the per-candidate
+result records are all-gathered over RCCL at the end of each step.
+
+The Sim3 loop-closure batch (config 3: 32 pairs x 1000 matches, iterate(300)) is measured in the
+same run and reported under "sim3".
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "orb-slam2-optimized_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+RELOC = (0.99, 10, 300, 4, 0.5, 5.991)
+LOOP = (0.99, 20, 300)
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--candidates", type=int, default=64)
+    p.add_argument("--corrs", type=int, default=2000)
+    p.add_argument("--iters", type=int, default=300)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-sim3", action="store_true")
+    return p.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local, dist
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def pnp_batch(rng, C, N, ratio):
+    from rsc import synth
+    return [synth.make_pnp_scene(rng, N, ratio) for _ in range(C)]
+
+
+def run_pnp(engine, ctx, scenes, args, dist, rank, world):
+    solvers = [engine.PnPSolver(ctx, sc, 1) for sc in scenes]
+    C = len(solvers)
+    gather = None
+    if dist is not None:
+        import torch
+        rec = torch.zeros(C, 20, dtype=torch.float32, device="cuda")
+        gather = (torch, rec, torch.zeros(world * C, 20, dtype=torch.float32, device="cuda"))
+
+    def step(s):
+        for c, sv in enumerate(solvers):
+            sv.reset(1 + c + C * (s + 1000 * rank))
+            sv.set_ransac_parameters(*RELOC)
+        outs = engine.pnp_iterate_many(solvers, args.iters, with_masks=False)
+        if gather is not None:
+            torch, rec, allrec = gather
+            h = np.zeros((C, 20), np.float32)
+            for i, o in enumerate(outs):
+                h[i, 0], h[i, 1], h[i, 2], h[i, 3] = o["ok"], o["no_more"], o["n_inliers"], o["iterations"]
+                h[i, 4:20] = o["T"].ravel()
+            rec.copy_(torch.from_numpy(h))
+            dist.all_gather_into_tensor(allrec, rec)  # RCCL over xGMI: winner records of all ranks
+            torch.cuda.synchronize()
+        return sum(o["iterations"] for o in outs), outs
+
+    for s in range(args.warmup):
+        step(s)
+    ctx.enable_timing(True)
+    solve_ms = scan_ms = 0.0
+    launches = 0
+    barrier(dist)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    hyps = 0
+    for s in range(args.steps):
+        n, outs = step(args.warmup + s)
+        hyps += n
+        tm = ctx.last_timing()
+        solve_ms += tm["solve_ms"]
+        scan_ms += tm["scan_ms"]
+        launches += tm["solve_launches"]
+    ctx.synchronize()
+    barrier(dist)
+    dt = time.perf_counter() - t0
+    ctx.enable_timing(False)
+    return dict(seconds=dt, hyps=hyps, problems=C * args.steps, solve_ms=solve_ms / max(launches, 1),
+                scan_ms=scan_ms / max(launches, 1), launches=launches, last=outs)
+
+
+def run_sim3(engine, ctx, rng, args):
+    from rsc import synth
+    pairs = [synth.make_sim3_pair(rng, 1000, 15) for _ in range(32)]
+    solvers = [engine.Sim3Solver(ctx, p, 1) for p in pairs]
+
+    def step(s):
+        for c, sv in enumerate(solvers):
+            sv.reset(1 + c + 32 * s)
+            sv.set_ransac_parameters(*LOOP)
+        outs = engine.sim3_iterate_many(solvers, args.iters, with_masks=False)
+        return sum(o["iterations"] for o in outs)
+
+    for s in range(args.warmup):
+        step(s)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    h = 0
+    for s in range(args.steps):
+        h += step(args.warmup + s)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    return dict(hyp_per_s=h / dt, ms_per_step=1e3 * dt / args.steps, hypotheses_per_step=h // args.steps,
+                pairs=32, correspondences=1000)
+
+
+def cpu_baseline(scenes, args):
+    """Oracle restatement (test infrastructure) of the same workload on ONE host core."""
+    import oracle_lib as ol
+    L = ol.lib()
+    C = len(scenes)
+    n = np.array([sc.n for sc in scenes], np.int32)
+    off = np.concatenate([[0], np.cumsum(n)[:-1]]).astype(np.int64)
+    p2d = np.ascontiguousarray(np.concatenate([sc.p2d for sc in scenes]), np.float32)
+    p3d = np.ascontiguousarray(np.concatenate([sc.p3dw for sc in scenes]), np.float32)
+    s2 = np.ascontiguousarray(np.concatenate([sc.sigma2 for sc in scenes]), np.float32)
+    out_i4 = np.zeros(4 * C, np.int32)
+    out_T = np.zeros(16 * C, np.float32)
+    sc0 = scenes[0]
+    hyps = 0
+    batches = 0
+    t0 = time.perf_counter()
+    while True:
+        seeds = (1 + np.arange(C) + C * batches).astype(np.uint32)
+        L.ora_pnp_run_batch(C, n, off, p2d, p3d, s2, sc0.fx, sc0.fy, sc0.cx, sc0.cy, seeds, *RELOC, args.iters,
+                            1, out_i4, out_T, None)
+        hyps += int(out_i4.reshape(C, 4)[:, 3].sum())
+        batches += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=hyps / dt, unit="hypotheses/s", cores=1, kind="port",
+                sample=f"{batches} full batches ({C} candidates x {sc0.n} corrs x iterate({args.iters})) "
+                       f"= {hyps} hypotheses in {dt:.1f} s, oracle restatement, 1 thread")
+
+
+def main():
+    args = parse()
+    world, rank, local, dist = dist_setup(args)
+    from rsc import engine
+    ctx = engine.Context(local)
+    rng = np.random.default_rng(20240 + rank)
+    scenes = pnp_batch(rng, args.candidates, args.corrs, 0.4)
+    r = run_pnp(engine, ctx, scenes, args, dist, rank, world)
+    # max over ranks of the timed region
+    dt = r["seconds"]
+    hyps_total = r["hyps"]
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt, float(r["hyps"])], dtype=torch.float64, device="cuda")
+        mx = t.clone()
+        dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        dt = float(mx[0])
+        hyps_total = int(t[1])
+    sim3 = None
+    if rank == 0 and not args.no_sim3:
+        sim3 = run_sim3(engine, ctx, np.random.default_rng(77), args)
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    value = hyps_total / dt
+    per_launch_hyps = args.candidates * args.iters
+    B_h = 24 * args.corrs  # PnP scan bytes per hypothesis (p3D 12 + p2D 8 + maxErr 4)
+    algo_bytes = per_launch_hyps * B_h
+    solve_s = r["solve_ms"] * 1e-3
+    scan_s = r["scan_ms"] * 1e-3
+    achieved = algo_bytes / (solve_s + scan_s) / 1e9 if solve_s + scan_s > 0 else 0.0
+    out = {
+        "metric": "RANSAC hypotheses/sec (EPnP relocalization batch, 2k corrs x 64 candidates per GPU)",
+        "value": round(value, 1),
+        "unit": "hypotheses/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * dt / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded EuRoC-shaped scenes; no dataset)",
+        "config": {"workload": "reloc_pnp: candidates x correspondences, iterate(300), exhaustive (40% inliers)",
+                   "candidates_per_gpu": args.candidates, "correspondences": args.corrs,
+                   "hypotheses_per_candidate": args.iters, "params": "SetRansacParameters(0.99,10,300,4,0.5,5.991)",
+                   "parallelism": f"candidates sharded, {world} rank(s), RCCL all-gather of result records"},
+        "poses_per_s": round(world * r["problems"] / dt, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel": "pnp_solve_kernel<4> + pnp_scan_kernel<8> (per launch)",
+                     "solve_ms_per_launch": round(r["solve_ms"], 4), "scan_ms_per_launch": round(r["scan_ms"], 4),
+                     "algorithmic_bytes_per_launch": algo_bytes},
+    }
+    if sim3 is not None:
+        out["sim3"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in sim3.items()}
+    if not args.no_cpu and world == 1:
+        out["cpu_baseline"] = cpu_baseline(scenes, args)
+        out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 1)
+        out["speedup_vs_cpu_1core"] = round(value / out["cpu_baseline"]["value"], 1)
+    print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

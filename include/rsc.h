@@ -1,0 +1,138 @@
+/*
+ * rsc.h — C ABI of the MI355X RANSAC pose engine (librsc.so).
+ *
+ * Drop-in boundary for the hot path of Luigi940260/orb-slam2-optimized: the geometric RANSAC
+ * solvers called by Tracking::Relocalization() and LoopClosing::ComputeSim3().  Every entry point
+ * below replaces one member of the reference classes (file:line of the reference cited per
+ * function); the C++ facade in orb-slam2-optimized_amd/csrc/facade/ re-exposes them with the
+ * reference's exact class signatures.  Plain pointers and sizes only; no torch / HIP types.
+ *
+ * Semantics are the reference's, including its quirks, with one
+ * documented contract change (H4): rand() is a per-solver glibc stream seeded with `seed`
+ * instead of the process-global stream.
+ *
+ * Status codes: 0 = ok, < 0 = error (see rsc_status_string).  The library fails loudly: when no
+ * HIP device is present, rsc_context_create returns RSC_ERR_NODEVICE; there is no CPU fallback.
+ */
+#ifndef RSC_H_
+#define RSC_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSC_OK 0
+#define RSC_ERR_ARG (-1)
+#define RSC_ERR_HIP (-2)
+#define RSC_ERR_OOM (-3)
+#define RSC_ERR_UNSUPPORTED (-4)
+#define RSC_ERR_NODEVICE (-5)
+
+typedef struct rsc_context rsc_context;
+typedef struct rsc_pnp rsc_pnp;
+typedef struct rsc_sim3 rsc_sim3;
+
+/* ---- library / context ------------------------------------------------------------------ */
+int rsc_version(void);
+const char* rsc_status_string(int status);
+/* One context per host thread (reference: the Tracking and LoopClosing threads each own their
+ * solvers, System.cpp:58-69).  Owns a HIP stream, the rand() jump table and work buffers. */
+int rsc_context_create(int device, rsc_context** out);
+void rsc_context_destroy(rsc_context* ctx);
+/* Use a caller-owned hipStream_t (e.g. torch's current stream) instead of the private one. */
+int rsc_context_set_stream(rsc_context* ctx, void* hip_stream);
+int rsc_context_synchronize(rsc_context* ctx);
+/* Per-kernel timing of the last iterate call, in milliseconds (HIP events on the context stream):
+ * out[0] = hypothesis-solve kernels, out[1] = inlier-scan kernels, out[2] = refine kernels,
+ * out[3] = number of solve launches, out[4] = hypotheses solved. */
+int rsc_context_last_timing(rsc_context* ctx, double out[5]);
+int rsc_context_enable_timing(rsc_context* ctx, int enable);
+
+/* ---- PnPsolver (include/PnPsolver.hpp:21-138, src/PnPsolver.cpp) ------------------------------ */
+typedef struct {
+    int32_t n;               /* compacted valid matches N (PnPsolver.cpp:22-44) */
+    int32_t n_points;        /* vpMapPointMatches.size(): length of the returned inlier vector */
+    const float* p2d;        /* [n][2] mvP2D = mvKeysUn[i].pt                       (:33) */
+    const float* p3dw;       /* [n][3] mvP3Dw = MapPoint::GetWorldPos()             (:36) */
+    const float* sigma2;     /* [n] mvSigma2 = mvLevelSigma2[kp.octave]             (:34) */
+    const int32_t* kp_index; /* [n] mvKeyPointIndices; NULL = identity               (:38) */
+    float fx, fy, cx, cy;    /* Frame::fx,fy,cx,cy (static float members, :47-50)       */
+} rsc_pnp_problem;
+
+typedef struct {
+    int32_t ok;         /* iterate()/find() return value */
+    int32_t no_more;    /* bNoMore */
+    int32_t n_inliers;  /* nInliers */
+    int32_t iterations; /* mnIterations after the call */
+    float T[16];        /* row-major Tcw; written only when ok (PnPsolver.cpp:166,185) */
+} rsc_pnp_result;
+
+/* PnPsolver::PnPsolver (PnPsolver.cpp:11-55).  Copies the arrays to HBM. */
+int rsc_pnp_create(rsc_context* ctx, const rsc_pnp_problem* problem, uint32_t seed, rsc_pnp** out);
+void rsc_pnp_destroy(rsc_pnp* s);
+/* PnPsolver::SetRansacParameters (PnPsolver.cpp:58-94; defaults 0.99, 8, 300, 4, 0.4, 5.991). */
+int rsc_pnp_set_ransac_parameters(rsc_pnp* s, double probability, int min_inliers, int max_iterations,
+                                  int min_set, float epsilon, float th2);
+/* PnPsolver::iterate (PnPsolver.cpp:102-191).  `inliers` receives n_points bytes (vbInliers) or
+ * is left untouched when the reference returns an empty vector (:105); may be NULL. */
+int rsc_pnp_iterate(rsc_pnp* s, int n_iterations, rsc_pnp_result* out, uint8_t* inliers);
+/* PnPsolver::find (PnPsolver.cpp:96-100). */
+int rsc_pnp_find(rsc_pnp* s, rsc_pnp_result* out, uint8_t* inliers);
+/* iterate() on `count` solvers of ONE context at once (the relocalization candidates of
+ * Tracking.cpp:1239-1334); all hypotheses of all solvers run in the same kernel launches.
+ * Results are identical to calling rsc_pnp_iterate on each solver in order. */
+int rsc_pnp_iterate_many(rsc_pnp* const* solvers, int count, const int32_t* n_iterations, rsc_pnp_result* out,
+                         uint8_t* const* inliers);
+/* Back to the freshly constructed state with a new rand() stream (reuse HBM-resident data). */
+int rsc_pnp_reset(rsc_pnp* s, uint32_t seed);
+/* out: [0] mnIterations [1] mRansacMaxIts [2] mRansacMinInliers [3] mnBestInliers
+ *      [4] maximum_number_of_correspondences [5] N [6] N_points [7] mRansacMinSet */
+int rsc_pnp_get_state(const rsc_pnp* s, int32_t out[8]);
+/* Debug/parity hook: sample indices (8 per hypothesis) of the last launch for this solver. */
+int rsc_pnp_last_samples(rsc_pnp* s, int32_t* out, int cap);
+
+/* ---- Sim3Solver (include/Sim3Solver.hpp:16-103, src/Sim3Solver.cpp) --------------------------- */
+/* Raw constructor inputs for one keyframe pair (Sim3Solver.cpp:6-85), per match slot i1 < n1. */
+typedef struct {
+    int32_t n1;              /* vpMatched12.size() */
+    const uint8_t* valid;    /* slot usable: match, pMP1, not bad, both indices >= 0 (:28-43) */
+    const float* Xw1;        /* [n1][3] pMP1->GetWorldPos() */
+    const float* Xw2;        /* [n1][3] pMP2->GetWorldPos() */
+    const float* sigma2_1;   /* [n1] pKF1->mvLevelSigma2[kp1.octave] */
+    const float* sigma2_2;   /* [n1] pKF2->mvLevelSigma2[kp2.octave] */
+    float R1[9], t1[3];      /* pKF1->GetRotation()/GetTranslation(), row-major */
+    float R2[9], t2[3];
+    float K1[4], K2[4];      /* fx, fy, cx, cy of KeyFrame::mK */
+} rsc_sim3_input;
+
+/* Sim3Solver::Sim3Solver (Sim3Solver.cpp:6-85, includes its SetRansacParameters() call). */
+int rsc_sim3_create(rsc_context* ctx, const rsc_sim3_input* in, uint32_t seed, rsc_sim3** out);
+void rsc_sim3_destroy(rsc_sim3* s);
+/* Sim3Solver::SetRansacParameters (Sim3Solver.cpp:87-111; defaults 0.99, 6, 300). */
+int rsc_sim3_set_ransac_parameters(rsc_sim3* s, double probability, int min_inliers, int max_iterations);
+typedef struct {
+    int32_t ok, no_more, n_inliers, iterations;
+    float R[9], t[3];    /* GetEstimatedRotation()/GetEstimatedTranslation() after the call */
+} rsc_sim3_result;
+/* Sim3Solver::iterate (Sim3Solver.cpp:113-178); `inliers` receives n1 bytes (always sized). */
+int rsc_sim3_iterate(rsc_sim3* s, int n_iterations, rsc_sim3_result* out, uint8_t* inliers);
+int rsc_sim3_find(rsc_sim3* s, rsc_sim3_result* out, uint8_t* inliers);
+int rsc_sim3_iterate_many(rsc_sim3* const* solvers, int count, const int32_t* n_iterations, rsc_sim3_result* out,
+                          uint8_t* const* inliers);
+int rsc_sim3_reset(rsc_sim3* s, uint32_t seed);
+/* out: [0] mnIterations [1] mRansacMaxIts [2] mRansacMinInliers [3] mnBestInliers [4] N [5] mN1 */
+int rsc_sim3_get_state(const rsc_sim3* s, int32_t out[6]);
+/* Prepared per-correspondence arrays built by the constructor (for parity tests):
+ * X1c/X2c [N][3], P1im1/P2im2 [N][2], max_err1/2 [N] (size_t thresholds), indices1 [N]. */
+int rsc_sim3_prepared(const rsc_sim3* s, float* X1c, float* X2c, float* P1im1, float* P2im2, uint64_t* max_err1,
+                      uint64_t* max_err2, int32_t* indices1);
+
+/* ---- glibc rand() helpers (Thirdparty/DBoW2/DUtils/Random.cpp:33-50) -------------------------- */
+/* First n rand() outputs after srand(seed), produced with the device jump table (parity hook). */
+int rsc_rand_stream(rsc_context* ctx, uint32_t seed, int n, int32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSC_H_ */

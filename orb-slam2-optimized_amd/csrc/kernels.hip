@@ -1,0 +1,382 @@
+// kernels.hip — gfx950 kernels of the RANSAC pose engine.
+//
+//   pnp_solve_kernel<NS>   one LANE = one EPnP hypothesis (sample -> compute_pose), 64-lane
+//                          workgroups, 80 KiB LDS slab (12x12 eigenproblem per lane).
+//   pnp_scan_kernel<PPT>   PnPsolver::CheckInliers for a chunk of hypotheses of one problem:
+//                          256 threads hold the problem's correspondences in VGPRs (PPT per
+//                          thread); per hypothesis every lane tests its points, __ballot gives the
+//                          64-bit inlier words, popcount gives the count.
+//   pnp_refine_kernel      PnPsolver::Refine: compaction of the best inlier set into the grow-only
+//                          EPnP buffers, EPnP over n_r rows (MtM built block-parallel), then the
+//                          block-parallel CheckInliers of the refined pose.
+//   sim3_solve_kernel / sim3_scan_kernel   the same split for Sim3Solver (Horn, float).
+//
+// Reference: src/PnPsolver.cpp, src/Sim3Solver.cpp (see rsc_core.h for the arithmetic contract).
+#include <hip/hip_runtime.h>
+#include "rsc_core.h"
+#include "rsc_epnp.h"
+#include "rsc_sim3.h"
+#include "rsc_kernels.h"
+
+namespace rsc {
+
+// ------------------------------------------------------------------------------------------------
+// PnP hypotheses
+// ------------------------------------------------------------------------------------------------
+template <int NS>
+__global__ __launch_bounds__(64) void pnp_solve_kernel(const DevPnP* __restrict__ probs,
+                                                       const LaunchProb* __restrict__ lps,
+                                                       const int2* __restrict__ wg_table,
+                                                       const uint32_t* __restrict__ rng_T,
+                                                       float* __restrict__ poses, int32_t* __restrict__ samples) {
+    __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles * 64];
+    const int lane = threadIdx.x;
+    const int2 wt = wg_table[blockIdx.x];
+    const LaunchProb& lp = lps[wt.x];
+    const int h = wt.y + lane;
+    if (h >= lp.H) return;
+    const DevPnP& P = probs[lp.prob];
+
+    uint32_t w[31];
+    RSC_UNROLL for (int j = 0; j < 31; ++j) w[j] = lp.window[j];
+    uint32_t words[NS];
+    RSC_UNROLL for (int d = 0; d < NS; ++d) words[d] = rng_word(rng_T, w, lp.g0 + h * NS + d);
+    int idx[NS];
+    swap_remove_sample<NS>(words, NS, P.n, idx);
+
+    HypStore<NS> st;
+    RSC_UNROLL for (int i = 0; i < NS; ++i) {
+        const float4 p = P.pts[idx[i]];
+        const float2 q = P.uv[idx[i]];
+        st.pw_[i][0] = p.x; st.pw_[i][1] = p.y; st.pw_[i][2] = p.z;
+        st.u_[i][0] = q.x; st.u_[i][1] = q.y;
+    }
+    st.rows_ = P.rows;
+    st.spw = P.pws;
+    st.sal = P.als;
+    const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
+    LaneMat S{slab + lane, 64};
+    float R[9], t[3];
+    epnp_compute_pose(st, K, S, R, t);
+
+    float* out = poses + (size_t)(lp.out0 + h) * 12;
+    RSC_UNROLL for (int k = 0; k < 9; ++k) out[k] = R[k];
+    RSC_UNROLL for (int k = 0; k < 3; ++k) out[9 + k] = t[k];
+    if (samples) {
+        RSC_UNROLL for (int i = 0; i < NS; ++i) samples[(size_t)(lp.out0 + h) * 8 + i] = idx[i];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// PnP inlier scan (CheckInliers) — points-stationary, pose broadcast.
+// ------------------------------------------------------------------------------------------------
+template <int PPT>
+__global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict__ probs,
+                                                       const LaunchProb* __restrict__ lps,
+                                                       const int4* __restrict__ wg_table,  // lp, hyp0, count
+                                                       const float* __restrict__ poses,
+                                                       int32_t* __restrict__ counts,
+                                                       uint64_t* __restrict__ masks, int mask_words) {
+    __shared__ int wave_cnt[4][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int4 wt = wg_table[blockIdx.x];
+    const LaunchProb& lp = lps[wt.x];
+    const DevPnP& P = probs[lp.prob];
+    const double fx = P.fx, fy = P.fy, cx = P.cx, cy = P.cy;
+    float X[PPT], Y[PPT], Z[PPT], U[PPT], V[PPT], E[PPT];
+    RSC_UNROLL for (int s = 0; s < PPT; ++s) {
+        const int i = s * 256 + tid;
+        if (i < P.n) {
+            const float4 p = P.pts[i];
+            const float2 q = P.uv[i];
+            X[s] = p.x; Y[s] = p.y; Z[s] = p.z; E[s] = p.w * P.th2; U[s] = q.x; V[s] = q.y;  // mvMaxError (:91-93)
+        } else {
+            X[s] = 0.f; Y[s] = 0.f; Z[s] = 1.f; E[s] = -1.f; U[s] = 0.f; V[s] = 0.f;  // never an inlier
+        }
+    }
+    for (int j = 0; j < wt.z; ++j) {
+        const int h = wt.y + j;
+        const float* pp = poses + (size_t)(lp.out0 + h) * 12;
+        float R[9], t[3];
+        RSC_UNROLL for (int k = 0; k < 9; ++k) R[k] = pp[k];
+        RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = pp[9 + k];
+        int cnt = 0;
+        uint64_t* mw = masks ? masks + (size_t)(lp.out0 + h) * mask_words : nullptr;
+        RSC_UNROLL for (int s = 0; s < PPT; ++s) {
+            const bool inl = pnp_inlier(R, t, fx, fy, cx, cy, X[s], Y[s], Z[s], U[s], V[s], E[s]);
+            const uint64_t b = __ballot(inl);
+            cnt += __popcll(b);
+            if (mw && lane == 0) mw[s * 4 + wave] = b;
+        }
+        if (lane == 0) wave_cnt[wave][j & 63] = cnt;
+        if ((j & 63) == 63 || j == wt.z - 1) {
+            __syncthreads();
+            const int base = j & ~63;
+            if (tid <= (j & 63)) {
+                const int c = wave_cnt[0][tid] + wave_cnt[1][tid] + wave_cnt[2][tid] + wave_cnt[3][tid];
+                counts[lp.out0 + wt.y + base + tid] = c;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// PnP Refine: one 256-thread workgroup per refining problem.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restrict__ probs,
+                                                         const RefineJob* __restrict__ jobs,
+                                                         int mask_words_out) {
+    __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles];
+    __shared__ int prefix[129];
+    __shared__ double cws_sh[12];
+    __shared__ float pose_sh[12];
+    __shared__ int cnt_sh[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const RefineJob& J = jobs[blockIdx.x];
+    const DevPnP& P = probs[J.prob];
+    const int n = P.n;
+    const int nwords = (n + 63) / 64;
+
+    // 1. compaction of the best-inlier set (PnPsolver.cpp:195-214), in index order.
+    if (tid == 0) {
+        int acc = 0;
+        for (int wd = 0; wd < nwords; ++wd) { prefix[wd] = acc; acc += __popcll(J.best_mask[wd]); }
+        prefix[nwords] = acc;
+    }
+    __syncthreads();
+    const int nr = prefix[nwords];
+    for (int wd = tid; wd < nwords; wd += 256) {
+        uint64_t m = J.best_mask[wd];
+        int r = prefix[wd];
+        while (m) {
+            const int b = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const int i = wd * 64 + b;
+            const float4 p = P.pts[i];
+            const float2 q = P.uv[i];
+            P.pws[3 * r + 0] = p.x; P.pws[3 * r + 1] = p.y; P.pws[3 * r + 2] = p.z;
+            P.us[2 * r + 0] = q.x; P.us[2 * r + 1] = q.y;
+            ++r;
+        }
+    }
+    // set_maximum_number_of_correspondences(nr): growth zero-fills (the rows beyond nr do not
+    // exist after growth; rows = nr).  Without growth the rows beyond nr stay stale (Q6).
+    const int rows = J.rows_after;
+    __syncthreads();
+
+    RowStore st{nr, rows, P.pws, P.us, P.als};
+    const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
+    LaneMat S{slab, 1};
+    // 2. control points + alphas (single lane, sequential sums as in the reference)
+    if (tid == 0) {
+        double cws[4][3];
+        control_points_and_alphas(st, cws);
+        RSC_UNROLL for (int i = 0; i < 4; ++i)
+            RSC_UNROLL for (int c = 0; c < 3; ++c) cws_sh[3 * i + c] = cws[i][c];
+    }
+    __syncthreads();
+    // 3. MtM lower triangle, one entry per thread
+    if (tid < 78) {
+        int a = 0, b = tid;
+        while (b > a) { b -= a + 1; ++a; }  // tid -> (a,b) with b <= a, row-major lower triangle
+        double s = M_entry(st, K, 0, a) * M_entry(st, K, 0, b);
+        for (int r = 1; r < 2 * nr; ++r) s = s + M_entry(st, K, r, a) * M_entry(st, K, r, b);
+        S.at(a, b) = s;
+    }
+    __syncthreads();
+    // 4. eigensolver + betas + Gauss-Newton + R,t (single lane)
+    if (tid == 0) {
+        double cws[4][3];
+        RSC_UNROLL for (int i = 0; i < 4; ++i)
+            RSC_UNROLL for (int c = 0; c < 3; ++c) cws[i][c] = cws_sh[3 * i + c];
+        float R[9], t[3];
+        epnp_stage_c(st, K, S, cws, R, t);
+        RSC_UNROLL for (int k = 0; k < 9; ++k) pose_sh[k] = R[k];
+        RSC_UNROLL for (int k = 0; k < 3; ++k) pose_sh[9 + k] = t[k];
+    }
+    __syncthreads();
+    // 5. CheckInliers of the refined pose
+    float R[9], t[3];
+    RSC_UNROLL for (int k = 0; k < 9; ++k) R[k] = pose_sh[k];
+    RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = pose_sh[9 + k];
+    int cnt = 0;
+    const double fx = P.fx, fy = P.fy, cx = P.cx, cy = P.cy;
+    for (int base = 0; base < mask_words_out * 64; base += 256) {
+        const int i = base + tid;
+        bool inl = false;
+        if (i < n) {
+            const float4 p = P.pts[i];
+            const float2 q = P.uv[i];
+            inl = pnp_inlier(R, t, fx, fy, cx, cy, p.x, p.y, p.z, q.x, q.y, p.w * P.th2);
+        }
+        const uint64_t b = __ballot(inl);
+        cnt += __popcll(b);
+        if (lane == 0 && (base / 64 + wave) < mask_words_out) J.out_mask[base / 64 + wave] = b;
+    }
+    if (lane == 0) cnt_sh[wave] = cnt;
+    __syncthreads();
+    if (tid == 0) {
+        *J.out_count = cnt_sh[0] + cnt_sh[1] + cnt_sh[2] + cnt_sh[3];
+        RSC_UNROLL for (int k = 0; k < 12; ++k) J.out_pose[k] = pose_sh[k];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Sim3 hypotheses + scan
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void sim3_solve_kernel(const DevSim3* __restrict__ probs,
+                                                        const LaunchProb* __restrict__ lps,
+                                                        const int2* __restrict__ wg_table,
+                                                        const uint32_t* __restrict__ rng_T,
+                                                        float* __restrict__ poses, int32_t* __restrict__ samples) {
+    const int lane = threadIdx.x;
+    const int2 wt = wg_table[blockIdx.x];
+    const LaunchProb& lp = lps[wt.x];
+    const int h = wt.y + lane;
+    if (h >= lp.H) return;
+    const DevSim3& P = probs[lp.prob];
+    uint32_t w[31];
+    RSC_UNROLL for (int j = 0; j < 31; ++j) w[j] = lp.window[j];
+    uint32_t words[3];
+    RSC_UNROLL for (int d = 0; d < 3; ++d) words[d] = rng_word(rng_T, w, lp.g0 + h * 3 + d);
+    int idx[3];
+    swap_remove_sample<3>(words, 3, P.n, idx);
+    float P1[3][3], P2[3][3];
+    RSC_UNROLL for (int i = 0; i < 3; ++i) {
+        const float4 a = P.x1[idx[i]];
+        const float4 b = P.x2[idx[i]];
+        P1[0][i] = a.x; P1[1][i] = a.y; P1[2][i] = a.z;
+        P2[0][i] = b.x; P2[1][i] = b.y; P2[2][i] = b.z;
+    }
+    Sim3Pose T;
+    sim3_compute(P1, P2, T);
+    float* out = poses + (size_t)(lp.out0 + h) * 24;
+    RSC_UNROLL for (int k = 0; k < 9; ++k) out[k] = T.R12[k];
+    RSC_UNROLL for (int k = 0; k < 3; ++k) out[9 + k] = T.t12[k];
+    RSC_UNROLL for (int k = 0; k < 9; ++k) out[12 + k] = T.R21[k];
+    RSC_UNROLL for (int k = 0; k < 3; ++k) out[21 + k] = T.t21[k];
+    if (samples) {
+        RSC_UNROLL for (int i = 0; i < 3; ++i) samples[(size_t)(lp.out0 + h) * 8 + i] = idx[i];
+    }
+}
+
+template <int PPT>
+__global__ __launch_bounds__(256) void sim3_scan_kernel(const DevSim3* __restrict__ probs,
+                                                        const LaunchProb* __restrict__ lps,
+                                                        const int4* __restrict__ wg_table,
+                                                        const float* __restrict__ poses,
+                                                        int32_t* __restrict__ counts,
+                                                        uint64_t* __restrict__ masks, int mask_words) {
+    __shared__ int wave_cnt[4][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int4 wt = wg_table[blockIdx.x];
+    const LaunchProb& lp = lps[wt.x];
+    const DevSim3& P = probs[lp.prob];
+    const float K1[4] = {P.K1[0], P.K1[1], P.K1[2], P.K1[3]};
+    const float K2[4] = {P.K2[0], P.K2[1], P.K2[2], P.K2[3]};
+    float A[PPT][3], B[PPT][3], p1u[PPT], p1v[PPT], p2u[PPT], p2v[PPT], e1[PPT], e2[PPT];
+    RSC_UNROLL for (int s = 0; s < PPT; ++s) {
+        const int i = s * 256 + tid;
+        if (i < P.n) {
+            const float4 a = P.x1[i], b = P.x2[i], pp = P.pim[i];
+            A[s][0] = a.x; A[s][1] = a.y; A[s][2] = a.z; e1[s] = a.w;
+            B[s][0] = b.x; B[s][1] = b.y; B[s][2] = b.z; e2[s] = b.w;
+            p1u[s] = pp.x; p1v[s] = pp.y; p2u[s] = pp.z; p2v[s] = pp.w;
+        } else {
+            A[s][0] = A[s][1] = 0.f; A[s][2] = 1.f; B[s][0] = B[s][1] = 0.f; B[s][2] = 1.f;
+            e1[s] = e2[s] = -1.f; p1u[s] = p1v[s] = p2u[s] = p2v[s] = 0.f;
+        }
+    }
+    for (int j = 0; j < wt.z; ++j) {
+        const int h = wt.y + j;
+        const float* pp = poses + (size_t)(lp.out0 + h) * 24;
+        Sim3Pose T;
+        RSC_UNROLL for (int k = 0; k < 9; ++k) { T.R12[k] = pp[k]; T.R21[k] = pp[12 + k]; }
+        RSC_UNROLL for (int k = 0; k < 3; ++k) { T.t12[k] = pp[9 + k]; T.t21[k] = pp[21 + k]; }
+        int cnt = 0;
+        uint64_t* mw = masks ? masks + (size_t)(lp.out0 + h) * mask_words : nullptr;
+        RSC_UNROLL for (int s = 0; s < PPT; ++s) {
+            const bool inl = sim3_inlier(T, K1, K2, A[s], B[s], p1u[s], p1v[s], p2u[s], p2v[s], e1[s], e2[s]);
+            const uint64_t b = __ballot(inl);
+            cnt += __popcll(b);
+            if (mw && lane == 0) mw[s * 4 + wave] = b;
+        }
+        if (lane == 0) wave_cnt[wave][j & 63] = cnt;
+        if ((j & 63) == 63 || j == wt.z - 1) {
+            __syncthreads();
+            const int base = j & ~63;
+            if (tid <= (j & 63)) {
+                const int c = wave_cnt[0][tid] + wave_cnt[1][tid] + wave_cnt[2][tid] + wave_cnt[3][tid];
+                counts[lp.out0 + wt.y + base + tid] = c;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// rand() outputs straight from the jump table (parity hook for the RNG contract).
+__global__ void rng_stream_kernel(const uint32_t* __restrict__ T, Window31 w, int g0, int n, int32_t* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t ww[31];
+    RSC_UNROLL for (int j = 0; j < 31; ++j) ww[j] = w.w[j];
+    out[i] = (int32_t)(rng_word(T, ww, g0 + i) >> 1);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Launchers
+// ------------------------------------------------------------------------------------------------
+hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
+                            const uint32_t* T, float* poses, int32_t* samples, hipStream_t st) {
+    switch (ns) {
+        case 4: pnp_solve_kernel<4><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples); break;
+        case 5: pnp_solve_kernel<5><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples); break;
+        case 6: pnp_solve_kernel<6><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,
+                           const float* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st) {
+    switch (ppt) {
+#define RSC_CASE(P) case P: pnp_scan_kernel<P><<<nwg, 256, 0, st>>>(probs, lps, wgt, poses, counts, masks, mask_words); break;
+        RSC_CASE(1) RSC_CASE(2) RSC_CASE(4) RSC_CASE(8) RSC_CASE(16) RSC_CASE(32)
+#undef RSC_CASE
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, int mask_words_out,
+                             hipStream_t st) {
+    pnp_refine_kernel<<<njobs, 256, 0, st>>>(probs, jobs, mask_words_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sim3_solve(int nwg, const DevSim3* probs, const LaunchProb* lps, const int2* wgt, const uint32_t* T,
+                             float* poses, int32_t* samples, hipStream_t st) {
+    sim3_solve_kernel<<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples);
+    return hipGetLastError();
+}
+
+hipError_t launch_sim3_scan(int ppt, int nwg, const DevSim3* probs, const LaunchProb* lps, const int4* wgt,
+                            const float* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st) {
+    switch (ppt) {
+#define RSC_CASE(P) case P: sim3_scan_kernel<P><<<nwg, 256, 0, st>>>(probs, lps, wgt, poses, counts, masks, mask_words); break;
+        RSC_CASE(1) RSC_CASE(2) RSC_CASE(4) RSC_CASE(8) RSC_CASE(16) RSC_CASE(32)
+#undef RSC_CASE
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_rng_stream(const uint32_t* T, const uint32_t* window, int g0, int n, int32_t* out, hipStream_t st) {
+    Window31 w;
+    for (int j = 0; j < 31; ++j) w.w[j] = window[j];
+    rng_stream_kernel<<<(n + 255) / 256, 256, 0, st>>>(T, w, g0, n, out);
+    return hipGetLastError();
+}
+
+}  // namespace rsc

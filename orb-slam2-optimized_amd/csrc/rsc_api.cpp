@@ -1,0 +1,838 @@
+// rsc_api.cpp — C ABI (include/rsc.h) and HIP backend of the RANSAC engine.
+//
+// Data layout in HBM (per solver, resident for the solver's lifetime):
+//   PnP : pts float4[N] = (X, Y, Z, sigma^2), uv float2[N], EPnP grow-only buffers
+//         pws/us/als double[N][3|2|4], best/refined inlier bitsets uint64[ceil(N/64)].
+//   Sim3: x1 float4[N] = (X1c, maxErr1), x2 float4[N] = (X2c, maxErr2), pim float4[N].
+// Per context (reused across calls, grown on demand): the rand() jump table (2.1 MB), pose
+// records float[H][12|24], counts int32[H], inlier bitsets uint64[H][W], launch descriptors.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <memory>
+#include "../../include/rsc.h"
+#include "rsc_kernels.h"
+#include "rsc_engine.h"
+
+using namespace rsc;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+#define RSC_HIP(call)                                                                         \
+    do {                                                                                      \
+        hipError_t _e = (call);                                                               \
+        if (_e != hipSuccess) {                                                               \
+            g_last_error = std::string(#call) + ": " + hipGetErrorString(_e);                  \
+            return RSC_ERR_HIP;                                                               \
+        }                                                                                     \
+    } while (0)
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max(n, (size_t)64);
+        hipError_t e = hipMalloc(&p, want * sizeof(T));
+        if (e != hipSuccess) {
+            g_last_error = std::string("hipMalloc: ") + hipGetErrorString(e);
+            return RSC_ERR_OOM;
+        }
+        cap = want;
+        return 0;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+template <typename T>
+struct PinBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return 0;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max(n, (size_t)64);
+        hipError_t e = hipHostMalloc(&p, want * sizeof(T), hipHostMallocDefault);
+        if (e != hipSuccess) {
+            g_last_error = std::string("hipHostMalloc: ") + hipGetErrorString(e);
+            return RSC_ERR_OOM;
+        }
+        cap = want;
+        return 0;
+    }
+    ~PinBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
+int ppt_for(int n) {
+    int need = (n + 255) / 256;
+    int p = 1;
+    while (p < need) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+struct rsc_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    RngTable table;
+    DevBuf<uint32_t> d_table;
+    // speculation work buffers
+    DevBuf<float> d_poses;
+    DevBuf<int32_t> d_counts;
+    DevBuf<uint64_t> d_masks;
+    DevBuf<int32_t> d_samples;
+    DevBuf<char> d_desc;
+    PinBuf<char> h_desc;
+    PinBuf<int32_t> h_counts;
+    PinBuf<float> h_small;
+    DevBuf<char> d_refine;
+    int mask_words = 0;  // per hypothesis, last speculation
+    bool keep_samples = true;
+    // timing
+    bool timing = false;
+    hipEvent_t ev[6] = {};
+    double last_ms[5] = {0, 0, 0, 0, 0};
+};
+
+struct rsc_pnp {
+    rsc_context* ctx = nullptr;
+    PnPState st;
+    float4* d_pts = nullptr;
+    float2* d_uv = nullptr;
+    double* d_pws = nullptr;
+    double* d_us = nullptr;
+    double* d_als = nullptr;
+    uint64_t* d_best = nullptr;
+    uint64_t* d_refined = nullptr;
+    int words = 0;
+    // position in the last speculation of its context
+    int spec_out0 = -1, spec_H = 0;
+    ~rsc_pnp() {
+        for (void* p : {(void*)d_pts, (void*)d_uv, (void*)d_pws, (void*)d_us, (void*)d_als, (void*)d_best,
+                        (void*)d_refined})
+            if (p) (void)hipFree(p);
+    }
+};
+
+struct rsc_sim3 {
+    rsc_context* ctx = nullptr;
+    Sim3State st;
+    // prepared arrays (host copies for rsc_sim3_prepared)
+    std::vector<float> X1c, X2c, P1, P2;
+    std::vector<uint64_t> e1, e2;
+    float K1[4], K2[4];
+    float4* d_x1 = nullptr;
+    float4* d_x2 = nullptr;
+    float4* d_pim = nullptr;
+    int spec_out0 = -1, spec_H = 0;
+    ~rsc_sim3() {
+        for (void* p : {(void*)d_x1, (void*)d_x2, (void*)d_pim})
+            if (p) (void)hipFree(p);
+    }
+};
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// Launch-descriptor packing: one pinned blob -> one H2D copy per launch round.
+// ------------------------------------------------------------------------------------------------
+struct Blob {
+    std::vector<char> bytes;
+    size_t add(const void* p, size_t n) {
+        size_t off = (bytes.size() + 15) & ~(size_t)15;
+        bytes.resize(off + n);
+        std::memcpy(bytes.data() + off, p, n);
+        return off;
+    }
+};
+
+int upload_blob(rsc_context* C, const Blob& b) {
+    if (int e = C->h_desc.ensure(b.bytes.size())) return e;
+    if (int e = C->d_desc.ensure(b.bytes.size())) return e;
+    // the previous round's H2D copy must be finished before the pinned staging is overwritten
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    std::memcpy(C->h_desc.p, b.bytes.data(), b.bytes.size());
+    RSC_HIP(hipMemcpyAsync(C->d_desc.p, C->h_desc.p, b.bytes.size(), hipMemcpyHostToDevice, C->stream));
+    return 0;
+}
+
+void timing_begin(rsc_context* C, int slot) {
+    if (C->timing) (void)hipEventRecord(C->ev[slot], C->stream);
+}
+
+// ------------------------------------------------------------------------------------------------
+// PnP backend
+// ------------------------------------------------------------------------------------------------
+struct HipPnPBackend : PnPBackend {
+    rsc_context* C;
+    std::vector<rsc_pnp*> solvers;  // index = state slot in the current call
+    explicit HipPnPBackend(rsc_context* c) : C(c) {}
+    rsc_pnp* of(PnPState* s) {
+        for (auto* p : solvers)
+            if (&p->st == s) return p;
+        return nullptr;
+    }
+    DevPnP dev_of(rsc_pnp* p) {
+        DevPnP d;
+        d.pts = p->d_pts;
+        d.uv = p->d_uv;
+        d.n = p->st.N;
+        d.fx = p->st.fx; d.fy = p->st.fy; d.cx = p->st.cx; d.cy = p->st.cy;
+        d.th2 = p->st.th2;
+        d.rows = p->st.max_rows;
+        d.pws = p->d_pws; d.us = p->d_us; d.als = p->d_als;
+        return d;
+    }
+
+    int speculate(PnPState* const* S, int count, const int* H, std::vector<std::vector<int32_t>>& counts) override {
+        // group by min_set (template parameter of the solve kernel)
+        int total = 0, maxN = 1;
+        std::vector<DevPnP> probs(count);
+        std::vector<LaunchProb> lps(count);
+        for (int i = 0; i < count; ++i) {
+            rsc_pnp* p = of(S[i]);
+            if (!p) return RSC_ERR_ARG;
+            if (S[i]->mRansacMinSet < 4 || S[i]->mRansacMinSet > 6) {
+                g_last_error = "min_set outside the supported range [4,6]";
+                return RSC_ERR_UNSUPPORTED;
+            }
+            S[i]->rng.ensure(C->table, H[i] * S[i]->mRansacMinSet);
+            probs[i] = dev_of(p);
+            LaunchProb& lp = lps[i];
+            lp.prob = i;
+            lp.H = H[i];
+            lp.out0 = total;
+            lp.g0 = S[i]->rng.g;
+            std::memcpy(lp.window, S[i]->rng.window, sizeof(lp.window));
+            lp.pad = 0;
+            p->spec_out0 = total;
+            p->spec_H = H[i];
+            total += H[i];
+            maxN = std::max(maxN, S[i]->N);
+        }
+        const int ppt = ppt_for(maxN);
+        if (ppt > 32) {
+            g_last_error = "more than 8192 correspondences per problem";
+            return RSC_ERR_UNSUPPORTED;
+        }
+        const int mw = ppt * 4;
+        C->mask_words = mw;
+        // work tables
+        std::vector<std::vector<int2>> solve_wgs(3);
+        std::vector<int4> scan_wgs;
+        const int HC = 32;  // hypotheses per scan workgroup
+        for (int i = 0; i < count; ++i) {
+            const int g = S[i]->mRansacMinSet - 4;
+            for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs[g].push_back(make_int2(i, h0));
+            for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
+        }
+        Blob b;
+        const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevPnP));
+        const size_t o_lps = b.add(lps.data(), lps.size() * sizeof(LaunchProb));
+        size_t o_solve[3];
+        for (int g = 0; g < 3; ++g) o_solve[g] = b.add(solve_wgs[g].data(), solve_wgs[g].size() * sizeof(int2));
+        const size_t o_scan = b.add(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
+        if (int e = upload_blob(C, b)) return e;
+        if (int e = C->d_poses.ensure((size_t)total * 12)) return e;
+        if (int e = C->d_counts.ensure((size_t)total)) return e;
+        if (int e = C->d_masks.ensure((size_t)total * mw)) return e;
+        if (C->keep_samples)
+            if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
+        const char* base = C->d_desc.p;
+        const DevPnP* dprobs = reinterpret_cast<const DevPnP*>(base + o_probs);
+        const LaunchProb* dlps = reinterpret_cast<const LaunchProb*>(base + o_lps);
+        timing_begin(C, 0);
+        for (int g = 0; g < 3; ++g) {
+            if (solve_wgs[g].empty()) continue;
+            RSC_HIP(launch_pnp_solve(4 + g, (int)solve_wgs[g].size(), dprobs, dlps,
+                                     reinterpret_cast<const int2*>(base + o_solve[g]), C->d_table.p, C->d_poses.p,
+                                     C->keep_samples ? C->d_samples.p : nullptr, C->stream));
+        }
+        timing_begin(C, 1);
+        RSC_HIP(launch_pnp_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
+                                C->d_poses.p, C->d_counts.p, C->d_masks.p, mw, C->stream));
+        timing_begin(C, 2);
+        if (int e = C->h_counts.ensure(total)) return e;
+        RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        if (C->timing) {
+            float a = 0, s = 0;
+            (void)hipEventElapsedTime(&a, C->ev[0], C->ev[1]);
+            (void)hipEventElapsedTime(&s, C->ev[1], C->ev[2]);
+            C->last_ms[0] += a;
+            C->last_ms[1] += s;
+            C->last_ms[3] += 1;
+            C->last_ms[4] += total;
+        }
+        counts.assign(count, {});
+        for (int i = 0; i < count; ++i)
+            counts[i].assign(C->h_counts.p + lps[i].out0, C->h_counts.p + lps[i].out0 + H[i]);
+        return 0;
+    }
+
+    int adopt_best(PnPState* s, int i, int k) override {
+        rsc_pnp* p = of(s);
+        const size_t rec = (size_t)(p->spec_out0 + k);
+        RSC_HIP(hipMemcpyAsync(p->d_best, C->d_masks.p + rec * C->mask_words, (size_t)p->words * 8,
+                               hipMemcpyDeviceToDevice, C->stream));
+        if (int e = C->h_small.ensure(12)) return e;
+        RSC_HIP(hipMemcpyAsync(C->h_small.p, C->d_poses.p + rec * 12, 48, hipMemcpyDeviceToHost, C->stream));
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        pose12_to_T(C->h_small.p, s->mBestTcw);
+        (void)i;
+        return 0;
+    }
+
+    int refine(PnPState* const* S, int count, const int* rows_after, int* rcount, float (*rpose)[12]) override {
+        std::vector<DevPnP> probs(count);
+        std::vector<RefineJob> jobs(count);
+        if (int e = C->d_refine.ensure((size_t)count * 64)) return e;
+        float* d_out_pose = reinterpret_cast<float*>(C->d_refine.p);
+        int32_t* d_out_cnt = reinterpret_cast<int32_t*>(C->d_refine.p + (size_t)count * 48);
+        int maxw = 1;
+        for (int i = 0; i < count; ++i) {
+            rsc_pnp* p = of(S[i]);
+            probs[i] = dev_of(p);
+            jobs[i].prob = i;
+            jobs[i].rows_after = rows_after[i];
+            jobs[i].best_mask = p->d_best;
+            jobs[i].out_pose = d_out_pose + 12 * i;
+            jobs[i].out_count = d_out_cnt + i;
+            jobs[i].out_mask = p->d_refined;
+            maxw = std::max(maxw, p->words);
+        }
+        Blob b;
+        const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevPnP));
+        const size_t o_jobs = b.add(jobs.data(), jobs.size() * sizeof(RefineJob));
+        if (int e = upload_blob(C, b)) return e;
+        timing_begin(C, 3);
+        // refined masks are written with a per-solver word count: launch per distinct width
+        RSC_HIP(launch_pnp_refine(count, reinterpret_cast<const DevPnP*>(C->d_desc.p + o_probs),
+                                  reinterpret_cast<const RefineJob*>(C->d_desc.p + o_jobs), maxw, C->stream));
+        timing_begin(C, 4);
+        if (int e = C->h_small.ensure((size_t)count * 16)) return e;
+        RSC_HIP(hipMemcpyAsync(C->h_small.p, C->d_refine.p, (size_t)count * 52, hipMemcpyDeviceToHost, C->stream));
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        if (C->timing) {
+            float r = 0;
+            (void)hipEventElapsedTime(&r, C->ev[3], C->ev[4]);
+            C->last_ms[2] += r;
+        }
+        const int32_t* hc = reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(C->h_small.p) + (size_t)count * 48);
+        for (int i = 0; i < count; ++i) {
+            rcount[i] = hc[i];
+            std::memcpy(rpose[i], C->h_small.p + 12 * i, 48);
+        }
+        return 0;
+    }
+
+    int fetch_mask(PnPState* const* S, int count, const int* kind, uint8_t* const* out) override {
+        std::vector<std::vector<uint64_t>> words(count);
+        for (int i = 0; i < count; ++i) {
+            rsc_pnp* p = of(S[i]);
+            words[i].resize(p->words);
+            RSC_HIP(hipMemcpyAsync(words[i].data(), kind[i] == 1 ? p->d_refined : p->d_best, (size_t)p->words * 8,
+                                   hipMemcpyDeviceToHost, C->stream));
+        }
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        for (int i = 0; i < count; ++i) {
+            const PnPState& s = *S[i];
+            std::memset(out[i], 0, s.N_points);
+            for (int j = 0; j < s.N; ++j)
+                if ((words[i][j >> 6] >> (j & 63)) & 1ull) out[i][s.kp_index[j]] = 1;
+        }
+        return 0;
+    }
+};
+
+// ------------------------------------------------------------------------------------------------
+// Sim3 backend
+// ------------------------------------------------------------------------------------------------
+struct HipSim3Backend : Sim3Backend {
+    rsc_context* C;
+    std::vector<rsc_sim3*> solvers;  // slot j of the last speculation
+    explicit HipSim3Backend(rsc_context* c) : C(c) {}
+    rsc_sim3* of(Sim3State* s, const std::vector<rsc_sim3*>& all) {
+        for (auto* p : all)
+            if (&p->st == s) return p;
+        return nullptr;
+    }
+    std::vector<rsc_sim3*> all;
+
+    int speculate(Sim3State* const* S, int count, const int* H, std::vector<std::vector<int32_t>>& counts) override {
+        int total = 0, maxN = 1;
+        std::vector<DevSim3> probs(count);
+        std::vector<LaunchProb> lps(count);
+        solvers.assign(count, nullptr);
+        for (int i = 0; i < count; ++i) {
+            rsc_sim3* p = of(S[i], all);
+            if (!p) return RSC_ERR_ARG;
+            solvers[i] = p;
+            S[i]->rng.ensure(C->table, H[i] * 3);
+            DevSim3& d = probs[i];
+            d.x1 = p->d_x1; d.x2 = p->d_x2; d.pim = p->d_pim; d.n = S[i]->N;
+            std::memcpy(d.K1, p->K1, sizeof(d.K1));
+            std::memcpy(d.K2, p->K2, sizeof(d.K2));
+            LaunchProb& lp = lps[i];
+            lp.prob = i; lp.H = H[i]; lp.out0 = total; lp.g0 = S[i]->rng.g; lp.pad = 0;
+            std::memcpy(lp.window, S[i]->rng.window, sizeof(lp.window));
+            p->spec_out0 = total;
+            p->spec_H = H[i];
+            total += H[i];
+            maxN = std::max(maxN, S[i]->N);
+        }
+        const int ppt = ppt_for(maxN);
+        if (ppt > 32) {
+            g_last_error = "more than 8192 correspondences per problem";
+            return RSC_ERR_UNSUPPORTED;
+        }
+        const int mw = ppt * 4;
+        C->mask_words = mw;
+        std::vector<int2> solve_wgs;
+        std::vector<int4> scan_wgs;
+        const int HC = 32;
+        for (int i = 0; i < count; ++i) {
+            for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs.push_back(make_int2(i, h0));
+            for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
+        }
+        Blob b;
+        const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevSim3));
+        const size_t o_lps = b.add(lps.data(), lps.size() * sizeof(LaunchProb));
+        const size_t o_solve = b.add(solve_wgs.data(), solve_wgs.size() * sizeof(int2));
+        const size_t o_scan = b.add(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
+        if (int e = upload_blob(C, b)) return e;
+        if (int e = C->d_poses.ensure((size_t)total * 24)) return e;
+        if (int e = C->d_counts.ensure((size_t)total)) return e;
+        if (int e = C->d_masks.ensure((size_t)total * mw)) return e;
+        if (C->keep_samples)
+            if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
+        const char* base = C->d_desc.p;
+        const DevSim3* dprobs = reinterpret_cast<const DevSim3*>(base + o_probs);
+        const LaunchProb* dlps = reinterpret_cast<const LaunchProb*>(base + o_lps);
+        timing_begin(C, 0);
+        RSC_HIP(launch_sim3_solve((int)solve_wgs.size(), dprobs, dlps, reinterpret_cast<const int2*>(base + o_solve),
+                                  C->d_table.p, C->d_poses.p, C->keep_samples ? C->d_samples.p : nullptr, C->stream));
+        timing_begin(C, 1);
+        RSC_HIP(launch_sim3_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
+                                 C->d_poses.p, C->d_counts.p, C->d_masks.p, mw, C->stream));
+        timing_begin(C, 2);
+        if (int e = C->h_counts.ensure(total)) return e;
+        RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        if (C->timing) {
+            float a = 0, s = 0;
+            (void)hipEventElapsedTime(&a, C->ev[0], C->ev[1]);
+            (void)hipEventElapsedTime(&s, C->ev[1], C->ev[2]);
+            C->last_ms[0] += a;
+            C->last_ms[1] += s;
+            C->last_ms[3] += 1;
+            C->last_ms[4] += total;
+        }
+        counts.assign(count, {});
+        for (int i = 0; i < count; ++i)
+            counts[i].assign(C->h_counts.p + lps[i].out0, C->h_counts.p + lps[i].out0 + H[i]);
+        return 0;
+    }
+
+    int fetch_pose(int j, int k, float* pose12) override {
+        rsc_sim3* p = solvers[j];
+        if (int e = C->h_small.ensure(12)) return e;
+        RSC_HIP(hipMemcpyAsync(C->h_small.p, C->d_poses.p + (size_t)(p->spec_out0 + k) * 24, 48, hipMemcpyDeviceToHost,
+                               C->stream));
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        std::memcpy(pose12, C->h_small.p, 48);
+        return 0;
+    }
+
+    int fetch_mask(const int* wj, const int* wk, Sim3State* const* S, int count, uint8_t* const* out) override {
+        std::vector<std::vector<uint64_t>> words(count);
+        for (int q = 0; q < count; ++q) {
+            rsc_sim3* p = solvers[wj[q]];
+            const int nw = (S[q]->N + 63) / 64;
+            words[q].resize(nw);
+            RSC_HIP(hipMemcpyAsync(words[q].data(), C->d_masks.p + (size_t)(p->spec_out0 + wk[q]) * C->mask_words,
+                                   (size_t)nw * 8, hipMemcpyDeviceToHost, C->stream));
+        }
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        for (int q = 0; q < count; ++q) {
+            const Sim3State& s = *S[q];
+            std::memset(out[q], 0, s.mN1);
+            for (int j = 0; j < s.N; ++j)
+                if ((words[q][j >> 6] >> (j & 63)) & 1ull) out[q][s.indices1[j]] = 1;
+        }
+        return 0;
+    }
+};
+
+void to_result(const PnPResult& r, rsc_pnp_result* o) {
+    o->ok = r.ok;
+    o->no_more = r.no_more;
+    o->n_inliers = r.n_inliers;
+    o->iterations = r.iterations;
+    if (r.ok) std::memcpy(o->T, r.T, sizeof(o->T));
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+int rsc_version(void) { return 1; }
+
+const char* rsc_status_string(int status) {
+    switch (status) {
+        case RSC_OK: return "ok";
+        case RSC_ERR_ARG: return "invalid argument";
+        case RSC_ERR_HIP: return g_last_error.empty() ? "HIP error" : g_last_error.c_str();
+        case RSC_ERR_OOM: return g_last_error.empty() ? "out of device memory" : g_last_error.c_str();
+        case RSC_ERR_UNSUPPORTED: return g_last_error.empty() ? "unsupported" : g_last_error.c_str();
+        case RSC_ERR_NODEVICE: return "no HIP device";
+        default: return "unknown status";
+    }
+}
+
+int rsc_context_create(int device, rsc_context** out) {
+    if (!out) return RSC_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RSC_ERR_NODEVICE;
+    if (device < 0 || device >= ndev) return RSC_ERR_ARG;
+    RSC_HIP(hipSetDevice(device));
+    std::unique_ptr<rsc_context> C(new rsc_context());
+    C->device = device;
+    RSC_HIP(hipStreamCreateWithFlags(&C->stream, hipStreamNonBlocking));
+    C->own_stream = true;
+    C->table.build();
+    if (int e = C->d_table.ensure(C->table.T.size())) return e;
+    RSC_HIP(hipMemcpy(C->d_table.p, C->table.T.data(), C->table.T.size() * 4, hipMemcpyHostToDevice));
+    for (auto& e : C->ev) RSC_HIP(hipEventCreate(&e));
+    *out = C.release();
+    return RSC_OK;
+}
+
+void rsc_context_destroy(rsc_context* C) {
+    if (!C) return;
+    (void)hipSetDevice(C->device);
+    if (C->stream) (void)hipStreamSynchronize(C->stream);
+    for (auto& e : C->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (C->own_stream && C->stream) (void)hipStreamDestroy(C->stream);
+    delete C;
+}
+
+int rsc_context_set_stream(rsc_context* C, void* s) {
+    if (!C) return RSC_ERR_ARG;
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    if (C->own_stream) (void)hipStreamDestroy(C->stream);
+    C->stream = reinterpret_cast<hipStream_t>(s);
+    C->own_stream = false;
+    return RSC_OK;
+}
+
+int rsc_context_synchronize(rsc_context* C) {
+    if (!C) return RSC_ERR_ARG;
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    return RSC_OK;
+}
+
+int rsc_context_enable_timing(rsc_context* C, int enable) {
+    if (!C) return RSC_ERR_ARG;
+    C->timing = enable != 0;
+    return RSC_OK;
+}
+
+int rsc_context_last_timing(rsc_context* C, double out[5]) {
+    if (!C || !out) return RSC_ERR_ARG;
+    for (int i = 0; i < 5; ++i) out[i] = C->last_ms[i];
+    return RSC_OK;
+}
+
+// ---- PnP ----
+int rsc_pnp_create(rsc_context* C, const rsc_pnp_problem* pb, uint32_t seed, rsc_pnp** out) {
+    if (!C || !pb || !out || pb->n < 0 || pb->n_points < pb->n) return RSC_ERR_ARG;
+    if (pb->n > 0 && (!pb->p2d || !pb->p3dw || !pb->sigma2)) return RSC_ERR_ARG;
+    *out = nullptr;
+    RSC_HIP(hipSetDevice(C->device));
+    std::unique_ptr<rsc_pnp> S(new rsc_pnp());
+    S->ctx = C;
+    PnPState& s = S->st;
+    s.N = pb->n;
+    s.N_points = pb->n_points;
+    s.fx = pb->fx; s.fy = pb->fy; s.cx = pb->cx; s.cy = pb->cy;
+    s.kp_index.resize(pb->n);
+    for (int i = 0; i < pb->n; ++i) s.kp_index[i] = pb->kp_index ? pb->kp_index[i] : i;
+    s.sigma2.assign(pb->sigma2, pb->sigma2 + pb->n);
+    s.reset(seed);
+    const int n = std::max(pb->n, 1);
+    S->words = (n + 63) / 64;
+    std::vector<float4> pts(n);
+    std::vector<float2> uv(n);
+    for (int i = 0; i < pb->n; ++i) {
+        pts[i] = make_float4(pb->p3dw[3 * i], pb->p3dw[3 * i + 1], pb->p3dw[3 * i + 2], pb->sigma2[i]);
+        uv[i] = make_float2(pb->p2d[2 * i], pb->p2d[2 * i + 1]);
+    }
+    const size_t cap = (size_t)std::max(n, 8);
+    RSC_HIP(hipMalloc(&S->d_pts, n * sizeof(float4)));
+    RSC_HIP(hipMalloc(&S->d_uv, n * sizeof(float2)));
+    RSC_HIP(hipMalloc(&S->d_pws, cap * 3 * sizeof(double)));
+    RSC_HIP(hipMalloc(&S->d_us, cap * 2 * sizeof(double)));
+    RSC_HIP(hipMalloc(&S->d_als, cap * 4 * sizeof(double)));
+    RSC_HIP(hipMalloc(&S->d_best, S->words * 8));
+    RSC_HIP(hipMalloc(&S->d_refined, S->words * 8));
+    RSC_HIP(hipMemcpy(S->d_pts, pts.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    RSC_HIP(hipMemcpy(S->d_uv, uv.data(), n * sizeof(float2), hipMemcpyHostToDevice));
+    RSC_HIP(hipMemset(S->d_pws, 0, cap * 3 * sizeof(double)));
+    RSC_HIP(hipMemset(S->d_us, 0, cap * 2 * sizeof(double)));
+    RSC_HIP(hipMemset(S->d_als, 0, cap * 4 * sizeof(double)));
+    RSC_HIP(hipMemset(S->d_best, 0, S->words * 8));
+    RSC_HIP(hipMemset(S->d_refined, 0, S->words * 8));
+    // PnPsolver does not call SetRansacParameters in its constructor; iterate() before it is UB in
+    // the reference.  Install the declared defaults so that the object is always usable.
+    pnp_set_params(s, 0.99, 8, 300, 4, 0.4f, 5.991f);
+    *out = S.release();
+    return RSC_OK;
+}
+
+void rsc_pnp_destroy(rsc_pnp* s) { delete s; }
+
+int rsc_pnp_set_ransac_parameters(rsc_pnp* s, double probability, int min_inliers, int max_iterations, int min_set,
+                                  float epsilon, float th2) {
+    if (!s) return RSC_ERR_ARG;
+    pnp_set_params(s->st, probability, min_inliers, max_iterations, min_set, epsilon, th2);
+    return RSC_OK;
+}
+
+int rsc_pnp_iterate_many(rsc_pnp* const* solvers, int count, const int32_t* n_its, rsc_pnp_result* out,
+                         uint8_t* const* inliers) {
+    if (count <= 0) return RSC_OK;
+    if (!solvers || !n_its || !out) return RSC_ERR_ARG;
+    rsc_context* C = solvers[0]->ctx;
+    for (int i = 0; i < count; ++i)
+        if (!solvers[i] || solvers[i]->ctx != C) return RSC_ERR_ARG;
+    RSC_HIP(hipSetDevice(C->device));
+    for (double& v : C->last_ms) v = 0;
+    HipPnPBackend be(C);
+    be.solvers.assign(solvers, solvers + count);
+    std::vector<PnPState*> S(count);
+    std::vector<int> its(count);
+    for (int i = 0; i < count; ++i) { S[i] = &solvers[i]->st; its[i] = n_its[i]; }
+    std::vector<PnPResult> res(count);
+    int st = pnp_iterate_many(be, S.data(), count, its.data(), res.data(), inliers);
+    if (st) return st;
+    for (int i = 0; i < count; ++i) to_result(res[i], &out[i]);
+    return RSC_OK;
+}
+
+int rsc_pnp_iterate(rsc_pnp* s, int n_its, rsc_pnp_result* out, uint8_t* inliers) {
+    if (!s || !out) return RSC_ERR_ARG;
+    int32_t n = n_its;
+    uint8_t* const m[1] = {inliers};
+    return rsc_pnp_iterate_many(&s, 1, &n, out, m);
+}
+
+int rsc_pnp_find(rsc_pnp* s, rsc_pnp_result* out, uint8_t* inliers) {
+    if (!s) return RSC_ERR_ARG;
+    return rsc_pnp_iterate(s, s->st.mRansacMaxIts, out, inliers);
+}
+
+int rsc_pnp_reset(rsc_pnp* s, uint32_t seed) {
+    if (!s) return RSC_ERR_ARG;
+    s->st.reset(seed);
+    return RSC_OK;
+}
+
+int rsc_pnp_get_state(const rsc_pnp* s, int32_t out[8]) {
+    if (!s || !out) return RSC_ERR_ARG;
+    const PnPState& t = s->st;
+    out[0] = t.mnIterations; out[1] = t.mRansacMaxIts; out[2] = t.mRansacMinInliers; out[3] = t.mnBestInliers;
+    out[4] = t.max_rows; out[5] = t.N; out[6] = t.N_points; out[7] = t.mRansacMinSet;
+    return RSC_OK;
+}
+
+int rsc_pnp_last_samples(rsc_pnp* s, int32_t* out, int cap) {
+    if (!s || !out) return RSC_ERR_ARG;
+    rsc_context* C = s->ctx;
+    if (s->spec_out0 < 0 || !C->d_samples.p) return 0;
+    const int n = std::min(cap, s->spec_H);
+    RSC_HIP(hipMemcpy(out, C->d_samples.p + (size_t)s->spec_out0 * 8, (size_t)n * 8 * 4, hipMemcpyDeviceToHost));
+    return n;
+}
+
+// ---- Sim3 ----
+int rsc_sim3_create(rsc_context* C, const rsc_sim3_input* in, uint32_t seed, rsc_sim3** out) {
+    if (!C || !in || !out || in->n1 < 0) return RSC_ERR_ARG;
+    *out = nullptr;
+    RSC_HIP(hipSetDevice(C->device));
+    std::unique_ptr<rsc_sim3> S(new rsc_sim3());
+    S->ctx = C;
+    Sim3State& s = S->st;
+    s.mN1 = in->n1;
+    // Sim3Solver::Sim3Solver (Sim3Solver.cpp:26-68): camera-frame points (float), size_t thresholds
+    for (int i1 = 0; i1 < in->n1; ++i1) {
+        if (!in->valid[i1]) continue;
+        S->e1.push_back((uint64_t)(9.210 * in->sigma2_1[i1]));
+        S->e2.push_back((uint64_t)(9.210 * in->sigma2_2[i1]));
+        s.indices1.push_back(i1);
+        const float* a = &in->Xw1[3 * i1];
+        const float* b = &in->Xw2[3 * i1];
+        for (int r = 0; r < 3; ++r)
+            S->X1c.push_back(in->R1[3 * r] * a[0] + in->R1[3 * r + 1] * a[1] + in->R1[3 * r + 2] * a[2] + in->t1[r]);
+        for (int r = 0; r < 3; ++r)
+            S->X2c.push_back(in->R2[3 * r] * b[0] + in->R2[3 * r + 1] * b[1] + in->R2[3 * r + 2] * b[2] + in->t2[r]);
+    }
+    s.N = (int)s.indices1.size();
+    std::memcpy(S->K1, in->K1, sizeof(S->K1));
+    std::memcpy(S->K2, in->K2, sizeof(S->K2));
+    // FromCameraToImage (Sim3Solver.cpp:329-347)
+    auto to_image = [](const std::vector<float>& X, std::vector<float>& P, const float K[4]) {
+        const size_t n = X.size() / 3;
+        P.resize(2 * n);
+        for (size_t i = 0; i < n; ++i) {
+            const float invz = 1 / X[3 * i + 2];
+            const float x = X[3 * i] * invz;
+            const float y = X[3 * i + 1] * invz;
+            P[2 * i] = K[0] * x + K[2];
+            P[2 * i + 1] = K[1] * y + K[3];
+        }
+    };
+    to_image(S->X1c, S->P1, S->K1);
+    to_image(S->X2c, S->P2, S->K2);
+    const int n = std::max(s.N, 1);
+    std::vector<float4> x1(n), x2(n), pim(n);
+    for (int i = 0; i < s.N; ++i) {
+        x1[i] = make_float4(S->X1c[3 * i], S->X1c[3 * i + 1], S->X1c[3 * i + 2], (float)S->e1[i]);
+        x2[i] = make_float4(S->X2c[3 * i], S->X2c[3 * i + 1], S->X2c[3 * i + 2], (float)S->e2[i]);
+        pim[i] = make_float4(S->P1[2 * i], S->P1[2 * i + 1], S->P2[2 * i], S->P2[2 * i + 1]);
+    }
+    RSC_HIP(hipMalloc(&S->d_x1, n * sizeof(float4)));
+    RSC_HIP(hipMalloc(&S->d_x2, n * sizeof(float4)));
+    RSC_HIP(hipMalloc(&S->d_pim, n * sizeof(float4)));
+    RSC_HIP(hipMemcpy(S->d_x1, x1.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    RSC_HIP(hipMemcpy(S->d_x2, x2.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    RSC_HIP(hipMemcpy(S->d_pim, pim.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    s.reset(seed);
+    sim3_set_params(s, 0.99, 6, 300);  // the constructor's SetRansacParameters() (:84)
+    *out = S.release();
+    return RSC_OK;
+}
+
+void rsc_sim3_destroy(rsc_sim3* s) { delete s; }
+
+int rsc_sim3_set_ransac_parameters(rsc_sim3* s, double probability, int min_inliers, int max_iterations) {
+    if (!s) return RSC_ERR_ARG;
+    sim3_set_params(s->st, probability, min_inliers, max_iterations);
+    return RSC_OK;
+}
+
+int rsc_sim3_iterate_many(rsc_sim3* const* solvers, int count, const int32_t* n_its, rsc_sim3_result* out,
+                          uint8_t* const* inliers) {
+    if (count <= 0) return RSC_OK;
+    if (!solvers || !n_its || !out) return RSC_ERR_ARG;
+    rsc_context* C = solvers[0]->ctx;
+    for (int i = 0; i < count; ++i)
+        if (!solvers[i] || solvers[i]->ctx != C) return RSC_ERR_ARG;
+    RSC_HIP(hipSetDevice(C->device));
+    for (double& v : C->last_ms) v = 0;
+    HipSim3Backend be(C);
+    be.all.assign(solvers, solvers + count);
+    std::vector<Sim3State*> S(count);
+    std::vector<int> its(count);
+    for (int i = 0; i < count; ++i) { S[i] = &solvers[i]->st; its[i] = n_its[i]; }
+    std::vector<Sim3Result> res(count);
+    int st = sim3_iterate_many(be, S.data(), count, its.data(), res.data(), inliers);
+    if (st) return st;
+    for (int i = 0; i < count; ++i) {
+        out[i].ok = res[i].ok;
+        out[i].no_more = res[i].no_more;
+        out[i].n_inliers = res[i].n_inliers;
+        out[i].iterations = res[i].iterations;
+        std::memcpy(out[i].R, res[i].R, sizeof(out[i].R));
+        std::memcpy(out[i].t, res[i].t, sizeof(out[i].t));
+    }
+    return RSC_OK;
+}
+
+int rsc_sim3_iterate(rsc_sim3* s, int n_its, rsc_sim3_result* out, uint8_t* inliers) {
+    if (!s || !out) return RSC_ERR_ARG;
+    int32_t n = n_its;
+    uint8_t* const m[1] = {inliers};
+    return rsc_sim3_iterate_many(&s, 1, &n, out, m);
+}
+
+int rsc_sim3_find(rsc_sim3* s, rsc_sim3_result* out, uint8_t* inliers) {
+    if (!s) return RSC_ERR_ARG;
+    return rsc_sim3_iterate(s, s->st.mRansacMaxIts, out, inliers);
+}
+
+int rsc_sim3_reset(rsc_sim3* s, uint32_t seed) {
+    if (!s) return RSC_ERR_ARG;
+    const int mi = s->st.mRansacMinInliers, mx = s->st.mRansacMaxIts;
+    (void)mi; (void)mx;
+    s->st.reset(seed);
+    return RSC_OK;
+}
+
+int rsc_sim3_get_state(const rsc_sim3* s, int32_t out[6]) {
+    if (!s || !out) return RSC_ERR_ARG;
+    const Sim3State& t = s->st;
+    out[0] = t.mnIterations; out[1] = t.mRansacMaxIts; out[2] = t.mRansacMinInliers; out[3] = t.mnBestInliers;
+    out[4] = t.N; out[5] = t.mN1;
+    return RSC_OK;
+}
+
+int rsc_sim3_prepared(const rsc_sim3* s, float* X1c, float* X2c, float* P1im1, float* P2im2, uint64_t* e1,
+                      uint64_t* e2, int32_t* idx) {
+    if (!s) return RSC_ERR_ARG;
+    const int N = s->st.N;
+    if (X1c) std::memcpy(X1c, s->X1c.data(), 12 * (size_t)N);
+    if (X2c) std::memcpy(X2c, s->X2c.data(), 12 * (size_t)N);
+    if (P1im1) std::memcpy(P1im1, s->P1.data(), 8 * (size_t)N);
+    if (P2im2) std::memcpy(P2im2, s->P2.data(), 8 * (size_t)N);
+    if (e1) std::memcpy(e1, s->e1.data(), 8 * (size_t)N);
+    if (e2) std::memcpy(e2, s->e2.data(), 8 * (size_t)N);
+    if (idx) std::memcpy(idx, s->st.indices1.data(), 4 * (size_t)N);
+    return RSC_OK;
+}
+
+// ---- RNG parity hook ----
+int rsc_rand_stream(rsc_context* C, uint32_t seed, int n, int32_t* out) {
+    if (!C || !out || n < 0) return RSC_ERR_ARG;
+    if (n == 0) return RSC_OK;
+    RSC_HIP(hipSetDevice(C->device));
+    RngStream r;
+    r.seed(seed);
+    int done = 0;
+    DevBuf<int32_t> d;
+    if (int e = d.ensure(std::min(n, 8192))) return e;
+    while (done < n) {
+        const int chunk = std::min(8192, n - done);
+        r.ensure(C->table, chunk);
+        RSC_HIP(launch_rng_stream(C->d_table.p, r.window, r.g, chunk, d.p, C->stream));
+        RSC_HIP(hipMemcpyAsync(out + done, d.p, (size_t)chunk * 4, hipMemcpyDeviceToHost, C->stream));
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        r.g += chunk;
+        done += chunk;
+    }
+    return RSC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,835 @@
+// rsc_core.h — per-lane numeric core of the MI355X RANSAC pose engine.
+//
+// Every function here runs in ONE lane for ONE hypothesis (SIMT over hypotheses, see DESIGN.md
+// "Kernel mapping").  Small matrices live in VGPRs with compile-time indices (all loops with
+// static bounds are unrolled; data-dependent loops are written as unrolled, predicated sweeps so
+// that no register array is ever indexed dynamically).  The 12x12 symmetric eigenproblem of EPnP
+// lives in a per-lane LDS slab (LaneMat, element-major: element e of lane l at base[e*stride + l],
+// so a wave's 64 lanes touch 64 consecutive doubles — conflict-free ds_read_b64/ds_write_b64).
+//
+// Algorithms follow the reference solvers (src/PnPsolver.cpp, src/Sim3Solver.cpp) and the Eigen
+// routines they call (SelfAdjointEigenSolver, JacobiSVD+ColPivHouseholderQR, Matrix3d::inverse,
+// Quaternion::toRotationMatrix).  Arithmetic contract: every sum left to right in index
+// order, no FMA contraction (compiled with -ffp-contract=off), IEEE-correct division and sqrt.
+//
+// The header is also compiled for the host by the test-only emulation library
+// (tests/hostemu/), so the device arithmetic can be checked against the oracle on a CPU.
+#pragma once
+#include <cstdint>
+#include <cfloat>
+#include <cmath>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RSC_HD __host__ __device__ __forceinline__
+#else
+#define RSC_HD inline
+#endif
+#define RSC_UNROLL _Pragma("unroll")
+
+namespace rsc {
+
+template <typename S> struct lim;
+template <> struct lim<double> {
+    RSC_HD static double eps() { return 2.220446049250313080847e-16; }
+    RSC_HD static double min() { return 2.2250738585072013830903e-308; }
+};
+template <> struct lim<float> {
+    RSC_HD static float eps() { return 1.1920928955078125e-07f; }
+    RSC_HD static float min() { return 1.17549435082228750797e-38f; }
+};
+
+RSC_HD double rsqrt_(double x) { return sqrt(x); }
+RSC_HD float rsqrt_(float x) { return sqrtf(x); }
+RSC_HD double rabs(double x) { return fabs(x); }
+RSC_HD float rabs(float x) { return fabsf(x); }
+template <typename T> RSC_HD void rswap(T& a, T& b) { T t = a; a = b; b = t; }
+
+// Per-lane strided view of an LDS (or host) slab.
+struct LaneMat {
+    double* base;
+    int stride;
+    RSC_HD double& operator()(int e) const { return base[e * stride]; }
+    RSC_HD double& at(int r, int c) const { return base[(r * 12 + c) * stride]; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Eigen building blocks (Jacobi.h, MathFunctions.h)
+// ---------------------------------------------------------------------------------------------
+template <typename S> RSC_HD S eig_hypot(S x, S y) {
+    S ax = rabs(x), ay = rabs(y), p, qp;
+    if (ax > ay) { p = ax; qp = ay / p; } else { p = ay; qp = ax / p; }
+    if (p == S(0)) return S(0);
+    return p * rsqrt_(S(1) + qp * qp);
+}
+
+template <typename S> RSC_HD void make_givens(S p, S q, S& c, S& s) {
+    if (q == S(0)) {
+        c = p < S(0) ? S(-1) : S(1);
+        s = S(0);
+    } else if (p == S(0)) {
+        c = S(0);
+        s = q < S(0) ? S(1) : S(-1);
+    } else if (rabs(p) > rabs(q)) {
+        S t = q / p;
+        S u = rsqrt_(S(1) + t * t);
+        if (p < S(0)) u = -u;
+        c = S(1) / u;
+        s = -t * c;
+    } else {
+        S t = p / q;
+        S u = rsqrt_(S(1) + t * t);
+        if (q < S(0)) u = -u;
+        s = -S(1) / u;
+        c = -t * s;
+    }
+}
+
+// Implicit symmetric QR iterations on (diag, sub) with the rotations handed to `qapply(k,c,s)`
+// (which must perform Q = Q * G on columns k,k+1).  computeFromTridiagonal_impl + sort.
+// Returns Eigen's "Success".  perm receives nothing: the sort is performed through `qswap(i,j)`.
+template <typename S, int n, typename QApply, typename QSwap>
+RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply qapply, QSwap qswap) {
+    const int maxIterations = 30;
+    int end = n - 1, start = 0, iter = 0;
+    const S considerAsZero = lim<S>::min();
+    const S precision_inv = S(1) / lim<S>::eps();
+    while (end > 0) {
+        RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
+            if (i >= start && i < end) {
+                if (rabs(sub[i]) < considerAsZero) {
+                    sub[i] = S(0);
+                } else {
+                    const S scaled = precision_inv * sub[i];
+                    if (scaled * scaled <= (rabs(diag[i]) + rabs(diag[i + 1]))) sub[i] = S(0);
+                }
+            }
+        }
+        RSC_UNROLL for (int i = n - 2; i >= 0; --i)
+            if (i == end - 1 && sub[i] == S(0)) end--;
+        if (end <= 0) break;
+        iter++;
+        if (iter > maxIterations * n) break;
+        start = end - 1;
+        RSC_UNROLL for (int i = n - 2; i >= 0; --i)
+            if (i == start - 1 && sub[i] != S(0)) start--;
+        // ---- tridiagonal_qr_step(diag, sub, start, end) ----
+        S dEm1 = S(0), dE = S(0), eE = S(0), dS = S(0), zS = S(0);
+        RSC_UNROLL for (int j = 1; j < n; ++j)
+            if (j == end) { dEm1 = diag[j - 1]; dE = diag[j]; eE = sub[j - 1]; }
+        RSC_UNROLL for (int j = 0; j < n - 1; ++j)
+            if (j == start) { dS = diag[j]; zS = sub[j]; }
+        S td = (dEm1 - dE) * S(0.5);
+        S e = eE;
+        S mu = dE;
+        if (td == S(0)) {
+            mu -= rabs(e);
+        } else {
+            S e2 = eE * eE;
+            S h = eig_hypot(td, e);
+            if (e2 == S(0))
+                mu -= (e / (td + (td > S(0) ? S(1) : S(-1)))) * (e / h);
+            else
+                mu -= e2 / (td + (td > S(0) ? h : -h));
+        }
+        S x = dS - mu;
+        S z = zS;
+        RSC_UNROLL for (int k = 0; k < n - 1; ++k) {
+            if (k >= start && k < end) {
+                S c, s;
+                make_givens(x, z, c, s);
+                S sdk = s * diag[k] + c * sub[k];
+                S dkp1 = s * sub[k] + c * diag[k + 1];
+                diag[k] = c * (c * diag[k] - s * sub[k]) - s * (c * sub[k] - s * diag[k + 1]);
+                diag[k + 1] = s * sdk + c * dkp1;
+                sub[k] = c * sdk - s * dkp1;
+                if (k > 0 && k > start) sub[k - 1] = c * sub[k - 1] - s * z;
+                x = sub[k];
+                if (k < n - 2 && k < end - 1) {
+                    z = -s * sub[k + 1];
+                    sub[k + 1] = c * sub[k + 1];
+                }
+                if (!(c == S(1) && s == S(0))) qapply(k, c, s);
+            }
+        }
+    }
+    const bool ok = (iter <= maxIterations * n);
+    if (ok) {
+        RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
+            int kk = 0;
+            S mn = diag[i];
+            RSC_UNROLL for (int j = 1; j < n - i; ++j)
+                if (diag[i + j] < mn) { mn = diag[i + j]; kk = j; }
+            if (kk > 0) {
+                RSC_UNROLL for (int j = 1; j < n - i; ++j)
+                    if (j == kk) { rswap(diag[i], diag[i + j]); qswap(i, i + j); }
+            }
+        }
+    }
+    return ok;
+}
+
+// Householder reflector of a register vector v[0..len) (MatrixBase::makeHouseholder).
+template <typename S, int len>
+RSC_HD void make_householder(S (&v)[len], S& tau, S& beta) {
+    S tail = S(0);
+    if (len > 1) {
+        tail = v[1] * v[1];
+        RSC_UNROLL for (int k = 2; k < len; ++k) tail = tail + v[k] * v[k];
+    }
+    S c0 = v[0];
+    if (tail <= lim<S>::min()) {
+        tau = S(0);
+        beta = c0;
+        RSC_UNROLL for (int k = 1; k < len; ++k) v[k] = S(0);
+    } else {
+        beta = rsqrt_(c0 * c0 + tail);
+        if (c0 >= S(0)) beta = -beta;
+        S den = c0 - beta;
+        RSC_UNROLL for (int k = 1; k < len; ++k) v[k] = v[k] / den;
+        tau = (beta - c0) / beta;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// SelfAdjointEigenSolver<Matrix<S,n,n>>::compute, register version (n = 3 or 4).
+// A: lower triangle read.  V: eigenvectors in columns (ascending).  Returns "Success".
+// ---------------------------------------------------------------------------------------------
+template <typename S, int n>
+RSC_HD bool sym_eig_reg(const S (&A)[n][n], S (&V)[n][n], S (&w)[n]) {
+    S mat[n][n];
+    RSC_UNROLL for (int i = 0; i < n; ++i)
+        RSC_UNROLL for (int j = 0; j < n; ++j) mat[i][j] = (i >= j) ? A[i][j] : S(0);
+    S scale = rabs(mat[0][0]);
+    RSC_UNROLL for (int j = 0; j < n; ++j)
+        RSC_UNROLL for (int i = 0; i < n; ++i) {
+            if (i == 0 && j == 0) continue;
+            S v = rabs(mat[i][j]);
+            if (v > scale) scale = v;
+        }
+    if (scale == S(0)) scale = S(1);
+    RSC_UNROLL for (int j = 0; j < n; ++j)
+        RSC_UNROLL for (int i = j; i < n; ++i) mat[i][j] = mat[i][j] / scale;
+    S diag[n], sub[n - 1];
+    if (n == 3) {
+        diag[0] = mat[0][0];
+        S v1norm2 = mat[2][0] * mat[2][0];
+        if (v1norm2 <= lim<S>::min()) {
+            diag[1] = mat[1][1];
+            diag[2] = mat[2][2];
+            sub[0] = mat[1][0];
+            sub[1] = mat[2][1];
+            RSC_UNROLL for (int i = 0; i < n; ++i)
+                RSC_UNROLL for (int j = 0; j < n; ++j) V[i][j] = (i == j) ? S(1) : S(0);
+        } else {
+            S beta = rsqrt_(mat[1][0] * mat[1][0] + v1norm2);
+            S invBeta = S(1) / beta;
+            S m01 = mat[1][0] * invBeta;
+            S m02 = mat[2][0] * invBeta;
+            S q = S(2) * m01 * mat[2][1] + m02 * (mat[2][2] - mat[1][1]);
+            diag[1] = mat[1][1] + m02 * q;
+            diag[2] = mat[2][2] - m02 * q;
+            sub[0] = beta;
+            sub[1] = mat[2][1] - m01 * q;
+            V[0][0] = S(1); V[0][1] = S(0); V[0][2] = S(0);
+            V[1][0] = S(0); V[1][1] = m01;  V[1][2] = m02;
+            V[2][0] = S(0); V[2][1] = m02;  V[2][2] = -m01;
+        }
+    } else {
+        S hC[n];
+        RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
+            const int rs = n - i - 1;
+            S v[n], hc[n], w2[n];
+            RSC_UNROLL for (int k = 0; k < n; ++k) v[k] = S(0);
+            RSC_UNROLL for (int k = 0; k < n; ++k) if (k < rs) v[k] = mat[i + 1 + k][i];
+            // makeHouseholder on v[0..rs)
+            S tail = S(0);
+            if (rs > 1) {
+                tail = v[1] * v[1];
+                RSC_UNROLL for (int k = 2; k < n; ++k) if (k < rs) tail = tail + v[k] * v[k];
+            }
+            S c0 = v[0], h, beta;
+            if (tail <= lim<S>::min()) {
+                h = S(0);
+                beta = c0;
+                RSC_UNROLL for (int k = 1; k < n; ++k) if (k < rs) v[k] = S(0);
+            } else {
+                beta = rsqrt_(c0 * c0 + tail);
+                if (c0 >= S(0)) beta = -beta;
+                S den = c0 - beta;
+                RSC_UNROLL for (int k = 1; k < n; ++k) if (k < rs) v[k] = v[k] / den;
+                h = (beta - c0) / beta;
+            }
+            v[0] = S(1);
+            RSC_UNROLL for (int k = 1; k < n; ++k) if (k < rs) mat[i + 1 + k][i] = v[k];
+            RSC_UNROLL for (int k = 0; k < n; ++k) w2[k] = h * v[k];
+            RSC_UNROLL for (int k = 0; k < n; ++k) {
+                if (k < rs) {
+                    S acc = S(0);
+                    RSC_UNROLL for (int m = 0; m < n; ++m) {
+                        if (m < rs) {
+                            const int r = i + 1 + k, c = i + 1 + m;
+                            S a = (r >= c) ? mat[r][c] : mat[c][r];
+                            acc = (m == 0) ? a * w2[m] : acc + a * w2[m];
+                        }
+                    }
+                    hc[k] = acc;
+                }
+            }
+            S dot = hc[0] * v[0];
+            RSC_UNROLL for (int k = 1; k < n; ++k) if (k < rs) dot = dot + hc[k] * v[k];
+            S alpha = (h * S(-0.5)) * dot;
+            RSC_UNROLL for (int k = 0; k < n; ++k) if (k < rs) hc[k] = hc[k] + alpha * v[k];
+            RSC_UNROLL for (int c = 0; c < n; ++c) {
+                if (c < rs) {
+                    S s1 = -v[c], s2 = -hc[c];
+                    RSC_UNROLL for (int r = 0; r < n; ++r)
+                        if (r >= c && r < rs) {
+                            S& a = mat[i + 1 + r][i + 1 + c];
+                            a = a + (s1 * hc[r] + s2 * v[r]);
+                        }
+                }
+            }
+            mat[i + 1][i] = beta;
+            hC[i] = h;
+        }
+        RSC_UNROLL for (int k = 0; k < n; ++k) diag[k] = mat[k][k];
+        RSC_UNROLL for (int k = 0; k < n - 1; ++k) sub[k] = mat[k + 1][k];
+        // Householder sequence evalTo, in place (diag=1, strictly upper=0, reverse application)
+        RSC_UNROLL for (int i = 0; i < n; ++i) {
+            mat[i][i] = S(1);
+            RSC_UNROLL for (int j = 0; j < n; ++j) if (j > i) mat[i][j] = S(0);
+        }
+        RSC_UNROLL for (int k = n - 2; k >= 0; --k) {
+            const int cs = n - k - 1, b0 = k + 1;
+            const S tau = hC[k];
+            if (cs == 1) {
+                mat[b0][b0] = mat[b0][b0] * (S(1) - tau);
+            } else if (tau != S(0)) {
+                S tmp[n];
+                RSC_UNROLL for (int c = 0; c < n; ++c) {
+                    if (c < cs) {
+                        S acc = mat[k + 2][k] * mat[b0 + 1][b0 + c];
+                        RSC_UNROLL for (int r = 1; r < n; ++r)
+                            if (r < cs - 1) acc = acc + mat[k + 2 + r][k] * mat[b0 + 1 + r][b0 + c];
+                        tmp[c] = acc + mat[b0][b0 + c];
+                    }
+                }
+                RSC_UNROLL for (int c = 0; c < n; ++c) if (c < cs) mat[b0][b0 + c] = mat[b0][b0 + c] - tau * tmp[c];
+                RSC_UNROLL for (int r = 0; r < n; ++r) {
+                    if (r < cs - 1) {
+                        S te = tau * mat[k + 2 + r][k];
+                        RSC_UNROLL for (int c = 0; c < n; ++c)
+                            if (c < cs) mat[b0 + 1 + r][b0 + c] = mat[b0 + 1 + r][b0 + c] - tmp[c] * te;
+                    }
+                }
+            }
+            RSC_UNROLL for (int r = 0; r < n; ++r) if (r > k) mat[r][k] = S(0);
+        }
+        RSC_UNROLL for (int i = 0; i < n; ++i)
+            RSC_UNROLL for (int j = 0; j < n; ++j) V[i][j] = mat[i][j];
+    }
+    auto qapply = [&](int k, S c, S s) {
+        RSC_UNROLL for (int i = 0; i < n; ++i) {
+            S xi = V[i][k], yi = V[i][k + 1];
+            V[i][k] = c * xi - s * yi;
+            V[i][k + 1] = s * xi + c * yi;
+        }
+    };
+    auto qswap = [&](int a, int b) {
+        RSC_UNROLL for (int r = 0; r < n; ++r) rswap(V[r][a], V[r][b]);
+    };
+    bool ok = tridiag_qr<S, n>(diag, sub, qapply, qswap);
+    RSC_UNROLL for (int i = 0; i < n; ++i) w[i] = diag[i] * scale;
+    return ok;
+}
+
+// ---------------------------------------------------------------------------------------------
+// 12x12 SelfAdjointEigenSolver::compute with the matrix in a per-lane LDS slab (LaneMat, row-major
+// e = r*12 + c).  On entry the lower triangle holds MtM; on exit the slab holds the eigenvectors
+// (columns, ascending eigenvalues).  Only the eigenvector matrix is needed by EPnP.
+// ---------------------------------------------------------------------------------------------
+RSC_HD bool sym_eig12(const LaneMat& M) {
+    constexpr int n = 12;
+    // mat = lower triangle (upper zeroed); scale = max |.| in column-major order
+    double scale = rabs(M.at(0, 0));
+    RSC_UNROLL for (int j = 0; j < n; ++j)
+        RSC_UNROLL for (int i = 0; i < n; ++i) {
+            if (i < j) { M.at(i, j) = 0.0; continue; }
+            if (i == 0 && j == 0) continue;
+            double v = rabs(M.at(i, j));
+            if (v > scale) scale = v;
+        }
+    if (scale == 0.0) scale = 1.0;
+    RSC_UNROLL for (int j = 0; j < n; ++j)
+        RSC_UNROLL for (int i = j; i < n; ++i) M.at(i, j) = M.at(i, j) / scale;
+
+    double hC[n - 1];
+    RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
+        constexpr int NN = n - 1;
+        const int rs = n - i - 1;
+        double v[NN], w2[NN], hc[NN];
+        RSC_UNROLL for (int k = 0; k < NN; ++k) v[k] = (k < rs) ? M.at(i + 1 + k, i) : 0.0;
+        double tail = 0.0;
+        if (rs > 1) {
+            tail = v[1] * v[1];
+            RSC_UNROLL for (int k = 2; k < NN; ++k) if (k < rs) tail = tail + v[k] * v[k];
+        }
+        double c0 = v[0], h, beta;
+        if (tail <= lim<double>::min()) {
+            h = 0.0;
+            beta = c0;
+            RSC_UNROLL for (int k = 1; k < NN; ++k) if (k < rs) v[k] = 0.0;
+        } else {
+            beta = sqrt(c0 * c0 + tail);
+            if (c0 >= 0.0) beta = -beta;
+            double den = c0 - beta;
+            RSC_UNROLL for (int k = 1; k < NN; ++k) if (k < rs) v[k] = v[k] / den;
+            h = (beta - c0) / beta;
+        }
+        v[0] = 1.0;
+        RSC_UNROLL for (int k = 1; k < NN; ++k) if (k < rs) M.at(i + 1 + k, i) = v[k];
+        RSC_UNROLL for (int k = 0; k < NN; ++k) w2[k] = h * v[k];
+        RSC_UNROLL for (int k = 0; k < NN; ++k) {
+            if (k < rs) {
+                double acc = 0.0;
+                RSC_UNROLL for (int m = 0; m < NN; ++m) {
+                    if (m < rs) {
+                        const int r = i + 1 + k, c = i + 1 + m;
+                        double a = (r >= c) ? M.at(r, c) : M.at(c, r);
+                        acc = (m == 0) ? a * w2[m] : acc + a * w2[m];
+                    }
+                }
+                hc[k] = acc;
+            }
+        }
+        double dot = hc[0] * v[0];
+        RSC_UNROLL for (int k = 1; k < NN; ++k) if (k < rs) dot = dot + hc[k] * v[k];
+        double alpha = (h * -0.5) * dot;
+        RSC_UNROLL for (int k = 0; k < NN; ++k) if (k < rs) hc[k] = hc[k] + alpha * v[k];
+        RSC_UNROLL for (int c = 0; c < NN; ++c) {
+            if (c < rs) {
+                double s1 = -v[c], s2 = -hc[c];
+                RSC_UNROLL for (int r = 0; r < NN; ++r)
+                    if (r >= c && r < rs) {
+                        double& a = M.at(i + 1 + r, i + 1 + c);
+                        a = a + (s1 * hc[r] + s2 * v[r]);
+                    }
+            }
+        }
+        M.at(i + 1, i) = beta;
+        hC[i] = h;
+    }
+    double diag[n], sub[n - 1];
+    RSC_UNROLL for (int k = 0; k < n; ++k) diag[k] = M.at(k, k);
+    RSC_UNROLL for (int k = 0; k < n - 1; ++k) sub[k] = M.at(k + 1, k);
+    RSC_UNROLL for (int i = 0; i < n; ++i) {
+        M.at(i, i) = 1.0;
+        RSC_UNROLL for (int j = i + 1; j < n; ++j) M.at(i, j) = 0.0;
+    }
+    RSC_UNROLL for (int k = n - 2; k >= 0; --k) {
+        const int cs = n - k - 1, b0 = k + 1;
+        const double tau = hC[k];
+        if (cs == 1) {
+            M.at(b0, b0) = M.at(b0, b0) * (1.0 - tau);
+        } else if (tau != 0.0) {
+            double tmp[n - 1];
+            RSC_UNROLL for (int c = 0; c < n - 1; ++c) {
+                if (c < cs) {
+                    double acc = M.at(k + 2, k) * M.at(b0 + 1, b0 + c);
+                    RSC_UNROLL for (int r = 1; r < n - 1; ++r)
+                        if (r < cs - 1) acc = acc + M.at(k + 2 + r, k) * M.at(b0 + 1 + r, b0 + c);
+                    tmp[c] = acc + M.at(b0, b0 + c);
+                }
+            }
+            RSC_UNROLL for (int c = 0; c < n - 1; ++c) if (c < cs) M.at(b0, b0 + c) = M.at(b0, b0 + c) - tau * tmp[c];
+            RSC_UNROLL for (int r = 0; r < n - 1; ++r) {
+                if (r < cs - 1) {
+                    double te = tau * M.at(k + 2 + r, k);
+                    RSC_UNROLL for (int c = 0; c < n - 1; ++c)
+                        if (c < cs) M.at(b0 + 1 + r, b0 + c) = M.at(b0 + 1 + r, b0 + c) - tmp[c] * te;
+                }
+            }
+        }
+        RSC_UNROLL for (int r = k + 1; r < n; ++r) M.at(r, k) = 0.0;
+    }
+    auto qapply = [&](int k, double c, double s) {
+        RSC_UNROLL for (int i = 0; i < n; ++i) {
+            double xi = M.at(i, k), yi = M.at(i, k + 1);
+            M.at(i, k) = c * xi - s * yi;
+            M.at(i, k + 1) = s * xi + c * yi;
+        }
+    };
+    auto qswap = [&](int a, int b) {
+        RSC_UNROLL for (int r = 0; r < n; ++r) rswap(M.at(r, a), M.at(r, b));
+    };
+    return tridiag_qr<double, n>(diag, sub, qapply, qswap);
+}
+
+// ---------------------------------------------------------------------------------------------
+// JacobiSVD<MatrixXd>(A 6xk, ThinU|ThinV).solve(b) — see oracle/ora_linalg.h for the structure.
+// ---------------------------------------------------------------------------------------------
+template <int k>
+RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6], double (&x)[k]) {
+    constexpr int rows = 6;
+    const double eps = lim<double>::eps();
+    const double precision = 2.0 * eps;
+    const double considerAsZero = lim<double>::min();
+    double scale = rabs(Ain[0][0]);
+    RSC_UNROLL for (int c = 0; c < k; ++c)
+        RSC_UNROLL for (int r = 0; r < rows; ++r) {
+            if (r == 0 && c == 0) continue;
+            double v = rabs(Ain[r][c]);
+            if (v > scale) scale = v;
+        }
+    if (scale == 0.0) scale = 1.0;
+    double qr[rows][k];
+    RSC_UNROLL for (int r = 0; r < rows; ++r)
+        RSC_UNROLL for (int c = 0; c < k; ++c) qr[r][c] = Ain[r][c] / scale;
+    double hCoeffs[k], nU[k], nD[k];
+    int perm[k];
+    RSC_UNROLL for (int c = 0; c < k; ++c) {
+        double s = qr[0][c] * qr[0][c];
+        RSC_UNROLL for (int r = 1; r < rows; ++r) s = s + qr[r][c] * qr[r][c];
+        nD[c] = sqrt(s);
+        nU[c] = nD[c];
+        perm[c] = c;
+    }
+    const double ndt = sqrt(eps);
+    RSC_UNROLL for (int kk = 0; kk < k; ++kk) {
+        int big = kk;
+        double bv = nU[kk];
+        RSC_UNROLL for (int c = kk + 1; c < k; ++c)
+            if (nU[c] > bv) { bv = nU[c]; big = c; }
+        // transposition kk <-> big: swap columns, norms, and the permutation indices
+        RSC_UNROLL for (int c = kk + 1; c < k; ++c) {
+            if (c == big) {
+                RSC_UNROLL for (int r = 0; r < rows; ++r) rswap(qr[r][kk], qr[r][c]);
+                rswap(nU[kk], nU[c]);
+                rswap(nD[kk], nD[c]);
+                rswap(perm[kk], perm[c]);
+            }
+        }
+        // Householder of qr[kk..5][kk]
+        constexpr int L = rows;
+        double v[L];
+        RSC_UNROLL for (int r = 0; r < L; ++r) v[r] = 0.0;
+        RSC_UNROLL for (int r = 0; r < L; ++r) if (r < rows - kk) v[r] = qr[kk + r][kk];
+        double tail = 0.0;
+        const int len = rows - kk;
+        if (len > 1) {
+            tail = v[1] * v[1];
+            RSC_UNROLL for (int r = 2; r < L; ++r) if (r < len) tail = tail + v[r] * v[r];
+        }
+        double c0 = v[0], tau, beta;
+        if (tail <= considerAsZero) {
+            tau = 0.0;
+            beta = c0;
+            RSC_UNROLL for (int r = 1; r < L; ++r) if (r < len) v[r] = 0.0;
+        } else {
+            beta = sqrt(c0 * c0 + tail);
+            if (c0 >= 0.0) beta = -beta;
+            double den = c0 - beta;
+            RSC_UNROLL for (int r = 1; r < L; ++r) if (r < len) v[r] = v[r] / den;
+            tau = (beta - c0) / beta;
+        }
+        hCoeffs[kk] = tau;
+        qr[kk][kk] = beta;
+        RSC_UNROLL for (int r = 1; r < L; ++r) if (r < len) qr[kk + r][kk] = v[r];
+        const int bc = k - kk - 1;
+        if (bc > 0 && tau != 0.0) {
+            double tmp[k];
+            RSC_UNROLL for (int c = 0; c < k; ++c) {
+                if (c < bc) {
+                    double acc = qr[kk + 1][kk] * qr[kk + 1][kk + 1 + c];
+                    RSC_UNROLL for (int r = 2; r < rows; ++r)
+                        if (r < len) acc = acc + qr[kk + r][kk] * qr[kk + r][kk + 1 + c];
+                    tmp[c] = acc + qr[kk][kk + 1 + c];
+                }
+            }
+            RSC_UNROLL for (int c = 0; c < k; ++c) if (c < bc) qr[kk][kk + 1 + c] = qr[kk][kk + 1 + c] - tau * tmp[c];
+            RSC_UNROLL for (int r = 1; r < rows; ++r) {
+                if (r < len) {
+                    double te = tau * qr[kk + r][kk];
+                    RSC_UNROLL for (int c = 0; c < k; ++c)
+                        if (c < bc) qr[kk + r][kk + 1 + c] = qr[kk + r][kk + 1 + c] - tmp[c] * te;
+                }
+            }
+        }
+        RSC_UNROLL for (int j = kk + 1; j < k; ++j) {
+            if (nU[j] != 0.0) {
+                double temp = rabs(qr[kk][j]) / nU[j];
+                temp = (1.0 + temp) * (1.0 - temp);
+                temp = temp < 0.0 ? 0.0 : temp;
+                double q = nU[j] / nD[j];
+                double temp2 = temp * (q * q);
+                if (temp2 <= ndt) {
+                    double s = 0.0;
+                    if (kk + 1 < rows) {
+                        s = qr[kk + 1][j] * qr[kk + 1][j];
+                        RSC_UNROLL for (int r = kk + 2; r < rows; ++r) s = s + qr[r][j] * qr[r][j];
+                    }
+                    nD[j] = sqrt(s);
+                    nU[j] = nD[j];
+                } else {
+                    nU[j] *= sqrt(temp);
+                }
+            }
+        }
+    }
+    double W[k][k], U[rows][k], V[k][k];
+    RSC_UNROLL for (int r = 0; r < k; ++r)
+        RSC_UNROLL for (int c = 0; c < k; ++c) W[r][c] = (c >= r) ? qr[r][c] : 0.0;
+    RSC_UNROLL for (int r = 0; r < rows; ++r)
+        RSC_UNROLL for (int c = 0; c < k; ++c) U[r][c] = (r == c) ? 1.0 : 0.0;
+    RSC_UNROLL for (int kk = k - 1; kk >= 0; --kk) {
+        const double tau = hCoeffs[kk];
+        const int len = rows - kk;
+        if (tau != 0.0) {
+            double tmp[k];
+            RSC_UNROLL for (int c = 0; c < k; ++c) {
+                double acc = qr[kk + 1][kk] * U[kk + 1][c];
+                RSC_UNROLL for (int r = 2; r < rows; ++r) if (r < len) acc = acc + qr[kk + r][kk] * U[kk + r][c];
+                tmp[c] = acc + U[kk][c];
+            }
+            RSC_UNROLL for (int c = 0; c < k; ++c) U[kk][c] = U[kk][c] - tau * tmp[c];
+            RSC_UNROLL for (int r = 1; r < rows; ++r) {
+                if (r < len) {
+                    double te = tau * qr[kk + r][kk];
+                    RSC_UNROLL for (int c = 0; c < k; ++c) U[kk + r][c] = U[kk + r][c] - tmp[c] * te;
+                }
+            }
+        }
+    }
+    RSC_UNROLL for (int r = 0; r < k; ++r)
+        RSC_UNROLL for (int c = 0; c < k; ++c) V[r][c] = (perm[c] == r) ? 1.0 : 0.0;
+
+    double maxDiag = rabs(W[0][0]);
+    RSC_UNROLL for (int i = 1; i < k; ++i) if (rabs(W[i][i]) > maxDiag) maxDiag = rabs(W[i][i]);
+    bool finished = false;
+    while (!finished) {
+        finished = true;
+        RSC_UNROLL for (int p = 1; p < k; ++p) {
+            RSC_UNROLL for (int q = 0; q < p; ++q) {
+                double pt = precision * maxDiag;
+                double threshold = (considerAsZero < pt) ? pt : considerAsZero;
+                if (rabs(W[p][q]) > threshold || rabs(W[q][p]) > threshold) {
+                    finished = false;
+                    double m00 = W[p][p], m01 = W[p][q], m10 = W[q][p], m11 = W[q][q];
+                    double c1, s1;
+                    double t = m00 + m11;
+                    double d = m10 - m01;
+                    if (rabs(d) < considerAsZero) {
+                        s1 = 0.0; c1 = 1.0;
+                    } else {
+                        double u = t / d;
+                        double tmp = sqrt(1.0 + u * u);
+                        s1 = 1.0 / tmp;
+                        c1 = u / tmp;
+                    }
+                    if (!(c1 == 1.0 && s1 == 0.0)) {
+                        double x0 = m00, y0 = m10, x1 = m01, y1 = m11;
+                        m00 = c1 * x0 + s1 * y0; m10 = -s1 * x0 + c1 * y0;
+                        m01 = c1 * x1 + s1 * y1; m11 = -s1 * x1 + c1 * y1;
+                    }
+                    double cr, sr;
+                    {
+                        double deno = 2.0 * rabs(m01);
+                        if (deno < considerAsZero) {
+                            cr = 1.0; sr = 0.0;
+                        } else {
+                            double tau = (m00 - m11) / deno;
+                            double w = sqrt(tau * tau + 1.0);
+                            double tt;
+                            if (tau > 0.0) tt = 1.0 / (tau + w); else tt = 1.0 / (tau - w);
+                            double sign_t = tt > 0.0 ? 1.0 : -1.0;
+                            double nn = 1.0 / sqrt(tt * tt + 1.0);
+                            sr = -sign_t * (m01 / rabs(m01)) * rabs(tt) * nn;
+                            cr = nn;
+                        }
+                    }
+                    double crt = cr, srt = -sr;
+                    double cl = c1 * crt - s1 * srt;
+                    double sl = c1 * srt + s1 * crt;
+                    if (!(cl == 1.0 && sl == 0.0)) {
+                        RSC_UNROLL for (int c = 0; c < k; ++c) {
+                            double xi = W[p][c], yi = W[q][c];
+                            W[p][c] = cl * xi + sl * yi;
+                            W[q][c] = -sl * xi + cl * yi;
+                        }
+                        RSC_UNROLL for (int r = 0; r < rows; ++r) {
+                            double xi = U[r][p], yi = U[r][q];
+                            U[r][p] = cl * xi + sl * yi;
+                            U[r][q] = -sl * xi + cl * yi;
+                        }
+                    }
+                    if (!(cr == 1.0 && sr == 0.0)) {
+                        RSC_UNROLL for (int r = 0; r < k; ++r) {
+                            double xi = W[r][p], yi = W[r][q];
+                            W[r][p] = cr * xi - sr * yi;
+                            W[r][q] = sr * xi + cr * yi;
+                        }
+                        RSC_UNROLL for (int r = 0; r < k; ++r) {
+                            double xi = V[r][p], yi = V[r][q];
+                            V[r][p] = cr * xi - sr * yi;
+                            V[r][q] = sr * xi + cr * yi;
+                        }
+                    }
+                    double a = rabs(W[p][p]), bq = rabs(W[q][q]);
+                    double mm = (a < bq) ? bq : a;
+                    maxDiag = (maxDiag < mm) ? mm : maxDiag;
+                }
+            }
+        }
+    }
+    double sv[k];
+    RSC_UNROLL for (int i = 0; i < k; ++i) {
+        double a = W[i][i];
+        sv[i] = rabs(a);
+        if (a < 0.0) RSC_UNROLL for (int r = 0; r < rows; ++r) U[r][i] = -U[r][i];
+    }
+    RSC_UNROLL for (int i = 0; i < k; ++i) sv[i] = sv[i] * scale;
+    int nonzero = k;
+    bool stop = false;
+    RSC_UNROLL for (int i = 0; i < k; ++i) {
+        if (!stop) {
+            int pos = 0;
+            double mv = sv[i];
+            RSC_UNROLL for (int j = 1; j < k; ++j)
+                if (j < k - i && sv[i + j] > mv) { mv = sv[i + j]; pos = j; }
+            if (mv == 0.0) {
+                nonzero = i;
+                stop = true;
+            } else if (pos) {
+                RSC_UNROLL for (int j = 1; j < k; ++j) {
+                    if (j == pos && i + j < k) {
+                        rswap(sv[i], sv[i + j]);
+                        RSC_UNROLL for (int r = 0; r < rows; ++r) rswap(U[r][i + j], U[r][i]);
+                        RSC_UNROLL for (int r = 0; r < k; ++r) rswap(V[r][i + j], V[r][i]);
+                    }
+                }
+            }
+        }
+    }
+    double thr = sv[0] * ((double)k * eps);
+    double premult = (thr < considerAsZero) ? considerAsZero : thr;
+    // SVDBase::rank(): i = nonzero-1; while (i >= 0 && sv[i] < premult) --i;
+    int i2 = nonzero - 1;
+    RSC_UNROLL for (int t = k - 1; t >= 0; --t)
+        if (t == i2 && sv[t] < premult) i2--;
+    const int rank = i2 + 1;
+    double tmpv[k];
+    RSC_UNROLL for (int j = 0; j < k; ++j) {
+        if (j < rank) {
+            double acc = U[0][j] * b[0];
+            RSC_UNROLL for (int r = 1; r < rows; ++r) acc = acc + U[r][j] * b[r];
+            tmpv[j] = (1.0 / sv[j]) * acc;
+        }
+    }
+    RSC_UNROLL for (int r = 0; r < k; ++r) {
+        if (rank == 0) { x[r] = 0.0; continue; }
+        double acc = V[r][0] * tmpv[0];
+        RSC_UNROLL for (int j = 1; j < k; ++j) if (j < rank) acc = acc + V[r][j] * tmpv[j];
+        x[r] = acc;
+    }
+}
+
+// Matrix3d::inverse (cofactors); result(r,c) = cofactor(c,r) * invdet.
+RSC_HD void inverse3(const double (&m)[3][3], double (&o)[3][3]) {
+    double cof[3][3];
+    RSC_UNROLL for (int i = 0; i < 3; ++i)
+        RSC_UNROLL for (int j = 0; j < 3; ++j) {
+            const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+            cof[i][j] = m[i1][j1] * m[i2][j2] - m[i1][j2] * m[i2][j1];
+        }
+    double det = cof[0][0] * m[0][0] + cof[1][0] * m[1][0] + cof[2][0] * m[2][0];
+    double invdet = 1.0 / det;
+    RSC_UNROLL for (int r = 0; r < 3; ++r)
+        RSC_UNROLL for (int c = 0; c < 3; ++c) o[r][c] = cof[c][r] * invdet;
+}
+
+template <typename S>
+RSC_HD void quat_to_R(S w, S x, S y, S z, S (&R)[3][3]) {
+    const S tx = S(2) * x, ty = S(2) * y, tz = S(2) * z;
+    const S twx = tx * w, twy = ty * w, twz = tz * w;
+    const S txx = tx * x, txy = ty * x, txz = tz * x;
+    const S tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0][0] = S(1) - (tyy + tzz); R[0][1] = txy - twz;          R[0][2] = txz + twy;
+    R[1][0] = txy + twz;          R[1][1] = S(1) - (txx + tzz); R[1][2] = tyz - twx;
+    R[2][0] = txz - twy;          R[2][1] = tyz + twx;          R[2][2] = S(1) - (txx + tyy);
+}
+
+RSC_HD double det3(const double (&m)[3][3]) {
+    double h0 = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]);
+    double h1 = m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]);
+    double h2 = m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+    return h0 - h1 + h2;
+}
+
+// ---------------------------------------------------------------------------------------------
+// glibc TYPE_3 rand() stream, jump-ahead form.  The generator is linear over Z/2^32:
+//   r[i] = r[i-31] + r[i-3], output = r >> 1.
+// A problem's stream position is a 31-word window w = (r[m-31], ..., r[m-1]); the g-th next raw
+// word is r[m+g] = sum_j T[g][j] * w[j] (mod 2^32) with T built on the host (rsc_rng_table).
+// ---------------------------------------------------------------------------------------------
+RSC_HD uint32_t rng_word(const uint32_t* __restrict__ T /* [g][32] */, const uint32_t (&w)[31], int g) {
+    const uint32_t* t = T + (size_t)g * 32;
+    uint32_t acc = 0;
+    RSC_UNROLL for (int j = 0; j < 31; ++j) acc += t[j] * w[j];
+    return acc;
+}
+
+// DUtils::Random::RandomInt(0, size-1) given the raw word.
+RSC_HD int random_index(uint32_t word, int size) {
+    const int32_t r = (int32_t)(word >> 1);
+    return int(((double)r / ((double)2147483647 + 1.0)) * size);
+}
+
+// Swap-remove sampling of `ms` indices over [0,N) from a fresh index list (PnPsolver.cpp:125-138).
+template <int MAXS>
+RSC_HD void swap_remove_sample(const uint32_t* words, int ms, int N, int (&out)[MAXS]) {
+    int pos[MAXS], val[MAXS];
+    int nmod = 0;
+    RSC_UNROLL for (int i = 0; i < MAXS; ++i) {
+        if (i < ms) {
+            const int size = N - i;
+            const int randi = random_index(words[i], size);
+            auto lookup = [&](int p) {
+                int v = p;
+                RSC_UNROLL for (int t = 0; t < MAXS; ++t)
+                    if (t < nmod && pos[t] == p) v = val[t];
+                return v;
+            };
+            const int idx = lookup(randi);
+            out[i] = idx;
+            const int back = lookup(size - 1);
+            bool found = false;
+            RSC_UNROLL for (int t = 0; t < MAXS; ++t)
+                if (t < nmod && pos[t] == randi) { val[t] = back; found = true; }
+            if (!found) {
+                RSC_UNROLL for (int t = 0; t < MAXS; ++t)
+                    if (t == nmod) { pos[t] = randi; val[t] = back; }
+                nmod++;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// PnPsolver::CheckInliers for one correspondence (PnPsolver.cpp:245-266): float rotation,
+// float reciprocal, projection in double rounded to float, float squared error, strict '<'.
+// ---------------------------------------------------------------------------------------------
+RSC_HD bool pnp_inlier(const float (&R)[9], const float (&t)[3], double fx, double fy, double cx, double cy,
+                       float X, float Y, float Z, float u, float v, float maxErr) {
+    float Xc = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    float Yc = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    float Zc = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    float invZc = 1.0f / Zc;
+    float ue = (float)(cx + fx * (double)Xc * (double)invZc);
+    float ve = (float)(cy + fy * (double)Yc * (double)invZc);
+    float du = ue - u, dv = ve - v;
+    float e2 = du * du + dv * dv;
+    return e2 < maxErr;
+}
+
+}  // namespace rsc

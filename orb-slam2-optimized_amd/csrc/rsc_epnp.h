@@ -1,0 +1,427 @@
+// rsc_epnp.h — per-lane EPnP pose (PnPsolver::compute_pose, src/PnPsolver.cpp:359-415) and the
+// helpers it calls, written for one hypothesis per lane.
+//
+// Row storage is abstracted by a Store:
+//   HypStore<NS>: the NS sampled correspondences of a RANSAC hypothesis in VGPRs (static indices);
+//   RowStore:     all rows in global memory (Refine over the best inlier set, n up to N).
+// Both expose the reference's grow-only EPnP buffers (Q6): rows [n, rows) are the stale rows left
+// by earlier Refine() calls; every column sum over "all allocated rows" (PnPsolver.cpp:301, :356,
+// :435-436) reads them, exactly as the reference does.
+#pragma once
+#include "rsc_core.h"
+
+namespace rsc {
+
+struct Intrinsics {
+    double fx, fy, cx, cy;
+};
+
+// Free slots of the per-lane slab once the 12x12 eigenvectors are formed: columns 4..11 of every
+// row (96 doubles) plus 16 extra doubles after the matrix.  L_6x10 and rho live there.
+RSC_HD int slab_free(int q) { return q < 96 ? (q >> 3) * 12 + 4 + (q & 7) : 144 + (q - 96); }
+constexpr int kSlabDoubles = 160;  // per lane: 64 lanes x 160 x 8 B = 80 KiB per workgroup
+
+template <int NS>
+struct HypStore {
+    double pw_[NS][3], u_[NS][2], al_[NS][4];
+    int rows_;                      // maximum_number_of_correspondences
+    const double* __restrict__ spw;  // stale pws  [rows][3]   (global, rows >= NS read)
+    const double* __restrict__ sal;  // stale alphas [rows][4]
+    RSC_HD static constexpr int n() { return NS; }
+    RSC_HD int rows() const { return rows_; }
+    RSC_HD double pw(int i, int c) const { return pw_[i][c]; }
+    RSC_HD double u(int i, int c) const { return u_[i][c]; }
+    RSC_HD double al(int i, int j) const { return al_[i][j]; }
+    RSC_HD void set_al(int i, int j, double v) { al_[i][j] = v; }
+    RSC_HD double stale_pw(int i, int c) const { return spw[3 * i + c]; }
+    RSC_HD double stale_al(int i, int j) const { return sal[4 * i + j]; }
+};
+
+struct RowStore {
+    int n_, rows_;
+    double* __restrict__ pws;     // [rows][3]
+    const double* __restrict__ us; // [n][2]
+    double* __restrict__ als;     // [rows][4]
+    RSC_HD int n() const { return n_; }
+    RSC_HD int rows() const { return rows_; }
+    RSC_HD double pw(int i, int c) const { return pws[3 * i + c]; }
+    RSC_HD double u(int i, int c) const { return us[2 * i + c]; }
+    RSC_HD double al(int i, int j) const { return als[4 * i + j]; }
+    RSC_HD void set_al(int i, int j, double v) { als[4 * i + j] = v; }
+    RSC_HD double stale_pw(int i, int c) const { return pws[3 * i + c]; }
+    RSC_HD double stale_al(int i, int j) const { return als[4 * i + j]; }
+};
+
+// Column sum of pws over ALL allocated rows (current rows first, then stale rows).
+template <class St>
+RSC_HD double sum_pw_col(const St& st, int c) {
+    double s = st.pw(0, c);
+    RSC_UNROLL for (int i = 1; i < st.n(); ++i) s = s + st.pw(i, c);
+    for (int i = st.n(); i < st.rows(); ++i) s = s + st.stale_pw(i, c);
+    return s;
+}
+
+// choose_control_points + compute_barycentric_coordinates (PnPsolver.cpp:296-343).
+// Returns cws (4x3).
+template <class St>
+RSC_HD void control_points_and_alphas(St& st, double (&cws)[4][3]) {
+    const int n = st.n();
+    RSC_UNROLL for (int c = 0; c < 3; ++c) cws[0][c] = sum_pw_col(st, c);
+    RSC_UNROLL for (int c = 0; c < 3; ++c) cws[0][c] = cws[0][c] / n;
+    double A[3][3];
+    RSC_UNROLL for (int a = 0; a < 3; ++a)
+        RSC_UNROLL for (int b = 0; b < 3; ++b) {
+            double s = (st.pw(0, a) - cws[0][a]) * (st.pw(0, b) - cws[0][b]);
+            RSC_UNROLL for (int i = 1; i < n; ++i) s = s + (st.pw(i, a) - cws[0][a]) * (st.pw(i, b) - cws[0][b]);
+            A[a][b] = s;
+        }
+    double V[3][3], w[3];
+    sym_eig_reg<double, 3>(A, V, w);
+    RSC_UNROLL for (int i = 0; i < 3; ++i) {
+        double k = sqrt(w[i] / n);
+        RSC_UNROLL for (int c = 0; c < 3; ++c) cws[i + 1][c] = cws[0][c] + k * V[c][i];
+    }
+    double CC[3][3], CCi[3][3];
+    RSC_UNROLL for (int i = 0; i < 3; ++i)
+        RSC_UNROLL for (int j = 1; j < 4; ++j) CC[i][j - 1] = cws[j][i] - cws[0][i];
+    inverse3(CC, CCi);
+    RSC_UNROLL for (int i = 0; i < n; ++i) {
+        double d0 = st.pw(i, 0) - cws[0][0];
+        double d1 = st.pw(i, 1) - cws[0][1];
+        double d2 = st.pw(i, 2) - cws[0][2];
+        double a1 = CCi[0][0] * d0 + CCi[0][1] * d1 + CCi[0][2] * d2;
+        double a2 = CCi[1][0] * d0 + CCi[1][1] * d1 + CCi[1][2] * d2;
+        double a3 = CCi[2][0] * d0 + CCi[2][1] * d1 + CCi[2][2] * d2;
+        st.set_al(i, 1, a1);
+        st.set_al(i, 2, a2);
+        st.set_al(i, 3, a3);
+        st.set_al(i, 0, 1.0 - a1 - a2 - a3);
+    }
+}
+
+// Entry (r, col) of the 2n x 12 matrix M (PnPsolver.cpp:365-377).
+template <class St>
+RSC_HD double M_entry(const St& st, const Intrinsics& K, int r, int col) {
+    const int i = r >> 1, j = col / 3, s = col % 3;
+    const double a = st.al(i, j);
+    if ((r & 1) == 0) {
+        if (s == 0) return a * K.fx;
+        if (s == 1) return 0.0;
+        return a * (K.cx - st.u(i, 0));
+    } else {
+        if (s == 0) return 0.0;
+        if (s == 1) return a * K.fy;
+        return a * (K.cy - st.u(i, 1));
+    }
+}
+
+// Lower triangle of MtM = M^T M into the slab (sum over the 2n rows, first term first).
+template <class St>
+RSC_HD void build_MtM(const St& st, const Intrinsics& K, const LaneMat& S) {
+    const int rows2 = 2 * st.n();
+    RSC_UNROLL for (int a = 0; a < 12; ++a)
+        RSC_UNROLL for (int b = 0; b <= a; ++b) {
+            double s = M_entry(st, K, 0, a) * M_entry(st, K, 0, b);
+            RSC_UNROLL for (int r = 1; r < rows2; ++r) s = s + M_entry(st, K, r, a) * M_entry(st, K, r, b);
+            S.at(a, b) = s;
+        }
+}
+
+RSC_HD double& Lref(const LaneMat& S, int i, int j) { return S(slab_free(i * 10 + j)); }
+RSC_HD double& rhoref(const LaneMat& S, int i) { return S(slab_free(60 + i)); }
+
+// compute_L_6x10 (PnPsolver.cpp:604-637) from the eigenvector columns 0..3 held in the slab.
+RSC_HD void compute_L_6x10(const LaneMat& S) {
+    RSC_UNROLL for (int j = 0; j < 6; ++j) {
+        const int a = (j < 3) ? 0 : (j < 5 ? 1 : 2);
+        const int b = (j < 3) ? j + 1 : (j < 5 ? j - 1 : 3);
+        double dv[4][3];
+        RSC_UNROLL for (int i = 0; i < 4; ++i)
+            RSC_UNROLL for (int c = 0; c < 3; ++c) dv[i][c] = S.at(3 * a + c, i) - S.at(3 * b + c, i);
+        auto dot = [&](int x, int y) { return dv[x][0] * dv[y][0] + dv[x][1] * dv[y][1] + dv[x][2] * dv[y][2]; };
+        Lref(S, j, 0) = dot(0, 0);
+        Lref(S, j, 1) = 2.0 * dot(0, 1);
+        Lref(S, j, 2) = dot(1, 1);
+        Lref(S, j, 3) = 2.0 * dot(0, 2);
+        Lref(S, j, 4) = 2.0 * dot(1, 2);
+        Lref(S, j, 5) = dot(2, 2);
+        Lref(S, j, 6) = 2.0 * dot(0, 3);
+        Lref(S, j, 7) = 2.0 * dot(1, 3);
+        Lref(S, j, 8) = 2.0 * dot(2, 3);
+        Lref(S, j, 9) = dot(3, 3);
+    }
+}
+
+// qr_solve (PnPsolver.cpp:693-796).  Returns false on the singular bail-out (X left unchanged).
+RSC_HD bool qr_solve_6x4(double (&A)[6][4], double (&b)[6], double (&X)[4]) {
+    double A1[4], A2[4];
+    bool singular = false;
+    RSC_UNROLL for (int k = 0; k < 4; k++) {
+        if (!singular) {
+            double eta = rabs(A[k][k]);
+            RSC_UNROLL for (int i = k + 1; i < 6; i++) {
+                double elt = rabs(A[i][k]);
+                if (eta < elt) eta = elt;
+            }
+            if (eta == 0) {
+                singular = true;
+            } else {
+                double sum = 0.0, inv_eta = 1. / eta;
+                RSC_UNROLL for (int i = k; i < 6; i++) {
+                    A[i][k] *= inv_eta;
+                    sum += A[i][k] * A[i][k];
+                }
+                double sigma = sqrt(sum);
+                if (A[k][k] < 0) sigma = -sigma;
+                A[k][k] += sigma;
+                A1[k] = sigma * A[k][k];
+                A2[k] = -eta * sigma;
+                RSC_UNROLL for (int j = k + 1; j < 4; j++) {
+                    double s = 0;
+                    RSC_UNROLL for (int i = k; i < 6; i++) s += A[i][k] * A[i][j];
+                    double tau = s / A1[k];
+                    RSC_UNROLL for (int i = k; i < 6; i++) A[i][j] -= tau * A[i][k];
+                }
+            }
+        }
+    }
+    if (singular) return false;
+    RSC_UNROLL for (int j = 0; j < 4; j++) {
+        double tau = 0;
+        RSC_UNROLL for (int i = j; i < 6; i++) tau += A[i][j] * b[i];
+        tau /= A1[j];
+        RSC_UNROLL for (int i = j; i < 6; i++) b[i] -= tau * A[i][j];
+    }
+    X[3] = b[3] / A2[3];
+    RSC_UNROLL for (int i = 2; i >= 0; i--) {
+        double s = 0;
+        RSC_UNROLL for (int j = i + 1; j < 4; j++) s += A[i][j] * X[j];
+        X[i] = (b[i] - s) / A2[i];
+    }
+    return true;
+}
+
+// gauss_newton (PnPsolver.cpp:649-691); X persists across the 5 iterations (Q9).
+RSC_HD void gauss_newton(const LaneMat& S, double (&betas)[4]) {
+    double X[4] = {0.0, 0.0, 0.0, 0.0};
+    RSC_UNROLL for (int it = 0; it < 5; it++) {
+        double A[6][4], B[6];
+        RSC_UNROLL for (int i = 0; i < 6; i++) {
+            double l[10];
+            RSC_UNROLL for (int j = 0; j < 10; ++j) l[j] = Lref(S, i, j);
+            const double Lt[4][4] = {{2 * l[0], l[1], l[3], l[6]},
+                                     {l[1], 2 * l[2], l[4], l[7]},
+                                     {l[3], l[4], 2 * l[5], l[8]},
+                                     {l[6], l[7], l[8], 2 * l[9]}};
+            RSC_UNROLL for (int r = 0; r < 4; ++r)
+                A[i][r] = Lt[r][0] * betas[0] + Lt[r][1] * betas[1] + Lt[r][2] * betas[2] + Lt[r][3] * betas[3];
+            const double* b = betas;
+            B[i] = rhoref(S, i) - (l[0] * b[0] * b[0] + l[1] * b[0] * b[1] + l[2] * b[1] * b[1] +
+                                   l[3] * b[0] * b[2] + l[4] * b[1] * b[2] + l[5] * b[2] * b[2] +
+                                   l[6] * b[0] * b[3] + l[7] * b[1] * b[3] + l[8] * b[2] * b[3] +
+                                   l[9] * b[3] * b[3]);
+        }
+        qr_solve_6x4(A, B, X);
+        RSC_UNROLL for (int c = 0; c < 4; ++c) betas[c] = betas[c] + X[c];
+    }
+}
+
+// find_betas_approx_{1,2,3} (PnPsolver.cpp:520-602).
+template <int which>
+RSC_HD void find_betas(const LaneMat& S, double (&betas)[4]) {
+    double rho[6];
+    RSC_UNROLL for (int r = 0; r < 6; ++r) rho[r] = rhoref(S, r);
+    if (which == 1) {
+        double A[6][4], b4[4];
+        RSC_UNROLL for (int r = 0; r < 6; ++r) {
+            A[r][0] = Lref(S, r, 0); A[r][1] = Lref(S, r, 1); A[r][2] = Lref(S, r, 3); A[r][3] = Lref(S, r, 6);
+        }
+        jacobi_svd_solve_6xk<4>(A, rho, b4);
+        if (b4[0] < 0) {
+            betas[0] = sqrt(-b4[0]);
+            betas[1] = -b4[1] / betas[0];
+            betas[2] = -b4[2] / betas[0];
+            betas[3] = -b4[3] / betas[0];
+        } else {
+            betas[0] = sqrt(b4[0]);
+            betas[1] = b4[1] / betas[0];
+            betas[2] = b4[2] / betas[0];
+            betas[3] = b4[3] / betas[0];
+        }
+    } else if (which == 2) {
+        double A[6][3], b3[3];
+        RSC_UNROLL for (int r = 0; r < 6; ++r) { A[r][0] = Lref(S, r, 0); A[r][1] = Lref(S, r, 1); A[r][2] = Lref(S, r, 2); }
+        jacobi_svd_solve_6xk<3>(A, rho, b3);
+        if (b3[0] < 0) {
+            betas[0] = sqrt(-b3[0]);
+            betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
+        } else {
+            betas[0] = sqrt(b3[0]);
+            betas[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0;
+        }
+        if (b3[1] < 0) betas[0] = -betas[0];
+        betas[2] = 0.0;
+        betas[3] = 0.0;
+    } else {
+        double A[6][5], b5[5];
+        RSC_UNROLL for (int r = 0; r < 6; ++r)
+            RSC_UNROLL for (int c = 0; c < 5; ++c) A[r][c] = Lref(S, r, c);
+        jacobi_svd_solve_6xk<5>(A, rho, b5);
+        if (b5[0] < 0) {
+            betas[0] = sqrt(-b5[0]);
+            betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
+        } else {
+            betas[0] = sqrt(b5[0]);
+            betas[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0;
+        }
+        if (b5[1] < 0) betas[0] = -betas[0];
+        betas[2] = b5[3] / betas[0];
+        betas[3] = 0.0;
+    }
+}
+
+// compute_R_and_t (PnPsolver.cpp:504-515) = compute_ccs + compute_pcs + solve_for_sign +
+// estimate_R_and_t (:433-493, Horn with float N entries, conjugated quaternion) +
+// reprojection_error (:417-431).  pw0 equals the centroid cws[0] (same sum, same division).
+template <class St>
+RSC_HD double compute_R_and_t(const St& st, const Intrinsics& K, const LaneMat& S, const double (&betas)[4],
+                              const double (&pw0)[3], double (&R)[3][3], double (&t)[3]) {
+    const int n = st.n();
+    double ccs[4][3];
+    RSC_UNROLL for (int i = 0; i < 4; i++)
+        RSC_UNROLL for (int c = 0; c < 3; ++c) {
+            double s = 0.0;
+            RSC_UNROLL for (int j = 0; j < 4; j++) s = s + betas[j] * S.at(3 * i + c, j);
+            ccs[i][c] = s;
+        }
+    // solve_for_sign: pcs(0,2) with the unflipped ccs
+    const double pcs02 = st.al(0, 0) * ccs[0][2] + st.al(0, 1) * ccs[1][2] + st.al(0, 2) * ccs[2][2] +
+                         st.al(0, 3) * ccs[3][2];
+    if (pcs02 < 0.0) {
+        RSC_UNROLL for (int i = 0; i < 4; ++i)
+            RSC_UNROLL for (int c = 0; c < 3; ++c) ccs[i][c] = -ccs[i][c];
+    }
+    auto pcs = [&](int i, int c) {
+        return st.al(i, 0) * ccs[0][c] + st.al(i, 1) * ccs[1][c] + st.al(i, 2) * ccs[2][c] + st.al(i, 3) * ccs[3][c];
+    };
+    auto pcs_stale = [&](int i, int c) {
+        return st.stale_al(i, 0) * ccs[0][c] + st.stale_al(i, 1) * ccs[1][c] + st.stale_al(i, 2) * ccs[2][c] +
+               st.stale_al(i, 3) * ccs[3][c];
+    };
+    double pc0[3];
+    RSC_UNROLL for (int c = 0; c < 3; ++c) {
+        double s = pcs(0, c);
+        RSC_UNROLL for (int i = 1; i < n; ++i) s = s + pcs(i, c);
+        for (int i = n; i < st.rows(); ++i) s = s + pcs_stale(i, c);
+        pc0[c] = s / n;
+    }
+    double M[3][3];
+    RSC_UNROLL for (int r = 0; r < 3; ++r)
+        RSC_UNROLL for (int c = 0; c < 3; ++c) M[r][c] = 0.0;
+    RSC_UNROLL for (int i = 0; i < n; ++i) {
+        double a[3], b[3];
+        RSC_UNROLL for (int c = 0; c < 3; ++c) { a[c] = pcs(i, c) - pc0[c]; b[c] = st.pw(i, c) - pw0[c]; }
+        RSC_UNROLL for (int r = 0; r < 3; ++r)
+            RSC_UNROLL for (int c = 0; c < 3; ++c) M[r][c] = M[r][c] + a[r] * b[c];
+    }
+    const float N11 = M[0][0] + M[1][1] + M[2][2];
+    const float N12 = M[1][2] - M[2][1];
+    const float N13 = M[2][0] - M[0][2];
+    const float N14 = M[0][1] - M[1][0];
+    const float N22 = M[0][0] - M[1][1] - M[2][2];
+    const float N23 = M[0][1] + M[1][0];
+    const float N24 = M[2][0] + M[0][2];
+    const float N33 = -M[0][0] + M[1][1] - M[2][2];
+    const float N34 = M[1][2] + M[2][1];
+    const float N44 = -M[0][0] - M[1][1] + M[2][2];
+    const double Nm[4][4] = {{N11, N12, N13, N14}, {N12, N22, N23, N24}, {N13, N23, N33, N34}, {N14, N24, N34, N44}};
+    double V[4][4], w[4];
+    sym_eig_reg<double, 4>(Nm, V, w);
+    quat_to_R<double>(V[0][3], -V[1][3], -V[2][3], -V[3][3], R);
+    if (det3(R) < 0) {
+        RSC_UNROLL for (int c = 0; c < 3; ++c) R[2][c] = -R[2][c];
+    }
+    RSC_UNROLL for (int r = 0; r < 3; ++r) t[r] = pc0[r] - (R[r][0] * pw0[0] + R[r][1] * pw0[1] + R[r][2] * pw0[2]);
+    // reprojection_error
+    double sum2 = 0.0;
+    RSC_UNROLL for (int i = 0; i < n; i++) {
+        const double P0 = st.pw(i, 0), P1 = st.pw(i, 1), P2 = st.pw(i, 2);
+        double X = R[0][0] * P0 + R[0][1] * P1 + R[0][2] * P2 + t[0];
+        double Y = R[1][0] * P0 + R[1][1] * P1 + R[1][2] * P2 + t[1];
+        double Z = R[2][0] * P0 + R[2][1] * P1 + R[2][2] * P2 + t[2];
+        double inv_Zc = 1.0 / Z;
+        double u = K.cx + K.fx * X * inv_Zc;
+        double v = K.cy + K.fy * Y * inv_Zc;
+        double du = st.u(i, 0) - u, dv = st.u(i, 1) - v;
+        sum2 += sqrt(du * du + dv * dv);
+    }
+    return sum2 / n;
+}
+
+// Second half of compute_pose: with the lower triangle of MtM already in the slab, run the 12x12
+// eigensolver, L_6x10/rho, the three beta approximations + Gauss-Newton + compute_R_and_t, and
+// keep the smallest reprojection error (PnPsolver.cpp:379-414).
+template <class St>
+RSC_HD double epnp_stage_c(const St& st, const Intrinsics& K, const LaneMat& S, const double (&cws)[4][3],
+                           float (&Rf)[9], float (&tf)[3]) {
+    sym_eig12(S);
+    compute_L_6x10(S);
+    {
+        auto d2 = [&](int a, int b) {
+            double x = cws[a][0] - cws[b][0], y = cws[a][1] - cws[b][1], z = cws[a][2] - cws[b][2];
+            return x * x + y * y + z * z;
+        };
+        rhoref(S, 0) = d2(0, 1); rhoref(S, 1) = d2(0, 2); rhoref(S, 2) = d2(0, 3);
+        rhoref(S, 3) = d2(1, 2); rhoref(S, 4) = d2(1, 3); rhoref(S, 5) = d2(2, 3);
+    }
+    const double pw0[3] = {cws[0][0], cws[0][1], cws[0][2]};
+    double bestR[3][3], bestt[3], best_err;
+    {
+        double betas[4] = {0.0, 0.0, 0.0, 0.0};
+        find_betas<1>(S, betas);
+        gauss_newton(S, betas);
+        best_err = compute_R_and_t(st, K, S, betas, pw0, bestR, bestt);
+    }
+    {
+        double betas[4] = {0.0, 0.0, 0.0, 0.0}, R[3][3], t[3];
+        find_betas<2>(S, betas);
+        gauss_newton(S, betas);
+        double e = compute_R_and_t(st, K, S, betas, pw0, R, t);
+        if (e < best_err) {
+            best_err = e;
+            RSC_UNROLL for (int r = 0; r < 3; ++r) {
+                bestt[r] = t[r];
+                RSC_UNROLL for (int c = 0; c < 3; ++c) bestR[r][c] = R[r][c];
+            }
+        }
+    }
+    {
+        double betas[4] = {0.0, 0.0, 0.0, 0.0}, R[3][3], t[3];
+        find_betas<3>(S, betas);
+        gauss_newton(S, betas);
+        double e = compute_R_and_t(st, K, S, betas, pw0, R, t);
+        if (e < best_err) {
+            best_err = e;
+            RSC_UNROLL for (int r = 0; r < 3; ++r) {
+                bestt[r] = t[r];
+                RSC_UNROLL for (int c = 0; c < 3; ++c) bestR[r][c] = R[r][c];
+            }
+        }
+    }
+    RSC_UNROLL for (int r = 0; r < 3; ++r) {
+        tf[r] = (float)bestt[r];
+        RSC_UNROLL for (int c = 0; c < 3; ++c) Rf[3 * r + c] = (float)bestR[r][c];
+    }
+    return best_err;
+}
+
+// PnPsolver::compute_pose (PnPsolver.cpp:359-415) for one lane.  Outputs float R (row-major) and t.
+template <class St>
+RSC_HD double epnp_compute_pose(St& st, const Intrinsics& K, const LaneMat& S, float (&Rf)[9], float (&tf)[3]) {
+    double cws[4][3];
+    control_points_and_alphas(st, cws);
+    build_MtM(st, K, S);
+    return epnp_stage_c(st, K, S, cws, Rf, tf);
+}
+
+}  // namespace rsc

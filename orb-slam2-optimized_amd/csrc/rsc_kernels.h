@@ -1,0 +1,66 @@
+// rsc_kernels.h — device-visible descriptors shared by kernels.hip and the HIP backend.
+#pragma once
+#include <cstdint>
+#include <hip/hip_runtime.h>
+
+namespace rsc {
+
+// One PnP problem (= one PnPsolver) resident in HBM.
+struct DevPnP {
+    const float4* pts;  // [n] x, y, z (mvP3Dw), w = sigma^2 (mvSigma2)
+    const float2* uv;   // [n] mvP2D
+    int n;              // N
+    float fx, fy, cx, cy;  // Frame static float intrinsics (widened to double in the kernels)
+    float th2;          // SetRansacParameters th2: mvMaxError[i] = sigma2[i] * th2 (float)
+    int rows;           // maximum_number_of_correspondences of the grow-only EPnP buffers
+    double* pws;        // [cap][3] EPnP buffers (rows >= min_set are stale rows from Refine)
+    double* us;         // [cap][2]
+    double* als;        // [cap][4]
+};
+
+// One Sim3 problem (= one Sim3Solver after construction).
+struct DevSim3 {
+    const float4* x1;   // [n] mvX3Dc1, w = (float)mvnMaxError1
+    const float4* x2;   // [n] mvX3Dc2, w = (float)mvnMaxError2
+    const float4* pim;  // [n] (mvP1im1.x, .y, mvP2im2.x, .y)
+    int n;
+    float K1[4], K2[4];  // fx, fy, cx, cy
+};
+
+// Per-launch, per-problem speculation record: hypotheses [0, H) of this launch use draws
+// g0 + h*min_set + d of the glibc stream whose window is `window`.
+struct LaunchProb {
+    int prob;
+    int H;
+    int out0;  // first record index of this problem in the launch's pose/count/mask arrays
+    int g0;
+    uint32_t window[31];
+    int pad;
+};
+
+struct RefineJob {
+    int prob;
+    int rows_after;             // maximum_number_of_correspondences after set_maximum(n_r)
+    const uint64_t* best_mask;  // mvbBestInliers as bits
+    float* out_pose;            // 12 floats
+    int32_t* out_count;
+    uint64_t* out_mask;         // mvbRefinedInliers as bits
+};
+
+struct Window31 {
+    uint32_t w[31];
+};
+hipError_t launch_rng_stream(const uint32_t* T, const uint32_t* window, int g0, int n, int32_t* out, hipStream_t st);
+
+hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
+                            const uint32_t* T, float* poses, int32_t* samples, hipStream_t st);
+hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,
+                           const float* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st);
+hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, int mask_words_out,
+                             hipStream_t st);
+hipError_t launch_sim3_solve(int nwg, const DevSim3* probs, const LaunchProb* lps, const int2* wgt,
+                             const uint32_t* T, float* poses, int32_t* samples, hipStream_t st);
+hipError_t launch_sim3_scan(int ppt, int nwg, const DevSim3* probs, const LaunchProb* lps, const int4* wgt,
+                            const float* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st);
+
+}  // namespace rsc

@@ -1,0 +1,301 @@
+"""ctypes binding of librsc.so (include/rsc.h) with the reference's solver API.
+
+``PnPSolver`` / ``Sim3Solver`` mirror ORB_SLAM_CUSTOM::PnPsolver / Sim3Solver
+(include/PnPsolver.hpp:24-31, include/Sim3Solver.hpp:21-30): same constructor inputs (already
+reduced to plain arrays), ``set_ransac_parameters`` / ``iterate`` / ``find`` with the same argument
+meaning and results.  Every call runs on the MI355X; there is no CPU fallback — if librsc.so is
+missing or no HIP device is present the calls raise ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "librsc.so")
+
+RSC_OK = 0
+
+_lib = None
+
+f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+
+# Every symbol declared in include/rsc.h (checked by tests/test_cpu_abi.py).
+EXPORTED = [
+    "rsc_version", "rsc_status_string", "rsc_context_create", "rsc_context_destroy", "rsc_context_set_stream",
+    "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_enable_timing",
+    "rsc_pnp_create", "rsc_pnp_destroy", "rsc_pnp_set_ransac_parameters", "rsc_pnp_iterate", "rsc_pnp_find",
+    "rsc_pnp_iterate_many", "rsc_pnp_reset", "rsc_pnp_get_state", "rsc_pnp_last_samples",
+    "rsc_sim3_create", "rsc_sim3_destroy", "rsc_sim3_set_ransac_parameters", "rsc_sim3_iterate", "rsc_sim3_find",
+    "rsc_sim3_iterate_many", "rsc_sim3_reset", "rsc_sim3_get_state", "rsc_sim3_prepared", "rsc_rand_stream",
+]
+
+
+class PnPProblem(C.Structure):
+    _fields_ = [("n", C.c_int32), ("n_points", C.c_int32), ("p2d", C.c_void_p), ("p3dw", C.c_void_p),
+                ("sigma2", C.c_void_p), ("kp_index", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float)]
+
+
+class PnPResult(C.Structure):
+    _fields_ = [("ok", C.c_int32), ("no_more", C.c_int32), ("n_inliers", C.c_int32), ("iterations", C.c_int32),
+                ("T", C.c_float * 16)]
+
+
+class Sim3Input(C.Structure):
+    _fields_ = [("n1", C.c_int32), ("valid", C.c_void_p), ("Xw1", C.c_void_p), ("Xw2", C.c_void_p),
+                ("sigma2_1", C.c_void_p), ("sigma2_2", C.c_void_p), ("R1", C.c_float * 9), ("t1", C.c_float * 3),
+                ("R2", C.c_float * 9), ("t2", C.c_float * 3), ("K1", C.c_float * 4), ("K2", C.c_float * 4)]
+
+
+class Sim3Result(C.Structure):
+    _fields_ = [("ok", C.c_int32), ("no_more", C.c_int32), ("n_inliers", C.c_int32), ("iterations", C.c_int32),
+                ("R", C.c_float * 9), ("t", C.c_float * 3)]
+
+
+def load_library(path: str = LIB_PATH):
+    """Load librsc.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"librsc.so not found at {path}: run __graft_entry__.build() / make")
+    L = C.CDLL(path)
+    vp = C.c_void_p
+    L.rsc_version.restype = C.c_int
+    L.rsc_status_string.restype = C.c_char_p
+    L.rsc_status_string.argtypes = [C.c_int]
+    L.rsc_context_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.rsc_context_destroy.argtypes = [vp]
+    L.rsc_context_set_stream.argtypes = [vp, vp]
+    L.rsc_context_synchronize.argtypes = [vp]
+    L.rsc_context_last_timing.argtypes = [vp, C.POINTER(C.c_double)]
+    L.rsc_context_enable_timing.argtypes = [vp, C.c_int]
+    L.rsc_pnp_create.argtypes = [vp, C.POINTER(PnPProblem), C.c_uint32, C.POINTER(vp)]
+    L.rsc_pnp_destroy.argtypes = [vp]
+    L.rsc_pnp_set_ransac_parameters.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
+    L.rsc_pnp_iterate.argtypes = [vp, C.c_int, C.POINTER(PnPResult), C.c_void_p]
+    L.rsc_pnp_find.argtypes = [vp, C.POINTER(PnPResult), C.c_void_p]
+    L.rsc_pnp_iterate_many.argtypes = [C.POINTER(vp), C.c_int, i32p, C.POINTER(PnPResult), C.POINTER(C.c_void_p)]
+    L.rsc_pnp_reset.argtypes = [vp, C.c_uint32]
+    L.rsc_pnp_get_state.argtypes = [vp, i32p]
+    L.rsc_pnp_last_samples.argtypes = [vp, i32p, C.c_int]
+    L.rsc_sim3_create.argtypes = [vp, C.POINTER(Sim3Input), C.c_uint32, C.POINTER(vp)]
+    L.rsc_sim3_destroy.argtypes = [vp]
+    L.rsc_sim3_set_ransac_parameters.argtypes = [vp, C.c_double, C.c_int, C.c_int]
+    L.rsc_sim3_iterate.argtypes = [vp, C.c_int, C.POINTER(Sim3Result), C.c_void_p]
+    L.rsc_sim3_find.argtypes = [vp, C.POINTER(Sim3Result), C.c_void_p]
+    L.rsc_sim3_iterate_many.argtypes = [C.POINTER(vp), C.c_int, i32p, C.POINTER(Sim3Result), C.POINTER(C.c_void_p)]
+    L.rsc_sim3_reset.argtypes = [vp, C.c_uint32]
+    L.rsc_sim3_get_state.argtypes = [vp, i32p]
+    L.rsc_sim3_prepared.argtypes = [vp, f32p, f32p, f32p, f32p, u64p, u64p, i32p]
+    L.rsc_rand_stream.argtypes = [vp, C.c_uint32, C.c_int, i32p]
+    _lib = L
+    return L
+
+
+def _check(st: int, what: str):
+    if st != RSC_OK:
+        raise RuntimeError(f"rsc: {what}: {load_library().rsc_status_string(st).decode()} ({st})")
+
+
+class Context:
+    """One engine context (HIP stream + work buffers + rand() jump table) on one device."""
+
+    def __init__(self, device: int = 0):
+        L = load_library()
+        h = C.c_void_p()
+        _check(L.rsc_context_create(device, C.byref(h)), "rsc_context_create")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            load_library().rsc_context_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_stream(self, stream_ptr: int):
+        _check(load_library().rsc_context_set_stream(self.h, C.c_void_p(stream_ptr)), "set_stream")
+
+    def synchronize(self):
+        _check(load_library().rsc_context_synchronize(self.h), "synchronize")
+
+    def enable_timing(self, on: bool = True):
+        _check(load_library().rsc_context_enable_timing(self.h, int(on)), "enable_timing")
+
+    def last_timing(self):
+        out = (C.c_double * 5)()
+        _check(load_library().rsc_context_last_timing(self.h, out), "last_timing")
+        return dict(solve_ms=out[0], scan_ms=out[1], refine_ms=out[2], solve_launches=int(out[3]),
+                    hypotheses=int(out[4]))
+
+    def rand_stream(self, seed: int, n: int) -> np.ndarray:
+        out = np.zeros(n, np.int32)
+        _check(load_library().rsc_rand_stream(self.h, seed, n, out), "rand_stream")
+        return out
+
+
+def _pnp_out(r: PnPResult, mask: np.ndarray) -> dict:
+    T = np.array(r.T, dtype=np.float32).reshape(4, 4)
+    return dict(ok=bool(r.ok), no_more=bool(r.no_more), n_inliers=int(r.n_inliers), iterations=int(r.iterations),
+                T=T, inliers=(mask.astype(bool) if r.ok else np.zeros(0, bool)))
+
+
+class PnPSolver:
+    """PnPsolver (PnPsolver.cpp) on the GPU.  ``scene`` carries the compacted constructor arrays."""
+
+    def __init__(self, ctx: Context, scene, seed: int = 1):
+        L = load_library()
+        self.ctx = ctx
+        self._keep = [np.ascontiguousarray(scene.p2d, np.float32), np.ascontiguousarray(scene.p3dw, np.float32),
+                      np.ascontiguousarray(scene.sigma2, np.float32), np.ascontiguousarray(scene.kp_index, np.int32)]
+        pb = PnPProblem(int(scene.n), int(scene.n_points), self._keep[0].ctypes.data, self._keep[1].ctypes.data,
+                        self._keep[2].ctypes.data, self._keep[3].ctypes.data, float(scene.fx), float(scene.fy),
+                        float(scene.cx), float(scene.cy))
+        h = C.c_void_p()
+        _check(L.rsc_pnp_create(ctx.h, C.byref(pb), seed, C.byref(h)), "rsc_pnp_create")
+        self.h = h
+        self.n_points = int(scene.n_points)
+        self.n = int(scene.n)
+
+    def close(self):
+        if getattr(self, "h", None):
+            load_library().rsc_pnp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_ransac_parameters(self, probability=0.99, min_inliers=8, max_iterations=300, min_set=4, epsilon=0.4,
+                              th2=5.991):
+        _check(load_library().rsc_pnp_set_ransac_parameters(self.h, probability, min_inliers, max_iterations,
+                                                            min_set, epsilon, th2), "SetRansacParameters")
+
+    def iterate(self, n_iterations: int) -> dict:
+        r = PnPResult()
+        mask = np.zeros(max(self.n_points, 1), np.uint8)
+        _check(load_library().rsc_pnp_iterate(self.h, n_iterations, C.byref(r), mask.ctypes.data), "iterate")
+        return _pnp_out(r, mask[:self.n_points])
+
+    def find(self) -> dict:
+        r = PnPResult()
+        mask = np.zeros(max(self.n_points, 1), np.uint8)
+        _check(load_library().rsc_pnp_find(self.h, C.byref(r), mask.ctypes.data), "find")
+        return _pnp_out(r, mask[:self.n_points])
+
+    def reset(self, seed: int):
+        _check(load_library().rsc_pnp_reset(self.h, seed), "reset")
+
+    def state(self) -> dict:
+        out = np.zeros(8, np.int32)
+        _check(load_library().rsc_pnp_get_state(self.h, out), "get_state")
+        return dict(iterations=int(out[0]), max_iterations=int(out[1]), min_inliers=int(out[2]),
+                    best_inliers=int(out[3]), max_rows=int(out[4]), N=int(out[5]), n_points=int(out[6]),
+                    min_set=int(out[7]))
+
+    def last_samples(self, cap: int = 100000) -> np.ndarray:
+        out = np.zeros((cap, 8), np.int32)
+        n = load_library().rsc_pnp_last_samples(self.h, out.reshape(-1), cap)
+        return out[:max(n, 0)]
+
+
+def pnp_iterate_many(solvers, n_iterations, with_masks: bool = True):
+    """rsc_pnp_iterate_many: iterate() of every solver in one set of launches."""
+    L = load_library()
+    n = len(solvers)
+    hs = (C.c_void_p * n)(*[s.h.value for s in solvers])
+    its = np.ascontiguousarray(np.broadcast_to(np.asarray(n_iterations, np.int32), (n,)))
+    res = (PnPResult * n)()
+    masks = [np.zeros(max(s.n_points, 1), np.uint8) for s in solvers]
+    mp = (C.c_void_p * n)(*[(m.ctypes.data if with_masks else None) for m in masks])
+    _check(L.rsc_pnp_iterate_many(hs, n, its, res, mp), "iterate_many")
+    return [_pnp_out(res[i], masks[i][:solvers[i].n_points]) for i in range(n)]
+
+
+def _sim3_out(r: Sim3Result, mask: np.ndarray) -> dict:
+    return dict(ok=bool(r.ok), no_more=bool(r.no_more), n_inliers=int(r.n_inliers), iterations=int(r.iterations),
+                R=np.array(r.R, np.float32).reshape(3, 3), t=np.array(r.t, np.float32), inliers=mask.astype(bool))
+
+
+class Sim3Solver:
+    """Sim3Solver (Sim3Solver.cpp) on the GPU, built from the raw keyframe-pair inputs."""
+
+    def __init__(self, ctx: Context, pair, seed: int = 1):
+        L = load_library()
+        self.ctx = ctx
+        self._keep = [np.ascontiguousarray(a) for a in (
+            pair.valid.astype(np.uint8), pair.Xw1.astype(np.float32), pair.Xw2.astype(np.float32),
+            pair.sigma2_1.astype(np.float32), pair.sigma2_2.astype(np.float32))]
+        inp = Sim3Input()
+        inp.n1 = int(pair.n1)
+        inp.valid, inp.Xw1, inp.Xw2, inp.sigma2_1, inp.sigma2_2 = [a.ctypes.data for a in self._keep]
+        inp.R1[:] = [float(x) for x in np.asarray(pair.R1, np.float32).ravel()]
+        inp.t1[:] = [float(x) for x in np.asarray(pair.t1, np.float32)]
+        inp.R2[:] = [float(x) for x in np.asarray(pair.R2, np.float32).ravel()]
+        inp.t2[:] = [float(x) for x in np.asarray(pair.t2, np.float32)]
+        inp.K1[:] = [float(x) for x in np.asarray(pair.K1, np.float32)]
+        inp.K2[:] = [float(x) for x in np.asarray(pair.K2, np.float32)]
+        h = C.c_void_p()
+        _check(L.rsc_sim3_create(ctx.h, C.byref(inp), seed, C.byref(h)), "rsc_sim3_create")
+        self.h = h
+        self.n1 = int(pair.n1)
+
+    def close(self):
+        if getattr(self, "h", None):
+            load_library().rsc_sim3_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_ransac_parameters(self, probability=0.99, min_inliers=6, max_iterations=300):
+        _check(load_library().rsc_sim3_set_ransac_parameters(self.h, probability, min_inliers, max_iterations),
+               "SetRansacParameters")
+
+    def iterate(self, n_iterations: int) -> dict:
+        r = Sim3Result()
+        mask = np.zeros(max(self.n1, 1), np.uint8)
+        _check(load_library().rsc_sim3_iterate(self.h, n_iterations, C.byref(r), mask.ctypes.data), "iterate")
+        return _sim3_out(r, mask[:self.n1])
+
+    def find(self) -> dict:
+        r = Sim3Result()
+        mask = np.zeros(max(self.n1, 1), np.uint8)
+        _check(load_library().rsc_sim3_find(self.h, C.byref(r), mask.ctypes.data), "find")
+        return _sim3_out(r, mask[:self.n1])
+
+    def reset(self, seed: int):
+        _check(load_library().rsc_sim3_reset(self.h, seed), "reset")
+
+    def state(self) -> dict:
+        out = np.zeros(6, np.int32)
+        _check(load_library().rsc_sim3_get_state(self.h, out), "get_state")
+        return dict(iterations=int(out[0]), max_iterations=int(out[1]), min_inliers=int(out[2]),
+                    best_inliers=int(out[3]), N=int(out[4]), n1=int(out[5]))
+
+    def prepared(self) -> dict:
+        N = self.state()["N"]
+        X1 = np.zeros((N, 3), np.float32); X2 = np.zeros((N, 3), np.float32)
+        P1 = np.zeros((N, 2), np.float32); P2 = np.zeros((N, 2), np.float32)
+        e1 = np.zeros(N, np.uint64); e2 = np.zeros(N, np.uint64); idx = np.zeros(N, np.int32)
+        _check(load_library().rsc_sim3_prepared(self.h, X1, X2, P1, P2, e1, e2, idx), "prepared")
+        return dict(X1c=X1, X2c=X2, P1im1=P1, P2im2=P2, maxerr1=e1, maxerr2=e2, indices=idx)
+
+
+def sim3_iterate_many(solvers, n_iterations, with_masks: bool = True):
+    L = load_library()
+    n = len(solvers)
+    hs = (C.c_void_p * n)(*[s.h.value for s in solvers])
+    its = np.ascontiguousarray(np.broadcast_to(np.asarray(n_iterations, np.int32), (n,)))
+    res = (Sim3Result * n)()
+    masks = [np.zeros(max(s.n1, 1), np.uint8) for s in solvers]
+    mp = (C.c_void_p * n)(*[(m.ctypes.data if with_masks else None) for m in masks])
+    _check(L.rsc_sim3_iterate_many(hs, n, its, res, mp), "iterate_many")
+    return [_sim3_out(res[i], masks[i][:solvers[i].n1]) for i in range(n)]

@@ -1,0 +1,127 @@
+// Drives the C++ facade (PnPsolver / Sim3Solver templates) with mock Frame / KeyFrame / MapPoint
+// types built from a binary scene file written by tests/test_gpu_facade.py, and writes every
+// iterate() result back for comparison with the oracle.  Runs on the GPU box.
+#include <cstdio>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <vector>
+#include "PnPsolver.hpp"
+#include "Sim3Solver.hpp"
+
+struct Vec3 { float v[3]; float operator()(int i) const { return v[i]; } float& operator()(int i) { return v[i]; } };
+struct Mat3 { float m[3][3]; float operator()(int r, int c) const { return m[r][c]; } float& operator()(int r, int c) { return m[r][c]; } };
+struct Mat4 { float m[4][4]; float& operator()(int r, int c) { return m[r][c]; } };
+struct Pt { float x, y; };
+struct KeyPoint { Pt pt; int octave; };
+struct Frame { std::vector<KeyPoint> mvKeysUn; std::vector<float> mvLevelSigma2; float fx, fy, cx, cy; };
+struct KeyFrame;
+struct MapPoint {
+    bool bad = false; Vec3 X; int idx1 = -1, idx2 = -1; KeyFrame* kf1 = nullptr;
+    bool isBad() const { return bad; }
+    Vec3 GetWorldPos() const { return X; }
+    int GetIndexInKeyFrame(const std::shared_ptr<KeyFrame>& kf) const;
+};
+struct KeyFrame {
+    std::vector<KeyPoint> mvKeysUn; std::vector<float> mvLevelSigma2; Mat3 mK; Mat3 R; Vec3 t;
+    std::vector<std::shared_ptr<MapPoint>> mps;
+    std::vector<std::shared_ptr<MapPoint>> GetMapPointMatches() { return mps; }
+    Mat3 GetRotation() const { return R; }
+    Vec3 GetTranslation() const { return t; }
+};
+int MapPoint::GetIndexInKeyFrame(const std::shared_ptr<KeyFrame>& kf) const { return kf.get() == kf1 ? idx1 : idx2; }
+
+template <class T> T rd(FILE* f) { T v; if (fread(&v, sizeof(T), 1, f) != 1) throw std::runtime_error("short read"); return v; }
+template <class T> void wr(FILE* f, T v) { fwrite(&v, sizeof(T), 1, f); }
+
+int main(int argc, char** argv) {
+    if (argc != 3) { fprintf(stderr, "usage: facade_test in.bin out.bin\n"); return 2; }
+    FILE* in = fopen(argv[1], "rb");
+    FILE* out = fopen(argv[2], "wb");
+    if (!in || !out) return 2;
+    const int mode = rd<int32_t>(in);
+    if (mode == 1) {
+        Frame F;
+        const int n = rd<int32_t>(in);
+        F.fx = rd<float>(in); F.fy = rd<float>(in); F.cx = rd<float>(in); F.cy = rd<float>(in);
+        const int nl = rd<int32_t>(in);
+        for (int l = 0; l < nl; ++l) F.mvLevelSigma2.push_back(rd<float>(in));
+        std::vector<std::shared_ptr<MapPoint>> matches(n);
+        F.mvKeysUn.resize(n);
+        for (int i = 0; i < n; ++i) {
+            const int present = rd<int32_t>(in);
+            KeyPoint k; k.pt.x = rd<float>(in); k.pt.y = rd<float>(in); k.octave = rd<int32_t>(in);
+            Vec3 X; X.v[0] = rd<float>(in); X.v[1] = rd<float>(in); X.v[2] = rd<float>(in);
+            F.mvKeysUn[i] = k;
+            if (present) { auto mp = std::make_shared<MapPoint>(); mp->bad = (present == 2); mp->X = X; matches[i] = mp; }
+        }
+        const uint32_t seed = rd<uint32_t>(in);
+        const double prob = rd<double>(in);
+        const int mi = rd<int32_t>(in), mx = rd<int32_t>(in), ms = rd<int32_t>(in);
+        const float eps = rd<float>(in), th2 = rd<float>(in);
+        const int ncalls = rd<int32_t>(in);
+        rsc_orb::PnPsolver<Frame, MapPoint> solver(F, matches, seed);
+        solver.SetRansacParameters(prob, mi, mx, ms, eps, th2);
+        for (int c = 0; c < ncalls; ++c) {
+            const int its = rd<int32_t>(in);
+            bool nm = false; std::vector<bool> inl; int ni = -1; Mat4 T; std::memset(&T, 0, sizeof(T));
+            bool ok = its < 0 ? solver.find(inl, ni, T) : solver.iterate(its, nm, inl, ni, T);
+            wr<int32_t>(out, ok); wr<int32_t>(out, nm); wr<int32_t>(out, ni);
+            for (int a = 0; a < 4; ++a) for (int b = 0; b < 4; ++b) wr<float>(out, T.m[a][b]);
+            wr<int32_t>(out, (int32_t)inl.size());
+            for (bool v : inl) wr<uint8_t>(out, v ? 1 : 0);
+        }
+    } else if (mode == 2) {
+        auto kf1 = std::make_shared<KeyFrame>(), kf2 = std::make_shared<KeyFrame>();
+        const int n1 = rd<int32_t>(in);
+        for (auto* kf : {kf1.get(), kf2.get()}) {
+            for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) kf->R.m[r][c] = rd<float>(in);
+            for (int r = 0; r < 3; ++r) kf->t.v[r] = rd<float>(in);
+            float K[4]; for (float& k : K) k = rd<float>(in);
+            std::memset(&kf->mK, 0, sizeof(Mat3));
+            kf->mK.m[0][0] = K[0]; kf->mK.m[1][1] = K[1]; kf->mK.m[0][2] = K[2]; kf->mK.m[1][2] = K[3]; kf->mK.m[2][2] = 1;
+            const int nl = rd<int32_t>(in);
+            for (int l = 0; l < nl; ++l) kf->mvLevelSigma2.push_back(rd<float>(in));
+            kf->mvKeysUn.resize(n1);
+            kf->mps.resize(n1);
+        }
+        std::vector<std::shared_ptr<MapPoint>> matched(n1);
+        for (int i = 0; i < n1; ++i) {
+            const int flags = rd<int32_t>(in);  // bit0 matched, bit1 mp1, bit2 bad1, bit3 bad2, bit4 idx1 invalid, bit5 idx2 invalid
+            Vec3 a, b; for (int r = 0; r < 3; ++r) a.v[r] = rd<float>(in);
+            for (int r = 0; r < 3; ++r) b.v[r] = rd<float>(in);
+            const int o1 = rd<int32_t>(in), o2 = rd<int32_t>(in);
+            kf1->mvKeysUn[i].octave = o1;
+            kf2->mvKeysUn[i].octave = o2;
+            if (flags & 2) {
+                auto mp1 = std::make_shared<MapPoint>(); mp1->X = a; mp1->bad = flags & 4; mp1->kf1 = kf1.get();
+                mp1->idx1 = (flags & 16) ? -1 : i; mp1->idx2 = -1; kf1->mps[i] = mp1;
+            }
+            if (flags & 1) {
+                auto mp2 = std::make_shared<MapPoint>(); mp2->X = b; mp2->bad = flags & 8; mp2->kf1 = kf1.get();
+                mp2->idx1 = -1; mp2->idx2 = (flags & 32) ? -1 : i; matched[i] = mp2;
+            }
+        }
+        const uint32_t seed = rd<uint32_t>(in);
+        const double prob = rd<double>(in);
+        const int mi = rd<int32_t>(in), mx = rd<int32_t>(in);
+        const int ncalls = rd<int32_t>(in);
+        rsc_orb::Sim3Solver<KeyFrame, MapPoint> solver(kf1, kf2, matched, seed);
+        solver.SetRansacParameters(prob, mi, mx);
+        for (int c = 0; c < ncalls; ++c) {
+            const int its = rd<int32_t>(in);
+            bool nm = false; std::vector<bool> inl; int ni = -1;
+            bool ok = its < 0 ? solver.find(inl, ni) : solver.iterate(its, nm, inl, ni);
+            Mat3 R = solver.GetEstimatedRotation<Mat3>();
+            Vec3 t = solver.GetEstimatedTranslation<Vec3>();
+            wr<int32_t>(out, ok); wr<int32_t>(out, nm); wr<int32_t>(out, ni);
+            for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) wr<float>(out, R.m[a][b]);
+            for (int a = 0; a < 3; ++a) wr<float>(out, t.v[a]);
+            wr<int32_t>(out, (int32_t)inl.size());
+            for (bool v : inl) wr<uint8_t>(out, v ? 1 : 0);
+        }
+    }
+    fclose(in);
+    fclose(out);
+    return 0;
+}
