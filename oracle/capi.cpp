@@ -9,8 +9,25 @@
 #include "glibc_rand.h"
 #include "pnp_oracle.h"
 #include "sim3_oracle.h"
+#include "ora_linalg.h"
 
 using namespace rsc_oracle;
+
+template <int n>
+static int sym_eig_n(const double* A, double* V, double* w) {
+    double M[n][n];
+    for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) M[i][j] = A[i * n + j];
+    SymEig<double, n> e = sym_eig<double, n>(M);
+    for (int i = 0; i < n; ++i) { w[i] = e.w[i]; for (int j = 0; j < n; ++j) V[i * n + j] = e.V[i][j]; }
+    return e.ok ? 0 : 1;
+}
+
+template <int k>
+static void svd_k(const double* A, const double* b, double* x) {
+    double M[6][k];
+    for (int r = 0; r < 6; ++r) for (int c = 0; c < k; ++c) M[r][c] = A[r * k + c];
+    jacobi_svd_solve_6xk<k>(M, b, x);
+}
 
 extern "C" {
 
@@ -35,6 +52,36 @@ void ora_sample_stream(uint32_t seed, int N, int min_set, int hyps, int32_t* out
             av.pop_back();
         }
     }
+}
+
+// ---- linear-algebra restatements (numpy cross-checks) ----
+int ora_sym_eig(int n, const double* A, double* V, double* w) {
+    switch (n) {
+        case 3: return sym_eig_n<3>(A, V, w);
+        case 4: return sym_eig_n<4>(A, V, w);
+        case 12: return sym_eig_n<12>(A, V, w);
+    }
+    return -1;
+}
+int ora_sym_eig4f(const float* A, float* V, float* w) {
+    float M[4][4];
+    for (int i = 0; i < 4; ++i) for (int j = 0; j < 4; ++j) M[i][j] = A[i * 4 + j];
+    SymEig<float, 4> e = sym_eig<float, 4>(M);
+    for (int i = 0; i < 4; ++i) { w[i] = e.w[i]; for (int j = 0; j < 4; ++j) V[i * 4 + j] = e.V[i][j]; }
+    return e.ok ? 0 : 1;
+}
+int ora_svd_solve(int k, const double* A, const double* b, double* x) {
+    switch (k) {
+        case 3: svd_k<3>(A, b, x); return 0;
+        case 4: svd_k<4>(A, b, x); return 0;
+        case 5: svd_k<5>(A, b, x); return 0;
+    }
+    return -1;
+}
+int ora_random_int(uint32_t seed, int n_draws, const int32_t* maxes, int32_t* out) {
+    GlibcRand g(seed);
+    for (int i = 0; i < n_draws; ++i) out[i] = g.random_int(0, maxes[i]);
+    return 0;
 }
 
 // ---- PnP ----

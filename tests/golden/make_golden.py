@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Generates the committed fixtures under tests/golden/.
+
+* glibc_rand.json — rand() after srand(seed) from THIS container's glibc (2.35) through ctypes,
+  plus DUtils::Random::RandomInt swap-remove sample streams computed in pure Python from those
+  libc outputs (Random.cpp:47-50, PnPsolver.cpp:125-138).  Independent of the oracle.
+* pnp_traces.npz / sim3_traces.npz — per-hypothesis sample indices, inlier counts and poses of the
+  oracle restatement on small seeded scenes (regression pins of the oracle; the reference itself
+  cannot be built here, see DESIGN.md "Oracle").
+
+Run from the repo root:  python tests/golden/make_golden.py
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "orb-slam2-optimized_amd"))
+
+SEEDS = [0, 1, 42, 1234, 987654321]
+
+
+def libc_rand(seed, n):
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(ctypes.c_uint(seed))
+    return [libc.rand() for _ in range(n)]
+
+
+def python_sample_stream(rands, N, min_set, hyps):
+    it = iter(rands)
+    out = []
+    for _ in range(hyps):
+        av = list(range(N))
+        s = []
+        for _ in range(min_set):
+            d = len(av)
+            randi = int((next(it) / (2147483647 + 1.0)) * d)
+            s.append(av[randi])
+            av[randi] = av[-1]
+            av.pop()
+        out.append(s)
+    return out
+
+
+def main():
+    g = {"glibc": "2.35 (ctypes libc.so.6)", "rand": {}, "samples": []}
+    for s in SEEDS:
+        g["rand"][str(s)] = libc_rand(s, 2000)
+    for (seed, N, ms, hyps) in [(1, 4, 4, 5), (1, 7, 4, 20), (42, 500, 4, 50), (1234, 2000, 4, 50), (7, 1000, 3, 60),
+                                (9, 600, 6, 30)]:
+        r = libc_rand(seed, ms * hyps)
+        g["samples"].append({"seed": seed, "N": N, "min_set": ms, "hyps": hyps,
+                             "idx": python_sample_stream(r, N, ms, hyps)})
+    with open(os.path.join(HERE, "glibc_rand.json"), "w") as f:
+        json.dump(g, f)
+
+    import oracle_lib as ol
+    from rsc import synth
+    out = {}
+    for k, (n, ratio, seed) in enumerate([(64, 0.5, 1), (120, 0.7, 2), (300, 0.4, 3)]):
+        sc = synth.make_pnp_scene(np.random.default_rng(900 + k), n, ratio)
+        o = ol.OraclePnP(sc, seed)
+        o.set_ransac_parameters(0.99, 10, 300, 4, 0.5, 5.991)
+        o.enable_trace()
+        r = o.iterate(80)
+        ints, fl = o.trace()
+        out[f"s{k}_ints"] = ints
+        out[f"s{k}_poses"] = fl
+        out[f"s{k}_result"] = np.array([r["ok"], r["no_more"], r["n_inliers"]], np.int32)
+        out[f"s{k}_T"] = r["T"]
+        out[f"s{k}_mask"] = r["inliers"].astype(np.uint8)
+        out[f"s{k}_meta"] = np.array([n, seed, 900 + k], np.int64)
+        out[f"s{k}_ratio"] = np.array([ratio])
+    np.savez_compressed(os.path.join(HERE, "pnp_traces.npz"), **out)
+    out = {}
+    for k, (n1, ninl, seed) in enumerate([(80, 40, 1), (300, 90, 2)]):
+        pair = synth.make_sim3_pair(np.random.default_rng(950 + k), n1, ninl, invalid_frac=0.1)
+        o = ol.OracleSim3(pair, seed)
+        o.set_ransac_parameters(0.99, 20, 300)
+        o.enable_trace()
+        r = o.iterate(60)
+        ints, fl = o.trace()
+        out[f"s{k}_ints"] = ints
+        out[f"s{k}_poses"] = fl
+        out[f"s{k}_result"] = np.array([r["ok"], r["no_more"], r["n_inliers"]], np.int32)
+        out[f"s{k}_meta"] = np.array([n1, ninl, seed, 950 + k], np.int64)
+    np.savez_compressed(os.path.join(HERE, "sim3_traces.npz"), **out)
+    print("golden fixtures written")
+
+
+if __name__ == "__main__":
+    main()

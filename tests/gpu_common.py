@@ -36,3 +36,16 @@ def assert_sim3_equal(g, o, where=""):
     assert np.array_equal(bits(g["R"]), bits(o["R"])), f"{where} R"
     assert np.array_equal(bits(g["t"]), bits(o["t"])), f"{where} t"
     assert np.array_equal(g["inliers"], o["inliers"]), f"{where} inliers"
+
+
+# Scenes where PnPsolver::Refine() FAILS at least once in 20 rounds of iterate(5) (found by scanning
+# the generator; they exercise re-speculation after a failed Refine with stale EPnP rows, Q6).
+REFINE_FAIL_CASES = [1, 4, 17, 43, 66, 72, 74, 83, 95, 98]
+
+
+def refine_fail_scene(s):
+    from rsc import synth
+    rng = np.random.default_rng(5000 + s)
+    n = int(rng.integers(40, 300))
+    ratio = float(rng.uniform(0.5, 0.6))
+    return synth.make_pnp_scene(rng, n, ratio), s + 1

@@ -135,3 +135,143 @@ int he_sim3_count(const float* pose24, const float* K1, const float* K2, int n, 
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// CPU backends of rsc_engine.h (TEST-ONLY): the same replay code the HIP backend drives, with the
+// kernels replaced by loops over the per-lane functions.
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+struct EmuPnP {
+    PnPState st;
+    std::vector<float> pts4, uv;  // x,y,z,sigma2 / u,v
+    std::vector<double> pws, us, als;
+    std::vector<uint64_t> best, refined;
+    int words = 0;
+    // last speculation
+    std::vector<float> poses;
+    std::vector<std::vector<uint64_t>> masks;
+};
+
+struct EmuPnPBackend : PnPBackend {
+    std::vector<EmuPnP*> all;
+    std::vector<EmuPnP*> spec;
+    EmuPnP* of(PnPState* s) { for (auto* p : all) if (&p->st == s) return p; return nullptr; }
+    int speculate(PnPState* const* S, int count, const int* H, std::vector<std::vector<int32_t>>& counts) override {
+        counts.assign(count, {});
+        spec.assign(count, nullptr);
+        for (int i = 0; i < count; ++i) {
+            EmuPnP* p = of(S[i]);
+            spec[i] = p;
+            PnPState& s = *S[i];
+            s.rng.ensure(tab(), H[i] * s.mRansacMinSet);
+            const float K[4] = {s.fx, s.fy, s.cx, s.cy};
+            p->poses.assign((size_t)H[i] * 12, 0.f);
+            p->masks.assign(H[i], std::vector<uint64_t>(p->words, 0));
+            for (int h = 0; h < H[i]; ++h) {
+                int32_t idx[8];
+                float R[9], t[3];
+                he_pnp_hypothesis(s.mRansacMinSet, s.rng.window, s.rng.g, h, s.N, p->pts4.data(), p->uv.data(), K,
+                                  s.max_rows, p->pws.data(), p->als.data(), idx, R, t);
+                std::memcpy(&p->poses[12 * h], R, 36);
+                std::memcpy(&p->poses[12 * h + 9], t, 12);
+                std::vector<uint8_t> m(s.N);
+                int c = he_pnp_count(R, t, K, s.th2, s.N, p->pts4.data(), p->uv.data(), m.data());
+                for (int j = 0; j < s.N; ++j) if (m[j]) p->masks[h][j >> 6] |= 1ull << (j & 63);
+                counts[i].push_back(c);
+            }
+        }
+        return 0;
+    }
+    int adopt_best(PnPState* s, int i, int k) override {
+        EmuPnP* p = spec[i];
+        p->best = p->masks[k];
+        pose12_to_T(&p->poses[12 * k], s->mBestTcw);
+        return 0;
+    }
+    int refine(PnPState* const* S, int count, const int* rows_after, int* rcount, float (*rpose)[12]) override {
+        for (int i = 0; i < count; ++i) {
+            EmuPnP* p = of(S[i]);
+            PnPState& s = *S[i];
+            int r = 0;
+            for (int j = 0; j < s.N; ++j)
+                if ((p->best[j >> 6] >> (j & 63)) & 1ull) {
+                    for (int c = 0; c < 3; ++c) p->pws[3 * r + c] = p->pts4[4 * j + c];
+                    p->us[2 * r] = p->uv[2 * j]; p->us[2 * r + 1] = p->uv[2 * j + 1];
+                    ++r;
+                }
+            const float K[4] = {s.fx, s.fy, s.cx, s.cy};
+            float R[9], t[3];
+            he_pnp_rows(r, rows_after[i], p->pws.data(), p->us.data(), p->als.data(), K, R, t);
+            std::vector<uint8_t> m(s.N);
+            rcount[i] = he_pnp_count(R, t, K, s.th2, s.N, p->pts4.data(), p->uv.data(), m.data());
+            p->refined.assign(p->words, 0);
+            for (int j = 0; j < s.N; ++j) if (m[j]) p->refined[j >> 6] |= 1ull << (j & 63);
+            std::memcpy(rpose[i], R, 36);
+            std::memcpy(rpose[i] + 9, t, 12);
+        }
+        return 0;
+    }
+    int fetch_mask(PnPState* const* S, int count, const int* kind, uint8_t* const* out) override {
+        for (int i = 0; i < count; ++i) {
+            EmuPnP* p = of(S[i]);
+            const std::vector<uint64_t>& w = kind[i] == 1 ? p->refined : p->best;
+            std::memset(out[i], 0, S[i]->N_points);
+            for (int j = 0; j < S[i]->N; ++j) if ((w[j >> 6] >> (j & 63)) & 1ull) out[i][S[i]->kp_index[j]] = 1;
+        }
+        return 0;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+void* he_pnp_create(int n, int n_points, const float* p2d, const float* p3dw, const float* sigma2,
+                    const int32_t* kp_index, float fx, float fy, float cx, float cy, uint32_t seed) {
+    EmuPnP* p = new EmuPnP();
+    PnPState& s = p->st;
+    s.N = n; s.N_points = n_points; s.fx = fx; s.fy = fy; s.cx = cx; s.cy = cy;
+    s.kp_index.assign(kp_index, kp_index + n);
+    s.sigma2.assign(sigma2, sigma2 + n);
+    s.reset(seed);
+    p->pts4.resize(4 * (size_t)n);
+    p->uv.assign(p2d, p2d + 2 * (size_t)n);
+    for (int i = 0; i < n; ++i) {
+        for (int c = 0; c < 3; ++c) p->pts4[4 * i + c] = p3dw[3 * i + c];
+        p->pts4[4 * i + 3] = sigma2[i];
+    }
+    const size_t cap = std::max(n, 8);
+    p->pws.assign(3 * cap, 0.0); p->us.assign(2 * cap, 0.0); p->als.assign(4 * cap, 0.0);
+    p->words = (std::max(n, 1) + 63) / 64;
+    p->best.assign(p->words, 0); p->refined.assign(p->words, 0);
+    pnp_set_params(s, 0.99, 8, 300, 4, 0.4f, 5.991f);
+    return p;
+}
+void he_pnp_destroy(void* h) { delete static_cast<EmuPnP*>(h); }
+void he_pnp_set_params(void* h, double prob, int mi, int mx, int ms, float eps, float th2) {
+    pnp_set_params(static_cast<EmuPnP*>(h)->st, prob, mi, mx, ms, eps, th2);
+}
+// results: per solver int4 (ok, no_more, n_inliers, iterations) + T[16]; masks n_points bytes each
+int he_pnp_iterate_many(void** hs, int count, const int32_t* its, int32_t* out_i4, float* out_T, uint8_t** masks) {
+    EmuPnPBackend be;
+    std::vector<PnPState*> S(count);
+    std::vector<int> n(its, its + count);
+    for (int i = 0; i < count; ++i) { be.all.push_back(static_cast<EmuPnP*>(hs[i])); S[i] = &be.all[i]->st; }
+    std::vector<PnPResult> res(count);
+    int st = pnp_iterate_many(be, S.data(), count, n.data(), res.data(), masks);
+    for (int i = 0; i < count; ++i) {
+        out_i4[4 * i] = res[i].ok; out_i4[4 * i + 1] = res[i].no_more; out_i4[4 * i + 2] = res[i].n_inliers;
+        out_i4[4 * i + 3] = res[i].iterations;
+        if (res[i].ok) std::memcpy(out_T + 16 * i, res[i].T, 64);
+        if (!res[i].ok && masks && masks[i]) masks[i][0] = 0;
+    }
+    return st;
+}
+void he_pnp_state(void* h, int32_t* out) {
+    const PnPState& t = static_cast<EmuPnP*>(h)->st;
+    out[0] = t.mnIterations; out[1] = t.mRansacMaxIts; out[2] = t.mRansacMinInliers; out[3] = t.mnBestInliers;
+    out[4] = t.max_rows;
+}
+
+}  // extern "C"

@@ -74,3 +74,58 @@ def pnp_count(scene, R, t, th2=5.991):
     c = lib().he_pnp_count(np.ascontiguousarray(R, np.float32).ravel(), np.ascontiguousarray(t, np.float32), K,
                            th2, scene.n, pts4, uv, m)
     return c, m.astype(bool)
+
+
+class EmuPnP:
+    """Full PnPsolver::iterate emulation on the CPU: product replay logic (rsc_engine.h) + the
+    host-compiled per-lane device numerics.  TEST-ONLY."""
+
+    def __init__(self, scene, seed=1):
+        L = lib()
+        L.he_pnp_create.restype = C.c_void_p
+        L.he_pnp_create.argtypes = [C.c_int, C.c_int, f32p, f32p, f32p, i32p, C.c_float, C.c_float, C.c_float,
+                                    C.c_float, C.c_uint32]
+        L.he_pnp_destroy.argtypes = [C.c_void_p]
+        L.he_pnp_set_params.argtypes = [C.c_void_p, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
+        L.he_pnp_iterate_many.argtypes = [C.POINTER(C.c_void_p), C.c_int, i32p, i32p, f32p, C.POINTER(C.c_void_p)]
+        L.he_pnp_state.argtypes = [C.c_void_p, i32p]
+        self._keep = (np.ascontiguousarray(scene.p2d, np.float32), np.ascontiguousarray(scene.p3dw, np.float32),
+                      np.ascontiguousarray(scene.sigma2, np.float32), np.ascontiguousarray(scene.kp_index, np.int32))
+        self.n_points = int(scene.n_points)
+        self.h = L.he_pnp_create(scene.n, self.n_points, *self._keep, scene.fx, scene.fy, scene.cx, scene.cy, seed)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().he_pnp_destroy(self.h)
+            self.h = None
+
+    def set_ransac_parameters(self, *p):
+        lib().he_pnp_set_params(self.h, *p)
+
+    def state(self):
+        out = np.zeros(5, np.int32)
+        lib().he_pnp_state(self.h, out)
+        return dict(iterations=int(out[0]), max_iterations=int(out[1]), min_inliers=int(out[2]),
+                    best_inliers=int(out[3]), max_rows=int(out[4]))
+
+    def iterate(self, n):
+        return iterate_many([self], n)[0]
+
+
+def iterate_many(emus, n):
+    k = len(emus)
+    hs = (C.c_void_p * k)(*[e.h for e in emus])
+    its = np.ascontiguousarray(np.broadcast_to(np.asarray(n, np.int32), (k,)))
+    i4 = np.zeros(4 * k, np.int32)
+    T = np.zeros(16 * k, np.float32)
+    masks = [np.zeros(max(e.n_points, 1), np.uint8) for e in emus]
+    mp = (C.c_void_p * k)(*[m.ctypes.data for m in masks])
+    st = lib().he_pnp_iterate_many(hs, k, its, i4, T, mp)
+    assert st == 0
+    out = []
+    for i in range(k):
+        ok = bool(i4[4 * i])
+        out.append(dict(ok=ok, no_more=bool(i4[4 * i + 1]), n_inliers=int(i4[4 * i + 2]),
+                        iterations=int(i4[4 * i + 3]), T=T[16 * i:16 * i + 16].reshape(4, 4),
+                        inliers=(masks[i][:emus[i].n_points].astype(bool) if ok else np.zeros(0, bool))))
+    return out

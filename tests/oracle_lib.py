@@ -80,8 +80,43 @@ def lib():
     L.ora_sim3_trace_get.argtypes = [vp, C.c_int, i32p, f32p]
     L.ora_sim3_run_prepared_batch.argtypes = [C.c_int, i32p, i64p, f32p, f32p, f32p, f32p, u64p, u64p, f32p, f32p,
                                               u32p, C.c_double, C.c_int, C.c_int, C.c_int, C.c_int, i32p, f32p]
+    f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+    L.ora_sym_eig.argtypes = [C.c_int, f64p, f64p, f64p]
+    L.ora_sym_eig4f.argtypes = [f32p, f32p, f32p]
+    L.ora_svd_solve.argtypes = [C.c_int, f64p, f64p, f64p]
+    L.ora_random_int.argtypes = [C.c_uint32, C.c_int, i32p, i32p]
     _lib = L
     return L
+
+
+def sym_eig(A):
+    A = np.ascontiguousarray(A, np.float64)
+    n = A.shape[0]
+    V = np.zeros((n, n)); w = np.zeros(n)
+    st = lib().ora_sym_eig(n, A.ravel(), V.reshape(-1), w)
+    return w, V, st == 0
+
+
+def sym_eig4f(A):
+    A = np.ascontiguousarray(A, np.float32)
+    V = np.zeros((4, 4), np.float32); w = np.zeros(4, np.float32)
+    st = lib().ora_sym_eig4f(A.ravel(), V.reshape(-1), w)
+    return w, V, st == 0
+
+
+def svd_solve(A, b):
+    A = np.ascontiguousarray(A, np.float64)
+    k = A.shape[1]
+    x = np.zeros(k)
+    lib().ora_svd_solve(k, A.ravel(), np.ascontiguousarray(b, np.float64), x)
+    return x
+
+
+def random_int(seed, maxes):
+    maxes = np.ascontiguousarray(maxes, np.int32)
+    out = np.zeros(len(maxes), np.int32)
+    lib().ora_random_int(seed, len(maxes), maxes, out)
+    return out
 
 
 def glibc_rand(seed: int, n: int) -> np.ndarray:
@@ -121,7 +156,7 @@ class OraclePnP:
         T = np.zeros(16, dtype=np.float32)
         ok = lib().ora_pnp_iterate(self.h, n_iterations, C.byref(nm), mask, C.byref(ml), C.byref(ni), T)
         return dict(ok=bool(ok), no_more=bool(nm.value), n_inliers=ni.value,
-                    inliers=mask[:ml.value].astype(bool), T=T.reshape(4, 4))
+                    inliers=mask[:ml.value].astype(bool), T=T.reshape(4, 4), iterations=self.info()["iterations"])
 
     def info(self):
         out = np.zeros(5, dtype=np.int32)
@@ -194,7 +229,7 @@ class OracleSim3:
         R = np.zeros(9, np.float32); t = np.zeros(3, np.float32)
         lib().ora_sim3_estimate(self.h, R, t)
         return dict(ok=bool(ok), no_more=bool(nm.value), n_inliers=ni.value, inliers=mask[:self.n1].astype(bool),
-                    R=R.reshape(3, 3), t=t)
+                    R=R.reshape(3, 3), t=t, iterations=self.info()["iterations"])
 
     def info(self):
         out = np.zeros(3, np.int32)

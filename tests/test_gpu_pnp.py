@@ -118,3 +118,14 @@ def test_iterate_many_equals_sequential():
     for i in range(6):
         one = b[i].iterate(120)
         assert_pnp_equal(many[i], one, f"cand {i}")
+
+
+@pytest.mark.parametrize("case", [1, 4, 17, 43, 66, 72, 74, 83, 95, 98])
+def test_refine_failure_respeculation(case):
+    """Failed Refine -> stale EPnP rows -> later hypotheses recomputed on the GPU (Q6, Q8)."""
+    from gpu_common import refine_fail_scene
+    sc, seed = refine_fail_scene(case)
+    g, o = make(sc, seed)
+    for rnd in range(20):
+        assert_pnp_equal(g.iterate(5), o.iterate(5), f"round {rnd}")
+        assert g.state()["max_rows"] == o.info()["max_rows"]
