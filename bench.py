@@ -70,6 +70,7 @@ def pnp_batch(rng, C, N, ratio):
 
 def run_pnp(engine, ctx, scenes, args, dist, rank, world):
     solvers = [engine.PnPSolver(ctx, sc, 1) for sc in scenes]
+    batch = engine.SolverBatch(solvers)
     C = len(solvers)
     gather = None
     if dist is not None:
@@ -78,10 +79,9 @@ def run_pnp(engine, ctx, scenes, args, dist, rank, world):
         gather = (torch, rec, torch.zeros(world * C, 20, dtype=torch.float32, device="cuda"))
 
     def step(s):
-        for c, sv in enumerate(solvers):
-            sv.reset(1 + c + C * (s + 1000 * rank))
-            sv.set_ransac_parameters(*RELOC)
-        outs = engine.pnp_iterate_many(solvers, args.iters, with_masks=False)
+        batch.reset(1 + np.arange(C) + C * (s + 1000 * rank))
+        batch.set_ransac_parameters(*RELOC)
+        outs = batch.iterate(args.iters)
         if gather is not None:
             torch, rec, allrec = gather
             h = np.zeros((C, 20), np.float32)
@@ -121,12 +121,12 @@ def run_sim3(engine, ctx, rng, args):
     from rsc import synth
     pairs = [synth.make_sim3_pair(rng, 1000, 15) for _ in range(32)]
     solvers = [engine.Sim3Solver(ctx, p, 1) for p in pairs]
+    batch = engine.SolverBatch(solvers)
 
     def step(s):
-        for c, sv in enumerate(solvers):
-            sv.reset(1 + c + 32 * s)
-            sv.set_ransac_parameters(*LOOP)
-        outs = engine.sim3_iterate_many(solvers, args.iters, with_masks=False)
+        batch.reset(1 + np.arange(32) + 32 * s)
+        batch.set_ransac_parameters(*LOOP)
+        outs = batch.iterate(args.iters)
         return sum(o["iterations"] for o in outs)
 
     for s in range(args.warmup):

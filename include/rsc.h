@@ -86,6 +86,10 @@ int rsc_pnp_iterate_many(rsc_pnp* const* solvers, int count, const int32_t* n_it
                          uint8_t* const* inliers);
 /* Back to the freshly constructed state with a new rand() stream (reuse HBM-resident data). */
 int rsc_pnp_reset(rsc_pnp* s, uint32_t seed);
+/* rsc_pnp_reset / rsc_pnp_set_ransac_parameters over `count` solvers in one call. */
+int rsc_pnp_reset_many(rsc_pnp* const* solvers, int count, const uint32_t* seeds);
+int rsc_pnp_set_ransac_parameters_many(rsc_pnp* const* solvers, int count, double probability, int min_inliers,
+                                       int max_iterations, int min_set, float epsilon, float th2);
 /* out: [0] mnIterations [1] mRansacMaxIts [2] mRansacMinInliers [3] mnBestInliers
  *      [4] maximum_number_of_correspondences [5] N [6] N_points [7] mRansacMinSet */
 int rsc_pnp_get_state(const rsc_pnp* s, int32_t out[8]);
@@ -121,6 +125,9 @@ int rsc_sim3_find(rsc_sim3* s, rsc_sim3_result* out, uint8_t* inliers);
 int rsc_sim3_iterate_many(rsc_sim3* const* solvers, int count, const int32_t* n_iterations, rsc_sim3_result* out,
                           uint8_t* const* inliers);
 int rsc_sim3_reset(rsc_sim3* s, uint32_t seed);
+int rsc_sim3_reset_many(rsc_sim3* const* solvers, int count, const uint32_t* seeds);
+int rsc_sim3_set_ransac_parameters_many(rsc_sim3* const* solvers, int count, double probability, int min_inliers,
+                                        int max_iterations);
 /* out: [0] mnIterations [1] mRansacMaxIts [2] mRansacMinInliers [3] mnBestInliers [4] N [5] mN1 */
 int rsc_sim3_get_state(const rsc_sim3* s, int32_t out[6]);
 /* Prepared per-correspondence arrays built by the constructor (for parity tests):

@@ -23,12 +23,26 @@ namespace rsc {
 // ------------------------------------------------------------------------------------------------
 // PnP hypotheses
 // ------------------------------------------------------------------------------------------------
-template <int NS>
+// Diagnostic phase stamps (s_memtime) — only the STAMP=true instantiation executes them; the
+// production kernel passes NoStamp (inlined away).
+struct ClockStamp {
+    uint64_t* out;
+    __device__ void operator()(int k) const {
+        unsigned long long t;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        out[k] = t;
+    }
+};
+
+template <int NS, bool STAMP>
 __global__ __launch_bounds__(64) void pnp_solve_kernel(const DevPnP* __restrict__ probs,
                                                        const LaunchProb* __restrict__ lps,
                                                        const int2* __restrict__ wg_table,
                                                        const uint32_t* __restrict__ rng_T,
-                                                       float* __restrict__ poses, int32_t* __restrict__ samples) {
+                                                       float* __restrict__ poses, int32_t* __restrict__ samples,
+                                                       uint64_t* __restrict__ stamps) {
     __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles * 64];
     const int lane = threadIdx.x;
     const int2 wt = wg_table[blockIdx.x];
@@ -37,6 +51,9 @@ __global__ __launch_bounds__(64) void pnp_solve_kernel(const DevPnP* __restrict_
     if (h >= lp.H) return;
     const DevPnP& P = probs[lp.prob];
 
+    uint64_t st_local[10];
+    ClockStamp cs{st_local};
+    if (STAMP) cs(0);
     uint32_t w[31];
     RSC_UNROLL for (int j = 0; j < 31; ++j) w[j] = lp.window[j];
     uint32_t words[NS];
@@ -57,7 +74,13 @@ __global__ __launch_bounds__(64) void pnp_solve_kernel(const DevPnP* __restrict_
     const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
     LaneMat S{slab + lane, 64};
     float R[9], t[3];
-    epnp_compute_pose(st, K, S, R, t);
+    if (STAMP) {
+        epnp_compute_pose(st, K, S, R, t, cs);
+        cs(9);
+        for (int k = 0; k < 10; ++k) stamps[(size_t)(lp.out0 + h) * 10 + k] = st_local[k];
+    } else {
+        epnp_compute_pose(st, K, S, R, t);
+    }
 
     float* out = poses + (size_t)(lp.out0 + h) * 12;
     RSC_UNROLL for (int k = 0; k < 9; ++k) out[k] = R[k];
@@ -330,9 +353,9 @@ __global__ void rng_stream_kernel(const uint32_t* __restrict__ T, Window31 w, in
 hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                             const uint32_t* T, float* poses, int32_t* samples, hipStream_t st) {
     switch (ns) {
-        case 4: pnp_solve_kernel<4><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples); break;
-        case 5: pnp_solve_kernel<5><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples); break;
-        case 6: pnp_solve_kernel<6><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples); break;
+        case 4: pnp_solve_kernel<4, false><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples, nullptr); break;
+        case 5: pnp_solve_kernel<5, false><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples, nullptr); break;
+        case 6: pnp_solve_kernel<6, false><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples, nullptr); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -376,6 +399,12 @@ hipError_t launch_rng_stream(const uint32_t* T, const uint32_t* window, int g0, 
     Window31 w;
     for (int j = 0; j < 31; ++j) w.w[j] = window[j];
     rng_stream_kernel<<<(n + 255) / 256, 256, 0, st>>>(T, w, g0, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pnp_solve_stamped(int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
+                                    const uint32_t* T, float* poses, uint64_t* stamps, hipStream_t st) {
+    pnp_solve_kernel<4, true><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, nullptr, stamps);
     return hipGetLastError();
 }
 

@@ -182,6 +182,7 @@ void timing_begin(rsc_context* C, int slot) {
 // ------------------------------------------------------------------------------------------------
 struct HipPnPBackend : PnPBackend {
     rsc_context* C;
+    uint64_t* diag_stamps = nullptr;  // diagnostic phase-stamp build (rsc_diag_pnp_phase_stamps)
     std::vector<rsc_pnp*> solvers;  // index = state slot in the current call
     explicit HipPnPBackend(rsc_context* c) : C(c) {}
     rsc_pnp* of(PnPState* s) {
@@ -259,11 +260,21 @@ struct HipPnPBackend : PnPBackend {
         const DevPnP* dprobs = reinterpret_cast<const DevPnP*>(base + o_probs);
         const LaunchProb* dlps = reinterpret_cast<const LaunchProb*>(base + o_lps);
         timing_begin(C, 0);
-        for (int g = 0; g < 3; ++g) {
-            if (solve_wgs[g].empty()) continue;
-            RSC_HIP(launch_pnp_solve(4 + g, (int)solve_wgs[g].size(), dprobs, dlps,
-                                     reinterpret_cast<const int2*>(base + o_solve[g]), C->d_table.p, C->d_poses.p,
-                                     C->keep_samples ? C->d_samples.p : nullptr, C->stream));
+        if (diag_stamps) {
+            DevBuf<uint64_t> d;
+            if (int e = d.ensure((size_t)total * 10)) return e;
+            RSC_HIP(launch_pnp_solve_stamped((int)solve_wgs[0].size(), dprobs, dlps,
+                                             reinterpret_cast<const int2*>(base + o_solve[0]), C->d_table.p,
+                                             C->d_poses.p, d.p, C->stream));
+            RSC_HIP(hipMemcpyAsync(diag_stamps, d.p, (size_t)total * 80, hipMemcpyDeviceToHost, C->stream));
+            RSC_HIP(hipStreamSynchronize(C->stream));
+        } else {
+            for (int g = 0; g < 3; ++g) {
+                if (solve_wgs[g].empty()) continue;
+                RSC_HIP(launch_pnp_solve(4 + g, (int)solve_wgs[g].size(), dprobs, dlps,
+                                         reinterpret_cast<const int2*>(base + o_solve[g]), C->d_table.p, C->d_poses.p,
+                                         C->keep_samples ? C->d_samples.p : nullptr, C->stream));
+            }
         }
         timing_begin(C, 1);
         RSC_HIP(launch_pnp_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
@@ -833,6 +844,69 @@ int rsc_rand_stream(rsc_context* C, uint32_t seed, int n, int32_t* out) {
         done += chunk;
     }
     return RSC_OK;
+}
+
+// ---- batched state helpers ----
+int rsc_pnp_reset_many(rsc_pnp* const* s, int count, const uint32_t* seeds) {
+    if (count < 0 || (count && (!s || !seeds))) return RSC_ERR_ARG;
+    for (int i = 0; i < count; ++i) {
+        if (!s[i]) return RSC_ERR_ARG;
+        s[i]->st.reset(seeds[i]);
+    }
+    return RSC_OK;
+}
+
+int rsc_pnp_set_ransac_parameters_many(rsc_pnp* const* s, int count, double probability, int min_inliers,
+                                       int max_iterations, int min_set, float epsilon, float th2) {
+    if (count < 0 || (count && !s)) return RSC_ERR_ARG;
+    for (int i = 0; i < count; ++i) {
+        if (!s[i]) return RSC_ERR_ARG;
+        pnp_set_params(s[i]->st, probability, min_inliers, max_iterations, min_set, epsilon, th2);
+    }
+    return RSC_OK;
+}
+
+int rsc_sim3_reset_many(rsc_sim3* const* s, int count, const uint32_t* seeds) {
+    if (count < 0 || (count && (!s || !seeds))) return RSC_ERR_ARG;
+    for (int i = 0; i < count; ++i) {
+        if (!s[i]) return RSC_ERR_ARG;
+        s[i]->st.reset(seeds[i]);
+    }
+    return RSC_OK;
+}
+
+int rsc_sim3_set_ransac_parameters_many(rsc_sim3* const* s, int count, double probability, int min_inliers,
+                                        int max_iterations) {
+    if (count < 0 || (count && !s)) return RSC_ERR_ARG;
+    for (int i = 0; i < count; ++i) {
+        if (!s[i]) return RSC_ERR_ARG;
+        sim3_set_params(s[i]->st, probability, min_inliers, max_iterations);
+    }
+    return RSC_OK;
+}
+
+// ---- diagnostics (not part of the drop-in boundary) ----
+// s_memtime stamps at the phase boundaries of the EPnP solve for H hypotheses of each solver
+// (min_set 4, state unchanged): out[(solver*H + h)*10 + k].
+int rsc_diag_pnp_phase_stamps(rsc_pnp* const* solvers, int count, int H, uint64_t* out) {
+    if (count <= 0 || !solvers || !out || H <= 0) return RSC_ERR_ARG;
+    rsc_context* C = solvers[0]->ctx;
+    RSC_HIP(hipSetDevice(C->device));
+    HipPnPBackend be(C);
+    be.solvers.assign(solvers, solvers + count);
+    be.diag_stamps = out;
+    std::vector<PnPState*> S(count);
+    std::vector<int> Hs(count, H);
+    std::vector<RngStream> keep(count);
+    for (int i = 0; i < count; ++i) {
+        S[i] = &solvers[i]->st;
+        if (S[i]->mRansacMinSet != 4) return RSC_ERR_UNSUPPORTED;
+        keep[i] = S[i]->rng;
+    }
+    std::vector<std::vector<int32_t>> counts;
+    int st = be.speculate(S.data(), count, Hs.data(), counts);
+    for (int i = 0; i < count; ++i) S[i]->rng = keep[i];
+    return st;
 }
 
 }  // extern "C"

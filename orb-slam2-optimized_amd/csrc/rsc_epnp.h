@@ -361,10 +361,15 @@ RSC_HD double compute_R_and_t(const St& st, const Intrinsics& K, const LaneMat& 
 // Second half of compute_pose: with the lower triangle of MtM already in the slab, run the 12x12
 // eigensolver, L_6x10/rho, the three beta approximations + Gauss-Newton + compute_R_and_t, and
 // keep the smallest reprojection error (PnPsolver.cpp:379-414).
-template <class St>
+struct NoStamp {
+    RSC_HD void operator()(int) const {}
+};
+
+template <class St, class Stamp = NoStamp>
 RSC_HD double epnp_stage_c(const St& st, const Intrinsics& K, const LaneMat& S, const double (&cws)[4][3],
-                           float (&Rf)[9], float (&tf)[3]) {
+                           float (&Rf)[9], float (&tf)[3], Stamp stamp = Stamp()) {
     sym_eig12(S);
+    stamp(3);
     compute_L_6x10(S);
     {
         auto d2 = [&](int a, int b) {
@@ -379,14 +384,18 @@ RSC_HD double epnp_stage_c(const St& st, const Intrinsics& K, const LaneMat& S, 
     {
         double betas[4] = {0.0, 0.0, 0.0, 0.0};
         find_betas<1>(S, betas);
+        stamp(4);
         gauss_newton(S, betas);
+        stamp(5);
         best_err = compute_R_and_t(st, K, S, betas, pw0, bestR, bestt);
+        stamp(6);
     }
     {
         double betas[4] = {0.0, 0.0, 0.0, 0.0}, R[3][3], t[3];
         find_betas<2>(S, betas);
         gauss_newton(S, betas);
         double e = compute_R_and_t(st, K, S, betas, pw0, R, t);
+        stamp(7);
         if (e < best_err) {
             best_err = e;
             RSC_UNROLL for (int r = 0; r < 3; ++r) {
@@ -400,6 +409,7 @@ RSC_HD double epnp_stage_c(const St& st, const Intrinsics& K, const LaneMat& S, 
         find_betas<3>(S, betas);
         gauss_newton(S, betas);
         double e = compute_R_and_t(st, K, S, betas, pw0, R, t);
+        stamp(8);
         if (e < best_err) {
             best_err = e;
             RSC_UNROLL for (int r = 0; r < 3; ++r) {
@@ -416,12 +426,15 @@ RSC_HD double epnp_stage_c(const St& st, const Intrinsics& K, const LaneMat& S, 
 }
 
 // PnPsolver::compute_pose (PnPsolver.cpp:359-415) for one lane.  Outputs float R (row-major) and t.
-template <class St>
-RSC_HD double epnp_compute_pose(St& st, const Intrinsics& K, const LaneMat& S, float (&Rf)[9], float (&tf)[3]) {
+template <class St, class Stamp = NoStamp>
+RSC_HD double epnp_compute_pose(St& st, const Intrinsics& K, const LaneMat& S, float (&Rf)[9], float (&tf)[3],
+                                Stamp stamp = Stamp()) {
     double cws[4][3];
     control_points_and_alphas(st, cws);
+    stamp(1);
     build_MtM(st, K, S);
-    return epnp_stage_c(st, K, S, cws, Rf, tf);
+    stamp(2);
+    return epnp_stage_c(st, K, S, cws, Rf, tf, stamp);
 }
 
 }  // namespace rsc

@@ -54,6 +54,8 @@ hipError_t launch_rng_stream(const uint32_t* T, const uint32_t* window, int g0, 
 
 hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                             const uint32_t* T, float* poses, int32_t* samples, hipStream_t st);
+hipError_t launch_pnp_solve_stamped(int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
+                                    const uint32_t* T, float* poses, uint64_t* stamps, hipStream_t st);
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,
                            const float* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st);
 hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, int mask_words_out,

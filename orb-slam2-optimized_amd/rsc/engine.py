@@ -32,6 +32,8 @@ EXPORTED = [
     "rsc_pnp_iterate_many", "rsc_pnp_reset", "rsc_pnp_get_state", "rsc_pnp_last_samples",
     "rsc_sim3_create", "rsc_sim3_destroy", "rsc_sim3_set_ransac_parameters", "rsc_sim3_iterate", "rsc_sim3_find",
     "rsc_sim3_iterate_many", "rsc_sim3_reset", "rsc_sim3_get_state", "rsc_sim3_prepared", "rsc_rand_stream",
+    "rsc_pnp_reset_many", "rsc_pnp_set_ransac_parameters_many", "rsc_sim3_reset_many",
+    "rsc_sim3_set_ransac_parameters_many",
 ]
 
 
@@ -94,6 +96,14 @@ def load_library(path: str = LIB_PATH):
     L.rsc_sim3_get_state.argtypes = [vp, i32p]
     L.rsc_sim3_prepared.argtypes = [vp, f32p, f32p, f32p, f32p, u64p, u64p, i32p]
     L.rsc_rand_stream.argtypes = [vp, C.c_uint32, C.c_int, i32p]
+    u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+    L.rsc_pnp_reset_many.argtypes = [C.POINTER(vp), C.c_int, u32p]
+    L.rsc_pnp_set_ransac_parameters_many.argtypes = [C.POINTER(vp), C.c_int, C.c_double, C.c_int, C.c_int, C.c_int,
+                                                     C.c_float, C.c_float]
+    L.rsc_sim3_reset_many.argtypes = [C.POINTER(vp), C.c_int, u32p]
+    L.rsc_sim3_set_ransac_parameters_many.argtypes = [C.POINTER(vp), C.c_int, C.c_double, C.c_int, C.c_int]
+    L.rsc_diag_pnp_phase_stamps.argtypes = [C.POINTER(vp), C.c_int, C.c_int,
+                                            np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
     _lib = L
     return L
 
@@ -299,3 +309,37 @@ def sim3_iterate_many(solvers, n_iterations, with_masks: bool = True):
     mp = (C.c_void_p * n)(*[(m.ctypes.data if with_masks else None) for m in masks])
     _check(L.rsc_sim3_iterate_many(hs, n, its, res, mp), "iterate_many")
     return [_sim3_out(res[i], masks[i][:solvers[i].n1]) for i in range(n)]
+
+
+class SolverBatch:
+    """A fixed list of solvers (one context) with batched reset / SetRansacParameters / iterate —
+    the relocalization (PnP) or loop-closure (Sim3) candidate set of one event."""
+
+    def __init__(self, solvers):
+        self.solvers = list(solvers)
+        self.kind = "pnp" if isinstance(self.solvers[0], PnPSolver) else "sim3"
+        self._h = (C.c_void_p * len(self.solvers))(*[s.h.value for s in self.solvers])
+
+    def reset(self, seeds):
+        seeds = np.ascontiguousarray(np.asarray(seeds, np.uint32))
+        L = load_library()
+        f = L.rsc_pnp_reset_many if self.kind == "pnp" else L.rsc_sim3_reset_many
+        _check(f(self._h, len(self.solvers), seeds), "reset_many")
+
+    def set_ransac_parameters(self, *params):
+        L = load_library()
+        if self.kind == "pnp":
+            _check(L.rsc_pnp_set_ransac_parameters_many(self._h, len(self.solvers), *params), "params_many")
+        else:
+            _check(L.rsc_sim3_set_ransac_parameters_many(self._h, len(self.solvers), *params), "params_many")
+
+    def iterate(self, n_iterations, with_masks=False):
+        if self.kind == "pnp":
+            return pnp_iterate_many(self.solvers, n_iterations, with_masks)
+        return sim3_iterate_many(self.solvers, n_iterations, with_masks)
+
+    def phase_stamps(self, H):
+        """Diagnostic: per-hypothesis s_memtime stamps at the EPnP phase boundaries (PnP only)."""
+        out = np.zeros(len(self.solvers) * H * 10, np.uint64)
+        _check(load_library().rsc_diag_pnp_phase_stamps(self._h, len(self.solvers), H, out), "phase_stamps")
+        return out.reshape(len(self.solvers), H, 10)
