@@ -78,20 +78,22 @@ def run_pnp(engine, ctx, scenes, args, dist, rank, world):
         rec = torch.zeros(C, 20, dtype=torch.float32, device="cuda")
         gather = (torch, rec, torch.zeros(world * C, 20, dtype=torch.float32, device="cuda"))
 
+    seeds = np.zeros(C, np.uint32)
+    h = np.zeros((C, 20), np.float32)
+
     def step(s):
-        batch.reset(1 + np.arange(C) + C * (s + 1000 * rank))
+        seeds[:] = 1 + np.arange(C) + C * (s + 1000 * rank)
+        batch.reset(seeds)
         batch.set_ransac_parameters(*RELOC)
-        outs = batch.iterate(args.iters)
+        outs = batch.iterate_raw(args.iters)
         if gather is not None:
             torch, rec, allrec = gather
-            h = np.zeros((C, 20), np.float32)
-            for i, o in enumerate(outs):
-                h[i, 0], h[i, 1], h[i, 2], h[i, 3] = o["ok"], o["no_more"], o["n_inliers"], o["iterations"]
-                h[i, 4:20] = o["T"].ravel()
+            h[:, 0], h[:, 1], h[:, 2], h[:, 3] = outs["ok"], outs["no_more"], outs["n_inliers"], outs["iterations"]
+            h[:, 4:20] = outs["T"].reshape(C, 16)
             rec.copy_(torch.from_numpy(h))
             dist.all_gather_into_tensor(allrec, rec)  # RCCL over xGMI: winner records of all ranks
             torch.cuda.synchronize()
-        return sum(o["iterations"] for o in outs), outs
+        return int(outs["iterations"].sum()), outs
 
     for s in range(args.warmup):
         step(s)
@@ -126,8 +128,7 @@ def run_sim3(engine, ctx, rng, args):
     def step(s):
         batch.reset(1 + np.arange(32) + 32 * s)
         batch.set_ransac_parameters(*LOOP)
-        outs = batch.iterate(args.iters)
-        return sum(o["iterations"] for o in outs)
+        return int(batch.iterate_raw(args.iters)["iterations"].sum())
 
     for s in range(args.warmup):
         step(s)

@@ -48,6 +48,11 @@ int rsc_context_synchronize(rsc_context* ctx);
  * out[3] = number of solve launches, out[4] = hypotheses solved. */
 int rsc_context_last_timing(rsc_context* ctx, double out[5]);
 int rsc_context_enable_timing(rsc_context* ctx, int enable);
+/* Hypothesis-solve kernel family for PnP (all produce bit-identical results):
+ * 0 = auto, 1 = single kernel (one lane per hypothesis), 2 = quad-cooperative eigenvectors +
+ * one wave per beta approximation, 3 = lane-per-hypothesis eigenvectors + per-approximation waves.
+ * The environment variable RSC_SOLVE_MODE (mono|quad|split) sets the initial value. */
+int rsc_context_set_solve_mode(rsc_context* ctx, int mode);
 
 /* ---- PnPsolver (include/PnPsolver.hpp:21-138, src/PnPsolver.cpp) ------------------------------ */
 typedef struct {

@@ -16,6 +16,7 @@
 #include "rsc_core.h"
 #include "rsc_epnp.h"
 #include "rsc_sim3.h"
+#include "rsc_quad.h"
 #include "rsc_kernels.h"
 
 namespace rsc {
@@ -88,6 +89,41 @@ __global__ __launch_bounds__(64) void pnp_solve_kernel(const DevPnP* __restrict_
     if (samples) {
         RSC_UNROLL for (int i = 0; i < NS; ++i) samples[(size_t)(lp.out0 + h) * 8 + i] = idx[i];
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// PnP hypotheses, two-kernel form (rsc_quad.h): quad-cooperative eigenvectors, then one wave per
+// beta approximation.
+// ------------------------------------------------------------------------------------------------
+template <int NS>
+__global__ __launch_bounds__(64, 2) void pnp_eig_quad_kernel(const DevPnP* __restrict__ probs,
+                                                          const LaunchProb* __restrict__ lps,
+                                                          const int2* __restrict__ wg_table,
+                                                          const uint32_t* __restrict__ rng_T,
+                                                          double* __restrict__ stage, int32_t* __restrict__ samples) {
+    __shared__ __attribute__((aligned(16))) double smem[kQuadHyps * kQuadRegion];
+    pnp_eig_quad_body<NS, 99>(probs, lps, wg_table, rng_T, stage, samples, smem);
+}
+
+template <int NS>
+__global__ __launch_bounds__(64) void pnp_eig_lane_kernel(const DevPnP* __restrict__ probs,
+                                                          const LaunchProb* __restrict__ lps,
+                                                          const int2* __restrict__ wg_table,
+                                                          const uint32_t* __restrict__ rng_T,
+                                                          double* __restrict__ stage, int32_t* __restrict__ samples) {
+    __shared__ __attribute__((aligned(16))) double slab[144 * 64];
+    pnp_eig_lane_body<NS>(probs, lps, wg_table, rng_T, stage, samples, slab);
+}
+
+template <int NS>
+__global__ __launch_bounds__(192, 2) void pnp_betas_kernel(const DevPnP* __restrict__ probs,
+                                                        const LaunchProb* __restrict__ lps,
+                                                        const int2* __restrict__ wg_table,
+                                                        const double* __restrict__ stage,
+                                                        const int32_t* __restrict__ samples,
+                                                        float* __restrict__ poses) {
+    __shared__ __attribute__((aligned(16))) double smem[kBetasSmemDoubles];
+    pnp_betas_body<NS>(probs, lps, wg_table, stage, samples, poses, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -356,6 +392,25 @@ hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchPr
         case 4: pnp_solve_kernel<4, false><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples, nullptr); break;
         case 5: pnp_solve_kernel<5, false><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples, nullptr); break;
         case 6: pnp_solve_kernel<6, false><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples, nullptr); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_pnp_solve_split(bool quad, int ns, int nwg16, const int2* wgt16, int nwg64, const int2* wgt64,
+                                  const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
+                                  float* poses, int32_t* samples, hipStream_t st) {
+    switch (ns) {
+#define RSC_CASE(N)                                                                                   \
+    case N:                                                                                           \
+        if (quad)                                                                                     \
+            pnp_eig_quad_kernel<N><<<nwg16, 64, 0, st>>>(probs, lps, wgt16, T, stage, samples);       \
+        else                                                                                          \
+            pnp_eig_lane_kernel<N><<<nwg64, 64, 0, st>>>(probs, lps, wgt64, T, stage, samples);       \
+        pnp_betas_kernel<N><<<nwg64, 192, 0, st>>>(probs, lps, wgt64, stage, samples, poses);         \
+        break;
+        RSC_CASE(4) RSC_CASE(5) RSC_CASE(6)
+#undef RSC_CASE
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

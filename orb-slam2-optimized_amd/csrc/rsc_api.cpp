@@ -98,6 +98,7 @@ struct rsc_context {
     DevBuf<int32_t> d_counts;
     DevBuf<uint64_t> d_masks;
     DevBuf<int32_t> d_samples;
+    DevBuf<double> d_stage;  // quad path: per-hypothesis stage records between the two solve kernels
     DevBuf<char> d_desc;
     PinBuf<char> h_desc;
     PinBuf<int32_t> h_counts;
@@ -105,6 +106,10 @@ struct rsc_context {
     DevBuf<char> d_refine;
     int mask_words = 0;  // per hypothesis, last speculation
     bool keep_samples = true;
+    // PnP hypothesis kernels ($RSC_SOLVE_MODE): 0 = auto, 1 = "mono" (one kernel, lane per
+    // hypothesis), 2 = "quad" (quad-cooperative eigenvectors + per-approximation waves),
+    // 3 = "split" (lane-per-hypothesis eigenvectors + per-approximation waves).
+    int solve_mode = 0;
     // timing
     bool timing = false;
     hipEvent_t ev[6] = {};
@@ -236,26 +241,34 @@ struct HipPnPBackend : PnPBackend {
         const int mw = ppt * 4;
         C->mask_words = mw;
         // work tables
-        std::vector<std::vector<int2>> solve_wgs(3);
+        std::vector<std::vector<int2>> solve_wgs(3), quad_wgs(3);
         std::vector<int4> scan_wgs;
         const int HC = 32;  // hypotheses per scan workgroup
+        const int mode = diag_stamps ? 1 : (C->solve_mode ? C->solve_mode : kAutoSolveMode);
+        const bool quad = (mode == 2), split = (mode == 2 || mode == 3);
         for (int i = 0; i < count; ++i) {
             const int g = S[i]->mRansacMinSet - 4;
             for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs[g].push_back(make_int2(i, h0));
+            if (quad)
+                for (int h0 = 0; h0 < H[i]; h0 += kQuadHyps) quad_wgs[g].push_back(make_int2(i, h0));
             for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
         }
         Blob b;
         const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevPnP));
         const size_t o_lps = b.add(lps.data(), lps.size() * sizeof(LaunchProb));
         size_t o_solve[3];
+        size_t o_quad[3];
         for (int g = 0; g < 3; ++g) o_solve[g] = b.add(solve_wgs[g].data(), solve_wgs[g].size() * sizeof(int2));
+        for (int g = 0; g < 3; ++g) o_quad[g] = b.add(quad_wgs[g].data(), quad_wgs[g].size() * sizeof(int2));
         const size_t o_scan = b.add(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
         if (int e = upload_blob(C, b)) return e;
         if (int e = C->d_poses.ensure((size_t)total * 12)) return e;
         if (int e = C->d_counts.ensure((size_t)total)) return e;
         if (int e = C->d_masks.ensure((size_t)total * mw)) return e;
-        if (C->keep_samples)
+        if (C->keep_samples || split)
             if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
+        if (split)
+            if (int e = C->d_stage.ensure((size_t)total * kStageDoubles)) return e;
         const char* base = C->d_desc.p;
         const DevPnP* dprobs = reinterpret_cast<const DevPnP*>(base + o_probs);
         const LaunchProb* dlps = reinterpret_cast<const LaunchProb*>(base + o_lps);
@@ -271,9 +284,18 @@ struct HipPnPBackend : PnPBackend {
         } else {
             for (int g = 0; g < 3; ++g) {
                 if (solve_wgs[g].empty()) continue;
-                RSC_HIP(launch_pnp_solve(4 + g, (int)solve_wgs[g].size(), dprobs, dlps,
-                                         reinterpret_cast<const int2*>(base + o_solve[g]), C->d_table.p, C->d_poses.p,
-                                         C->keep_samples ? C->d_samples.p : nullptr, C->stream));
+                if (split) {
+                    RSC_HIP(launch_pnp_solve_split(quad, 4 + g, (int)quad_wgs[g].size(),
+                                                  reinterpret_cast<const int2*>(base + o_quad[g]),
+                                                  (int)solve_wgs[g].size(),
+                                                  reinterpret_cast<const int2*>(base + o_solve[g]), dprobs, dlps,
+                                                  C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p,
+                                                  C->stream));
+                } else {
+                    RSC_HIP(launch_pnp_solve(4 + g, (int)solve_wgs[g].size(), dprobs, dlps,
+                                             reinterpret_cast<const int2*>(base + o_solve[g]), C->d_table.p,
+                                             C->d_poses.p, C->keep_samples ? C->d_samples.p : nullptr, C->stream));
+                }
             }
         }
         timing_begin(C, 1);
@@ -532,6 +554,11 @@ int rsc_context_create(int device, rsc_context** out) {
     C->device = device;
     RSC_HIP(hipStreamCreateWithFlags(&C->stream, hipStreamNonBlocking));
     C->own_stream = true;
+    if (const char* m = std::getenv("RSC_SOLVE_MODE")) {
+        if (!std::strcmp(m, "mono")) C->solve_mode = 1;
+        else if (!std::strcmp(m, "quad")) C->solve_mode = 2;
+        else if (!std::strcmp(m, "split")) C->solve_mode = 3;
+    }
     C->table.build();
     if (int e = C->d_table.ensure(C->table.T.size())) return e;
     RSC_HIP(hipMemcpy(C->d_table.p, C->table.T.data(), C->table.T.size() * 4, hipMemcpyHostToDevice));
@@ -562,6 +589,12 @@ int rsc_context_set_stream(rsc_context* C, void* s) {
 int rsc_context_synchronize(rsc_context* C) {
     if (!C) return RSC_ERR_ARG;
     RSC_HIP(hipStreamSynchronize(C->stream));
+    return RSC_OK;
+}
+
+int rsc_context_set_solve_mode(rsc_context* C, int mode) {
+    if (!C || mode < 0 || mode > 3) return RSC_ERR_ARG;
+    C->solve_mode = mode;
     return RSC_OK;
 }
 

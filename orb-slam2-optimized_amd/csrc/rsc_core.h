@@ -26,6 +26,15 @@
 #define RSC_HD inline
 #endif
 #define RSC_UNROLL _Pragma("unroll")
+// End of a data-dependent loop body whose last statement is conditional: a convergent no-op that
+// keeps LLVM from tail-duplicating the latch.  Without it the loop gets two backedges and
+// LoopSimplify splits it into a nested loop, in which the lanes of a wave that took different
+// backedges wait for each other (measured 2.6x on the 12x12 eigensolver).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RSC_LOOP_FENCE() __builtin_amdgcn_wave_barrier()
+#else
+#define RSC_LOOP_FENCE() ((void)0)
+#endif
 
 namespace rsc {
 
@@ -56,45 +65,75 @@ struct LaneMat {
 // ---------------------------------------------------------------------------------------------
 // Eigen building blocks (Jacobi.h, MathFunctions.h)
 // ---------------------------------------------------------------------------------------------
+// The two helpers below are written with value selects instead of if/else: in a wave whose lanes
+// hold different hypotheses both branches would execute (two divisions and a square root each);
+// the selected operands feed the same operations, so the results are bit-identical to Eigen's.
 template <typename S> RSC_HD S eig_hypot(S x, S y) {
-    S ax = rabs(x), ay = rabs(y), p, qp;
-    if (ax > ay) { p = ax; qp = ay / p; } else { p = ay; qp = ax / p; }
-    if (p == S(0)) return S(0);
-    return p * rsqrt_(S(1) + qp * qp);
+    const S ax = rabs(x), ay = rabs(y);
+    const bool gx = ax > ay;
+    const S p = gx ? ax : ay;
+    const S qp = (gx ? ay : ax) / p;
+    const S r = p * rsqrt_(S(1) + qp * qp);
+    return (p == S(0)) ? S(0) : r;
 }
 
+// JacobiRotation::makeGivens (real case).
 template <typename S> RSC_HD void make_givens(S p, S q, S& c, S& s) {
-    if (q == S(0)) {
-        c = p < S(0) ? S(-1) : S(1);
-        s = S(0);
-    } else if (p == S(0)) {
-        c = S(0);
-        s = q < S(0) ? S(1) : S(-1);
-    } else if (rabs(p) > rabs(q)) {
-        S t = q / p;
-        S u = rsqrt_(S(1) + t * t);
-        if (p < S(0)) u = -u;
-        c = S(1) / u;
-        s = -t * c;
-    } else {
-        S t = p / q;
-        S u = rsqrt_(S(1) + t * t);
-        if (q < S(0)) u = -u;
-        s = -S(1) / u;
-        c = -t * s;
+    const bool big = rabs(p) > rabs(q);
+    const S t = (big ? q : p) / (big ? p : q);
+    S u = rsqrt_(S(1) + t * t);
+    if ((big ? p : q) < S(0)) u = -u;
+    const S r = S(1) / u;  // big: c = 1/u, s = -t*c;  else: s = -1/u (= -(1/u)), c = -t*s
+    const S sb = -r;
+    S cc = big ? r : (-t) * sb;
+    S ss = big ? (-t) * r : sb;
+    if (p == S(0)) { cc = S(0); ss = (q < S(0)) ? S(1) : S(-1); }
+    if (q == S(0)) { cc = (p < S(0)) ? S(-1) : S(1); ss = S(0); }
+    c = cc;
+    s = ss;
+}
+
+// Ascending selection sort of the eigenvalues (end of computeFromTridiagonal_impl): the same
+// comparisons and swaps as Eigen, recorded as a permutation (sorted column c = column perm[c]).
+// Written with value selects only — conditional stores into the arrays would let LLVM merge the
+// mutually exclusive swaps into one dynamically indexed store, forcing the arrays to scratch.
+template <typename S, int n>
+RSC_HD void eig_sort(S (&diag)[n], int (&perm)[n]) {
+    RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
+        int kk = 0;
+        S mn = diag[i];
+        RSC_UNROLL for (int j = 1; j < n - i; ++j) {
+            const bool lt = diag[i + j] < mn;
+            mn = lt ? diag[i + j] : mn;
+            kk = lt ? j : kk;
+        }
+        RSC_UNROLL for (int j = 1; j < n - i; ++j) {
+            const bool sw = (j == kk);
+            const S a = diag[i], b = diag[i + j];
+            diag[i] = sw ? b : a;
+            diag[i + j] = sw ? a : b;
+            const int pa = perm[i], pb = perm[i + j];
+            perm[i] = sw ? pb : pa;
+            perm[i + j] = sw ? pa : pb;
+        }
     }
 }
 
-// Implicit symmetric QR iterations on (diag, sub) with the rotations handed to `qapply(k,c,s)`
-// (which must perform Q = Q * G on columns k,k+1).  computeFromTridiagonal_impl + sort.
-// Returns Eigen's "Success".  perm receives nothing: the sort is performed through `qswap(i,j)`.
-template <typename S, int n, typename QApply, typename QSwap>
-RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply qapply, QSwap qswap) {
+// Implicit symmetric QR iterations on (diag, sub) with the rotations handed to
+// `qapply(k, c, s, apply)` (which must perform Q = Q * G on columns k,k+1 when `apply`, and leave
+// Q bit-identical otherwise).  computeFromTridiagonal_impl + sort.
+// Returns Eigen's "Success".  perm: the sort's column permutation (identity when not converged,
+// as Eigen skips the sort then); the caller applies it to its eigenvector storage.
+template <typename S, int n, typename QApply>
+RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply qapply, int (&perm)[n]) {
     const int maxIterations = 30;
     int end = n - 1, start = 0, iter = 0;
     const S considerAsZero = lim<S>::min();
     const S precision_inv = S(1) / lim<S>::eps();
-    while (end > 0) {
+    // Single-exit loop (Eigen's two `break`s folded into `run`): with several exits the CFG
+    // structurizer nests the loop and every lane pays for the extra control flow.
+    bool run = true;
+    while (run) {
         RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
             if (i >= start && i < end) {
                 if (rabs(sub[i]) < considerAsZero) {
@@ -107,9 +146,12 @@ RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply qapply, QSwap qswap
         }
         RSC_UNROLL for (int i = n - 2; i >= 0; --i)
             if (i == end - 1 && sub[i] == S(0)) end--;
-        if (end <= 0) break;
-        iter++;
-        if (iter > maxIterations * n) break;
+        run = end > 0;
+        if (run) {
+            iter++;
+            run = iter <= maxIterations * n;
+        }
+        if (!run) continue;
         start = end - 1;
         RSC_UNROLL for (int i = n - 2; i >= 0; --i)
             if (i == start - 1 && sub[i] != S(0)) start--;
@@ -149,23 +191,20 @@ RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply qapply, QSwap qswap
                     z = -s * sub[k + 1];
                     sub[k + 1] = c * sub[k + 1];
                 }
-                if (!(c == S(1) && s == S(0))) qapply(k, c, s);
+                // Eigen skips identity rotations; qapply receives the flag and selects (a
+                // conditional call here gets tail-duplicated into the loop latch, which turns
+                // the QR loop into a nested loop that serialises the lanes of a wave)
+                qapply(k, c, s, !(c == S(1) && s == S(0)));
             }
         }
+        RSC_LOOP_FENCE();
     }
     const bool ok = (iter <= maxIterations * n);
-    if (ok) {
-        RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
-            int kk = 0;
-            S mn = diag[i];
-            RSC_UNROLL for (int j = 1; j < n - i; ++j)
-                if (diag[i + j] < mn) { mn = diag[i + j]; kk = j; }
-            if (kk > 0) {
-                RSC_UNROLL for (int j = 1; j < n - i; ++j)
-                    if (j == kk) { rswap(diag[i], diag[i + j]); qswap(i, i + j); }
-            }
-        }
-    }
+#ifdef RSC_QR_STATS
+    rsc_qr_stats_hook(n, iter);  // host-side diagnostics only (tools/)
+#endif
+    RSC_UNROLL for (int i = 0; i < n; ++i) perm[i] = i;
+    if (ok) eig_sort<S, n>(diag, perm);
     return ok;
 }
 
@@ -329,17 +368,24 @@ RSC_HD bool sym_eig_reg(const S (&A)[n][n], S (&V)[n][n], S (&w)[n]) {
         RSC_UNROLL for (int i = 0; i < n; ++i)
             RSC_UNROLL for (int j = 0; j < n; ++j) V[i][j] = mat[i][j];
     }
-    auto qapply = [&](int k, S c, S s) {
+    auto qapply = [&](int k, S c, S s, bool apply) {
         RSC_UNROLL for (int i = 0; i < n; ++i) {
             S xi = V[i][k], yi = V[i][k + 1];
-            V[i][k] = c * xi - s * yi;
-            V[i][k + 1] = s * xi + c * yi;
+            V[i][k] = apply ? c * xi - s * yi : xi;
+            V[i][k + 1] = apply ? s * xi + c * yi : yi;
         }
     };
-    auto qswap = [&](int a, int b) {
-        RSC_UNROLL for (int r = 0; r < n; ++r) rswap(V[r][a], V[r][b]);
-    };
-    bool ok = tridiag_qr<S, n>(diag, sub, qapply, qswap);
+    int perm[n];
+    bool ok = tridiag_qr<S, n>(diag, sub, qapply, perm);
+    S Vs[n][n];
+    RSC_UNROLL for (int r = 0; r < n; ++r)
+        RSC_UNROLL for (int c = 0; c < n; ++c) {
+            S x = V[r][0];
+            RSC_UNROLL for (int p = 1; p < n; ++p) x = (perm[c] == p) ? V[r][p] : x;
+            Vs[r][c] = x;
+        }
+    RSC_UNROLL for (int r = 0; r < n; ++r)
+        RSC_UNROLL for (int c = 0; c < n; ++c) V[r][c] = Vs[r][c];
     RSC_UNROLL for (int i = 0; i < n; ++i) w[i] = diag[i] * scale;
     return ok;
 }
@@ -349,7 +395,9 @@ RSC_HD bool sym_eig_reg(const S (&A)[n][n], S (&V)[n][n], S (&w)[n]) {
 // e = r*12 + c).  On entry the lower triangle holds MtM; on exit the slab holds the eigenvectors
 // (columns, ascending eigenvalues).  Only the eigenvector matrix is needed by EPnP.
 // ---------------------------------------------------------------------------------------------
-RSC_HD bool sym_eig12(const LaneMat& M) {
+// Part 1: scaling, Householder tridiagonalisation and accumulation of the Householder sequence
+// into the slab.  Returns the scale; diag/sub receive the tridiagonal matrix.
+RSC_HD double sym_eig12_tridiag(const LaneMat& M, double (&diag)[12], double (&sub)[11]) {
     constexpr int n = 12;
     // mat = lower triangle (upper zeroed); scale = max |.| in column-major order
     double scale = rabs(M.at(0, 0));
@@ -420,7 +468,6 @@ RSC_HD bool sym_eig12(const LaneMat& M) {
         M.at(i + 1, i) = beta;
         hC[i] = h;
     }
-    double diag[n], sub[n - 1];
     RSC_UNROLL for (int k = 0; k < n; ++k) diag[k] = M.at(k, k);
     RSC_UNROLL for (int k = 0; k < n - 1; ++k) sub[k] = M.at(k + 1, k);
     RSC_UNROLL for (int i = 0; i < n; ++i) {
@@ -453,17 +500,37 @@ RSC_HD bool sym_eig12(const LaneMat& M) {
         }
         RSC_UNROLL for (int r = k + 1; r < n; ++r) M.at(r, k) = 0.0;
     }
-    auto qapply = [&](int k, double c, double s) {
+    return scale;
+}
+
+// Part 2: implicit symmetric QR on (diag, sub) accumulating the rotations into the slab's
+// eigenvector matrix, then the ascending sort (columns 0..3 materialised).
+RSC_HD bool sym_eig12_qr(const LaneMat& M, double (&diag)[12], double (&sub)[11]) {
+    constexpr int n = 12;
+    auto qapply = [&](int k, double c, double s, bool apply) {
         RSC_UNROLL for (int i = 0; i < n; ++i) {
             double xi = M.at(i, k), yi = M.at(i, k + 1);
-            M.at(i, k) = c * xi - s * yi;
-            M.at(i, k + 1) = s * xi + c * yi;
+            M.at(i, k) = apply ? c * xi - s * yi : xi;
+            M.at(i, k + 1) = apply ? s * xi + c * yi : yi;
         }
     };
-    auto qswap = [&](int a, int b) {
-        RSC_UNROLL for (int r = 0; r < n; ++r) rswap(M.at(r, a), M.at(r, b));
-    };
-    return tridiag_qr<double, n>(diag, sub, qapply, qswap);
+    int perm[n];
+    const bool ok = tridiag_qr<double, n>(diag, sub, qapply, perm);
+    // Only the eigenvector columns EPnP reads (0..3, the four smallest eigenvalues) are
+    // materialised in sorted order; columns 4..11 keep the unsorted vectors (they are reused as
+    // scratch for L_6x10 and rho).
+    RSC_UNROLL for (int r = 0; r < n; ++r) {
+        double v[4];
+        RSC_UNROLL for (int c = 0; c < 4; ++c) v[c] = M.at(r, perm[c]);
+        RSC_UNROLL for (int c = 0; c < 4; ++c) M.at(r, c) = v[c];
+    }
+    return ok;
+}
+
+RSC_HD bool sym_eig12(const LaneMat& M) {
+    double diag[12], sub[11];
+    sym_eig12_tridiag(M, diag, sub);
+    return sym_eig12_qr(M, diag, sub);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -681,6 +748,7 @@ RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6]
                 }
             }
         }
+        RSC_LOOP_FENCE();
     }
     double sv[k];
     RSC_UNROLL for (int i = 0; i < k; ++i) {

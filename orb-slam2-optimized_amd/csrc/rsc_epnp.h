@@ -130,25 +130,45 @@ RSC_HD void build_MtM(const St& st, const Intrinsics& K, const LaneMat& S) {
 RSC_HD double& Lref(const LaneMat& S, int i, int j) { return S(slab_free(i * 10 + j)); }
 RSC_HD double& rhoref(const LaneMat& S, int i) { return S(slab_free(60 + i)); }
 
+// Stage-C storage views: eigenvector columns 0..3 (ev), L_6x10 and rho.
+// SlabView: everything inside one per-lane slab (the lane-per-hypothesis kernels and Refine).
+struct SlabView {
+    LaneMat S;
+    RSC_HD double ev(int r, int c) const { return S.at(r, c); }
+    RSC_HD double& L(int i, int j) const { return Lref(S, i, j); }
+    RSC_HD double& rho(int i) const { return rhoref(S, i); }
+};
+// SplitView: eigenvectors [12][4], L [6][10] + rho [6] in separate (LDS) arrays, element stride
+// `stride` (1 = contiguous per hypothesis, 64 = element-major across a wave).
+struct SplitView {
+    const double* evp;
+    double* Lp;
+    int stride;
+    RSC_HD double ev(int r, int c) const { return evp[(r * 4 + c) * stride]; }
+    RSC_HD double& L(int i, int j) const { return Lp[(i * 10 + j) * stride]; }
+    RSC_HD double& rho(int i) const { return Lp[(60 + i) * stride]; }
+};
+
 // compute_L_6x10 (PnPsolver.cpp:604-637) from the eigenvector columns 0..3 held in the slab.
-RSC_HD void compute_L_6x10(const LaneMat& S) {
+template <class SV>
+RSC_HD void compute_L_6x10(const SV& S) {
     RSC_UNROLL for (int j = 0; j < 6; ++j) {
         const int a = (j < 3) ? 0 : (j < 5 ? 1 : 2);
         const int b = (j < 3) ? j + 1 : (j < 5 ? j - 1 : 3);
         double dv[4][3];
         RSC_UNROLL for (int i = 0; i < 4; ++i)
-            RSC_UNROLL for (int c = 0; c < 3; ++c) dv[i][c] = S.at(3 * a + c, i) - S.at(3 * b + c, i);
+            RSC_UNROLL for (int c = 0; c < 3; ++c) dv[i][c] = S.ev(3 * a + c, i) - S.ev(3 * b + c, i);
         auto dot = [&](int x, int y) { return dv[x][0] * dv[y][0] + dv[x][1] * dv[y][1] + dv[x][2] * dv[y][2]; };
-        Lref(S, j, 0) = dot(0, 0);
-        Lref(S, j, 1) = 2.0 * dot(0, 1);
-        Lref(S, j, 2) = dot(1, 1);
-        Lref(S, j, 3) = 2.0 * dot(0, 2);
-        Lref(S, j, 4) = 2.0 * dot(1, 2);
-        Lref(S, j, 5) = dot(2, 2);
-        Lref(S, j, 6) = 2.0 * dot(0, 3);
-        Lref(S, j, 7) = 2.0 * dot(1, 3);
-        Lref(S, j, 8) = 2.0 * dot(2, 3);
-        Lref(S, j, 9) = dot(3, 3);
+        S.L(j, 0) = dot(0, 0);
+        S.L(j, 1) = 2.0 * dot(0, 1);
+        S.L(j, 2) = dot(1, 1);
+        S.L(j, 3) = 2.0 * dot(0, 2);
+        S.L(j, 4) = 2.0 * dot(1, 2);
+        S.L(j, 5) = dot(2, 2);
+        S.L(j, 6) = 2.0 * dot(0, 3);
+        S.L(j, 7) = 2.0 * dot(1, 3);
+        S.L(j, 8) = 2.0 * dot(2, 3);
+        S.L(j, 9) = dot(3, 3);
     }
 }
 
@@ -202,13 +222,14 @@ RSC_HD bool qr_solve_6x4(double (&A)[6][4], double (&b)[6], double (&X)[4]) {
 }
 
 // gauss_newton (PnPsolver.cpp:649-691); X persists across the 5 iterations (Q9).
-RSC_HD void gauss_newton(const LaneMat& S, double (&betas)[4]) {
+template <class SV>
+RSC_HD void gauss_newton(const SV& S, double (&betas)[4]) {
     double X[4] = {0.0, 0.0, 0.0, 0.0};
     RSC_UNROLL for (int it = 0; it < 5; it++) {
         double A[6][4], B[6];
         RSC_UNROLL for (int i = 0; i < 6; i++) {
             double l[10];
-            RSC_UNROLL for (int j = 0; j < 10; ++j) l[j] = Lref(S, i, j);
+            RSC_UNROLL for (int j = 0; j < 10; ++j) l[j] = S.L(i, j);
             const double Lt[4][4] = {{2 * l[0], l[1], l[3], l[6]},
                                      {l[1], 2 * l[2], l[4], l[7]},
                                      {l[3], l[4], 2 * l[5], l[8]},
@@ -216,7 +237,7 @@ RSC_HD void gauss_newton(const LaneMat& S, double (&betas)[4]) {
             RSC_UNROLL for (int r = 0; r < 4; ++r)
                 A[i][r] = Lt[r][0] * betas[0] + Lt[r][1] * betas[1] + Lt[r][2] * betas[2] + Lt[r][3] * betas[3];
             const double* b = betas;
-            B[i] = rhoref(S, i) - (l[0] * b[0] * b[0] + l[1] * b[0] * b[1] + l[2] * b[1] * b[1] +
+            B[i] = S.rho(i) - (l[0] * b[0] * b[0] + l[1] * b[0] * b[1] + l[2] * b[1] * b[1] +
                                    l[3] * b[0] * b[2] + l[4] * b[1] * b[2] + l[5] * b[2] * b[2] +
                                    l[6] * b[0] * b[3] + l[7] * b[1] * b[3] + l[8] * b[2] * b[3] +
                                    l[9] * b[3] * b[3]);
@@ -227,14 +248,14 @@ RSC_HD void gauss_newton(const LaneMat& S, double (&betas)[4]) {
 }
 
 // find_betas_approx_{1,2,3} (PnPsolver.cpp:520-602).
-template <int which>
-RSC_HD void find_betas(const LaneMat& S, double (&betas)[4]) {
+template <int which, class SV>
+RSC_HD void find_betas(const SV& S, double (&betas)[4]) {
     double rho[6];
-    RSC_UNROLL for (int r = 0; r < 6; ++r) rho[r] = rhoref(S, r);
+    RSC_UNROLL for (int r = 0; r < 6; ++r) rho[r] = S.rho(r);
     if (which == 1) {
         double A[6][4], b4[4];
         RSC_UNROLL for (int r = 0; r < 6; ++r) {
-            A[r][0] = Lref(S, r, 0); A[r][1] = Lref(S, r, 1); A[r][2] = Lref(S, r, 3); A[r][3] = Lref(S, r, 6);
+            A[r][0] = S.L(r, 0); A[r][1] = S.L(r, 1); A[r][2] = S.L(r, 3); A[r][3] = S.L(r, 6);
         }
         jacobi_svd_solve_6xk<4>(A, rho, b4);
         if (b4[0] < 0) {
@@ -250,7 +271,7 @@ RSC_HD void find_betas(const LaneMat& S, double (&betas)[4]) {
         }
     } else if (which == 2) {
         double A[6][3], b3[3];
-        RSC_UNROLL for (int r = 0; r < 6; ++r) { A[r][0] = Lref(S, r, 0); A[r][1] = Lref(S, r, 1); A[r][2] = Lref(S, r, 2); }
+        RSC_UNROLL for (int r = 0; r < 6; ++r) { A[r][0] = S.L(r, 0); A[r][1] = S.L(r, 1); A[r][2] = S.L(r, 2); }
         jacobi_svd_solve_6xk<3>(A, rho, b3);
         if (b3[0] < 0) {
             betas[0] = sqrt(-b3[0]);
@@ -265,7 +286,7 @@ RSC_HD void find_betas(const LaneMat& S, double (&betas)[4]) {
     } else {
         double A[6][5], b5[5];
         RSC_UNROLL for (int r = 0; r < 6; ++r)
-            RSC_UNROLL for (int c = 0; c < 5; ++c) A[r][c] = Lref(S, r, c);
+            RSC_UNROLL for (int c = 0; c < 5; ++c) A[r][c] = S.L(r, c);
         jacobi_svd_solve_6xk<5>(A, rho, b5);
         if (b5[0] < 0) {
             betas[0] = sqrt(-b5[0]);
@@ -283,15 +304,15 @@ RSC_HD void find_betas(const LaneMat& S, double (&betas)[4]) {
 // compute_R_and_t (PnPsolver.cpp:504-515) = compute_ccs + compute_pcs + solve_for_sign +
 // estimate_R_and_t (:433-493, Horn with float N entries, conjugated quaternion) +
 // reprojection_error (:417-431).  pw0 equals the centroid cws[0] (same sum, same division).
-template <class St>
-RSC_HD double compute_R_and_t(const St& st, const Intrinsics& K, const LaneMat& S, const double (&betas)[4],
+template <class St, class SV>
+RSC_HD double compute_R_and_t(const St& st, const Intrinsics& K, const SV& S, const double (&betas)[4],
                               const double (&pw0)[3], double (&R)[3][3], double (&t)[3]) {
     const int n = st.n();
     double ccs[4][3];
     RSC_UNROLL for (int i = 0; i < 4; i++)
         RSC_UNROLL for (int c = 0; c < 3; ++c) {
             double s = 0.0;
-            RSC_UNROLL for (int j = 0; j < 4; j++) s = s + betas[j] * S.at(3 * i + c, j);
+            RSC_UNROLL for (int j = 0; j < 4; j++) s = s + betas[j] * S.ev(3 * i + c, j);
             ccs[i][c] = s;
         }
     // solve_for_sign: pcs(0,2) with the unflipped ccs
@@ -370,14 +391,22 @@ RSC_HD double epnp_stage_c(const St& st, const Intrinsics& K, const LaneMat& S, 
                            float (&Rf)[9], float (&tf)[3], Stamp stamp = Stamp()) {
     sym_eig12(S);
     stamp(3);
+    return epnp_betas_and_pose(st, K, SlabView{S}, cws, Rf, tf, stamp);
+}
+
+// L_6x10, rho, the three beta approximations + Gauss-Newton + compute_R_and_t, smallest
+// reprojection error wins (PnPsolver.cpp:383-414), given the eigenvectors in the view.
+template <class St, class SV, class Stamp = NoStamp>
+RSC_HD double epnp_betas_and_pose(const St& st, const Intrinsics& K, const SV& S, const double (&cws)[4][3],
+                                  float (&Rf)[9], float (&tf)[3], Stamp stamp = Stamp()) {
     compute_L_6x10(S);
     {
         auto d2 = [&](int a, int b) {
             double x = cws[a][0] - cws[b][0], y = cws[a][1] - cws[b][1], z = cws[a][2] - cws[b][2];
             return x * x + y * y + z * z;
         };
-        rhoref(S, 0) = d2(0, 1); rhoref(S, 1) = d2(0, 2); rhoref(S, 2) = d2(0, 3);
-        rhoref(S, 3) = d2(1, 2); rhoref(S, 4) = d2(1, 3); rhoref(S, 5) = d2(2, 3);
+        S.rho(0) = d2(0, 1); S.rho(1) = d2(0, 2); S.rho(2) = d2(0, 3);
+        S.rho(3) = d2(1, 2); S.rho(4) = d2(1, 3); S.rho(5) = d2(2, 3);
     }
     const double pw0[3] = {cws[0][0], cws[0][1], cws[0][2]};
     double bestR[3][3], bestt[3], best_err;

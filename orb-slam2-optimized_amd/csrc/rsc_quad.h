@@ -1,0 +1,422 @@
+// rsc_quad.h — quad-cooperative EPnP hypothesis (4 lanes of a wave per hypothesis).
+//
+// Why: one lane per hypothesis runs PnPsolver::compute_pose as one long dependent FP64 chain, and a
+// relocalization batch (19,200 hypotheses) fills only 300 of the 1,024 SIMDs with one wave each, so
+// the solve is latency-bound.  Four lanes per hypothesis give 4x the waves and split the chain:
+//   * 12x12 Householder tridiagonalisation: lane q owns rows 4j+q (j = 0..2) of the full symmetric
+//     matrix in VGPRs; the Householder vector and A*v are exchanged with DPP quad broadcasts;
+//   * accumulation of the Householder sequence: lane q owns columns 4j+q of Q;
+//   * implicit QR: the Givens chase is computed redundantly by the 4 lanes (bitwise identical),
+//     each lane applies the rotations to its own 3 rows of Q;
+//   * the three beta approximations of PnPsolver.cpp:383-414 (+ Gauss-Newton + compute_R_and_t)
+//     run in a second kernel, one wave per approximation over 64 hypotheses, and the smallest
+//     error wins in the reference's order.
+// Every scalar is produced by the same operations on the same operands as the sequential
+// restatement (rsc_core.h / oracle), so results are bitwise identical; the only reorderings are of
+// independent scalars (and of max(), which is order-free for the non-NaN case handled below).
+#pragma once
+#include "rsc_core.h"
+#include "rsc_epnp.h"
+#include "rsc_kernels.h"
+
+namespace rsc {
+
+constexpr int kQuadT = 144;  // MtM lower triangle, then the Q transpose
+constexpr int kQuadE = 55;   // Householder essential vectors
+constexpr int kQuadRegion = kQuadT + kQuadE + 1;  // 200 doubles per hypothesis
+// stage record offsets (rsc_kernels.h kStageDoubles)
+constexpr int kStEv = 0, kStAl = 48, kStCws = 72;
+// pnp_betas_kernel LDS: eigenvectors [48][64], L+rho [66][64], errors [3][64], poses [3][12][64] f32
+constexpr int kBetasSmemDoubles = (48 + 66) * 64 + 3 * 64 + 3 * 12 * 64 / 2;
+
+// Offset of step i's essential Householder vector (entries v[1..10-i]) in the E region.
+RSC_HD constexpr int quad_eoff(int i) { return 10 * i - (i * (i - 1)) / 2; }
+
+template <int SRC>
+__device__ __forceinline__ double qb_(double x) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), SRC * 0x55, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), SRC * 0x55, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+// Value of x in lane `src` of this lane's quad (src is a compile-time constant after unrolling).
+__device__ __forceinline__ double qb(double x, int src) {
+    switch (src & 3) {
+        case 0: return qb_<0>(x);
+        case 1: return qb_<1>(x);
+        case 2: return qb_<2>(x);
+        default: return qb_<3>(x);
+    }
+}
+
+// x[base + q] of a register array (static base), 0 outside [0, n).
+template <int n>
+__device__ __forceinline__ double sel4(const double (&x)[n], int base, int q) {
+    double r = 0.0;
+    RSC_UNROLL for (int t = 0; t < 4; ++t) {
+        const int i = base + t;
+        if (i >= 0 && i < n && q == t) r = x[i];
+    }
+    return r;
+}
+
+// Tridiagonalisation of the scaled 12x12 (sym_eig12_tridiag, Householder part).  A: own rows,
+// full symmetric.  E: this hypothesis' essential-vector region (written by lane 0).
+__device__ __forceinline__ void quad_tridiag(double (&A)[3][12], int q, double* E, double (&diag)[12],
+                                             double (&sub)[11], double (&hC)[11]) {
+    constexpr int n = 12, NN = 11;
+    RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
+        const int rs = n - i - 1;
+        double v[NN], w2[NN], hcv[NN];
+        RSC_UNROLL for (int k = 0; k < NN; ++k) {
+            v[k] = 0.0;
+            hcv[k] = 0.0;
+            if (k < rs) v[k] = qb(A[(i + 1 + k) >> 2][i], (i + 1 + k) & 3);
+        }
+        double tail = 0.0;
+        if (rs > 1) {
+            tail = v[1] * v[1];
+            RSC_UNROLL for (int k = 2; k < NN; ++k) if (k < rs) tail = tail + v[k] * v[k];
+        }
+        const double c0 = v[0];
+        double h, beta;
+        if (tail <= lim<double>::min()) {
+            h = 0.0;
+            beta = c0;
+            RSC_UNROLL for (int k = 1; k < NN; ++k) if (k < rs) v[k] = 0.0;
+        } else {
+            beta = sqrt(c0 * c0 + tail);
+            if (c0 >= 0.0) beta = -beta;
+            const double den = c0 - beta;
+            RSC_UNROLL for (int k = 1; k < NN; ++k) if (k < rs) v[k] = v[k] / den;
+            h = (beta - c0) / beta;
+        }
+        v[0] = 1.0;
+        if (q == 0) {
+            RSC_UNROLL for (int k = 1; k < NN; ++k) if (k < rs) E[quad_eoff(i) + k - 1] = v[k];
+        }
+        RSC_UNROLL for (int k = 0; k < NN; ++k) w2[k] = h * v[k];
+        // own rows of hc = A_sub * (h v)
+        double hco[3];
+        RSC_UNROLL for (int j = 0; j < 3; ++j) {
+            hco[j] = 0.0;
+            if (4 * j + 3 >= i + 1) {
+                double acc = A[j][i + 1] * w2[0];
+                RSC_UNROLL for (int m = 1; m < NN; ++m) if (m < rs) acc = acc + A[j][i + 1 + m] * w2[m];
+                hco[j] = acc;
+            }
+        }
+        RSC_UNROLL for (int k = 0; k < NN; ++k) if (k < rs) hcv[k] = qb(hco[(i + 1 + k) >> 2], (i + 1 + k) & 3);
+        double dot = hcv[0] * v[0];
+        RSC_UNROLL for (int k = 1; k < NN; ++k) if (k < rs) dot = dot + hcv[k] * v[k];
+        const double alpha = (h * -0.5) * dot;
+        RSC_UNROLL for (int k = 0; k < NN; ++k) if (k < rs) hcv[k] = hcv[k] + alpha * v[k];
+        // rank-2 update of the own rows (both triangles: the mirrored element gets the same bits,
+        // the two products are the same and IEEE addition commutes)
+        RSC_UNROLL for (int j = 0; j < 3; ++j) {
+            if (4 * j + 3 >= i + 1) {
+                const int kr = 4 * j + q - (i + 1);
+                const double vo = sel4(v, 4 * j - (i + 1), q);
+                const double ho = sel4(hcv, 4 * j - (i + 1), q);
+                if (kr >= 0) {
+                    RSC_UNROLL for (int c = 0; c < NN; ++c)
+                        if (c < rs) A[j][i + 1 + c] = A[j][i + 1 + c] + ((-v[c]) * ho + (-hcv[c]) * vo);
+                }
+            }
+        }
+        if (q == ((i + 1) & 3)) A[(i + 1) >> 2][i] = beta;
+        hC[i] = h;
+    }
+    RSC_UNROLL for (int k = 0; k < n; ++k) diag[k] = qb(A[k >> 2][k], k & 3);
+    RSC_UNROLL for (int k = 0; k < n - 1; ++k) sub[k] = qb(A[(k + 1) >> 2][k], (k + 1) & 3);
+}
+
+// Householder sequence evalTo (sym_eig12_tridiag, accumulation part), own columns 4j+q of Q.
+__device__ __forceinline__ void quad_accumulate(double (&Qc)[3][12], int q, const double* E, const double (&hC)[11]) {
+    RSC_UNROLL for (int j = 0; j < 3; ++j)
+        RSC_UNROLL for (int r = 0; r < 12; ++r) Qc[j][r] = (r == 4 * j + q) ? 1.0 : 0.0;
+    RSC_UNROLL for (int k = 10; k >= 0; --k) {
+        const int cs = 11 - k, b0 = k + 1;
+        const double tau = hC[k];
+        if (cs == 1) {
+            if (q == 3) Qc[2][11] = Qc[2][11] * (1.0 - tau);
+        } else if (tau != 0.0) {
+            double ev[10];
+            RSC_UNROLL for (int r = 0; r < 10; ++r) ev[r] = (r < cs - 1) ? E[quad_eoff(k) + r] : 0.0;
+            RSC_UNROLL for (int j = 0; j < 3; ++j) {
+                if (4 * j + 3 >= b0 && 4 * j + q >= b0) {
+                    double acc = ev[0] * Qc[j][b0 + 1];
+                    RSC_UNROLL for (int r = 1; r < 10; ++r) if (r < cs - 1) acc = acc + ev[r] * Qc[j][b0 + 1 + r];
+                    const double tmp = acc + Qc[j][b0];
+                    Qc[j][b0] = Qc[j][b0] - tau * tmp;
+                    RSC_UNROLL for (int r = 0; r < 10; ++r) {
+                        if (r < cs - 1) {
+                            const double te = tau * ev[r];
+                            Qc[j][b0 + 1 + r] = Qc[j][b0 + 1 + r] - tmp * te;
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+
+// Kernel 1 of the two-kernel hypothesis solve: sample, control points, alphas, MtM, and the 12x12
+// eigenvectors (quad-cooperative).  Writes the stage record (eigenvectors, alphas, cws) and the
+// sample indices.  STOP < 99 truncates (diagnostics only, tools/phase_bench).
+template <int NS, int STOP>
+__device__ __forceinline__ void pnp_eig_quad_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
+                                                  const int2* __restrict__ wg_table, const uint32_t* __restrict__ rng_T,
+                                                  double* __restrict__ stage, int32_t* __restrict__ samples,
+                                                  double* smem) {
+    const int lane = threadIdx.x, g = lane >> 2, q = lane & 3;
+    const int2 wt = wg_table[blockIdx.x];
+    const LaunchProb& lp = lps[wt.x];
+    const bool active = wt.y + g < lp.H;
+    const int h = active ? wt.y + g : lp.H - 1;  // idle quads repeat the last hypothesis (no writes)
+    const DevPnP& P = probs[lp.prob];
+    const size_t rec = (size_t)(lp.out0 + h);
+    double* out = stage + rec * kStageDoubles;
+    double* T = smem + g * kQuadRegion;
+    double* E = T + kQuadT;
+
+    // ---- A: sample, control points, alphas, MtM (all four lanes, identical values) ----
+    {
+        int idx[NS];
+        uint32_t w[31];
+        RSC_UNROLL for (int j = 0; j < 31; ++j) w[j] = lp.window[j];
+        uint32_t words[NS];
+        RSC_UNROLL for (int d = 0; d < NS; ++d) words[d] = rng_word(rng_T, w, lp.g0 + h * NS + d);
+        swap_remove_sample<NS>(words, NS, P.n, idx);
+        HypStore<NS> st;
+        RSC_UNROLL for (int i = 0; i < NS; ++i) {
+            const float4 p = P.pts[idx[i]];
+            const float2 uv = P.uv[idx[i]];
+            st.pw_[i][0] = p.x; st.pw_[i][1] = p.y; st.pw_[i][2] = p.z;
+            st.u_[i][0] = uv.x; st.u_[i][1] = uv.y;
+        }
+        st.rows_ = P.rows;
+        st.spw = P.pws;
+        st.sal = P.als;
+        const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
+        double cws[4][3];
+        control_points_and_alphas(st, cws);
+        if (q == 0) {
+            build_MtM(st, K, LaneMat{T, 1});
+            if (active) {
+                RSC_UNROLL for (int i = 0; i < NS; ++i)
+                    RSC_UNROLL for (int j = 0; j < 4; ++j) out[kStAl + i * 4 + j] = st.al(i, j);
+                RSC_UNROLL for (int i = 0; i < 4; ++i)
+                    RSC_UNROLL for (int c = 0; c < 3; ++c) out[kStCws + i * 3 + c] = cws[i][c];
+                RSC_UNROLL for (int i = 0; i < NS; ++i) samples[rec * 8 + i] = idx[i];
+            }
+        }
+    }
+    __syncthreads();
+    if (STOP == 1) {
+        if (active && q == 0) out[0] = T[0] + T[143];
+        return;
+    }
+
+    // ---- B: scale + tridiagonalise (own rows) ----
+    double diag[12], sub[11], hC[11];
+    {
+        double A[3][12];
+        double m = 0.0;
+        RSC_UNROLL for (int j = 0; j < 3; ++j) {
+            const int R = 4 * j + q;
+            RSC_UNROLL for (int c = 0; c < 12; ++c) {
+                A[j][c] = T[(R >= c) ? R * 12 + c : c * 12 + R];
+                const double a = fabs(A[j][c]);
+                if (c <= R && a > m) m = a;
+            }
+        }
+        // SelfAdjointEigenSolver scale = max |lower triangle|; a NaN M(0,0) poisons it, as there
+        double scale = qb_<0>(m);
+        const double m1 = qb_<1>(m), m2 = qb_<2>(m), m3 = qb_<3>(m);
+        if (m1 > scale) scale = m1;
+        if (m2 > scale) scale = m2;
+        if (m3 > scale) scale = m3;
+        const double a00 = fabs(qb_<0>(A[0][0]));
+        if (a00 != a00) scale = a00;
+        if (scale == 0.0) scale = 1.0;
+        RSC_UNROLL for (int j = 0; j < 3; ++j)
+            RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = A[j][c] / scale;
+        quad_tridiag(A, q, E, diag, sub, hC);
+    }
+    __syncthreads();
+    if (STOP == 2) {
+        if (active && q == 0) {
+            double acc = 0.0;
+            RSC_UNROLL for (int k = 0; k < 12; ++k) acc += diag[k];
+            RSC_UNROLL for (int k = 0; k < 11; ++k) acc += sub[k] + hC[k];
+            out[0] = acc;
+        }
+        return;
+    }
+
+    // ---- C: accumulate Q (own columns), transpose to own rows through LDS ----
+    double Q[3][12];
+    {
+        double Qc[3][12];
+        quad_accumulate(Qc, q, E, hC);
+        RSC_UNROLL for (int j = 0; j < 3; ++j)
+            RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + 4 * j + q] = Qc[j][r];
+    }
+    __syncthreads();
+    RSC_UNROLL for (int j = 0; j < 3; ++j)
+        RSC_UNROLL for (int c = 0; c < 12; ++c) Q[j][c] = T[(4 * j + q) * 12 + c];
+    if (STOP == 3) {
+        if (active) {
+            double acc = 0.0;
+            RSC_UNROLL for (int j = 0; j < 3; ++j) RSC_UNROLL for (int c = 0; c < 12; ++c) acc += Q[j][c];
+            out[q] = acc + diag[0] + sub[0];
+        }
+        return;
+    }
+
+    // ---- D: implicit symmetric QR, rotations applied to the own rows ----
+    {
+        auto qapply = [&](int k, double c, double s, bool apply) {
+            RSC_UNROLL for (int j = 0; j < 3; ++j) {
+                const double xi = Q[j][k], yi = Q[j][k + 1];
+                Q[j][k] = apply ? c * xi - s * yi : xi;
+                Q[j][k + 1] = apply ? s * xi + c * yi : yi;
+            }
+        };
+        int perm[12];
+        tridiag_qr<double, 12>(diag, sub, qapply, perm);
+        // sorted eigenvector columns 0..3 (the four smallest eigenvalues) of the own rows
+        if (active) {
+            RSC_UNROLL for (int j = 0; j < 3; ++j)
+                RSC_UNROLL for (int c = 0; c < 4; ++c) {
+                    double x = Q[j][0];
+                    RSC_UNROLL for (int p = 1; p < 12; ++p) x = (perm[c] == p) ? Q[j][p] : x;
+                    out[kStEv + (4 * j + q) * 4 + c] = x;
+                }
+        }
+    }
+}
+
+// Kernel 1, lane form: one lane per hypothesis (sample, control points, alphas, MtM, 12x12
+// eigenvectors in the per-lane LDS slab), same stage record as the quad form.
+template <int NS>
+__device__ __forceinline__ void pnp_eig_lane_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
+                                                  const int2* __restrict__ wg_table, const uint32_t* __restrict__ rng_T,
+                                                  double* __restrict__ stage, int32_t* __restrict__ samples,
+                                                  double* slab) {
+    const int lane = threadIdx.x;
+    const int2 wt = wg_table[blockIdx.x];
+    const LaunchProb& lp = lps[wt.x];
+    const int h = wt.y + lane;
+    if (h >= lp.H) return;
+    const DevPnP& P = probs[lp.prob];
+    const size_t rec = (size_t)(lp.out0 + h);
+    double* out = stage + rec * kStageDoubles;
+    int idx[NS];
+    {
+        uint32_t w[31];
+        RSC_UNROLL for (int j = 0; j < 31; ++j) w[j] = lp.window[j];
+        uint32_t words[NS];
+        RSC_UNROLL for (int d = 0; d < NS; ++d) words[d] = rng_word(rng_T, w, lp.g0 + h * NS + d);
+        swap_remove_sample<NS>(words, NS, P.n, idx);
+    }
+    RSC_UNROLL for (int i = 0; i < NS; ++i) samples[rec * 8 + i] = idx[i];
+    const LaneMat S{slab + lane, 64};
+    {
+        HypStore<NS> st;
+        RSC_UNROLL for (int i = 0; i < NS; ++i) {
+            const float4 p = P.pts[idx[i]];
+            const float2 uv = P.uv[idx[i]];
+            st.pw_[i][0] = p.x; st.pw_[i][1] = p.y; st.pw_[i][2] = p.z;
+            st.u_[i][0] = uv.x; st.u_[i][1] = uv.y;
+        }
+        st.rows_ = P.rows;
+        st.spw = P.pws;
+        st.sal = P.als;
+        const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
+        double cws[4][3];
+        control_points_and_alphas(st, cws);
+        RSC_UNROLL for (int i = 0; i < NS; ++i)
+            RSC_UNROLL for (int j = 0; j < 4; ++j) out[kStAl + i * 4 + j] = st.al(i, j);
+        RSC_UNROLL for (int i = 0; i < 4; ++i)
+            RSC_UNROLL for (int c = 0; c < 3; ++c) out[kStCws + i * 3 + c] = cws[i][c];
+        build_MtM(st, K, S);
+    }
+    sym_eig12(S);
+    RSC_UNROLL for (int r = 0; r < 12; ++r)
+        RSC_UNROLL for (int c = 0; c < 4; ++c) out[kStEv + r * 4 + c] = S.at(r, c);
+}
+
+// Kernel 2: 192 threads = 3 waves over the same 64 hypotheses; wave w runs find_betas_approx_{w+1}
+// + gauss_newton + compute_R_and_t (PnPsolver.cpp:383-408), wave 0 keeps the smallest error in the
+// reference's order (:393-414) and writes the float pose.
+template <int NS>
+__device__ __forceinline__ void pnp_betas_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
+                                               const int2* __restrict__ wg_table, const double* __restrict__ stage,
+                                               const int32_t* __restrict__ samples, float* __restrict__ poses,
+                                               double* smem) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int2 wt = wg_table[blockIdx.x];
+    const LaunchProb& lp = lps[wt.x];
+    const bool active = wt.y + lane < lp.H;
+    const int h = active ? wt.y + lane : lp.H - 1;
+    const DevPnP& P = probs[lp.prob];
+    const size_t rec = (size_t)(lp.out0 + h);
+    const double* in = stage + rec * kStageDoubles;
+    double* EV = smem;
+    double* LR = EV + 48 * 64;
+    double* ERR = LR + 66 * 64;
+    float* PZ = reinterpret_cast<float*>(ERR + 3 * 64);
+    RSC_UNROLL for (int e = 0; e < 16; ++e) EV[(16 * wave + e) * 64 + lane] = in[kStEv + 16 * wave + e];
+    double cws[4][3];
+    RSC_UNROLL for (int i = 0; i < 4; ++i)
+        RSC_UNROLL for (int c = 0; c < 3; ++c) cws[i][c] = in[kStCws + i * 3 + c];
+    __syncthreads();
+    const SplitView V{EV + lane, LR + lane, 64};
+    if (wave == 0) {
+        compute_L_6x10(V);
+        auto d2 = [&](int a, int b) {
+            double x = cws[a][0] - cws[b][0], y = cws[a][1] - cws[b][1], z = cws[a][2] - cws[b][2];
+            return x * x + y * y + z * z;
+        };
+        V.rho(0) = d2(0, 1); V.rho(1) = d2(0, 2); V.rho(2) = d2(0, 3);
+        V.rho(3) = d2(1, 2); V.rho(4) = d2(1, 3); V.rho(5) = d2(2, 3);
+    }
+    __syncthreads();
+    HypStore<NS> st;
+    RSC_UNROLL for (int i = 0; i < NS; ++i) {
+        const int id = samples[rec * 8 + i];
+        const float4 p = P.pts[id];
+        const float2 uv = P.uv[id];
+        st.pw_[i][0] = p.x; st.pw_[i][1] = p.y; st.pw_[i][2] = p.z;
+        st.u_[i][0] = uv.x; st.u_[i][1] = uv.y;
+        RSC_UNROLL for (int j = 0; j < 4; ++j) st.al_[i][j] = in[kStAl + i * 4 + j];
+    }
+    st.rows_ = P.rows;
+    st.spw = P.pws;
+    st.sal = P.als;
+    const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
+    double betas[4] = {0.0, 0.0, 0.0, 0.0};
+    if (wave == 0) find_betas<1>(V, betas);
+    else if (wave == 1) find_betas<2>(V, betas);
+    else find_betas<3>(V, betas);
+    gauss_newton(V, betas);
+    const double pw0[3] = {cws[0][0], cws[0][1], cws[0][2]};
+    double R[3][3], t[3];
+    ERR[wave * 64 + lane] = compute_R_and_t(st, K, V, betas, pw0, R, t);
+    RSC_UNROLL for (int r = 0; r < 3; ++r)
+        RSC_UNROLL for (int c = 0; c < 3; ++c) PZ[(wave * 12 + 3 * r + c) * 64 + lane] = (float)R[r][c];
+    RSC_UNROLL for (int r = 0; r < 3; ++r) PZ[(wave * 12 + 9 + r) * 64 + lane] = (float)t[r];
+    __syncthreads();
+    if (wave == 0 && active) {
+        int best = 0;
+        double be = ERR[lane];
+        if (ERR[64 + lane] < be) { be = ERR[64 + lane]; best = 1; }
+        if (ERR[128 + lane] < be) { be = ERR[128 + lane]; best = 2; }
+        float* o = poses + rec * 12;
+        RSC_UNROLL for (int k = 0; k < 12; ++k) o[k] = PZ[(best * 12 + k) * 64 + lane];
+    }
+}
+
+}  // namespace rsc

@@ -27,7 +27,7 @@ u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
 # Every symbol declared in include/rsc.h (checked by tests/test_cpu_abi.py).
 EXPORTED = [
     "rsc_version", "rsc_status_string", "rsc_context_create", "rsc_context_destroy", "rsc_context_set_stream",
-    "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_enable_timing",
+    "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_enable_timing", "rsc_context_set_solve_mode",
     "rsc_pnp_create", "rsc_pnp_destroy", "rsc_pnp_set_ransac_parameters", "rsc_pnp_iterate", "rsc_pnp_find",
     "rsc_pnp_iterate_many", "rsc_pnp_reset", "rsc_pnp_get_state", "rsc_pnp_last_samples",
     "rsc_sim3_create", "rsc_sim3_destroy", "rsc_sim3_set_ransac_parameters", "rsc_sim3_iterate", "rsc_sim3_find",
@@ -77,6 +77,7 @@ def load_library(path: str = LIB_PATH):
     L.rsc_context_synchronize.argtypes = [vp]
     L.rsc_context_last_timing.argtypes = [vp, C.POINTER(C.c_double)]
     L.rsc_context_enable_timing.argtypes = [vp, C.c_int]
+    L.rsc_context_set_solve_mode.argtypes = [vp, C.c_int]
     L.rsc_pnp_create.argtypes = [vp, C.POINTER(PnPProblem), C.c_uint32, C.POINTER(vp)]
     L.rsc_pnp_destroy.argtypes = [vp]
     L.rsc_pnp_set_ransac_parameters.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
@@ -139,6 +140,12 @@ class Context:
 
     def enable_timing(self, on: bool = True):
         _check(load_library().rsc_context_enable_timing(self.h, int(on)), "enable_timing")
+
+    SOLVE_MODES = {"auto": 0, "mono": 1, "quad": 2, "split": 3}
+
+    def set_solve_mode(self, mode: str):
+        """PnP hypothesis kernels: auto | mono | quad | split (bit-identical results)."""
+        _check(load_library().rsc_context_set_solve_mode(self.h, self.SOLVE_MODES[mode]), "set_solve_mode")
 
     def last_timing(self):
         out = (C.c_double * 5)()
@@ -337,6 +344,23 @@ class SolverBatch:
         if self.kind == "pnp":
             return pnp_iterate_many(self.solvers, n_iterations, with_masks)
         return sim3_iterate_many(self.solvers, n_iterations, with_masks)
+
+    def iterate_raw(self, n_iterations):
+        """iterate() of every solver without inlier vectors; returns the C result records as a
+        numpy structured array (fields ok, no_more, n_inliers, iterations, T | R, t) without
+        per-solver Python objects (the hot loop of bench.py)."""
+        n = len(self.solvers)
+        if not hasattr(self, "_raw"):
+            rec = PnPResult if self.kind == "pnp" else Sim3Result
+            self._raw = (rec * n)()
+            self._its = np.zeros(n, np.int32)
+            self._nomask = (C.c_void_p * n)()
+            self._view = np.ctypeslib.as_array(self._raw)
+        self._its[:] = n_iterations
+        L = load_library()
+        f = L.rsc_pnp_iterate_many if self.kind == "pnp" else L.rsc_sim3_iterate_many
+        _check(f(self._h, n, self._its, self._raw, self._nomask), "iterate_many")
+        return self._view
 
     def phase_stamps(self, H):
         """Diagnostic: per-hypothesis s_memtime stamps at the EPnP phase boundaries (PnP only)."""

@@ -129,3 +129,36 @@ def test_refine_failure_respeculation(case):
     for rnd in range(20):
         assert_pnp_equal(g.iterate(5), o.iterate(5), f"round {rnd}")
         assert g.state()["max_rows"] == o.info()["max_rows"]
+
+
+@pytest.mark.parametrize("mode", ["mono", "quad", "split"])
+def test_solve_modes_bitexact(mode):
+    """Every hypothesis-kernel family against the oracle (samples, counts, poses), min_set 4..6."""
+    from rsc import engine
+    rng = np.random.default_rng(7)
+    c = engine.Context(0)
+    c.set_solve_mode(mode)
+    for ms in (4, 5, 6):
+        sc = synth.make_pnp_scene(rng, 700, 0.5)
+        params = (0.99, 10, 300, ms, 0.5, 5.991)
+        g = engine.PnPSolver(c, sc, 100 + ms)
+        g.set_ransac_parameters(*params)
+        o = ol.OraclePnP(sc, 100 + ms)
+        o.set_ransac_parameters(*params)
+        for k in range(3):
+            assert_pnp_equal(g.iterate(37), o.iterate(37), f"{mode} ms={ms} call {k}")
+
+
+def test_batch_iterate_raw_matches_dicts():
+    from rsc import engine
+    rng = np.random.default_rng(8)
+    scenes = [synth.make_pnp_scene(rng, 600, 0.4) for _ in range(5)]
+    a = engine.SolverBatch([make(sc, 60 + i)[0] for i, sc in enumerate(scenes)])
+    b = engine.SolverBatch([make(sc, 60 + i)[0] for i, sc in enumerate(scenes)])
+    raw = a.iterate_raw(90)
+    outs = b.iterate(90)
+    for i, o in enumerate(outs):
+        assert raw["ok"][i] == o["ok"] and raw["n_inliers"][i] == o["n_inliers"]
+        assert raw["iterations"][i] == o["iterations"] and raw["no_more"][i] == o["no_more"]
+        if o["ok"]:
+            assert bits(raw["T"][i].reshape(4, 4)).tolist() == bits(o["T"]).tolist()
