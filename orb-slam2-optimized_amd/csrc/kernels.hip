@@ -374,6 +374,22 @@ __global__ __launch_bounds__(256) void sim3_scan_kernel(const DevSim3* __restric
     }
 }
 
+// Gather `take` floats of records idx[q] (record stride `stride` floats) into dst[q][take].
+__global__ void gather_records_kernel(const float* __restrict__ src, int stride, int take,
+                                      const int32_t* __restrict__ idx, int n, float* __restrict__ dst) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * take) return;
+    const int q = t / take, e = t - q * take;
+    dst[t] = src[(size_t)idx[q] * stride + e];
+}
+
+hipError_t launch_gather_records(const float* src, int stride, int take, const int32_t* idx, int n, float* dst,
+                                 hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    gather_records_kernel<<<(n * take + 255) / 256, 256, 0, st>>>(src, stride, take, idx, n, dst);
+    return hipGetLastError();
+}
+
 // rand() outputs straight from the jump table (parity hook for the RNG contract).
 __global__ void rng_stream_kernel(const uint32_t* __restrict__ T, Window31 w, int g0, int n, int32_t* __restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;

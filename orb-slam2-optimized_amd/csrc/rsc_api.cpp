@@ -99,6 +99,7 @@ struct rsc_context {
     DevBuf<uint64_t> d_masks;
     DevBuf<int32_t> d_samples;
     DevBuf<double> d_stage;  // quad path: per-hypothesis stage records between the two solve kernels
+    DevBuf<float> d_gather;  // gathered pose records (+ their indices)
     DevBuf<char> d_desc;
     PinBuf<char> h_desc;
     PinBuf<int32_t> h_counts;
@@ -484,13 +485,18 @@ struct HipSim3Backend : Sim3Backend {
         return 0;
     }
 
-    int fetch_pose(int j, int k, float* pose12) override {
-        rsc_sim3* p = solvers[j];
-        if (int e = C->h_small.ensure(12)) return e;
-        RSC_HIP(hipMemcpyAsync(C->h_small.p, C->d_poses.p + (size_t)(p->spec_out0 + k) * 24, 48, hipMemcpyDeviceToHost,
-                               C->stream));
+    int fetch_poses(const int* j, const int* k, int n, float (*pose12)[12]) override {
+        // record indices -> one gather kernel -> one D2H copy
+        if (int e = C->h_small.ensure((size_t)n * 13)) return e;
+        int32_t* hidx = reinterpret_cast<int32_t*>(C->h_small.p + (size_t)n * 12);
+        for (int q = 0; q < n; ++q) hidx[q] = solvers[j[q]]->spec_out0 + k[q];
+        if (int e = C->d_gather.ensure((size_t)n * 13)) return e;
+        int32_t* didx = reinterpret_cast<int32_t*>(C->d_gather.p + (size_t)n * 12);
+        RSC_HIP(hipMemcpyAsync(didx, hidx, (size_t)n * 4, hipMemcpyHostToDevice, C->stream));
+        RSC_HIP(launch_gather_records(C->d_poses.p, 24, 12, didx, n, C->d_gather.p, C->stream));
+        RSC_HIP(hipMemcpyAsync(C->h_small.p, C->d_gather.p, (size_t)n * 48, hipMemcpyDeviceToHost, C->stream));
         RSC_HIP(hipStreamSynchronize(C->stream));
-        std::memcpy(pose12, C->h_small.p, 48);
+        std::memcpy(pose12, C->h_small.p, (size_t)n * 48);
         return 0;
     }
 

@@ -360,8 +360,8 @@ struct Sim3Result {
 
 struct Sim3Backend {
     virtual int speculate(Sim3State* const* states, int count, const int* H, std::vector<std::vector<int32_t>>& counts) = 0;
-    // pose (R12 9 + t12 3) of hypothesis k of solver i of the last speculation
-    virtual int fetch_pose(int i, int k, float* pose12) = 0;
+    // poses (R12 9 + t12 3) of hypotheses k[q] of solvers i[q] of the last speculation, q < n
+    virtual int fetch_poses(const int* i, const int* k, int n, float (*pose12)[12]) = 0;
     virtual int fetch_mask(const int* which_i, const int* which_k, Sim3State* const* states, int count,
                            uint8_t* const* out) = 0;
     virtual ~Sim3Backend() {}
@@ -388,7 +388,7 @@ inline int sim3_iterate_many(Sim3Backend& be, Sim3State* const* S, int count, co
         int st = be.speculate(spec.data(), (int)spec.size(), H.data(), counts);
         if (st) return st;
     }
-    std::vector<int> mi, mk;
+    std::vector<int> mi, mk, pj, pk;
     std::vector<Sim3State*> ms;
     std::vector<uint8_t*> mo;
     for (size_t j = 0; j < spec.size(); ++j) {
@@ -411,17 +411,24 @@ inline int sim3_iterate_many(Sim3Backend& be, Sim3State* const* S, int count, co
             }
         }
         if (best_k >= 0) {
-            float p[12];
-            int st = be.fetch_pose((int)j, best_k, p);
-            if (st) return st;
-            std::memcpy(s.mBestRotation, p, 9 * sizeof(float));
-            std::memcpy(s.mBestTranslation, p + 9, 3 * sizeof(float));
+            pj.push_back((int)j);
+            pk.push_back(best_k);
         }
         if (res[i].ok && inliers && inliers[i]) {
             mi.push_back((int)j);
             mk.push_back(res[i].mask_k);
             ms.push_back(&s);
             mo.push_back(inliers[i]);
+        }
+    }
+    if (!pj.empty()) {  // mBestRotation / mBestTranslation of every solver that improved, one fetch
+        std::vector<float> p(pj.size() * 12);
+        int st = be.fetch_poses(pj.data(), pk.data(), (int)pj.size(), reinterpret_cast<float(*)[12]>(p.data()));
+        if (st) return st;
+        for (size_t q = 0; q < pj.size(); ++q) {
+            Sim3State& s = *spec[pj[q]];
+            std::memcpy(s.mBestRotation, &p[q * 12], 9 * sizeof(float));
+            std::memcpy(s.mBestTranslation, &p[q * 12 + 9], 3 * sizeof(float));
         }
     }
     for (int i = 0; i < count; ++i) {

@@ -50,6 +50,8 @@ struct RefineJob {
 struct Window31 {
     uint32_t w[31];
 };
+hipError_t launch_gather_records(const float* src, int stride, int take, const int32_t* idx, int n, float* dst,
+                                 hipStream_t st);
 hipError_t launch_rng_stream(const uint32_t* T, const uint32_t* window, int g0, int n, int32_t* out, hipStream_t st);
 
 hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
