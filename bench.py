@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-sim3", action="store_true")
+    p.add_argument("--no-mlpnp", action="store_true")
     return p.parse_args()
 
 
@@ -143,6 +144,32 @@ def run_sim3(engine, ctx, rng, args):
                 pairs=32, correspondences=1000)
 
 
+def run_mlpnp(engine, ctx, rng, args):
+    """Config 4 on one GPU: 32 candidates x 4096 correspondences, MLPnP SetRansacParameters
+    (0.99,10,300,6,0.5,5.991) (commented call Tracking.cpp:1227-1228), iterate(300), exhaustive."""
+    from rsc import synth
+    scenes = [synth.make_pnp_scene(rng, 4096, 0.4) for _ in range(32)]
+    batch = engine.SolverBatch([engine.MLPnPSolver(ctx, sc, 1) for sc in scenes])
+
+    def step(s):
+        batch.reset(1 + np.arange(32) + 32 * s)
+        batch.set_ransac_parameters(0.99, 10, 300, 6, 0.5, 5.991)
+        return int(batch.iterate_raw(args.iters)["iterations"].sum())
+
+    for s in range(args.warmup):
+        step(s)
+    ctx.synchronize()
+    steps = max(1, args.steps // 4)
+    t0 = time.perf_counter()
+    h = 0
+    for s in range(steps):
+        h += step(args.warmup + s)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    return dict(hyp_per_s=h / dt, ms_per_step=1e3 * dt / steps, hypotheses_per_step=h // steps, candidates=32,
+                correspondences=4096, steps=steps)
+
+
 def cpu_baseline(scenes, args):
     """Oracle restatement (test infrastructure) of the same workload on ONE host core."""
     import oracle_lib as ol
@@ -192,9 +219,11 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         dt = float(mx[0])
         hyps_total = int(t[1])
-    sim3 = None
+    sim3 = mlpnp = None
     if rank == 0 and not args.no_sim3:
         sim3 = run_sim3(engine, ctx, np.random.default_rng(77), args)
+    if rank == 0 and not args.no_mlpnp:
+        mlpnp = run_mlpnp(engine, ctx, np.random.default_rng(78), args)
     if rank != 0:
         if dist is not None:
             dist.barrier()
@@ -233,6 +262,8 @@ def main():
     }
     if sim3 is not None:
         out["sim3"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in sim3.items()}
+    if mlpnp is not None:
+        out["mlpnp"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in mlpnp.items()}
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(scenes, args)
         out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 1)

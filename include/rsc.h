@@ -32,6 +32,7 @@ extern "C" {
 typedef struct rsc_context rsc_context;
 typedef struct rsc_pnp rsc_pnp;
 typedef struct rsc_sim3 rsc_sim3;
+typedef struct rsc_mlpnp rsc_mlpnp;
 
 /* ---- library / context ------------------------------------------------------------------ */
 int rsc_version(void);
@@ -139,6 +140,31 @@ int rsc_sim3_get_state(const rsc_sim3* s, int32_t out[6]);
  * X1c/X2c [N][3], P1im1/P2im2 [N][2], max_err1/2 [N] (size_t thresholds), indices1 [N]. */
 int rsc_sim3_prepared(const rsc_sim3* s, float* X1c, float* X2c, float* P1im1, float* P2im2, uint64_t* max_err1,
                       uint64_t* max_err2, int32_t* indices1);
+
+/* ---- MLPnPsolver (include/MLPnPsolver.hpp:10-199, src/MLPnPsolver.cpp) ----------------------------
+ * Dormant in the reference (not compiled, call sites commented out, Tracking.cpp:1222,1227-1228);
+ * exported for BASELINE config 4.  Same problem struct and result record as PnP.  Parity of this
+ * solver against the reference is unpinned. */
+/* MLPnPsolver::MLPnPsolver (MLPnPsolver.cpp:5-53, includes its SetRansacParameters() call). */
+int rsc_mlpnp_create(rsc_context* ctx, const rsc_pnp_problem* problem, uint32_t seed, rsc_mlpnp** out);
+void rsc_mlpnp_destroy(rsc_mlpnp* s);
+/* MLPnPsolver::SetRansacParameters (MLPnPsolver.cpp:185-220; defaults 0.99, 8, 300, 6, 0.4, 5.991).
+ * min_set must be in [6, 8] (computePose asserts n > 5, :324) -> RSC_ERR_UNSUPPORTED otherwise. */
+int rsc_mlpnp_set_ransac_parameters(rsc_mlpnp* s, double probability, int min_inliers, int max_iterations,
+                                    int min_set, float epsilon, float th2);
+int rsc_mlpnp_set_ransac_parameters_many(rsc_mlpnp* const* solvers, int count, double probability, int min_inliers,
+                                         int max_iterations, int min_set, float epsilon, float th2);
+/* MLPnPsolver::iterate (MLPnPsolver.cpp:56-183): T is identity unless ok (Tout.setIdentity(), :57). */
+int rsc_mlpnp_iterate(rsc_mlpnp* s, int n_iterations, rsc_pnp_result* out, uint8_t* inliers);
+int rsc_mlpnp_iterate_many(rsc_mlpnp* const* solvers, int count, const int32_t* n_iterations, rsc_pnp_result* out,
+                           uint8_t* const* inliers);
+int rsc_mlpnp_reset(rsc_mlpnp* s, uint32_t seed);
+int rsc_mlpnp_reset_many(rsc_mlpnp* const* solvers, int count, const uint32_t* seeds);
+/* out: [0] mnIterations [1] mRansacMaxIts [2] mRansacMinInliers [3] mnBestInliers [4] N [5] mRansacMinSet */
+int rsc_mlpnp_get_state(const rsc_mlpnp* s, int32_t out[6]);
+/* Parity hooks: double poses (R 9 + t 3) and sample indices (8 per hypothesis) of the last launch. */
+int rsc_mlpnp_last_poses(rsc_mlpnp* s, double* out, int cap);
+int rsc_mlpnp_last_samples(rsc_mlpnp* s, int32_t* out, int cap);
 
 /* ---- glibc rand() helpers (Thirdparty/DBoW2/DUtils/Random.cpp:33-50) -------------------------- */
 /* First n rand() outputs after srand(seed), produced with the device jump table (parity hook). */

@@ -9,6 +9,8 @@
 #include "glibc_rand.h"
 #include "pnp_oracle.h"
 #include "sim3_oracle.h"
+#include "mlpnp_oracle.h"
+#include "../orb-slam2-optimized_amd/csrc/rsc_math.h"
 #include "ora_linalg.h"
 
 using namespace rsc_oracle;
@@ -328,4 +330,93 @@ void ora_sim3_run_prepared_batch(int C, const int32_t* n, const int64_t* off, co
     }
 }
 
+
+// ---- MLPnPsolver (mlpnp_oracle.h) ----------------------------------------------------------------
+void* ora_mlpnp_create(int n, int n_points, const float* p2d, const float* p3dw, const float* sigma2,
+                       const int32_t* kp_index, float fx, float fy, float cx, float cy, uint32_t seed) {
+    return new MLPnPOracle(n, n_points, p2d, p3dw, sigma2, kp_index, fx, fy, cx, cy, seed);
+}
+void ora_mlpnp_destroy(void* h) { delete static_cast<MLPnPOracle*>(h); }
+void ora_mlpnp_set_params(void* h, double prob, int min_inliers, int max_its, int min_set, float eps, float th2) {
+    static_cast<MLPnPOracle*>(h)->SetRansacParameters(prob, min_inliers, max_its, min_set, eps, th2);
+}
+int ora_mlpnp_iterate(void* h, int n_its, int* no_more, uint8_t* inliers, int* mask_len, int* n_inliers, float* T) {
+    std::vector<uint8_t> v;
+    bool nm = false;
+    int ni = 0;
+    bool ok = static_cast<MLPnPOracle*>(h)->iterate(n_its, nm, v, ni, T);
+    *no_more = nm;
+    *n_inliers = ni;
+    *mask_len = (int)v.size();
+    if (!v.empty()) std::memcpy(inliers, v.data(), v.size());
+    return ok;
+}
+void ora_mlpnp_info(void* h, int* out) {
+    auto* s = static_cast<MLPnPOracle*>(h);
+    out[0] = s->iterations();
+    out[1] = s->max_iterations();
+    out[2] = s->min_inliers();
+    out[3] = s->best_inliers();
+}
+void ora_mlpnp_compute_pose(void* h, const int* idx, int n, double* R, double* t) {
+    static_cast<MLPnPOracle*>(h)->compute_pose_public(idx, n, R, t);
+}
+// per-hypothesis trace: ints [8 sample + count], doubles [R 9 + t 3]
+void ora_mlpnp_trace_enable(void* h) {
+    auto* s = static_cast<MLPnPOracle*>(h);
+    if (!s->trace) s->trace = new std::vector<MLPnPOracle::Trace>();
+}
+int ora_mlpnp_trace_get(void* h, int cap, int32_t* ints, double* dbls) {
+    auto* s = static_cast<MLPnPOracle*>(h);
+    if (!s->trace) return 0;
+    const int n = std::min(cap, (int)s->trace->size());
+    for (int i = 0; i < n; ++i) {
+        const auto& t = (*s->trace)[i];
+        for (int k = 0; k < 8; ++k) ints[9 * i + k] = t.sample[k];
+        ints[9 * i + 8] = t.n_inliers;
+        for (int k = 0; k < 9; ++k) dbls[12 * i + k] = t.R[k];
+        for (int k = 0; k < 3; ++k) dbls[12 * i + 9 + k] = t.t[k];
+    }
+    return n;
+}
+void ora_mlpnp_run_batch(int C, const int32_t* n, const int64_t* off, const float* p2d, const float* p3dw,
+                         const float* sigma2, float fx, float fy, float cx, float cy, const uint32_t* seeds,
+                         double prob, int min_inliers, int max_its, int min_set, float eps, float th2, int n_its,
+                         int nthreads, int32_t* out_i4, float* out_T) {
+    std::atomic<int> next(0);
+    auto worker = [&]() {
+        for (;;) {
+            int c = next.fetch_add(1);
+            if (c >= C) break;
+            const int64_t o = off[c];
+            std::vector<int32_t> kp(n[c]);
+            for (int i = 0; i < n[c]; ++i) kp[i] = i;
+            MLPnPOracle s(n[c], n[c], p2d + 2 * o, p3dw + 3 * o, sigma2 + o, kp.data(), fx, fy, cx, cy, seeds[c]);
+            s.SetRansacParameters(prob, min_inliers, max_its, min_set, eps, th2);
+            std::vector<uint8_t> v;
+            bool nm = false;
+            int ni = 0;
+            float T[16];
+            bool ok = s.iterate(n_its, nm, v, ni, T);
+            out_i4[4 * c + 0] = ok;
+            out_i4[4 * c + 1] = nm;
+            out_i4[4 * c + 2] = ni;
+            out_i4[4 * c + 3] = s.iterations();
+            std::memcpy(out_T + 16 * c, T, sizeof(T));
+        }
+    };
+    if (nthreads <= 1) {
+        worker();
+    } else {
+        std::vector<std::thread> th;
+        for (int i = 0; i < nthreads; ++i) th.emplace_back(worker);
+        for (auto& t : th) t.join();
+    }
+}
+
+// deterministic libm (csrc/rsc_math.h) for the accuracy tests
+double ora_dm_sin(double x) { return rsc::dm::sin(x); }
+double ora_dm_cos(double x) { return rsc::dm::cos(x); }
+double ora_dm_acos(double x) { return rsc::dm::acos(x); }
+double ora_dm_cbrt(double x) { return rsc::dm::cbrt(x); }
 }  // extern "C"

@@ -1,0 +1,758 @@
+// TEST INFRASTRUCTURE — parity oracle, never linked into the product library.
+// Restatement of src/MLPnPsolver.cpp (reference) — see mlpnp_oracle.h.  Line numbers cite the reference.
+#include "mlpnp_oracle.h"
+#include "ora_linalg.h"
+#include "../orb-slam2-optimized_amd/csrc/rsc_math.h"
+#include <cassert>
+#include <cmath>
+#include <cstring>
+#include <algorithm>
+#include <limits>
+
+namespace rsc_oracle {
+
+namespace {
+
+const double kEps = std::numeric_limits<double>::epsilon();
+
+double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+double norm3(const double* a) { return std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); }
+void cross3(const double* a, const double* b, double* o) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+// Matrix3d::determinant (bruteforce cofactors along the first column)
+double det3m(const double m[3][3]) {
+    return m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) - m[1][0] * (m[0][1] * m[2][2] - m[0][2] * m[2][1]) +
+           m[2][0] * (m[0][1] * m[1][2] - m[0][2] * m[1][1]);
+}
+
+// block.applyHouseholderOnTheLeft(essential, tau) for a row-major block of `rows` x `cols` at
+// M + r0*ld + c0 (Householder.h): tmp = essential^T * bottom; tmp += row0; row0 -= tau*tmp;
+// bottom -= (tau*essential) * tmp.
+void apply_householder_left(double* M, int ld, int r0, int c0, int rows, int cols, const double* ess, double tau) {
+    if (rows == 1) {
+        for (int c = 0; c < cols; ++c) M[r0 * ld + c0 + c] *= (1.0 - tau);
+        return;
+    }
+    if (tau == 0.0) return;
+    std::vector<double> tmp(cols);
+    for (int c = 0; c < cols; ++c) {
+        double acc = ess[0] * M[(r0 + 1) * ld + c0 + c];
+        for (int r = 1; r < rows - 1; ++r) acc = acc + ess[r] * M[(r0 + 1 + r) * ld + c0 + c];
+        tmp[c] = acc + M[r0 * ld + c0 + c];
+    }
+    for (int c = 0; c < cols; ++c) M[r0 * ld + c0 + c] = M[r0 * ld + c0 + c] - tau * tmp[c];
+    for (int r = 0; r < rows - 1; ++r) {
+        const double te = tau * ess[r];
+        for (int c = 0; c < cols; ++c) M[(r0 + 1 + r) * ld + c0 + c] = M[(r0 + 1 + r) * ld + c0 + c] - te * tmp[c];
+    }
+}
+
+// Nullspace of a bearing vector (MLPnPsolver.cpp:336-339): JacobiSVD<MatrixXd,
+// HouseholderQRPreconditioner>(f^T, ComputeFullV).matrixV().block(0,1,3,2).  For the 1x3 input the
+// preconditioner QR-decomposes f/scale (one Householder reflector) and V = householderQ(); the 1x1
+// Jacobi step does nothing to V.
+void bearing_nullspace(const double f[3], double Ns[3][2]) {
+    double scale = std::fabs(f[0]);
+    for (int k = 1; k < 3; ++k) if (std::fabs(f[k]) > scale) scale = std::fabs(f[k]);
+    if (scale == 0.0) scale = 1.0;
+    double v[3] = {f[0] / scale, f[1] / scale, f[2] / scale};
+    double tau, beta;
+    make_householder(v, 1, 3, tau, beta);
+    double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    apply_householder_left(&V[0][0], 3, 0, 0, 3, 3, &v[1], tau);
+    for (int r = 0; r < 3; ++r) { Ns[r][0] = V[r][1]; Ns[r][1] = V[r][2]; }
+}
+
+// FullPivHouseholderQR<Matrix3d>(A).rank() (FullPivHouseholderQR.h computeInPlace + rank()).
+int fullpiv_rank3(const double A[3][3]) {
+    double m[3][3];
+    std::memcpy(m, A, sizeof(m));
+    const int size = 3;
+    const double precision = kEps * size;
+    double biggest = 0.0, maxpivot = 0.0;
+    int nonzero = size;
+    for (int k = 0; k < size; ++k) {
+        // bottomRightCorner(3-k,3-k).cwiseAbs().maxCoeff(&row,&col): column-major visit, strict '>'
+        int br = k, bc = k;
+        double bv = std::fabs(m[k][k]);
+        for (int c = k; c < size; ++c)
+            for (int r = k; r < size; ++r) {
+                if (r == k && c == k) continue;
+                if (std::fabs(m[r][c]) > bv) { bv = std::fabs(m[r][c]); br = r; bc = c; }
+            }
+        if (k == 0) biggest = bv;
+        if (bv <= biggest * precision) {  // isMuchSmallerThan
+            nonzero = k;
+            break;
+        }
+        if (k != br) for (int c = k; c < size; ++c) std::swap(m[k][c], m[br][c]);
+        if (k != bc) for (int r = 0; r < size; ++r) std::swap(m[r][k], m[r][bc]);
+        double col[3], tau, beta;
+        for (int r = k; r < size; ++r) col[r - k] = m[r][k];
+        make_householder(col, 1, size - k, tau, beta);
+        for (int r = k + 1; r < size; ++r) m[r][k] = col[r - k];
+        m[k][k] = beta;
+        if (std::fabs(beta) > maxpivot) maxpivot = std::fabs(beta);
+        if (size - k - 1 > 0) apply_householder_left(&m[0][0], 3, k, k + 1, size - k, size - k - 1, &col[1], tau);
+    }
+    const double thr = std::fabs(maxpivot) * precision;
+    int rank = 0;
+    for (int i = 0; i < nonzero; ++i) rank += (std::fabs(m[i][i]) > thr) ? 1 : 0;
+    return rank;
+}
+
+// JacobiSVD of a square n x n matrix (no preconditioner), ComputeFull{U,V}; singular values sorted
+// descending with the matching U/V columns (JacobiSVD.h compute()).  Row-major, A[r*n+c].
+void jacobi_svd_square(int n, const double* Ain, bool wantU, double* U, double* sv, double* V) {
+    const double precision = 2.0 * kEps;
+    const double considerAsZero = std::numeric_limits<double>::min();
+    double scale = std::fabs(Ain[0]);
+    for (int c = 0; c < n; ++c)
+        for (int r = 0; r < n; ++r) {
+            if (r == 0 && c == 0) continue;
+            if (std::fabs(Ain[r * n + c]) > scale) scale = std::fabs(Ain[r * n + c]);
+        }
+    if (scale == 0.0) scale = 1.0;
+    std::vector<double> W(n * n);
+    for (int i = 0; i < n * n; ++i) W[i] = Ain[i] / scale;
+    for (int r = 0; r < n; ++r)
+        for (int c = 0; c < n; ++c) {
+            V[r * n + c] = (r == c) ? 1.0 : 0.0;
+            if (wantU) U[r * n + c] = (r == c) ? 1.0 : 0.0;
+        }
+    double maxDiag = std::fabs(W[0]);
+    for (int i = 1; i < n; ++i) if (std::fabs(W[i * n + i]) > maxDiag) maxDiag = std::fabs(W[i * n + i]);
+    bool finished = false;
+    while (!finished) {
+        finished = true;
+        for (int p = 1; p < n; ++p) {
+            for (int q = 0; q < p; ++q) {
+                const double pt = precision * maxDiag;
+                const double threshold = (considerAsZero < pt) ? pt : considerAsZero;
+                if (!(std::fabs(W[p * n + q]) > threshold || std::fabs(W[q * n + p]) > threshold)) continue;
+                finished = false;
+                double m00 = W[p * n + p], m01 = W[p * n + q], m10 = W[q * n + p], m11 = W[q * n + q];
+                double c1, s1;
+                const double t = m00 + m11;
+                const double d = m10 - m01;
+                if (std::fabs(d) < considerAsZero) {
+                    s1 = 0.0; c1 = 1.0;
+                } else {
+                    const double u = t / d;
+                    const double tmp = std::sqrt(1.0 + u * u);
+                    s1 = 1.0 / tmp;
+                    c1 = u / tmp;
+                }
+                if (!(c1 == 1.0 && s1 == 0.0)) {
+                    const double x0 = m00, y0 = m10, x1 = m01, y1 = m11;
+                    m00 = c1 * x0 + s1 * y0; m10 = -s1 * x0 + c1 * y0;
+                    m01 = c1 * x1 + s1 * y1; m11 = -s1 * x1 + c1 * y1;
+                }
+                double cr, sr;
+                {
+                    const double deno = 2.0 * std::fabs(m01);
+                    if (deno < considerAsZero) {
+                        cr = 1.0; sr = 0.0;
+                    } else {
+                        const double tau = (m00 - m11) / deno;
+                        const double w = std::sqrt(tau * tau + 1.0);
+                        const double tt = (tau > 0.0) ? 1.0 / (tau + w) : 1.0 / (tau - w);
+                        const double sign_t = tt > 0.0 ? 1.0 : -1.0;
+                        const double nn = 1.0 / std::sqrt(tt * tt + 1.0);
+                        sr = -sign_t * (m01 / std::fabs(m01)) * std::fabs(tt) * nn;
+                        cr = nn;
+                    }
+                }
+                const double crt = cr, srt = -sr;
+                const double cl = c1 * crt - s1 * srt;
+                const double sl = c1 * srt + s1 * crt;
+                if (!(cl == 1.0 && sl == 0.0)) {
+                    for (int c = 0; c < n; ++c) {
+                        const double xi = W[p * n + c], yi = W[q * n + c];
+                        W[p * n + c] = cl * xi + sl * yi;
+                        W[q * n + c] = -sl * xi + cl * yi;
+                    }
+                    if (wantU)
+                        for (int r = 0; r < n; ++r) {
+                            const double xi = U[r * n + p], yi = U[r * n + q];
+                            U[r * n + p] = cl * xi + sl * yi;
+                            U[r * n + q] = -sl * xi + cl * yi;
+                        }
+                }
+                if (!(cr == 1.0 && sr == 0.0)) {
+                    for (int r = 0; r < n; ++r) {
+                        const double xi = W[r * n + p], yi = W[r * n + q];
+                        W[r * n + p] = cr * xi - sr * yi;
+                        W[r * n + q] = sr * xi + cr * yi;
+                    }
+                    for (int r = 0; r < n; ++r) {
+                        const double xi = V[r * n + p], yi = V[r * n + q];
+                        V[r * n + p] = cr * xi - sr * yi;
+                        V[r * n + q] = sr * xi + cr * yi;
+                    }
+                }
+                const double a = std::fabs(W[p * n + p]), b = std::fabs(W[q * n + q]);
+                const double mm = (a < b) ? b : a;
+                maxDiag = (maxDiag < mm) ? mm : maxDiag;
+            }
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        const double a = W[i * n + i];
+        sv[i] = std::fabs(a);
+        if (wantU && a < 0.0)
+            for (int r = 0; r < n; ++r) U[r * n + i] = -U[r * n + i];
+    }
+    for (int i = 0; i < n; ++i) sv[i] = sv[i] * scale;
+    for (int i = 0; i < n; ++i) {
+        int pos = 0;
+        double mv = sv[i];
+        for (int j = 1; j < n - i; ++j)
+            if (sv[i + j] > mv) { mv = sv[i + j]; pos = j; }
+        if (mv == 0.0) break;
+        if (pos) {
+            pos += i;
+            std::swap(sv[i], sv[pos]);
+            if (wantU) for (int r = 0; r < n; ++r) std::swap(U[r * n + pos], U[r * n + i]);
+            for (int r = 0; r < n; ++r) std::swap(V[r * n + pos], V[r * n + i]);
+        }
+    }
+}
+
+// Matrix4d::inverse, generic cofactor form: result(j,i) = (-1)^(i+j) * cof(i,j), cof(i,j) =
+// sum of the three det3 helpers of the rotated minor; det = sum_k m(k,0)*result(0,k); result /= det.
+void inverse4(const double m[4][4], double out[4][4]) {
+    auto h = [&](int i1, int i2, int i3, int j1, int j2, int j3) {
+        return m[i1][j1] * (m[i2][j2] * m[i3][j3] - m[i2][j3] * m[i3][j2]);
+    };
+    auto cof = [&](int i, int j) {
+        const int i1 = (i + 1) % 4, i2 = (i + 2) % 4, i3 = (i + 3) % 4;
+        const int j1 = (j + 1) % 4, j2 = (j + 2) % 4, j3 = (j + 3) % 4;
+        return h(i1, i2, i3, j1, j2, j3) + h(i2, i3, i1, j1, j2, j3) + h(i3, i1, i2, j1, j2, j3);
+    };
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            const double c = cof(i, j);
+            out[j][i] = ((i + j) & 1) ? -c : c;
+        }
+    const double det = ((m[0][0] * out[0][0] + m[1][0] * out[0][1]) + m[2][0] * out[0][2]) + m[3][0] * out[0][3];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) out[r][c] = out[r][c] / det;
+}
+
+// LDLT<MatrixXd>(A).solve(b), 6x6 (LDLT.h ldlt_inplace<Lower>::unblocked + _solve_impl).
+void ldlt_solve6(const double Ain[6][6], const double b[6], double x[6]) {
+    const int n = 6;
+    double m[6][6];
+    std::memcpy(m, Ain, sizeof(m));
+    int transp[6];
+    for (int k = 0; k < n; ++k) {
+        int big = k;
+        double bv = std::fabs(m[k][k]);
+        for (int i = k + 1; i < n; ++i)
+            if (std::fabs(m[i][i]) > bv) { bv = std::fabs(m[i][i]); big = i; }
+        transp[k] = big;
+        if (k != big) {
+            const int s = n - big - 1;
+            for (int j = 0; j < k; ++j) std::swap(m[k][j], m[big][j]);
+            for (int j = 0; j < s; ++j) std::swap(m[big + 1 + j][k], m[big + 1 + j][big]);
+            std::swap(m[k][k], m[big][big]);
+            for (int i = k + 1; i < big; ++i) {
+                const double tmp = m[i][k];
+                m[i][k] = m[big][i];
+                m[big][i] = tmp;
+            }
+        }
+        const int rs = n - k - 1;
+        if (k > 0) {
+            double temp[6];
+            for (int j = 0; j < k; ++j) temp[j] = m[j][j] * m[k][j];
+            double acc = m[k][0] * temp[0];
+            for (int j = 1; j < k; ++j) acc = acc + m[k][j] * temp[j];
+            m[k][k] -= acc;
+            for (int r = 0; r < rs; ++r) {
+                double a = m[k + 1 + r][0] * temp[0];
+                for (int j = 1; j < k; ++j) a = a + m[k + 1 + r][j] * temp[j];
+                m[k + 1 + r][k] -= a;
+            }
+        }
+        const double akk = m[k][k];
+        const bool valid = std::fabs(akk) > 0.0;
+        if (k == 0 && !valid) {  // whole diagonal zero
+            for (int j = 0; j < n; ++j) transp[j] = j;
+            break;
+        }
+        if (rs > 0 && valid)
+            for (int r = 0; r < rs; ++r) m[k + 1 + r][k] /= akk;
+    }
+    double y[6];
+    std::memcpy(y, b, sizeof(y));
+    for (int k = 0; k < n; ++k) std::swap(y[k], y[transp[k]]);  // P b
+    for (int i = 0; i < n; ++i) {                                // L (unit lower) forward
+        double acc = 0.0;
+        bool first = true;
+        for (int j = 0; j < i; ++j) {
+            acc = first ? m[i][j] * y[j] : acc + m[i][j] * y[j];
+            first = false;
+        }
+        if (i > 0) y[i] -= acc;
+    }
+    const double tol = std::numeric_limits<double>::min();
+    for (int i = 0; i < n; ++i) y[i] = (std::fabs(m[i][i]) > tol) ? y[i] / m[i][i] : 0.0;
+    for (int i = n - 1; i >= 0; --i) {  // L^T back
+        double acc = 0.0;
+        bool first = true;
+        for (int j = i + 1; j < n; ++j) {
+            acc = first ? m[j][i] * y[j] : acc + m[j][i] * y[j];
+            first = false;
+        }
+        if (i < n - 1) y[i] -= acc;
+    }
+    for (int k = n - 1; k >= 0; --k) std::swap(y[k], y[transp[k]]);  // P^T
+    std::memcpy(x, y, sizeof(y));
+}
+
+// rodrigues2rot (MLPnPsolver.cpp:628-643)
+void rodrigues2rot(const double w[3], double R[3][3]) {
+    const double S[3][3] = {{0.0, -w[2], w[1]}, {w[2], 0.0, -w[0]}, {-w[1], w[0], 0.0}};
+    const double nrm = norm3(w);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[i][j] = (i == j) ? 1.0 : 0.0;
+    if (nrm > kEps) {
+        const double a = rsc::dm::sin(nrm) / nrm;
+        const double b = (1.0 - rsc::dm::cos(nrm)) / (nrm * nrm);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                const double ss = S[i][0] * S[0][j] + S[i][1] * S[1][j] + S[i][2] * S[2][j];
+                R[i][j] = (R[i][j] + a * S[i][j]) + b * ss;
+            }
+    }
+}
+
+// rot2rodrigues (MLPnPsolver.cpp:645-657)
+void rot2rodrigues(const double R[3][3], double w[3]) {
+    w[0] = w[1] = w[2] = 0.0;
+    const double trace = ((R[0][0] + R[1][1]) + R[2][2]) - 1.0;
+    const double wnorm = rsc::dm::acos(trace / 2.0);
+    if (wnorm > kEps) {
+        w[0] = R[2][1] - R[1][2];
+        w[1] = R[0][2] - R[2][0];
+        w[2] = R[1][0] - R[0][1];
+        const double sc = wnorm / (2.0 * rsc::dm::sin(wnorm));
+        for (int k = 0; k < 3; ++k) w[k] *= sc;
+    }
+}
+
+// Residual Jacobian of r = n^T (R(w) X + t) / |R(w) X + t| for n in {n_r, n_s}
+// (replaces mlpnpJacs, MLPnPsolver.cpp:773-1020 — same function, analytic form):
+//   dr/dy = (n - (n.u) u) / |y|,  dy/dt = I,
+//   dy/dw_k = (w_k (w x z) + c_k x z) / |w|^2 with z = R X, c_k = w x (e_k - R e_k).
+void mlpnp_jac(const double X[3], const double nr[3], const double ns[3], const double w[3], const double t[3],
+               double J[2][6]) {
+    const double th2 = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
+    const double th = std::sqrt(th2);
+    const double a = rsc::dm::sin(th) / th;
+    const double b = (1.0 - rsc::dm::cos(th)) / th2;
+    const double S[3][3] = {{0.0, -w[2], w[1]}, {w[2], 0.0, -w[0]}, {-w[1], w[0], 0.0}};
+    double R[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            const double ss = S[i][0] * S[0][j] + S[i][1] * S[1][j] + S[i][2] * S[2][j];
+            R[i][j] = (((i == j) ? 1.0 : 0.0) + a * S[i][j]) + b * ss;
+        }
+    double z[3], y[3], u[3];
+    for (int i = 0; i < 3; ++i) {
+        z[i] = R[i][0] * X[0] + R[i][1] * X[1] + R[i][2] * X[2];
+        y[i] = z[i] + t[i];
+    }
+    const double ny = norm3(y);
+    for (int i = 0; i < 3; ++i) u[i] = y[i] / ny;
+    double wz[3], dy[3][3];
+    cross3(w, z, wz);
+    for (int k = 0; k < 3; ++k) {
+        double v[3], ck[3], cz[3];
+        for (int i = 0; i < 3; ++i) v[i] = ((i == k) ? 1.0 : 0.0) - R[i][k];
+        cross3(w, v, ck);
+        cross3(ck, z, cz);
+        for (int i = 0; i < 3; ++i) dy[k][i] = (w[k] * wz[i] + cz[i]) / th2;
+    }
+    const double* nv[2] = {nr, ns};
+    for (int row = 0; row < 2; ++row) {
+        const double* n = nv[row];
+        const double nu = dot3(n, u);
+        double g[3];
+        for (int i = 0; i < 3; ++i) g[i] = (n[i] - nu * u[i]) / ny;
+        for (int k = 0; k < 3; ++k) J[row][k] = dot3(g, dy[k]);
+        for (int i = 0; i < 3; ++i) J[row][3 + i] = g[i];
+    }
+}
+
+// mlpnp_gn (MLPnPsolver.cpp:659-723), use_cov = false.
+void mlpnp_gn(double x[6], int n, const double (*pts)[3], const double (*Ns)[3][2]) {
+    std::vector<double> r(2 * n), Jm(2 * n * 6), dl(2 * n);
+    int it = 0;
+    bool stop = false;
+    while (it < 5 && !stop) {
+        // mlpnp_residuals_and_jacs (:725-771)
+        double R[3][3];
+        rodrigues2rot(x, R);
+        for (int i = 0; i < n; ++i) {
+            double pc[3];
+            for (int k = 0; k < 3; ++k)
+                pc[k] = (R[k][0] * pts[i][0] + R[k][1] * pts[i][1] + R[k][2] * pts[i][2]) + x[3 + k];
+            const double nrm = norm3(pc);
+            for (int k = 0; k < 3; ++k) pc[k] = pc[k] / nrm;
+            const double nr[3] = {Ns[i][0][0], Ns[i][1][0], Ns[i][2][0]};
+            const double ns[3] = {Ns[i][0][1], Ns[i][1][1], Ns[i][2][1]};
+            r[2 * i] = dot3(nr, pc);
+            r[2 * i + 1] = dot3(ns, pc);
+            double J[2][6];
+            mlpnp_jac(pts[i], nr, ns, x, x + 3, J);
+            for (int k = 0; k < 6; ++k) { Jm[(2 * i) * 6 + k] = J[0][k]; Jm[(2 * i + 1) * 6 + k] = J[1][k]; }
+        }
+        double A[6][6], g[6], dx[6];
+        for (int a = 0; a < 6; ++a) {
+            for (int b = 0; b < 6; ++b) {
+                double s = Jm[a] * Jm[b];
+                for (int q = 1; q < 2 * n; ++q) s = s + Jm[q * 6 + a] * Jm[q * 6 + b];
+                A[a][b] = s;
+            }
+            double s = Jm[a] * r[0];
+            for (int q = 1; q < 2 * n; ++q) s = s + Jm[q * 6 + a] * r[q];
+            g[a] = s;
+        }
+        ldlt_solve6(A, g, dx);
+        double mx = std::fabs(dx[0]), mn = std::fabs(dx[0]);
+        for (int k = 1; k < 6; ++k) {
+            const double v = std::fabs(dx[k]);
+            mx = (mx < v) ? v : mx;
+            mn = (v < mn) ? v : mn;
+        }
+        if (mx > 5.0 || mn > 1.0) break;
+        double dlm = 0.0;
+        for (int q = 0; q < 2 * n; ++q) {
+            double s = Jm[q * 6] * dx[0];
+            for (int k = 1; k < 6; ++k) s = s + Jm[q * 6 + k] * dx[k];
+            const double v = std::fabs(s);
+            dlm = (q == 0) ? v : ((dlm < v) ? v : dlm);
+        }
+        for (int k = 0; k < 6; ++k) x[k] = x[k] - dx[k];
+        if (dlm < 1e-5) {
+            stop = true;
+            break;
+        }
+        ++it;
+    }
+}
+
+}  // namespace
+
+// MLPnPsolver.cpp:5-53
+MLPnPOracle::MLPnPOracle(int n, int n_points, const float* p2d, const float* p3dw, const float* sigma2,
+                         const int32_t* kp_index, float fx_, float fy_, float cx_, float cy_, uint32_t seed)
+    : fx(fx_), fy(fy_), cx(cx_), cy(cy_), N_points(n_points), rng(seed) {
+    mvP2D.assign(p2d, p2d + 2 * n);
+    mvSigma2.assign(sigma2, sigma2 + n);
+    mvKeyPointIndices.assign(kp_index, kp_index + n);
+    mvBearing.resize(3 * n);
+    mvP3Dw.resize(3 * n);
+    for (int i = 0; i < n; ++i) {
+        const float x = (p2d[2 * i] - cx) / fx;  // float arithmetic (:32-33)
+        const float y = (p2d[2 * i + 1] - cy) / fy;
+        mvBearing[3 * i] = x;
+        mvBearing[3 * i + 1] = y;
+        mvBearing[3 * i + 2] = 1.0;
+        for (int c = 0; c < 3; ++c) mvP3Dw[3 * i + c] = p3dw[3 * i + c];
+    }
+    mvAllIndices.resize(n);
+    for (int i = 0; i < n; ++i) mvAllIndices[i] = i;
+    for (int i = 0; i < 16; ++i) mBestTcw[i] = (i % 5 == 0) ? 1.f : 0.f;
+    for (int i = 0; i < 3; ++i) { mti[i] = 0.0; for (int j = 0; j < 3; ++j) mRi[i][j] = 0.0; }
+    SetRansacParameters();
+}
+
+// MLPnPsolver.cpp:185-220 (same adjustment as PnPsolver, eps^3 — Q2)
+void MLPnPOracle::SetRansacParameters(double probability, int minInliers, int maxIterations, int minSet,
+                                      float epsilon, float th2) {
+    mRansacProb = probability;
+    mRansacMinInliers = minInliers;
+    mRansacMaxIts = maxIterations;
+    mRansacEpsilon = epsilon;
+    mRansacMinSet = minSet;
+    N = (int)mvSigma2.size();
+    mvbInliersi.assign(N, 0);
+    int nMinInliers = N * mRansacEpsilon;
+    if (nMinInliers < mRansacMinInliers) nMinInliers = mRansacMinInliers;
+    if (nMinInliers < minSet) nMinInliers = minSet;
+    mRansacMinInliers = nMinInliers;
+    if (mRansacEpsilon < (float)mRansacMinInliers / N) mRansacEpsilon = (float)mRansacMinInliers / N;
+    int nIterations;
+    if (mRansacMinInliers == N)
+        nIterations = 1;
+    else
+        nIterations = (int)std::ceil(std::log(1 - mRansacProb) / std::log(1 - std::pow((double)mRansacEpsilon, 3.0)));
+    mRansacMaxIts = std::max(1, std::min(nIterations, mRansacMaxIts));
+    mvMaxError.resize(mvSigma2.size());
+    for (size_t i = 0; i < mvSigma2.size(); i++) mvMaxError[i] = mvSigma2[i] * th2;
+}
+
+// MLPnPsolver.cpp:222-255: double rotation of the float point, rounded to float; float projection.
+void MLPnPOracle::CheckInliers() {
+    mnInliersi = 0;
+    for (int i = 0; i < N; i++) {
+        const float X = (float)mvP3Dw[3 * i], Y = (float)mvP3Dw[3 * i + 1], Z = (float)mvP3Dw[3 * i + 2];
+        const float xc = (float)(mRi[0][0] * X + mRi[0][1] * Y + mRi[0][2] * Z + mti[0]);
+        const float yc = (float)(mRi[1][0] * X + mRi[1][1] * Y + mRi[1][2] * Z + mti[1]);
+        const float zc = (float)(mRi[2][0] * X + mRi[2][1] * Y + mRi[2][2] * Z + mti[2]);
+        const float u = fx * xc / zc + cx;
+        const float v = fy * yc / zc + cy;
+        const float dX = mvP2D[2 * i] - u;
+        const float dY = mvP2D[2 * i + 1] - v;
+        const float error2 = dX * dX + dY * dY;
+        mvbInliersi[i] = error2 < mvMaxError[i];
+        if (mvbInliersi[i]) mnInliersi++;
+    }
+}
+
+// computePose (MLPnPsolver.cpp:321-623) with covs.size() == 1 (use_cov false, Q15).
+void MLPnPOracle::computePose(const int* idx, int n, double Rout[3][3], double tout[3]) {
+    assert(n > 5);
+    std::vector<double> P(3 * n), P0(3 * n);
+    std::vector<double[3][2]> Ns(n);
+    for (int i = 0; i < n; ++i) {
+        const double* f = &mvBearing[3 * idx[i]];
+        bearing_nullspace(f, Ns[i]);
+        for (int c = 0; c < 3; ++c) P[3 * i + c] = P0[3 * i + c] = mvP3Dw[3 * idx[i] + c];
+    }
+    // 1. planarity: FullPivHouseholderQR(points3 * points3^T).rank() == 2
+    double PPt[3][3];
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+            double s = P[a] * P[b];
+            for (int i = 1; i < n; ++i) s = s + P[3 * i + a] * P[3 * i + b];
+            PPt[a][b] = s;
+        }
+    const bool planar = fullpiv_rank3(PPt) == 2;
+    double eigenRot[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    if (planar) {
+        const SymEig<double, 3> es = sym_eig<double, 3>(PPt);
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) eigenRot[r][c] = es.V[c][r];  // eigenvectors()^T
+        for (int i = 0; i < n; ++i) {
+            double q[3];
+            for (int r = 0; r < 3; ++r)
+                q[r] = eigenRot[r][0] * P[3 * i] + eigenRot[r][1] * P[3 * i + 1] + eigenRot[r][2] * P[3 * i + 2];
+            for (int r = 0; r < 3; ++r) P[3 * i + r] = q[r];
+        }
+    }
+    // 3. design matrix A (2n x 12, or 2n x 9 when planar) and 4. A^T A, JacobiSVD, last V column
+    const int colsA = planar ? 9 : 12;
+    std::vector<double> A(2 * n * colsA, 0.0);
+    for (int i = 0; i < n; ++i) {
+        const double* pt = &P[3 * i];
+        for (int s = 0; s < 2; ++s) {
+            double* row = &A[(2 * i + s) * colsA];
+            const double n0 = Ns[i][0][s], n1 = Ns[i][1][s], n2 = Ns[i][2][s];
+            if (planar) {
+                row[0] = n0 * pt[1]; row[1] = n0 * pt[2];
+                row[2] = n1 * pt[1]; row[3] = n1 * pt[2];
+                row[4] = n2 * pt[1]; row[5] = n2 * pt[2];
+                row[6] = n0; row[7] = n1; row[8] = n2;
+            } else {
+                row[0] = n0 * pt[0]; row[1] = n0 * pt[1]; row[2] = n0 * pt[2];
+                row[3] = n1 * pt[0]; row[4] = n1 * pt[1]; row[5] = n1 * pt[2];
+                row[6] = n2 * pt[0]; row[7] = n2 * pt[1]; row[8] = n2 * pt[2];
+                row[9] = n0; row[10] = n1; row[11] = n2;
+            }
+        }
+    }
+    std::vector<double> AtA(colsA * colsA), Vs(colsA * colsA), sv(colsA);
+    for (int a = 0; a < colsA; ++a)
+        for (int b = 0; b < colsA; ++b) {
+            double s = A[a] * A[b];
+            for (int r = 1; r < 2 * n; ++r) s = s + A[r * colsA + a] * A[r * colsA + b];
+            AtA[a * colsA + b] = s;
+        }
+    jacobi_svd_square(colsA, AtA.data(), false, nullptr, sv.data(), Vs.data());
+    double r1[12];
+    for (int k = 0; k < colsA; ++k) r1[k] = Vs[k * colsA + colsA - 1];
+
+    double R[3][3], t[3];
+    if (planar) {
+        double tmp[3][3] = {{0.0, r1[0], r1[1]}, {0.0, r1[2], r1[3]}, {0.0, r1[4], r1[5]}};
+        {
+            const double c1[3] = {tmp[0][1], tmp[1][1], tmp[2][1]}, c2[3] = {tmp[0][2], tmp[1][2], tmp[2][2]};
+            double c0[3];
+            cross3(c1, c2, c0);
+            for (int r = 0; r < 3; ++r) tmp[r][0] = c0[r];
+        }
+        double tt[3][3];
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) tt[r][c] = tmp[c][r];
+        const double cn1[3] = {tt[0][1], tt[1][1], tt[2][1]}, cn2[3] = {tt[0][2], tt[1][2], tt[2][2]};
+        const double scale = 1.0 / std::sqrt(std::fabs(norm3(cn1) * norm3(cn2)));
+        double U3[9], S3[3], V3[9], R1[3][3];
+        jacobi_svd_square(3, &tt[0][0], true, U3, S3, V3);
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) R1[r][c] = U3[r * 3] * V3[c * 3] + U3[r * 3 + 1] * V3[c * 3 + 1] + U3[r * 3 + 2] * V3[c * 3 + 2];
+        if (det3m(R1) < 0) for (auto& row : R1) for (double& v : row) v *= -1.0;
+        double R2[3][3];  // eigenRot^T * Rout1
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) R2[r][c] = eigenRot[0][r] * R1[0][c] + eigenRot[1][r] * R1[1][c] + eigenRot[2][r] * R1[2][c];
+        const double tv[3] = {scale * r1[6], scale * r1[7], scale * r1[8]};
+        double Ro[3][3];
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Ro[r][c] = -R2[c][r];  // transpose, *= -1
+        if (det3m(Ro) < 0.0) for (int r = 0; r < 3; ++r) Ro[r][2] = -Ro[r][2];
+        double Rc[4][3][3], Tc[4][3];
+        for (int k = 0; k < 4; ++k) {
+            const bool flipR = k >= 2, flipT = (k & 1) != 0;
+            for (int r = 0; r < 3; ++r) {
+                for (int c = 0; c < 3; ++c) Rc[k][r][c] = (flipR && c < 2) ? -Ro[r][c] : Ro[r][c];
+                Tc[k][r] = flipT ? -tv[r] : tv[r];
+            }
+        }
+        double normVal[4];
+        for (int k = 0; k < 4; ++k) {
+            double norms = 0.0;
+            for (int p = 0; p < 6; ++p) {
+                double v[3];
+                for (int r = 0; r < 3; ++r)
+                    v[r] = (Rc[k][r][0] * P0[3 * p] + Rc[k][r][1] * P0[3 * p + 1] + Rc[k][r][2] * P0[3 * p + 2]) + Tc[k][r];
+                const double nv = norm3(v);
+                for (int r = 0; r < 3; ++r) v[r] = v[r] / nv;
+                norms += (1.0 - dot3(v, &mvBearing[3 * idx[p]]));
+            }
+            normVal[k] = norms;
+        }
+        int best = 0;
+        for (int k = 1; k < 4; ++k) if (normVal[k] < normVal[best]) best = k;
+        std::memcpy(R, Rc[best], sizeof(R));
+        std::memcpy(t, Tc[best], sizeof(t));
+    } else {
+        double tmp[3][3] = {{r1[0], r1[3], r1[6]}, {r1[1], r1[4], r1[7]}, {r1[2], r1[5], r1[8]}};
+        const double c0[3] = {tmp[0][0], tmp[1][0], tmp[2][0]}, c1[3] = {tmp[0][1], tmp[1][1], tmp[2][1]},
+                     c2[3] = {tmp[0][2], tmp[1][2], tmp[2][2]};
+        const double scale = 1.0 / rsc::dm::cbrt(std::fabs(norm3(c0) * norm3(c1) * norm3(c2)));
+        double U3[9], S3[3], V3[9];
+        jacobi_svd_square(3, &tmp[0][0], true, U3, S3, V3);
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) R[r][c] = U3[r * 3] * V3[c * 3] + U3[r * 3 + 1] * V3[c * 3 + 1] + U3[r * 3 + 2] * V3[c * 3 + 2];
+        if (det3m(R) < 0) for (auto& row : R) for (double& v : row) v *= -1.0;
+        const double ts[3] = {scale * r1[9], scale * r1[10], scale * r1[11]};
+        double tv[3];
+        for (int r = 0; r < 3; ++r) tv[r] = R[r][0] * ts[0] + R[r][1] * ts[1] + R[r][2] * ts[2];
+        // 2-way sign test on the first 6 correspondences with the inverted transforms (:570-601)
+        double err[2], Ti[2][4][4];
+        for (int s = 0; s < 2; ++s) {
+            double T4[4][4] = {{R[0][0], R[0][1], R[0][2], s ? -tv[0] : tv[0]},
+                               {R[1][0], R[1][1], R[1][2], s ? -tv[1] : tv[1]},
+                               {R[2][0], R[2][1], R[2][2], s ? -tv[2] : tv[2]},
+                               {0.0, 0.0, 0.0, 1.0}};
+            inverse4(T4, Ti[s]);
+            err[s] = 0.0;
+            for (int p = 0; p < 6; ++p) {
+                double v[3];
+                for (int r = 0; r < 3; ++r)
+                    v[r] = (Ti[s][r][0] * P0[3 * p] + Ti[s][r][1] * P0[3 * p + 1] + Ti[s][r][2] * P0[3 * p + 2]) + Ti[s][r][3];
+                const double nv = norm3(v);
+                for (int r = 0; r < 3; ++r) v[r] = v[r] / nv;
+                err[s] += (1.0 - dot3(v, &mvBearing[3 * idx[p]]));
+            }
+        }
+        const int k = (err[0] < err[1]) ? 0 : 1;
+        for (int r = 0; r < 3; ++r) {
+            t[r] = Ti[k][r][3];
+            for (int c = 0; c < 3; ++c) R[r][c] = Ti[0][r][c];
+        }
+    }
+    // 5. Gauss-Newton on (rodrigues, t)
+    double x[6];
+    rot2rodrigues(R, x);
+    x[3] = t[0]; x[4] = t[1]; x[5] = t[2];
+    std::vector<double> pts(3 * n);
+    for (int i = 0; i < 3 * n; ++i) pts[i] = P0[i];
+    mlpnp_gn(x, n, reinterpret_cast<const double(*)[3]>(pts.data()), Ns.data());
+    rodrigues2rot(x, Rout);
+    tout[0] = x[3]; tout[1] = x[4]; tout[2] = x[5];
+}
+
+void MLPnPOracle::compute_pose_public(const int* idx, int n, double R[9], double t[3]) {
+    double Rm[3][3];
+    computePose(idx, n, Rm, t);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) R[3 * r + c] = Rm[r][c];
+}
+
+// MLPnPsolver.cpp:56-183
+bool MLPnPOracle::iterate(int nIterations, bool& bNoMore, std::vector<uint8_t>& vbInliers, int& nInliers,
+                          float T[16]) {
+    for (int i = 0; i < 16; ++i) T[i] = (i % 5 == 0) ? 1.f : 0.f;  // Tout.setIdentity() (Q10)
+    bNoMore = false;
+    vbInliers.clear();
+    nInliers = 0;
+    if (N < mRansacMinInliers) {
+        bNoMore = true;
+        return false;
+    }
+    int nCurrentIterations = 0;
+    std::vector<int> sample(mRansacMinSet);
+    while (mnIterations < mRansacMaxIts || nCurrentIterations < nIterations) {  // Q1
+        nCurrentIterations++;
+        mnIterations++;
+        std::vector<int32_t> avail = mvAllIndices;
+        Trace tr{};
+        for (short i = 0; i < mRansacMinSet; ++i) {
+            const int randi = rng.random_int(0, (int)avail.size() - 1);
+            sample[i] = avail[randi];
+            if (i < 8) tr.sample[i] = sample[i];
+            avail[randi] = avail.back();
+            avail.pop_back();
+        }
+        computePose(sample.data(), mRansacMinSet, mRi, mti);
+        CheckInliers();
+        if (trace) {
+            tr.n_inliers = mnInliersi;
+            for (int r = 0; r < 3; ++r) { tr.t[r] = mti[r]; for (int c = 0; c < 3; ++c) tr.R[3 * r + c] = mRi[r][c]; }
+            trace->push_back(tr);
+        }
+        if (mnInliersi >= mRansacMinInliers) {
+            if (mnInliersi > mnBestInliers) {
+                mvbBestInliers = mvbInliersi;
+                mnBestInliers = mnInliersi;
+                for (int r = 0; r < 3; ++r) {
+                    for (int c = 0; c < 3; ++c) mBestTcw[4 * r + c] = (float)mRi[r][c];
+                    mBestTcw[4 * r + 3] = (float)mti[r];
+                }
+            }
+            // Refine(): computePose over the best inliers is discarded and CheckInliers() re-counts
+            // the current hypothesis (:290-296), so the refined set is the current one.
+            if (mnInliersi > mRansacMinInliers) {
+                nInliers = mnInliersi;
+                vbInliers.assign(N_points, 0);
+                for (int i = 0; i < N; i++)
+                    if (mvbInliersi[i]) vbInliers[mvKeyPointIndices[i]] = 1;
+                for (int r = 0; r < 3; ++r) {
+                    for (int c = 0; c < 3; ++c) T[4 * r + c] = (float)mRi[r][c];
+                    T[4 * r + 3] = (float)mti[r];
+                }
+                return true;
+            }
+        }
+    }
+    if (mnIterations >= mRansacMaxIts) {
+        bNoMore = true;
+        if (mnBestInliers >= mRansacMinInliers) {
+            nInliers = mnBestInliers;
+            vbInliers.assign(N_points, 0);
+            for (int i = 0; i < N; i++)
+                if (mvbBestInliers[i]) vbInliers[mvKeyPointIndices[i]] = 1;
+            std::memcpy(T, mBestTcw, sizeof(mBestTcw));
+            return true;
+        }
+    }
+    return false;
+}
+
+}  // namespace rsc_oracle

@@ -100,6 +100,7 @@ struct rsc_context {
     DevBuf<int32_t> d_samples;
     DevBuf<double> d_stage;  // quad path: per-hypothesis stage records between the two solve kernels
     DevBuf<float> d_gather;  // gathered pose records (+ their indices)
+    DevBuf<double> d_mposes; // MLPnP hypothesis poses, double[12] per record
     DevBuf<char> d_desc;
     PinBuf<char> h_desc;
     PinBuf<int32_t> h_counts;
@@ -150,6 +151,22 @@ struct rsc_sim3 {
     int spec_out0 = -1, spec_H = 0;
     ~rsc_sim3() {
         for (void* p : {(void*)d_x1, (void*)d_x2, (void*)d_pim})
+            if (p) (void)hipFree(p);
+    }
+};
+
+struct rsc_mlpnp {
+    rsc_context* ctx = nullptr;
+    MLState st;
+    float fx = 0, fy = 0, cx = 0, cy = 0;
+    float4* d_pts = nullptr;
+    float2* d_uv = nullptr;
+    float2* d_brg = nullptr;
+    uint64_t* d_best = nullptr;
+    int words = 0;
+    int spec_out0 = -1, spec_H = 0;
+    ~rsc_mlpnp() {
+        for (void* p : {(void*)d_pts, (void*)d_uv, (void*)d_brg, (void*)d_best})
             if (p) (void)hipFree(p);
     }
 };
@@ -515,6 +532,152 @@ struct HipSim3Backend : Sim3Backend {
             std::memset(out[q], 0, s.mN1);
             for (int j = 0; j < s.N; ++j)
                 if ((words[q][j >> 6] >> (j & 63)) & 1ull) out[q][s.indices1[j]] = 1;
+        }
+        return 0;
+    }
+};
+
+// ------------------------------------------------------------------------------------------------
+// MLPnP backend
+// ------------------------------------------------------------------------------------------------
+struct HipMLBackend : MLBackend {
+    rsc_context* C;
+    std::vector<rsc_mlpnp*> all;      // solvers of the call
+    std::vector<rsc_mlpnp*> solvers;  // slot j of the last speculation
+    explicit HipMLBackend(rsc_context* c) : C(c) {}
+    rsc_mlpnp* of(MLState* s) {
+        for (auto* p : all)
+            if (&p->st == s) return p;
+        return nullptr;
+    }
+
+    int speculate(MLState* const* S, int count, const int* H, std::vector<std::vector<int32_t>>& counts) override {
+        int total = 0, maxN = 1;
+        std::vector<DevML> probs(count);
+        std::vector<LaunchProb> lps(count);
+        solvers.assign(count, nullptr);
+        for (int i = 0; i < count; ++i) {
+            rsc_mlpnp* p = of(S[i]);
+            if (!p) return RSC_ERR_ARG;
+            solvers[i] = p;
+            S[i]->rng.ensure(C->table, H[i] * S[i]->mRansacMinSet);
+            DevML& d = probs[i];
+            d.pts = p->d_pts; d.uv = p->d_uv; d.brg = p->d_brg; d.n = S[i]->N;
+            d.fx = p->fx; d.fy = p->fy; d.cx = p->cx; d.cy = p->cy; d.th2 = S[i]->th2;
+            LaunchProb& lp = lps[i];
+            lp.prob = i;
+            lp.H = H[i];
+            lp.out0 = total;
+            lp.g0 = S[i]->rng.g;
+            std::memcpy(lp.window, S[i]->rng.window, sizeof(lp.window));
+            lp.pad = 0;
+            p->spec_out0 = total;
+            p->spec_H = H[i];
+            total += H[i];
+            maxN = std::max(maxN, S[i]->N);
+        }
+        const int ppt = ppt_for(maxN);
+        if (ppt > 32) {
+            g_last_error = "more than 8192 correspondences per problem";
+            return RSC_ERR_UNSUPPORTED;
+        }
+        const int mw = ppt * 4;
+        C->mask_words = mw;
+        std::vector<std::vector<int2>> solve_wgs(3);
+        std::vector<int4> scan_wgs;
+        const int HC = 32;
+        for (int i = 0; i < count; ++i) {
+            const int g = S[i]->mRansacMinSet - 6;
+            for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs[g].push_back(make_int2(i, h0));
+            for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
+        }
+        Blob b;
+        const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevML));
+        const size_t o_lps = b.add(lps.data(), lps.size() * sizeof(LaunchProb));
+        size_t o_solve[3];
+        for (int g = 0; g < 3; ++g) o_solve[g] = b.add(solve_wgs[g].data(), solve_wgs[g].size() * sizeof(int2));
+        const size_t o_scan = b.add(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
+        if (int e = upload_blob(C, b)) return e;
+        if (int e = C->d_mposes.ensure((size_t)total * 12)) return e;
+        if (int e = C->d_counts.ensure((size_t)total)) return e;
+        if (int e = C->d_masks.ensure((size_t)total * mw)) return e;
+        if (C->keep_samples)
+            if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
+        const char* base = C->d_desc.p;
+        const DevML* dprobs = reinterpret_cast<const DevML*>(base + o_probs);
+        const LaunchProb* dlps = reinterpret_cast<const LaunchProb*>(base + o_lps);
+        timing_begin(C, 0);
+        for (int g = 0; g < 3; ++g) {
+            if (solve_wgs[g].empty()) continue;
+            RSC_HIP(launch_mlpnp_solve(6 + g, (int)solve_wgs[g].size(), dprobs, dlps,
+                                       reinterpret_cast<const int2*>(base + o_solve[g]), C->d_table.p, C->d_mposes.p,
+                                       C->keep_samples ? C->d_samples.p : nullptr, C->stream));
+        }
+        timing_begin(C, 1);
+        RSC_HIP(launch_mlpnp_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
+                                  C->d_mposes.p, C->d_counts.p, C->d_masks.p, mw, C->stream));
+        timing_begin(C, 2);
+        if (int e = C->h_counts.ensure(total)) return e;
+        RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        if (C->timing) {
+            float a = 0, sc = 0;
+            (void)hipEventElapsedTime(&a, C->ev[0], C->ev[1]);
+            (void)hipEventElapsedTime(&sc, C->ev[1], C->ev[2]);
+            C->last_ms[0] += a;
+            C->last_ms[1] += sc;
+            C->last_ms[3] += 1;
+            C->last_ms[4] += total;
+        }
+        counts.assign(count, {});
+        for (int i = 0; i < count; ++i)
+            counts[i].assign(C->h_counts.p + lps[i].out0, C->h_counts.p + lps[i].out0 + H[i]);
+        return 0;
+    }
+
+    int pose_of(int j, int k, float* pose12) {
+        // R, t double -> float (cv::Mat::convertTo(CV_32F), MLPnPsolver.cpp:152-153)
+        double d[12];
+        RSC_HIP(hipMemcpyAsync(d, C->d_mposes.p + (size_t)(solvers[j]->spec_out0 + k) * 12, 96, hipMemcpyDeviceToHost,
+                               C->stream));
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        for (int q = 0; q < 12; ++q) pose12[q] = (float)d[q];
+        return 0;
+    }
+
+    int adopt_best(MLState* s, int j, int k) override {
+        rsc_mlpnp* p = solvers[j];
+        const size_t rec = (size_t)(p->spec_out0 + k);
+        RSC_HIP(hipMemcpyAsync(p->d_best, C->d_masks.p + rec * C->mask_words, (size_t)p->words * 8,
+                               hipMemcpyDeviceToDevice, C->stream));
+        float pose[12];
+        if (int e = pose_of(j, k, pose)) return e;
+        pose12_to_T(pose, s->mBestTcw);
+        return 0;
+    }
+
+    int fetch_poses(const int* j, const int* k, int n, float (*pose12)[12]) override {
+        for (int q = 0; q < n; ++q)
+            if (int e = pose_of(j[q], k[q], pose12[q])) return e;
+        return 0;
+    }
+
+    int fetch_mask(MLState* const* S, int count, const int* kind, const int* j, const int* k,
+                   uint8_t* const* out) override {
+        std::vector<std::vector<uint64_t>> words(count);
+        for (int q = 0; q < count; ++q) {
+            rsc_mlpnp* p = of(S[q]);
+            words[q].resize(p->words);
+            const uint64_t* src = (kind[q] == 2) ? p->d_best
+                                                 : C->d_masks.p + (size_t)(solvers[j[q]]->spec_out0 + k[q]) * C->mask_words;
+            RSC_HIP(hipMemcpyAsync(words[q].data(), src, (size_t)p->words * 8, hipMemcpyDeviceToHost, C->stream));
+        }
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        for (int q = 0; q < count; ++q) {
+            const MLState& s = *S[q];
+            std::memset(out[q], 0, s.N_points);
+            for (int i = 0; i < s.N; ++i)
+                if ((words[q][i >> 6] >> (i & 63)) & 1ull) out[q][s.kp_index[i]] = 1;
         }
         return 0;
     }
@@ -948,4 +1111,140 @@ int rsc_diag_pnp_phase_stamps(rsc_pnp* const* solvers, int count, int H, uint64_
     return st;
 }
 
+
+// ---- MLPnP ----
+int rsc_mlpnp_create(rsc_context* C, const rsc_pnp_problem* pb, uint32_t seed, rsc_mlpnp** out) {
+    if (!C || !pb || !out || pb->n < 0 || pb->n_points < pb->n) return RSC_ERR_ARG;
+    if (pb->n > 0 && (!pb->p2d || !pb->p3dw || !pb->sigma2)) return RSC_ERR_ARG;
+    *out = nullptr;
+    RSC_HIP(hipSetDevice(C->device));
+    std::unique_ptr<rsc_mlpnp> S(new rsc_mlpnp());
+    S->ctx = C;
+    MLState& s = S->st;
+    s.N = pb->n;
+    s.N_points = pb->n_points;
+    S->fx = pb->fx; S->fy = pb->fy; S->cx = pb->cx; S->cy = pb->cy;
+    s.kp_index.resize(pb->n);
+    for (int i = 0; i < pb->n; ++i) s.kp_index[i] = pb->kp_index ? pb->kp_index[i] : i;
+    s.reset(seed);
+    const int n = std::max(pb->n, 1);
+    S->words = (n + 63) / 64;
+    std::vector<float4> pts(n);
+    std::vector<float2> uv(n), brg(n);
+    for (int i = 0; i < pb->n; ++i) {
+        pts[i] = make_float4(pb->p3dw[3 * i], pb->p3dw[3 * i + 1], pb->p3dw[3 * i + 2], pb->sigma2[i]);
+        uv[i] = make_float2(pb->p2d[2 * i], pb->p2d[2 * i + 1]);
+        // bearing (x, y, 1): float arithmetic as MLPnPsolver.cpp:32-33
+        const float bx = (pb->p2d[2 * i] - pb->cx) / pb->fx;
+        const float by = (pb->p2d[2 * i + 1] - pb->cy) / pb->fy;
+        brg[i] = make_float2(bx, by);
+    }
+    RSC_HIP(hipMalloc(&S->d_pts, n * sizeof(float4)));
+    RSC_HIP(hipMalloc(&S->d_uv, n * sizeof(float2)));
+    RSC_HIP(hipMalloc(&S->d_brg, n * sizeof(float2)));
+    RSC_HIP(hipMalloc(&S->d_best, S->words * 8));
+    RSC_HIP(hipMemcpy(S->d_pts, pts.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    RSC_HIP(hipMemcpy(S->d_uv, uv.data(), n * sizeof(float2), hipMemcpyHostToDevice));
+    RSC_HIP(hipMemcpy(S->d_brg, brg.data(), n * sizeof(float2), hipMemcpyHostToDevice));
+    RSC_HIP(hipMemset(S->d_best, 0, S->words * 8));
+    mlpnp_set_params(s, 0.99, 8, 300, 6, 0.4f, 5.991f);  // the ctor's SetRansacParameters() (:52)
+    *out = S.release();
+    return RSC_OK;
+}
+
+void rsc_mlpnp_destroy(rsc_mlpnp* s) { delete s; }
+
+int rsc_mlpnp_set_ransac_parameters(rsc_mlpnp* s, double probability, int min_inliers, int max_iterations,
+                                    int min_set, float epsilon, float th2) {
+    if (!s) return RSC_ERR_ARG;
+    if (min_set < 6 || min_set > 8) {
+        g_last_error = "MLPnP min_set outside [6,8] (computePose asserts n > 5, MLPnPsolver.cpp:324)";
+        return RSC_ERR_UNSUPPORTED;
+    }
+    mlpnp_set_params(s->st, probability, min_inliers, max_iterations, min_set, epsilon, th2);
+    return RSC_OK;
+}
+
+int rsc_mlpnp_set_ransac_parameters_many(rsc_mlpnp* const* s, int count, double probability, int min_inliers,
+                                         int max_iterations, int min_set, float epsilon, float th2) {
+    for (int i = 0; i < count; ++i)
+        if (int e = rsc_mlpnp_set_ransac_parameters(s[i], probability, min_inliers, max_iterations, min_set, epsilon,
+                                                    th2))
+            return e;
+    return RSC_OK;
+}
+
+int rsc_mlpnp_iterate_many(rsc_mlpnp* const* solvers, int count, const int32_t* n_its, rsc_pnp_result* out,
+                           uint8_t* const* inliers) {
+    if (count <= 0) return RSC_OK;
+    if (!solvers || !n_its || !out) return RSC_ERR_ARG;
+    rsc_context* C = solvers[0]->ctx;
+    for (int i = 0; i < count; ++i)
+        if (!solvers[i] || solvers[i]->ctx != C) return RSC_ERR_ARG;
+    RSC_HIP(hipSetDevice(C->device));
+    for (double& v : C->last_ms) v = 0;
+    HipMLBackend be(C);
+    be.all.assign(solvers, solvers + count);
+    std::vector<MLState*> S(count);
+    for (int i = 0; i < count; ++i) S[i] = &solvers[i]->st;
+    std::vector<MLResult> res(count);
+    if (int st = mlpnp_iterate_many(be, S.data(), count, n_its, res.data(), inliers)) return st;
+    for (int i = 0; i < count; ++i) {
+        out[i].ok = res[i].ok;
+        out[i].no_more = res[i].no_more;
+        out[i].n_inliers = res[i].n_inliers;
+        out[i].iterations = res[i].iterations;
+        std::memcpy(out[i].T, res[i].T, sizeof(out[i].T));
+    }
+    return RSC_OK;
+}
+
+int rsc_mlpnp_iterate(rsc_mlpnp* s, int n_its, rsc_pnp_result* out, uint8_t* inliers) {
+    if (!s || !out) return RSC_ERR_ARG;
+    int32_t n = n_its;
+    uint8_t* const m[1] = {inliers};
+    return rsc_mlpnp_iterate_many(&s, 1, &n, out, m);
+}
+
+int rsc_mlpnp_reset(rsc_mlpnp* s, uint32_t seed) {
+    if (!s) return RSC_ERR_ARG;
+    s->st.reset(seed);
+    return RSC_OK;
+}
+
+int rsc_mlpnp_reset_many(rsc_mlpnp* const* s, int count, const uint32_t* seeds) {
+    if (count > 0 && (!s || !seeds)) return RSC_ERR_ARG;
+    for (int i = 0; i < count; ++i) {
+        if (!s[i]) return RSC_ERR_ARG;
+        s[i]->st.reset(seeds[i]);
+    }
+    return RSC_OK;
+}
+
+int rsc_mlpnp_get_state(const rsc_mlpnp* s, int32_t out[6]) {
+    if (!s || !out) return RSC_ERR_ARG;
+    const MLState& t = s->st;
+    out[0] = t.mnIterations; out[1] = t.mRansacMaxIts; out[2] = t.mRansacMinInliers; out[3] = t.mnBestInliers;
+    out[4] = t.N; out[5] = t.mRansacMinSet;
+    return RSC_OK;
+}
+
+// Parity hook: double poses (R row-major 9 + t 3) of the last launch's hypotheses of this solver.
+int rsc_mlpnp_last_poses(rsc_mlpnp* s, double* out, int cap) {
+    if (!s || !out) return RSC_ERR_ARG;
+    rsc_context* C = s->ctx;
+    if (s->spec_out0 < 0 || !C->d_mposes.p) return 0;
+    const int n = std::min(cap, s->spec_H);
+    RSC_HIP(hipMemcpy(out, C->d_mposes.p + (size_t)s->spec_out0 * 12, (size_t)n * 96, hipMemcpyDeviceToHost));
+    return n;
+}
+
+int rsc_mlpnp_last_samples(rsc_mlpnp* s, int32_t* out, int cap) {
+    if (!s || !out) return RSC_ERR_ARG;
+    rsc_context* C = s->ctx;
+    if (s->spec_out0 < 0 || !C->d_samples.p) return 0;
+    const int n = std::min(cap, s->spec_H);
+    RSC_HIP(hipMemcpy(out, C->d_samples.p + (size_t)s->spec_out0 * 8, (size_t)n * 8 * 4, hipMemcpyDeviceToHost));
+    return n;
+}
 }  // extern "C"

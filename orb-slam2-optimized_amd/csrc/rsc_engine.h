@@ -446,4 +446,193 @@ inline int sim3_iterate_many(Sim3Backend& be, Sim3State* const* S, int count, co
     return 0;
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// MLPnPsolver state (include/MLPnPsolver.hpp:10-199) and iterate() replay (MLPnPsolver.cpp:56-183)
+// ------------------------------------------------------------------------------------------------
+struct MLState {
+    int N = 0, N_points = 0;
+    std::vector<int32_t> kp_index;
+    double mRansacProb = 0.99;
+    int mRansacMinInliers = 0, mRansacMaxIts = 0, mRansacMinSet = 6;
+    float mRansacEpsilon = 0.4f, th2 = 5.991f;
+    int mnIterations = 0;
+    int mnBestInliers = 0;
+    float mBestTcw[16];
+    RngStream rng;
+    uint32_t seed = 1;
+    void reset(uint32_t s) {
+        mnIterations = 0;
+        mnBestInliers = 0;
+        for (int i = 0; i < 16; ++i) mBestTcw[i] = (i % 5 == 0) ? 1.f : 0.f;
+        seed = s;
+        rng.seed(s);
+    }
+};
+
+// MLPnPsolver::SetRansacParameters (MLPnPsolver.cpp:185-220): the PnPsolver formula (Q2).
+inline void mlpnp_set_params(MLState& S, double probability, int minInliers, int maxIterations, int minSet,
+                             float epsilon, float th2) {
+    S.mRansacProb = probability;
+    S.mRansacMinInliers = minInliers;
+    S.mRansacMaxIts = maxIterations;
+    S.mRansacEpsilon = epsilon;
+    S.mRansacMinSet = minSet;
+    const int N = S.N;
+    int nMinInliers = N * S.mRansacEpsilon;
+    if (nMinInliers < S.mRansacMinInliers) nMinInliers = S.mRansacMinInliers;
+    if (nMinInliers < minSet) nMinInliers = minSet;
+    S.mRansacMinInliers = nMinInliers;
+    if (S.mRansacEpsilon < (float)S.mRansacMinInliers / N) S.mRansacEpsilon = (float)S.mRansacMinInliers / N;
+    int nIterations;
+    if (S.mRansacMinInliers == N)
+        nIterations = 1;
+    else
+        nIterations = (int)std::ceil(std::log(1 - S.mRansacProb) / std::log(1 - std::pow((double)S.mRansacEpsilon, 3.0)));
+    S.mRansacMaxIts = std::max(1, std::min(nIterations, S.mRansacMaxIts));
+    S.th2 = th2;
+}
+
+struct MLResult {
+    int ok = 0, no_more = 0, n_inliers = 0, iterations = 0;
+    float T[16];
+    int mask_kind = 0;  // 0: empty, 1: the returning hypothesis (= Refine's re-count), 2: best
+    int mask_j = -1, mask_k = -1;
+    MLResult() {
+        for (int i = 0; i < 16; ++i) T[i] = (i % 5 == 0) ? 1.f : 0.f;  // Tout.setIdentity() (Q10)
+    }
+};
+
+struct MLBackend {
+    virtual int speculate(MLState* const* states, int count, const int* H, std::vector<std::vector<int32_t>>& counts) = 0;
+    // mvbBestInliers / mBestTcw := hypothesis k of slot j of the last speculation
+    virtual int adopt_best(MLState* s, int j, int k) = 0;
+    // float poses (R 9 + t 3) of hypotheses (j[q], k[q]) of the last speculation
+    virtual int fetch_poses(const int* j, const int* k, int n, float (*pose12)[12]) = 0;
+    // masks: kind 1 = hypothesis (j, k) of the last speculation, kind 2 = the solver's best mask
+    virtual int fetch_mask(MLState* const* states, int count, const int* kind, const int* j, const int* k,
+                           uint8_t* const* out) = 0;
+    virtual ~MLBackend() {}
+};
+
+// MLPnPsolver::iterate for `count` solvers.  Refine() re-counts the current hypothesis (its
+// computePose result is discarded, MLPnPsolver.cpp:290), so the call returns at the first
+// hypothesis whose count is > minInliers; the best is updated on '>' among counts >= minInliers.
+inline int mlpnp_iterate_many(MLBackend& be, MLState* const* S, int count, const int* n_its, MLResult* res,
+                              uint8_t* const* inliers) {
+    std::vector<int> ncur(count, 0), active;
+    for (int i = 0; i < count; ++i) {
+        res[i] = MLResult();
+        MLState& s = *S[i];
+        if (s.N < s.mRansacMinInliers) {
+            res[i].no_more = 1;
+            res[i].iterations = s.mnIterations;
+            continue;
+        }
+        active.push_back(i);
+    }
+    auto loop_len = [&](int i) {
+        const MLState& s = *S[i];
+        return std::max(0, std::max(n_its[i] - ncur[i], s.mRansacMaxIts - s.mnIterations));
+    };
+    std::vector<char> done(count, 0);
+    std::vector<int> succ_i, succ_j, succ_k;
+    while (!active.empty()) {
+        std::vector<MLState*> spec;
+        std::vector<int> H, who;
+        for (int i : active) {
+            const int h = std::min(loop_len(i), kMaxSpeculate);
+            if (h > 0) { spec.push_back(S[i]); H.push_back(h); who.push_back(i); }
+        }
+        if (spec.empty()) break;
+        std::vector<std::vector<int32_t>> counts;
+        if (int st = be.speculate(spec.data(), (int)spec.size(), H.data(), counts)) return st;
+        std::vector<int> pj, pk, pi;
+        for (size_t j = 0; j < spec.size(); ++j) {
+            MLState& s = *spec[j];
+            const int i = who[j];
+            for (int k = 0; k < H[j]; ++k) {
+                ncur[i]++;
+                s.mnIterations++;
+                s.rng.g += s.mRansacMinSet;
+                const int c = counts[j][k];
+                if (c >= s.mRansacMinInliers) {
+                    if (c > s.mnBestInliers) {
+                        s.mnBestInliers = c;
+                        if (int st = be.adopt_best(&s, (int)j, k)) return st;
+                    }
+                    if (c > s.mRansacMinInliers) {
+                        res[i].ok = 1;
+                        res[i].n_inliers = c;
+                        res[i].mask_kind = 1;
+                        res[i].mask_j = (int)j;
+                        res[i].mask_k = k;
+                        pj.push_back((int)j);
+                        pk.push_back(k);
+                        pi.push_back(i);
+                        done[i] = 1;
+                        break;
+                    }
+                }
+            }
+        }
+        if (!pj.empty()) {
+            std::vector<float> p(pj.size() * 12);
+            if (int st = be.fetch_poses(pj.data(), pk.data(), (int)pj.size(), reinterpret_cast<float(*)[12]>(p.data())))
+                return st;
+            for (size_t q = 0; q < pj.size(); ++q) pose12_to_T(&p[12 * q], res[pi[q]].T);
+            // the masks of returning hypotheses must be read before the next speculation reuses
+            // the record buffers
+            std::vector<MLState*> ms;
+            std::vector<int> kinds, mj, mk;
+            std::vector<uint8_t*> outs;
+            for (size_t q = 0; q < pj.size(); ++q)
+                if (inliers && inliers[pi[q]]) {
+                    ms.push_back(S[pi[q]]);
+                    kinds.push_back(1);
+                    mj.push_back(pj[q]);
+                    mk.push_back(pk[q]);
+                    outs.push_back(inliers[pi[q]]);
+                }
+            if (!ms.empty())
+                if (int st = be.fetch_mask(ms.data(), (int)ms.size(), kinds.data(), mj.data(), mk.data(), outs.data()))
+                    return st;
+        }
+        std::vector<int> next;
+        for (size_t j = 0; j < spec.size(); ++j) {
+            const int i = who[j];
+            if (!done[i] && loop_len(i) > 0) next.push_back(i);
+        }
+        active.swap(next);
+    }
+    std::vector<MLState*> ms;
+    std::vector<int> kinds, mj, mk;
+    std::vector<uint8_t*> outs;
+    for (int i = 0; i < count; ++i) {
+        MLResult& R = res[i];
+        MLState& s = *S[i];
+        if (R.ok || R.no_more) { R.iterations = s.mnIterations; continue; }
+        if (s.mnIterations >= s.mRansacMaxIts) {
+            R.no_more = 1;
+            if (s.mnBestInliers >= s.mRansacMinInliers) {
+                R.ok = 1;
+                R.n_inliers = s.mnBestInliers;
+                std::memcpy(R.T, s.mBestTcw, sizeof(R.T));
+                R.mask_kind = 2;
+                if (inliers && inliers[i]) {
+                    ms.push_back(&s);
+                    kinds.push_back(2);
+                    mj.push_back(-1);
+                    mk.push_back(-1);
+                    outs.push_back(inliers[i]);
+                }
+            }
+        }
+        R.iterations = s.mnIterations;
+    }
+    if (!ms.empty())
+        if (int st = be.fetch_mask(ms.data(), (int)ms.size(), kinds.data(), mj.data(), mk.data(), outs.data())) return st;
+    return 0;
+}
+
 }  // namespace rsc

@@ -27,6 +27,16 @@ struct DevSim3 {
     float K1[4], K2[4];  // fx, fy, cx, cy
 };
 
+// One MLPnP problem (= one MLPnPsolver) resident in HBM.
+struct DevML {
+    const float4* pts;  // [n] x, y, z (mvP3Dw), w = sigma^2
+    const float2* uv;   // [n] mvP2D
+    const float2* brg;  // [n] bearing x, y (z = 1), float arithmetic of MLPnPsolver.cpp:32-33
+    int n;
+    float fx, fy, cx, cy;  // float members (MLPnPsolver.hpp:198)
+    float th2;
+};
+
 // Per-launch, per-problem speculation record: hypotheses [0, H) of this launch use draws
 // g0 + h*min_set + d of the glibc stream whose window is `window`.
 struct LaunchProb {
@@ -50,6 +60,11 @@ struct RefineJob {
 struct Window31 {
     uint32_t w[31];
 };
+// MLPnP: one lane per hypothesis (min_set 6..8), poses as double[12] records (R row-major, t).
+hipError_t launch_mlpnp_solve(int ns, int nwg, const DevML* probs, const LaunchProb* lps, const int2* wgt,
+                              const uint32_t* T, double* poses, int32_t* samples, hipStream_t st);
+hipError_t launch_mlpnp_scan(int ppt, int nwg, const DevML* probs, const LaunchProb* lps, const int4* wgt,
+                             const double* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st);
 hipError_t launch_gather_records(const float* src, int stride, int take, const int32_t* idx, int n, float* dst,
                                  hipStream_t st);
 hipError_t launch_rng_stream(const uint32_t* T, const uint32_t* window, int g0, int n, int32_t* out, hipStream_t st);

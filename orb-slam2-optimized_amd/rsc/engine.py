@@ -34,6 +34,9 @@ EXPORTED = [
     "rsc_sim3_iterate_many", "rsc_sim3_reset", "rsc_sim3_get_state", "rsc_sim3_prepared", "rsc_rand_stream",
     "rsc_pnp_reset_many", "rsc_pnp_set_ransac_parameters_many", "rsc_sim3_reset_many",
     "rsc_sim3_set_ransac_parameters_many",
+    "rsc_mlpnp_create", "rsc_mlpnp_destroy", "rsc_mlpnp_set_ransac_parameters",
+    "rsc_mlpnp_set_ransac_parameters_many", "rsc_mlpnp_iterate", "rsc_mlpnp_iterate_many", "rsc_mlpnp_reset",
+    "rsc_mlpnp_reset_many", "rsc_mlpnp_get_state", "rsc_mlpnp_last_poses", "rsc_mlpnp_last_samples",
 ]
 
 
@@ -103,6 +106,19 @@ def load_library(path: str = LIB_PATH):
                                                      C.c_float, C.c_float]
     L.rsc_sim3_reset_many.argtypes = [C.POINTER(vp), C.c_int, u32p]
     L.rsc_sim3_set_ransac_parameters_many.argtypes = [C.POINTER(vp), C.c_int, C.c_double, C.c_int, C.c_int]
+    f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+    L.rsc_mlpnp_create.argtypes = [vp, C.POINTER(PnPProblem), C.c_uint32, C.POINTER(vp)]
+    L.rsc_mlpnp_destroy.argtypes = [vp]
+    L.rsc_mlpnp_set_ransac_parameters.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
+    L.rsc_mlpnp_set_ransac_parameters_many.argtypes = [C.POINTER(vp), C.c_int, C.c_double, C.c_int, C.c_int,
+                                                       C.c_int, C.c_float, C.c_float]
+    L.rsc_mlpnp_iterate.argtypes = [vp, C.c_int, C.POINTER(PnPResult), C.c_void_p]
+    L.rsc_mlpnp_iterate_many.argtypes = [C.POINTER(vp), C.c_int, i32p, C.POINTER(PnPResult), C.POINTER(C.c_void_p)]
+    L.rsc_mlpnp_reset.argtypes = [vp, C.c_uint32]
+    L.rsc_mlpnp_reset_many.argtypes = [C.POINTER(vp), C.c_int, u32p]
+    L.rsc_mlpnp_get_state.argtypes = [vp, i32p]
+    L.rsc_mlpnp_last_poses.argtypes = [vp, f64p, C.c_int]
+    L.rsc_mlpnp_last_samples.argtypes = [vp, i32p, C.c_int]
     L.rsc_diag_pnp_phase_stamps.argtypes = [C.POINTER(vp), C.c_int, C.c_int,
                                             np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
     _lib = L
@@ -236,6 +252,19 @@ def pnp_iterate_many(solvers, n_iterations, with_masks: bool = True):
     return [_pnp_out(res[i], masks[i][:solvers[i].n_points]) for i in range(n)]
 
 
+def mlpnp_iterate_many(solvers, n_iterations, with_masks: bool = True):
+    """rsc_mlpnp_iterate_many: iterate() of every MLPnP solver in one set of launches."""
+    L = load_library()
+    n = len(solvers)
+    hs = (C.c_void_p * n)(*[s.h.value for s in solvers])
+    its = np.ascontiguousarray(np.broadcast_to(np.asarray(n_iterations, np.int32), (n,)))
+    res = (PnPResult * n)()
+    masks = [np.zeros(max(s.n_points, 1), np.uint8) for s in solvers]
+    mp = (C.c_void_p * n)(*[(m.ctypes.data if with_masks else None) for m in masks])
+    _check(L.rsc_mlpnp_iterate_many(hs, n, its, res, mp), "mlpnp_iterate_many")
+    return [_pnp_out(res[i], masks[i][:solvers[i].n_points]) for i in range(n)]
+
+
 def _sim3_out(r: Sim3Result, mask: np.ndarray) -> dict:
     return dict(ok=bool(r.ok), no_more=bool(r.no_more), n_inliers=int(r.n_inliers), iterations=int(r.iterations),
                 R=np.array(r.R, np.float32).reshape(3, 3), t=np.array(r.t, np.float32), inliers=mask.astype(bool))
@@ -318,31 +347,92 @@ def sim3_iterate_many(solvers, n_iterations, with_masks: bool = True):
     return [_sim3_out(res[i], masks[i][:solvers[i].n1]) for i in range(n)]
 
 
+class MLPnPSolver:
+    """MLPnPsolver (MLPnPsolver.cpp) on the GPU; same constructor arrays as PnPSolver."""
+
+    def __init__(self, ctx: Context, scene, seed: int = 1):
+        L = load_library()
+        self.ctx = ctx
+        self._keep = [np.ascontiguousarray(scene.p2d, np.float32), np.ascontiguousarray(scene.p3dw, np.float32),
+                      np.ascontiguousarray(scene.sigma2, np.float32), np.ascontiguousarray(scene.kp_index, np.int32)]
+        pb = PnPProblem(int(scene.n), int(scene.n_points), self._keep[0].ctypes.data, self._keep[1].ctypes.data,
+                        self._keep[2].ctypes.data, self._keep[3].ctypes.data, float(scene.fx), float(scene.fy),
+                        float(scene.cx), float(scene.cy))
+        h = C.c_void_p()
+        _check(L.rsc_mlpnp_create(ctx.h, C.byref(pb), seed, C.byref(h)), "rsc_mlpnp_create")
+        self.h = h
+        self.n_points = int(scene.n_points)
+        self.n = int(scene.n)
+
+    def close(self):
+        if getattr(self, "h", None):
+            load_library().rsc_mlpnp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_ransac_parameters(self, probability=0.99, min_inliers=8, max_iterations=300, min_set=6, epsilon=0.4,
+                              th2=5.991):
+        _check(load_library().rsc_mlpnp_set_ransac_parameters(self.h, probability, min_inliers, max_iterations,
+                                                              min_set, epsilon, th2), "SetRansacParameters")
+
+    def iterate(self, n_iterations: int) -> dict:
+        r = PnPResult()
+        mask = np.zeros(max(self.n_points, 1), np.uint8)
+        _check(load_library().rsc_mlpnp_iterate(self.h, n_iterations, C.byref(r), mask.ctypes.data), "iterate")
+        return _pnp_out(r, mask[:self.n_points])
+
+    def reset(self, seed: int):
+        _check(load_library().rsc_mlpnp_reset(self.h, seed), "reset")
+
+    def state(self) -> dict:
+        out = np.zeros(6, np.int32)
+        _check(load_library().rsc_mlpnp_get_state(self.h, out), "get_state")
+        return dict(iterations=int(out[0]), max_iterations=int(out[1]), min_inliers=int(out[2]),
+                    best_inliers=int(out[3]), n=int(out[4]), min_set=int(out[5]))
+
+    def last_hypotheses(self, cap=4096):
+        """(samples [H, 8], double poses [H, 12]) of the last launch (parity hook)."""
+        smp = np.zeros((cap, 8), np.int32)
+        pos = np.zeros((cap, 12))
+        L = load_library()
+        n = L.rsc_mlpnp_last_samples(self.h, smp.reshape(-1), cap)
+        m = L.rsc_mlpnp_last_poses(self.h, pos.reshape(-1), cap)
+        assert n == m
+        return smp[:n], pos[:n]
+
+
 class SolverBatch:
     """A fixed list of solvers (one context) with batched reset / SetRansacParameters / iterate —
     the relocalization (PnP) or loop-closure (Sim3) candidate set of one event."""
 
     def __init__(self, solvers):
         self.solvers = list(solvers)
-        self.kind = "pnp" if isinstance(self.solvers[0], PnPSolver) else "sim3"
+        first = self.solvers[0]
+        self.kind = "pnp" if isinstance(first, PnPSolver) else ("mlpnp" if isinstance(first, MLPnPSolver) else "sim3")
         self._h = (C.c_void_p * len(self.solvers))(*[s.h.value for s in self.solvers])
 
     def reset(self, seeds):
         seeds = np.ascontiguousarray(np.asarray(seeds, np.uint32))
         L = load_library()
-        f = L.rsc_pnp_reset_many if self.kind == "pnp" else L.rsc_sim3_reset_many
+        f = {"pnp": L.rsc_pnp_reset_many, "mlpnp": L.rsc_mlpnp_reset_many, "sim3": L.rsc_sim3_reset_many}[self.kind]
         _check(f(self._h, len(self.solvers), seeds), "reset_many")
 
     def set_ransac_parameters(self, *params):
         L = load_library()
         if self.kind == "pnp":
             _check(L.rsc_pnp_set_ransac_parameters_many(self._h, len(self.solvers), *params), "params_many")
+        elif self.kind == "mlpnp":
+            _check(L.rsc_mlpnp_set_ransac_parameters_many(self._h, len(self.solvers), *params), "params_many")
         else:
             _check(L.rsc_sim3_set_ransac_parameters_many(self._h, len(self.solvers), *params), "params_many")
 
     def iterate(self, n_iterations, with_masks=False):
         if self.kind == "pnp":
             return pnp_iterate_many(self.solvers, n_iterations, with_masks)
+        if self.kind == "mlpnp":
+            return mlpnp_iterate_many(self.solvers, n_iterations, with_masks)
         return sim3_iterate_many(self.solvers, n_iterations, with_masks)
 
     def iterate_raw(self, n_iterations):
@@ -351,14 +441,14 @@ class SolverBatch:
         per-solver Python objects (the hot loop of bench.py)."""
         n = len(self.solvers)
         if not hasattr(self, "_raw"):
-            rec = PnPResult if self.kind == "pnp" else Sim3Result
+            rec = Sim3Result if self.kind == "sim3" else PnPResult
             self._raw = (rec * n)()
             self._its = np.zeros(n, np.int32)
             self._nomask = (C.c_void_p * n)()
             self._view = np.ctypeslib.as_array(self._raw)
         self._its[:] = n_iterations
         L = load_library()
-        f = L.rsc_pnp_iterate_many if self.kind == "pnp" else L.rsc_sim3_iterate_many
+        f = {"pnp": L.rsc_pnp_iterate_many, "mlpnp": L.rsc_mlpnp_iterate_many, "sim3": L.rsc_sim3_iterate_many}[self.kind]
         _check(f(self._h, n, self._its, self._raw, self._nomask), "iterate_many")
         return self._view
 

@@ -8,6 +8,7 @@
 #include <vector>
 #include "PnPsolver.hpp"
 #include "Sim3Solver.hpp"
+#include "MLPnPsolver.hpp"
 
 struct Vec3 { float v[3]; float operator()(int i) const { return v[i]; } float& operator()(int i) { return v[i]; } };
 struct Mat3 { float m[3][3]; float operator()(int r, int c) const { return m[r][c]; } float& operator()(int r, int c) { return m[r][c]; } };
@@ -40,7 +41,7 @@ int main(int argc, char** argv) {
     FILE* out = fopen(argv[2], "wb");
     if (!in || !out) return 2;
     const int mode = rd<int32_t>(in);
-    if (mode == 1) {
+    if (mode == 1 || mode == 3) {
         Frame F;
         const int n = rd<int32_t>(in);
         F.fx = rd<float>(in); F.fy = rd<float>(in); F.cx = rd<float>(in); F.cy = rd<float>(in);
@@ -60,12 +61,20 @@ int main(int argc, char** argv) {
         const int mi = rd<int32_t>(in), mx = rd<int32_t>(in), ms = rd<int32_t>(in);
         const float eps = rd<float>(in), th2 = rd<float>(in);
         const int ncalls = rd<int32_t>(in);
-        rsc_orb::PnPsolver<Frame, MapPoint> solver(F, matches, seed);
-        solver.SetRansacParameters(prob, mi, mx, ms, eps, th2);
+        std::unique_ptr<rsc_orb::PnPsolver<Frame, MapPoint>> pnp;
+        std::unique_ptr<rsc_orb::MLPnPsolver<Frame, MapPoint>> ml;
+        if (mode == 1) {
+            pnp.reset(new rsc_orb::PnPsolver<Frame, MapPoint>(F, matches, seed));
+            pnp->SetRansacParameters(prob, mi, mx, ms, eps, th2);
+        } else {
+            ml.reset(new rsc_orb::MLPnPsolver<Frame, MapPoint>(F, matches, seed));
+            ml->SetRansacParameters(prob, mi, mx, ms, eps, th2);
+        }
         for (int c = 0; c < ncalls; ++c) {
             const int its = rd<int32_t>(in);
             bool nm = false; std::vector<bool> inl; int ni = -1; Mat4 T; std::memset(&T, 0, sizeof(T));
-            bool ok = its < 0 ? solver.find(inl, ni, T) : solver.iterate(its, nm, inl, ni, T);
+            bool ok = ml ? ml->iterate(its, nm, inl, ni, T)
+                         : (its < 0 ? pnp->find(inl, ni, T) : pnp->iterate(its, nm, inl, ni, T));
             wr<int32_t>(out, ok); wr<int32_t>(out, nm); wr<int32_t>(out, ni);
             for (int a = 0; a < 4; ++a) for (int b = 0; b < 4; ++b) wr<float>(out, T.m[a][b]);
             wr<int32_t>(out, (int32_t)inl.size());

@@ -7,6 +7,7 @@
 #include "../../orb-slam2-optimized_amd/csrc/rsc_epnp.h"
 #include "../../orb-slam2-optimized_amd/csrc/rsc_sim3.h"
 #include "../../orb-slam2-optimized_amd/csrc/rsc_engine.h"
+#include "../../orb-slam2-optimized_amd/csrc/rsc_mlpnp.h"
 
 using namespace rsc;
 
@@ -274,4 +275,56 @@ void he_pnp_state(void* h, int32_t* out) {
     out[4] = t.max_rows;
 }
 
+}  // extern "C"
+
+template <int NS>
+static void mlpnp_hyp(const uint32_t* window, int g0, int h, int n, const float* pts4, const float* brg2,
+                      int32_t* idx_out, double* R, double* t) {
+    uint32_t w[31];
+    std::memcpy(w, window, sizeof(w));
+    uint32_t words[NS];
+    for (int d = 0; d < NS; ++d) words[d] = rng_word(tab().T.data(), w, g0 + h * NS + d);
+    int idx[NS];
+    swap_remove_sample<NS>(words, NS, n, idx);
+    double pw[NS][3], f[NS][3];
+    for (int i = 0; i < NS; ++i) {
+        for (int c = 0; c < 3; ++c) pw[i][c] = pts4[4 * idx[i] + c];
+        f[i][0] = brg2[2 * idx[i]];
+        f[i][1] = brg2[2 * idx[i] + 1];
+        f[i][2] = 1.0;
+        idx_out[i] = idx[i];
+    }
+    std::vector<double> slab(kMlSlabDoubles);
+    LaneMat S{slab.data(), 1};
+    double Rm[3][3], tv[3];
+    mlpnp_compute_pose<NS>(pw, f, S, Rm, tv);
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) R[3 * r + c] = Rm[r][c];
+    for (int r = 0; r < 3; ++r) t[r] = tv[r];
+}
+
+extern "C" {
+// MLPnP hypothesis h of a stream (window, g0): sample, device-path computePose (double R, t).
+int he_mlpnp_hypothesis(int ns, const uint32_t* window, int g0, int h, int n, const float* pts4, const float* brg2,
+                        int32_t* idx, double* R, double* t) {
+    switch (ns) {
+        case 6: mlpnp_hyp<6>(window, g0, h, n, pts4, brg2, idx, R, t); return 0;
+        case 7: mlpnp_hyp<7>(window, g0, h, n, pts4, brg2, idx, R, t); return 0;
+        case 8: mlpnp_hyp<8>(window, g0, h, n, pts4, brg2, idx, R, t); return 0;
+    }
+    return -1;
+}
+int he_mlpnp_count(const double* R, const double* t, const float* K, float th2, int n, const float* pts4,
+                   const float* uv2, uint8_t* mask) {
+    double Rr[9], tt[3];
+    std::memcpy(Rr, R, sizeof(Rr));
+    std::memcpy(tt, t, sizeof(tt));
+    int c = 0;
+    for (int i = 0; i < n; ++i) {
+        const bool in = mlpnp_inlier(Rr, tt, K[0], K[1], K[2], K[3], pts4[4 * i], pts4[4 * i + 1], pts4[4 * i + 2],
+                                     uv2[2 * i], uv2[2 * i + 1], pts4[4 * i + 3] * th2);
+        mask[i] = in;
+        c += in;
+    }
+    return c;
+}
 }  // extern "C"

@@ -29,6 +29,8 @@ def lib():
         L.he_pnp_count.argtypes = [f32p, f32p, f32p, C.c_float, C.c_int, f32p, f32p, u8p]
         L.he_pnp_rows.restype = C.c_double
         L.he_pnp_rows.argtypes = [C.c_int, C.c_int, f64p, f64p, f64p, f32p, f32p, f32p]
+        L.he_mlpnp_hypothesis.argtypes = [C.c_int, u32p, C.c_int, C.c_int, C.c_int, f32p, f32p, i32p, f64p, f64p]
+        L.he_mlpnp_count.argtypes = [f64p, f64p, f32p, C.c_float, C.c_int, f32p, f32p, u8p]
         L.he_sim3_hypothesis.argtypes = [u32p, C.c_int, C.c_int, C.c_int, f32p, f32p, i32p, f32p]
         L.he_sim3_count.argtypes = [f32p, f32p, f32p, C.c_int, f32p, f32p, f32p, f32p, u64p, u64p, u8p]
         _lib = L
@@ -73,6 +75,32 @@ def pnp_count(scene, R, t, th2=5.991):
     m = np.zeros(scene.n, np.uint8)
     c = lib().he_pnp_count(np.ascontiguousarray(R, np.float32).ravel(), np.ascontiguousarray(t, np.float32), K,
                            th2, scene.n, pts4, uv, m)
+    return c, m.astype(bool)
+
+
+def bearings(scene):
+    """MLPnPsolver bearing (x, y) per correspondence, float arithmetic (MLPnPsolver.cpp:32-33)."""
+    fx, fy, cx, cy = (np.float32(v) for v in (scene.fx, scene.fy, scene.cx, scene.cy))
+    p = np.asarray(scene.p2d, np.float32)
+    return np.ascontiguousarray(np.stack([(p[:, 0] - cx) / fx, (p[:, 1] - cy) / fy], 1).astype(np.float32))
+
+
+def mlpnp_hypothesis(scene, seed, h, ns=6):
+    w, g0 = window(seed)
+    pts4, _ = pack_pts(scene)
+    idx = np.zeros(8, np.int32)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    lib().he_mlpnp_hypothesis(ns, w, g0, h, scene.n, pts4, bearings(scene), idx, R, t)
+    return idx[:ns], R.reshape(3, 3), t
+
+
+def mlpnp_count(scene, R, t, th2=5.991):
+    pts4, uv = pack_pts(scene)
+    K = np.array([scene.fx, scene.fy, scene.cx, scene.cy], np.float32)
+    m = np.zeros(scene.n, np.uint8)
+    c = lib().he_mlpnp_count(np.ascontiguousarray(R, np.float64).ravel(), np.ascontiguousarray(t, np.float64), K,
+                             th2, scene.n, pts4, uv, m)
     return c, m.astype(bool)
 
 

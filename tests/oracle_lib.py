@@ -81,6 +81,23 @@ def lib():
     L.ora_sim3_run_prepared_batch.argtypes = [C.c_int, i32p, i64p, f32p, f32p, f32p, f32p, u64p, u64p, f32p, f32p,
                                               u32p, C.c_double, C.c_int, C.c_int, C.c_int, C.c_int, i32p, f32p]
     f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+    L.ora_mlpnp_create.restype = vp
+    L.ora_mlpnp_create.argtypes = [C.c_int, C.c_int, f32p, f32p, f32p, i32p, C.c_float, C.c_float, C.c_float,
+                                   C.c_float, C.c_uint32]
+    L.ora_mlpnp_destroy.argtypes = [vp]
+    L.ora_mlpnp_set_params.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
+    L.ora_mlpnp_iterate.argtypes = [vp, C.c_int, C.POINTER(C.c_int), u8p, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                    f32p]
+    L.ora_mlpnp_info.argtypes = [vp, i32p]
+    L.ora_mlpnp_compute_pose.argtypes = [vp, i32p, C.c_int, f64p, f64p]
+    L.ora_mlpnp_trace_enable.argtypes = [vp]
+    L.ora_mlpnp_trace_get.argtypes = [vp, C.c_int, i32p, f64p]
+    L.ora_mlpnp_run_batch.argtypes = [C.c_int, i32p, i64p, f32p, f32p, f32p, C.c_float, C.c_float, C.c_float,
+                                      C.c_float, u32p, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
+                                      C.c_int, C.c_int, i32p, f32p]
+    for fn in ("ora_dm_sin", "ora_dm_cos", "ora_dm_acos", "ora_dm_cbrt"):
+        getattr(L, fn).restype = C.c_double
+        getattr(L, fn).argtypes = [C.c_double]
     L.ora_sym_eig.argtypes = [C.c_int, f64p, f64p, f64p]
     L.ora_sym_eig4f.argtypes = [f32p, f32p, f32p]
     L.ora_svd_solve.argtypes = [C.c_int, f64p, f64p, f64p]
@@ -249,3 +266,53 @@ class OracleSim3:
         fl = np.zeros((cap, 12), np.float32)
         n = lib().ora_sim3_trace_get(self.h, cap, ints, fl)
         return ints[:n], fl[:n]
+
+
+class OracleMLPnP:
+    """MLPnPsolver restatement (parity unpinned, see oracle/mlpnp_oracle.h)."""
+
+    def __init__(self, scene, seed: int = 1):
+        self._keep = (np.ascontiguousarray(scene.p2d, np.float32), np.ascontiguousarray(scene.p3dw, np.float32),
+                      np.ascontiguousarray(scene.sigma2, np.float32), np.ascontiguousarray(scene.kp_index, np.int32))
+        self.n_points = int(scene.n_points)
+        self.h = lib().ora_mlpnp_create(scene.n, self.n_points, *self._keep, scene.fx, scene.fy, scene.cx,
+                                        scene.cy, seed)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ora_mlpnp_destroy(self.h)
+            self.h = None
+
+    def set_ransac_parameters(self, probability=0.99, min_inliers=8, max_iterations=300, min_set=6, epsilon=0.4,
+                              th2=5.991):
+        lib().ora_mlpnp_set_params(self.h, probability, min_inliers, max_iterations, min_set, epsilon, th2)
+
+    def iterate(self, n_iterations: int):
+        nm, ml, ni = C.c_int(), C.c_int(), C.c_int()
+        mask = np.zeros(max(self.n_points, 1), np.uint8)
+        T = np.zeros(16, np.float32)
+        ok = lib().ora_mlpnp_iterate(self.h, n_iterations, C.byref(nm), mask, C.byref(ml), C.byref(ni), T)
+        return dict(ok=bool(ok), no_more=bool(nm.value), n_inliers=ni.value,
+                    inliers=mask[:ml.value].astype(bool), T=T.reshape(4, 4), iterations=self.info()["iterations"])
+
+    def info(self):
+        out = np.zeros(4, np.int32)
+        lib().ora_mlpnp_info(self.h, out)
+        return dict(iterations=int(out[0]), max_iterations=int(out[1]), min_inliers=int(out[2]),
+                    best_inliers=int(out[3]))
+
+    def compute_pose(self, idx):
+        idx = np.ascontiguousarray(idx, np.int32)
+        R = np.zeros(9)
+        t = np.zeros(3)
+        lib().ora_mlpnp_compute_pose(self.h, idx, len(idx), R, t)
+        return R.reshape(3, 3), t
+
+    def enable_trace(self):
+        lib().ora_mlpnp_trace_enable(self.h)
+
+    def trace(self, cap=100000):
+        ints = np.zeros((cap, 9), np.int32)
+        dbl = np.zeros((cap, 12))
+        n = lib().ora_mlpnp_trace_get(self.h, cap, ints, dbl)
+        return ints[:n], dbl[:n]

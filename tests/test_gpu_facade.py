@@ -114,3 +114,48 @@ def test_sim3_facade_matches_oracle():
         assert (bool(ok), bool(nm), ni) == (r["ok"], r["no_more"], r["n_inliers"])
         assert np.array_equal(bits(R), bits(r["R"])) and np.array_equal(bits(t), bits(r["t"]))
         assert np.array_equal(mask, r["inliers"])
+
+
+def test_mlpnp_facade_matches_oracle():
+    rng = np.random.default_rng(8)
+    n_frame = 600
+    s2 = synth.level_sigma2()
+    sc = synth.make_pnp_scene(rng, 480, 0.58)
+    slots = np.sort(rng.choice(n_frame, sc.n, replace=False))
+    bad = rng.random(sc.n) < 0.05
+    octaves = np.array([int(np.where(s2 == v)[0][0]) for v in sc.sigma2])
+    buf = struct.pack("<i", 3) + struct.pack("<i4f", n_frame, sc.fx, sc.fy, sc.cx, sc.cy)
+    buf += struct.pack("<i", len(s2)) + s2.astype("<f4").tobytes()
+    present = np.zeros(n_frame, np.int32)
+    kp = np.zeros((n_frame, 2), np.float32)
+    oc = np.zeros(n_frame, np.int32)
+    X = np.zeros((n_frame, 3), np.float32)
+    present[slots] = np.where(bad, 2, 1)
+    kp[slots] = sc.p2d
+    oc[slots] = octaves
+    X[slots] = sc.p3dw
+    for i in range(n_frame):
+        buf += struct.pack("<i2fi3f", present[i], kp[i, 0], kp[i, 1], oc[i], *X[i])
+    calls = [5, 5, 5, 40]
+    buf += struct.pack("<I", 4) + struct.pack("<d", 0.99) + struct.pack("<iii", 10, 300, 6)
+    buf += struct.pack("<ff", 0.5, 5.991) + struct.pack("<i", len(calls)) + struct.pack(f"<{len(calls)}i", *calls)
+    out = run(buf)
+    keep = ~bad
+    comp = synth.PnPScene(p2d=sc.p2d[keep], p3dw=sc.p3dw[keep], sigma2=sc.sigma2[keep],
+                          kp_index=slots[keep].astype(np.int32), n_points=n_frame, R_true=sc.R_true,
+                          t_true=sc.t_true, inlier_true=sc.inlier_true[keep])
+    o = ol.OracleMLPnP(comp, 4)
+    o.set_ransac_parameters(0.99, 10, 300, 6, 0.5, 5.991)
+    off = 0
+    for c in calls:
+        ok, nm, ni = struct.unpack_from("<3i", out, off); off += 12
+        T = np.frombuffer(out, "<f4", 16, off).reshape(4, 4); off += 64
+        (ml,) = struct.unpack_from("<i", out, off); off += 4
+        mask = np.frombuffer(out, np.uint8, ml, off).astype(bool); off += ml
+        r = o.iterate(c)
+        assert (bool(ok), bool(nm), ni) == (r["ok"], r["no_more"], r["n_inliers"])
+        assert np.array_equal(bits(T), bits(r["T"]))
+        if r["ok"]:
+            assert np.array_equal(mask, r["inliers"])
+        else:
+            assert ml == 0
