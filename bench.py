@@ -43,6 +43,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-sim3", action="store_true")
     p.add_argument("--no-mlpnp", action="store_true")
+    p.add_argument("--no-events", action="store_true")
     return p.parse_args()
 
 
@@ -170,6 +171,66 @@ def run_mlpnp(engine, ctx, rng, args):
                 correspondences=4096, steps=steps)
 
 
+def run_events(engine, ctx, args, dist, rank, world):
+    """Config 5: the EuRoC-MH01-shaped event stream (150 relocalization + 20 loop events, seed-fixed
+    sizes), whole events sharded across ranks by cost (LPT), each event run with the reference's
+    iterate(5) round-robin (rsc_reloc_events / rsc_loop_events: all candidates of all local events in
+    the same launches), then ONE all-gather of the per-event winner records (RCCL over xGMI).
+    A step = reset + SetRansacParameters of every candidate + both drivers + the all-gather."""
+    from rsc import events as rev
+    evs = rev.make_event_stream()
+    mine = rev.shard_events([ev.cost for ev in evs], world)[rank]
+    groups = {"reloc": [], "loop": []}
+    for i in mine:
+        ev = evs[i]
+        cls = engine.PnPSolver if ev.kind == "reloc" else engine.Sim3Solver
+        groups[ev.kind].append((ev, [cls(ctx, x, s) for x, s in zip(rev.event_inputs(ev), ev.seeds)]))
+    drivers = []
+    for kind, params in (("reloc", rev.RELOC_PARAMS), ("loop", rev.LOOP_PARAMS)):
+        if groups[kind]:
+            eb = engine.EventBatch([g[1] for g in groups[kind]])
+            seeds = np.array([s for ev, _ in groups[kind] for s in ev.seeds], np.uint32)
+            drivers.append((eb, params, seeds, [ev.eid for ev, _ in groups[kind]]))
+    max_per_rank = max(len(p) for p in rev.shard_events([ev.cost for ev in evs], world))
+
+    def step():
+        recs, hyps = [], 0
+        for eb, params, seeds, eids in drivers:
+            eb.batch.reset(seeds)
+            eb.batch.set_ransac_parameters(*params)
+            eb.run()
+            hyps += int(eb.cand["iterations"].sum())
+            recs.append(rev.pack_events(eids, eb.per_event, eb.winner_poses()))
+        rec = np.concatenate(recs) if recs else np.zeros((0, rev.EVENT_RECORD), np.float32)
+        if dist is not None:
+            rec = rev.all_gather_events(dist, rec, max_per_rank, device="cuda")
+        return hyps, rec
+
+    for _ in range(args.warmup):
+        step()
+    barrier(dist)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    hyps = 0
+    for _ in range(args.steps):
+        h, rec = step()
+        hyps += h
+    ctx.synchronize()
+    barrier(dist)
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt, float(hyps)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        dt, hyps = float(t[0]), int(t[1])
+    n_ev = len(evs) * args.steps
+    return dict(events_per_s=n_ev / dt, ms_per_stream=1e3 * dt / args.steps, hyp_per_s=hyps / dt,
+                events=len(evs), candidates=sum(len(ev.sizes) for ev in evs),
+                resolved=int((rec[:, 1] >= 0).sum()),
+                sharding=f"{world} rank(s), LPT by N*300, RCCL all-gather of {rev.EVENT_RECORD}-float records")
+
+
 def cpu_baseline(scenes, args):
     """Oracle restatement (test infrastructure) of the same workload on ONE host core."""
     import oracle_lib as ol
@@ -219,6 +280,7 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         dt = float(mx[0])
         hyps_total = int(t[1])
+    events = None if args.no_events else run_events(engine, ctx, args, dist, rank, world)
     sim3 = mlpnp = None
     if rank == 0 and not args.no_sim3:
         sim3 = run_sim3(engine, ctx, np.random.default_rng(77), args)
@@ -262,6 +324,8 @@ def main():
     }
     if sim3 is not None:
         out["sim3"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in sim3.items()}
+    if events is not None:
+        out["events"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in events.items()}
     if mlpnp is not None:
         out["mlpnp"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in mlpnp.items()}
     if not args.no_cpu and world == 1:

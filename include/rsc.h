@@ -166,6 +166,31 @@ int rsc_mlpnp_get_state(const rsc_mlpnp* s, int32_t out[6]);
 int rsc_mlpnp_last_poses(rsc_mlpnp* s, double* out, int cap);
 int rsc_mlpnp_last_samples(rsc_mlpnp* s, int32_t* out, int cap);
 
+/* ---- Event drivers (BASELINE config 5) -----------------------------------------------------------
+ * One relocalization or loop-closure event = the candidate solvers one Tracking::Relocalization() /
+ * LoopClosing::ComputeSim3() call builds (Tracking.cpp:1207-1232, LoopClosing.cpp:238-265), stored
+ * contiguously: event e owns solvers[event_begin[e] .. event_begin[e+1]).  Every candidate of every
+ * event runs in the same launches. */
+typedef struct {
+    int32_t winner;      /* first candidate (in the reference's round-robin order) whose iterate()
+                            returns a pose, -1 if none: the pose the reference hands to
+                            PoseOptimization / SearchBySim3 first */
+    int32_t round;       /* round of iterate(5) calls in which it returns */
+    int32_t hypothesis;  /* index of the returning hypothesis in that candidate's stream */
+    int32_t n_inliers;
+} rsc_event_result;
+/* Relocalization (Tracking.cpp:1239-1262): rounds of iterate(5) over the non-discarded candidates
+ * (bNoMore discards) until a candidate returns a pose; per_candidate receives each candidate's last
+ * iterate() result (candidates after the winner in the winning round are iterated as well — the
+ * reference reaches them only if the downstream check rejects the winner, with identical results). */
+int rsc_reloc_events(rsc_pnp* const* solvers, const int32_t* event_begin, int n_events, rsc_pnp_result* per_candidate,
+                     rsc_event_result* per_event);
+/* Loop closure (LoopClosing.cpp:271-286): each candidate's stream is run to its first success or
+ * to mRansacMaxIts in one call; the winner is the lexicographically smallest (round, candidate) with
+ * round = hypothesis / 5 — identical to the reference's round-robin of iterate(5) calls. */
+int rsc_loop_events(rsc_sim3* const* solvers, const int32_t* event_begin, int n_events,
+                    rsc_sim3_result* per_candidate, rsc_event_result* per_event);
+
 /* ---- glibc rand() helpers (Thirdparty/DBoW2/DUtils/Random.cpp:33-50) -------------------------- */
 /* First n rand() outputs after srand(seed), produced with the device jump table (parity hook). */
 int rsc_rand_stream(rsc_context* ctx, uint32_t seed, int n, int32_t* out);

@@ -1247,4 +1247,90 @@ int rsc_mlpnp_last_samples(rsc_mlpnp* s, int32_t* out, int cap) {
     RSC_HIP(hipMemcpy(out, C->d_samples.p + (size_t)s->spec_out0 * 8, (size_t)n * 8 * 4, hipMemcpyDeviceToHost));
     return n;
 }
+
+// ---- Event drivers (config 5) ----
+int rsc_reloc_events(rsc_pnp* const* solvers, const int32_t* event_begin, int n_events, rsc_pnp_result* per_candidate,
+                     rsc_event_result* per_event) {
+    if (n_events <= 0) return RSC_OK;
+    if (!solvers || !event_begin || !per_candidate || !per_event) return RSC_ERR_ARG;
+    const int total = event_begin[n_events];
+    for (int e = 0; e < n_events; ++e) {
+        if (event_begin[e + 1] < event_begin[e]) return RSC_ERR_ARG;
+        per_event[e] = rsc_event_result{-1, -1, -1, 0};
+    }
+    std::vector<char> discarded(total, 0), resolved(n_events, 0);
+    std::vector<int32_t> start_it(total);
+    for (int i = 0; i < total; ++i) {
+        if (!solvers[i]) return RSC_ERR_ARG;
+        start_it[i] = solvers[i]->st.mnIterations;
+    }
+    for (int round = 0;; ++round) {
+        std::vector<rsc_pnp*> act;
+        std::vector<int> idx;
+        for (int e = 0; e < n_events; ++e) {
+            if (resolved[e]) continue;
+            for (int i = event_begin[e]; i < event_begin[e + 1]; ++i)
+                if (!discarded[i]) { act.push_back(solvers[i]); idx.push_back(i); }
+        }
+        if (act.empty()) break;
+        std::vector<int32_t> its(act.size(), 5);
+        std::vector<rsc_pnp_result> r(act.size());
+        std::vector<uint8_t*> nomask(act.size(), nullptr);
+        if (int st = rsc_pnp_iterate_many(act.data(), (int)act.size(), its.data(), r.data(), nomask.data())) return st;
+        std::vector<char> iterated(total, 0);
+        for (size_t q = 0; q < act.size(); ++q) {
+            iterated[idx[q]] = 1;
+            per_candidate[idx[q]] = r[q];
+            if (r[q].no_more) discarded[idx[q]] = 1;  // Tracking.cpp:1257-1261
+        }
+        for (int e = 0; e < n_events; ++e) {
+            if (resolved[e]) continue;
+            bool any_active = false;
+            for (int i = event_begin[e]; i < event_begin[e + 1]; ++i) {
+                if (!iterated[i]) continue;  // candidates iterated this round, in order
+                if (per_candidate[i].ok) {
+                    per_event[e].winner = i - event_begin[e];
+                    per_event[e].round = round;
+                    per_event[e].hypothesis = per_candidate[i].iterations - 1 - start_it[i];
+                    per_event[e].n_inliers = per_candidate[i].n_inliers;
+                    resolved[e] = 1;
+                    break;
+                }
+                if (!discarded[i]) any_active = true;
+            }
+            if (!resolved[e] && !any_active) resolved[e] = 1;
+        }
+    }
+    return RSC_OK;
+}
+
+int rsc_loop_events(rsc_sim3* const* solvers, const int32_t* event_begin, int n_events,
+                    rsc_sim3_result* per_candidate, rsc_event_result* per_event) {
+    if (n_events <= 0) return RSC_OK;
+    if (!solvers || !event_begin || !per_candidate || !per_event) return RSC_ERR_ARG;
+    const int total = event_begin[n_events];
+    std::vector<int32_t> its(total), start_it(total);
+    for (int i = 0; i < total; ++i) {
+        if (!solvers[i]) return RSC_ERR_ARG;
+        start_it[i] = solvers[i]->st.mnIterations;
+        its[i] = std::max(1, solvers[i]->st.mRansacMaxIts - solvers[i]->st.mnIterations);
+    }
+    std::vector<uint8_t*> nomask(total, nullptr);
+    if (total > 0)
+        if (int st = rsc_sim3_iterate_many(solvers, total, its.data(), per_candidate, nomask.data())) return st;
+    for (int e = 0; e < n_events; ++e) {
+        per_event[e] = rsc_event_result{-1, -1, -1, 0};
+        int best_round = 0;
+        for (int i = event_begin[e]; i < event_begin[e + 1]; ++i) {
+            if (!per_candidate[i].ok) continue;
+            const int h = per_candidate[i].iterations - 1 - start_it[i];
+            const int round = h / 5;
+            if (per_event[e].winner < 0 || round < best_round) {
+                best_round = round;
+                per_event[e] = rsc_event_result{i - event_begin[e], round, h, per_candidate[i].n_inliers};
+            }
+        }
+    }
+    return RSC_OK;
+}
 }  // extern "C"

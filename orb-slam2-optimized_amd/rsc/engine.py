@@ -37,7 +37,12 @@ EXPORTED = [
     "rsc_mlpnp_create", "rsc_mlpnp_destroy", "rsc_mlpnp_set_ransac_parameters",
     "rsc_mlpnp_set_ransac_parameters_many", "rsc_mlpnp_iterate", "rsc_mlpnp_iterate_many", "rsc_mlpnp_reset",
     "rsc_mlpnp_reset_many", "rsc_mlpnp_get_state", "rsc_mlpnp_last_poses", "rsc_mlpnp_last_samples",
+    "rsc_reloc_events", "rsc_loop_events",
 ]
+
+
+class EventResult(C.Structure):
+    _fields_ = [("winner", C.c_int32), ("round", C.c_int32), ("hypothesis", C.c_int32), ("n_inliers", C.c_int32)]
 
 
 class PnPProblem(C.Structure):
@@ -119,6 +124,8 @@ def load_library(path: str = LIB_PATH):
     L.rsc_mlpnp_get_state.argtypes = [vp, i32p]
     L.rsc_mlpnp_last_poses.argtypes = [vp, f64p, C.c_int]
     L.rsc_mlpnp_last_samples.argtypes = [vp, i32p, C.c_int]
+    L.rsc_reloc_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(PnPResult), C.POINTER(EventResult)]
+    L.rsc_loop_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(Sim3Result), C.POINTER(EventResult)]
     L.rsc_diag_pnp_phase_stamps.argtypes = [C.POINTER(vp), C.c_int, C.c_int,
                                             np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
     _lib = L
@@ -457,3 +464,45 @@ class SolverBatch:
         out = np.zeros(len(self.solvers) * H * 10, np.uint64)
         _check(load_library().rsc_diag_pnp_phase_stamps(self._h, len(self.solvers), H, out), "phase_stamps")
         return out.reshape(len(self.solvers), H, 10)
+
+
+class EventBatch:
+    """Config-5 style event driver: many relocalization (PnP) or loop-closure (Sim3) events, each a
+    contiguous group of candidate solvers; all candidates of all events run in the same launches
+    (rsc_reloc_events / rsc_loop_events)."""
+
+    def __init__(self, events):
+        self.events = [list(ev) for ev in events]
+        flat = [s for ev in self.events for s in ev]
+        self.kind = "sim3" if isinstance(flat[0], Sim3Solver) else "pnp"
+        self.batch = SolverBatch(flat)
+        self.begin = np.zeros(len(self.events) + 1, np.int32)
+        self.begin[1:] = np.cumsum([len(ev) for ev in self.events])
+        rec = Sim3Result if self.kind == "sim3" else PnPResult
+        self._cand = (rec * len(flat))()
+        self._ev = (EventResult * len(self.events))()
+        self.cand = np.ctypeslib.as_array(self._cand)
+        self.per_event = np.ctypeslib.as_array(self._ev)
+
+    def run(self):
+        L = load_library()
+        f = L.rsc_loop_events if self.kind == "sim3" else L.rsc_reloc_events
+        _check(f(self.batch._h, self.begin, len(self.events), self._cand, self._ev), "events")
+        return self.per_event
+
+    def winner_poses(self) -> np.ndarray:
+        """[n_events, 16] float32 pose of each event's winning candidate (PnP Tcw row-major, Sim3
+        [R|t; 0 0 0 1]); zeros for events without a winner."""
+        out = np.zeros((len(self.events), 16), np.float32)
+        for e in range(len(self.events)):
+            w = int(self.per_event["winner"][e])
+            if w < 0:
+                continue
+            r = self.cand[self.begin[e] + w]
+            if self.kind == "pnp":
+                out[e] = np.asarray(r["T"], np.float32).ravel()
+            else:
+                R = np.asarray(r["R"], np.float32).reshape(3, 3)
+                out[e, 0:3], out[e, 4:7], out[e, 8:11] = R[0], R[1], R[2]
+                out[e, 3], out[e, 7], out[e, 11], out[e, 15] = r["t"][0], r["t"][1], r["t"][2], 1.0
+        return out

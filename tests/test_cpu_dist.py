@@ -93,3 +93,54 @@ def test_gloo_world2_matches_single_process():
     single = rdist.pack_pnp(list(range(len(scenes))), _solve(range(len(scenes)), scenes))
     assert np.array_equal(allr, single)
     assert win == rdist.reloc_winner(single)
+
+
+def _events_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "orb-slam2-optimized_amd"))
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import torch.distributed as dist
+    import events_oracle as eo
+    from rsc import events as rev
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    evs = rev.make_event_stream(seed=13, n_reloc=8, n_loop=3)
+    mine = rev.shard_events([ev.cost for ev in evs], world)[rank]
+    rec = eo.run_events([evs[i] for i in mine])
+    allr = rev.all_gather_events(dist, rec, max_per_rank=len(evs))
+    if rank == 0:
+        q.put((allr, mine))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_events_partition_and_balance():
+    from rsc import events as rev
+    evs = rev.make_event_stream()
+    assert len(evs) == 170 and sum(ev.kind == "loop" for ev in evs) == 20
+    costs = [ev.cost for ev in evs]
+    for world in (1, 2, 4, 8):
+        parts = rev.shard_events(costs, world)
+        assert sorted(i for p in parts for i in p) == list(range(len(evs)))
+        loads = [sum(costs[i] for i in p) for p in parts]
+        assert max(loads) <= sum(costs) / world + max(costs)  # LPT bound
+
+
+def test_gloo_world2_events_match_single_process():
+    import events_oracle as eo
+    from rsc import events as rev
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_events_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    allr, mine = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    evs = rev.make_event_stream(seed=13, n_reloc=8, n_loop=3)
+    assert 0 < len(mine) < len(evs)
+    single = eo.run_events(evs)
+    assert np.array_equal(allr.view(np.uint32), single.view(np.uint32))
