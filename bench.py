@@ -29,6 +29,16 @@ RELOC = (0.99, 10, 300, 4, 0.5, 5.991)
 LOOP = (0.99, 20, 300)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec)
+PROFILE_DIR = "profiles/r01"
+
+
+def _profile_json(name):
+    """Committed measurement side files (op-count, PMC traffic) of this round, or None."""
+    path = os.path.join(ROOT, PROFILE_DIR, name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
 
 
 def parse():
@@ -100,7 +110,7 @@ def run_pnp(engine, ctx, scenes, args, dist, rank, world):
     for s in range(args.warmup):
         step(s)
     ctx.enable_timing(True)
-    solve_ms = scan_ms = 0.0
+    solve_ms = scan_ms = eig_ms = 0.0
     launches = 0
     barrier(dist)
     ctx.synchronize()
@@ -112,13 +122,14 @@ def run_pnp(engine, ctx, scenes, args, dist, rank, world):
         tm = ctx.last_timing()
         solve_ms += tm["solve_ms"]
         scan_ms += tm["scan_ms"]
+        eig_ms += tm["eig_ms"]
         launches += tm["solve_launches"]
     ctx.synchronize()
     barrier(dist)
     dt = time.perf_counter() - t0
     ctx.enable_timing(False)
     return dict(seconds=dt, hyps=hyps, problems=C * args.steps, solve_ms=solve_ms / max(launches, 1),
-                scan_ms=scan_ms / max(launches, 1), launches=launches, last=outs)
+                scan_ms=scan_ms / max(launches, 1), eig_ms=eig_ms / max(launches, 1), launches=launches, last=outs)
 
 
 def run_sim3(engine, ctx, rng, args):
@@ -295,9 +306,19 @@ def main():
     per_launch_hyps = args.candidates * args.iters
     B_h = 24 * args.corrs  # PnP scan bytes per hypothesis (p3D 12 + p2D 8 + maxErr 4)
     algo_bytes = per_launch_hyps * B_h
-    solve_s = r["solve_ms"] * 1e-3
-    scan_s = r["scan_ms"] * 1e-3
-    achieved = algo_bytes / (solve_s + scan_s) / 1e9 if solve_s + scan_s > 0 else 0.0
+    eig_ms, solve_ms, scan_ms = r["eig_ms"], r["solve_ms"], r["scan_ms"]
+    set_ms = solve_ms + scan_ms
+    achieved = algo_bytes / (set_ms * 1e-3) / 1e9 if set_ms > 0 else 0.0
+    opc = _profile_json("opcount.json")
+    traffic = _profile_json("pmc_traffic.json")
+    S_h = opc["fp64_flops_mean"] if opc else None
+    fp64 = None
+    if S_h and solve_ms > 0:
+        tf = per_launch_hyps * S_h / (solve_ms * 1e-3) / 1e12
+        fp64 = {"kernel": "pnp_eig_quad_kernel<4> + pnp_betas_kernel<4> (hypothesis solve)",
+                "achieved": round(tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(tf / FP64_PEAK_TFLOPS, 5), "S_h_fp64_flops_per_hypothesis": S_h,
+                "S_h_source": "tools/opcount.cpp (op-counter build of the oracle EPnP), " + PROFILE_DIR}
     out = {
         "metric": "RANSAC hypotheses/sec (EPnP relocalization batch, 2k corrs x 64 candidates per GPU)",
         "value": round(value, 1),
@@ -316,12 +337,20 @@ def main():
                    "hypotheses_per_candidate": args.iters, "params": "SetRansacParameters(0.99,10,300,4,0.5,5.991)",
                    "parallelism": f"candidates sharded, {world} rank(s), RCCL all-gather of result records"},
         "poses_per_s": round(world * r["problems"] / dt, 2),
+        # achieved = effective scan bandwidth of one EPnP launch set
+        # (C*H hypotheses x B_h algorithmic bytes) / (HIP-event time of eig + betas + scan kernels).
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                     "kernel": "pnp_solve_kernel<4> + pnp_scan_kernel<8> (per launch)",
-                     "solve_ms_per_launch": round(r["solve_ms"], 4), "scan_ms_per_launch": round(r["scan_ms"], 4),
-                     "algorithmic_bytes_per_launch": algo_bytes},
+                     "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": round(traffic["epnp_launch_set_bytes"]) if traffic else None,
+                     "kernel": "EPnP launch set: pnp_eig_quad_kernel<4> + pnp_betas_kernel<4> + pnp_scan_kernel<8>",
+                     "ms_per_launch": {"eig": round(eig_ms, 4), "betas": round(solve_ms - eig_ms, 4),
+                                       "scan": round(scan_ms, 4), "set": round(set_ms, 4)},
+                     "launches": r["launches"], "algorithmic_bytes_per_launch": algo_bytes,
+                     "traffic_source": (PROFILE_DIR + "/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE)")
+                     if traffic else None},
     }
+    if fp64 is not None:
+        out["roofline_fp64"] = fp64
     if sim3 is not None:
         out["sim3"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in sim3.items()}
     if events is not None:

@@ -48,6 +48,8 @@ int rsc_context_synchronize(rsc_context* ctx);
  * out[0] = hypothesis-solve kernels, out[1] = inlier-scan kernels, out[2] = refine kernels,
  * out[3] = number of solve launches, out[4] = hypotheses solved. */
 int rsc_context_last_timing(rsc_context* ctx, double out[5]);
+/* As above plus out[5] = eigen-stage kernel (pnp_eig_quad/lane_kernel) alone, split solve modes. */
+int rsc_context_last_kernel_timing(rsc_context* ctx, double out[6]);
 int rsc_context_enable_timing(rsc_context* ctx, int enable);
 /* Hypothesis-solve kernel family for PnP (all produce bit-identical results):
  * 0 = auto, 1 = single kernel (one lane per hypothesis), 2 = quad-cooperative eigenvectors +

@@ -361,16 +361,16 @@ void PnPOracle::estimate_R_and_t(double R[3][3], double t[3]) {
             for (int c = 0; c < 3; ++c) M[r][c] = M[r][c] + a[r] * b[c];
     }
     float N11, N12, N13, N14, N22, N23, N24, N33, N34, N44;
-    N11 = M[0][0] + M[1][1] + M[2][2];
-    N12 = M[1][2] - M[2][1];
-    N13 = M[2][0] - M[0][2];
-    N14 = M[0][1] - M[1][0];
-    N22 = M[0][0] - M[1][1] - M[2][2];
-    N23 = M[0][1] + M[1][0];
-    N24 = M[2][0] + M[0][2];
-    N33 = -M[0][0] + M[1][1] - M[2][2];
-    N34 = M[1][2] + M[2][1];
-    N44 = -M[0][0] - M[1][1] + M[2][2];
+    N11 = (float)(M[0][0] + M[1][1] + M[2][2]);
+    N12 = (float)(M[1][2] - M[2][1]);
+    N13 = (float)(M[2][0] - M[0][2]);
+    N14 = (float)(M[0][1] - M[1][0]);
+    N22 = (float)(M[0][0] - M[1][1] - M[2][2]);
+    N23 = (float)(M[0][1] + M[1][0]);
+    N24 = (float)(M[2][0] + M[0][2]);
+    N33 = (float)(-M[0][0] + M[1][1] - M[2][2]);
+    N34 = (float)(M[1][2] + M[2][1]);
+    N44 = (float)(-M[0][0] - M[1][1] + M[2][2]);
     double Nm[4][4] = {{N11, N12, N13, N14}, {N12, N22, N23, N24}, {N13, N23, N33, N34}, {N14, N24, N34, N44}};
     SymEig<double, 4> es = sym_eig<double, 4>(Nm);
     double qw = es.V[0][3], qx = -es.V[1][3], qy = -es.V[2][3], qz = -es.V[3][3];

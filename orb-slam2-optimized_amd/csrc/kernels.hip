@@ -182,14 +182,55 @@ __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------------
-// PnP Refine: one 256-thread workgroup per refining problem.
+// PnP Refine: one 256-thread workgroup (4 waves) per refining problem.
+//
+// EPnP over the n_r best inliers is a chain of left-to-right sums over the rows (arithmetic
+// contract: same association as the reference).  The per-row TERMS of every sum are independent,
+// so a wave evaluates 64 rows' terms at once into LDS and then K lanes fold the K columns in row
+// order (wave_ordered_sum); only the additions stay serial.  The three beta approximations, each
+// with its compute_R_and_t over all rows, run on waves 0..2 in parallel.
 // ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Ordered sums of K columns of per-row terms over rows [0, count), by one wave.  term(i, t[K]).
+// from_zero: s = ((0.0 + t0) + t1) + ... (loops starting from 0.0), else s = (t0 + t1) + ...
+// Returns column k's sum in lane k (k < K); buf holds 64*K doubles of this wave.
+template <int K, class Term>
+__device__ double wave_ordered_sum(int count, double* buf, bool from_zero, Term&& term) {
+    const int lane = threadIdx.x & 63;
+    double s = 0.0;
+    for (int base = 0; base < count; base += 64) {
+        const int i = base + lane;
+        if (i < count) {
+            double t[K];
+            term(i, t);
+            RSC_UNROLL for (int k = 0; k < K; ++k) buf[k * 64 + lane] = t[k];
+        }
+        wave_lds_sync();
+        if (lane < K) {
+            const int m = min(64, count - base);
+            const double* col = buf + lane * 64;
+            int r = 0;
+            if (base == 0 && !from_zero) { s = col[0]; r = 1; }
+            for (; r < m; ++r) s = s + col[r];
+        }
+        wave_lds_sync();
+    }
+    return s;
+}
+
 __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restrict__ probs,
                                                          const RefineJob* __restrict__ jobs,
                                                          int mask_words_out) {
     __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles];
+    __shared__ __attribute__((aligned(16))) double wbuf[4][64 * 9];
     __shared__ int prefix[129];
-    __shared__ double cws_sh[12];
+    __shared__ double cen_sh[3], cws_sh[12], cci_sh[9];
+    __shared__ double res_sh[3][13];  // per approximation: R[9], t[3], error
     __shared__ float pose_sh[12];
     __shared__ int cnt_sh[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -197,7 +238,12 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     const DevPnP& P = probs[J.prob];
     const int n = P.n;
     const int nwords = (n + 63) / 64;
+    double* buf = wbuf[wave];
 
+    // 0. new-best bookkeeping (PnPsolver.cpp:147-156) fused here: mvbBestInliers, mBestTcw.
+    if (J.adopt_mask)
+        for (int wd = tid; wd < nwords; wd += 256) J.adopt_mask[wd] = J.best_mask[wd];
+    if (J.adopt_pose && tid < 12) J.out_best_pose[tid] = J.adopt_pose[tid];
     // 1. compaction of the best-inlier set (PnPsolver.cpp:195-214), in index order.
     if (tid == 0) {
         int acc = 0;
@@ -225,16 +271,59 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     const int rows = J.rows_after;
     __syncthreads();
 
+    const double* __restrict__ pws = P.pws;
+    const double* __restrict__ us = P.us;
+    double* __restrict__ als = P.als;
     RowStore st{nr, rows, P.pws, P.us, P.als};
     const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
     LaneMat S{slab, 1};
-    // 2. control points + alphas (single lane, sequential sums as in the reference)
-    if (tid == 0) {
-        double cws[4][3];
-        control_points_and_alphas(st, cws);
-        RSC_UNROLL for (int i = 0; i < 4; ++i)
-            RSC_UNROLL for (int c = 0; c < 3; ++c) cws_sh[3 * i + c] = cws[i][c];
+    // 2. choose_control_points + barycentric coordinates (PnPsolver.cpp:296-343), wave 0
+    if (wave == 0) {
+        const double cs = wave_ordered_sum<3>(rows, buf, false, [&](int i, double (&t)[3]) {
+            t[0] = pws[3 * i]; t[1] = pws[3 * i + 1]; t[2] = pws[3 * i + 2];
+        });
+        if (lane < 3) cen_sh[lane] = cs / nr;
+        wave_lds_sync();
+        const double c0 = cen_sh[0], c1 = cen_sh[1], c2 = cen_sh[2];
+        // A[a][b], (a,b) in (00 01 02 11 12 22); A[b][a] is the same sum of the same products
+        const double as = wave_ordered_sum<6>(nr, buf, false, [&](int i, double (&t)[6]) {
+            const double d0 = pws[3 * i] - c0, d1 = pws[3 * i + 1] - c1, d2 = pws[3 * i + 2] - c2;
+            t[0] = d0 * d0; t[1] = d0 * d1; t[2] = d0 * d2; t[3] = d1 * d1; t[4] = d1 * d2; t[5] = d2 * d2;
+        });
+        if (lane < 6) buf[lane] = as;
+        wave_lds_sync();
+        if (lane == 0) {
+            double cws[4][3];
+            cws[0][0] = c0; cws[0][1] = c1; cws[0][2] = c2;
+            const double A[3][3] = {{buf[0], buf[1], buf[2]}, {buf[1], buf[3], buf[4]}, {buf[2], buf[4], buf[5]}};
+            double V[3][3], w[3];
+            sym_eig_reg<double, 3>(A, V, w);
+            RSC_UNROLL for (int i = 0; i < 3; ++i) {
+                double k = sqrt(w[i] / nr);
+                RSC_UNROLL for (int c = 0; c < 3; ++c) cws[i + 1][c] = cws[0][c] + k * V[c][i];
+            }
+            double CC[3][3], CCi[3][3];
+            RSC_UNROLL for (int i = 0; i < 3; ++i)
+                RSC_UNROLL for (int j = 1; j < 4; ++j) CC[i][j - 1] = cws[j][i] - cws[0][i];
+            inverse3(CC, CCi);
+            RSC_UNROLL for (int i = 0; i < 4; ++i)
+                RSC_UNROLL for (int c = 0; c < 3; ++c) cws_sh[3 * i + c] = cws[i][c];
+            RSC_UNROLL for (int i = 0; i < 3; ++i)
+                RSC_UNROLL for (int c = 0; c < 3; ++c) cci_sh[3 * i + c] = CCi[i][c];
+        }
     }
+    __syncthreads();
+    for (int i = tid; i < nr; i += 256) {
+        const double d0 = pws[3 * i] - cws_sh[0], d1 = pws[3 * i + 1] - cws_sh[1], d2 = pws[3 * i + 2] - cws_sh[2];
+        const double a1 = cci_sh[0] * d0 + cci_sh[1] * d1 + cci_sh[2] * d2;
+        const double a2 = cci_sh[3] * d0 + cci_sh[4] * d1 + cci_sh[5] * d2;
+        const double a3 = cci_sh[6] * d0 + cci_sh[7] * d1 + cci_sh[8] * d2;
+        als[4 * i + 1] = a1;
+        als[4 * i + 2] = a2;
+        als[4 * i + 3] = a3;
+        als[4 * i + 0] = 1.0 - a1 - a2 - a3;
+    }
+    __threadfence_block();
     __syncthreads();
     // 3. MtM lower triangle, one entry per thread
     if (tid < 78) {
@@ -245,18 +334,90 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
         S.at(a, b) = s;
     }
     __syncthreads();
-    // 4. eigensolver + betas + Gauss-Newton + R,t (single lane)
+    // 4. 12x12 eigenvectors, L_6x10 and rho (single lane)
     if (tid == 0) {
-        double cws[4][3];
-        RSC_UNROLL for (int i = 0; i < 4; ++i)
-            RSC_UNROLL for (int c = 0; c < 3; ++c) cws[i][c] = cws_sh[3 * i + c];
-        float R[9], t[3];
-        epnp_stage_c(st, K, S, cws, R, t);
-        RSC_UNROLL for (int k = 0; k < 9; ++k) pose_sh[k] = R[k];
-        RSC_UNROLL for (int k = 0; k < 3; ++k) pose_sh[9 + k] = t[k];
+        sym_eig12(S);
+        compute_L_6x10(SlabView{S});
+        auto d2 = [&](int a, int b) {
+            double x = cws_sh[3 * a] - cws_sh[3 * b], y = cws_sh[3 * a + 1] - cws_sh[3 * b + 1],
+                   z = cws_sh[3 * a + 2] - cws_sh[3 * b + 2];
+            return x * x + y * y + z * z;
+        };
+        const SlabView SV{S};
+        SV.rho(0) = d2(0, 1); SV.rho(1) = d2(0, 2); SV.rho(2) = d2(0, 3);
+        SV.rho(3) = d2(1, 2); SV.rho(4) = d2(1, 3); SV.rho(5) = d2(2, 3);
     }
     __syncthreads();
-    // 5. CheckInliers of the refined pose
+    // 5. beta approximation (wave + 1), Gauss-Newton, compute_R_and_t over all rows
+    if (wave < 3) {
+        const SlabView SV{S};
+        __shared__ double ccs_sh[3][12];
+        if (lane == 0) {
+            double betas[4] = {0.0, 0.0, 0.0, 0.0};
+            if (wave == 0) find_betas<1>(SV, betas);
+            else if (wave == 1) find_betas<2>(SV, betas);
+            else find_betas<3>(SV, betas);
+            gauss_newton(SV, betas);
+            double ccs[4][3];
+            ccs_with_sign(st, SV, betas, ccs);
+            RSC_UNROLL for (int i = 0; i < 4; ++i)
+                RSC_UNROLL for (int c = 0; c < 3; ++c) ccs_sh[wave][3 * i + c] = ccs[i][c];
+        }
+        wave_lds_sync();
+        double ccs[4][3];
+        RSC_UNROLL for (int i = 0; i < 4; ++i)
+            RSC_UNROLL for (int c = 0; c < 3; ++c) ccs[i][c] = ccs_sh[wave][3 * i + c];
+        const double pw0[3] = {cws_sh[0], cws_sh[1], cws_sh[2]};
+        // pc0 over all allocated rows (stale rows use their stale alphas, Q6)
+        const double ps = wave_ordered_sum<3>(rows, buf, false, [&](int i, double (&t)[3]) {
+            const double a[4] = {als[4 * i], als[4 * i + 1], als[4 * i + 2], als[4 * i + 3]};
+            RSC_UNROLL for (int c = 0; c < 3; ++c) t[c] = pcs_of(a, ccs, c);
+        });
+        __shared__ double pc0_sh[3][3];
+        if (lane < 3) pc0_sh[wave][lane] = ps / nr;
+        wave_lds_sync();
+        const double pc0[3] = {pc0_sh[wave][0], pc0_sh[wave][1], pc0_sh[wave][2]};
+        const double ms = wave_ordered_sum<9>(nr, buf, true, [&](int i, double (&t)[9]) {
+            const double al4[4] = {als[4 * i], als[4 * i + 1], als[4 * i + 2], als[4 * i + 3]};
+            double a[3], b[3];
+            RSC_UNROLL for (int c = 0; c < 3; ++c) { a[c] = pcs_of(al4, ccs, c) - pc0[c]; b[c] = pws[3 * i + c] - pw0[c]; }
+            RSC_UNROLL for (int r = 0; r < 3; ++r)
+                RSC_UNROLL for (int c = 0; c < 3; ++c) t[3 * r + c] = a[r] * b[c];
+        });
+        __shared__ double m_sh[3][9];
+        if (lane < 9) m_sh[wave][lane] = ms;
+        wave_lds_sync();
+        __shared__ double rt_sh[3][12];
+        if (lane == 0) {
+            double M[3][3], R[3][3], t[3];
+            RSC_UNROLL for (int r = 0; r < 3; ++r)
+                RSC_UNROLL for (int c = 0; c < 3; ++c) M[r][c] = m_sh[wave][3 * r + c];
+            horn_from_M(M, pc0, pw0, R, t);
+            RSC_UNROLL for (int k = 0; k < 9; ++k) rt_sh[wave][k] = R[k / 3][k % 3];
+            RSC_UNROLL for (int k = 0; k < 3; ++k) rt_sh[wave][9 + k] = t[k];
+        }
+        wave_lds_sync();
+        double R[3][3], t[3];
+        RSC_UNROLL for (int k = 0; k < 9; ++k) R[k / 3][k % 3] = rt_sh[wave][k];
+        RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = rt_sh[wave][9 + k];
+        const double es = wave_ordered_sum<1>(nr, buf, true, [&](int i, double (&tt)[1]) {
+            tt[0] = reproj_term(R, t, K, pws[3 * i], pws[3 * i + 1], pws[3 * i + 2], us[2 * i], us[2 * i + 1]);
+        });
+        if (lane == 0) {
+            RSC_UNROLL for (int k = 0; k < 12; ++k) res_sh[wave][k] = rt_sh[wave][k];
+            res_sh[wave][12] = es / nr;
+        }
+    }
+    __syncthreads();
+    // smallest reprojection error, approximations in order 1, 2, 3 (strict <, PnPsolver.cpp:405-411)
+    if (tid == 0) {
+        int b = 0;
+        if (res_sh[1][12] < res_sh[b][12]) b = 1;
+        if (res_sh[2][12] < res_sh[b][12]) b = 2;
+        RSC_UNROLL for (int k = 0; k < 12; ++k) pose_sh[k] = (float)res_sh[b][k];
+    }
+    __syncthreads();
+    // 6. CheckInliers of the refined pose
     float R[9], t[3];
     RSC_UNROLL for (int k = 0; k < 9; ++k) R[k] = pose_sh[k];
     RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = pose_sh[9 + k];
@@ -529,7 +690,10 @@ hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchPr
 
 hipError_t launch_pnp_solve_split(bool quad, int ns, int nwg16, const int2* wgt16, int nwg64, const int2* wgt64,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
-                                  float* poses, int32_t* samples, hipStream_t st) {
+                                  float* poses, int32_t* samples, hipStream_t st, hipEvent_t eig_begin,
+                                  hipEvent_t eig_end) {
+    if (ns < 4 || ns > 6) return hipErrorInvalidValue;
+    if (eig_begin) (void)hipEventRecord(eig_begin, st);
     switch (ns) {
 #define RSC_CASE(N)                                                                                   \
     case N:                                                                                           \
@@ -537,6 +701,7 @@ hipError_t launch_pnp_solve_split(bool quad, int ns, int nwg16, const int2* wgt1
             pnp_eig_quad_kernel<N><<<nwg16, 64, 0, st>>>(probs, lps, wgt16, T, stage, samples);       \
         else                                                                                          \
             pnp_eig_lane_kernel<N><<<nwg64, 64, 0, st>>>(probs, lps, wgt64, T, stage, samples);       \
+        if (eig_end) (void)hipEventRecord(eig_end, st);                                               \
         pnp_betas_kernel<N><<<nwg64, 192, 0, st>>>(probs, lps, wgt64, stage, samples, poses);         \
         break;
         RSC_CASE(4) RSC_CASE(5) RSC_CASE(6)

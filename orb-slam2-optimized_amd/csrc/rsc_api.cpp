@@ -114,8 +114,8 @@ struct rsc_context {
     int solve_mode = 0;
     // timing
     bool timing = false;
-    hipEvent_t ev[6] = {};
-    double last_ms[5] = {0, 0, 0, 0, 0};
+    hipEvent_t ev[12] = {};  // [0..5] phase marks, [6+2g], [7+2g] eigen-stage kernel of sample-size group g
+    double last_ms[6] = {0, 0, 0, 0, 0, 0};
 };
 
 struct rsc_pnp {
@@ -308,7 +308,8 @@ struct HipPnPBackend : PnPBackend {
                                                   (int)solve_wgs[g].size(),
                                                   reinterpret_cast<const int2*>(base + o_solve[g]), dprobs, dlps,
                                                   C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p,
-                                                  C->stream));
+                                                  C->stream, C->timing ? C->ev[6 + 2 * g] : nullptr,
+                                                  C->timing ? C->ev[7 + 2 * g] : nullptr));
                 } else {
                     RSC_HIP(launch_pnp_solve(4 + g, (int)solve_wgs[g].size(), dprobs, dlps,
                                              reinterpret_cast<const int2*>(base + o_solve[g]), C->d_table.p,
@@ -331,6 +332,13 @@ struct HipPnPBackend : PnPBackend {
             C->last_ms[1] += s;
             C->last_ms[3] += 1;
             C->last_ms[4] += total;
+            if (split && !diag_stamps)
+                for (int g = 0; g < 3; ++g) {
+                    if (solve_wgs[g].empty()) continue;
+                    float e = 0;
+                    (void)hipEventElapsedTime(&e, C->ev[6 + 2 * g], C->ev[7 + 2 * g]);
+                    C->last_ms[5] += e;
+                }
         }
         counts.assign(count, {});
         for (int i = 0; i < count; ++i)
@@ -338,32 +346,33 @@ struct HipPnPBackend : PnPBackend {
         return 0;
     }
 
-    int adopt_best(PnPState* s, int i, int k) override {
-        rsc_pnp* p = of(s);
-        const size_t rec = (size_t)(p->spec_out0 + k);
-        RSC_HIP(hipMemcpyAsync(p->d_best, C->d_masks.p + rec * C->mask_words, (size_t)p->words * 8,
-                               hipMemcpyDeviceToDevice, C->stream));
-        if (int e = C->h_small.ensure(12)) return e;
-        RSC_HIP(hipMemcpyAsync(C->h_small.p, C->d_poses.p + rec * 12, 48, hipMemcpyDeviceToHost, C->stream));
-        RSC_HIP(hipStreamSynchronize(C->stream));
-        pose12_to_T(C->h_small.p, s->mBestTcw);
-        (void)i;
-        return 0;
-    }
-
-    int refine(PnPState* const* S, int count, const int* rows_after, int* rcount, float (*rpose)[12]) override {
+    int refine(PnPState* const* S, int count, const int* spec_j, const int* adopt_k, const int* rows_after,
+               int* rcount, float (*rpose)[12]) override {
         std::vector<DevPnP> probs(count);
         std::vector<RefineJob> jobs(count);
-        if (int e = C->d_refine.ensure((size_t)count * 64)) return e;
+        // out: refined poses [count][12] | counts [count] | adopted best poses [count][12]
+        if (int e = C->d_refine.ensure((size_t)count * 100)) return e;
         float* d_out_pose = reinterpret_cast<float*>(C->d_refine.p);
         int32_t* d_out_cnt = reinterpret_cast<int32_t*>(C->d_refine.p + (size_t)count * 48);
+        float* d_out_best = reinterpret_cast<float*>(C->d_refine.p + (size_t)count * 52);
         int maxw = 1;
         for (int i = 0; i < count; ++i) {
             rsc_pnp* p = of(S[i]);
             probs[i] = dev_of(p);
             jobs[i].prob = i;
             jobs[i].rows_after = rows_after[i];
-            jobs[i].best_mask = p->d_best;
+            (void)spec_j;
+            if (adopt_k[i] >= 0) {
+                const size_t rec = (size_t)(p->spec_out0 + adopt_k[i]);
+                jobs[i].best_mask = C->d_masks.p + rec * C->mask_words;
+                jobs[i].adopt_mask = p->d_best;
+                jobs[i].adopt_pose = C->d_poses.p + rec * 12;
+            } else {
+                jobs[i].best_mask = p->d_best;
+                jobs[i].adopt_mask = nullptr;
+                jobs[i].adopt_pose = nullptr;
+            }
+            jobs[i].out_best_pose = d_out_best + 12 * i;
             jobs[i].out_pose = d_out_pose + 12 * i;
             jobs[i].out_count = d_out_cnt + i;
             jobs[i].out_mask = p->d_refined;
@@ -378,8 +387,8 @@ struct HipPnPBackend : PnPBackend {
         RSC_HIP(launch_pnp_refine(count, reinterpret_cast<const DevPnP*>(C->d_desc.p + o_probs),
                                   reinterpret_cast<const RefineJob*>(C->d_desc.p + o_jobs), maxw, C->stream));
         timing_begin(C, 4);
-        if (int e = C->h_small.ensure((size_t)count * 16)) return e;
-        RSC_HIP(hipMemcpyAsync(C->h_small.p, C->d_refine.p, (size_t)count * 52, hipMemcpyDeviceToHost, C->stream));
+        if (int e = C->h_small.ensure((size_t)count * 25)) return e;
+        RSC_HIP(hipMemcpyAsync(C->h_small.p, C->d_refine.p, (size_t)count * 100, hipMemcpyDeviceToHost, C->stream));
         RSC_HIP(hipStreamSynchronize(C->stream));
         if (C->timing) {
             float r = 0;
@@ -390,6 +399,7 @@ struct HipPnPBackend : PnPBackend {
         for (int i = 0; i < count; ++i) {
             rcount[i] = hc[i];
             std::memcpy(rpose[i], C->h_small.p + 12 * i, 48);
+            if (adopt_k[i] >= 0) pose12_to_T(C->h_small.p + 13 * count + 12 * i, S[i]->mBestTcw);
         }
         return 0;
     }
@@ -776,6 +786,12 @@ int rsc_context_enable_timing(rsc_context* C, int enable) {
 int rsc_context_last_timing(rsc_context* C, double out[5]) {
     if (!C || !out) return RSC_ERR_ARG;
     for (int i = 0; i < 5; ++i) out[i] = C->last_ms[i];
+    return RSC_OK;
+}
+
+int rsc_context_last_kernel_timing(rsc_context* C, double out[6]) {
+    if (!C || !out) return RSC_ERR_ARG;
+    for (int i = 0; i < 6; ++i) out[i] = C->last_ms[i];
     return RSC_OK;
 }
 

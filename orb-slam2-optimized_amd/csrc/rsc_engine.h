@@ -156,12 +156,12 @@ struct PnPBackend {
     // Speculate hypotheses [0, H[i]) for solver states[i] (from their current rng position and
     // EPnP buffer rows).  Fills counts[i][0..H[i]).
     virtual int speculate(PnPState* const* states, int count, const int* H, std::vector<std::vector<int32_t>>& counts) = 0;
-    // mvbBestInliers/mBestTcw := hypothesis k of solver i of the last speculation.
-    virtual int adopt_best(PnPState* s, int i, int k) = 0;
-    // Refine() for each listed solver: uses its best mask and max_rows; writes
-    // s->mnRefinedInliers and s->mRefinedTcw (if the caller decides success) into the out arrays.
-    virtual int refine(PnPState* const* states, int count, const int* rows_after, int* refined_count,
-                       float (*refined_pose)[12]) = 0;
+    // Refine() for each listed solver, preceded (adopt_k[q] >= 0) by the new-best bookkeeping of
+    // PnPsolver.cpp:147-156: mvbBestInliers/mBestTcw := hypothesis adopt_k[q] of speculation slot
+    // spec_j[q] (the backend writes states[q]->mBestTcw).  Uses the best mask and rows_after; writes
+    // the refined count and pose (the caller decides success) into the out arrays.
+    virtual int refine(PnPState* const* states, int count, const int* spec_j, const int* adopt_k,
+                       const int* rows_after, int* refined_count, float (*refined_pose)[12]) = 0;
     // vbInliers: scatter best (kind 2) or refined (kind 1) mask through kp_index into n_points bytes.
     virtual int fetch_mask(PnPState* const* states, int count, const int* kind, uint8_t* const* out) = 0;
     virtual ~PnPBackend() {}
@@ -217,7 +217,7 @@ inline int pnp_iterate_many(PnPBackend& be, PnPState* const* S, int count, const
             if (st) return st;
         }
         // replay, pausing at qualifying hypotheses (they need Refine)
-        std::vector<int> pause_k(spec.size(), -1);
+        std::vector<int> pause_k(spec.size(), -1), adopt_k(spec.size(), -1);
         for (size_t j = 0; j < spec.size(); ++j) {
             PnPState& s = *spec[j];
             const int i = who[j];
@@ -229,8 +229,7 @@ inline int pnp_iterate_many(PnPBackend& be, PnPState* const* S, int count, const
                 if (c >= s.mRansacMinInliers) {
                     if (c > s.mnBestInliers) {
                         s.mnBestInliers = c;
-                        int st = be.adopt_best(&s, (int)j, k);
-                        if (st) return st;
+                        adopt_k[j] = k;  // applied by the backend together with Refine()
                     }
                     pause_k[j] = k;
                     break;
@@ -239,7 +238,7 @@ inline int pnp_iterate_many(PnPBackend& be, PnPState* const* S, int count, const
         }
         // Refine() for every paused solver
         std::vector<PnPState*> rs;
-        std::vector<int> rows_after, rj;
+        std::vector<int> rows_after, rj, rk;
         for (size_t j = 0; j < spec.size(); ++j)
             if (pause_k[j] >= 0) {
                 PnPState& s = *spec[j];
@@ -248,11 +247,12 @@ inline int pnp_iterate_many(PnPBackend& be, PnPState* const* S, int count, const
                 rs.push_back(&s);
                 rows_after.push_back(ra);
                 rj.push_back((int)j);
+                rk.push_back(adopt_k[j]);
             }
         std::vector<int> rcount(rs.size());
         std::vector<float> rpose(rs.size() * 12);
         if (!rs.empty()) {
-            int st = be.refine(rs.data(), (int)rs.size(), rows_after.data(), rcount.data(),
+            int st = be.refine(rs.data(), (int)rs.size(), rj.data(), rk.data(), rows_after.data(), rcount.data(),
                                reinterpret_cast<float(*)[12]>(rpose.data()));
             if (st) return st;
         }

@@ -301,6 +301,66 @@ RSC_HD void find_betas(const SV& S, double (&betas)[4]) {
     }
 }
 
+// compute_ccs (PnPsolver.cpp:285-294) + the sign test of solve_for_sign (:445-456): pcs(0,2) of
+// the unflipped ccs decides whether every ccs is negated.
+template <class St, class SV>
+RSC_HD void ccs_with_sign(const St& st, const SV& S, const double (&betas)[4], double (&ccs)[4][3]) {
+    RSC_UNROLL for (int i = 0; i < 4; i++)
+        RSC_UNROLL for (int c = 0; c < 3; ++c) {
+            double s = 0.0;
+            RSC_UNROLL for (int j = 0; j < 4; j++) s = s + betas[j] * S.ev(3 * i + c, j);
+            ccs[i][c] = s;
+        }
+    const double pcs02 = st.al(0, 0) * ccs[0][2] + st.al(0, 1) * ccs[1][2] + st.al(0, 2) * ccs[2][2] +
+                         st.al(0, 3) * ccs[3][2];
+    if (pcs02 < 0.0) {
+        RSC_UNROLL for (int i = 0; i < 4; ++i)
+            RSC_UNROLL for (int c = 0; c < 3; ++c) ccs[i][c] = -ccs[i][c];
+    }
+}
+
+// pcs row i (compute_pcs, :296-305) from alphas a[4] and ccs.
+RSC_HD double pcs_of(const double (&a)[4], const double (&ccs)[4][3], int c) {
+    return a[0] * ccs[0][c] + a[1] * ccs[1][c] + a[2] * ccs[2][c] + a[3] * ccs[3][c];
+}
+
+// Horn step of estimate_R_and_t (:474-493) from the accumulated M: float N entries, 4x4
+// eigenvectors, conjugated quaternion, det fix, t = pc0 - R pw0.
+RSC_HD void horn_from_M(const double (&M)[3][3], const double (&pc0)[3], const double (&pw0)[3], double (&R)[3][3],
+                        double (&t)[3]) {
+    const float N11 = M[0][0] + M[1][1] + M[2][2];
+    const float N12 = M[1][2] - M[2][1];
+    const float N13 = M[2][0] - M[0][2];
+    const float N14 = M[0][1] - M[1][0];
+    const float N22 = M[0][0] - M[1][1] - M[2][2];
+    const float N23 = M[0][1] + M[1][0];
+    const float N24 = M[2][0] + M[0][2];
+    const float N33 = -M[0][0] + M[1][1] - M[2][2];
+    const float N34 = M[1][2] + M[2][1];
+    const float N44 = -M[0][0] - M[1][1] + M[2][2];
+    const double Nm[4][4] = {{N11, N12, N13, N14}, {N12, N22, N23, N24}, {N13, N23, N33, N34}, {N14, N24, N34, N44}};
+    double V[4][4], w[4];
+    sym_eig_reg<double, 4>(Nm, V, w);
+    quat_to_R<double>(V[0][3], -V[1][3], -V[2][3], -V[3][3], R);
+    if (det3(R) < 0) {
+        RSC_UNROLL for (int c = 0; c < 3; ++c) R[2][c] = -R[2][c];
+    }
+    RSC_UNROLL for (int r = 0; r < 3; ++r) t[r] = pc0[r] - (R[r][0] * pw0[0] + R[r][1] * pw0[1] + R[r][2] * pw0[2]);
+}
+
+// One term of reprojection_error (:417-431).
+RSC_HD double reproj_term(const double (&R)[3][3], const double (&t)[3], const Intrinsics& K, double P0, double P1,
+                          double P2, double u0, double u1) {
+    double X = R[0][0] * P0 + R[0][1] * P1 + R[0][2] * P2 + t[0];
+    double Y = R[1][0] * P0 + R[1][1] * P1 + R[1][2] * P2 + t[1];
+    double Z = R[2][0] * P0 + R[2][1] * P1 + R[2][2] * P2 + t[2];
+    double inv_Zc = 1.0 / Z;
+    double u = K.cx + K.fx * X * inv_Zc;
+    double v = K.cy + K.fy * Y * inv_Zc;
+    double du = u0 - u, dv = u1 - v;
+    return sqrt(du * du + dv * dv);
+}
+
 // compute_R_and_t (PnPsolver.cpp:504-515) = compute_ccs + compute_pcs + solve_for_sign +
 // estimate_R_and_t (:433-493, Horn with float N entries, conjugated quaternion) +
 // reprojection_error (:417-431).  pw0 equals the centroid cws[0] (same sum, same division).
@@ -309,19 +369,7 @@ RSC_HD double compute_R_and_t(const St& st, const Intrinsics& K, const SV& S, co
                               const double (&pw0)[3], double (&R)[3][3], double (&t)[3]) {
     const int n = st.n();
     double ccs[4][3];
-    RSC_UNROLL for (int i = 0; i < 4; i++)
-        RSC_UNROLL for (int c = 0; c < 3; ++c) {
-            double s = 0.0;
-            RSC_UNROLL for (int j = 0; j < 4; j++) s = s + betas[j] * S.ev(3 * i + c, j);
-            ccs[i][c] = s;
-        }
-    // solve_for_sign: pcs(0,2) with the unflipped ccs
-    const double pcs02 = st.al(0, 0) * ccs[0][2] + st.al(0, 1) * ccs[1][2] + st.al(0, 2) * ccs[2][2] +
-                         st.al(0, 3) * ccs[3][2];
-    if (pcs02 < 0.0) {
-        RSC_UNROLL for (int i = 0; i < 4; ++i)
-            RSC_UNROLL for (int c = 0; c < 3; ++c) ccs[i][c] = -ccs[i][c];
-    }
+    ccs_with_sign(st, S, betas, ccs);
     auto pcs = [&](int i, int c) {
         return st.al(i, 0) * ccs[0][c] + st.al(i, 1) * ccs[1][c] + st.al(i, 2) * ccs[2][c] + st.al(i, 3) * ccs[3][c];
     };
@@ -345,37 +393,10 @@ RSC_HD double compute_R_and_t(const St& st, const Intrinsics& K, const SV& S, co
         RSC_UNROLL for (int r = 0; r < 3; ++r)
             RSC_UNROLL for (int c = 0; c < 3; ++c) M[r][c] = M[r][c] + a[r] * b[c];
     }
-    const float N11 = M[0][0] + M[1][1] + M[2][2];
-    const float N12 = M[1][2] - M[2][1];
-    const float N13 = M[2][0] - M[0][2];
-    const float N14 = M[0][1] - M[1][0];
-    const float N22 = M[0][0] - M[1][1] - M[2][2];
-    const float N23 = M[0][1] + M[1][0];
-    const float N24 = M[2][0] + M[0][2];
-    const float N33 = -M[0][0] + M[1][1] - M[2][2];
-    const float N34 = M[1][2] + M[2][1];
-    const float N44 = -M[0][0] - M[1][1] + M[2][2];
-    const double Nm[4][4] = {{N11, N12, N13, N14}, {N12, N22, N23, N24}, {N13, N23, N33, N34}, {N14, N24, N34, N44}};
-    double V[4][4], w[4];
-    sym_eig_reg<double, 4>(Nm, V, w);
-    quat_to_R<double>(V[0][3], -V[1][3], -V[2][3], -V[3][3], R);
-    if (det3(R) < 0) {
-        RSC_UNROLL for (int c = 0; c < 3; ++c) R[2][c] = -R[2][c];
-    }
-    RSC_UNROLL for (int r = 0; r < 3; ++r) t[r] = pc0[r] - (R[r][0] * pw0[0] + R[r][1] * pw0[1] + R[r][2] * pw0[2]);
-    // reprojection_error
+    horn_from_M(M, pc0, pw0, R, t);
     double sum2 = 0.0;
-    RSC_UNROLL for (int i = 0; i < n; i++) {
-        const double P0 = st.pw(i, 0), P1 = st.pw(i, 1), P2 = st.pw(i, 2);
-        double X = R[0][0] * P0 + R[0][1] * P1 + R[0][2] * P2 + t[0];
-        double Y = R[1][0] * P0 + R[1][1] * P1 + R[1][2] * P2 + t[1];
-        double Z = R[2][0] * P0 + R[2][1] * P1 + R[2][2] * P2 + t[2];
-        double inv_Zc = 1.0 / Z;
-        double u = K.cx + K.fx * X * inv_Zc;
-        double v = K.cy + K.fy * Y * inv_Zc;
-        double du = st.u(i, 0) - u, dv = st.u(i, 1) - v;
-        sum2 += sqrt(du * du + dv * dv);
-    }
+    RSC_UNROLL for (int i = 0; i < n; i++)
+        sum2 += reproj_term(R, t, K, st.pw(i, 0), st.pw(i, 1), st.pw(i, 2), st.u(i, 0), st.u(i, 1));
     return sum2 / n;
 }
 

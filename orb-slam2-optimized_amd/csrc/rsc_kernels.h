@@ -51,7 +51,10 @@ struct LaunchProb {
 struct RefineJob {
     int prob;
     int rows_after;             // maximum_number_of_correspondences after set_maximum(n_r)
-    const uint64_t* best_mask;  // mvbBestInliers as bits
+    const uint64_t* best_mask;  // mvbBestInliers as bits (the adopted hypothesis' scan record, or the solver's)
+    uint64_t* adopt_mask;       // non-null: copy best_mask here (the solver's persistent mvbBestInliers)
+    const float* adopt_pose;    // non-null: hypothesis pose record (12 floats) copied to out_best_pose
+    float* out_best_pose;
     float* out_pose;            // 12 floats
     int32_t* out_count;
     uint64_t* out_mask;         // mvbRefinedInliers as bits
@@ -79,7 +82,8 @@ constexpr int kStageDoubles = 48 + 24 + 12;
 // three beta approximations (one wave each) + selection.
 hipError_t launch_pnp_solve_split(bool quad, int ns, int nwg16, const int2* wgt16, int nwg64, const int2* wgt64,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
-                                  float* poses, int32_t* samples, hipStream_t st);
+                                  float* poses, int32_t* samples, hipStream_t st, hipEvent_t eig_begin = nullptr,
+                                  hipEvent_t eig_end = nullptr);
 hipError_t launch_pnp_solve_stamped(int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                                     const uint32_t* T, float* poses, uint64_t* stamps, hipStream_t st);
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,

@@ -184,16 +184,16 @@ struct EmuPnPBackend : PnPBackend {
         }
         return 0;
     }
-    int adopt_best(PnPState* s, int i, int k) override {
-        EmuPnP* p = spec[i];
-        p->best = p->masks[k];
-        pose12_to_T(&p->poses[12 * k], s->mBestTcw);
-        return 0;
-    }
-    int refine(PnPState* const* S, int count, const int* rows_after, int* rcount, float (*rpose)[12]) override {
+    int refine(PnPState* const* S, int count, const int* spec_j, const int* adopt_k, const int* rows_after,
+               int* rcount, float (*rpose)[12]) override {
         for (int i = 0; i < count; ++i) {
             EmuPnP* p = of(S[i]);
             PnPState& s = *S[i];
+            if (adopt_k[i] >= 0) {
+                EmuPnP* q = spec[spec_j[i]];
+                p->best = q->masks[adopt_k[i]];
+                pose12_to_T(&q->poses[12 * adopt_k[i]], s.mBestTcw);
+            }
             int r = 0;
             for (int j = 0; j < s.N; ++j)
                 if ((p->best[j >> 6] >> (j & 63)) & 1ull) {
