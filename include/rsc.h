@@ -50,6 +50,9 @@ int rsc_context_synchronize(rsc_context* ctx);
 int rsc_context_last_timing(rsc_context* ctx, double out[5]);
 /* As above plus out[5] = eigen-stage kernel (pnp_eig_quad/lane_kernel) alone, split solve modes. */
 int rsc_context_last_kernel_timing(rsc_context* ctx, double out[6]);
+/* Diagnostic: host clock of the last rsc_pnp_iterate_many in microseconds from entry to
+ * [0] first launch, [1] kernels enqueued, [2] results back on the host, [3] return. */
+int rsc_diag_host_timing(rsc_context* ctx, double out[4]);
 int rsc_context_enable_timing(rsc_context* ctx, int enable);
 /* Hypothesis-solve kernel family for PnP (all produce bit-identical results):
  * 0 = auto, 1 = single kernel (one lane per hypothesis), 2 = quad-cooperative eigenvectors +

@@ -154,20 +154,34 @@ __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict_
             X[s] = 0.f; Y[s] = 0.f; Z[s] = 1.f; E[s] = -1.f; U[s] = 0.f; V[s] = 0.f;  // never an inlier
         }
     }
+    // The PPT points of a lane are independent: all ballots are taken first and the mask words
+    // are stored by lanes 0..PPT-1 in one predicated store, so the compiler can interleave the
+    // points' arithmetic (a lane-0 branch per point would serialise them).  The next pose is
+    // loaded before the current one is used.
+    const float* pp = poses + (size_t)(lp.out0 + wt.y) * 12;
+    float Rn[9], tn[3];
+    RSC_UNROLL for (int k = 0; k < 9; ++k) Rn[k] = pp[k];
+    RSC_UNROLL for (int k = 0; k < 3; ++k) tn[k] = pp[9 + k];
     for (int j = 0; j < wt.z; ++j) {
         const int h = wt.y + j;
-        const float* pp = poses + (size_t)(lp.out0 + h) * 12;
         float R[9], t[3];
-        RSC_UNROLL for (int k = 0; k < 9; ++k) R[k] = pp[k];
-        RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = pp[9 + k];
-        int cnt = 0;
-        uint64_t* mw = masks ? masks + (size_t)(lp.out0 + h) * mask_words : nullptr;
-        RSC_UNROLL for (int s = 0; s < PPT; ++s) {
-            const bool inl = pnp_inlier(R, t, fx, fy, cx, cy, X[s], Y[s], Z[s], U[s], V[s], E[s]);
-            const uint64_t b = __ballot(inl);
-            cnt += __popcll(b);
-            if (mw && lane == 0) mw[s * 4 + wave] = b;
+        RSC_UNROLL for (int k = 0; k < 9; ++k) R[k] = Rn[k];
+        RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = tn[k];
+        if (j + 1 < wt.z) {
+            pp += 12;
+            RSC_UNROLL for (int k = 0; k < 9; ++k) Rn[k] = pp[k];
+            RSC_UNROLL for (int k = 0; k < 3; ++k) tn[k] = pp[9 + k];
         }
+        uint64_t b[PPT];
+        RSC_UNROLL for (int s = 0; s < PPT; ++s)
+            b[s] = __ballot(pnp_inlier(R, t, fx, fy, cx, cy, X[s], Y[s], Z[s], U[s], V[s], E[s]));
+        int cnt = 0;
+        uint64_t mine = 0;
+        RSC_UNROLL for (int s = 0; s < PPT; ++s) {
+            cnt += __popcll(b[s]);
+            mine = (lane == s) ? b[s] : mine;
+        }
+        if (masks && lane < PPT) masks[(size_t)(lp.out0 + h) * mask_words + lane * 4 + wave] = mine;
         if (lane == 0) wave_cnt[wave][j & 63] = cnt;
         if ((j & 63) == 63 || j == wt.z - 1) {
             __syncthreads();

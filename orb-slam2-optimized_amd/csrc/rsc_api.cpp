@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -78,6 +79,14 @@ struct PinBuf {
     }
 };
 
+// Hypotheses per scan workgroup: enough workgroups for ~8 waves per SIMD (256 CUs x 4 SIMDs,
+// 4 waves per workgroup) without going below 8 hypotheses per point load.
+int scan_chunk(int total_hyps) {
+    int hc = 32;
+    while (hc > 8 && (total_hyps + hc - 1) / hc < 2048) hc >>= 1;
+    return hc;
+}
+
 int ppt_for(int n) {
     int need = (n + 255) / 256;
     int p = 1;
@@ -116,6 +125,11 @@ struct rsc_context {
     bool timing = false;
     hipEvent_t ev[12] = {};  // [0..5] phase marks, [6+2g], [7+2g] eigen-stage kernel of sample-size group g
     double last_ms[6] = {0, 0, 0, 0, 0, 0};
+    // host-side phase clock of the last PnP iterate_many (diagnostic): microseconds from entry to
+    // [0] speculation inputs built, [1] kernels enqueued, [2] counts back (sync), [3] return
+    double host_us[4] = {0, 0, 0, 0};
+    bool direct_counts = true;  // env RSC_DIRECT_COUNTS=0 restores the HBM buffer + D2H copy
+    std::chrono::steady_clock::time_point t_entry;
 };
 
 struct rsc_pnp {
@@ -196,6 +210,23 @@ int upload_blob(rsc_context* C, const Blob& b) {
     return 0;
 }
 
+// Inlier counts of a speculation round: written by the scan kernel straight into pinned host
+// memory (one fewer copy and no blit launch before the host replay), or into HBM + a D2H copy.
+int counts_target(rsc_context* C, int total, int32_t** dst) {
+    if (int e = C->h_counts.ensure((size_t)total)) return e;
+    if (C->direct_counts) {
+        *dst = C->h_counts.p;
+        return 0;
+    }
+    if (int e = C->d_counts.ensure((size_t)total)) return e;
+    *dst = C->d_counts.p;
+    return 0;
+}
+
+void host_mark(rsc_context* C, int k) {
+    C->host_us[k] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - C->t_entry).count();
+}
+
 void timing_begin(rsc_context* C, int slot) {
     if (C->timing) (void)hipEventRecord(C->ev[slot], C->stream);
 }
@@ -261,7 +292,7 @@ struct HipPnPBackend : PnPBackend {
         // work tables
         std::vector<std::vector<int2>> solve_wgs(3), quad_wgs(3);
         std::vector<int4> scan_wgs;
-        const int HC = 32;  // hypotheses per scan workgroup
+        const int HC = scan_chunk(total);  // hypotheses per scan workgroup
         const int mode = diag_stamps ? 1 : (C->solve_mode ? C->solve_mode : kAutoSolveMode);
         const bool quad = (mode == 2), split = (mode == 2 || mode == 3);
         for (int i = 0; i < count; ++i) {
@@ -281,7 +312,8 @@ struct HipPnPBackend : PnPBackend {
         const size_t o_scan = b.add(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
         if (int e = upload_blob(C, b)) return e;
         if (int e = C->d_poses.ensure((size_t)total * 12)) return e;
-        if (int e = C->d_counts.ensure((size_t)total)) return e;
+        int32_t* cnt_dst = nullptr;
+        if (int e = counts_target(C, total, &cnt_dst)) return e;
         if (int e = C->d_masks.ensure((size_t)total * mw)) return e;
         if (C->keep_samples || split)
             if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
@@ -290,6 +322,7 @@ struct HipPnPBackend : PnPBackend {
         const char* base = C->d_desc.p;
         const DevPnP* dprobs = reinterpret_cast<const DevPnP*>(base + o_probs);
         const LaunchProb* dlps = reinterpret_cast<const LaunchProb*>(base + o_lps);
+        host_mark(C, 0);
         timing_begin(C, 0);
         if (diag_stamps) {
             DevBuf<uint64_t> d;
@@ -300,16 +333,19 @@ struct HipPnPBackend : PnPBackend {
             RSC_HIP(hipMemcpyAsync(diag_stamps, d.p, (size_t)total * 80, hipMemcpyDeviceToHost, C->stream));
             RSC_HIP(hipStreamSynchronize(C->stream));
         } else {
+            bool first_group = true;
             for (int g = 0; g < 3; ++g) {
                 if (solve_wgs[g].empty()) continue;
                 if (split) {
+                    // the first group's eigen stage starts at ev[0]: no extra event in the queue
+                    hipEvent_t eb = (C->timing && !first_group) ? C->ev[6 + 2 * g] : nullptr;
                     RSC_HIP(launch_pnp_solve_split(quad, 4 + g, (int)quad_wgs[g].size(),
                                                   reinterpret_cast<const int2*>(base + o_quad[g]),
                                                   (int)solve_wgs[g].size(),
                                                   reinterpret_cast<const int2*>(base + o_solve[g]), dprobs, dlps,
                                                   C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p,
-                                                  C->stream, C->timing ? C->ev[6 + 2 * g] : nullptr,
-                                                  C->timing ? C->ev[7 + 2 * g] : nullptr));
+                                                  C->stream, eb, C->timing ? C->ev[7 + 2 * g] : nullptr));
+                    first_group = false;
                 } else {
                     RSC_HIP(launch_pnp_solve(4 + g, (int)solve_wgs[g].size(), dprobs, dlps,
                                              reinterpret_cast<const int2*>(base + o_solve[g]), C->d_table.p,
@@ -319,11 +355,13 @@ struct HipPnPBackend : PnPBackend {
         }
         timing_begin(C, 1);
         RSC_HIP(launch_pnp_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
-                                C->d_poses.p, C->d_counts.p, C->d_masks.p, mw, C->stream));
+                                C->d_poses.p, cnt_dst, C->d_masks.p, mw, C->stream));
         timing_begin(C, 2);
-        if (int e = C->h_counts.ensure(total)) return e;
-        RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
+        if (!C->direct_counts)
+            RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
+        host_mark(C, 1);
         RSC_HIP(hipStreamSynchronize(C->stream));
+        host_mark(C, 2);
         if (C->timing) {
             float a = 0, s = 0;
             (void)hipEventElapsedTime(&a, C->ev[0], C->ev[1]);
@@ -332,13 +370,16 @@ struct HipPnPBackend : PnPBackend {
             C->last_ms[1] += s;
             C->last_ms[3] += 1;
             C->last_ms[4] += total;
-            if (split && !diag_stamps)
+            if (split && !diag_stamps) {
+                bool first_group = true;
                 for (int g = 0; g < 3; ++g) {
                     if (solve_wgs[g].empty()) continue;
                     float e = 0;
-                    (void)hipEventElapsedTime(&e, C->ev[6 + 2 * g], C->ev[7 + 2 * g]);
+                    (void)hipEventElapsedTime(&e, first_group ? C->ev[0] : C->ev[6 + 2 * g], C->ev[7 + 2 * g]);
                     C->last_ms[5] += e;
+                    first_group = false;
                 }
+            }
         }
         counts.assign(count, {});
         for (int i = 0; i < count; ++i)
@@ -480,7 +521,8 @@ struct HipSim3Backend : Sim3Backend {
         const size_t o_scan = b.add(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
         if (int e = upload_blob(C, b)) return e;
         if (int e = C->d_poses.ensure((size_t)total * 24)) return e;
-        if (int e = C->d_counts.ensure((size_t)total)) return e;
+        int32_t* cnt_dst = nullptr;
+        if (int e = counts_target(C, total, &cnt_dst)) return e;
         if (int e = C->d_masks.ensure((size_t)total * mw)) return e;
         if (C->keep_samples)
             if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
@@ -492,10 +534,10 @@ struct HipSim3Backend : Sim3Backend {
                                   C->d_table.p, C->d_poses.p, C->keep_samples ? C->d_samples.p : nullptr, C->stream));
         timing_begin(C, 1);
         RSC_HIP(launch_sim3_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
-                                 C->d_poses.p, C->d_counts.p, C->d_masks.p, mw, C->stream));
+                                 C->d_poses.p, cnt_dst, C->d_masks.p, mw, C->stream));
         timing_begin(C, 2);
-        if (int e = C->h_counts.ensure(total)) return e;
-        RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
+        if (!C->direct_counts)
+            RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
         RSC_HIP(hipStreamSynchronize(C->stream));
         if (C->timing) {
             float a = 0, s = 0;
@@ -609,7 +651,8 @@ struct HipMLBackend : MLBackend {
         const size_t o_scan = b.add(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
         if (int e = upload_blob(C, b)) return e;
         if (int e = C->d_mposes.ensure((size_t)total * 12)) return e;
-        if (int e = C->d_counts.ensure((size_t)total)) return e;
+        int32_t* cnt_dst = nullptr;
+        if (int e = counts_target(C, total, &cnt_dst)) return e;
         if (int e = C->d_masks.ensure((size_t)total * mw)) return e;
         if (C->keep_samples)
             if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
@@ -625,10 +668,10 @@ struct HipMLBackend : MLBackend {
         }
         timing_begin(C, 1);
         RSC_HIP(launch_mlpnp_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
-                                  C->d_mposes.p, C->d_counts.p, C->d_masks.p, mw, C->stream));
+                                  C->d_mposes.p, cnt_dst, C->d_masks.p, mw, C->stream));
         timing_begin(C, 2);
-        if (int e = C->h_counts.ensure(total)) return e;
-        RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
+        if (!C->direct_counts)
+            RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
         RSC_HIP(hipStreamSynchronize(C->stream));
         if (C->timing) {
             float a = 0, sc = 0;
@@ -738,6 +781,7 @@ int rsc_context_create(int device, rsc_context** out) {
         else if (!std::strcmp(m, "quad")) C->solve_mode = 2;
         else if (!std::strcmp(m, "split")) C->solve_mode = 3;
     }
+    if (const char* m = std::getenv("RSC_DIRECT_COUNTS")) C->direct_counts = std::strcmp(m, "0") != 0;
     C->table.build();
     if (int e = C->d_table.ensure(C->table.T.size())) return e;
     RSC_HIP(hipMemcpy(C->d_table.p, C->table.T.data(), C->table.T.size() * 4, hipMemcpyHostToDevice));
@@ -857,6 +901,7 @@ int rsc_pnp_iterate_many(rsc_pnp* const* solvers, int count, const int32_t* n_it
     rsc_context* C = solvers[0]->ctx;
     for (int i = 0; i < count; ++i)
         if (!solvers[i] || solvers[i]->ctx != C) return RSC_ERR_ARG;
+    C->t_entry = std::chrono::steady_clock::now();
     RSC_HIP(hipSetDevice(C->device));
     for (double& v : C->last_ms) v = 0;
     HipPnPBackend be(C);
@@ -868,6 +913,13 @@ int rsc_pnp_iterate_many(rsc_pnp* const* solvers, int count, const int32_t* n_it
     int st = pnp_iterate_many(be, S.data(), count, its.data(), res.data(), inliers);
     if (st) return st;
     for (int i = 0; i < count; ++i) to_result(res[i], &out[i]);
+    host_mark(C, 3);
+    return RSC_OK;
+}
+
+int rsc_diag_host_timing(rsc_context* C, double out[4]) {
+    if (!C || !out) return RSC_ERR_ARG;
+    for (int i = 0; i < 4; ++i) out[i] = C->host_us[i];
     return RSC_OK;
 }
 

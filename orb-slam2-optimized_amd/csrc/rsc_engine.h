@@ -221,19 +221,22 @@ inline int pnp_iterate_many(PnPBackend& be, PnPState* const* S, int count, const
         for (size_t j = 0; j < spec.size(); ++j) {
             PnPState& s = *spec[j];
             const int i = who[j];
-            for (int k = 0; k < H[j]; ++k) {
-                ncur[i]++;
-                s.mnIterations++;
-                s.rng.g += s.mRansacMinSet;
-                const int c = counts[j][k];
-                if (c >= s.mRansacMinInliers) {
-                    if (c > s.mnBestInliers) {
-                        s.mnBestInliers = c;
-                        adopt_k[j] = k;  // applied by the backend together with Refine()
-                    }
-                    pause_k[j] = k;
-                    break;
+            // hypotheses [0, k) are below minInliers: they only advance the counters
+            const int32_t* cj = counts[j].data();
+            const int hj = H[j], mi = s.mRansacMinInliers;
+            int k = 0;
+            while (k < hj && cj[k] < mi) ++k;
+            const int ran = (k < hj) ? k + 1 : hj;
+            ncur[i] += ran;
+            s.mnIterations += ran;
+            s.rng.g += ran * s.mRansacMinSet;
+            if (k < hj) {
+                const int c = cj[k];
+                if (c > s.mnBestInliers) {
+                    s.mnBestInliers = c;
+                    adopt_k[j] = k;  // applied by the backend together with Refine()
                 }
+                pause_k[j] = k;
             }
         }
         // Refine() for every paused solver
@@ -395,20 +398,25 @@ inline int sim3_iterate_many(Sim3Backend& be, Sim3State* const* S, int count, co
         Sim3State& s = *spec[j];
         const int i = who[j];
         int best_k = -1;
-        for (int k = 0; k < H[j]; ++k) {
-            s.mnIterations++;
-            s.rng.g += 3;
-            const int c = counts[j][k];
-            if (c >= s.mnBestInliers) {
-                s.mnBestInliers = c;
+        const int32_t* cj = counts[j].data();
+        const int hj = H[j], mi_ = s.mRansacMinInliers;
+        int best = s.mnBestInliers, k = 0;
+        for (; k < hj; ++k) {
+            const int c = cj[k];
+            if (c >= best) {
+                best = c;
                 best_k = k;
-                if (c > s.mRansacMinInliers) {
-                    res[i].ok = 1;
-                    res[i].n_inliers = c;
-                    res[i].mask_k = k;
-                    break;
-                }
+                if (c > mi_) break;
             }
+        }
+        const int ran = (k < hj) ? k + 1 : hj;
+        s.mnIterations += ran;
+        s.rng.g += 3 * ran;
+        s.mnBestInliers = best;
+        if (k < hj) {
+            res[i].ok = 1;
+            res[i].n_inliers = cj[k];
+            res[i].mask_k = k;
         }
         if (best_k >= 0) {
             pj.push_back((int)j);

@@ -27,7 +27,7 @@ u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
 # Every symbol declared in include/rsc.h (checked by tests/test_cpu_abi.py).
 EXPORTED = [
     "rsc_version", "rsc_status_string", "rsc_context_create", "rsc_context_destroy", "rsc_context_set_stream",
-    "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_last_kernel_timing", "rsc_context_enable_timing", "rsc_context_set_solve_mode",
+    "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_last_kernel_timing", "rsc_diag_host_timing", "rsc_context_enable_timing", "rsc_context_set_solve_mode",
     "rsc_pnp_create", "rsc_pnp_destroy", "rsc_pnp_set_ransac_parameters", "rsc_pnp_iterate", "rsc_pnp_find",
     "rsc_pnp_iterate_many", "rsc_pnp_reset", "rsc_pnp_get_state", "rsc_pnp_last_samples",
     "rsc_sim3_create", "rsc_sim3_destroy", "rsc_sim3_set_ransac_parameters", "rsc_sim3_iterate", "rsc_sim3_find",
@@ -85,6 +85,7 @@ def load_library(path: str = LIB_PATH):
     L.rsc_context_synchronize.argtypes = [vp]
     L.rsc_context_last_timing.argtypes = [vp, C.POINTER(C.c_double)]
     L.rsc_context_last_kernel_timing.argtypes = [vp, C.POINTER(C.c_double)]
+    L.rsc_diag_host_timing.argtypes = [vp, C.POINTER(C.c_double)]
     L.rsc_context_enable_timing.argtypes = [vp, C.c_int]
     L.rsc_context_set_solve_mode.argtypes = [vp, C.c_int]
     L.rsc_pnp_create.argtypes = [vp, C.POINTER(PnPProblem), C.c_uint32, C.POINTER(vp)]
@@ -176,6 +177,12 @@ class Context:
         _check(load_library().rsc_context_last_kernel_timing(self.h, out), "last_timing")
         return dict(solve_ms=out[0], scan_ms=out[1], refine_ms=out[2], solve_launches=int(out[3]),
                     hypotheses=int(out[4]), eig_ms=out[5])
+
+    def host_timing(self):
+        """Diagnostic host clock (us) of the last PnP iterate_many: first launch, enqueued, synced, return."""
+        out = (C.c_double * 4)()
+        _check(load_library().rsc_diag_host_timing(self.h, out), "host_timing")
+        return list(out)
 
     def rand_stream(self, seed: int, n: int) -> np.ndarray:
         out = np.zeros(n, np.int32)
