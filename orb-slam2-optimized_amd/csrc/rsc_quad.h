@@ -350,13 +350,15 @@ __device__ __forceinline__ void pnp_eig_lane_body(const DevPnP* __restrict__ pro
 
 // Kernel 2: 192 threads = 3 waves over the same 64 hypotheses; wave w runs find_betas_approx_{w+1}
 // + gauss_newton + compute_R_and_t (PnPsolver.cpp:383-408), wave 0 keeps the smallest error in the
-// reference's order (:393-414) and writes the float pose.
-template <int NS>
+// reference's order (:393-414) and writes the float pose.  FORCE >= 0 (diagnostics only,
+// tools/quad_bench) makes every wave run approximation FORCE + 1.
+template <int NS, int FORCE = -1>
 __device__ __forceinline__ void pnp_betas_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
                                                const int2* __restrict__ wg_table, const double* __restrict__ stage,
                                                const int32_t* __restrict__ samples, float* __restrict__ poses,
                                                double* smem) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int apx = FORCE >= 0 ? FORCE : wave;
     const int2 wt = wg_table[blockIdx.x];
     const LaunchProb& lp = lps[wt.x];
     const bool active = wt.y + lane < lp.H;
@@ -398,8 +400,8 @@ __device__ __forceinline__ void pnp_betas_body(const DevPnP* __restrict__ probs,
     st.sal = P.als;
     const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
     double betas[4] = {0.0, 0.0, 0.0, 0.0};
-    if (wave == 0) find_betas<1>(V, betas);
-    else if (wave == 1) find_betas<2>(V, betas);
+    if (apx == 0) find_betas<1>(V, betas);
+    else if (apx == 1) find_betas<2>(V, betas);
     else find_betas<3>(V, betas);
     gauss_newton(V, betas);
     const double pw0[3] = {cws[0][0], cws[0][1], cws[0][2]};

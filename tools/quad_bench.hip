@@ -135,10 +135,11 @@ __global__ __launch_bounds__(64) void pb4(const float4* __restrict__ pts, const 
     RSC_UNROLL for (int e = 0; e < 144; ++e) acc += S(e);
     out[(size_t)h * kStageDoubles] = acc;
 }
+template <int FORCE = -1>
 __global__ __launch_bounds__(192, 2) void betas_k(const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                                                const double* stage, const int32_t* samples, float* poses) {
     __shared__ __attribute__((aligned(16))) double smem[kBetasSmemDoubles];
-    pnp_betas_body<4>(probs, lps, wgt, stage, samples, poses, smem);
+    pnp_betas_body<4, FORCE>(probs, lps, wgt, stage, samples, poses, smem);
 }
 
 int main(int argc, char** argv) {
@@ -260,5 +261,8 @@ int main(int argc, char** argv) {
         printf("pb4 variant %d         %8.1f us\n", v, us);
     }
     printf("betas                 %8.1f us\n", timeit([&] { betas_k<<<n64, 192>>>(dprobs, dlps, dw64, dst, dsm, dpo); }));
+    printf("betas all approx1     %8.1f us\n", timeit([&] { betas_k<0><<<n64, 192>>>(dprobs, dlps, dw64, dst, dsm, dpo); }));
+    printf("betas all approx2     %8.1f us\n", timeit([&] { betas_k<1><<<n64, 192>>>(dprobs, dlps, dw64, dst, dsm, dpo); }));
+    printf("betas all approx3     %8.1f us\n", timeit([&] { betas_k<2><<<n64, 192>>>(dprobs, dlps, dw64, dst, dsm, dpo); }));
     return 0;
 }
