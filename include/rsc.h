@@ -196,6 +196,39 @@ int rsc_reloc_events(rsc_pnp* const* solvers, const int32_t* event_begin, int n_
 int rsc_loop_events(rsc_sim3* const* solvers, const int32_t* event_begin, int n_events,
                     rsc_sim3_result* per_candidate, rsc_event_result* per_event);
 
+/* ---- Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) ------------------------------------
+ * The pose-only g2o optimisation every tracking step and Tracking::Relocalization()
+ * (Tracking.cpp:1284,1300,1315) run on the RANSAC pose: Levenberg-Marquardt of one VertexSE3Expmap
+ * over EdgeSE3ProjectXYZOnlyPose edges with a Huber kernel (delta = sqrt(5.991)), 4 rounds of 10
+ * iterations, each restarted from the entry pose, with chi2 > 5.991 outlier re-classification.
+ * Monocular edges only (mvuRight < 0, Optimizer.cpp:252); stereo slots -> RSC_ERR_UNSUPPORTED.
+ * Parity against the reference is unpinned (g2o/Eigen cannot be built here). */
+typedef struct {
+    int32_t n;                /* pFrame->N keypoint slots */
+    const uint8_t* has_mp;    /* [n] mvpMapPoints[i] != NULL (an edge is built); NULL = every slot */
+    const float* uv;          /* [n][2] mvKeysUn[i].pt */
+    const float* Xw;          /* [n][3] MapPoint::GetWorldPos() */
+    const float* inv_sigma2;  /* [n] mvInvLevelSigma2[kpUn.octave] (information = I * invSigma2) */
+    const float* u_right;     /* [n] mvuRight, or NULL for a monocular Frame */
+    float fx, fy, cx, cy;     /* Frame::fx,fy,cx,cy */
+    float Tcw[16];            /* row-major pFrame->mTcw on entry */
+} rsc_poseopt_problem;
+
+typedef struct {
+    int32_t n_good;        /* return value: nInitialCorrespondences - nBad (0 if < 3 edges) */
+    int32_t n_initial;     /* nInitialCorrespondences */
+    int32_t rounds;        /* outer rounds run (breaks after one when fewer than 10 edges) */
+    int32_t lm_iterations; /* OptimizationAlgorithmLevenberg::solve calls */
+    int32_t lm_trials;     /* linear solves (Levenberg trials) */
+    float Tcw[16];         /* row-major pose after the call (pFrame->SetPose, Optimizer.cpp:420-421);
+                              the entry pose when fewer than 3 edges (the reference returns early) */
+} rsc_poseopt_result;
+
+/* Optimizer::PoseOptimization on `count` Frames in one launch (one workgroup per Frame).
+ * outlier[c] receives mvbOutlier for the slots with a map point (others untouched); may be NULL. */
+int rsc_pose_optimization_many(rsc_context* ctx, const rsc_poseopt_problem* problems, int count,
+                               rsc_poseopt_result* out, uint8_t* const* outlier);
+
 /* ---- glibc rand() helpers (Thirdparty/DBoW2/DUtils/Random.cpp:33-50) -------------------------- */
 /* First n rand() outputs after srand(seed), produced with the device jump table (parity hook). */
 int rsc_rand_stream(rsc_context* ctx, uint32_t seed, int n, int32_t* out);

@@ -1,0 +1,517 @@
+// TEST INFRASTRUCTURE — parity oracle, never linked into the product library.
+// Sequential restatement of Optimizer::PoseOptimization + the g2o code it runs (see header).
+#include "poseopt_oracle.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <limits>
+#include <utility>
+#include <vector>
+#include "../orb-slam2-optimized_amd/csrc/rsc_math.h"
+
+namespace rsc_oracle {
+namespace {
+
+// ---- Eigen::Quaterniond / g2o::SE3Quat (types/se3quat.h) ---------------------------------------
+struct Quat {
+    double x, y, z, w;  // Eigen coefficient order
+};
+struct SE3 {
+    Quat r;
+    double t[3];
+};
+
+// Quaterniond(const Matrix3d&) — Eigen quaternionbase_assign_impl<Matrix3>.
+Quat quat_from_R(const double m[3][3]) {
+    Quat q;
+    double c[3];
+    double t = m[0][0] + m[1][1] + m[2][2];
+    if (t > 0.0) {
+        t = std::sqrt(t + 1.0);
+        q.w = 0.5 * t;
+        t = 0.5 / t;
+        q.x = (m[2][1] - m[1][2]) * t;
+        q.y = (m[0][2] - m[2][0]) * t;
+        q.z = (m[1][0] - m[0][1]) * t;
+        return q;
+    }
+    int i = 0;
+    if (m[1][1] > m[0][0]) i = 1;
+    if (m[2][2] > m[i][i]) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = std::sqrt(m[i][i] - m[j][j] - m[k][k] + 1.0);
+    c[i] = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (m[k][j] - m[j][k]) * t;
+    c[j] = (m[j][i] + m[i][j]) * t;
+    c[k] = (m[k][i] + m[i][k]) * t;
+    q.x = c[0];
+    q.y = c[1];
+    q.z = c[2];
+    return q;
+}
+
+// QuaternionBase::toRotationMatrix.
+void quat_to_R(const Quat& q, double R[3][3]) {
+    const double tx = 2.0 * q.x, ty = 2.0 * q.y, tz = 2.0 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    R[0][0] = 1.0 - (tyy + tzz); R[0][1] = txy - twz;         R[0][2] = txz + twy;
+    R[1][0] = txy + twz;         R[1][1] = 1.0 - (txx + tzz); R[1][2] = tyz - twx;
+    R[2][0] = txz - twy;         R[2][1] = tyz + twx;         R[2][2] = 1.0 - (txx + tyy);
+}
+
+// Generic quat_product (Eigen Geometry/Quaternion.h).
+Quat quat_mul(const Quat& a, const Quat& b) {
+    Quat r;
+    r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+    r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+    r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+    r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+    return r;
+}
+
+void cross(const double a[3], const double b[3], double o[3]) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// Quaternion * Vector3 (QuaternionBase::_transformVector).
+void quat_rotate(const Quat& q, const double v[3], double o[3]) {
+    const double qv[3] = {q.x, q.y, q.z};
+    double uv[3], c[3];
+    cross(qv, v, uv);
+    for (int i = 0; i < 3; ++i) uv[i] = uv[i] + uv[i];
+    cross(qv, uv, c);
+    for (int i = 0; i < 3; ++i) o[i] = v[i] + q.w * uv[i] + c[i];
+}
+
+// SE3Quat::normalizeRotation: w >= 0, then Quaternion::normalize (coeffs /= sqrt(squaredNorm)).
+void normalize_rotation(Quat& q) {
+    if (q.w < 0.0) { q.x *= -1.0; q.y *= -1.0; q.z *= -1.0; q.w *= -1.0; }
+    const double z = q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
+    if (z > 0.0) {
+        const double s = std::sqrt(z);
+        q.x /= s; q.y /= s; q.z /= s; q.w /= s;
+    }
+}
+
+SE3 se3_from_Rt(const double R[3][3], const double t[3]) {
+    SE3 s;
+    s.r = quat_from_R(R);
+    for (int i = 0; i < 3; ++i) s.t[i] = t[i];
+    normalize_rotation(s.r);
+    return s;
+}
+
+// SE3Quat::operator*(const SE3Quat&).
+SE3 se3_mul(const SE3& a, const SE3& b) {
+    SE3 r = a;
+    double rb[3];
+    quat_rotate(a.r, b.t, rb);
+    for (int i = 0; i < 3; ++i) r.t[i] = r.t[i] + rb[i];
+    r.r = quat_mul(a.r, b.r);
+    normalize_rotation(r.r);
+    return r;
+}
+
+// SE3Quat::map.
+void se3_map(const SE3& s, const double p[3], double o[3]) {
+    double rp[3];
+    quat_rotate(s.r, p, rp);
+    for (int i = 0; i < 3; ++i) o[i] = rp[i] + s.t[i];
+}
+
+// pow(x, 3) restated as the correctly rounded cube (a double-double product).
+double cube(double x) {
+    const double p = x * x;
+    const double e1 = std::fma(x, x, -p);
+    const double c = p * x;
+    const double e2 = std::fma(p, x, -c);
+    return c + (e2 + e1 * x);
+}
+
+void mat3_mul(const double A[3][3], const double B[3][3], double C[3][3]) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) C[i][j] = A[i][0] * B[0][j] + A[i][1] * B[1][j] + A[i][2] * B[2][j];
+}
+
+// SE3Quat::exp (se3quat.h): update = (omega, upsilon).
+SE3 se3_exp(const double u[6]) {
+    const double omega[3] = {u[0], u[1], u[2]};
+    const double ups[3] = {u[3], u[4], u[5]};
+    const double theta = std::sqrt(omega[0] * omega[0] + omega[1] * omega[1] + omega[2] * omega[2]);
+    double Om[3][3] = {{0.0, -omega[2], omega[1]}, {omega[2], 0.0, -omega[0]}, {-omega[1], omega[0], 0.0}};
+    double Om2[3][3], R[3][3], V[3][3];
+    mat3_mul(Om, Om, Om2);
+    if (theta < 0.00001) {
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) R[i][j] = ((i == j ? 1.0 : 0.0) + Om[i][j]) + Om2[i][j];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) V[i][j] = R[i][j];
+    } else {
+        const double st = rsc::dm::sin(theta), ct = rsc::dm::cos(theta);
+        const double a = st / theta;
+        const double b = (1.0 - ct) / (theta * theta);
+        const double c = (theta - st) / cube(theta);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                const double I = (i == j) ? 1.0 : 0.0;
+                R[i][j] = (I + a * Om[i][j]) + b * Om2[i][j];
+                V[i][j] = (I + b * Om[i][j]) + c * Om2[i][j];
+            }
+    }
+    double t[3];
+    for (int i = 0; i < 3; ++i) t[i] = V[i][0] * ups[0] + V[i][1] * ups[1] + V[i][2] * ups[2];
+    return se3_from_Rt(R, t);
+}
+
+// ---- Eigen::LDLT<MatrixXd> (lower triangle) with isPositive(), 6x6 --------------------------------
+// ldlt_inplace<Lower>::unblocked (Eigen/src/Cholesky/LDLT.h) + LDLT::_solve_impl.
+bool ldlt_solve6(double A[6][6], const double b[6], double x[6]) {
+    const int n = 6;
+    enum { Zero, Pos, Neg, Indef } sign = Zero;
+    int tr[6];
+    double temp[6];
+    for (int k = 0; k < n; ++k) {
+        int big = k;
+        double bv = std::fabs(A[k][k]);
+        for (int i = k + 1; i < n; ++i)
+            if (std::fabs(A[i][i]) > bv) { bv = std::fabs(A[i][i]); big = i; }
+        tr[k] = big;
+        if (k != big) {
+            for (int j = 0; j < k; ++j) std::swap(A[k][j], A[big][j]);
+            for (int i = big + 1; i < n; ++i) std::swap(A[i][k], A[i][big]);
+            std::swap(A[k][k], A[big][big]);
+            for (int i = k + 1; i < big; ++i) {
+                const double t = A[i][k];
+                A[i][k] = A[big][i];
+                A[big][i] = t;
+            }
+        }
+        const int rs = n - k - 1;
+        if (k > 0) {
+            for (int j = 0; j < k; ++j) temp[j] = A[j][j] * A[k][j];
+            double acc = A[k][0] * temp[0];
+            for (int j = 1; j < k; ++j) acc = acc + A[k][j] * temp[j];
+            A[k][k] -= acc;
+            for (int r = k + 1; r < n; ++r) {
+                double a = A[r][0] * temp[0];
+                for (int j = 1; j < k; ++j) a = a + A[r][j] * temp[j];
+                A[r][k] -= a;
+            }
+        }
+        const double akk = A[k][k];
+        const bool valid = std::fabs(akk) > 0.0;
+        if (k == 0 && !valid) {
+            sign = Zero;
+            for (int j = 0; j < n; ++j) tr[j] = j;
+            break;
+        }
+        if (rs > 0 && valid)
+            for (int r = k + 1; r < n; ++r) A[r][k] /= akk;
+        if (sign == Pos) {
+            if (akk < 0.0) sign = Indef;
+        } else if (sign == Neg) {
+            if (akk > 0.0) sign = Indef;
+        } else if (sign == Zero) {
+            if (akk > 0.0) sign = Pos;
+            else if (akk < 0.0) sign = Neg;
+        }
+    }
+    if (!(sign == Pos || sign == Zero)) return false;  // isPositive()
+    double y[6];
+    for (int i = 0; i < n; ++i) y[i] = b[i];
+    for (int k = 0; k < n; ++k) std::swap(y[k], y[tr[k]]);
+    for (int i = 1; i < n; ++i) {
+        double acc = A[i][0] * y[0];
+        for (int j = 1; j < i; ++j) acc = acc + A[i][j] * y[j];
+        y[i] -= acc;
+    }
+    const double tol = DBL_MIN;
+    for (int i = 0; i < n; ++i) y[i] = (std::fabs(A[i][i]) > tol) ? y[i] / A[i][i] : 0.0;
+    for (int i = n - 2; i >= 0; --i) {
+        double acc = A[i + 1][i] * y[i + 1];
+        for (int j = i + 2; j < n; ++j) acc = acc + A[j][i] * y[j];
+        y[i] -= acc;
+    }
+    for (int k = n - 1; k >= 0; --k) std::swap(y[k], y[tr[k]]);
+    for (int i = 0; i < n; ++i) x[i] = y[i];
+    return true;
+}
+
+// ---- EdgeSE3ProjectXYZOnlyPose + RobustKernelHuber ------------------------------------------------
+struct Edge {
+    double Xw[3];
+    double obs[2];
+    double inv;      // information = Identity * invSigma2
+    double err[2];   // _error (last computeError)
+    int level;
+    bool robust;
+    int slot;
+};
+
+struct Cam {
+    double fx, fy, cx, cy;
+};
+
+void compute_error(Edge& e, const SE3& est, const Cam& K) {
+    double p[3];
+    se3_map(est, e.Xw, p);
+    const double pr0 = p[0] / p[2], pr1 = p[1] / p[2];
+    const double r0 = pr0 * K.fx + K.cx, r1 = pr1 * K.fy + K.cy;
+    e.err[0] = e.obs[0] - r0;
+    e.err[1] = e.obs[1] - r1;
+}
+
+double chi2(const Edge& e) {  // _error.dot(information() * _error)
+    const double w0 = e.inv * e.err[0] + 0.0 * e.err[1];
+    const double w1 = 0.0 * e.err[0] + e.inv * e.err[1];
+    return e.err[0] * w0 + e.err[1] * w1;
+}
+
+struct Huber {
+    double delta, dsqr;
+    void robustify(double e, double rho[3]) const {
+        if (e <= dsqr) {
+            rho[0] = e; rho[1] = 1.0; rho[2] = 0.0;
+        } else {
+            const double sqrte = std::sqrt(e);
+            rho[0] = 2 * sqrte * delta - dsqr;
+            rho[1] = delta / sqrte;
+            rho[2] = -0.5 * rho[1] / e;
+        }
+    }
+};
+
+void linearize(const Edge& e, const SE3& est, const Cam& K, double J[2][6]) {
+    double p[3];
+    se3_map(est, e.Xw, p);
+    const double x = p[0], y = p[1];
+    const double invz = 1.0 / p[2];
+    const double invz_2 = invz * invz;
+    J[0][0] = x * y * invz_2 * K.fx;
+    J[0][1] = -(1 + (x * x * invz_2)) * K.fx;
+    J[0][2] = y * invz * K.fx;
+    J[0][3] = -invz * K.fx;
+    J[0][4] = 0;
+    J[0][5] = x * invz_2 * K.fx;
+    J[1][0] = (1 + y * y * invz_2) * K.fy;
+    J[1][1] = -x * y * invz_2 * K.fy;
+    J[1][2] = -x * invz * K.fy;
+    J[1][3] = 0;
+    J[1][4] = -invz * K.fy;
+    J[1][5] = y * invz_2 * K.fy;
+}
+
+struct Problem {
+    std::vector<Edge> edges;
+    Cam K;
+    Huber huber;
+    // LM state that lives in the g2o objects across rounds
+    double x[6] = {0, 0, 0, 0, 0, 0};  // BlockSolver::_x (zeroed once at allocation, solver.cpp:53-56)
+    double lambda = -1.0, ni = 2.0;
+    int nBadLM = 0;
+    PoseOptStats st = {0, 0, 0};
+
+    double active_robust_chi2() const {
+        double chi = 0.0;
+        for (const Edge& e : edges) {
+            if (e.level != 0) continue;
+            if (e.robust) {
+                double rho[3];
+                huber.robustify(chi2(e), rho);
+                chi += rho[0];
+            } else {
+                chi += chi2(e);
+            }
+        }
+        return chi;
+    }
+    void compute_active_errors(const SE3& est) {
+        for (Edge& e : edges)
+            if (e.level == 0) compute_error(e, est, K);
+    }
+    // BlockSolver::buildSystem: H (vertex hessian, full 6x6) and b.
+    void build_system(const SE3& est, double H[6][6], double b[6]) const {
+        for (int i = 0; i < 6; ++i) {
+            b[i] = 0.0;
+            for (int j = 0; j < 6; ++j) H[i][j] = 0.0;
+        }
+        for (const Edge& e : edges) {
+            if (e.level != 0) continue;
+            double A[2][6];
+            linearize(e, est, K, A);
+            const double om[2][2] = {{e.inv, 0.0}, {0.0, e.inv}};
+            if (e.robust) {
+                double rho[3];
+                huber.robustify(chi2(e), rho);
+                double W[2][2];
+                for (int r = 0; r < 2; ++r)
+                    for (int c = 0; c < 2; ++c) W[r][c] = rho[1] * om[r][c];
+                for (int i = 0; i < 6; ++i) {
+                    double t2[2];
+                    for (int k = 0; k < 2; ++k) t2[k] = (rho[1] * A[0][i]) * om[0][k] + (rho[1] * A[1][i]) * om[1][k];
+                    b[i] -= t2[0] * e.err[0] + t2[1] * e.err[1];
+                }
+                for (int i = 0; i < 6; ++i) {
+                    double t[2];
+                    for (int k = 0; k < 2; ++k) t[k] = A[0][i] * W[0][k] + A[1][i] * W[1][k];
+                    for (int j = 0; j < 6; ++j) H[i][j] += t[0] * A[0][j] + t[1] * A[1][j];
+                }
+            } else {
+                for (int i = 0; i < 6; ++i) {
+                    double t[2];
+                    for (int k = 0; k < 2; ++k) t[k] = A[0][i] * om[0][k] + A[1][i] * om[1][k];
+                    b[i] -= t[0] * e.err[0] + t[1] * e.err[1];
+                    for (int j = 0; j < 6; ++j) H[i][j] += t[0] * A[0][j] + t[1] * A[1][j];
+                }
+            }
+        }
+    }
+
+    enum Result { OK, Terminate };
+
+    // OptimizationAlgorithmLevenberg::solve(iteration, online = false).
+    Result lm_solve(int iteration, SE3& est) {
+        st.lm_iterations++;
+        compute_active_errors(est);
+        double currentChi = active_robust_chi2();
+        double tempChi = currentChi;
+        const double iniChi = currentChi;
+        double H[6][6], b[6];
+        build_system(est, H, b);
+        if (iteration == 0) {
+            double maxDiagonal = 0.;
+            for (int j = 0; j < 6; ++j) maxDiagonal = std::max(std::fabs(H[j][j]), maxDiagonal);
+            lambda = 1e-5 * maxDiagonal;
+            ni = 2;
+            nBadLM = 0;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            st.lm_trials++;
+            const SE3 saved = est;  // push
+            double Hd[6][6];
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 6; ++j) Hd[i][j] = H[i][j];
+            for (int i = 0; i < 6; ++i) Hd[i][i] += lambda;  // setLambda
+            double xs[6];
+            const bool ok2 = ldlt_solve6(Hd, b, xs);
+            if (ok2)
+                for (int i = 0; i < 6; ++i) x[i] = xs[i];
+            est = se3_mul(se3_exp(x), est);  // update -> VertexSE3Expmap::oplusImpl
+            compute_active_errors(est);
+            tempChi = active_robust_chi2();
+            if (!ok2) tempChi = std::numeric_limits<double>::max();
+            rho = (currentChi - tempChi);
+            double scale = 0.;
+            for (int j = 0; j < 6; ++j) scale += x[j] * (lambda * x[j] + b[j]);
+            scale += 1e-3;
+            rho /= scale;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - cube(2 * rho - 1);
+                alpha = std::min(alpha, 2. / 3.);
+                const double scaleFactor = std::max(1. / 3., alpha);
+                lambda *= scaleFactor;
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                est = saved;  // pop
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10);
+        if (qmax == 10 || rho == 0) return Terminate;
+        if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
+        else nBadLM = 0;
+        if (nBadLM >= 3) return Terminate;
+        return OK;
+    }
+
+    // SparseOptimizer::optimize(iterations) after initializeOptimization(0).
+    void optimize(int iterations, SE3& est) {
+        bool any = false;
+        for (const Edge& e : edges) any |= (e.level == 0);
+        if (!any) return;  // no active vertex: "0 vertices to optimize", returns -1
+        bool ok = true;
+        for (int i = 0; i < iterations && ok; i++) ok = (lm_solve(i, est) == OK);
+    }
+};
+
+}  // namespace
+
+int pose_optimization(const PoseOptInput& in, float Tcw_out[16], uint8_t* outlier, PoseOptStats* stats) {
+    Problem P;
+    P.K = {(double)in.fx, (double)in.fy, (double)in.cx, (double)in.cy};
+    const float deltaMono = std::sqrt(5.991);
+    P.huber.delta = deltaMono;
+    P.huber.dsqr = P.huber.delta * P.huber.delta;
+    for (int i = 0; i < in.n; ++i) {
+        if (in.has_mp && !in.has_mp[i]) continue;
+        outlier[i] = 0;
+        Edge e;
+        for (int c = 0; c < 3; ++c) e.Xw[c] = in.Xw[3 * i + c];
+        e.obs[0] = in.uv[2 * i];
+        e.obs[1] = in.uv[2 * i + 1];
+        e.inv = in.inv_sigma2[i];
+        e.err[0] = e.err[1] = 0.0;
+        e.level = 0;
+        e.robust = true;
+        e.slot = i;
+        P.edges.push_back(e);
+    }
+    const int nInitialCorrespondences = (int)P.edges.size();
+    if (stats) *stats = P.st;
+    if (nInitialCorrespondences < 3) return 0;
+
+    // Converter::toSE3Quat(pFrame->mTcw): rotation() taken as linear()
+    double R0[3][3], t0[3];
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) R0[r][c] = in.Tcw[4 * r + c];
+        t0[r] = in.Tcw[4 * r + 3];
+    }
+    const SE3 init = se3_from_Rt(R0, t0);
+    const float chi2Mono[4] = {5.991, 5.991, 5.991, 5.991};
+    const int its[4] = {10, 10, 10, 10};
+    SE3 est = init;
+    int nBad = 0;
+    for (size_t it = 0; it < 4; it++) {
+        P.st.rounds++;
+        est = init;  // vSE3->setEstimate(Converter::toSE3Quat(pFrame->mTcw)); mTcw is not updated in the loop
+        P.optimize(its[it], est);
+        nBad = 0;
+        for (Edge& e : P.edges) {
+            if (outlier[e.slot]) compute_error(e, est, P.K);
+            const float c2 = chi2(e);
+            if (c2 > chi2Mono[it]) {
+                outlier[e.slot] = 1;
+                e.level = 1;
+                nBad++;
+            } else {
+                outlier[e.slot] = 0;
+                e.level = 0;
+            }
+            if (it == 2) e.robust = false;
+        }
+        if (P.edges.size() < 10) break;
+    }
+    // Converter::toIso(SE3quat_recov): to_homogeneous_matrix().cast<float>()
+    double R[3][3];
+    quat_to_R(est.r, R);
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) Tcw_out[4 * r + c] = (float)R[r][c];
+        Tcw_out[4 * r + 3] = (float)est.t[r];
+    }
+    Tcw_out[12] = Tcw_out[13] = Tcw_out[14] = 0.0f;
+    Tcw_out[15] = 1.0f;
+    if (stats) *stats = P.st;
+    return nInitialCorrespondences - nBad;
+}
+
+}  // namespace rsc_oracle

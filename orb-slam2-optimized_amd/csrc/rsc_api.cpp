@@ -17,6 +17,7 @@
 #include "../../include/rsc.h"
 #include "rsc_kernels.h"
 #include "rsc_engine.h"
+#include "rsc_poseopt.h"
 
 using namespace rsc;
 
@@ -115,6 +116,12 @@ struct rsc_context {
     PinBuf<int32_t> h_counts;
     PinBuf<float> h_small;
     DevBuf<char> d_refine;
+    // PoseOptimization: packed inputs (problems | xw | uv), edge error scratch, results (outliers | poses)
+    DevBuf<char> d_po_in;
+    DevBuf<double2> d_po_err;
+    DevBuf<char> d_po_res;
+    PinBuf<char> h_po_in;
+    PinBuf<char> h_po_res;
     int mask_words = 0;  // per hypothesis, last speculation
     bool keep_samples = true;
     // PnP hypothesis kernels ($RSC_SOLVE_MODE): 0 = auto, 1 = "mono" (one kernel, lane per
@@ -1091,6 +1098,119 @@ int rsc_sim3_prepared(const rsc_sim3* s, float* X1c, float* X2c, float* P1im1, f
     if (e1) std::memcpy(e1, s->e1.data(), 8 * (size_t)N);
     if (e2) std::memcpy(e2, s->e2.data(), 8 * (size_t)N);
     if (idx) std::memcpy(idx, s->st.indices1.data(), 4 * (size_t)N);
+    return RSC_OK;
+}
+
+
+// ---- Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) ----
+int rsc_pose_optimization_many(rsc_context* C, const rsc_poseopt_problem* P, int count, rsc_poseopt_result* out,
+                               uint8_t* const* outlier) {
+    if (!C || count < 0 || (count && (!P || !out))) return RSC_ERR_ARG;
+    if (count == 0) return RSC_OK;
+    // compaction of the slots with a map point (the edges, Optimizer.cpp:247-325), in slot order
+    std::vector<int> run;             // problems with >= 3 edges (the others return 0, :329-330)
+    std::vector<size_t> eoff(1, 0);   // edge offsets of the run problems
+    for (int c = 0; c < count; ++c) {
+        const rsc_poseopt_problem& q = P[c];
+        if (q.n < 0 || (q.n > 0 && (!q.uv || !q.Xw || !q.inv_sigma2))) return RSC_ERR_ARG;
+        int ne = 0;
+        for (int i = 0; i < q.n; ++i) {
+            if (q.has_mp && !q.has_mp[i]) continue;
+            if (q.u_right && q.u_right[i] >= 0) {
+                g_last_error = "stereo observations (mvuRight >= 0) are not supported";
+                return RSC_ERR_UNSUPPORTED;
+            }
+            ++ne;
+        }
+        if (ne > kPoseMaxEdges) {
+            g_last_error = "more than 8192 map-point matches in one Frame";
+            return RSC_ERR_UNSUPPORTED;
+        }
+        rsc_poseopt_result& r = out[c];
+        std::memset(&r, 0, sizeof(r));
+        r.n_initial = ne;
+        std::memcpy(r.Tcw, q.Tcw, sizeof(r.Tcw));
+        if (outlier && outlier[c])
+            for (int i = 0; i < q.n; ++i)
+                if (!q.has_mp || q.has_mp[i]) outlier[c][i] = 0;
+        if (ne >= 3) {
+            run.push_back(c);
+            eoff.push_back(eoff.back() + (size_t)ne);
+        }
+    }
+    const int R = (int)run.size();
+    if (R == 0) return RSC_OK;
+    const size_t E = eoff.back();
+    RSC_HIP(hipSetDevice(C->device));
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_probs = 0, o_xw = al(sizeof(DevPoseProb) * R), o_uv = o_xw + al(sizeof(float4) * E);
+    const size_t in_bytes = o_uv + al(sizeof(float2) * E);
+    const size_t r_out = 0, r_flags = al(sizeof(float) * 16 * R);
+    const size_t res_bytes = r_flags + al(E);
+    if (int e = C->h_po_in.ensure(in_bytes)) return e;
+    if (int e = C->d_po_in.ensure(in_bytes)) return e;
+    if (int e = C->h_po_res.ensure(res_bytes)) return e;
+    if (int e = C->d_po_res.ensure(res_bytes)) return e;
+    if (int e = C->d_po_err.ensure(E)) return e;
+    // the previous call's copies out of the pinned staging must be complete
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    char* h = C->h_po_in.p;
+    char* d = C->d_po_in.p;
+    DevPoseProb* hp = reinterpret_cast<DevPoseProb*>(h + o_probs);
+    float4* hxw = reinterpret_cast<float4*>(h + o_xw);
+    float2* huv = reinterpret_cast<float2*>(h + o_uv);
+    for (int k = 0; k < R; ++k) {
+        const rsc_poseopt_problem& q = P[run[k]];
+        size_t e = eoff[k];
+        for (int i = 0; i < q.n; ++i) {
+            if (q.has_mp && !q.has_mp[i]) continue;
+            hxw[e] = make_float4(q.Xw[3 * i], q.Xw[3 * i + 1], q.Xw[3 * i + 2], q.inv_sigma2[i]);
+            huv[e] = make_float2(q.uv[2 * i], q.uv[2 * i + 1]);
+            ++e;
+        }
+        DevPoseProb& dp = hp[k];
+        dp.xw = reinterpret_cast<const float4*>(d + o_xw) + eoff[k];
+        dp.uv = reinterpret_cast<const float2*>(d + o_uv) + eoff[k];
+        dp.err = C->d_po_err.p + eoff[k];
+        dp.outlier = reinterpret_cast<uint8_t*>(C->d_po_res.p + r_flags) + eoff[k];
+        dp.out = reinterpret_cast<float*>(C->d_po_res.p + r_out) + 16 * k;
+        dp.n = (int)(eoff[k + 1] - eoff[k]);
+        dp.fx = q.fx; dp.fy = q.fy; dp.cx = q.cx; dp.cy = q.cy;
+        for (int j = 0; j < 12; ++j) dp.T[j] = q.Tcw[j];
+    }
+    RSC_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, C->stream));
+    timing_begin(C, 3);
+    RSC_HIP(launch_poseopt(R, reinterpret_cast<const DevPoseProb*>(d + o_probs), C->stream));
+    timing_begin(C, 4);
+    RSC_HIP(hipMemcpyAsync(C->h_po_res.p, C->d_po_res.p, res_bytes, hipMemcpyDeviceToHost, C->stream));
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    if (C->timing) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, C->ev[3], C->ev[4]);
+        C->last_ms[2] = ms;
+    }
+    const float* ho = reinterpret_cast<const float*>(C->h_po_res.p + r_out);
+    const uint8_t* hf = reinterpret_cast<const uint8_t*>(C->h_po_res.p + r_flags);
+    for (int k = 0; k < R; ++k) {
+        const int c = run[k];
+        const rsc_poseopt_problem& q = P[c];
+        rsc_poseopt_result& r = out[c];
+        const float* o = ho + 16 * k;
+        for (int j = 0; j < 12; ++j) r.Tcw[j] = o[j];
+        r.Tcw[12] = r.Tcw[13] = r.Tcw[14] = 0.0f;
+        r.Tcw[15] = 1.0f;
+        std::memcpy(&r.n_good, o + 12, 4);
+        std::memcpy(&r.rounds, o + 13, 4);
+        std::memcpy(&r.lm_iterations, o + 14, 4);
+        std::memcpy(&r.lm_trials, o + 15, 4);
+        if (outlier && outlier[c]) {
+            size_t e = eoff[k];
+            for (int i = 0; i < q.n; ++i) {
+                if (q.has_mp && !q.has_mp[i]) continue;
+                outlier[c][i] = hf[e++];
+            }
+        }
+    }
     return RSC_OK;
 }
 

@@ -37,7 +37,7 @@ EXPORTED = [
     "rsc_mlpnp_create", "rsc_mlpnp_destroy", "rsc_mlpnp_set_ransac_parameters",
     "rsc_mlpnp_set_ransac_parameters_many", "rsc_mlpnp_iterate", "rsc_mlpnp_iterate_many", "rsc_mlpnp_reset",
     "rsc_mlpnp_reset_many", "rsc_mlpnp_get_state", "rsc_mlpnp_last_poses", "rsc_mlpnp_last_samples",
-    "rsc_reloc_events", "rsc_loop_events",
+    "rsc_reloc_events", "rsc_loop_events", "rsc_pose_optimization_many",
 ]
 
 
@@ -65,6 +65,17 @@ class Sim3Input(C.Structure):
 class Sim3Result(C.Structure):
     _fields_ = [("ok", C.c_int32), ("no_more", C.c_int32), ("n_inliers", C.c_int32), ("iterations", C.c_int32),
                 ("R", C.c_float * 9), ("t", C.c_float * 3)]
+
+
+class PoseOptProblem(C.Structure):
+    _fields_ = [("n", C.c_int32), ("has_mp", C.c_void_p), ("uv", C.c_void_p), ("Xw", C.c_void_p),
+                ("inv_sigma2", C.c_void_p), ("u_right", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float),
+                ("cx", C.c_float), ("cy", C.c_float), ("Tcw", C.c_float * 16)]
+
+
+class PoseOptResult(C.Structure):
+    _fields_ = [("n_good", C.c_int32), ("n_initial", C.c_int32), ("rounds", C.c_int32),
+                ("lm_iterations", C.c_int32), ("lm_trials", C.c_int32), ("Tcw", C.c_float * 16)]
 
 
 def load_library(path: str = LIB_PATH):
@@ -127,6 +138,8 @@ def load_library(path: str = LIB_PATH):
     L.rsc_mlpnp_last_poses.argtypes = [vp, f64p, C.c_int]
     L.rsc_mlpnp_last_samples.argtypes = [vp, i32p, C.c_int]
     L.rsc_reloc_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(PnPResult), C.POINTER(EventResult)]
+    L.rsc_pose_optimization_many.argtypes = [vp, C.POINTER(PoseOptProblem), C.c_int, C.POINTER(PoseOptResult),
+                                             C.POINTER(C.c_void_p)]
     L.rsc_loop_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(Sim3Result), C.POINTER(EventResult)]
     L.rsc_diag_pnp_phase_stamps.argtypes = [C.POINTER(vp), C.c_int, C.c_int,
                                             np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
@@ -514,3 +527,40 @@ class EventBatch:
                 out[e, 0:3], out[e, 4:7], out[e, 8:11] = R[0], R[1], R[2]
                 out[e, 3], out[e, 7], out[e, 11], out[e, 15] = r["t"][0], r["t"][1], r["t"][2], 1.0
         return out
+
+
+def pose_optimization_many(ctx: Context, frames, with_outliers: bool = True):
+    """Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) on every frame in one launch.
+
+    frames: objects with has_mp, uv, Xw, inv_sigma2, Tcw, fx..cy (rsc.synth.PoseOptFrame).  Returns
+    per frame a dict: n_good (the reference's return value), n_initial, rounds, lm_iterations,
+    lm_trials, Tcw float32[4,4] (pFrame->mTcw after the call), outlier uint8[n] (mvbOutlier; 255 on
+    slots without a map point)."""
+    L = load_library()
+    n = len(frames)
+    probs = (PoseOptProblem * max(n, 1))()
+    res = (PoseOptResult * max(n, 1))()
+    keep = []
+    outs = []
+    ptrs = (C.c_void_p * max(n, 1))()
+    for i, f in enumerate(frames):
+        arrs = [np.ascontiguousarray(f.has_mp, np.uint8), np.ascontiguousarray(f.uv, np.float32).reshape(-1),
+                np.ascontiguousarray(f.Xw, np.float32).reshape(-1), np.ascontiguousarray(f.inv_sigma2, np.float32)]
+        keep.append(arrs)
+        p = probs[i]
+        p.n = f.n
+        p.has_mp, p.uv, p.Xw, p.inv_sigma2 = (a.ctypes.data for a in arrs)
+        p.u_right = None
+        p.fx, p.fy, p.cx, p.cy = float(f.fx), float(f.fy), float(f.cx), float(f.cy)
+        p.Tcw[:] = [float(v) for v in np.asarray(f.Tcw, np.float32).reshape(16)]
+        o = np.full(max(f.n, 1), 255, np.uint8)
+        outs.append(o)
+        ptrs[i] = o.ctypes.data if with_outliers else None
+    _check(L.rsc_pose_optimization_many(ctx.h, probs, n, res, ptrs), "rsc_pose_optimization_many")
+    out = []
+    for i, f in enumerate(frames):
+        r = res[i]
+        out.append({"n_good": r.n_good, "n_initial": r.n_initial, "rounds": r.rounds,
+                    "lm_iterations": r.lm_iterations, "lm_trials": r.lm_trials,
+                    "Tcw": np.array(r.Tcw[:], np.float32).reshape(4, 4), "outlier": outs[i][:f.n]})
+    return out

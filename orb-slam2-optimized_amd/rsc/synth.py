@@ -173,3 +173,44 @@ def make_sim3_pair(rng: np.random.Generator, n1: int, n_inliers: int, invalid_fr
                     sigma2_1=s2[levels1].astype(np.float32), sigma2_2=s2[levels2].astype(np.float32),
                     R1=R1.astype(np.float32), t1=t1.astype(np.float32), R2=R2.astype(np.float32),
                     t2=t2.astype(np.float32), K1=K, K2=K.copy(), inlier_true=inl)
+
+
+@dataclasses.dataclass
+class PoseOptFrame:
+    """Optimizer::PoseOptimization inputs (Optimizer.cpp:205-318) for one monocular Frame."""
+    has_mp: np.ndarray      # uint8 [n]   mvpMapPoints[i] != NULL
+    uv: np.ndarray          # float32 [n,2] mvKeysUn[i].pt
+    Xw: np.ndarray          # float32 [n,3] MapPoint::GetWorldPos() (0 where has_mp == 0)
+    inv_sigma2: np.ndarray  # float32 [n]   mvInvLevelSigma2[octave] = 1.0f / mvLevelSigma2
+    Tcw: np.ndarray         # float32 [4,4] initial pFrame->mTcw (e.g. the RANSAC pose)
+    R_true: np.ndarray
+    t_true: np.ndarray
+    inlier_true: np.ndarray  # bool [n]
+    fx: np.float32 = FX
+    fy: np.float32 = FY
+    cx: np.float32 = CX
+    cy: np.float32 = CY
+
+    @property
+    def n(self) -> int:
+        return int(self.uv.shape[0])
+
+
+def make_poseopt_frame(rng: np.random.Generator, n: int, inlier_ratio: float = 0.8, rot_noise: float = 0.02,
+                       trans_noise: float = 0.05, no_mp_frac: float = 0.0, noise: bool = True) -> PoseOptFrame:
+    """A PnP-shaped scene whose initial Tcw is the true pose perturbed like a RANSAC estimate."""
+    sc = make_pnp_scene(rng, n, inlier_ratio, noise=noise)
+    dR = random_rotation(rng, rot_noise)
+    R0 = dR @ sc.R_true
+    t0 = sc.t_true + rng.normal(size=3) * trans_noise
+    T = np.eye(4, dtype=np.float32)
+    T[:3, :3] = R0.astype(np.float32)
+    T[:3, 3] = t0.astype(np.float32)
+    has = np.ones(n, dtype=np.uint8)
+    if no_mp_frac > 0:
+        has[rng.random(n) < no_mp_frac] = 0
+    Xw = sc.p3dw.copy()
+    Xw[has == 0] = 0.0
+    inv = (np.float32(1.0) / sc.sigma2).astype(np.float32)
+    return PoseOptFrame(has_mp=has, uv=sc.p2d, Xw=Xw, inv_sigma2=inv, Tcw=T, R_true=sc.R_true, t_true=sc.t_true,
+                        inlier_true=sc.inlier_true)

@@ -4,6 +4,8 @@
 * glibc_rand.json — rand() after srand(seed) from THIS container's glibc (2.35) through ctypes,
   plus DUtils::Random::RandomInt swap-remove sample streams computed in pure Python from those
   libc outputs (Random.cpp:47-50, PnPsolver.cpp:125-138).  Independent of the oracle.
+* poseopt_traces.npz — Optimizer::PoseOptimization oracle outputs (pose bits, nGood, round / LM
+  iteration / trial counts) on seeded synthetic Frames (regression pins, parity unpinned).
 * pnp_traces.npz / sim3_traces.npz — per-hypothesis sample indices, inlier counts and poses of the
   oracle restatement on small seeded scenes (regression pins of the oracle; the reference itself
   cannot be built here, see DESIGN.md "Oracle").
@@ -48,6 +50,7 @@ def python_sample_stream(rands, N, min_set, hyps):
 
 
 def main():
+    poseopt()
     g = {"glibc": "2.35 (ctypes libc.so.6)", "rand": {}, "samples": []}
     for s in SEEDS:
         g["rand"][str(s)] = libc_rand(s, 2000)
@@ -93,5 +96,22 @@ def main():
     print("golden fixtures written")
 
 
+def poseopt():
+    import oracle_lib as ol
+    from rsc import synth
+    cases = [(11, 300, 0.8, 0.0), (12, 50, 0.6, 0.2), (13, 9, 1.0, 0.0), (14, 1500, 0.5, 0.1), (15, 120, 0.95, 0.0)]
+    out = {"seeds": [], "ns": [], "ratios": [], "no_mp": [], "n_good": [], "T": [], "stats": []}
+    for seed, n, ratio, nomp in cases:
+        f = synth.make_poseopt_frame(np.random.default_rng(seed), n, ratio, no_mp_frac=nomp)
+        r, T, o, st = ol.pose_optimization(f)
+        for k, v in zip(["seeds", "ns", "ratios", "no_mp", "n_good", "T", "stats"],
+                        [seed, n, ratio, nomp, r, T.reshape(16), st]):
+            out[k].append(v)
+    np.savez_compressed(os.path.join(HERE, "poseopt_traces.npz"), **{k: np.array(v) for k, v in out.items()})
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "poseopt":
+        poseopt()
+        sys.exit(0)
     main()

@@ -2,12 +2,15 @@
 // rsc_sim3.h / rsc_engine.h RNG).  The product library never contains this code path; it exists
 // so that the arithmetic the kernels run can be compared with the oracle on a CPU.
 #include <cstdint>
+#include <cfloat>
+#include <cmath>
 #include <cstring>
 #include <vector>
 #include "../../orb-slam2-optimized_amd/csrc/rsc_epnp.h"
 #include "../../orb-slam2-optimized_amd/csrc/rsc_sim3.h"
 #include "../../orb-slam2-optimized_amd/csrc/rsc_engine.h"
 #include "../../orb-slam2-optimized_amd/csrc/rsc_mlpnp.h"
+#include "../../orb-slam2-optimized_amd/csrc/rsc_poseopt.h"
 
 using namespace rsc;
 
@@ -326,5 +329,144 @@ int he_mlpnp_count(const double* R, const double* t, const float* K, float th2, 
         c += in;
     }
     return c;
+}
+
+// PoseOptimization in the device orchestration (poseopt.hip), run sequentially: the same per-edge
+// functions and the same edge-order folds.  xw4 [n][4] = (X, Y, Z, invSigma2), uv [n][2].
+// out[16]: Tcw rows 0..2, then n_good, rounds, lm_iterations, lm_trials (as int bits).
+void he_pose_optimization(int n, const float* xw4, const float* uv, const float* K4, const float* T12, float* out,
+                          uint8_t* outlier) {
+    using namespace rsc;
+    const PoCam K{(double)K4[0], (double)K4[1], (double)K4[2], (double)K4[3]};
+    const float deltaMono = std::sqrt(5.991);
+    const double delta = deltaMono, dsqr = delta * delta;
+    std::vector<double> err(2 * (size_t)n, 0.0);
+    std::vector<uint8_t> lvl(n, 0);
+    double R0[3][3], t0[3];
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) R0[r][c] = T12[4 * r + c];
+        t0[r] = T12[4 * r + 3];
+    }
+    const PoSE3 init = po_from_Rt(R0, t0);
+    for (int e = 0; e < n; ++e) outlier[e] = 0;
+    bool robust = true;
+    auto chi_pass = [&](const PoSE3& est) {
+        double acc = 0.0;
+        for (int e = 0; e < n; ++e) {
+            double t = 0.0;
+            if (lvl[e] == 0) {
+                const double X[3] = {xw4[4 * e], xw4[4 * e + 1], xw4[4 * e + 2]};
+                po_error(est, K, X, uv[2 * e], uv[2 * e + 1], err[2 * e], err[2 * e + 1]);
+                t = po_chi_term(robust, xw4[4 * e + 3], err[2 * e], err[2 * e + 1], delta, dsqr);
+            }
+            acc = acc + t;
+        }
+        return acc;
+    };
+    auto build_pass = [&](const PoSE3& est, double (&H)[6][6], double (&b)[6]) {
+        double acc[kPoseTerms];
+        for (int k = 0; k < kPoseTerms; ++k) acc[k] = 0.0;
+        for (int e = 0; e < n; ++e) {
+            double t[kPoseTerms];
+            for (int k = 0; k < kPoseTerms; ++k) t[k] = 0.0;
+            if (lvl[e] == 0) {
+                const double X[3] = {xw4[4 * e], xw4[4 * e + 1], xw4[4 * e + 2]};
+                po_quad_terms(est, K, X, xw4[4 * e + 3], err[2 * e], err[2 * e + 1], robust, delta, dsqr, t);
+            }
+            for (int k = 0; k < kPoseTerms; ++k) acc[k] = (k >= 21) ? acc[k] - t[k] : acc[k] + t[k];
+        }
+        int k = 0;
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j <= i; ++j) { H[i][j] = acc[k++]; H[j][i] = H[i][j]; }
+        for (int i = 0; i < 6; ++i) b[i] = acc[21 + i];
+    };
+    double x[6] = {0, 0, 0, 0, 0, 0};
+    double lambda = -1.0, ni = 2.0;
+    int nBadLM = 0, rounds = 0, lm_its = 0, lm_trials = 0, nBad = 0;
+    PoSE3 est = init;
+    for (int it = 0; it < 4; ++it) {
+        rounds++;
+        est = init;
+        bool any = false;
+        for (int e = 0; e < n; ++e) any |= (lvl[e] == 0);
+        if (any) {
+            bool ok = true;
+            for (int i = 0; i < 10 && ok; ++i) {
+                lm_its++;
+                double currentChi = chi_pass(est);
+                const double iniChi = currentChi;
+                double H[6][6], b[6];
+                build_pass(est, H, b);
+                if (i == 0) {
+                    double maxDiagonal = 0.;
+                    for (int j = 0; j < 6; ++j) { const double a = std::fabs(H[j][j]); maxDiagonal = (a < maxDiagonal) ? maxDiagonal : a; }
+                    lambda = 1e-5 * maxDiagonal;
+                    ni = 2;
+                    nBadLM = 0;
+                }
+                double rho = 0;
+                int qmax = 0;
+                do {
+                    lm_trials++;
+                    const PoSE3 saved = est;
+                    double Hd[6][6];
+                    for (int r = 0; r < 6; ++r) for (int c = 0; c < 6; ++c) Hd[r][c] = H[r][c];
+                    for (int r = 0; r < 6; ++r) Hd[r][r] += lambda;
+                    double xs[6];
+                    const bool ok2 = po_ldlt_solve6(Hd, b, xs);
+                    if (ok2) for (int j = 0; j < 6; ++j) x[j] = xs[j];
+                    est = po_mul(po_exp(x), est);
+                    double tempChi = chi_pass(est);
+                    if (!ok2) tempChi = DBL_MAX;
+                    rho = (currentChi - tempChi);
+                    double scale = 0.;
+                    for (int j = 0; j < 6; ++j) scale += x[j] * (lambda * x[j] + b[j]);
+                    scale += 1e-3;
+                    rho /= scale;
+                    if (rho > 0 && std::isfinite(tempChi)) {
+                        double alpha = 1. - po_cube(2 * rho - 1);
+                        alpha = (2. / 3. < alpha) ? 2. / 3. : alpha;
+                        const double scaleFactor = (1. / 3. < alpha) ? alpha : 1. / 3.;
+                        lambda *= scaleFactor;
+                        ni = 2;
+                        currentChi = tempChi;
+                    } else {
+                        lambda *= ni;
+                        ni *= 2;
+                        est = saved;
+                    }
+                    qmax++;
+                } while (rho < 0 && qmax < 10);
+                if (qmax == 10 || rho == 0) ok = false;
+                else {
+                    if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
+                    else nBadLM = 0;
+                    ok = nBadLM < 3;
+                }
+            }
+        }
+        nBad = 0;
+        for (int e = 0; e < n; ++e) {
+            if (lvl[e]) {
+                const double X[3] = {xw4[4 * e], xw4[4 * e + 1], xw4[4 * e + 2]};
+                po_error(est, K, X, uv[2 * e], uv[2 * e + 1], err[2 * e], err[2 * e + 1]);
+            }
+            const float c2 = (float)po_chi2(xw4[4 * e + 3], err[2 * e], err[2 * e + 1]);
+            const bool bad = c2 > 5.991f;
+            lvl[e] = bad;
+            outlier[e] = bad;
+            nBad += bad;
+        }
+        if (it == 2) robust = false;
+        if (n < 10) break;
+    }
+    double R[3][3];
+    po_quat_to_R(est.r, R);
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) out[4 * r + c] = (float)R[r][c];
+        out[4 * r + 3] = (float)est.t[r];
+    }
+    const int ints[4] = {n - nBad, rounds, lm_its, lm_trials};
+    std::memcpy(out + 12, ints, 16);
 }
 }  // extern "C"

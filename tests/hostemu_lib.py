@@ -33,6 +33,7 @@ def lib():
         L.he_mlpnp_count.argtypes = [f64p, f64p, f32p, C.c_float, C.c_int, f32p, f32p, u8p]
         L.he_sim3_hypothesis.argtypes = [u32p, C.c_int, C.c_int, C.c_int, f32p, f32p, i32p, f32p]
         L.he_sim3_count.argtypes = [f32p, f32p, f32p, C.c_int, f32p, f32p, f32p, f32p, u64p, u64p, u8p]
+        L.he_pose_optimization.argtypes = [C.c_int, f32p, f32p, f32p, f32p, f32p, u8p]
         _lib = L
     return _lib
 
@@ -157,3 +158,24 @@ def iterate_many(emus, n):
                         iterations=int(i4[4 * i + 3]), T=T[16 * i:16 * i + 16].reshape(4, 4),
                         inliers=(masks[i][:emus[i].n_points].astype(bool) if ok else np.zeros(0, bool))))
     return out
+
+
+def pose_optimization(frame):
+    """Host build of the device PoseOptimization orchestration: (n_good, Tcw[4,4], outlier over the
+    edges (slots with a map point, in slot order), stats[3])."""
+    sel = np.nonzero(frame.has_mp)[0]
+    n = len(sel)
+    xw4 = np.zeros((n, 4), np.float32)
+    xw4[:, :3] = frame.Xw[sel]
+    xw4[:, 3] = frame.inv_sigma2[sel]
+    uv = np.ascontiguousarray(frame.uv[sel], np.float32)
+    K = np.array([frame.fx, frame.fy, frame.cx, frame.cy], np.float32)
+    T12 = np.ascontiguousarray(frame.Tcw[:3], np.float32).reshape(12)
+    out = np.zeros(16, np.float32)
+    outl = np.zeros(max(n, 1), np.uint8)
+    lib().he_pose_optimization(n, xw4.reshape(-1) if n else np.zeros(4, np.float32), uv.reshape(-1) if n else
+                               np.zeros(2, np.float32), K, T12, out, outl)
+    ints = out[12:].view(np.int32)
+    T = np.eye(4, dtype=np.float32)
+    T[:3] = out[:12].reshape(3, 4)
+    return int(ints[0]), T, outl[:n], ints[1:].copy()
