@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--no-sim3", action="store_true")
     p.add_argument("--no-mlpnp", action="store_true")
     p.add_argument("--no-events", action="store_true")
+    p.add_argument("--no-poseopt", action="store_true")
     return p.parse_args()
 
 
@@ -254,6 +255,71 @@ def run_events(engine, ctx, args, dist, rank, world):
                 sharding=f"{world} rank(s), LPT by N*300, RCCL all-gather of {rev.EVENT_RECORD}-float records")
 
 
+def poseopt_frames(rng, F=64, N=2000, ratio=0.8):
+    from rsc import synth
+    return [synth.make_poseopt_frame(rng, N, ratio) for _ in range(F)]
+
+
+def run_poseopt(engine, ctx, frames, args):
+    """SURVEY §8(f) row 1: Optimizer::PoseOptimization (Optimizer.cpp:205-424) on a batch of Frames
+    (64 x 2000 map-point matches, 80 % inliers, start pose perturbed like a RANSAC estimate), one
+    rsc_pose_optimization_many call per step; kernel time from HIP events in a second pass."""
+    batch = engine.PoseOptBatch(ctx, frames)
+
+    def step():
+        batch.run()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    steps = max(1, args.steps // 2)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    res = batch.results()
+    ctx.enable_timing(True)
+    kms = 0.0
+    for _ in range(steps):
+        step()
+        kms += ctx.last_timing()["refine_ms"]
+    ctx.enable_timing(False)
+    its = sum(r["lm_iterations"] for r in res)
+    trials = sum(r["lm_trials"] for r in res)
+    F = len(frames)
+    return dict(poses_per_s=F * steps / dt, ms_per_step=1e3 * dt / steps, kernel_ms=kms / steps, frames=F,
+                edges_per_frame=frames[0].n, lm_iterations_per_frame=its / F, lm_trials_per_frame=trials / F,
+                steps=steps)
+
+
+def cpu_baseline_poseopt(frames, seconds):
+    """The PoseOptimization oracle on ONE host core over the same frames."""
+    import oracle_lib as ol
+    L = ol.lib()
+    F = len(frames)
+    n = np.array([f.n for f in frames], np.int64)
+    off = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)
+    uv = np.ascontiguousarray(np.concatenate([f.uv for f in frames]), np.float32)
+    Xw = np.ascontiguousarray(np.concatenate([f.Xw for f in frames]), np.float32)
+    inv = np.ascontiguousarray(np.concatenate([f.inv_sigma2 for f in frames]), np.float32)
+    T = np.ascontiguousarray(np.stack([f.Tcw.reshape(16) for f in frames]), np.float32).reshape(-1)
+    To = np.zeros(16 * F, np.float32)
+    outl = np.zeros(int(off[-1]), np.uint8)
+    good = np.zeros(F, np.int32)
+    f0 = frames[0]
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        L.ora_pose_optimization_batch(F, off, uv, Xw, inv, f0.fx, f0.fy, f0.cx, f0.cy, T, To, outl, good)
+        done += F
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=round(done / dt, 2), unit="poses/s", cores=1, kind="port",
+                sample=f"{done // F} batches of {F} Frames x {f0.n} edges in {dt:.1f} s, oracle restatement, 1 thread")
+
+
 def cpu_baseline(scenes, args):
     """Oracle restatement (test infrastructure) of the same workload on ONE host core."""
     import oracle_lib as ol
@@ -309,6 +375,10 @@ def main():
         sim3 = run_sim3(engine, ctx, np.random.default_rng(77), args)
     if rank == 0 and not args.no_mlpnp:
         mlpnp = run_mlpnp(engine, ctx, np.random.default_rng(78), args)
+    poseopt = po_frames = None
+    if rank == 0 and not args.no_poseopt:
+        po_frames = poseopt_frames(np.random.default_rng(79))
+        poseopt = run_poseopt(engine, ctx, po_frames, args)
     if rank != 0:
         if dist is not None:
             dist.barrier()
@@ -371,6 +441,12 @@ def main():
         out["events"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in events.items()}
     if mlpnp is not None:
         out["mlpnp"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in mlpnp.items()}
+    if poseopt is not None:
+        out["poseopt"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in poseopt.items()}
+        if not args.no_cpu and world == 1:
+            cb = cpu_baseline_poseopt(po_frames, min(3.0, args.cpu_seconds))
+            out["poseopt"]["cpu_baseline"] = cb
+            out["poseopt"]["speedup_vs_cpu_1core"] = round(poseopt["poses_per_s"] / cb["value"], 1)
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(scenes, args)
         out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 1)

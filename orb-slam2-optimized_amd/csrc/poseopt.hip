@@ -1,5 +1,15 @@
-// poseopt.hip — Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) kernel: one 256-thread
+// poseopt.hip — Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) kernel: one 512-thread
 // workgroup per Frame.  See rsc_poseopt.h for the mapping and the arithmetic contract.
+//
+// Where the time goes: every g2o reduction is a sequential sum over the edges, and only its
+// dependent FP64 additions are serial here.  A pass computes all per-edge terms in parallel, then
+// folds them in edge order out of LDS; the build pass folds the 27 H/b columns on lanes of wave 0
+// while the chi2 column (when needed) folds on wave 1, and chunk columns are padded so the 27
+// lanes read different banks.  The fold reads run 32 terms ahead of the additions.
+// OptimizationAlgorithmLevenberg::solve recomputes activeRobustChi2 at its start; that value is the
+// previous solve's currentChi at the same estimate (accepted trial -> the trial's chi2, rejected ->
+// popped to the state currentChi belongs to), so it is reused bit for bit instead of refolded, and
+// the per-edge errors are recomputed only when the last trial was rejected.
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include "rsc_poseopt.h"
@@ -9,90 +19,110 @@ namespace rsc {
 
 namespace {
 
-struct PoseShared {
-    double terms[kPoseTerms * kPoseThreads];  // per-chunk edge terms, column k at [k * 256]
-    double red[kPoseTerms];                   // folded sums
-    uint8_t lvl[kPoseMaxEdges];               // edge level: 0 active, 1 outlier (g2o setLevel)
-    int nbad;
+constexpr int kPoseChunk = 512;                 // edges per build chunk = threads per workgroup
+constexpr int kPoseCol = kPoseChunk + 2;        // padded column stride (doubles): 16 B bank shift per column
+constexpr int kPoseCols = kPoseTerms + 1;       // 27 H/b columns + the chi2 column
+constexpr int kPoseTermDoubles = kPoseCols * kPoseCol;
+static_assert(kPoseTermDoubles >= kPoseMaxEdges, "chi2 terms of a whole pass must fit the term buffer");
+constexpr size_t kPoseLds = sizeof(double) * kPoseTermDoubles + kPoseMaxEdges;
+
+struct PoseLds {
+    double* terms;
+    double* red;   // [32] folded sums
+    uint8_t* lvl;  // [kPoseMaxEdges] edge level: 0 active, 1 outlier (g2o setLevel)
+    int* nbad;
 };
 
+// Sequential fold acc (+|-)= c[0..m) in index order (c 16-byte aligned).  The loads of the next 32
+// terms are in flight while the current 32 are added.
+template <bool SUB>
+__device__ __forceinline__ double fold_run(double acc, const double* __restrict__ c, int m) {
+    constexpr int G = 16;  // double2 per group
+    const int g = m / (2 * G);
+    const double2* c2 = reinterpret_cast<const double2*>(c);
+    double2 nx[G];
+    if (g > 0) RSC_UNROLL for (int q = 0; q < G; ++q) nx[q] = c2[q];
+    for (int i = 0; i < g; ++i) {
+        double2 cu[G];
+        RSC_UNROLL for (int q = 0; q < G; ++q) cu[q] = nx[q];
+        if (i + 1 < g) RSC_UNROLL for (int q = 0; q < G; ++q) nx[q] = c2[G * (i + 1) + q];
+        RSC_UNROLL for (int q = 0; q < G; ++q) {
+            acc = SUB ? acc - cu[q].x : acc + cu[q].x;
+            acc = SUB ? acc - cu[q].y : acc + cu[q].y;
+        }
+    }
+    for (int r = g * 2 * G; r < m; ++r) acc = SUB ? acc - c[r] : acc + c[r];
+    return acc;
+}
+
+// Error of edge e at `est` (EdgeSE3ProjectXYZOnlyPose::computeError), stored as _error.
+__device__ __forceinline__ double2 po_edge_error(const DevPoseProb& P, int e, const PoSE3& est, const PoCam& K) {
+    const float4 xw = P.xw[e];
+    const float2 uv = P.uv[e];
+    const double X[3] = {(double)xw.x, (double)xw.y, (double)xw.z};
+    double e0, e1;
+    po_error(est, K, X, (double)uv.x, (double)uv.y, e0, e1);
+    const double2 er = make_double2(e0, e1);
+    P.err[e] = er;
+    return er;
+}
+
 // activeRobustChi2 after computeActiveErrors at `est` (sparse_optimizer.cpp:61-114): errors of the
-// level-0 edges are recomputed and stored, their robust chi2 terms folded in edge order.
-__device__ double po_chi_pass(const DevPoseProb& P, PoseShared& S, const PoSE3& est, const PoCam& K, bool robust,
+// level-0 edges recomputed and stored, their robust chi2 terms (0.0 for inactive edges — an exact
+// identity for a sum that starts at +0.0) folded in edge order by one lane.
+__device__ double po_chi_pass(const DevPoseProb& P, const PoseLds& S, const PoSE3& est, const PoCam& K, bool robust,
                               double delta, double dsqr) {
     const int tid = threadIdx.x;
-    double acc = 0.0;
-    for (int base = 0; base < P.n; base += kPoseThreads) {
-        const int e = base + tid;
+    for (int e = tid; e < P.n; e += kPoseChunk) {
         double t = 0.0;
-        if (e < P.n && S.lvl[e] == 0) {
-            const float4 xw = P.xw[e];
-            const float2 uv = P.uv[e];
-            const double X[3] = {(double)xw.x, (double)xw.y, (double)xw.z};
-            double e0, e1;
-            po_error(est, K, X, (double)uv.x, (double)uv.y, e0, e1);
-            P.err[e] = make_double2(e0, e1);
-            t = po_chi_term(robust, (double)xw.w, e0, e1, delta, dsqr);
+        if (S.lvl[e] == 0) {
+            const double2 er = po_edge_error(P, e, est, K);
+            t = po_chi_term(robust, (double)P.xw[e].w, er.x, er.y, delta, dsqr);
         }
-        S.terms[tid] = t;
-        __syncthreads();
-        if (tid == 0) {
-            const int m = min(kPoseThreads, P.n - base);
-            const double* c = S.terms;
-            int r = 0;
-            for (; r + 4 <= m; r += 4) {
-                const double a = c[r], b = c[r + 1], d = c[r + 2], f = c[r + 3];
-                acc = acc + a;
-                acc = acc + b;
-                acc = acc + d;
-                acc = acc + f;
-            }
-            for (; r < m; ++r) acc = acc + c[r];
-        }
-        __syncthreads();
+        S.terms[e] = t;
     }
-    if (tid == 0) S.red[0] = acc;
+    __syncthreads();
+    if (tid == 0) S.red[0] = fold_run<false>(0.0, S.terms, P.n);
     __syncthreads();
     const double chi = S.red[0];
     __syncthreads();
     return chi;
 }
 
-// BlockSolver::buildSystem (block_solver.hpp:502-560): H (lower triangle) and b, folded in edge
-// order on lanes 0..26 (H entries added, b entries subtracted, both from 0.0).
-__device__ void po_build_pass(const DevPoseProb& P, PoseShared& S, const PoSE3& est, const PoCam& K, bool robust,
-                              double delta, double dsqr, double (&H)[6][6], double (&b)[6]) {
+// computeActiveErrors (if `errors`) + activeRobustChi2 (if `chi`) + BlockSolver::buildSystem
+// (block_solver.hpp:502-560) in one pass over kPoseChunk-edge chunks: H lower triangle folded on
+// lanes 0..26 of wave 0 (added) and b (subtracted), both from 0.0; the chi2 column on wave 1.
+__device__ void po_build_pass(const DevPoseProb& P, const PoseLds& S, const PoSE3& est, const PoCam& K, bool robust,
+                              double delta, double dsqr, bool errors, bool chi, double (&H)[6][6], double (&b)[6],
+                              double& chi_out) {
     const int tid = threadIdx.x;
     double acc = 0.0;
-    for (int base = 0; base < P.n; base += kPoseThreads) {
+    for (int base = 0; base < P.n; base += kPoseChunk) {
         const int e = base + tid;
         double t[kPoseTerms];
         RSC_UNROLL for (int k = 0; k < kPoseTerms; ++k) t[k] = 0.0;
+        double tc = 0.0;
         if (e < P.n && S.lvl[e] == 0) {
+            const double2 er = errors ? po_edge_error(P, e, est, K) : P.err[e];
             const float4 xw = P.xw[e];
-            const double2 er = P.err[e];
             const double X[3] = {(double)xw.x, (double)xw.y, (double)xw.z};
             po_quad_terms(est, K, X, (double)xw.w, er.x, er.y, robust, delta, dsqr, t);
+            if (chi) tc = po_chi_term(robust, (double)xw.w, er.x, er.y, delta, dsqr);
         }
-        RSC_UNROLL for (int k = 0; k < kPoseTerms; ++k) S.terms[k * kPoseThreads + tid] = t[k];
+        RSC_UNROLL for (int k = 0; k < kPoseTerms; ++k) S.terms[k * kPoseCol + tid] = t[k];
+        if (chi) S.terms[kPoseTerms * kPoseCol + tid] = tc;
         __syncthreads();
+        const int m = min(kPoseChunk, P.n - base);
         if (tid < kPoseTerms) {
-            const int m = min(kPoseThreads, P.n - base);
-            const double* c = S.terms + tid * kPoseThreads;
-            const bool sub = tid >= 21;
-            int r = 0;
-            for (; r + 4 <= m; r += 4) {
-                const double a = c[r], bb = c[r + 1], d = c[r + 2], f = c[r + 3];
-                acc = sub ? acc - a : acc + a;
-                acc = sub ? acc - bb : acc + bb;
-                acc = sub ? acc - d : acc + d;
-                acc = sub ? acc - f : acc + f;
-            }
-            for (; r < m; ++r) acc = sub ? acc - c[r] : acc + c[r];
+            const double* c = S.terms + tid * kPoseCol;
+            acc = (tid >= 21) ? fold_run<true>(acc, c, m) : fold_run<false>(acc, c, m);
+        } else if (chi && tid == 64) {
+            acc = fold_run<false>(acc, S.terms + kPoseTerms * kPoseCol, m);
         }
         __syncthreads();
     }
     if (tid < kPoseTerms) S.red[tid] = acc;
+    if (chi && tid == 64) S.red[kPoseTerms] = acc;
     __syncthreads();
     int k = 0;
     RSC_UNROLL for (int i = 0; i < 6; ++i)
@@ -101,13 +131,17 @@ __device__ void po_build_pass(const DevPoseProb& P, PoseShared& S, const PoSE3& 
             H[j][i] = H[i][j];
         }
     RSC_UNROLL for (int i = 0; i < 6; ++i) b[i] = S.red[21 + i];
+    if (chi) chi_out = S.red[kPoseTerms];
     __syncthreads();
 }
 
 }  // namespace
 
-__global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb* __restrict__ probs) {
-    __shared__ PoseShared S;
+__global__ __launch_bounds__(kPoseChunk) void poseopt_kernel(const DevPoseProb* __restrict__ probs) {
+    extern __shared__ __attribute__((aligned(16))) double po_lds[];
+    __shared__ double red_sh[32];
+    __shared__ int nbad_sh;
+    const PoseLds S{po_lds, red_sh, reinterpret_cast<uint8_t*>(po_lds + kPoseTermDoubles), &nbad_sh};
     const DevPoseProb& P = probs[blockIdx.x];
     const int tid = threadIdx.x, n = P.n;
     const PoCam K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
@@ -120,11 +154,11 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
         t0[r] = (double)P.T[4 * r + 3];
     }
     const PoSE3 init = po_from_Rt(R0, t0);  // Converter::toSE3Quat (rotation() = linear(), Q14)
-    for (int e = tid; e < n; e += kPoseThreads) {
+    for (int e = tid; e < n; e += kPoseChunk) {
         S.lvl[e] = 0;
         P.outlier[e] = 0;
     }
-    if (tid == 0) S.nbad = 0;
+    if (tid == 0) *S.nbad = 0;
     __syncthreads();
 
     double x[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // BlockSolver::_x persists across rounds
@@ -136,16 +170,20 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
         rounds++;
         est = init;
         int mine = 0;
-        for (int e = tid; e < n; e += kPoseThreads) mine |= (S.lvl[e] == 0);
+        for (int e = tid; e < n; e += kPoseChunk) mine |= (S.lvl[e] == 0);
         const bool any = __syncthreads_or(mine) != 0;
         if (any) {
             bool ok = true;
+            double chiNow = 0.0;       // activeRobustChi2 at est, when chiKnown
+            bool chiKnown = false;     // (the previous solve's currentChi, computed at this est)
+            bool errorsAtEst = false;  // the stored _error values belong to est
             for (int i = 0; i < 10 && ok; ++i) {
                 lm_its++;
-                double currentChi = po_chi_pass(P, S, est, K, robust, delta, dsqr);
-                const double iniChi = currentChi;
                 double H[6][6], b[6];
-                po_build_pass(P, S, est, K, robust, delta, dsqr, H, b);
+                double chiFold = 0.0;
+                po_build_pass(P, S, est, K, robust, delta, dsqr, !errorsAtEst, !chiKnown, H, b, chiFold);
+                double currentChi = chiKnown ? chiNow : chiFold;
+                const double iniChi = currentChi;
                 if (i == 0) {
                     double maxDiagonal = 0.;
                     RSC_UNROLL for (int j = 0; j < 6; ++j) {  // std::max(fabs(H(j,j)), maxDiagonal)
@@ -158,6 +196,7 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
                 }
                 double rho = 0;
                 int qmax = 0;
+                bool chiReal = true;  // currentChi is a computed chi2 (not the DBL_MAX of a failed solve)
                 do {
                     lm_trials++;
                     const PoSE3 saved = est;
@@ -183,13 +222,18 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
                         lambda *= scaleFactor;
                         ni = 2;
                         currentChi = tempChi;
+                        chiReal = ok2;
+                        errorsAtEst = true;
                     } else {
                         lambda *= ni;
                         ni *= 2;
                         est = saved;
+                        errorsAtEst = false;
                     }
                     qmax++;
                 } while (rho < 0 && qmax < 10);
+                chiNow = currentChi;
+                chiKnown = chiReal;
                 if (qmax == 10 || rho == 0) {
                     ok = false;
                 } else {
@@ -201,28 +245,19 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
         }
         // re-classification (Optimizer.cpp:347-376)
         int cnt = 0;
-        for (int e = tid; e < n; e += kPoseThreads) {
-            double2 er;
-            if (S.lvl[e]) {
-                const float4 xw = P.xw[e];
-                const float2 uv = P.uv[e];
-                const double X[3] = {(double)xw.x, (double)xw.y, (double)xw.z};
-                po_error(est, K, X, (double)uv.x, (double)uv.y, er.x, er.y);
-                P.err[e] = er;
-            } else {
-                er = P.err[e];
-            }
+        for (int e = tid; e < n; e += kPoseChunk) {
+            const double2 er = S.lvl[e] ? po_edge_error(P, e, est, K) : P.err[e];
             const float c2 = (float)po_chi2((double)P.xw[e].w, er.x, er.y);
             const bool bad = c2 > chi2Mono;
             S.lvl[e] = bad ? 1 : 0;
             P.outlier[e] = bad ? 1 : 0;
             cnt += bad;
         }
-        if (cnt) atomicAdd(&S.nbad, cnt);
+        if (cnt) atomicAdd(S.nbad, cnt);
         __syncthreads();
-        nBad = S.nbad;
+        nBad = *S.nbad;
         __syncthreads();
-        if (tid == 0) S.nbad = 0;
+        if (tid == 0) *S.nbad = 0;
         if (it == 2) robust = false;
         if (n < 10) break;
     }
@@ -241,7 +276,14 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
 }
 
 hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st) {
-    poseopt_kernel<<<count, kPoseThreads, 0, st>>>(probs);
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&poseopt_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPoseLds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    poseopt_kernel<<<count, kPoseChunk, kPoseLds, st>>>(probs);
     return hipGetLastError();
 }
 

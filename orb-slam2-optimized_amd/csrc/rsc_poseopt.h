@@ -2,7 +2,7 @@
 // GPU: the g2o Levenberg-Marquardt of one VertexSE3Expmap over EdgeSE3ProjectXYZOnlyPose edges
 // with a Huber kernel, 4 rounds of 10 iterations with inlier/outlier re-classification.
 //
-// Mapping: one 256-thread workgroup per Frame (problem).  Threads own edges e = tid + 256 k and
+// Mapping: one 512-thread workgroup per Frame (problem).  Threads own edges e = tid + 512 k and
 // evaluate the per-edge work of a pass in parallel (error, robust chi2 term, Jacobian and its 27
 // Hessian/gradient terms); the reductions g2o performs as sequential loops over the active edges
 // (activeRobustChi2, buildSystem's H += J^T W J, b -= ...) are folded in edge order on one lane
@@ -22,7 +22,6 @@
 
 namespace rsc {
 
-constexpr int kPoseThreads = 256;
 constexpr int kPoseMaxEdges = 8192;  // LDS level flags per problem
 constexpr int kPoseTerms = 27;       // 21 lower-triangle H entries + 6 b entries
 

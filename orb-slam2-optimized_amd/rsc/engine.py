@@ -529,6 +529,47 @@ class EventBatch:
         return out
 
 
+class PoseOptBatch:
+    """Frames prepared once for repeated rsc_pose_optimization_many calls (the ctypes problem
+    records and contiguous arrays are built here, so a call is one C entry)."""
+
+    def __init__(self, ctx: Context, frames, with_outliers: bool = True):
+        self.ctx = ctx
+        self.frames = list(frames)
+        n = len(self.frames)
+        self.probs = (PoseOptProblem * max(n, 1))()
+        self.res = (PoseOptResult * max(n, 1))()
+        self.ptrs = (C.c_void_p * max(n, 1))()
+        self.keep, self.outs = [], []
+        for i, f in enumerate(self.frames):
+            arrs = [np.ascontiguousarray(f.has_mp, np.uint8), np.ascontiguousarray(f.uv, np.float32).reshape(-1),
+                    np.ascontiguousarray(f.Xw, np.float32).reshape(-1),
+                    np.ascontiguousarray(f.inv_sigma2, np.float32)]
+            self.keep.append(arrs)
+            p = self.probs[i]
+            p.n = f.n
+            p.has_mp, p.uv, p.Xw, p.inv_sigma2 = (a.ctypes.data for a in arrs)
+            p.u_right = None
+            p.fx, p.fy, p.cx, p.cy = float(f.fx), float(f.fy), float(f.cx), float(f.cy)
+            p.Tcw[:] = [float(v) for v in np.asarray(f.Tcw, np.float32).reshape(16)]
+            o = np.full(max(f.n, 1), 255, np.uint8)
+            self.outs.append(o)
+            self.ptrs[i] = o.ctypes.data if with_outliers else None
+
+    def run(self):
+        _check(load_library().rsc_pose_optimization_many(self.ctx.h, self.probs, len(self.frames), self.res,
+                                                         self.ptrs), "rsc_pose_optimization_many")
+
+    def results(self):
+        out = []
+        for i, f in enumerate(self.frames):
+            r = self.res[i]
+            out.append({"n_good": r.n_good, "n_initial": r.n_initial, "rounds": r.rounds,
+                        "lm_iterations": r.lm_iterations, "lm_trials": r.lm_trials,
+                        "Tcw": np.array(r.Tcw[:], np.float32).reshape(4, 4), "outlier": self.outs[i][:f.n].copy()})
+        return out
+
+
 def pose_optimization_many(ctx: Context, frames, with_outliers: bool = True):
     """Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) on every frame in one launch.
 
@@ -536,31 +577,6 @@ def pose_optimization_many(ctx: Context, frames, with_outliers: bool = True):
     per frame a dict: n_good (the reference's return value), n_initial, rounds, lm_iterations,
     lm_trials, Tcw float32[4,4] (pFrame->mTcw after the call), outlier uint8[n] (mvbOutlier; 255 on
     slots without a map point)."""
-    L = load_library()
-    n = len(frames)
-    probs = (PoseOptProblem * max(n, 1))()
-    res = (PoseOptResult * max(n, 1))()
-    keep = []
-    outs = []
-    ptrs = (C.c_void_p * max(n, 1))()
-    for i, f in enumerate(frames):
-        arrs = [np.ascontiguousarray(f.has_mp, np.uint8), np.ascontiguousarray(f.uv, np.float32).reshape(-1),
-                np.ascontiguousarray(f.Xw, np.float32).reshape(-1), np.ascontiguousarray(f.inv_sigma2, np.float32)]
-        keep.append(arrs)
-        p = probs[i]
-        p.n = f.n
-        p.has_mp, p.uv, p.Xw, p.inv_sigma2 = (a.ctypes.data for a in arrs)
-        p.u_right = None
-        p.fx, p.fy, p.cx, p.cy = float(f.fx), float(f.fy), float(f.cx), float(f.cy)
-        p.Tcw[:] = [float(v) for v in np.asarray(f.Tcw, np.float32).reshape(16)]
-        o = np.full(max(f.n, 1), 255, np.uint8)
-        outs.append(o)
-        ptrs[i] = o.ctypes.data if with_outliers else None
-    _check(L.rsc_pose_optimization_many(ctx.h, probs, n, res, ptrs), "rsc_pose_optimization_many")
-    out = []
-    for i, f in enumerate(frames):
-        r = res[i]
-        out.append({"n_good": r.n_good, "n_initial": r.n_initial, "rounds": r.rounds,
-                    "lm_iterations": r.lm_iterations, "lm_trials": r.lm_trials,
-                    "Tcw": np.array(r.Tcw[:], np.float32).reshape(4, 4), "outlier": outs[i][:f.n]})
-    return out
+    b = PoseOptBatch(ctx, frames, with_outliers)
+    b.run()
+    return b.results()

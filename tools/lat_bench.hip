@@ -21,6 +21,8 @@ __global__ __launch_bounds__(64) void chain(double* out, long long* cyc, int ite
             if (OP == 2) x[c] = sqrt(x[c]) + b;              // IEEE sqrt
             if (OP == 3) { double cc, ss; rsc::make_givens(x[c], b, cc, ss); x[c] = cc + ss + a; }
             if (OP == 4) x[c] = __builtin_fma(x[c], a, b);   // one FMA
+            if (OP == 8) { RSC_UNROLL for (int u = 0; u < 8; ++u) x[c] = x[c] + b; }   // 8 dependent adds
+            if (OP == 9) { float f = (float)x[c]; RSC_UNROLL for (int u = 0; u < 8; ++u) f = f + 0.5f; x[c] = f; }
             if (OP == 5) { float f = (float)x[c]; f = f * 1.0000001f + 0.5f; x[c] = f; }
         }
     }
@@ -65,6 +67,9 @@ int main() {
         run<3, 1>("make_givens chain", nwg);
         run<3, 4>("make_givens x4", nwg);
         run<5, 1>("f32 mul+add chain (+cvt)", nwg);
+        run<8, 1>("8 dependent f64 adds", nwg);
+        run<8, 2>("8 dep f64 adds x2 chains", nwg);
+        run<9, 1>("8 dependent f32 adds (+cvt)", nwg);
     }
     return 0;
 }
