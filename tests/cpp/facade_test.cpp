@@ -8,11 +8,12 @@
 #include <vector>
 #include "PnPsolver.hpp"
 #include "Sim3Solver.hpp"
+#include "Optimizer.hpp"
 #include "MLPnPsolver.hpp"
 
 struct Vec3 { float v[3]; float operator()(int i) const { return v[i]; } float& operator()(int i) { return v[i]; } };
 struct Mat3 { float m[3][3]; float operator()(int r, int c) const { return m[r][c]; } float& operator()(int r, int c) { return m[r][c]; } };
-struct Mat4 { float m[4][4]; float& operator()(int r, int c) { return m[r][c]; } };
+struct Mat4 { float m[4][4]; float& operator()(int r, int c) { return m[r][c]; } float operator()(int r, int c) const { return m[r][c]; } };
 struct Pt { float x, y; };
 struct KeyPoint { Pt pt; int octave; };
 struct Frame { std::vector<KeyPoint> mvKeysUn; std::vector<float> mvLevelSigma2; float fx, fy, cx, cy; };
@@ -31,6 +32,19 @@ struct KeyFrame {
     Vec3 GetTranslation() const { return t; }
 };
 int MapPoint::GetIndexInKeyFrame(const std::shared_ptr<KeyFrame>& kf) const { return kf.get() == kf1 ? idx1 : idx2; }
+
+// Frame as PoseOptimization sees it (include/Frame.hpp:52,131,142,145,153,169)
+struct PFrame {
+    std::vector<KeyPoint> mvKeysUn;
+    std::vector<std::shared_ptr<MapPoint>> mvpMapPoints;
+    std::vector<float> mvuRight;
+    std::vector<bool> mvbOutlier;
+    std::vector<float> mvInvLevelSigma2;
+    float fx, fy, cx, cy;
+    Mat4 mTcw;
+    int set_pose_calls = 0;
+    void SetPose(const Mat4& T) { mTcw = T; set_pose_calls++; }
+};
 
 template <class T> T rd(FILE* f) { T v; if (fread(&v, sizeof(T), 1, f) != 1) throw std::runtime_error("short read"); return v; }
 template <class T> void wr(FILE* f, T v) { fwrite(&v, sizeof(T), 1, f); }
@@ -80,6 +94,32 @@ int main(int argc, char** argv) {
             wr<int32_t>(out, (int32_t)inl.size());
             for (bool v : inl) wr<uint8_t>(out, v ? 1 : 0);
         }
+    } else if (mode == 4) {
+        // Optimizer::PoseOptimization on a mock Frame: n slots, fx..cy, Tcw, levels of
+        // mvInvLevelSigma2, per slot (present, u, v, octave, X, uR)
+        PFrame F;
+        const int n = rd<int32_t>(in);
+        F.fx = rd<float>(in); F.fy = rd<float>(in); F.cx = rd<float>(in); F.cy = rd<float>(in);
+        for (int r = 0; r < 4; ++r) for (int c = 0; c < 4; ++c) F.mTcw.m[r][c] = rd<float>(in);
+        const int nl = rd<int32_t>(in);
+        for (int l = 0; l < nl; ++l) F.mvInvLevelSigma2.push_back(rd<float>(in));
+        F.mvKeysUn.resize(n);
+        F.mvpMapPoints.resize(n);
+        F.mvuRight.resize(n);
+        F.mvbOutlier.assign(n, true);
+        for (int i = 0; i < n; ++i) {
+            const int present = rd<int32_t>(in);
+            KeyPoint k; k.pt.x = rd<float>(in); k.pt.y = rd<float>(in); k.octave = rd<int32_t>(in);
+            Vec3 X; X.v[0] = rd<float>(in); X.v[1] = rd<float>(in); X.v[2] = rd<float>(in);
+            F.mvuRight[i] = rd<float>(in);
+            F.mvKeysUn[i] = k;
+            if (present) { auto mp = std::make_shared<MapPoint>(); mp->X = X; F.mvpMapPoints[i] = mp; }
+        }
+        const int nGood = rsc_orb::PoseOptimization(&F);
+        wr<int32_t>(out, nGood);
+        wr<int32_t>(out, F.set_pose_calls);
+        for (int a = 0; a < 4; ++a) for (int b = 0; b < 4; ++b) wr<float>(out, F.mTcw.m[a][b]);
+        for (int i = 0; i < n; ++i) wr<uint8_t>(out, F.mvbOutlier[i] ? 1 : 0);
     } else if (mode == 2) {
         auto kf1 = std::make_shared<KeyFrame>(), kf2 = std::make_shared<KeyFrame>();
         const int n1 = rd<int32_t>(in);

@@ -159,3 +159,26 @@ def test_mlpnp_facade_matches_oracle():
             assert np.array_equal(mask, r["inliers"])
         else:
             assert ml == 0
+
+
+def test_pose_optimization_facade_matches_oracle():
+    """rsc_orb::PoseOptimization(Frame*) (Optimizer.cpp:205-424) on a mock Frame: slots without a
+    MapPoint keep mvbOutlier, SetPose is called once, nGood / pose / flags equal the oracle."""
+    rng = np.random.default_rng(31)
+    f = synth.make_poseopt_frame(rng, 900, 0.75, no_mp_frac=0.2)
+    inv_levels = (np.float32(1.0) / synth.level_sigma2()).astype(np.float32)
+    oc = np.array([int(np.where(inv_levels == v)[0][0]) for v in f.inv_sigma2])
+    buf = struct.pack("<i", 4) + struct.pack("<i4f", f.n, f.fx, f.fy, f.cx, f.cy)
+    buf += f.Tcw.astype("<f4").tobytes() + struct.pack("<i", len(inv_levels)) + inv_levels.astype("<f4").tobytes()
+    for i in range(f.n):
+        buf += struct.pack("<i2fi3ff", int(f.has_mp[i]), f.uv[i, 0], f.uv[i, 1], oc[i], *f.Xw[i], -1.0)
+    out = run(buf)
+    n_good, calls = struct.unpack_from("<ii", out, 0)
+    T = np.frombuffer(out, "<f4", 16, 8).reshape(4, 4)
+    flags = np.frombuffer(out, np.uint8, f.n, 8 + 64)
+    r, To, outl, st = ol.pose_optimization(f)
+    assert n_good == r and calls == 1
+    assert np.array_equal(bits(T), bits(To))
+    sel = f.has_mp == 1
+    assert np.array_equal(flags[sel], outl[sel])
+    assert (flags[~sel] == 1).all()  # untouched (the mock starts them at true)
