@@ -19,11 +19,15 @@ $(LIBDIR)/poseopt.o: $(CSRC)/poseopt.hip $(HDRS)
 	mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(LIBDIR)/orbmatch.o: $(CSRC)/orbmatch.hip $(HDRS)
+	mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(LIBDIR)/rsc_api.o: $(CSRC)/rsc_api.cpp $(HDRS)
 	mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIBDIR)/librsc.so: $(LIBDIR)/kernels.o $(LIBDIR)/poseopt.o $(LIBDIR)/rsc_api.o
+$(LIBDIR)/librsc.so: $(LIBDIR)/kernels.o $(LIBDIR)/poseopt.o $(LIBDIR)/orbmatch.o $(LIBDIR)/rsc_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 facade_test: $(LIBDIR)/facade_test

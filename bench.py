@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--no-mlpnp", action="store_true")
     p.add_argument("--no-events", action="store_true")
     p.add_argument("--no-poseopt", action="store_true")
+    p.add_argument("--no-bow", action="store_true")
     return p.parse_args()
 
 
@@ -293,6 +294,87 @@ def run_poseopt(engine, ctx, frames, args):
                 steps=steps)
 
 
+def bow_views(rng, C=64, N=2000):
+    """Relocalization-shaped SearchByBoW input: the current Frame (N features) and C candidate
+    KeyFrames sharing 10-70 % of its features (Tracking.cpp:1207-1214)."""
+    from rsc import synth
+    F = synth.make_bow_view(rng, N)
+    kfs = [synth.make_bow_related(rng, F, N, float(rng.uniform(0.1, 0.7)), float(rng.uniform(0, 360)),
+                                  mean_flips=float(rng.uniform(8, 30))) for _ in range(C)]
+    return F, kfs
+
+
+def bow_comparisons(F, kfs):
+    """Descriptor comparisons the reference's SearchByBoW(pKF, F) walk can make: sum over common
+    nodes of (#valid KF features) x (#Frame features) — an upper bound (matched Frame features are
+    skipped)."""
+    fsz = dict(zip(F.node_id.tolist(), np.diff(F.node_begin).tolist()))
+    tot = 0
+    for k in kfs:
+        for j, nid in enumerate(k.node_id.tolist()):
+            if nid in fsz:
+                tot += int(k.valid[k.feat[k.node_begin[j]:k.node_begin[j + 1]]].sum()) * fsz[nid]
+    return tot
+
+
+def run_bow(engine, ctx, F, kfs, args):
+    """SURVEY §8(f) row 2: ORBmatcher::SearchByBoW(pKF, F) of 64 candidate KeyFrames against the
+    current Frame (2000 features each, ORBmatcher(0.75, true) as in Tracking.cpp:1212), views
+    resident in HBM; one rsc_search_by_bow_frame_many per step."""
+    gF = engine.BowView(ctx, F)
+    gK = [engine.BowView(ctx, k) for k in kfs]
+    batch = engine.BowSearch(ctx, gF, gK, True, 0.75, True)
+    for _ in range(args.warmup):
+        batch.run()
+    ctx.synchronize()
+    steps = max(1, args.steps)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _, nm = batch.run()
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    ctx.enable_timing(True)
+    kms = 0.0
+    for _ in range(steps):
+        batch.run()
+        kms += ctx.last_timing()["refine_ms"]
+    ctx.enable_timing(False)
+    kms /= steps
+    cmp = bow_comparisons(F, kfs)
+    C = len(kfs)
+    # algorithmic bytes per launch: every descriptor row of both views once (32 B) + angle (4 B) +
+    # FeatureVector index (4 B) + validity (1 B) per feature, + the int32 output vector
+    algo = C * (F.n + kfs[0].n) * 41 + C * F.n * 4
+    return dict(pairs_per_s=C * steps / dt, ms_per_step=1e3 * dt / steps, kernel_ms=kms, pairs=C,
+                features=F.n, comparisons_per_pair=cmp / C, comparisons_per_s=cmp / (kms * 1e-3) if kms else None,
+                mean_matches=float(np.mean(nm)), algorithmic_bytes_per_launch=algo,
+                hbm_frac=(algo / (kms * 1e-3) / 1e9) / HBM_PEAK_GBS if kms else None, steps=steps)
+
+
+def cpu_baseline_bow(F, kfs, seconds):
+    """The SearchByBoW oracle (std::map FeatureVector walk, as the reference) on ONE host core."""
+    import ctypes
+    import oracle_lib as ol
+    L = ol.lib()
+    oF = ol.OracleBow(F)
+    oK = [ol.OracleBow(k) for k in kfs]
+    C = len(kfs)
+    hs = (ctypes.c_void_p * C)(*[o.h for o in oK])
+    out = np.zeros((C, F.n), np.int32)
+    nm = np.zeros(C, np.int32)
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        L.ora_search_by_bow_many(1, C, hs, oF.h, 0.75, 1, out.reshape(-1), F.n, nm)
+        done += C
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=round(done / dt, 2), unit="pairs/s", cores=1, kind="port",
+                sample=f"{done // C} batches of {C} KeyFrame x Frame searches ({F.n} features) in {dt:.1f} s, "
+                       "oracle restatement, 1 thread")
+
+
 def cpu_baseline_poseopt(frames, seconds):
     """The PoseOptimization oracle on ONE host core over the same frames."""
     import oracle_lib as ol
@@ -379,6 +461,10 @@ def main():
     if rank == 0 and not args.no_poseopt:
         po_frames = poseopt_frames(np.random.default_rng(79))
         poseopt = run_poseopt(engine, ctx, po_frames, args)
+    bow = bow_F = bow_K = None
+    if rank == 0 and not args.no_bow:
+        bow_F, bow_K = bow_views(np.random.default_rng(80))
+        bow = run_bow(engine, ctx, bow_F, bow_K, args)
     if rank != 0:
         if dist is not None:
             dist.barrier()
@@ -447,6 +533,12 @@ def main():
             cb = cpu_baseline_poseopt(po_frames, min(3.0, args.cpu_seconds))
             out["poseopt"]["cpu_baseline"] = cb
             out["poseopt"]["speedup_vs_cpu_1core"] = round(poseopt["poses_per_s"] / cb["value"], 1)
+    if bow is not None:
+        out["search_by_bow"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in bow.items()}
+        if not args.no_cpu and world == 1:
+            cb = cpu_baseline_bow(bow_F, bow_K, min(3.0, args.cpu_seconds))
+            out["search_by_bow"]["cpu_baseline"] = cb
+            out["search_by_bow"]["speedup_vs_cpu_1core"] = round(bow["pairs_per_s"] / cb["value"], 1)
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(scenes, args)
         out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 1)

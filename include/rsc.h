@@ -229,6 +229,46 @@ typedef struct {
 int rsc_pose_optimization_many(rsc_context* ctx, const rsc_poseopt_problem* problems, int count,
                                rsc_poseopt_result* out, uint8_t* const* outlier);
 
+/* ---- ORBmatcher::SearchByBoW (src/ORBmatcher.cpp:110-240, :354-488) -----------------------------
+ * The producer of every RANSAC correspondence set: Hamming-256 matching of ORB descriptors that
+ * share a DBoW2 FeatureVector node, with the nearest-neighbour ratio test and the rotation-histogram
+ * consistency check.  Views (KeyFrames, the current Frame) are uploaded once and stay resident in
+ * HBM; searches name them by handle.  Integer work: results are bit-exact with the reference. */
+typedef struct {
+    int32_t n;                 /* keypoints (KeyFrame::N / Frame::N), <= 8192 */
+    const uint8_t* desc;       /* [n][32] mDescriptors rows (CV_8U, 32 columns) */
+    const float* angle;        /* [n] keypoint angle: mvKeysUn[i].angle for a KeyFrame, mvKeys[i].angle for
+                                  the Frame (the angles the two overloads read, ORBmatcher.cpp:185,435) */
+    const uint8_t* valid;      /* [n] GetMapPointMatches()[i] != NULL && !isBad(); NULL = all.
+                                  Unused for the Frame side of the Frame overload. */
+    int32_t n_nodes;           /* mFeatVec.size() */
+    const uint32_t* node_id;   /* [n_nodes] mFeatVec keys, strictly ascending (std::map order) */
+    const int32_t* node_begin; /* [n_nodes + 1] CSR offsets into feat */
+    const uint32_t* feat;      /* [node_begin[n_nodes]] each node's vector<unsigned int>, in order; every
+                                  feature index < n and at most once overall (DBoW2 transform) */
+} rsc_bow_features;
+
+typedef struct rsc_bow rsc_bow;
+
+/* Upload a view's descriptors, angles, map-point validity and FeatureVector (KeyFrame::mFeatVec /
+ * Frame::mFeatVec after ComputeBoW) to HBM. */
+int rsc_bow_create(rsc_context* ctx, const rsc_bow_features* features, rsc_bow** out);
+void rsc_bow_destroy(rsc_bow* view);
+/* Refresh the map-point validity of a resident view (map points culled or replaced since upload). */
+int rsc_bow_set_valid(rsc_bow* view, const uint8_t* valid);
+
+/* SearchByBoW(pKF = kfs[c], F = frame, vpMapPointMatches) for c < count in one launch (the
+ * relocalization candidate loop, Tracking.cpp:1207-1232).  matches[c][i] (i < frame->n) = the
+ * KeyFrame feature whose map point matched Frame feature i (vpMapPointMatches[i] =
+ * kf.GetMapPointMatches()[matches[c][i]]), or -1; nmatches[c] = the return value. */
+int rsc_search_by_bow_frame_many(rsc_context* ctx, rsc_bow* const* kfs, int count, const rsc_bow* frame,
+                                 float nnratio, int check_orientation, int32_t* const* matches, int32_t* nmatches);
+/* SearchByBoW(pKF1 = kf1, pKF2 = kf2s[c], vpMatches12) for c < count in one launch (the loop
+ * candidate loop, LoopClosing.cpp:238-265).  matches12[c][i] (i < kf1->n) = the KF2 feature whose
+ * map point vpMatches12[i] is, or -1; nmatches[c] = the return value. */
+int rsc_search_by_bow_kf_many(rsc_context* ctx, const rsc_bow* kf1, rsc_bow* const* kf2s, int count,
+                              float nnratio, int check_orientation, int32_t* const* matches12, int32_t* nmatches);
+
 /* ---- glibc rand() helpers (Thirdparty/DBoW2/DUtils/Random.cpp:33-50) -------------------------- */
 /* First n rand() outputs after srand(seed), produced with the device jump table (parity hook). */
 int rsc_rand_stream(rsc_context* ctx, uint32_t seed, int n, int32_t* out);

@@ -11,6 +11,7 @@
 #include "sim3_oracle.h"
 #include "mlpnp_oracle.h"
 #include "poseopt_oracle.h"
+#include "orbmatch_oracle.h"
 #include "../orb-slam2-optimized_amd/csrc/rsc_math.h"
 #include "ora_linalg.h"
 
@@ -445,5 +446,59 @@ void ora_pose_optimization_batch(int count, const int64_t* off, const float* uv,
         std::memcpy(in.Tcw, Tcw_in + 16 * c, sizeof(in.Tcw));
         n_good[c] = pose_optimization(in, Tcw_out + 16 * c, outlier + o, nullptr);
     }
+}
+
+// ---- ORBmatcher::SearchByBoW (ORBmatcher.cpp:110-240, :354-488) ----
+// a BowView with its FeatureVector rebuilt from CSR (node ids ascending, node_begin[nn+1], feat);
+// arrays are copied so the handle owns its data
+struct OraBow {
+    std::vector<uint8_t> desc, valid;
+    std::vector<float> angle;
+    BowView v;
+};
+
+void* ora_bow_create(int n, const uint8_t* desc, const float* angle, const uint8_t* valid, int n_nodes,
+                     const uint32_t* node_id, const int32_t* node_begin, const uint32_t* feat) {
+    OraBow* b = new OraBow;
+    b->desc.assign(desc, desc + 32 * (size_t)n);
+    b->angle.assign(angle, angle + n);
+    if (valid) b->valid.assign(valid, valid + n);
+    b->v.n = n;
+    b->v.desc = b->desc.data();
+    b->v.angle = b->angle.data();
+    b->v.valid = valid ? b->valid.data() : nullptr;
+    for (int k = 0; k < n_nodes; ++k)
+        b->v.fv[node_id[k]].assign(feat + node_begin[k], feat + node_begin[k + 1]);
+    return b;
+}
+
+void ora_bow_destroy(void* h) { delete static_cast<OraBow*>(h); }
+
+// frame_variant = 1: SearchByBoW(pKF = a, F = b), out[b.n]; 0: SearchByBoW(pKF1 = a, pKF2 = b), out[a.n]
+int ora_search_by_bow(int frame_variant, void* a, void* b, float nnratio, int check_ori, int32_t* out) {
+    const BowView& A = static_cast<OraBow*>(a)->v;
+    const BowView& B = static_cast<OraBow*>(b)->v;
+    return frame_variant ? search_by_bow_frame(A, B, nnratio, check_ori != 0, out)
+                         : search_by_bow_kf(A, B, nnratio, check_ori != 0, out);
+}
+
+// `count` searches of a[c] against the shared b (the relocalization / loop-closure candidate loops,
+// Tracking.cpp:1207-1232, LoopClosing.cpp:238-265); out rows of out_stride; returns total matches
+int64_t ora_search_by_bow_many(int frame_variant, int count, void* const* a, void* b, float nnratio,
+                               int check_ori, int32_t* out, int64_t out_stride, int32_t* nmatches) {
+    int64_t tot = 0;
+    for (int c = 0; c < count; ++c) {
+        nmatches[c] = ora_search_by_bow(frame_variant, a[c], b, nnratio, check_ori, out + out_stride * c);
+        tot += nmatches[c];
+    }
+    return tot;
+}
+
+int ora_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descriptor_distance(a, b); }
+
+void ora_compute_three_maxima(const int32_t* sizes, int L, int32_t* ind) {
+    int i1 = -1, i2 = -1, i3 = -1;
+    compute_three_maxima(sizes, L, i1, i2, i3);
+    ind[0] = i1; ind[1] = i2; ind[2] = i3;
 }
 }  // extern "C"

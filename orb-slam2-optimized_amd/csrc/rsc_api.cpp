@@ -18,6 +18,7 @@
 #include "rsc_kernels.h"
 #include "rsc_engine.h"
 #include "rsc_poseopt.h"
+#include "rsc_orbmatch.h"
 
 using namespace rsc;
 
@@ -122,6 +123,9 @@ struct rsc_context {
     DevBuf<char> d_po_res;
     PinBuf<char> h_po_in;
     PinBuf<char> h_po_res;
+    // SearchByBoW: pair table + output vectors + match counts (device, pinned mirror)
+    DevBuf<char> d_bow;
+    PinBuf<char> h_bow;
     int mask_words = 0;  // per hypothesis, last speculation
     bool keep_samples = true;
     // PnP hypothesis kernels ($RSC_SOLVE_MODE): 0 = auto, 1 = "mono" (one kernel, lane per
@@ -1215,6 +1219,188 @@ int rsc_pose_optimization_many(rsc_context* C, const rsc_poseopt_problem* P, int
 }
 
 // ---- RNG parity hook ----
+
+// ---- ORBmatcher::SearchByBoW (src/ORBmatcher.cpp:110-240, :354-488) ----
+struct rsc_bow {
+    rsc_context* ctx = nullptr;
+    int n = 0;
+    int n_nodes = 0;
+    int n_feat = 0;
+    DevBuf<char> mem;            // DevBow header | desc | angle | node_id | node_begin | feat
+    size_t off_feat = 0;
+    std::vector<uint32_t> feat;  // host copy of the FeatureVector entries (validity flags re-applied)
+    const DevBow* hdr = nullptr;
+};
+
+namespace {
+size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+void flag_invalid(std::vector<uint32_t>& feat, const uint8_t* valid) {
+    for (uint32_t& x : feat) {
+        x &= ~kBowInvalid;
+        if (valid && !valid[x]) x |= kBowInvalid;
+    }
+}
+}  // namespace
+
+int rsc_bow_create(rsc_context* C, const rsc_bow_features* f, rsc_bow** out) {
+    if (!C || !f || !out) return RSC_ERR_ARG;
+    *out = nullptr;
+    const int n = f->n, nn = f->n_nodes;
+    if (n < 0 || nn < 0 || (n > 0 && (!f->desc || !f->angle)) || (nn > 0 && (!f->node_id || !f->node_begin || !f->feat)))
+        return RSC_ERR_ARG;
+    if (n > kBowMaxFeatures || nn > kBowMaxFeatures) {
+        g_last_error = "more than 8192 keypoints (or FeatureVector nodes) in one view";
+        return RSC_ERR_UNSUPPORTED;
+    }
+    // FeatureVector invariants the node-parallel walk relies on (DBoW2 transform guarantees them)
+    const int nf = nn ? f->node_begin[nn] : 0;
+    if (nn && f->node_begin[0] != 0) return RSC_ERR_ARG;
+    std::vector<uint8_t> seen((size_t)n, 0);
+    for (int k = 0; k < nn; ++k) {
+        if (f->node_begin[k + 1] < f->node_begin[k]) return RSC_ERR_ARG;
+        if (k && f->node_id[k] <= f->node_id[k - 1]) {
+            g_last_error = "FeatureVector node ids must be strictly ascending";
+            return RSC_ERR_ARG;
+        }
+    }
+    for (int i = 0; i < nf; ++i) {
+        const uint32_t x = f->feat[i];
+        if (x >= (uint32_t)n || seen[x]) {
+            g_last_error = "FeatureVector feature index out of range or repeated";
+            return RSC_ERR_ARG;
+        }
+        seen[x] = 1;
+    }
+    std::unique_ptr<rsc_bow> b(new rsc_bow);
+    b->ctx = C;
+    b->n = n;
+    b->n_nodes = nn;
+    b->n_feat = nf;
+    b->feat.assign(f->feat, f->feat + nf);
+    flag_invalid(b->feat, f->valid);
+    const size_t o_desc = al256(sizeof(DevBow)), o_ang = o_desc + al256(32 * (size_t)n);
+    const size_t o_id = o_ang + al256(4 * (size_t)n), o_beg = o_id + al256(4 * (size_t)nn);
+    const size_t o_feat = o_beg + al256(4 * ((size_t)nn + 1));
+    const size_t bytes = o_feat + al256(4 * (size_t)nf);
+    RSC_HIP(hipSetDevice(C->device));
+    if (int e = b->mem.ensure(bytes)) return e;
+    std::vector<char> h(bytes, 0);
+    char* d = b->mem.p;
+    DevBow hd;
+    hd.desc = reinterpret_cast<const uint4*>(d + o_desc);
+    hd.angle = reinterpret_cast<const float*>(d + o_ang);
+    hd.node_id = reinterpret_cast<const uint32_t*>(d + o_id);
+    hd.node_begin = reinterpret_cast<const int32_t*>(d + o_beg);
+    hd.feat = reinterpret_cast<const uint32_t*>(d + o_feat);
+    hd.n = n;
+    hd.n_nodes = nn;
+    std::memcpy(h.data(), &hd, sizeof(hd));
+    if (n) {
+        std::memcpy(h.data() + o_desc, f->desc, 32 * (size_t)n);
+        std::memcpy(h.data() + o_ang, f->angle, 4 * (size_t)n);
+    }
+    if (nn) {
+        std::memcpy(h.data() + o_id, f->node_id, 4 * (size_t)nn);
+        std::memcpy(h.data() + o_beg, f->node_begin, 4 * ((size_t)nn + 1));
+        if (nf) std::memcpy(h.data() + o_feat, b->feat.data(), 4 * (size_t)nf);
+    }
+    RSC_HIP(hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice));
+    b->off_feat = o_feat;
+    b->hdr = reinterpret_cast<const DevBow*>(d);
+    *out = b.release();
+    return RSC_OK;
+}
+
+void rsc_bow_destroy(rsc_bow* b) {
+    if (!b) return;
+    // searches already enqueued on the context stream may still read the view
+    (void)hipStreamSynchronize(b->ctx->stream);
+    delete b;
+}
+
+int rsc_bow_set_valid(rsc_bow* b, const uint8_t* valid) {
+    if (!b || (b->n && !valid)) return RSC_ERR_ARG;
+    if (!b->n_feat) return RSC_OK;
+    flag_invalid(b->feat, valid);
+    RSC_HIP(hipStreamSynchronize(b->ctx->stream));
+    RSC_HIP(hipMemcpy(b->mem.p + b->off_feat, b->feat.data(), 4 * (size_t)b->n_feat, hipMemcpyHostToDevice));
+    return RSC_OK;
+}
+
+namespace {
+// pairs[c] = (outer[c], inner[c]); out rows of out_n[c] int32 each
+int bow_search(rsc_context* C, bool frame_overload, const rsc_bow* const* outer, const rsc_bow* const* inner,
+               int count, float nnratio, int check_ori, int32_t* const* out, int32_t* nmatches) {
+    std::vector<size_t> ooff(count + 1, 0), roff(count + 1, 0), joff(count + 1, 0), toff(count + 1, 0);
+    for (int c = 0; c < count; ++c) {
+        if (!outer[c] || !inner[c] || outer[c]->ctx != C || inner[c]->ctx != C) return RSC_ERR_ARG;
+        const int on = frame_overload ? inner[c]->n : outer[c]->n;
+        if (on && !out[c]) return RSC_ERR_ARG;
+        ooff[c + 1] = ooff[c] + al256(4 * (size_t)on);
+        roff[c + 1] = roff[c] + (size_t)outer[c]->n_feat;
+        joff[c + 1] = joff[c] + (size_t)outer[c]->n_nodes;
+        toff[c + 1] = toff[c] + (size_t)outer[c]->n_nodes + (size_t)outer[c]->n_feat / 64 + 1;
+    }
+    const size_t o_pairs = 0, o_cnt = al256(sizeof(BowPair) * count), o_out = o_cnt + al256(4 * (size_t)count);
+    const size_t o_rec = o_out + ooff[count], o_nodes = o_rec + al256(16 * roff[count]);
+    const size_t o_tasks = o_nodes + al256(16 * joff[count]), o_nt = o_tasks + al256(16 * toff[count]);
+    const size_t bytes = o_nt + al256(8 * (size_t)count);
+    const size_t back = o_rec;  // counts + outputs come back
+    RSC_HIP(hipSetDevice(C->device));
+    if (int e = C->d_bow.ensure(bytes)) return e;
+    if (int e = C->h_bow.ensure(back)) return e;
+    RSC_HIP(hipStreamSynchronize(C->stream));  // the pinned mirror is free again
+    char* d = C->d_bow.p;
+    BowPair* hp = reinterpret_cast<BowPair*>(C->h_bow.p + o_pairs);
+    for (int c = 0; c < count; ++c) {
+        hp[c].outer = outer[c]->hdr;
+        hp[c].inner = inner[c]->hdr;
+        hp[c].rec = reinterpret_cast<uint4*>(d + o_rec) + roff[c];
+        hp[c].nodes = reinterpret_cast<int4*>(d + o_nodes) + joff[c];
+        hp[c].tasks = reinterpret_cast<int4*>(d + o_tasks) + toff[c];
+        hp[c].ntasks = reinterpret_cast<int32_t*>(d + o_nt) + 2 * c;
+        hp[c].out = reinterpret_cast<int32_t*>(d + o_out + ooff[c]);
+        hp[c].nmatches = reinterpret_cast<int32_t*>(d + o_cnt) + c;
+    }
+    RSC_HIP(hipMemcpyAsync(d, C->h_bow.p, o_cnt, hipMemcpyHostToDevice, C->stream));
+    timing_begin(C, 3);
+    RSC_HIP(launch_bow_search(frame_overload, count, reinterpret_cast<const BowPair*>(d + o_pairs), nnratio,
+                              check_ori ? 1 : 0, C->stream));
+    timing_begin(C, 4);
+    RSC_HIP(hipMemcpyAsync(C->h_bow.p + o_cnt, d + o_cnt, back - o_cnt, hipMemcpyDeviceToHost, C->stream));
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    if (C->timing) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, C->ev[3], C->ev[4]);
+        C->last_ms[2] = ms;
+    }
+    const int32_t* hc = reinterpret_cast<const int32_t*>(C->h_bow.p + o_cnt);
+    for (int c = 0; c < count; ++c) {
+        const int on = frame_overload ? inner[c]->n : outer[c]->n;
+        if (on) std::memcpy(out[c], C->h_bow.p + o_out + ooff[c], 4 * (size_t)on);
+        if (nmatches) nmatches[c] = hc[c];
+    }
+    return RSC_OK;
+}
+}  // namespace
+
+int rsc_search_by_bow_frame_many(rsc_context* C, rsc_bow* const* kfs, int count, const rsc_bow* frame, float nnratio,
+                                 int check_orientation, int32_t* const* matches, int32_t* nmatches) {
+    if (!C || count < 0 || (count && (!kfs || !frame || !matches))) return RSC_ERR_ARG;
+    if (count == 0) return RSC_OK;
+    std::vector<const rsc_bow*> inner((size_t)count, frame);
+    return bow_search(C, true, kfs, inner.data(), count, nnratio, check_orientation, matches, nmatches);
+}
+
+int rsc_search_by_bow_kf_many(rsc_context* C, const rsc_bow* kf1, rsc_bow* const* kf2s, int count, float nnratio,
+                              int check_orientation, int32_t* const* matches12, int32_t* nmatches) {
+    if (!C || count < 0 || (count && (!kf1 || !kf2s || !matches12))) return RSC_ERR_ARG;
+    if (count == 0) return RSC_OK;
+    std::vector<const rsc_bow*> outer((size_t)count, kf1);
+    return bow_search(C, false, outer.data(), kf2s, count, nnratio, check_orientation, matches12, nmatches);
+}
+
 int rsc_rand_stream(rsc_context* C, uint32_t seed, int n, int32_t* out) {
     if (!C || !out || n < 0) return RSC_ERR_ARG;
     if (n == 0) return RSC_OK;

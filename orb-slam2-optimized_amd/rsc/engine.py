@@ -38,6 +38,8 @@ EXPORTED = [
     "rsc_mlpnp_set_ransac_parameters_many", "rsc_mlpnp_iterate", "rsc_mlpnp_iterate_many", "rsc_mlpnp_reset",
     "rsc_mlpnp_reset_many", "rsc_mlpnp_get_state", "rsc_mlpnp_last_poses", "rsc_mlpnp_last_samples",
     "rsc_reloc_events", "rsc_loop_events", "rsc_pose_optimization_many",
+    "rsc_bow_create", "rsc_bow_destroy", "rsc_bow_set_valid", "rsc_search_by_bow_frame_many",
+    "rsc_search_by_bow_kf_many",
 ]
 
 
@@ -71,6 +73,11 @@ class PoseOptProblem(C.Structure):
     _fields_ = [("n", C.c_int32), ("has_mp", C.c_void_p), ("uv", C.c_void_p), ("Xw", C.c_void_p),
                 ("inv_sigma2", C.c_void_p), ("u_right", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float),
                 ("cx", C.c_float), ("cy", C.c_float), ("Tcw", C.c_float * 16)]
+
+
+class BowFeatures(C.Structure):
+    _fields_ = [("n", C.c_int32), ("desc", C.c_void_p), ("angle", C.c_void_p), ("valid", C.c_void_p),
+                ("n_nodes", C.c_int32), ("node_id", C.c_void_p), ("node_begin", C.c_void_p), ("feat", C.c_void_p)]
 
 
 class PoseOptResult(C.Structure):
@@ -140,6 +147,13 @@ def load_library(path: str = LIB_PATH):
     L.rsc_reloc_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(PnPResult), C.POINTER(EventResult)]
     L.rsc_pose_optimization_many.argtypes = [vp, C.POINTER(PoseOptProblem), C.c_int, C.POINTER(PoseOptResult),
                                              C.POINTER(C.c_void_p)]
+    L.rsc_bow_create.argtypes = [vp, C.POINTER(BowFeatures), C.POINTER(vp)]
+    L.rsc_bow_destroy.argtypes = [vp]
+    L.rsc_bow_set_valid.argtypes = [vp, u8p]
+    L.rsc_search_by_bow_frame_many.argtypes = [vp, C.POINTER(vp), C.c_int, vp, C.c_float, C.c_int,
+                                               C.POINTER(C.c_void_p), i32p]
+    L.rsc_search_by_bow_kf_many.argtypes = [vp, vp, C.POINTER(vp), C.c_int, C.c_float, C.c_int,
+                                            C.POINTER(C.c_void_p), i32p]
     L.rsc_loop_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(Sim3Result), C.POINTER(EventResult)]
     L.rsc_diag_pnp_phase_stamps.argtypes = [C.POINTER(vp), C.c_int, C.c_int,
                                             np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
@@ -580,3 +594,85 @@ def pose_optimization_many(ctx: Context, frames, with_outliers: bool = True):
     b = PoseOptBatch(ctx, frames, with_outliers)
     b.run()
     return b.results()
+
+
+class BowView:
+    """A KeyFrame's / Frame's ORB features resident in HBM for ORBmatcher::SearchByBoW: descriptors
+    (mDescriptors), keypoint angles, map-point validity and the DBoW2 FeatureVector (mFeatVec) as
+    CSR (rsc_bow_features, include/rsc.h).  `view` is an object with n, desc uint8[n,32],
+    angle float32[n], valid uint8[n] (or None), node_id uint32[], node_begin int32[], feat uint32[]
+    (rsc.synth.BowFeatures)."""
+
+    def __init__(self, ctx: Context, view):
+        self.ctx = ctx
+        self.n = int(view.n)
+        arrs = [np.ascontiguousarray(view.desc, np.uint8).reshape(-1), np.ascontiguousarray(view.angle, np.float32),
+                None if view.valid is None else np.ascontiguousarray(view.valid, np.uint8),
+                np.ascontiguousarray(view.node_id, np.uint32), np.ascontiguousarray(view.node_begin, np.int32),
+                np.ascontiguousarray(view.feat, np.uint32)]
+        f = BowFeatures()
+        f.n = self.n
+        f.desc, f.angle = arrs[0].ctypes.data, arrs[1].ctypes.data
+        f.valid = None if arrs[2] is None else arrs[2].ctypes.data
+        f.n_nodes = len(arrs[3])
+        f.node_id, f.node_begin, f.feat = arrs[3].ctypes.data, arrs[4].ctypes.data, arrs[5].ctypes.data
+        h = C.c_void_p()
+        _check(load_library().rsc_bow_create(ctx.h, C.byref(f), C.byref(h)), "rsc_bow_create")
+        self.h = h
+
+    def set_valid(self, valid):
+        _check(load_library().rsc_bow_set_valid(self.h, np.ascontiguousarray(valid, np.uint8)), "rsc_bow_set_valid")
+
+    def close(self):
+        if getattr(self, "h", None):
+            load_library().rsc_bow_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+class BowSearch:
+    """Prepared SearchByBoW batch (ORBmatcher.cpp:110-240 / :354-488): `count` searches in one launch.
+
+    frame_overload=True: SearchByBoW(pKF = others[c], F = shared) -> rows of shared.n (KeyFrame index
+    per Frame feature).  False: SearchByBoW(pKF1 = shared, pKF2 = others[c]) -> rows of shared.n
+    (KF2 index per KF1 feature)."""
+
+    def __init__(self, ctx: Context, shared: BowView, others, frame_overload: bool, nnratio: float = 0.75,
+                 check_orientation: bool = True):
+        self.ctx, self.shared, self.others = ctx, shared, list(others)
+        self.frame_overload = frame_overload
+        self.nnratio, self.check = float(nnratio), int(bool(check_orientation))
+        c = len(self.others)
+        self.handles = (C.c_void_p * max(c, 1))(*[o.h for o in self.others])
+        self.out = np.zeros((max(c, 1), max(shared.n, 1)), np.int32)
+        self.ptrs = (C.c_void_p * max(c, 1))(*[self.out[i].ctypes.data for i in range(c)])
+        self.nmatches = np.zeros(max(c, 1), np.int32)
+
+    def run(self):
+        L = load_library()
+        c = len(self.others)
+        if self.frame_overload:
+            st = L.rsc_search_by_bow_frame_many(self.ctx.h, self.handles, c, self.shared.h, self.nnratio, self.check,
+                                                self.ptrs, self.nmatches)
+        else:
+            st = L.rsc_search_by_bow_kf_many(self.ctx.h, self.shared.h, self.handles, c, self.nnratio, self.check,
+                                             self.ptrs, self.nmatches)
+        _check(st, "rsc_search_by_bow")
+        c = len(self.others)
+        return self.out[:c, :self.shared.n], self.nmatches[:c]
+
+
+def search_by_bow_frame_many(ctx: Context, kfs, frame, nnratio=0.75, check_orientation=True):
+    """SearchByBoW(pKF, F, vpMapPointMatches) for every KeyFrame view against one Frame view
+    (Tracking::Relocalization, Tracking.cpp:1207-1214: ORBmatcher(0.75, true)).  Returns
+    (matches int32[count, F.n] = KeyFrame feature index or -1, nmatches int32[count])."""
+    return BowSearch(ctx, frame, kfs, True, nnratio, check_orientation).run()
+
+
+def search_by_bow_kf_many(ctx: Context, kf1, kf2s, nnratio=0.75, check_orientation=True):
+    """SearchByBoW(pKF1, pKF2, vpMatches12) of one KeyFrame view against each candidate
+    (LoopClosing::ComputeSim3, LoopClosing.cpp:238-251).  Returns (matches12 int32[count, kf1.n],
+    nmatches int32[count])."""
+    return BowSearch(ctx, kf1, kf2s, False, nnratio, check_orientation).run()

@@ -214,3 +214,80 @@ def make_poseopt_frame(rng: np.random.Generator, n: int, inlier_ratio: float = 0
     inv = (np.float32(1.0) / sc.sigma2).astype(np.float32)
     return PoseOptFrame(has_mp=has, uv=sc.p2d, Xw=Xw, inv_sigma2=inv, Tcw=T, R_true=sc.R_true, t_true=sc.t_true,
                         inlier_true=sc.inlier_true)
+
+
+@dataclasses.dataclass
+class BowFeatures:
+    """One view's ORBmatcher::SearchByBoW inputs: ORB descriptors (mDescriptors, 32 B rows),
+    keypoint angles, map-point validity (GetMapPointMatches()[i] && !isBad()) and the DBoW2
+    FeatureVector (mFeatVec: node id -> ascending feature indices) as CSR."""
+    n: int
+    desc: np.ndarray        # uint8 [n,32]
+    angle: np.ndarray       # float32 [n] degrees in [0, 360)
+    valid: np.ndarray       # uint8 [n]
+    node_id: np.ndarray     # uint32 [nodes] ascending
+    node_begin: np.ndarray  # int32 [nodes+1]
+    feat: np.ndarray        # uint32 [n]
+
+
+# DBoW2 ORB vocabulary shape (k = 10, L = 6, ORBvoc.txt) and Frame::ComputeBoW's levelsup = 4
+# (src/Frame.cpp: transform(..., 4)): FeatureVector keys are node ids of depth 2, i.e. 11..110 with
+# the vocabulary's breadth-first numbering.
+BOW_NODE_IDS = np.arange(11, 111, dtype=np.uint32)
+
+
+def _feature_vector(nodes: np.ndarray):
+    """CSR of node -> ascending feature indices from a per-feature node id (DBoW2 adds features in
+    index order, so each node's vector is ascending)."""
+    order = np.lexsort((np.arange(len(nodes)), nodes))
+    ids, counts = np.unique(nodes[order], return_counts=True)
+    begin = np.zeros(len(ids) + 1, np.int32)
+    begin[1:] = np.cumsum(counts)
+    return ids.astype(np.uint32), begin, order.astype(np.uint32)
+
+
+def _node_draw(rng: np.random.Generator, n: int, skew: float) -> np.ndarray:
+    w = 1.0 / np.arange(1, len(BOW_NODE_IDS) + 1) ** skew
+    w = rng.permutation(w / w.sum())
+    return rng.choice(BOW_NODE_IDS, size=n, p=w)
+
+
+def make_bow_view(rng: np.random.Generator, n: int, valid_frac: float = 1.0, skew: float = 0.8,
+                  nodes: np.ndarray | None = None) -> BowFeatures:
+    """Random ORB view: uniform 256-bit descriptors and angles, Zipf-skewed node occupancy."""
+    if nodes is None:
+        nodes = _node_draw(rng, n, skew)
+    node_id, begin, feat = _feature_vector(np.asarray(nodes, np.uint32))
+    return BowFeatures(n, rng.integers(0, 256, size=(n, 32), dtype=np.uint8),
+                       rng.uniform(0, 360, n).astype(np.float32),
+                       (rng.random(n) < valid_frac).astype(np.uint8), node_id, begin, feat)
+
+
+def _flip_bits(rng: np.random.Generator, desc: np.ndarray, flips: np.ndarray) -> np.ndarray:
+    out = desc.copy()
+    for i, k in enumerate(flips):
+        bits = rng.choice(256, size=int(k), replace=False)
+        np.bitwise_xor.at(out[i], bits // 8, (1 << (bits % 8)).astype(np.uint8))
+    return out
+
+
+def make_bow_related(rng: np.random.Generator, src: BowFeatures, n: int, overlap: float, rot_deg: float,
+                     valid_frac: float = 0.85, same_node: float = 0.9, mean_flips: float = 18.0,
+                     skew: float = 0.8) -> BowFeatures:
+    """A second view sharing ~overlap*n features with `src`: a shared feature copies a source
+    descriptor with Poisson(mean_flips) bit flips, its angle rotated by rot_deg (+ 2 degree noise),
+    and keeps the source node with probability `same_node` (quantisation noise otherwise)."""
+    k = min(int(round(overlap * n)), src.n)
+    nodes = _node_draw(rng, n, skew)
+    v = make_bow_view(rng, n, valid_frac, skew, nodes)
+    src_nodes = np.empty(src.n, np.uint32)
+    for j in range(len(src.node_id)):
+        src_nodes[src.feat[src.node_begin[j]:src.node_begin[j + 1]]] = src.node_id[j]
+    dst = rng.choice(n, size=k, replace=False)
+    srcs = rng.choice(src.n, size=k, replace=False)
+    v.desc[dst] = _flip_bits(rng, src.desc[srcs], np.minimum(rng.poisson(mean_flips, k), 255))
+    v.angle[dst] = np.mod(src.angle[srcs] + np.float32(rot_deg) + rng.normal(0, 2, k), 360).astype(np.float32)
+    keep = rng.random(k) < same_node
+    nodes[dst[keep]] = src_nodes[srcs[keep]]
+    v.node_id, v.node_begin, v.feat = _feature_vector(nodes)
+    return v

@@ -6,6 +6,8 @@
   libc outputs (Random.cpp:47-50, PnPsolver.cpp:125-138).  Independent of the oracle.
 * poseopt_traces.npz — Optimizer::PoseOptimization oracle outputs (pose bits, nGood, round / LM
   iteration / trial counts) on seeded synthetic Frames (regression pins, parity unpinned).
+* bow_traces.npz — ORBmatcher::SearchByBoW (both overloads) inputs and oracle outputs on seeded
+  synthetic views (the views themselves are stored, so the fixture does not depend on the generator).
 * pnp_traces.npz / sim3_traces.npz — per-hypothesis sample indices, inlier counts and poses of the
   oracle restatement on small seeded scenes (regression pins of the oracle; the reference itself
   cannot be built here, see DESIGN.md "Oracle").
@@ -110,8 +112,40 @@ def poseopt():
     np.savez_compressed(os.path.join(HERE, "poseopt_traces.npz"), **{k: np.array(v) for k, v in out.items()})
 
 
+BOW_FIELDS = ("desc", "angle", "valid", "node_id", "node_begin", "feat")
+
+
+def bow():
+    import oracle_lib as ol
+    from rsc import synth
+    # (seed, nA, nB, overlap, flips, frame overload, nnratio, check orientation)
+    cases = [(21, 300, 400, 0.6, 15.0, True, 0.75, True), (22, 400, 300, 0.5, 25.0, False, 0.75, True),
+             (23, 1200, 1000, 0.4, 20.0, True, 0.7, True), (24, 200, 200, 0.8, 10.0, False, 0.9, False),
+             (25, 60, 900, 0.9, 30.0, True, 0.6, False), (26, 900, 60, 0.3, 12.0, False, 0.6, True)]
+    out = {}
+    for k, (seed, na, nb, ov, fl, fv, ratio, check) in enumerate(cases):
+        rng = np.random.default_rng(seed)
+        A = synth.make_bow_view(rng, na, valid_frac=0.85)
+        B = synth.make_bow_related(rng, A, nb, ov, rng.uniform(0, 360), mean_flips=fl)
+        nm, res = ol.search_by_bow(fv, ol.OracleBow(A), ol.OracleBow(B), ratio, check)
+        key = f"c{k}"
+        for side, v in (("A", A), ("B", B)):
+            for f in BOW_FIELDS:
+                out[f"{key}_{side}_{f}"] = getattr(v, f)
+        out[f"{key}_cfg"] = np.array([int(fv), int(check)], np.int32)
+        out[f"{key}_ratio"] = np.float32(ratio)
+        out[f"{key}_n"] = np.int32(nm)
+        out[f"{key}_out"] = res
+        print(key, "nmatches", nm)
+    out["cases"] = np.int32(len(cases))
+    np.savez_compressed(os.path.join(HERE, "bow_traces.npz"), **out)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "poseopt":
         poseopt()
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "bow":
+        bow()
         sys.exit(0)
     main()

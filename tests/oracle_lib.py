@@ -107,6 +107,15 @@ def lib():
     L.ora_sym_eig4f.argtypes = [f32p, f32p, f32p]
     L.ora_svd_solve.argtypes = [C.c_int, f64p, f64p, f64p]
     L.ora_random_int.argtypes = [C.c_uint32, C.c_int, i32p, i32p]
+    L.ora_bow_create.restype = vp
+    L.ora_bow_create.argtypes = [C.c_int, u8p, f32p, C.c_void_p, C.c_int, u32p, i32p, u32p]
+    L.ora_bow_destroy.argtypes = [vp]
+    L.ora_search_by_bow.argtypes = [C.c_int, vp, vp, C.c_float, C.c_int, i32p]
+    L.ora_search_by_bow_many.restype = C.c_int64
+    L.ora_search_by_bow_many.argtypes = [C.c_int, C.c_int, C.POINTER(vp), vp, C.c_float, C.c_int, i32p,
+                                         C.c_int64, i32p]
+    L.ora_descriptor_distance.argtypes = [u8p, u8p]
+    L.ora_compute_three_maxima.argtypes = [i32p, C.c_int, i32p]
     _lib = L
     return L
 
@@ -339,3 +348,63 @@ def pose_optimization(frame):
     if r == 0 and not T.any():
         T = np.ascontiguousarray(frame.Tcw, np.float32).reshape(16).copy()
     return r, T.reshape(4, 4), out, st
+
+
+class OracleBow:
+    """A view (rsc.synth.BowFeatures) held by the oracle with its FeatureVector as a std::map."""
+
+    def __init__(self, view):
+        self.n = int(view.n)
+        self._keep = [np.ascontiguousarray(view.desc, np.uint8).reshape(-1),
+                      np.ascontiguousarray(view.angle, np.float32),
+                      None if view.valid is None else np.ascontiguousarray(view.valid, np.uint8),
+                      np.ascontiguousarray(view.node_id, np.uint32), np.ascontiguousarray(view.node_begin, np.int32),
+                      np.ascontiguousarray(view.feat, np.uint32)]
+        d, a, v, ids, beg, feat = self._keep
+        if feat.size == 0:
+            feat = np.zeros(1, np.uint32)
+            self._keep[5] = feat
+        if d.size == 0:
+            d = np.zeros(32, np.uint8)
+            a = np.zeros(1, np.float32)
+            self._keep[0], self._keep[1] = d, a
+        if ids.size == 0:
+            ids = np.zeros(1, np.uint32)
+            self._keep[3] = ids
+        self.h = lib().ora_bow_create(self.n, d, a, None if v is None else v.ctypes.data,
+                                      len(view.node_id), ids, beg, feat)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ora_bow_destroy(self.h)
+            self.h = None
+
+
+def search_by_bow(frame_variant: bool, a: OracleBow, b: OracleBow, nnratio=0.75, check_ori=True):
+    """frame_variant: SearchByBoW(pKF = a, F = b) -> (nmatches, int32[b.n]); else
+    SearchByBoW(pKF1 = a, pKF2 = b) -> (nmatches, int32[a.n])."""
+    out = np.full(max(b.n if frame_variant else a.n, 1), -7, np.int32)
+    nm = lib().ora_search_by_bow(int(frame_variant), a.h, b.h, nnratio, int(check_ori), out)
+    return nm, out[:(b.n if frame_variant else a.n)]
+
+
+def search_by_bow_many(frame_variant: bool, others, shared, nnratio=0.75, check_ori=True):
+    """Frame variant: SearchByBoW(others[c], shared); KF variant: SearchByBoW(shared, others[c]).
+    Returns (matches int32[count, shared.n], nmatches int32[count])."""
+    L = lib()
+    out = np.full((max(len(others), 1), max(shared.n, 1)), -7, np.int32)
+    nm = np.zeros(max(len(others), 1), np.int32)
+    for c, o in enumerate(others):
+        a, b = (o, shared) if frame_variant else (shared, o)
+        nm[c] = L.ora_search_by_bow(int(frame_variant), a.h, b.h, nnratio, int(check_ori), out[c])
+    return out[:len(others), :shared.n], nm[:len(others)]
+
+
+def descriptor_distance(a, b) -> int:
+    return lib().ora_descriptor_distance(np.ascontiguousarray(a, np.uint8), np.ascontiguousarray(b, np.uint8))
+
+
+def compute_three_maxima(sizes):
+    ind = np.zeros(3, np.int32)
+    lib().ora_compute_three_maxima(np.ascontiguousarray(sizes, np.int32), len(sizes), ind)
+    return tuple(int(x) for x in ind)
