@@ -269,6 +269,9 @@ int rsc_search_by_bow_frame_many(rsc_context* ctx, rsc_bow* const* kfs, int coun
 int rsc_search_by_bow_kf_many(rsc_context* ctx, const rsc_bow* kf1, rsc_bow* const* kf2s, int count,
                               float nnratio, int check_orientation, int32_t* const* matches12, int32_t* nmatches);
 
+/* Diagnostic: wall-clock (100 MHz) phase stamps of the last SearchByBoW launch, [pair < 64][96]. */
+int rsc_diag_bow_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
+
 /* ---- glibc rand() helpers (Thirdparty/DBoW2/DUtils/Random.cpp:33-50) -------------------------- */
 /* First n rand() outputs after srand(seed), produced with the device jump table (parity hook). */
 int rsc_rand_stream(rsc_context* ctx, uint32_t seed, int n, int32_t* out);

@@ -1226,10 +1226,10 @@ struct rsc_bow {
     int n = 0;
     int n_nodes = 0;
     int n_feat = 0;
-    DevBuf<char> mem;            // DevBow header | desc | angle | node_id | node_begin | feat
+    DevBuf<char> mem;            // desc | desc_fv | angle | node_id | node_begin | feat
     size_t off_feat = 0;
     std::vector<uint32_t> feat;  // host copy of the FeatureVector entries (validity flags re-applied)
-    const DevBow* hdr = nullptr;
+    DevBow hdr;                  // device pointers of this view (copied into every BowPair)
 };
 
 namespace {
@@ -1279,7 +1279,7 @@ int rsc_bow_create(rsc_context* C, const rsc_bow_features* f, rsc_bow** out) {
     b->n_feat = nf;
     b->feat.assign(f->feat, f->feat + nf);
     flag_invalid(b->feat, f->valid);
-    const size_t o_desc = al256(sizeof(DevBow)), o_ang = o_desc + al256(32 * (size_t)n);
+    const size_t o_desc = 0, o_dfv = al256(32 * (size_t)n), o_ang = o_dfv + al256(32 * (size_t)nf);
     const size_t o_id = o_ang + al256(4 * (size_t)n), o_beg = o_id + al256(4 * (size_t)nn);
     const size_t o_feat = o_beg + al256(4 * ((size_t)nn + 1));
     const size_t bytes = o_feat + al256(4 * (size_t)nf);
@@ -1289,15 +1289,16 @@ int rsc_bow_create(rsc_context* C, const rsc_bow_features* f, rsc_bow** out) {
     char* d = b->mem.p;
     DevBow hd;
     hd.desc = reinterpret_cast<const uint4*>(d + o_desc);
+    hd.desc_fv = reinterpret_cast<const uint4*>(d + o_dfv);
     hd.angle = reinterpret_cast<const float*>(d + o_ang);
     hd.node_id = reinterpret_cast<const uint32_t*>(d + o_id);
     hd.node_begin = reinterpret_cast<const int32_t*>(d + o_beg);
     hd.feat = reinterpret_cast<const uint32_t*>(d + o_feat);
     hd.n = n;
     hd.n_nodes = nn;
-    std::memcpy(h.data(), &hd, sizeof(hd));
     if (n) {
         std::memcpy(h.data() + o_desc, f->desc, 32 * (size_t)n);
+        for (int e = 0; e < nf; ++e) std::memcpy(h.data() + o_dfv + 32 * (size_t)e, f->desc + 32 * (size_t)f->feat[e], 32);
         std::memcpy(h.data() + o_ang, f->angle, 4 * (size_t)n);
     }
     if (nn) {
@@ -1307,7 +1308,7 @@ int rsc_bow_create(rsc_context* C, const rsc_bow_features* f, rsc_bow** out) {
     }
     RSC_HIP(hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice));
     b->off_feat = o_feat;
-    b->hdr = reinterpret_cast<const DevBow*>(d);
+    b->hdr = hd;
     *out = b.release();
     return RSC_OK;
 }
@@ -1338,14 +1339,15 @@ int bow_search(rsc_context* C, bool frame_overload, const rsc_bow* const* outer,
         const int on = frame_overload ? inner[c]->n : outer[c]->n;
         if (on && !out[c]) return RSC_ERR_ARG;
         ooff[c + 1] = ooff[c] + al256(4 * (size_t)on);
-        roff[c + 1] = roff[c] + (size_t)outer[c]->n_feat;
+        roff[c + 1] = roff[c] + (size_t)outer[c]->n_feat * kBowMaxSegs;
         joff[c + 1] = joff[c] + (size_t)outer[c]->n_nodes;
-        toff[c + 1] = toff[c] + (size_t)outer[c]->n_nodes + (size_t)outer[c]->n_feat / 64 + 1;
+        toff[c + 1] = toff[c] + ((size_t)outer[c]->n_nodes + (size_t)outer[c]->n_feat / 64 + 1) * kBowMaxSegs;
     }
     const size_t o_pairs = 0, o_cnt = al256(sizeof(BowPair) * count), o_out = o_cnt + al256(4 * (size_t)count);
     const size_t o_rec = o_out + ooff[count], o_nodes = o_rec + al256(16 * roff[count]);
     const size_t o_tasks = o_nodes + al256(16 * joff[count]), o_nt = o_tasks + al256(16 * toff[count]);
-    const size_t bytes = o_nt + al256(8 * (size_t)count);
+    const size_t o_mcp = o_nt + al256(8 * (size_t)count);
+    const size_t bytes = o_mcp + al256(2 * roff[count] / kBowMaxSegs);
     const size_t back = o_rec;  // counts + outputs come back
     RSC_HIP(hipSetDevice(C->device));
     if (int e = C->d_bow.ensure(bytes)) return e;
@@ -1355,17 +1357,20 @@ int bow_search(rsc_context* C, bool frame_overload, const rsc_bow* const* outer,
     BowPair* hp = reinterpret_cast<BowPair*>(C->h_bow.p + o_pairs);
     for (int c = 0; c < count; ++c) {
         hp[c].outer = outer[c]->hdr;
-        hp[c].inner = inner[c]->hdr;
+        hp[c].inner = inner[c]->hdr;  // by value
         hp[c].rec = reinterpret_cast<uint4*>(d + o_rec) + roff[c];
         hp[c].nodes = reinterpret_cast<int4*>(d + o_nodes) + joff[c];
         hp[c].tasks = reinterpret_cast<int4*>(d + o_tasks) + toff[c];
         hp[c].ntasks = reinterpret_cast<int32_t*>(d + o_nt) + 2 * c;
+        hp[c].mcp = reinterpret_cast<int16_t*>(d + o_mcp) + roff[c] / kBowMaxSegs;
         hp[c].out = reinterpret_cast<int32_t*>(d + o_out + ooff[c]);
         hp[c].nmatches = reinterpret_cast<int32_t*>(d + o_cnt) + c;
     }
     RSC_HIP(hipMemcpyAsync(d, C->h_bow.p, o_cnt, hipMemcpyHostToDevice, C->stream));
     timing_begin(C, 3);
-    RSC_HIP(launch_bow_search(frame_overload, count, reinterpret_cast<const BowPair*>(d + o_pairs), nnratio,
+    int max_nodes = 0;
+    for (int c = 0; c < count; ++c) max_nodes = std::max(max_nodes, outer[c]->n_nodes);
+    RSC_HIP(launch_bow_search(frame_overload, count, max_nodes, reinterpret_cast<const BowPair*>(d + o_pairs), nnratio,
                               check_ori ? 1 : 0, C->stream));
     timing_begin(C, 4);
     RSC_HIP(hipMemcpyAsync(C->h_bow.p + o_cnt, d + o_cnt, back - o_cnt, hipMemcpyDeviceToHost, C->stream));
@@ -1384,6 +1389,13 @@ int bow_search(rsc_context* C, bool frame_overload, const rsc_bow* const* outer,
     return RSC_OK;
 }
 }  // namespace
+
+int rsc_diag_bow_phase_stamps(rsc_context* C, uint64_t* out, int cap) {
+    if (!C || !out || cap < 0) return RSC_ERR_ARG;
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    RSC_HIP(read_bow_stamps(out, cap));
+    return RSC_OK;
+}
 
 int rsc_search_by_bow_frame_many(rsc_context* C, rsc_bow* const* kfs, int count, const rsc_bow* frame, float nnratio,
                                  int check_orientation, int32_t* const* matches, int32_t* nmatches) {

@@ -17,15 +17,16 @@
 //     lane keeps the 4 smallest (distance, position) keys of its feature over the valid inner
 //     features, in the reference's first-minimum order, and stores them as one 16-B record.  The
 //     inner node is staged through a per-wave LDS segment.  Several workgroups per pair fill the chip.
-//  2. bow_resolve_kernel — the greedy walk, one wave per common node, one workgroup per pair: the
+//  2. bow_walk_kernel — the greedy walk, one wave per common node (all nodes of all pairs at once): the
 //     outer features of a node sit on the lanes 64 at a time, a ballot keeps those whose first key
 //     is within TH_LOW, and the wave visits them in order (readlane); the first two unmatched keys
 //     of a record give bestDist1 / bestIdx / bestDist2 exactly (a record ending in an empty slot is
 //     complete), with the node's matched positions held as per-lane bit masks.  Only when three of
 //     the four keys are already matched does the wave rescan the node (lanes = inner positions,
-//     butterfly merge of (first-min key, second-min distance)).  Then the orientation histogram
-//     (ComputeThreeMaxima, :1446-1487) filters the matches and the output vector is written
-//     coalesced.
+//     butterfly merge of (first-min key, second-min distance)).
+//  3. bow_resolve_kernel — one workgroup per pair: the matches become the reference's vector, the
+//     orientation histogram (ComputeThreeMaxima, :1446-1487) filters them and the output vector is
+//     written coalesced.
 //
 // Integer popcount + a handful of float ops: no MFMA; HBM traffic is the descriptor rows once plus
 // 16 B of record per outer feature.
@@ -41,7 +42,9 @@ constexpr int kBowThLow = 50;           // ORBmatcher::TH_LOW (ORBmatcher.cpp:9)
 constexpr int kBowHistoLength = 30;     // ORBmatcher::HISTO_LENGTH (ORBmatcher.cpp:10)
 constexpr int kBowTopkThreads = 256;    // kernel 1: 4 waves per workgroup
 constexpr int kBowTopkGroups = 8;       // kernel 1: workgroups per pair
-constexpr int kBowSeg = 128;            // kernel 1: inner-node positions staged in LDS per wave at a time
+constexpr int kBowMaxSegs = 8;          // inner nodes wider than 64 positions are scanned in up to 8
+                                        // segments by different waves (records merged in kernel 2)
+constexpr int kBowSeg = 256;            // kernel 1: inner-node positions staged in LDS per wave at a time
 constexpr int kBowResolveThreads = 1024;  // kernel 2: 16 waves, one workgroup per pair
 constexpr uint32_t kBowInvalid = 0x80000000u;  // flag on a FeatureVector entry: no map point / bad
 constexpr uint32_t kBowNoKey = (256u << 16) | 0xFFFFu;  // empty record slot (distance 256, no feature)
@@ -50,6 +53,8 @@ constexpr uint32_t kBowNoKey = (256u << 16) | 0xFFFFu;  // empty record slot (di
 // start of the view's allocation.
 struct DevBow {
     const uint4* desc;          // [n][2] descriptor rows (32 B, mDescriptors.row(i))
+    const uint4* desc_fv;       // [feat entries][2] the same rows in FeatureVector order (desc_fv[e] =
+                                // desc[feat[e]]), so a node's rows are one contiguous coalesced range
     const float* angle;         // [n] keypoint angle in degrees
     const uint32_t* node_id;    // [n_nodes] FeatureVector keys, strictly ascending
     const int32_t* node_begin;  // [n_nodes + 1] CSR offsets into feat
@@ -62,16 +67,24 @@ struct DevBow {
 // One searched pair.  outer = the side whose features are taken in turn (pKF in the Frame
 // overload, pKF1 in the KeyFrame overload), inner = the side searched (F, pKF2).
 struct BowPair {
-    const DevBow* outer;
-    const DevBow* inner;
-    uint4* rec;         // [outer feat entries] top-4 records (kernel 1 -> kernel 2)
-    int4* tasks;        // [outer n_nodes + outer feat entries / 64 + 1] (a first, a count, b0, nb) per
-                        // 64-feature chunk of each common node (kernel 0 -> kernel 1)
+    DevBow outer;       // view headers by value: one load per workgroup instead of a dependent chain
+    DevBow inner;
+    uint4* rec;         // [kBowMaxSegs][outer feat entries] top-4 records per inner segment (kernel 1 -> 2)
+    int4* tasks;        // [(outer n_nodes + outer feat entries / 64 + 1) * kBowMaxSegs] one per
+                        // (64-feature chunk, inner segment) of each common node (kernel 0 -> kernel 1):
+                        // (first | count << 16, b0 | segment << 16, nb, segment begin | length << 16)
     int4* nodes;        // [outer n_nodes] (a0, a1, b0, nb) per common node (kernel 0 -> kernel 2)
     int32_t* ntasks;    // [2] tasks, common nodes
+    int16_t* mcp;       // [outer feat entries] matched inner FeatureVector entry or -1 (kernel 2 -> 3)
     int32_t* out;       // Frame overload: [inner.n] outer index per inner feature; KF: [outer.n] inner index
     int32_t* nmatches;  // [1]
 };
+
+// segments of an inner node of nb positions: one per 64 positions, at most kBowMaxSegs
+__host__ __device__ inline int bow_segments(int nb) {
+    const int s = (nb + 63) / 64;
+    return s < 1 ? 1 : (s > kBowMaxSegs ? kBowMaxSegs : s);
+}
 
 // Orientation bin of a match (ORBmatcher.cpp:187-195, :437-445).  The reference's factor is
 // 1.0f / HISTO_LENGTH, so only bins 0..12 are reached; reproduced as written.
@@ -84,8 +97,11 @@ __host__ __device__ inline int bow_rot_bin(float angle_outer, float angle_inner)
     return bin;
 }
 
-// both kernels on `st`; frame_overload selects SearchByBoW(KeyFrame, Frame) semantics
-hipError_t launch_bow_search(bool frame_overload, int count, const BowPair* pairs, float nnratio, int check_ori,
-                             hipStream_t st);
+// diagnostic phase stamps of the last launch (see orbmatch.hip), up to cap values
+hipError_t read_bow_stamps(uint64_t* out, int cap);
+
+// all kernels on `st`; frame_overload selects SearchByBoW(KeyFrame, Frame) semantics
+hipError_t launch_bow_search(bool frame_overload, int count, int max_outer_nodes, const BowPair* pairs, float nnratio,
+                             int check_ori, hipStream_t st);
 
 }  // namespace rsc

@@ -10,12 +10,14 @@
 #include "Sim3Solver.hpp"
 #include "Optimizer.hpp"
 #include "MLPnPsolver.hpp"
+#include "ORBmatcher.hpp"
+#include <map>
 
 struct Vec3 { float v[3]; float operator()(int i) const { return v[i]; } float& operator()(int i) { return v[i]; } };
 struct Mat3 { float m[3][3]; float operator()(int r, int c) const { return m[r][c]; } float& operator()(int r, int c) { return m[r][c]; } };
 struct Mat4 { float m[4][4]; float& operator()(int r, int c) { return m[r][c]; } float operator()(int r, int c) const { return m[r][c]; } };
 struct Pt { float x, y; };
-struct KeyPoint { Pt pt; int octave; };
+struct KeyPoint { Pt pt; int octave; float angle = 0.f; };
 struct Frame { std::vector<KeyPoint> mvKeysUn; std::vector<float> mvLevelSigma2; float fx, fy, cx, cy; };
 struct KeyFrame;
 struct MapPoint {
@@ -33,6 +35,23 @@ struct KeyFrame {
 };
 int MapPoint::GetIndexInKeyFrame(const std::shared_ptr<KeyFrame>& kf) const { return kf.get() == kf1 ? idx1 : idx2; }
 
+// cv::Mat stand-in for descriptor rows (mDescriptors.ptr<uint8_t>(i)) and the SearchByBoW views
+struct DescMat {
+    std::vector<uint8_t> d;
+    template <class T> const T* ptr(int row) const { return reinterpret_cast<const T*>(d.data() + 32 * (size_t)row); }
+};
+using FeatVec = std::map<unsigned int, std::vector<unsigned int>>;
+struct BowKF {
+    int N = 0; DescMat mDescriptors; std::vector<KeyPoint> mvKeysUn; FeatVec mFeatVec;
+    std::vector<std::shared_ptr<MapPoint>> mps;
+    std::vector<std::shared_ptr<MapPoint>> GetMapPointMatches() const { return mps; }
+};
+struct BowFrame { int N = 0; DescMat mDescriptors; std::vector<KeyPoint> mvKeys; FeatVec mFeatVec; };
+
+// view record: n, desc[n*32], angle[n], valid[n] (u8), nodes, per node (id, count, feats[count])
+template <class V>
+void read_view(FILE* in, V& v, std::vector<KeyPoint>& kps, std::vector<std::shared_ptr<MapPoint>>* mps);
+
 // Frame as PoseOptimization sees it (include/Frame.hpp:52,131,142,145,153,169)
 struct PFrame {
     std::vector<KeyPoint> mvKeysUn;
@@ -48,6 +67,26 @@ struct PFrame {
 
 template <class T> T rd(FILE* f) { T v; if (fread(&v, sizeof(T), 1, f) != 1) throw std::runtime_error("short read"); return v; }
 template <class T> void wr(FILE* f, T v) { fwrite(&v, sizeof(T), 1, f); }
+
+template <class V>
+void read_view(FILE* in, V& v, std::vector<KeyPoint>& kps, std::vector<std::shared_ptr<MapPoint>>* mps) {
+    v.N = rd<int32_t>(in);
+    v.mDescriptors.d.resize(32 * (size_t)v.N);
+    if (v.N && fread(v.mDescriptors.d.data(), 1, 32 * (size_t)v.N, in) != 32 * (size_t)v.N) throw std::runtime_error("short read");
+    kps.resize(v.N);
+    for (int i = 0; i < v.N; ++i) kps[i].angle = rd<float>(in);
+    if (mps) mps->resize(v.N);
+    for (int i = 0; i < v.N; ++i) {
+        const uint8_t ok = rd<uint8_t>(in);  // 0 no map point, 1 good, 2 bad
+        if (mps && ok) { auto mp = std::make_shared<MapPoint>(); mp->bad = ok == 2; mp->idx1 = i; (*mps)[i] = mp; }
+    }
+    const int nn = rd<int32_t>(in);
+    for (int k = 0; k < nn; ++k) {
+        const uint32_t id = rd<uint32_t>(in), cnt = rd<uint32_t>(in);
+        auto& f = v.mFeatVec[id];
+        for (uint32_t j = 0; j < cnt; ++j) f.push_back(rd<uint32_t>(in));
+    }
+}
 
 int main(int argc, char** argv) {
     if (argc != 3) { fprintf(stderr, "usage: facade_test in.bin out.bin\n"); return 2; }
@@ -120,6 +159,52 @@ int main(int argc, char** argv) {
         wr<int32_t>(out, F.set_pose_calls);
         for (int a = 0; a < 4; ++a) for (int b = 0; b < 4; ++b) wr<float>(out, F.mTcw.m[a][b]);
         for (int i = 0; i < n; ++i) wr<uint8_t>(out, F.mvbOutlier[i] ? 1 : 0);
+    } else if (mode == 5) {
+        // ORBmatcher::SearchByBoW through rsc_orb::ORBmatcher: frame overload (pKF = views[c], F =
+        // shared) or KeyFrame overload (pKF1 = shared, pKF2 = views[c]); writes nmatches and, per
+        // slot of the result vector, the matched MapPoint's feature index in its KeyFrame or -1
+        const int frame_overload = rd<int32_t>(in);
+        const float ratio = rd<float>(in);
+        const int check = rd<int32_t>(in);
+        const int C = rd<int32_t>(in);
+        rsc_orb::ORBmatcher matcher(ratio, check != 0);
+        if (frame_overload) {
+            BowFrame F;
+            read_view(in, F, F.mvKeys, nullptr);
+            std::vector<std::shared_ptr<BowKF>> kfs(C);
+            for (auto& k : kfs) { k = std::make_shared<BowKF>(); read_view(in, *k, k->mvKeysUn, &k->mps); }
+            for (int c = 0; c < C; ++c) {  // the reference's per-candidate calls (Tracking.cpp:1214)
+                std::vector<std::shared_ptr<MapPoint>> m;
+                const int nm = matcher.SearchByBoW(kfs[c], F, m);
+                wr<int32_t>(out, nm);
+                wr<int32_t>(out, (int32_t)m.size());
+                for (auto& mp : m) wr<int32_t>(out, mp ? mp->idx1 : -1);
+            }
+            std::vector<std::vector<std::shared_ptr<MapPoint>>> mm;  // batched form, same results
+            const std::vector<int> nms = matcher.SearchByBoWMany(kfs, F, mm);
+            for (int c = 0; c < C; ++c) {
+                wr<int32_t>(out, nms[c]);
+                for (auto& mp : mm[c]) wr<int32_t>(out, mp ? mp->idx1 : -1);
+            }
+        } else {
+            auto K1 = std::make_shared<BowKF>();
+            read_view(in, *K1, K1->mvKeysUn, &K1->mps);
+            std::vector<std::shared_ptr<BowKF>> kfs(C);
+            for (auto& k : kfs) { k = std::make_shared<BowKF>(); read_view(in, *k, k->mvKeysUn, &k->mps); }
+            for (int c = 0; c < C; ++c) {  // LoopClosing.cpp:251
+                std::vector<std::shared_ptr<MapPoint>> m;
+                const int nm = matcher.SearchByBoW(K1, kfs[c], m);
+                wr<int32_t>(out, nm);
+                wr<int32_t>(out, (int32_t)m.size());
+                for (auto& mp : m) wr<int32_t>(out, mp ? mp->idx1 : -1);
+            }
+            std::vector<std::vector<std::shared_ptr<MapPoint>>> mm;
+            const std::vector<int> nms = matcher.SearchByBoWMany(K1, kfs, mm);
+            for (int c = 0; c < C; ++c) {
+                wr<int32_t>(out, nms[c]);
+                for (auto& mp : mm[c]) wr<int32_t>(out, mp ? mp->idx1 : -1);
+            }
+        }
     } else if (mode == 2) {
         auto kf1 = std::make_shared<KeyFrame>(), kf2 = std::make_shared<KeyFrame>();
         const int n1 = rd<int32_t>(in);

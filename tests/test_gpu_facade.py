@@ -182,3 +182,51 @@ def test_pose_optimization_facade_matches_oracle():
     sel = f.has_mp == 1
     assert np.array_equal(flags[sel], outl[sel])
     assert (flags[~sel] == 1).all()  # untouched (the mock starts them at true)
+
+
+def _view_bytes(v, mp_state):
+    """facade_test view record; mp_state[i]: 0 no map point, 1 good, 2 bad."""
+    b = struct.pack("<i", v.n) + np.ascontiguousarray(v.desc, np.uint8).tobytes()
+    b += np.ascontiguousarray(v.angle, "<f4").tobytes() + np.asarray(mp_state, np.uint8).tobytes()
+    b += struct.pack("<i", len(v.node_id))
+    for k in range(len(v.node_id)):
+        f = v.feat[v.node_begin[k]:v.node_begin[k + 1]]
+        b += struct.pack("<II", int(v.node_id[k]), len(f)) + np.asarray(f, "<u4").tobytes()
+    return b
+
+
+@pytest.mark.parametrize("frame_overload", [True, False])
+def test_orbmatcher_facade_matches_oracle(frame_overload):
+    """rsc_orb::ORBmatcher::SearchByBoW (ORBmatcher.cpp:110-240 / :354-488) on mock KeyFrames /
+    Frame (cv::Mat-like descriptor rows, std::map FeatureVector, null and bad MapPoints): per-call
+    and batched results equal the oracle, MapPoint by MapPoint."""
+    rng = np.random.default_rng(41 + frame_overload)
+    S = synth.make_bow_view(rng, 900)
+    views = [synth.make_bow_related(rng, S, int(rng.integers(300, 900)), float(rng.uniform(0.2, 0.7)),
+                                    float(rng.uniform(0, 360))) for _ in range(5)]
+    states = []
+    for v in [S] + views:
+        st = rng.choice([0, 1, 2], size=v.n, p=[0.1, 0.8, 0.1]).astype(np.uint8)
+        states.append(st)
+        v.valid = (st == 1).astype(np.uint8)
+    buf = struct.pack("<iifii", 5, int(frame_overload), 0.75, 1, len(views))
+    buf += _view_bytes(S, states[0])
+    for v, st in zip(views, states[1:]):
+        buf += _view_bytes(v, st)
+    out = np.frombuffer(run(buf), "<i4")
+    oS = ol.OracleBow(S)
+    pos = 0
+    expect = []
+    for v in views:
+        ov = ol.OracleBow(v)
+        nm, m = ol.search_by_bow(frame_overload, ov, oS) if frame_overload else ol.search_by_bow(False, oS, ov)
+        expect.append((nm, m))
+    for nm, m in expect:
+        assert out[pos] == nm and out[pos + 1] == len(m)
+        assert np.array_equal(out[pos + 2:pos + 2 + len(m)], m)
+        pos += 2 + len(m)
+    for nm, m in expect:  # batched form
+        assert out[pos] == nm
+        assert np.array_equal(out[pos + 1:pos + 1 + len(m)], m)
+        pos += 1 + len(m)
+    assert pos == len(out)
