@@ -255,8 +255,7 @@ __device__ __forceinline__ void pnp_eig_quad_body(const DevPnP* __restrict__ pro
         return;
     }
 
-    // ---- C: accumulate Q (own columns), transpose to own rows through LDS ----
-    double Q[3][12];
+    // ---- C: accumulate Q (own columns), transpose to row-major Q in this hypothesis' T region ----
     {
         double Qc[3][12];
         quad_accumulate(Qc, q, E, hC);
@@ -264,36 +263,43 @@ __device__ __forceinline__ void pnp_eig_quad_body(const DevPnP* __restrict__ pro
             RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + 4 * j + q] = Qc[j][r];
     }
     __syncthreads();
-    RSC_UNROLL for (int j = 0; j < 3; ++j)
-        RSC_UNROLL for (int c = 0; c < 12; ++c) Q[j][c] = T[(4 * j + q) * 12 + c];
     if (STOP == 3) {
         if (active) {
             double acc = 0.0;
-            RSC_UNROLL for (int j = 0; j < 3; ++j) RSC_UNROLL for (int c = 0; c < 12; ++c) acc += Q[j][c];
+            RSC_UNROLL for (int j = 0; j < 3; ++j)
+                RSC_UNROLL for (int c = 0; c < 12; ++c) acc += T[(4 * j + q) * 12 + c];
             out[q] = acc + diag[0] + sub[0];
         }
         return;
     }
 
     // ---- D: implicit symmetric QR, rotations applied to the own rows ----
+    // The own rows of Q stay in LDS (T, row-major): the rotations' read-modify-writes are off the
+    // Givens chase's dependency chain, and keeping 36 doubles per lane out of the register file
+    // removes the chase's register spills (scratch round trips inside the QR loop).
     {
         auto qapply = [&](int k, double c, double s, bool apply) {
             RSC_UNROLL for (int j = 0; j < 3; ++j) {
-                const double xi = Q[j][k], yi = Q[j][k + 1];
-                Q[j][k] = apply ? c * xi - s * yi : xi;
-                Q[j][k + 1] = apply ? s * xi + c * yi : yi;
+                double* row = T + (4 * j + q) * 12;
+                const double xi = row[k], yi = row[k + 1];
+                row[k] = apply ? c * xi - s * yi : xi;
+                row[k + 1] = apply ? s * xi + c * yi : yi;
             }
         };
         int perm[12];
         tridiag_qr<double, 12>(diag, sub, qapply, perm);
         // sorted eigenvector columns 0..3 (the four smallest eigenvalues) of the own rows
         if (active) {
-            RSC_UNROLL for (int j = 0; j < 3; ++j)
+            RSC_UNROLL for (int j = 0; j < 3; ++j) {
+                const double* row = T + (4 * j + q) * 12;
+                double Qr[12];
+                RSC_UNROLL for (int p = 0; p < 12; ++p) Qr[p] = row[p];
                 RSC_UNROLL for (int c = 0; c < 4; ++c) {
-                    double x = Q[j][0];
-                    RSC_UNROLL for (int p = 1; p < 12; ++p) x = (perm[c] == p) ? Q[j][p] : x;
+                    double x = Qr[0];
+                    RSC_UNROLL for (int p = 1; p < 12; ++p) x = (perm[c] == p) ? Qr[p] : x;
                     out[kStEv + (4 * j + q) * 4 + c] = x;
                 }
+            }
         }
     }
 }
