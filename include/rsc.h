@@ -269,6 +269,9 @@ int rsc_search_by_bow_frame_many(rsc_context* ctx, rsc_bow* const* kfs, int coun
 int rsc_search_by_bow_kf_many(rsc_context* ctx, const rsc_bow* kf1, rsc_bow* const* kf2s, int count,
                               float nnratio, int check_orientation, int32_t* const* matches12, int32_t* nmatches);
 
+/* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP refine launch, [job < 64][8]:
+ * entry, compaction, control points, MtM, eigen, betas, check, exit. */
+int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out);
 /* Diagnostic: wall-clock (100 MHz) phase stamps of the last SearchByBoW launch, [pair < 64][96]. */
 int rsc_diag_bow_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
 

@@ -237,6 +237,13 @@ __device__ double wave_ordered_sum(int count, double* buf, bool from_zero, Term&
     return s;
 }
 
+// Diagnostic phase stamps of the refine kernel (wall clock, 100 MHz): job 0..63 of the last
+// launch, [job][0..7] = entry, compaction, control points, MtM, eigen, betas, check, exit.
+__device__ uint64_t g_refine_stamps[64][8];
+__device__ __forceinline__ void refine_stamp(int slot) {
+    if (blockIdx.x < 64 && threadIdx.x == 0) g_refine_stamps[blockIdx.x][slot] = wall_clock64();
+}
+
 __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restrict__ probs,
                                                          const RefineJob* __restrict__ jobs,
                                                          int mask_words_out) {
@@ -254,6 +261,7 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     const int nwords = (n + 63) / 64;
     double* buf = wbuf[wave];
 
+    refine_stamp(0);
     // 0. new-best bookkeeping (PnPsolver.cpp:147-156) fused here: mvbBestInliers, mBestTcw.
     if (J.adopt_mask)
         for (int wd = tid; wd < nwords; wd += 256) J.adopt_mask[wd] = J.best_mask[wd];
@@ -284,6 +292,7 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     // exist after growth; rows = nr).  Without growth the rows beyond nr stay stale (Q6).
     const int rows = J.rows_after;
     __syncthreads();
+    refine_stamp(1);
 
     const double* __restrict__ pws = P.pws;
     const double* __restrict__ us = P.us;
@@ -339,18 +348,49 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     }
     __threadfence_block();
     __syncthreads();
-    // 3. MtM lower triangle, one entry per thread
-    if (tid < 78) {
+    refine_stamp(2);
+    // 3. MtM lower triangle, one entry per thread, each folded over the 2*nr rows in order.  The
+    // rows of M are staged through LDS (wbuf, 192 rows x 12 at a time) by all 256 threads, so the
+    // 78 folding threads read operands from LDS instead of recomputing them from global memory.
+    {
+        double* Mc = &wbuf[0][0];
+        constexpr int kRows = (4 * 64 * 9) / 12;
         int a = 0, b = tid;
         while (b > a) { b -= a + 1; ++a; }  // tid -> (a,b) with b <= a, row-major lower triangle
-        double s = M_entry(st, K, 0, a) * M_entry(st, K, 0, b);
-        for (int r = 1; r < 2 * nr; ++r) s = s + M_entry(st, K, r, a) * M_entry(st, K, r, b);
-        S.at(a, b) = s;
+        double s = 0.0;
+        for (int r0 = 0; r0 < 2 * nr; r0 += kRows) {
+            const int m = min(kRows, 2 * nr - r0);
+            __syncthreads();  // the previous chunk has been folded
+            for (int e = tid; e < m * 12; e += 256) Mc[e] = M_entry(st, K, r0 + e / 12, e % 12);
+            __syncthreads();
+            if (tid < 78) {
+                int r = 0;
+                if (r0 == 0) {
+                    s = Mc[a] * Mc[b];
+                    r = 1;
+                }
+                for (; r < m; ++r) s = s + Mc[r * 12 + a] * Mc[r * 12 + b];
+            }
+        }
+        if (tid < 78) S.at(a, b) = s;
     }
     __syncthreads();
-    // 4. 12x12 eigenvectors, L_6x10 and rho (single lane)
+    refine_stamp(3);
+    // 4. 12x12 eigenvectors (lanes 0-3 of wave 0 as one quad, quad_eig12_ev4), then L_6x10 and
+    // rho (single lane).  The MtM lower triangle in the slab is the quad's T region; wbuf the E
+    // scratch.  The eigenvector columns 0..3 go back to slab columns 0..3 (SlabView::ev).
+    if (tid < 4) {
+        double ev[3][4];
+        quad_eig12_ev4(slab, &wbuf[0][0], tid, [] {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }, ev);
+        RSC_UNROLL for (int j = 0; j < 3; ++j)
+            RSC_UNROLL for (int c = 0; c < 4; ++c) slab[(4 * j + tid) * 12 + c] = ev[j][c];
+    }
+    __syncthreads();
     if (tid == 0) {
-        sym_eig12(S);
         compute_L_6x10(SlabView{S});
         auto d2 = [&](int a, int b) {
             double x = cws_sh[3 * a] - cws_sh[3 * b], y = cws_sh[3 * a + 1] - cws_sh[3 * b + 1],
@@ -362,6 +402,7 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
         SV.rho(3) = d2(1, 2); SV.rho(4) = d2(1, 3); SV.rho(5) = d2(2, 3);
     }
     __syncthreads();
+    refine_stamp(4);
     // 5. beta approximation (wave + 1), Gauss-Newton, compute_R_and_t over all rows
     if (wave < 3) {
         const SlabView SV{S};
@@ -423,6 +464,7 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
         }
     }
     __syncthreads();
+    refine_stamp(5);
     // smallest reprojection error, approximations in order 1, 2, 3 (strict <, PnPsolver.cpp:405-411)
     if (tid == 0) {
         int b = 0;
@@ -451,6 +493,7 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     }
     if (lane == 0) cnt_sh[wave] = cnt;
     __syncthreads();
+    refine_stamp(6);
     if (tid == 0) {
         *J.out_count = cnt_sh[0] + cnt_sh[1] + cnt_sh[2] + cnt_sh[3];
         RSC_UNROLL for (int k = 0; k < 12; ++k) J.out_pose[k] = pose_sh[k];
@@ -734,6 +777,10 @@ hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchPr
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+hipError_t read_refine_stamps(uint64_t* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_refine_stamps), sizeof(uint64_t) * 64 * 8, 0, hipMemcpyDeviceToHost);
 }
 
 hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, int mask_words_out,

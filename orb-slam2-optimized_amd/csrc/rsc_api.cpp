@@ -1390,6 +1390,13 @@ int bow_search(rsc_context* C, bool frame_overload, const rsc_bow* const* outer,
 }
 }  // namespace
 
+int rsc_diag_refine_phase_stamps(rsc_context* C, uint64_t* out) {
+    if (!C || !out) return RSC_ERR_ARG;
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    RSC_HIP(read_refine_stamps(out));
+    return RSC_OK;
+}
+
 int rsc_diag_bow_phase_stamps(rsc_context* C, uint64_t* out, int cap) {
     if (!C || !out || cap < 0) return RSC_ERR_ARG;
     RSC_HIP(hipStreamSynchronize(C->stream));

@@ -88,6 +88,7 @@ hipError_t launch_pnp_solve_stamped(int nwg, const DevPnP* probs, const LaunchPr
                                     const uint32_t* T, float* poses, uint64_t* stamps, hipStream_t st);
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,
                            const float* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st);
+hipError_t read_refine_stamps(uint64_t* out);  // diagnostic, [64][8]
 hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, int mask_words_out,
                              hipStream_t st);
 hipError_t launch_sim3_solve(int nwg, const DevSim3* probs, const LaunchProb* lps, const int2* wgt,

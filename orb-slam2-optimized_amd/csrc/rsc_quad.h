@@ -161,6 +161,70 @@ __device__ __forceinline__ void quad_accumulate(double (&Qc)[3][12], int q, cons
 }
 
 
+// Eigenvectors of the four smallest eigenvalues of a symmetric 12x12 (SelfAdjointEigenSolver on
+// MtM, PnPsolver.cpp:379-382) by the four lanes of one quad (q = lane & 3): phases B-D of
+// pnp_eig_quad_body below as a standalone routine (used by the Refine kernel, where one quad of
+// wave 0 serves the workgroup).  T: the quad's 144-double LDS region holding the lower triangle
+// row-major (T[R*12+c], c <= R) on entry; E: 55 doubles of LDS scratch; sync(): an LDS
+// visibility point for the quad.  ev[j][c] = eigenvector column c of row 4j+q, bit-identical to
+// sym_eig12 (rsc_core.h) and to the hypothesis path.
+template <class Sync>
+__device__ __forceinline__ void quad_eig12_ev4(double* T, double* E, int q, Sync sync, double (&ev)[3][4]) {
+    double diag[12], sub[11], hC[11];
+    {
+        double A[3][12];
+        double m = 0.0;
+        RSC_UNROLL for (int j = 0; j < 3; ++j) {
+            const int R = 4 * j + q;
+            RSC_UNROLL for (int c = 0; c < 12; ++c) {
+                A[j][c] = T[(R >= c) ? R * 12 + c : c * 12 + R];
+                const double a = fabs(A[j][c]);
+                if (c <= R && a > m) m = a;
+            }
+        }
+        double scale = qb_<0>(m);
+        const double m1 = qb_<1>(m), m2 = qb_<2>(m), m3 = qb_<3>(m);
+        if (m1 > scale) scale = m1;
+        if (m2 > scale) scale = m2;
+        if (m3 > scale) scale = m3;
+        const double a00 = fabs(qb_<0>(A[0][0]));
+        if (a00 != a00) scale = a00;
+        if (scale == 0.0) scale = 1.0;
+        RSC_UNROLL for (int j = 0; j < 3; ++j)
+            RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = A[j][c] / scale;
+        sync();  // every lane has read T before phase C overwrites it
+        quad_tridiag(A, q, E, diag, sub, hC);
+    }
+    sync();
+    {
+        double Qc[3][12];
+        quad_accumulate(Qc, q, E, hC);
+        RSC_UNROLL for (int j = 0; j < 3; ++j)
+            RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + 4 * j + q] = Qc[j][r];
+    }
+    sync();
+    auto qapply = [&](int k, double c, double s, bool apply) {
+        RSC_UNROLL for (int j = 0; j < 3; ++j) {
+            double* row = T + (4 * j + q) * 12;
+            const double xi = row[k], yi = row[k + 1];
+            row[k] = apply ? c * xi - s * yi : xi;
+            row[k + 1] = apply ? s * xi + c * yi : yi;
+        }
+    };
+    int perm[12];
+    tridiag_qr<double, 12>(diag, sub, qapply, perm);
+    RSC_UNROLL for (int j = 0; j < 3; ++j) {
+        const double* row = T + (4 * j + q) * 12;
+        double Qr[12];
+        RSC_UNROLL for (int p = 0; p < 12; ++p) Qr[p] = row[p];
+        RSC_UNROLL for (int c = 0; c < 4; ++c) {
+            double x = Qr[0];
+            RSC_UNROLL for (int p = 1; p < 12; ++p) x = (perm[c] == p) ? Qr[p] : x;
+            ev[j][c] = x;
+        }
+    }
+}
+
 // Kernel 1 of the two-kernel hypothesis solve: sample, control points, alphas, MtM, and the 12x12
 // eigenvectors (quad-cooperative).  Writes the stage record (eigenvectors, alphas, cws) and the
 // sample indices.  STOP < 99 truncates (diagnostics only, tools/phase_bench).

@@ -39,7 +39,7 @@ EXPORTED = [
     "rsc_mlpnp_reset_many", "rsc_mlpnp_get_state", "rsc_mlpnp_last_poses", "rsc_mlpnp_last_samples",
     "rsc_reloc_events", "rsc_loop_events", "rsc_pose_optimization_many",
     "rsc_bow_create", "rsc_bow_destroy", "rsc_bow_set_valid", "rsc_search_by_bow_frame_many",
-    "rsc_search_by_bow_kf_many", "rsc_diag_bow_phase_stamps",
+    "rsc_search_by_bow_kf_many", "rsc_diag_bow_phase_stamps", "rsc_diag_refine_phase_stamps",
 ]
 
 
@@ -156,6 +156,7 @@ def load_library(path: str = LIB_PATH):
                                             C.POINTER(C.c_void_p), i32p]
     L.rsc_diag_bow_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"),
                                             C.c_int]
+    L.rsc_diag_refine_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
     L.rsc_loop_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(Sim3Result), C.POINTER(EventResult)]
     L.rsc_diag_pnp_phase_stamps.argtypes = [C.POINTER(vp), C.c_int, C.c_int,
                                             np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
