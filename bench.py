@@ -56,6 +56,7 @@ def parse():
     p.add_argument("--no-events", action="store_true")
     p.add_argument("--no-poseopt", action="store_true")
     p.add_argument("--no-bow", action="store_true")
+    p.add_argument("--no-sim3match", action="store_true")
     return p.parse_args()
 
 
@@ -375,6 +376,59 @@ def cpu_baseline_bow(F, kfs, seconds):
                        "oracle restatement, 1 thread")
 
 
+def run_sim3match(engine, ctx, probs, args):
+    """SURVEY §8(f) rank 3 (first half): ORBmatcher::SearchBySim3 (ORBmatcher.cpp:948-1170) on 32
+    loop-closure pairs (config-3 shape: ~1000 MapPoints per KeyFrame, 30 % already matched by the
+    Sim3 RANSAC), th = 7.5 as LoopClosing.cpp:309; one rsc_search_by_sim3_many per step (inputs
+    packed and uploaded in the call)."""
+    batch = engine.Sim3Search(ctx, probs, 7.5)
+    for _ in range(args.warmup):
+        batch.run()
+    steps = max(1, args.steps)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _, nf = batch.run()
+    dt = time.perf_counter() - t0
+    ctx.enable_timing(True)
+    kms = 0.0
+    for _ in range(steps):
+        batch.run()
+        kms += ctx.last_timing()["refine_ms"]
+    ctx.enable_timing(False)
+    C = len(probs)
+    pts = sum(p[0].n + p[1].n for p in probs)
+    return dict(pairs_per_s=C * steps / dt, ms_per_step=1e3 * dt / steps, kernel_ms=kms / steps, pairs=C,
+                points_per_pair=pts / C, mean_new_matches=float(np.mean(nf)), steps=steps)
+
+
+def cpu_baseline_sim3match(probs, seconds):
+    """The SearchBySim3 oracle on ONE host core over the same pairs (inputs marshalled once)."""
+    import ctypes
+    import oracle_lib as ol
+    from rsc import engine
+    L = ol.lib()
+    prepared = []
+    for kf1, kf2, R12, t12, m12 in probs:
+        k1, keep1 = engine.sim3_kf_struct(kf1)
+        k2, keep2 = engine.sim3_kf_struct(kf2)
+        prepared.append((k1, k2, keep1, keep2, np.ascontiguousarray(m12, np.int32),
+                         np.ascontiguousarray(np.asarray(R12, np.float32).reshape(9)),
+                         np.ascontiguousarray(np.asarray(t12, np.float32).reshape(3)),
+                         np.zeros(max(kf1.n, 1), np.int32)))
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        for k1, k2, _, _, m12, R, t, out in prepared:
+            L.ora_search_by_sim3(ctypes.addressof(k1), ctypes.addressof(k2), m12, R, t, 7.5, out)
+        done += len(probs)
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=round(done / dt, 2), unit="pairs/s", cores=1, kind="port",
+                sample=f"{done // len(probs)} batches of {len(probs)} KeyFrame pairs in {dt:.1f} s, oracle "
+                       "restatement, 1 thread")
+
+
 def cpu_baseline_poseopt(frames, seconds):
     """The PoseOptimization oracle on ONE host core over the same frames."""
     import oracle_lib as ol
@@ -461,6 +515,12 @@ def main():
     if rank == 0 and not args.no_poseopt:
         po_frames = poseopt_frames(np.random.default_rng(79))
         poseopt = run_poseopt(engine, ctx, po_frames, args)
+    s3m = s3m_probs = None
+    if rank == 0 and not args.no_sim3match:
+        from rsc import synth
+        r3 = np.random.default_rng(81)
+        s3m_probs = [synth.make_sim3match_pair(r3, 1000, 250, 0.3) for _ in range(32)]
+        s3m = run_sim3match(engine, ctx, s3m_probs, args)
     bow = bow_F = bow_K = None
     if rank == 0 and not args.no_bow:
         bow_F, bow_K = bow_views(np.random.default_rng(80))
@@ -539,6 +599,12 @@ def main():
             cb = cpu_baseline_bow(bow_F, bow_K, min(3.0, args.cpu_seconds))
             out["search_by_bow"]["cpu_baseline"] = cb
             out["search_by_bow"]["speedup_vs_cpu_1core"] = round(bow["pairs_per_s"] / cb["value"], 1)
+    if s3m is not None:
+        out["search_by_sim3"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in s3m.items()}
+        if not args.no_cpu and world == 1:
+            cb = cpu_baseline_sim3match(s3m_probs, min(2.0, args.cpu_seconds))
+            out["search_by_sim3"]["cpu_baseline"] = cb
+            out["search_by_sim3"]["speedup_vs_cpu_1core"] = round(s3m["pairs_per_s"] / cb["value"], 1)
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(scenes, args)
         out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 1)

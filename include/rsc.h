@@ -269,6 +269,47 @@ int rsc_search_by_bow_frame_many(rsc_context* ctx, rsc_bow* const* kfs, int coun
 int rsc_search_by_bow_kf_many(rsc_context* ctx, const rsc_bow* kf1, rsc_bow* const* kf2s, int count,
                               float nnratio, int check_orientation, int32_t* const* matches12, int32_t* nmatches);
 
+/* ---- ORBmatcher::SearchBySim3 (src/ORBmatcher.cpp:948-1170) ---------------------------------
+ * The loop-closure matcher run after a Sim3 RANSAC success (LoopClosing.cpp:296-309): unmatched
+ * MapPoints of each KeyFrame are projected into the other with (R12, t12), matched to the best
+ * descriptor among the keypoints of the predicted pyramid levels inside th * scale of the projection
+ * (KeyFrame::GetFeaturesInArea), and kept when both directions agree. */
+typedef struct {
+    int32_t n;                  /* KeyFrame::N */
+    const float* kp;            /* [n][2] mvKeysUn[i].pt */
+    const int32_t* octave;      /* [n] mvKeysUn[i].octave */
+    const uint8_t* desc;        /* [n][32] mDescriptors */
+    const int32_t* cell_begin;  /* [64*48 + 1] CSR over mGrid[ix][iy] (cell = ix * 48 + iy) */
+    const int32_t* cell_feat;   /* mGrid contents, each cell's vector<size_t> in order */
+    float min_x, max_x, min_y, max_y;  /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+    float grid_w_inv, grid_h_inv;      /* mfGridElementWidthInv, mfGridElementHeightInv */
+    float fx, fy, cx, cy;
+    const float* scale_factors; /* [n_levels] mvScaleFactors */
+    int32_t n_levels;           /* mnScaleLevels */
+    float log_scale_factor;     /* mfLogScaleFactor */
+    float Rcw[9], tcw[3];       /* GetRotation(), GetTranslation(), row-major */
+    const uint8_t* mp_state;    /* [n] GetMapPointMatches()[i]: 0 = NULL, 1 = good, 2 = isBad() */
+    const float* mp_pos;        /* [n][3] GetWorldPos() */
+    const float* mp_dmax;       /* [n] mfMaxDistance */
+    const float* mp_dmin;       /* [n] mfMinDistance */
+    const uint8_t* mp_desc;     /* [n][32] MapPoint::GetDescriptor() */
+} rsc_sim3_kf;
+
+typedef struct rsc_kfview rsc_kfview;
+/* Upload a KeyFrame's SearchBySim3 inputs (keypoints, grid, descriptors, pose, MapPoints) to HBM. */
+int rsc_kfview_create(rsc_context* ctx, const rsc_sim3_kf* kf, rsc_kfview** out);
+void rsc_kfview_destroy(rsc_kfview* view);
+
+/* SearchBySim3(pKF1 = kf1[c], pKF2 = kf2[c], vpMatches12, R12[c], t12[c], th) for c < count in one
+ * launch over resident views.  matched12[c][i1] (in, kf1[c] n entries): the KF2 keypoint index of
+ * the MapPoint already in vpMatches12[i1] (GetIndexInKeyFrame(pKF2)), -1 for NULL, -2 for a
+ * MapPoint not in KF2.  out12[c][i1]: the KF2 keypoint index of each new match
+ * (vpMatches12[i1] = vpMapPoints2[idx2]), else -1; nfound[c] = the return value.
+ * R12 [count][9] row-major, t12 [count][3]. */
+int rsc_search_by_sim3_many(rsc_context* ctx, rsc_kfview* const* kf1, rsc_kfview* const* kf2, int count,
+                            const float* R12, const float* t12, float th, const int32_t* const* matched12,
+                            int32_t* const* out12, int32_t* nfound);
+
 /* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP refine launch, [job < 64][8]:
  * entry, compaction, control points, MtM, eigen, betas, check, exit. */
 int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out);

@@ -12,6 +12,8 @@
 #include "mlpnp_oracle.h"
 #include "poseopt_oracle.h"
 #include "orbmatch_oracle.h"
+#include "sim3match_oracle.h"
+#include "../include/rsc.h"
 #include "../orb-slam2-optimized_amd/csrc/rsc_math.h"
 #include "ora_linalg.h"
 
@@ -493,6 +495,32 @@ int64_t ora_search_by_bow_many(int frame_variant, int count, void* const* a, voi
     }
     return tot;
 }
+
+// ---- ORBmatcher::SearchBySim3 (ORBmatcher.cpp:948-1170) ----
+static Sim3KF to_kf(const rsc_sim3_kf& k) {
+    Sim3KF o;
+    o.n = k.n; o.kp = k.kp; o.octave = k.octave; o.desc = k.desc; o.cell_begin = k.cell_begin;
+    o.cell_feat = k.cell_feat; o.min_x = k.min_x; o.max_x = k.max_x; o.min_y = k.min_y; o.max_y = k.max_y;
+    o.grid_w_inv = k.grid_w_inv; o.grid_h_inv = k.grid_h_inv; o.fx = k.fx; o.fy = k.fy; o.cx = k.cx;
+    o.cy = k.cy; o.scale_factors = k.scale_factors; o.n_levels = k.n_levels;
+    o.log_scale_factor = k.log_scale_factor;
+    std::memcpy(o.Rcw, k.Rcw, sizeof(o.Rcw));
+    std::memcpy(o.tcw, k.tcw, sizeof(o.tcw));
+    o.mp_state = k.mp_state; o.mp_pos = k.mp_pos; o.mp_dmax = k.mp_dmax; o.mp_dmin = k.mp_dmin;
+    o.mp_desc = k.mp_desc;
+    return o;
+}
+
+int ora_search_by_sim3(const rsc_sim3_kf* k1, const rsc_sim3_kf* k2, const int32_t* matched12, const float* R12,
+                       const float* t12, float th, int32_t* out12) {
+    return search_by_sim3(to_kf(*k1), to_kf(*k2), matched12, R12, t12, th, out12);
+}
+
+int ora_predict_scale(float dmax, float dist, float log_scale_factor, int n_levels) {
+    return predict_scale(dmax, dist, log_scale_factor, n_levels);
+}
+
+double ora_dm_log(double x) { return rsc::dm::log(x); }
 
 int ora_descriptor_distance(const uint8_t* a, const uint8_t* b) { return descriptor_distance(a, b); }
 

@@ -19,6 +19,7 @@
 #include "rsc_engine.h"
 #include "rsc_poseopt.h"
 #include "rsc_orbmatch.h"
+#include "rsc_sim3match.h"
 
 using namespace rsc;
 
@@ -123,6 +124,9 @@ struct rsc_context {
     DevBuf<char> d_po_res;
     PinBuf<char> h_po_in;
     PinBuf<char> h_po_res;
+    // SearchBySim3: packed KeyFrames + pair table + scratch + outputs (device, pinned mirror)
+    DevBuf<char> d_s3m;
+    PinBuf<char> h_s3m;
     // SearchByBoW: pair table + output vectors + match counts (device, pinned mirror)
     DevBuf<char> d_bow;
     PinBuf<char> h_bow;
@@ -1389,6 +1393,185 @@ int bow_search(rsc_context* C, bool frame_overload, const rsc_bow* const* outer,
     return RSC_OK;
 }
 }  // namespace
+
+
+// ---- ORBmatcher::SearchBySim3 (src/ORBmatcher.cpp:948-1170) ----
+namespace {
+struct S3Blob {
+    std::vector<char> h;
+    size_t add(const void* p, size_t n) {
+        const size_t off = (h.size() + 255) & ~(size_t)255;
+        h.resize(off + n);
+        if (n) std::memcpy(h.data() + off, p, n);
+        return off;
+    }
+    size_t reserve(size_t n) {
+        const size_t off = (h.size() + 255) & ~(size_t)255;
+        h.resize(off + n);
+        return off;
+    }
+};
+
+int check_sim3_kf(const rsc_sim3_kf& k) {
+    if (k.n < 0 || k.n_levels < 1 || !k.cell_begin || !k.scale_factors) return RSC_ERR_ARG;
+    if (k.n > 0 && (!k.kp || !k.octave || !k.desc || !k.mp_state || !k.mp_pos || !k.mp_dmax || !k.mp_dmin ||
+                    !k.mp_desc))
+        return RSC_ERR_ARG;
+    const int cells = kSim3GridCols * kSim3GridRows;
+    if (k.cell_begin[0] != 0) return RSC_ERR_ARG;
+    for (int c = 0; c < cells; ++c)
+        if (k.cell_begin[c + 1] < k.cell_begin[c]) return RSC_ERR_ARG;
+    const int nf = k.cell_begin[cells];
+    if (nf > 0 && !k.cell_feat) return RSC_ERR_ARG;
+    for (int e = 0; e < nf; ++e)
+        if (k.cell_feat[e] < 0 || k.cell_feat[e] >= k.n) {
+            g_last_error = "mGrid index out of range";
+            return RSC_ERR_ARG;
+        }
+    return 0;
+}
+}  // namespace
+
+struct rsc_kfview {
+    rsc_context* ctx = nullptr;
+    int n = 0;
+    DevBuf<char> mem;  // DevSim3KF header | kp | octave | desc | grid | scales | MapPoints
+    const DevSim3KF* hdr = nullptr;
+};
+
+int rsc_kfview_create(rsc_context* C, const rsc_sim3_kf* k, rsc_kfview** out) {
+    if (!C || !k || !out) return RSC_ERR_ARG;
+    *out = nullptr;
+    if (int e = check_sim3_kf(*k)) return e;
+    const int cells = kSim3GridCols * kSim3GridRows;
+    const size_t n = (size_t)k->n, nf = (size_t)k->cell_begin[cells];
+    // two passes over the same layout: sizes, then the copy into one host image
+    S3Blob b;
+    const size_t o_hdr = b.reserve(sizeof(DevSim3KF));
+    const size_t o_kp = b.add(k->kp, 8 * n), o_oct = b.add(k->octave, 4 * n), o_desc = b.add(k->desc, 32 * n);
+    const size_t o_cb = b.add(k->cell_begin, 4 * (size_t)(cells + 1)), o_cf = b.add(k->cell_feat, 4 * nf);
+    const size_t o_sc = b.add(k->scale_factors, 4 * (size_t)k->n_levels), o_st = b.add(k->mp_state, n);
+    const size_t o_pos = b.add(k->mp_pos, 12 * n), o_mx = b.add(k->mp_dmax, 4 * n), o_mn = b.add(k->mp_dmin, 4 * n);
+    const size_t o_md = b.add(k->mp_desc, 32 * n);
+    std::unique_ptr<rsc_kfview> v(new rsc_kfview);
+    v->ctx = C;
+    v->n = k->n;
+    RSC_HIP(hipSetDevice(C->device));
+    if (int e = v->mem.ensure(b.h.size())) return e;
+    char* d = v->mem.p;
+    DevSim3KF h;
+    h.kp = reinterpret_cast<const float2*>(d + o_kp);
+    h.octave = reinterpret_cast<const int32_t*>(d + o_oct);
+    h.desc = reinterpret_cast<const uint4*>(d + o_desc);
+    h.cell_begin = reinterpret_cast<const int32_t*>(d + o_cb);
+    h.cell_feat = reinterpret_cast<const int32_t*>(d + o_cf);
+    h.scale = reinterpret_cast<const float*>(d + o_sc);
+    h.mp_state = reinterpret_cast<const uint8_t*>(d + o_st);
+    h.mp_pos = reinterpret_cast<const float*>(d + o_pos);
+    h.mp_dmax = reinterpret_cast<const float*>(d + o_mx);
+    h.mp_dmin = reinterpret_cast<const float*>(d + o_mn);
+    h.mp_desc = reinterpret_cast<const uint4*>(d + o_md);
+    h.min_x = k->min_x; h.max_x = k->max_x; h.min_y = k->min_y; h.max_y = k->max_y;
+    h.gw_inv = k->grid_w_inv; h.gh_inv = k->grid_h_inv;
+    h.fx = k->fx; h.fy = k->fy; h.cx = k->cx; h.cy = k->cy;
+    h.log_sf = k->log_scale_factor;
+    std::memcpy(h.R, k->Rcw, sizeof(h.R));
+    std::memcpy(h.t, k->tcw, sizeof(h.t));
+    h.n = k->n;
+    h.n_levels = k->n_levels;
+    std::memcpy(b.h.data() + o_hdr, &h, sizeof(h));
+    RSC_HIP(hipMemcpy(d, b.h.data(), b.h.size(), hipMemcpyHostToDevice));
+    v->hdr = reinterpret_cast<const DevSim3KF*>(d + o_hdr);
+    *out = v.release();
+    return RSC_OK;
+}
+
+void rsc_kfview_destroy(rsc_kfview* v) {
+    if (!v) return;
+    (void)hipStreamSynchronize(v->ctx->stream);
+    delete v;
+}
+
+int rsc_search_by_sim3_many(rsc_context* C, rsc_kfview* const* kf1, rsc_kfview* const* kf2, int count,
+                            const float* R12, const float* t12, float th, const int32_t* const* matched12,
+                            int32_t* const* out12, int32_t* nfound) {
+    if (!C || count < 0 || (count && (!kf1 || !kf2 || !R12 || !t12 || !matched12 || !out12))) return RSC_ERR_ARG;
+    if (count == 0) return RSC_OK;
+    int max_points = 0;
+    for (int c = 0; c < count; ++c) {
+        if (!kf1[c] || !kf2[c] || kf1[c]->ctx != C || kf2[c]->ctx != C) return RSC_ERR_ARG;
+        if (kf1[c]->n && (!matched12[c] || !out12[c])) return RSC_ERR_ARG;
+        max_points = std::max(max_points, std::max(kf1[c]->n, kf2[c]->n));
+    }
+    // layout: pair table | vbAlreadyMatched1/2 flags (host-derived, :972-984) | vnMatch1/2 scratch |
+    // outputs (the only part that comes back)
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    std::vector<size_t> o_a1(count), o_a2(count), o_m1(count), o_m2(count), o_out(count), o_nf(count);
+    size_t off = al(sizeof(Sim3MatchPair) * count);
+    for (int c = 0; c < count; ++c) {
+        o_a1[c] = off; off = al(off + std::max(kf1[c]->n, 1));
+        o_a2[c] = off; off = al(off + std::max(kf2[c]->n, 1));
+    }
+    const size_t up = off;
+    for (int c = 0; c < count; ++c) {
+        o_m1[c] = off; off = al(off + 4 * (size_t)std::max(kf1[c]->n, 1));
+        o_m2[c] = off; off = al(off + 4 * (size_t)std::max(kf2[c]->n, 1));
+    }
+    const size_t back = off;
+    for (int c = 0; c < count; ++c) {
+        o_out[c] = off; off = al(off + 4 * (size_t)std::max(kf1[c]->n, 1));
+        o_nf[c] = off; off += 4;
+    }
+    const size_t bytes = al(off);
+    RSC_HIP(hipSetDevice(C->device));
+    if (int e = C->d_s3m.ensure(bytes)) return e;
+    if (int e = C->h_s3m.ensure(bytes)) return e;
+    RSC_HIP(hipStreamSynchronize(C->stream));  // the pinned mirror is free again
+    char* h = C->h_s3m.p;
+    char* d = C->d_s3m.p;
+    for (int c = 0; c < count; ++c) {
+        const int n1 = kf1[c]->n, n2 = kf2[c]->n;
+        uint8_t* a1 = reinterpret_cast<uint8_t*>(h + o_a1[c]);
+        uint8_t* a2 = reinterpret_cast<uint8_t*>(h + o_a2[c]);
+        std::memset(a1, 0, (size_t)std::max(n1, 1));
+        std::memset(a2, 0, (size_t)std::max(n2, 1));
+        for (int i = 0; i < n1; ++i) {
+            const int32_t m = matched12[c][i];
+            if (m < -2 || m >= n2) return RSC_ERR_ARG;
+            if (m == -1) continue;
+            a1[i] = 1;
+            if (m >= 0) a2[m] = 1;
+        }
+        Sim3MatchPair p;
+        p.k1 = kf1[c]->hdr;
+        p.k2 = kf2[c]->hdr;
+        std::memcpy(p.R12, R12 + 9 * c, sizeof(p.R12));
+        std::memcpy(p.t12, t12 + 3 * c, sizeof(p.t12));
+        p.already1 = reinterpret_cast<const uint8_t*>(d + o_a1[c]);
+        p.already2 = reinterpret_cast<const uint8_t*>(d + o_a2[c]);
+        p.m1 = reinterpret_cast<int32_t*>(d + o_m1[c]);
+        p.m2 = reinterpret_cast<int32_t*>(d + o_m2[c]);
+        p.out = reinterpret_cast<int32_t*>(d + o_out[c]);
+        p.nfound = reinterpret_cast<int32_t*>(d + o_nf[c]);
+        std::memcpy(h + sizeof(Sim3MatchPair) * c, &p, sizeof(p));
+    }
+    RSC_HIP(hipMemcpyAsync(d, h, up, hipMemcpyHostToDevice, C->stream));
+    timing_begin(C, 3);
+    RSC_HIP(launch_search_by_sim3(count, max_points, reinterpret_cast<const Sim3MatchPair*>(d), th, C->stream));
+    timing_begin(C, 4);
+    RSC_HIP(hipMemcpyAsync(h + back, d + back, bytes - back, hipMemcpyDeviceToHost, C->stream));
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    if (C->timing) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, C->ev[3], C->ev[4]);
+        C->last_ms[2] = ms;
+    }
+    for (int c = 0; c < count; ++c) {
+        if (kf1[c]->n) std::memcpy(out12[c], h + o_out[c], 4 * (size_t)kf1[c]->n);
+        if (nfound) std::memcpy(&nfound[c], h + o_nf[c], 4);
+    }
+    return RSC_OK;
+}
 
 int rsc_diag_refine_phase_stamps(rsc_context* C, uint64_t* out) {
     if (!C || !out) return RSC_ERR_ARG;

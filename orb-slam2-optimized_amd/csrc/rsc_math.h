@@ -253,5 +253,63 @@ RSCM_HD double cbrt(double x) {
     return from_words(hi_word(t) | sign, lo_word(t));
 }
 
+// e_log (fdlibm 5.3): argument reduction to [sqrt(2)/2, sqrt(2)], s = f/(2+f), minimax R(z).
+// Used by ORBmatcher::SearchBySim3 through MapPoint::PredictScale (MapPoint.cpp:367-381, log of a
+// float ratio; logf(x) is restated as the float rounding of this double log).
+RSCM_HD double log(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                 two54 = 1.80143985094819840000e+16, Lg1 = 6.666666666666735130e-01,
+                 Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                 Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01, Lg7 = 1.479819860511658591e-01;
+    int32_t hx = (int32_t)hi_word(x);
+    const uint32_t lx = lo_word(x);
+    int32_t k = 0;
+    if (hx < 0x00100000) {                                  // x < 2^-1022
+        if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -two54 / 0.0;  // log(+-0) = -inf
+        if (hx < 0) return (x - x) / 0.0;                   // log(-x) = NaN
+        k -= 54;
+        x *= two54;
+        hx = (int32_t)hi_word(x);
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    const int32_t i0 = (hx + 0x95f64) & 0x100000;
+    x = from_words((uint32_t)(hx | (i0 ^ 0x3ff00000)), lo_word(x));  // normalise x or x/2
+    k += (i0 >> 20);
+    const double f = x - 1.0;
+    if ((0x000fffff & (2 + hx)) < 3) {  // |f| < 2^-20
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            const double dk = (double)k;
+            return dk * ln2_hi + dk * ln2_lo;
+        }
+        const double R = f * f * (0.5 - 0.33333333333333333 * f);
+        if (k == 0) return f - R;
+        const double dk = (double)k;
+        return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    const double s = f / (2.0 + f);
+    const double dk = (double)k;
+    const double z = s * s;
+    int32_t i = hx - 0x6147a;
+    const double w = z * z;
+    const int32_t j = 0x6b851 - hx;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i |= j;
+    const double R = t2 + t1;
+    if (i > 0) {
+        const double hfsq = 0.5 * f * f;
+        if (k == 0) return f - (hfsq - s * (hfsq + R));
+        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    if (k == 0) return f - s * (f - R);
+    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+// logf as the float rounding of the double log above.
+RSCM_HD float logf(float x) { return (float)log((double)x); }
+
 }  // namespace dm
 }  // namespace rsc

@@ -40,6 +40,7 @@ EXPORTED = [
     "rsc_reloc_events", "rsc_loop_events", "rsc_pose_optimization_many",
     "rsc_bow_create", "rsc_bow_destroy", "rsc_bow_set_valid", "rsc_search_by_bow_frame_many",
     "rsc_search_by_bow_kf_many", "rsc_diag_bow_phase_stamps", "rsc_diag_refine_phase_stamps",
+    "rsc_search_by_sim3_many", "rsc_kfview_create", "rsc_kfview_destroy",
 ]
 
 
@@ -78,6 +79,99 @@ class PoseOptProblem(C.Structure):
 class BowFeatures(C.Structure):
     _fields_ = [("n", C.c_int32), ("desc", C.c_void_p), ("angle", C.c_void_p), ("valid", C.c_void_p),
                 ("n_nodes", C.c_int32), ("node_id", C.c_void_p), ("node_begin", C.c_void_p), ("feat", C.c_void_p)]
+
+
+class Sim3KFStruct(C.Structure):
+    """rsc_sim3_kf (include/rsc.h)."""
+    _fields_ = [("n", C.c_int32), ("kp", C.c_void_p), ("octave", C.c_void_p), ("desc", C.c_void_p),
+                ("cell_begin", C.c_void_p), ("cell_feat", C.c_void_p), ("min_x", C.c_float), ("max_x", C.c_float),
+                ("min_y", C.c_float), ("max_y", C.c_float), ("grid_w_inv", C.c_float), ("grid_h_inv", C.c_float),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("scale_factors", C.c_void_p), ("n_levels", C.c_int32), ("log_scale_factor", C.c_float),
+                ("Rcw", C.c_float * 9), ("tcw", C.c_float * 3), ("mp_state", C.c_void_p), ("mp_pos", C.c_void_p),
+                ("mp_dmax", C.c_void_p), ("mp_dmin", C.c_void_p), ("mp_desc", C.c_void_p)]
+
+
+def sim3_kf_struct(kf):
+    """(ctypes rsc_sim3_kf, keep-alive arrays) for a rsc.synth.Sim3KF-like object."""
+    from rsc import synth
+    keep = [np.ascontiguousarray(kf.kp, np.float32), np.ascontiguousarray(kf.octave, np.int32),
+            np.ascontiguousarray(kf.desc, np.uint8), np.ascontiguousarray(kf.cell_begin, np.int32),
+            np.ascontiguousarray(kf.cell_feat, np.int32), synth.scale_factors(),
+            np.ascontiguousarray(kf.mp_state, np.uint8), np.ascontiguousarray(kf.mp_pos, np.float32),
+            np.ascontiguousarray(kf.mp_dmax, np.float32), np.ascontiguousarray(kf.mp_dmin, np.float32),
+            np.ascontiguousarray(kf.mp_desc, np.uint8)]
+    if keep[4].size == 0:
+        keep[4] = np.zeros(1, np.int32)
+    k = Sim3KFStruct()
+    k.n = int(kf.n)
+    (k.kp, k.octave, k.desc, k.cell_begin, k.cell_feat, k.scale_factors, k.mp_state, k.mp_pos, k.mp_dmax,
+     k.mp_dmin, k.mp_desc) = (a.ctypes.data for a in keep)
+    k.min_x, k.max_x, k.min_y, k.max_y = kf.min_x, kf.max_x, kf.min_y, kf.max_y
+    k.grid_w_inv, k.grid_h_inv = float(synth.GRID_W_INV), float(synth.GRID_H_INV)
+    k.fx, k.fy, k.cx, k.cy = kf.fx, kf.fy, kf.cx, kf.cy
+    k.n_levels = len(keep[5])
+    k.log_scale_factor = float(synth.LOG_SCALE_FACTOR)
+    k.Rcw[:] = [float(v) for v in np.asarray(kf.Rcw, np.float32).reshape(9)]
+    k.tcw[:] = [float(v) for v in np.asarray(kf.tcw, np.float32).reshape(3)]
+    return k, keep
+
+
+class KFView:
+    """A KeyFrame's SearchBySim3 inputs resident in HBM (rsc_kfview_create)."""
+
+    def __init__(self, ctx: Context, kf):
+        self.ctx, self.n = ctx, int(kf.n)
+        k, keep = sim3_kf_struct(kf)
+        h = C.c_void_p()
+        _check(load_library().rsc_kfview_create(ctx.h, C.byref(k), C.byref(h)), "rsc_kfview_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            load_library().rsc_kfview_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+class Sim3Search:
+    """Prepared ORBmatcher::SearchBySim3 batch (ORBmatcher.cpp:948-1170): count (kf1, kf2, R12, t12,
+    matched12) problems in one launch over resident KeyFrame views, threshold th (7.5 in
+    LoopClosing.cpp:309).  The same KeyFrame object is uploaded once."""
+
+    def __init__(self, ctx: Context, problems, th: float = 7.5):
+        self.ctx, self.th = ctx, float(th)
+        c = len(problems)
+        self.count = c
+        self.views = {}
+        for p in problems:
+            for kf in (p[0], p[1]):
+                if id(kf) not in self.views:
+                    self.views[id(kf)] = KFView(ctx, kf)
+        self.h1 = (C.c_void_p * max(c, 1))(*[self.views[id(p[0])].h.value for p in problems])
+        self.h2 = (C.c_void_p * max(c, 1))(*[self.views[id(p[1])].h.value for p in problems])
+        self.R = np.ascontiguousarray(np.stack([np.asarray(p[2], np.float32).reshape(9) for p in problems]))
+        self.t = np.ascontiguousarray(np.stack([np.asarray(p[3], np.float32).reshape(3) for p in problems]))
+        self.m_in = [np.ascontiguousarray(p[4], np.int32) for p in problems]
+        self.out = [np.full(max(p[0].n, 1), -7, np.int32) for p in problems]
+        self.pin = (C.c_void_p * max(c, 1))(*[a.ctypes.data for a in self.m_in])
+        self.pout = (C.c_void_p * max(c, 1))(*[a.ctypes.data for a in self.out])
+        self.nfound = np.zeros(max(c, 1), np.int32)
+        self.n1 = [p[0].n for p in problems]
+
+    def run(self):
+        _check(load_library().rsc_search_by_sim3_many(self.ctx.h, self.h1, self.h2, self.count, self.R, self.t,
+                                                      self.th, self.pin, self.pout, self.nfound),
+               "rsc_search_by_sim3_many")
+        return [o[:n] for o, n in zip(self.out, self.n1)], self.nfound[:self.count]
+
+
+def search_by_sim3_many(ctx: Context, problems, th: float = 7.5):
+    """SearchBySim3 for each (kf1, kf2, R12, t12, matched12): returns (list of out12 int32 arrays =
+    new match's KF2 keypoint or -1, nfound int32[count])."""
+    return Sim3Search(ctx, problems, th).run()
 
 
 class PoseOptResult(C.Structure):
@@ -157,6 +251,11 @@ def load_library(path: str = LIB_PATH):
     L.rsc_diag_bow_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"),
                                             C.c_int]
     L.rsc_diag_refine_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
+    f32p_ = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+    L.rsc_kfview_create.argtypes = [vp, C.POINTER(Sim3KFStruct), C.POINTER(vp)]
+    L.rsc_kfview_destroy.argtypes = [vp]
+    L.rsc_search_by_sim3_many.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.c_int, f32p_, f32p_, C.c_float,
+                                          C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), i32p]
     L.rsc_loop_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(Sim3Result), C.POINTER(EventResult)]
     L.rsc_diag_pnp_phase_stamps.argtypes = [C.POINTER(vp), C.c_int, C.c_int,
                                             np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]

@@ -291,3 +291,128 @@ def make_bow_related(rng: np.random.Generator, src: BowFeatures, n: int, overlap
     nodes[dst[keep]] = src_nodes[srcs[keep]]
     v.node_id, v.node_begin, v.feat = _feature_vector(nodes)
     return v
+
+
+# ---- ORBmatcher::SearchBySim3 inputs ----------------------------------------------------------
+GRID_COLS, GRID_ROWS = 64, 48  # FRAME_GRID_COLS / ROWS (include/Frame.hpp:20-21)
+
+
+@dataclasses.dataclass
+class Sim3KF:
+    """One KeyFrame as SearchBySim3 reads it (rsc_sim3_kf, include/rsc.h)."""
+    n: int
+    kp: np.ndarray          # float32 [n,2] mvKeysUn[i].pt
+    octave: np.ndarray      # int32 [n]
+    desc: np.ndarray        # uint8 [n,32]
+    cell_begin: np.ndarray  # int32 [64*48+1]
+    cell_feat: np.ndarray   # int32 []
+    Rcw: np.ndarray         # float32 [3,3]
+    tcw: np.ndarray         # float32 [3]
+    mp_state: np.ndarray    # uint8 [n] 0 NULL, 1 good, 2 bad
+    mp_pos: np.ndarray      # float32 [n,3]
+    mp_dmax: np.ndarray     # float32 [n]
+    mp_dmin: np.ndarray     # float32 [n]
+    mp_desc: np.ndarray     # uint8 [n,32]
+    mp_id: np.ndarray       # int64 [n] MapPoint identity (-1 = none), to build matched12
+    fx: float = float(FX)
+    fy: float = float(FY)
+    cx: float = float(CX)
+    cy: float = float(CY)
+    min_x: float = 0.0
+    max_x: float = float(WIDTH)
+    min_y: float = 0.0
+    max_y: float = float(HEIGHT)
+
+
+def scale_factors() -> np.ndarray:
+    sf = [np.float32(1.0)]
+    for _ in range(1, N_LEVELS):
+        sf.append(np.float32(sf[-1] * SCALE_FACTOR))
+    return np.array(sf, np.float32)
+
+
+LOG_SCALE_FACTOR = np.float32(np.log(np.float32(1.2)))
+GRID_W_INV = np.float32(np.float32(GRID_COLS) / np.float32(WIDTH))   # mfGridElementWidthInv (Frame.cpp)
+GRID_H_INV = np.float32(np.float32(GRID_ROWS) / np.float32(HEIGHT))
+
+
+def build_grid(kp: np.ndarray):
+    """Frame::AssignFeaturesToGrid (PosInGrid with round()), as CSR over cell = ix * 48 + iy."""
+    px = np.floor((kp[:, 0] - 0.0) * GRID_W_INV + 0.5).astype(np.int64)
+    py = np.floor((kp[:, 1] - 0.0) * GRID_H_INV + 0.5).astype(np.int64)
+    ok = (px >= 0) & (px < GRID_COLS) & (py >= 0) & (py < GRID_ROWS)
+    cell = np.where(ok, px * GRID_ROWS + py, -1)
+    idx = np.nonzero(ok)[0]
+    order = idx[np.lexsort((idx, cell[idx]))]
+    counts = np.bincount(cell[order], minlength=GRID_COLS * GRID_ROWS)
+    begin = np.zeros(GRID_COLS * GRID_ROWS + 1, np.int32)
+    begin[1:] = np.cumsum(counts)
+    return begin, order.astype(np.int32)
+
+
+def _flip(rng, d, mean):
+    out = d.copy()
+    for i in range(len(out)):
+        k = min(int(rng.poisson(mean)), 255)
+        bits = rng.choice(256, size=k, replace=False)
+        np.bitwise_xor.at(out[i], bits // 8, (1 << (bits % 8)).astype(np.uint8))
+    return out
+
+
+def make_sim3match_pair(rng: np.random.Generator, n_points: int = 1000, n_extra: int = 300,
+                        matched_frac: float = 0.3, bad_frac: float = 0.03, noise_px: float = 1.0,
+                        pose_noise: float = 0.002):
+    """Two KeyFrames observing n_points common world points (plus n_extra unmatched keypoints each),
+    the relative pose (R12, t12) with a small error (a Sim3 RANSAC estimate), and the matched12 input
+    (a `matched_frac` share of common points already matched).  Returns (kf1, kf2, R12, t12, matched12)."""
+    sf = scale_factors()
+    P = np.stack([rng.uniform(-3, 3, n_points), rng.uniform(-2, 2, n_points), rng.uniform(2, 10, n_points)], 1)
+    R1 = random_rotation(rng, 0.2)
+    t1 = -R1 @ np.array([0.0, 0.0, 0.0])
+    R2 = random_rotation(rng, 0.15) @ R1
+    c2 = rng.normal(0, 0.3, 3)
+    t2 = -R2 @ c2
+    mp_ids = np.arange(n_points)
+    mp_desc = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    kfs = []
+    for R, t in ((R1, t1), (R2, t2)):
+        Xc = P @ R.T + t
+        uv = np.stack([FX * Xc[:, 0] / Xc[:, 2] + CX, FY * Xc[:, 1] / Xc[:, 2] + CY], 1)
+        vis = (Xc[:, 2] > 0.1) & (uv[:, 0] >= 0) & (uv[:, 0] < WIDTH) & (uv[:, 1] >= 0) & (uv[:, 1] < HEIGHT)
+        ids = np.nonzero(vis)[0]
+        m = len(ids) + n_extra
+        kp = np.zeros((m, 2), np.float32)
+        kp[:len(ids)] = uv[ids] + rng.normal(0, noise_px, (len(ids), 2))
+        kp[len(ids):] = np.stack([rng.uniform(0, WIDTH, n_extra), rng.uniform(0, HEIGHT, n_extra)], 1)
+        kp = np.clip(kp, 0, [WIDTH - 1e-3, HEIGHT - 1e-3]).astype(np.float32)
+        octave = rng.choice(N_LEVELS, size=m, p=level_probabilities()).astype(np.int32)
+        desc = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+        desc[:len(ids)] = _flip(rng, mp_desc[ids], 8.0)
+        perm = rng.permutation(m)  # keypoint order unrelated to point order
+        kp, octave, desc = kp[perm], octave[perm], desc[perm]
+        mp_id = np.full(m, -1, np.int64)
+        src = np.concatenate([ids, np.full(n_extra, -1)])[perm]
+        mp_id[:] = src
+        has = mp_id >= 0
+        state = np.where(has, 1, 0).astype(np.uint8)
+        state[has & (rng.random(m) < bad_frac)] = 2
+        pos = np.zeros((m, 3), np.float32)
+        pos[has] = P[mp_id[has]]
+        dist = np.linalg.norm(P[np.maximum(mp_id, 0)] - (-R.T @ t), axis=1)
+        dmax = np.where(has, dist * sf[octave], 0).astype(np.float32)   # MapPoint::UpdateNormalAndDepth
+        dmin = (dmax / sf[N_LEVELS - 1]).astype(np.float32)
+        mdesc = np.zeros((m, 32), np.uint8)
+        mdesc[has] = mp_desc[mp_id[has]]
+        begin, feat = build_grid(kp)
+        kfs.append(Sim3KF(m, kp, octave, desc, begin, feat, R.astype(np.float32), t.astype(np.float32), state,
+                          pos, dmax, dmin, mdesc, mp_id))
+    kf1, kf2 = kfs
+    # p1 = R12 p2 + t12 (camera 2 -> camera 1), perturbed like a RANSAC estimate
+    R12 = (random_rotation(rng, pose_noise) @ (R1 @ R2.T)).astype(np.float32)
+    t12 = (t1 - (R1 @ R2.T) @ t2 + rng.normal(0, pose_noise, 3)).astype(np.float32)
+    where2 = {int(i): j for j, i in enumerate(kf2.mp_id) if i >= 0}
+    matched12 = np.full(kf1.n, -1, np.int32)
+    for i, mid in enumerate(kf1.mp_id):
+        if mid >= 0 and rng.random() < matched_frac:
+            matched12[i] = where2.get(int(mid), -2)
+    return kf1, kf2, R12, t12, matched12

@@ -8,6 +8,8 @@
   iteration / trial counts) on seeded synthetic Frames (regression pins, parity unpinned).
 * bow_traces.npz — ORBmatcher::SearchByBoW (both overloads) inputs and oracle outputs on seeded
   synthetic views (the views themselves are stored, so the fixture does not depend on the generator).
+* sim3match_traces.npz — ORBmatcher::SearchBySim3 inputs (both KeyFrames, R12/t12, matched12) and
+  oracle outputs on seeded synthetic pairs.
 * pnp_traces.npz / sim3_traces.npz — per-hypothesis sample indices, inlier counts and poses of the
   oracle restatement on small seeded scenes (regression pins of the oracle; the reference itself
   cannot be built here, see DESIGN.md "Oracle").
@@ -141,7 +143,33 @@ def bow():
     np.savez_compressed(os.path.join(HERE, "bow_traces.npz"), **out)
 
 
+S3_FIELDS = ("kp", "octave", "desc", "cell_begin", "cell_feat", "Rcw", "tcw", "mp_state", "mp_pos", "mp_dmax",
+             "mp_dmin", "mp_desc")
+
+
+def sim3match():
+    import oracle_lib as ol
+    from rsc import synth
+    out = {}
+    cases = [(31, 300, 80, 0.3), (32, 600, 150, 0.5), (33, 150, 40, 0.0)]
+    for k, (seed, n, extra, mf) in enumerate(cases):
+        kf1, kf2, R12, t12, m12 = synth.make_sim3match_pair(np.random.default_rng(seed), n, extra, mf)
+        nf, res = ol.search_by_sim3(kf1, kf2, R12, t12, m12)
+        for side, v in (("A", kf1), ("B", kf2)):
+            for f in S3_FIELDS:
+                out[f"c{k}_{side}_{f}"] = getattr(v, f)
+        out[f"c{k}_R12"], out[f"c{k}_t12"], out[f"c{k}_m12"] = R12, t12, m12
+        out[f"c{k}_n"] = np.int32(nf)
+        out[f"c{k}_out"] = res
+        print(f"c{k} nfound", nf)
+    out["cases"] = np.int32(len(cases))
+    np.savez_compressed(os.path.join(HERE, "sim3match_traces.npz"), **out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "sim3match":
+        sim3match()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "poseopt":
         poseopt()
         sys.exit(0)

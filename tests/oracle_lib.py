@@ -115,6 +115,10 @@ def lib():
     L.ora_search_by_bow_many.argtypes = [C.c_int, C.c_int, C.POINTER(vp), vp, C.c_float, C.c_int, i32p,
                                          C.c_int64, i32p]
     L.ora_descriptor_distance.argtypes = [u8p, u8p]
+    L.ora_search_by_sim3.argtypes = [vp, vp, i32p, f32p, f32p, C.c_float, i32p]
+    L.ora_predict_scale.argtypes = [C.c_float, C.c_float, C.c_float, C.c_int]
+    L.ora_dm_log.restype = C.c_double
+    L.ora_dm_log.argtypes = [C.c_double]
     L.ora_compute_three_maxima.argtypes = [i32p, C.c_int, i32p]
     _lib = L
     return L
@@ -408,3 +412,15 @@ def compute_three_maxima(sizes):
     ind = np.zeros(3, np.int32)
     lib().ora_compute_three_maxima(np.ascontiguousarray(sizes, np.int32), len(sizes), ind)
     return tuple(int(x) for x in ind)
+
+
+def search_by_sim3(kf1, kf2, R12, t12, matched12, th=7.5):
+    """ORBmatcher::SearchBySim3 on the oracle: (nfound, out12 int32[kf1.n])."""
+    from rsc import engine
+    k1, keep1 = engine.sim3_kf_struct(kf1)
+    k2, keep2 = engine.sim3_kf_struct(kf2)
+    out = np.full(max(kf1.n, 1), -7, np.int32)
+    nf = lib().ora_search_by_sim3(C.addressof(k1), C.addressof(k2), np.ascontiguousarray(matched12, np.int32),
+                                  np.ascontiguousarray(np.asarray(R12, np.float32).reshape(9)),
+                                  np.ascontiguousarray(np.asarray(t12, np.float32).reshape(3)), th, out)
+    return nf, out[:kf1.n]
