@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cfloat>
 #include <cmath>
+#include <utility>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -119,13 +120,22 @@ RSC_HD void eig_sort(S (&diag)[n], int (&perm)[n]) {
     }
 }
 
+// Optional hook of a QR rotation sink: `q.prefetch(k)` is called at the top of the chase slot k,
+// before the Givens rotation is computed, so that a sink keeping Q in LDS issues the loads of
+// columns k, k+1 while the chase runs (each slot is its own basic block; loads placed inside
+// qapply are issued after the rotation and waited for at once, serialising the slots).
+template <typename Q, typename = void>
+struct qr_has_prefetch { static constexpr bool value = false; };
+template <typename Q>
+struct qr_has_prefetch<Q, decltype((void)std::declval<Q&>().prefetch(0))> { static constexpr bool value = true; };
+
 // Implicit symmetric QR iterations on (diag, sub) with the rotations handed to
 // `qapply(k, c, s, apply)` (which must perform Q = Q * G on columns k,k+1 when `apply`, and leave
 // Q bit-identical otherwise).  computeFromTridiagonal_impl + sort.
 // Returns Eigen's "Success".  perm: the sort's column permutation (identity when not converged,
 // as Eigen skips the sort then); the caller applies it to its eigenvector storage.
 template <typename S, int n, typename QApply>
-RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply qapply, int (&perm)[n]) {
+RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, int (&perm)[n]) {
     const int maxIterations = 30;
     int end = n - 1, start = 0, iter = 0;
     const S considerAsZero = lim<S>::min();
@@ -178,6 +188,7 @@ RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply qapply, int (&perm)
         S z = zS;
         RSC_UNROLL for (int k = 0; k < n - 1; ++k) {
             if (k >= start && k < end) {
+                if constexpr (qr_has_prefetch<QApply>::value) qapply.prefetch(k);
                 S c, s;
                 make_givens(x, z, c, s);
                 S sdk = s * diag[k] + c * sub[k];

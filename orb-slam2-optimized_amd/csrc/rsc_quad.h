@@ -160,6 +160,30 @@ __device__ __forceinline__ void quad_accumulate(double (&Qc)[3][12], int q, cons
     }
 }
 
+// The quad's own three rows of Q (rows q, q+4, q+8 of the row-major 12x12 in T) as the QR's
+// rotation sink: prefetch(k) loads columns k, k+1 at the top of the chase slot so the LDS round
+// trip overlaps the Givens computation; operator() rotates and stores them (tridiag_qr's
+// qapply contract: bit-identical values when !apply).
+struct QuadLdsRows {
+    double* T;
+    int q;
+    double x[3], y[3];
+    RSC_HD void prefetch(int k) {
+        RSC_UNROLL for (int j = 0; j < 3; ++j) {
+            const double* row = T + (4 * j + q) * 12;
+            x[j] = row[k];
+            y[j] = row[k + 1];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the rotation's chain
+    }
+    RSC_HD void operator()(int k, double c, double s, bool apply) {
+        RSC_UNROLL for (int j = 0; j < 3; ++j) {
+            double* row = T + (4 * j + q) * 12;
+            row[k] = apply ? c * x[j] - s * y[j] : x[j];
+            row[k + 1] = apply ? s * x[j] + c * y[j] : y[j];
+        }
+    }
+};
 
 // Eigenvectors of the four smallest eigenvalues of a symmetric 12x12 (SelfAdjointEigenSolver on
 // MtM, PnPsolver.cpp:379-382) by the four lanes of one quad (q = lane & 3): phases B-D of
@@ -203,14 +227,7 @@ __device__ __forceinline__ void quad_eig12_ev4(double* T, double* E, int q, Sync
             RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + 4 * j + q] = Qc[j][r];
     }
     sync();
-    auto qapply = [&](int k, double c, double s, bool apply) {
-        RSC_UNROLL for (int j = 0; j < 3; ++j) {
-            double* row = T + (4 * j + q) * 12;
-            const double xi = row[k], yi = row[k + 1];
-            row[k] = apply ? c * xi - s * yi : xi;
-            row[k + 1] = apply ? s * xi + c * yi : yi;
-        }
-    };
+    QuadLdsRows qapply{T, q};
     int perm[12];
     tridiag_qr<double, 12>(diag, sub, qapply, perm);
     RSC_UNROLL for (int j = 0; j < 3; ++j) {
@@ -342,14 +359,7 @@ __device__ __forceinline__ void pnp_eig_quad_body(const DevPnP* __restrict__ pro
     // Givens chase's dependency chain, and keeping 36 doubles per lane out of the register file
     // removes the chase's register spills (scratch round trips inside the QR loop).
     {
-        auto qapply = [&](int k, double c, double s, bool apply) {
-            RSC_UNROLL for (int j = 0; j < 3; ++j) {
-                double* row = T + (4 * j + q) * 12;
-                const double xi = row[k], yi = row[k + 1];
-                row[k] = apply ? c * xi - s * yi : xi;
-                row[k + 1] = apply ? s * xi + c * yi : yi;
-            }
-        };
+        QuadLdsRows qapply{T, q};
         int perm[12];
         tridiag_qr<double, 12>(diag, sub, qapply, perm);
         // sorted eigenvector columns 0..3 (the four smallest eigenvalues) of the own rows
