@@ -27,11 +27,15 @@ $(LIBDIR)/sim3match.o: $(CSRC)/sim3match.hip $(HDRS)
 	mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(LIBDIR)/kfdb.o: $(CSRC)/kfdb.hip $(HDRS)
+	mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(LIBDIR)/rsc_api.o: $(CSRC)/rsc_api.cpp $(HDRS)
 	mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIBDIR)/librsc.so: $(LIBDIR)/kernels.o $(LIBDIR)/poseopt.o $(LIBDIR)/orbmatch.o $(LIBDIR)/sim3match.o $(LIBDIR)/rsc_api.o
+$(LIBDIR)/librsc.so: $(LIBDIR)/kernels.o $(LIBDIR)/poseopt.o $(LIBDIR)/orbmatch.o $(LIBDIR)/sim3match.o $(LIBDIR)/kfdb.o $(LIBDIR)/rsc_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 facade_test: $(LIBDIR)/facade_test

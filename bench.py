@@ -57,6 +57,7 @@ def parse():
     p.add_argument("--no-poseopt", action="store_true")
     p.add_argument("--no-bow", action="store_true")
     p.add_argument("--no-sim3match", action="store_true")
+    p.add_argument("--no-kfdb", action="store_true")
     return p.parse_args()
 
 
@@ -429,6 +430,77 @@ def cpu_baseline_sim3match(probs, seconds):
                        "restatement, 1 thread")
 
 
+def kfdb_scene(seed=82, n_kfs=2000, n_queries=64):
+    """a 2000-KeyFrame database (600-word BowVectors, a long EuRoC/KITTI map)
+    and 64 relocalization queries (Frame BowVectors observed along the trajectory)."""
+    from rsc import synth
+    rng = np.random.default_rng(seed)
+    sc = synth.make_kfdb_scene(rng, n_kfs, words_per_kf=600)
+    queries = [synth.make_kfdb_query(rng, sc, rng.uniform(0, n_kfs - 1)) for _ in range(n_queries)]
+    return sc, queries
+
+
+def run_kfdb(engine, ctx, sc, queries, args):
+    """KeyFrameDatabase::DetectRelocalizationCandidates (KeyFrameDatabase.cpp:174-283) over the
+    resident database: one rsc_kfdb_detect_relocalization per query (query upload, four kernels,
+    candidates back), fresh Frame ids every step so every query walks the full path."""
+    n = len(sc.bows)
+    db = engine.KeyFrameDatabase(ctx, n)
+    for k in range(n):
+        db.add(k, *sc.bows[k])
+        db.set_covisibility(k, sc.covis[k])
+    fid = [1]
+
+    def step():
+        nc = 0
+        for ids, vals in queries:
+            nc += len(db.detect_relocalization(fid[0], ids, vals))
+            fid[0] += 1
+        return nc
+    for _ in range(args.warmup):
+        step()
+    steps = max(1, args.steps)
+    t0 = time.perf_counter()
+    nc = 0
+    for _ in range(steps):
+        nc += step()
+    dt = time.perf_counter() - t0
+    ctx.enable_timing(True)
+    kms = 0.0
+    for ids, vals in queries:
+        db.detect_relocalization(fid[0], ids, vals)
+        fid[0] += 1
+        kms += ctx.last_timing()["refine_ms"]
+    ctx.enable_timing(False)
+    Q = len(queries)
+    words = sum(len(b[0]) for b in sc.bows)
+    return dict(queries_per_s=Q * steps / dt, ms_per_query=1e3 * dt / (Q * steps), kernel_ms_per_query=kms / Q,
+                keyframes=n, words_per_keyframe=words / n, mean_candidates=nc / (Q * steps),
+                count_kernel_bytes=4 * words, steps=steps)
+
+
+def cpu_baseline_kfdb(sc, queries, seconds):
+    """The KeyFrameDatabase oracle on ONE host core, same database and queries."""
+    import oracle_lib as ol
+    n = len(sc.bows)
+    db = ol.OracleKFDB(n)
+    for k in range(n):
+        db.add(k, *sc.bows[k])
+        db.set_covisibility(k, sc.covis[k])
+    prepared = [(np.ascontiguousarray(i, np.uint32), np.ascontiguousarray(v, np.float64)) for i, v in queries]
+    done, fid = 0, 1
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for ids, vals in prepared:
+            db.detect_relocalization(fid, ids, vals)
+            fid += 1
+        done += len(prepared)
+    dt = time.perf_counter() - t0
+    return dict(value=round(done / dt, 2), unit="queries/s", cores=1, kind="port",
+                sample=f"{done} DetectRelocalizationCandidates queries on a {n}-KeyFrame database in {dt:.1f} s, "
+                       "oracle restatement, 1 thread")
+
+
 def cpu_baseline_poseopt(frames, seconds):
     """The PoseOptimization oracle on ONE host core over the same frames."""
     import oracle_lib as ol
@@ -521,6 +593,10 @@ def main():
         r3 = np.random.default_rng(81)
         s3m_probs = [synth.make_sim3match_pair(r3, 1000, 250, 0.3) for _ in range(32)]
         s3m = run_sim3match(engine, ctx, s3m_probs, args)
+    kfdb = kfdb_sc = kfdb_q = None
+    if rank == 0 and not args.no_kfdb:
+        kfdb_sc, kfdb_q = kfdb_scene()
+        kfdb = run_kfdb(engine, ctx, kfdb_sc, kfdb_q, args)
     bow = bow_F = bow_K = None
     if rank == 0 and not args.no_bow:
         bow_F, bow_K = bow_views(np.random.default_rng(80))
@@ -605,6 +681,12 @@ def main():
             cb = cpu_baseline_sim3match(s3m_probs, min(2.0, args.cpu_seconds))
             out["search_by_sim3"]["cpu_baseline"] = cb
             out["search_by_sim3"]["speedup_vs_cpu_1core"] = round(s3m["pairs_per_s"] / cb["value"], 1)
+    if kfdb is not None:
+        out["kfdb_relocalization"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in kfdb.items()}
+        if not args.no_cpu and world == 1:
+            cb = cpu_baseline_kfdb(kfdb_sc, kfdb_q, min(2.0, args.cpu_seconds))
+            out["kfdb_relocalization"]["cpu_baseline"] = cb
+            out["kfdb_relocalization"]["speedup_vs_cpu_1core"] = round(kfdb["queries_per_s"] / cb["value"], 1)
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(scenes, args)
         out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 1)

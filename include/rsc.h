@@ -310,6 +310,41 @@ int rsc_search_by_sim3_many(rsc_context* ctx, rsc_kfview* const* kf1, rsc_kfview
                             const float* R12, const float* t12, float th, const int32_t* const* matched12,
                             int32_t* const* out12, int32_t* nfound);
 
+/* ---- KeyFrameDatabase: BoW candidate scoring (src/KeyFrameDatabase.cpp) ---------------------- */
+/* A device-resident keyframe database: each KeyFrame is a slot in [0, capacity) holding its
+ * BowVector (word ids ascending, TF-IDF values, DBoW2 L1_NORM scoring), its
+ * GetBestCovisibilityKeyFrames(10) list and the per-KeyFrame query state of the reference
+ * (mnLoopQuery/mnLoopWords/mLoopScore, mnRelocQuery/mnRelocWords/mRelocScore, KeyFrame.hpp:129-134),
+ * which persists across queries exactly as the KeyFrame members do.  Replaces
+ * KeyFrameDatabase (include/KeyFrameDatabase.hpp). */
+typedef struct rsc_kfdb rsc_kfdb;
+/* KeyFrameDatabase(voc) (KeyFrameDatabase.cpp:8-13): vocab_words = voc->size() (word ids are below
+ * it; 10^6 for ORBvoc.txt), capacity slots, max_words (<= 4096) bounds one BowVector. */
+int rsc_kfdb_create(rsc_context* ctx, uint32_t vocab_words, int capacity, int max_words, rsc_kfdb** out);
+void rsc_kfdb_destroy(rsc_kfdb* db);
+/* add(pKF) (:15-21): ids strictly ascending (a std::map BowVector) and below vocab_words; a slot
+ * already present ->
+ * RSC_ERR_UNSUPPORTED (the reference would list it twice per word). */
+int rsc_kfdb_add(rsc_kfdb* db, int kf, int n_words, const uint32_t* word_id, const double* word_value);
+/* erase(pKF) (:23-43); erasing an absent slot is a no-op as in the reference. */
+int rsc_kfdb_erase(rsc_kfdb* db, int kf);
+/* clear() (:45-49): empties the inverted file; the per-KeyFrame query state is kept. */
+int rsc_kfdb_clear(rsc_kfdb* db);
+/* pKF->GetBestCovisibilityKeyFrames(10) of slot kf (n <= 10 slots, in order). */
+int rsc_kfdb_set_covisibility(rsc_kfdb* db, int kf, int n, const int32_t* best);
+/* DetectRelocalizationCandidates(F) (:174-283): frame_id = F->mnId, (word_id, word_value) =
+ * F->mBowVec.  candidates (capacity entries): the returned vector's slots in order. */
+int rsc_kfdb_detect_relocalization(rsc_kfdb* db, uint64_t frame_id, int n_words, const uint32_t* word_id,
+                                   const double* word_value, int32_t* candidates, int32_t* n_candidates);
+/* DetectLoopCandidates(pKF, minScore) (:52-172): kf_id = pKF->mnId, connected =
+ * pKF->GetConnectedKeyFrames() (slots). */
+int rsc_kfdb_detect_loop(rsc_kfdb* db, uint64_t kf_id, int n_words, const uint32_t* word_id,
+                         const double* word_value, int n_connected, const int32_t* connected, float min_score,
+                         int32_t* candidates, int32_t* n_candidates);
+/* Per-slot query state (parity hook): q[2] = {mnLoopQuery, mnRelocQuery}, w[2] = {mnLoopWords,
+ * mnRelocWords}, s[2] = {mLoopScore, mRelocScore}. */
+int rsc_kfdb_state(rsc_kfdb* db, int kf, uint64_t* q, int32_t* w, float* s);
+
 /* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP refine launch, [job < 64][8]:
  * entry, compaction, control points, MtM, eigen, betas, check, exit. */
 int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out);

@@ -1,0 +1,256 @@
+// kfdb.hip — KeyFrameDatabase candidate queries (src/KeyFrameDatabase.cpp:52-283); see rsc_kfdb.h.
+#include <hip/hip_runtime.h>
+#include <climits>
+#include "rsc_kfdb.h"
+
+namespace rsc {
+
+namespace {
+
+constexpr int kBatch = 8;     // words per lane per batch of loads
+constexpr int kRankLds = 1024;  // scored slots ranked from LDS (beyond: from global memory)
+
+// The query's word -> position table (wpos[word] = index in F->mBowVec, -1 elsewhere): scattered
+// before the count kernel, cleared by the finish kernel, so a lookup is one gather.
+__global__ __launch_bounds__(256) void kfdb_scatter_kernel(DevKFDB db, KfdbQuery q) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < q.n) db.wpos[db.qids[i]] = i;
+}
+
+// The inverted-file walk (:60-78 loop, :181-196 reloc) seen from one slot: the walk meets slot k
+// once per common word, first at the query word `first`, in list order (ascending seq) within a
+// word.  One wave per slot; lane 0 applies the walk's per-occurrence state rules in closed form.
+__global__ __launch_bounds__(256) void kfdb_count_kernel(DevKFDB db, KfdbQuery q) {
+    const int lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (slot >= db.cap) return;
+    if (lane == 0) db.list[slot] = 0;  // in lKFsSharingWords (a flag per slot: no shared counter)
+    const int len = db.len[slot];
+    if (len == 0) return;  // not in any list: the walk never touches its state
+    const uint32_t* ids = db.ids + (size_t)slot * db.max_words;
+    int c = 0, first = INT_MAX;
+    // kBatch words per lane in flight: the id loads, then the dependent table gathers, are issued
+    // back to back (clamped, unconditional) instead of one load-gather round trip per word
+    for (int base = 0; base < len; base += 64 * kBatch) {
+        uint32_t w[kBatch];
+        int p[kBatch];
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) w[b] = ids[min(base + b * 64 + lane, len - 1)];
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) p[b] = db.wpos[w[b]];
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b)
+            if (base + b * 64 + lane < len && p[b] >= 0) {
+                c++;
+                first = min(first, p[b]);
+            }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        c += __shfl_xor(c, off);
+        first = min(first, __shfl_xor(first, off));
+    }
+    if (lane != 0 || c == 0) return;
+    const int t = q.loop ? 0 : 1;
+    unsigned long long qb = db.query[t][slot];
+    int w = db.words[t][slot];
+    bool in_list = false;
+    if (qb != q.id) {
+        if (q.loop && db.conn[slot]) {
+            w = 1;  // connected: mnLoopWords = 0 then ++ at every occurrence, query id untouched
+        } else {
+            w = c;  // reset at the first occurrence, then one increment per occurrence
+            qb = q.id;
+            in_list = true;
+        }
+    } else {
+        w += c;  // already met by an earlier query with the same id: counts accumulate, not listed
+    }
+    db.query[t][slot] = qb;
+    db.words[t][slot] = w;
+    if (in_list) {
+        db.list[slot] = 1;
+        db.key[slot] = ((unsigned long long)first << 32) | db.seq[slot];
+    }
+}
+
+template <typename T, typename Op>
+__device__ T block_reduce(T v, T* s_red, Op op) {
+    for (int off = 32; off > 0; off >>= 1) v = op(v, __shfl_xor(v, off));
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_red[wave] = v;
+    __syncthreads();
+    T r = s_red[0];
+    for (int i = 1; i < nw; ++i) r = op(r, s_red[i]);
+    return r;
+}
+
+// The rest of the query in one workgroup (16 waves), phases separated by barriers:
+//   select:     maxCommonWords / minCommonWords (:86-93, :201-207) and the scored slots in
+//               lKFsSharingWords order (rank by the walk's first meeting);
+//   score:      L1Scoring::score(F->mBowVec, pKFi->mBowVec) (ScoringObject.cpp:23-67), one wave per
+//               scored slot: per-word terms in parallel, the sum in ascending word order;
+//   accumulate: covisibility accumulation (:118-147, :233-259), retain (> 0.75 * best) and
+//               first-occurrence de-duplication (:150-168, :262-279);
+//   and the word-position table is cleared for the next query.
+__global__ __launch_bounds__(1024) void kfdb_finish_kernel(DevKFDB db, KfdbQuery q) {
+    __shared__ int s_red[16];
+    __shared__ float s_redf[16];
+    __shared__ int s_wcnt[16];
+    __shared__ int s_cnt;
+    __shared__ unsigned long long s_key[kRankLds];
+    const int t = q.loop ? 0 : 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    // ---- select ----
+    const int n = db.cap;
+    int mx = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        if (db.list[i]) mx = max(mx, db.words[t][i]);
+    const int maxc = block_reduce(mx, s_red, [](int a, int b) { return max(a, b); });
+    const int minc = (int)((float)maxc * 0.8f);  // int minCommonWords = maxCommonWords*0.8f
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        if (db.list[i] && db.words[t][i] > minc) db.tmp[atomicAdd(&s_cnt, 1)] = i;
+    __syncthreads();
+    const int S = s_cnt;
+    if (S <= kRankLds) {
+        for (int i = threadIdx.x; i < S; i += blockDim.x) s_key[i] = db.key[db.tmp[i]];
+        __syncthreads();
+        for (int i = threadIdx.x; i < S; i += blockDim.x) {
+            const unsigned long long k = s_key[i];
+            int r = 0;
+            for (int j = 0; j < S; ++j) r += s_key[j] < k;
+            db.scored[r] = db.tmp[i];
+        }
+    } else {
+        for (int i = threadIdx.x; i < S; i += blockDim.x) {
+            const int kf = db.tmp[i];
+            const unsigned long long k = db.key[kf];
+            int r = 0;
+            for (int j = 0; j < S; ++j) r += db.key[db.tmp[j]] < k;
+            db.scored[r] = kf;
+        }
+    }
+    __syncthreads();
+    // ---- score ----
+    for (int e = wave; e < S; e += nw) {
+        const int kf = db.scored[e];
+        const int len = db.len[kf];
+        const uint32_t* ids = db.ids + (size_t)kf * db.max_words;
+        const double* vals = db.vals + (size_t)kf * db.max_words;
+        double score = 0;
+        for (int base = 0; base < len; base += 64 * kBatch) {
+            uint32_t w[kBatch];
+            double wv[kBatch], vv[kBatch];
+            int p[kBatch];
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) {
+                const int j = min(base + b * 64 + lane, len - 1);
+                w[b] = ids[j];
+                wv[b] = vals[j];
+            }
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) p[b] = base + b * 64 + lane < len ? db.wpos[w[b]] : -1;
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) vv[b] = db.qvals[max(p[b], 0)];
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) {
+                const double vi = vv[b], wi = wv[b];
+                const double term = fabs(vi - wi) - fabs(vi) - fabs(wi);
+                const long long tb = __double_as_longlong(term);
+                const int lo = (int)(tb & 0xffffffff), hi = (int)(tb >> 32);
+                unsigned long long m = __ballot(p[b] >= 0);
+                while (m) {  // ascending word order: batch b, then lane (uniform lane index)
+                    const int src = __builtin_amdgcn_readfirstlane(__ffsll((long long)m) - 1);
+                    const unsigned long long v = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(hi, src) << 32) |
+                                                 (uint32_t)__builtin_amdgcn_readlane(lo, src);
+                    score += __longlong_as_double((long long)v);
+                    m &= m - 1;
+                }
+            }
+        }
+        score = -score / 2.0;
+        const float si = (float)score;  // float si = mpVoc->score(...)
+        if (lane == 0) {
+            db.sc[e] = si;
+            db.score[t][kf] = si;  // mLoopScore / mRelocScore
+        }
+    }
+    __syncthreads();
+    // ---- accumulate ----
+    float m = q.loop ? q.min_score : 0.0f;  // bestAccScore's initial value
+    for (int i = threadIdx.x; i < S; i += blockDim.x) {
+        const int kf = db.scored[i];
+        const float si = db.sc[i];
+        if (q.loop && !(si >= q.min_score)) {  // not in lScoreAndMatch
+            db.best[i] = -1;
+            continue;
+        }
+        float bestScore = si, accScore = si;
+        int bk = kf;
+        const int nn = db.covis_n[kf];
+        int k2[kKfdbCovis], w2[kKfdbCovis];
+        unsigned long long q2[kKfdbCovis];
+        float s2[kKfdbCovis];
+#pragma unroll
+        for (int k = 0; k < kKfdbCovis; ++k) k2[k] = db.covis[kf * kKfdbCovis + k];  // rows zero-padded
+#pragma unroll
+        for (int k = 0; k < kKfdbCovis; ++k) {
+            q2[k] = db.query[t][k2[k]];
+            w2[k] = db.words[t][k2[k]];
+            s2[k] = db.score[t][k2[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < kKfdbCovis; ++k) {
+            if (k >= nn || q2[k] != q.id) continue;
+            if (q.loop && !(w2[k] > minc)) continue;
+            accScore += s2[k];
+            if (s2[k] > bestScore) {
+                bk = k2[k];
+                bestScore = s2[k];
+            }
+        }
+        db.acc[i] = accScore;
+        db.best[i] = bk;
+        if (accScore > m) m = accScore;
+    }
+    const float bestAcc = block_reduce(m, s_redf, [](float a, float b) { return a > b ? a : b; });
+    const float minRetain = 0.75f * bestAcc;
+    __syncthreads();
+    int total = 0;
+    for (int base = 0; base < S; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        bool keep = false;
+        if (i < S && db.best[i] >= 0 && db.acc[i] > minRetain) {
+            keep = true;
+            const int b = db.best[i];
+            for (int j = 0; j < i && keep; ++j)
+                if (db.best[j] == b && db.acc[j] > minRetain) keep = false;  // already added
+        }
+        const unsigned long long bal = __ballot(keep);
+        const int before = __popcll(bal & ((1ull << lane) - 1ull));
+        __syncthreads();
+        if (lane == 0) s_wcnt[wave] = __popcll(bal);
+        __syncthreads();
+        int off = total;
+        for (int w = 0; w < wave; ++w) off += s_wcnt[w];
+        if (keep) db.out[1 + off + before] = db.best[i];
+        for (int w = 0; w < nw; ++w) total += s_wcnt[w];
+    }
+    if (threadIdx.x == 0) db.out[0] = total;
+    // ---- clear the word-position table ----
+    for (int i = threadIdx.x; i < q.n; i += blockDim.x) db.wpos[db.qids[i]] = -1;
+}
+
+}  // namespace
+
+hipError_t launch_kfdb_query(const DevKFDB& db, const KfdbQuery& q, hipStream_t st) {
+    if (q.n < 0 || q.n > kKfdbMaxWords || db.cap <= 0) return hipErrorInvalidValue;
+    if (q.n > 0) kfdb_scatter_kernel<<<(q.n + 255) / 256, 256, 0, st>>>(db, q);
+    kfdb_count_kernel<<<(db.cap + 3) / 4, 256, 0, st>>>(db, q);
+    kfdb_finish_kernel<<<1, 1024, 0, st>>>(db, q);
+    return hipGetLastError();
+}
+
+}  // namespace rsc

@@ -20,6 +20,7 @@
 #include "rsc_poseopt.h"
 #include "rsc_orbmatch.h"
 #include "rsc_sim3match.h"
+#include "rsc_kfdb.h"
 
 using namespace rsc;
 
@@ -1569,6 +1570,237 @@ int rsc_search_by_sim3_many(rsc_context* C, rsc_kfview* const* kf1, rsc_kfview* 
     for (int c = 0; c < count; ++c) {
         if (kf1[c]->n) std::memcpy(out12[c], h + o_out[c], 4 * (size_t)kf1[c]->n);
         if (nfound) std::memcpy(&nfound[c], h + o_nf[c], 4);
+    }
+    return RSC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// KeyFrameDatabase (rsc_kfdb.h)
+// ------------------------------------------------------------------------------------------------
+struct rsc_kfdb {
+    rsc_context* ctx = nullptr;
+    int cap = 0, max_words = 0;
+    uint32_t vocab = 0;
+    uint32_t next_seq = 1;
+    std::vector<uint8_t> present;
+    DevBuf<uint32_t> ids, seq;
+    DevBuf<double> vals;
+    DevBuf<char> qbuf;  // the query BowVector: ids | vals (8-aligned), one upload per query
+    DevBuf<int32_t> wpos, len, covis, covis_n, words, list, scored, best, tmp, counters, out;
+    DevBuf<unsigned long long> query, key;
+    DevBuf<float> score, sc, acc;
+    DevBuf<uint8_t> conn;
+    PinBuf<char> stage;  // query upload | candidates download
+    DevKFDB dev() const {
+        DevKFDB d;
+        d.cap = cap;
+        d.max_words = max_words;
+        d.vocab = vocab;
+        d.wpos = wpos.p;
+        d.ids = ids.p;
+        d.vals = vals.p;
+        d.len = len.p;
+        d.seq = seq.p;
+        d.covis = covis.p;
+        d.covis_n = covis_n.p;
+        for (int t = 0; t < 2; ++t) {
+            d.query[t] = query.p + (size_t)t * cap;
+            d.words[t] = words.p + (size_t)t * cap;
+            d.score[t] = score.p + (size_t)t * cap;
+        }
+        d.list = list.p;
+        d.key = key.p;
+        d.scored = scored.p;
+        d.sc = sc.p;
+        d.acc = acc.p;
+        d.best = best.p;
+        d.tmp = tmp.p;
+        d.counters = counters.p;
+        d.out = out.p;
+        d.qids = reinterpret_cast<const uint32_t*>(qbuf.p);
+        d.qvals = reinterpret_cast<const double*>(qbuf.p);  // set per query (after the ids)
+        d.conn = conn.p;
+        return d;
+    }
+};
+
+namespace {
+int check_bow_vector(const rsc_kfdb* db, int n, const uint32_t* id, const double* val) {
+    if (n < 0 || n > db->max_words || (n && (!id || !val))) return RSC_ERR_ARG;
+    for (int i = 1; i < n; ++i)
+        if (id[i] <= id[i - 1]) return RSC_ERR_ARG;  // a BowVector (std::map) is strictly ascending
+    if (n && id[n - 1] >= db->vocab) return RSC_ERR_ARG;  // not a word of the vocabulary
+    return RSC_OK;
+}
+}  // namespace
+
+int rsc_kfdb_create(rsc_context* C, uint32_t vocab_words, int capacity, int max_words, rsc_kfdb** out) {
+    if (!C || !out || vocab_words == 0 || vocab_words > (1u << 30) || capacity <= 0 || max_words <= 0 ||
+        max_words > kKfdbMaxWords)
+        return RSC_ERR_ARG;
+    *out = nullptr;
+    std::unique_ptr<rsc_kfdb> db(new rsc_kfdb);
+    db->ctx = C;
+    db->cap = capacity;
+    db->max_words = max_words;
+    db->vocab = vocab_words;
+    db->present.assign(capacity, 0);
+    RSC_HIP(hipSetDevice(C->device));
+    const size_t K = (size_t)capacity;
+    int e = 0;
+    if ((e = db->wpos.ensure(vocab_words)) || (e = db->ids.ensure(K * max_words)) || (e = db->vals.ensure(K * max_words)) || (e = db->len.ensure(K)) ||
+        (e = db->seq.ensure(K)) || (e = db->covis.ensure(K * kKfdbCovis)) || (e = db->covis_n.ensure(K)) ||
+        (e = db->query.ensure(2 * K)) || (e = db->words.ensure(2 * K)) || (e = db->score.ensure(2 * K)) ||
+        (e = db->list.ensure(K)) || (e = db->key.ensure(K)) || (e = db->scored.ensure(K)) || (e = db->sc.ensure(K)) ||
+        (e = db->acc.ensure(K)) || (e = db->best.ensure(K)) || (e = db->tmp.ensure(K)) || (e = db->counters.ensure(4)) ||
+        (e = db->out.ensure(K + 1)) || (e = db->qbuf.ensure(16 * (size_t)max_words + 16)) ||
+        (e = db->conn.ensure(K)))
+        return e;
+    const size_t stage = std::max((size_t)max_words * 16 + 16 + K, (K + 1) * 4);
+    if ((e = db->stage.ensure(stage))) return e;
+    // KeyFrame.cpp:15: query ids and word counts start at 0; the scores (uninitialised in the
+    // reference) are defined as 0
+    RSC_HIP(hipMemsetAsync(db->wpos.p, 0xFF, 4 * (size_t)vocab_words, C->stream));  // -1: no query word
+    RSC_HIP(hipMemsetAsync(db->counters.p, 0, 16, C->stream));  // the finish kernel re-zeroes n_list
+    RSC_HIP(hipMemsetAsync(db->len.p, 0, 4 * K, C->stream));
+    RSC_HIP(hipMemsetAsync(db->covis_n.p, 0, 4 * K, C->stream));
+    RSC_HIP(hipMemsetAsync(db->covis.p, 0, 4 * K * kKfdbCovis, C->stream));  // padded rows read slot 0
+    RSC_HIP(hipMemsetAsync(db->query.p, 0, 16 * K, C->stream));
+    RSC_HIP(hipMemsetAsync(db->words.p, 0, 8 * K, C->stream));
+    RSC_HIP(hipMemsetAsync(db->score.p, 0, 8 * K, C->stream));
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    *out = db.release();
+    return RSC_OK;
+}
+
+void rsc_kfdb_destroy(rsc_kfdb* db) {
+    if (!db) return;
+    (void)hipStreamSynchronize(db->ctx->stream);
+    delete db;
+}
+
+int rsc_kfdb_add(rsc_kfdb* db, int kf, int n, const uint32_t* id, const double* val) {
+    if (!db || kf < 0 || kf >= db->cap) return RSC_ERR_ARG;
+    if (int e = check_bow_vector(db, n, id, val)) return e;
+    if (db->present[kf]) return RSC_ERR_UNSUPPORTED;
+    rsc_context* C = db->ctx;
+    RSC_HIP(hipSetDevice(C->device));
+    const size_t o = (size_t)kf * db->max_words;
+    const uint32_t s = db->next_seq++;
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    if (n) {
+        RSC_HIP(hipMemcpy(db->ids.p + o, id, 4 * (size_t)n, hipMemcpyHostToDevice));
+        RSC_HIP(hipMemcpy(db->vals.p + o, val, 8 * (size_t)n, hipMemcpyHostToDevice));
+    }
+    RSC_HIP(hipMemcpy(db->seq.p + kf, &s, 4, hipMemcpyHostToDevice));
+    RSC_HIP(hipMemcpy(db->len.p + kf, &n, 4, hipMemcpyHostToDevice));
+    db->present[kf] = 1;
+    return RSC_OK;
+}
+
+int rsc_kfdb_erase(rsc_kfdb* db, int kf) {
+    if (!db || kf < 0 || kf >= db->cap) return RSC_ERR_ARG;
+    if (!db->present[kf]) return RSC_OK;
+    RSC_HIP(hipSetDevice(db->ctx->device));
+    RSC_HIP(hipMemsetAsync(db->len.p + kf, 0, 4, db->ctx->stream));
+    RSC_HIP(hipStreamSynchronize(db->ctx->stream));
+    db->present[kf] = 0;
+    return RSC_OK;
+}
+
+int rsc_kfdb_clear(rsc_kfdb* db) {
+    if (!db) return RSC_ERR_ARG;
+    RSC_HIP(hipSetDevice(db->ctx->device));
+    RSC_HIP(hipMemsetAsync(db->len.p, 0, 4 * (size_t)db->cap, db->ctx->stream));
+    RSC_HIP(hipStreamSynchronize(db->ctx->stream));
+    std::fill(db->present.begin(), db->present.end(), 0);
+    return RSC_OK;
+}
+
+int rsc_kfdb_set_covisibility(rsc_kfdb* db, int kf, int n, const int32_t* best) {
+    if (!db || kf < 0 || kf >= db->cap || n < 0 || n > kKfdbCovis || (n && !best)) return RSC_ERR_ARG;
+    int32_t row[kKfdbCovis] = {};
+    for (int i = 0; i < n; ++i) {
+        if (best[i] < 0 || best[i] >= db->cap) return RSC_ERR_ARG;
+        row[i] = best[i];
+    }
+    RSC_HIP(hipSetDevice(db->ctx->device));
+    RSC_HIP(hipStreamSynchronize(db->ctx->stream));
+    RSC_HIP(hipMemcpy(db->covis.p + (size_t)kf * kKfdbCovis, row, sizeof(row), hipMemcpyHostToDevice));
+    RSC_HIP(hipMemcpy(db->covis_n.p + kf, &n, 4, hipMemcpyHostToDevice));
+    return RSC_OK;
+}
+
+namespace {
+int kfdb_query(rsc_kfdb* db, uint64_t qid, int n, const uint32_t* id, const double* val, int loop, int n_conn,
+               const int32_t* conn, float min_score, int32_t* cand, int32_t* n_cand) {
+    if (!db || !cand || !n_cand) return RSC_ERR_ARG;
+    if (int e = check_bow_vector(db, n, id, val)) return e;
+    if (loop && (n_conn < 0 || (n_conn && !conn))) return RSC_ERR_ARG;
+    rsc_context* C = db->ctx;
+    const size_t K = (size_t)db->cap;
+    RSC_HIP(hipSetDevice(C->device));
+    RSC_HIP(hipStreamSynchronize(C->stream));  // the staging buffer is free again
+    char* h = db->stage.p;
+    const size_t vo = (4 * (size_t)n + 7) & ~(size_t)7;  // vals offset in the packed query
+    if (n) {
+        std::memcpy(h, id, 4 * (size_t)n);
+        std::memcpy(h + vo, val, 8 * (size_t)n);
+        RSC_HIP(hipMemcpyAsync(db->qbuf.p, h, vo + 8 * (size_t)n, hipMemcpyHostToDevice, C->stream));
+    }
+    if (loop) {
+        uint8_t* m = reinterpret_cast<uint8_t*>(h + 16 * (size_t)db->max_words + 16);
+        std::memset(m, 0, K);
+        for (int i = 0; i < n_conn; ++i) {
+            if (conn[i] < 0 || conn[i] >= db->cap) return RSC_ERR_ARG;
+            m[conn[i]] = 1;
+        }
+        RSC_HIP(hipMemcpyAsync(db->conn.p, m, K, hipMemcpyHostToDevice, C->stream));
+    }
+    KfdbQuery q;
+    q.id = (unsigned long long)qid;
+    q.n = n;
+    q.loop = loop;
+    q.min_score = min_score;
+    timing_begin(C, 3);
+    DevKFDB d = db->dev();
+    d.qvals = reinterpret_cast<const double*>(db->qbuf.p + vo);
+    RSC_HIP(launch_kfdb_query(d, q, C->stream));
+    timing_begin(C, 4);
+    RSC_HIP(hipMemcpyAsync(h, db->out.p, 4 * (K + 1), hipMemcpyDeviceToHost, C->stream));
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    if (C->timing) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, C->ev[3], C->ev[4]);
+        C->last_ms[2] = ms;
+    }
+    const int32_t* o = reinterpret_cast<const int32_t*>(h);
+    *n_cand = o[0];
+    std::memcpy(cand, o + 1, 4 * (size_t)o[0]);
+    return RSC_OK;
+}
+}  // namespace
+
+int rsc_kfdb_detect_relocalization(rsc_kfdb* db, uint64_t frame_id, int n, const uint32_t* id, const double* val,
+                                   int32_t* cand, int32_t* n_cand) {
+    return kfdb_query(db, frame_id, n, id, val, 0, 0, nullptr, 0.0f, cand, n_cand);
+}
+
+int rsc_kfdb_detect_loop(rsc_kfdb* db, uint64_t kf_id, int n, const uint32_t* id, const double* val, int n_conn,
+                         const int32_t* conn, float min_score, int32_t* cand, int32_t* n_cand) {
+    return kfdb_query(db, kf_id, n, id, val, 1, n_conn, conn, min_score, cand, n_cand);
+}
+
+int rsc_kfdb_state(rsc_kfdb* db, int kf, uint64_t* q, int32_t* w, float* s) {
+    if (!db || kf < 0 || kf >= db->cap || !q || !w || !s) return RSC_ERR_ARG;
+    RSC_HIP(hipSetDevice(db->ctx->device));
+    RSC_HIP(hipStreamSynchronize(db->ctx->stream));
+    for (int t = 0; t < 2; ++t) {
+        unsigned long long qq = 0;
+        RSC_HIP(hipMemcpy(&qq, db->query.p + (size_t)t * db->cap + kf, 8, hipMemcpyDeviceToHost));
+        q[t] = qq;
+        RSC_HIP(hipMemcpy(&w[t], db->words.p + (size_t)t * db->cap + kf, 4, hipMemcpyDeviceToHost));
+        RSC_HIP(hipMemcpy(&s[t], db->score.p + (size_t)t * db->cap + kf, 4, hipMemcpyDeviceToHost));
     }
     return RSC_OK;
 }

@@ -41,6 +41,8 @@ EXPORTED = [
     "rsc_bow_create", "rsc_bow_destroy", "rsc_bow_set_valid", "rsc_search_by_bow_frame_many",
     "rsc_search_by_bow_kf_many", "rsc_diag_bow_phase_stamps", "rsc_diag_refine_phase_stamps",
     "rsc_search_by_sim3_many", "rsc_kfview_create", "rsc_kfview_destroy",
+    "rsc_kfdb_create", "rsc_kfdb_destroy", "rsc_kfdb_add", "rsc_kfdb_erase", "rsc_kfdb_clear",
+    "rsc_kfdb_set_covisibility", "rsc_kfdb_detect_relocalization", "rsc_kfdb_detect_loop", "rsc_kfdb_state",
 ]
 
 
@@ -174,6 +176,71 @@ def search_by_sim3_many(ctx: Context, problems, th: float = 7.5):
     return Sim3Search(ctx, problems, th).run()
 
 
+class KeyFrameDatabase:
+    """Device-resident KeyFrameDatabase (src/KeyFrameDatabase.cpp, rsc_kfdb_*): KeyFrames are slots
+    in [0, capacity); each BowVector is (word ids ascending uint32, values float64).  The per-
+    KeyFrame query state (mnLoopQuery/Words/Score, mnRelocQuery/Words/Score) persists across
+    queries as in the reference."""
+
+    def __init__(self, ctx: Context, capacity: int, max_words: int = 4096, vocab_words: int = 10 ** 6):
+        self.ctx, self.capacity = ctx, int(capacity)
+        h = C.c_void_p()
+        _check(load_library().rsc_kfdb_create(ctx.h, int(vocab_words), self.capacity, int(max_words), C.byref(h)),
+               "rsc_kfdb_create")
+        self.h = h
+        self._cand = np.zeros(max(self.capacity, 1), np.int32)
+        self._n = np.zeros(1, np.int32)
+
+    @staticmethod
+    def _bow(ids, vals):
+        return np.ascontiguousarray(ids, np.uint32), np.ascontiguousarray(vals, np.float64)
+
+    def add(self, kf: int, ids, vals):
+        i, v = self._bow(ids, vals)
+        _check(load_library().rsc_kfdb_add(self.h, int(kf), len(i), i, v), "rsc_kfdb_add")
+
+    def erase(self, kf: int):
+        _check(load_library().rsc_kfdb_erase(self.h, int(kf)), "rsc_kfdb_erase")
+
+    def clear(self):
+        _check(load_library().rsc_kfdb_clear(self.h), "rsc_kfdb_clear")
+
+    def set_covisibility(self, kf: int, best):
+        b = np.ascontiguousarray(best, np.int32)
+        _check(load_library().rsc_kfdb_set_covisibility(self.h, int(kf), len(b), b), "rsc_kfdb_set_covisibility")
+
+    def detect_relocalization(self, frame_id: int, ids, vals) -> np.ndarray:
+        """DetectRelocalizationCandidates(F) (:174-283): candidate slots in the reference's order."""
+        i, v = self._bow(ids, vals)
+        _check(load_library().rsc_kfdb_detect_relocalization(self.h, int(frame_id), len(i), i, v, self._cand,
+                                                              self._n), "rsc_kfdb_detect_relocalization")
+        return self._cand[:self._n[0]].copy()
+
+    def detect_loop(self, kf_id: int, ids, vals, connected, min_score: float) -> np.ndarray:
+        """DetectLoopCandidates(pKF, minScore) (:52-172)."""
+        i, v = self._bow(ids, vals)
+        c = np.ascontiguousarray(connected, np.int32)
+        _check(load_library().rsc_kfdb_detect_loop(self.h, int(kf_id), len(i), i, v, len(c), c, float(min_score),
+                                                   self._cand, self._n), "rsc_kfdb_detect_loop")
+        return self._cand[:self._n[0]].copy()
+
+    def state(self, kf: int):
+        """((mnLoopQuery, mnRelocQuery), (mnLoopWords, mnRelocWords), (mLoopScore, mRelocScore))"""
+        q = np.zeros(2, np.uint64)
+        w = np.zeros(2, np.int32)
+        s = np.zeros(2, np.float32)
+        _check(load_library().rsc_kfdb_state(self.h, int(kf), q, w, s), "rsc_kfdb_state")
+        return tuple(int(x) for x in q), tuple(int(x) for x in w), tuple(float(x) for x in s)
+
+    def close(self):
+        if getattr(self, "h", None):
+            load_library().rsc_kfdb_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
 class PoseOptResult(C.Structure):
     _fields_ = [("n_good", C.c_int32), ("n_initial", C.c_int32), ("rounds", C.c_int32),
                 ("lm_iterations", C.c_int32), ("lm_trials", C.c_int32), ("Tcw", C.c_float * 16)]
@@ -256,6 +323,18 @@ def load_library(path: str = LIB_PATH):
     L.rsc_kfview_destroy.argtypes = [vp]
     L.rsc_search_by_sim3_many.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.c_int, f32p_, f32p_, C.c_float,
                                           C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), i32p]
+    u32p_ = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+    f64p_ = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+    u64p_ = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+    L.rsc_kfdb_create.argtypes = [vp, C.c_uint32, C.c_int, C.c_int, C.POINTER(vp)]
+    L.rsc_kfdb_destroy.argtypes = [vp]
+    L.rsc_kfdb_add.argtypes = [vp, C.c_int, C.c_int, u32p_, f64p_]
+    L.rsc_kfdb_erase.argtypes = [vp, C.c_int]
+    L.rsc_kfdb_clear.argtypes = [vp]
+    L.rsc_kfdb_set_covisibility.argtypes = [vp, C.c_int, C.c_int, i32p]
+    L.rsc_kfdb_detect_relocalization.argtypes = [vp, C.c_uint64, C.c_int, u32p_, f64p_, i32p, i32p]
+    L.rsc_kfdb_detect_loop.argtypes = [vp, C.c_uint64, C.c_int, u32p_, f64p_, C.c_int, i32p, C.c_float, i32p, i32p]
+    L.rsc_kfdb_state.argtypes = [vp, C.c_int, u64p_, i32p, f32p_]
     L.rsc_loop_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(Sim3Result), C.POINTER(EventResult)]
     L.rsc_diag_pnp_phase_stamps.argtypes = [C.POINTER(vp), C.c_int, C.c_int,
                                             np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]

@@ -416,3 +416,56 @@ def make_sim3match_pair(rng: np.random.Generator, n_points: int = 1000, n_extra:
         if mid >= 0 and rng.random() < matched_frac:
             matched12[i] = where2.get(int(mid), -2)
     return kf1, kf2, R12, t12, matched12
+
+
+# ---- KeyFrameDatabase scenes (KeyFrameDatabase.cpp) ---------------------------------------------
+VOCAB_WORDS = 10 ** 6  # ORBvoc.txt: k = 10, L = 6 -> up to 10^6 leaves
+
+
+@dataclasses.dataclass
+class KFDBScene:
+    """KeyFrames along a trajectory: bows[k] = (word ids ascending uint32, L1-normalised float64
+    TF-IDF values), covis[k] = GetBestCovisibilityKeyFrames(10) (nearest along the trajectory);
+    the place-word pools make neighbouring KeyFrames share words and a small set of frequent words
+    makes most KeyFrames share a few (the inverted file's long lists)."""
+    bows: list
+    covis: list
+    pools: np.ndarray
+    frequent: np.ndarray
+    step: int
+    span: int
+
+
+def _bow_from(rng: np.random.Generator, words: np.ndarray):
+    ids = np.unique(words.astype(np.uint32))
+    vals = rng.exponential(1.0, len(ids)) * rng.uniform(0.5, 3.0, len(ids))  # tf * idf
+    s = vals.sum()
+    return ids, (vals / s if s > 0 else vals).astype(np.float64)
+
+
+def _place_words(rng, sc: KFDBScene, pos: float, n_words: int, noise_frac: float = 0.1):
+    c = int(round(pos * sc.step))
+    lo = max(0, min(len(sc.pools) - sc.span, c))
+    own = rng.choice(sc.pools[lo:lo + sc.span], size=int(n_words * (1 - noise_frac)), replace=False)
+    noise = rng.integers(0, VOCAB_WORDS, int(n_words * noise_frac))
+    freq = sc.frequent[rng.random(len(sc.frequent)) < 0.3]
+    return np.concatenate([own, noise, freq])
+
+
+def make_kfdb_scene(rng: np.random.Generator, n_kfs: int, words_per_kf: int = 600, step: int = 150,
+                    n_frequent: int = 40) -> KFDBScene:
+    span = 2 * words_per_kf
+    pools = rng.permutation(VOCAB_WORDS)[: n_kfs * step + span].astype(np.uint32)
+    frequent = rng.integers(0, VOCAB_WORDS, n_frequent).astype(np.uint32)
+    sc = KFDBScene([], [], pools, frequent, step, span)
+    for k in range(n_kfs):
+        sc.bows.append(_bow_from(rng, _place_words(rng, sc, k, words_per_kf)))
+    for k in range(n_kfs):
+        near = sorted((j for j in range(max(0, k - 8), min(n_kfs, k + 9)) if j != k), key=lambda j: (abs(j - k), j))
+        sc.covis.append(np.array(near[:10], np.int32))
+    return sc
+
+
+def make_kfdb_query(rng: np.random.Generator, sc: KFDBScene, pos: float, words: int = 600):
+    """A Frame's (or new KeyFrame's) BowVector observed at trajectory position pos."""
+    return _bow_from(rng, _place_words(rng, sc, pos, words))

@@ -166,7 +166,28 @@ def sim3match():
     np.savez_compressed(os.path.join(HERE, "sim3match_traces.npz"), **out)
 
 
+def kfdb():
+    import oracle_lib as ol
+    import kfdb_script as ks
+    out = {}
+    cases = [(11, 60, 40, 300), (12, 30, 25, 150)]
+    for c, (seed, n_kfs, nq, words) in enumerate(cases):
+        ops = ks.make_script(seed, n_kfs=n_kfs, n_queries=nq, words=words)
+        res = ks.run_script(ol.OracleKFDB(n_kfs), ops)
+        ks.save_script(f"c{c}", ops, out)
+        out[f"c{c}_cap"] = np.int32(n_kfs)
+        out[f"c{c}_nr"] = np.int32(len(res))
+        for i, r in enumerate(res):
+            out[f"c{c}_r{i}"] = r
+        print(f"c{c}: {len(res)} queries, candidates per query", [len(r) for r in res])
+    out["cases"] = np.int32(len(cases))
+    np.savez_compressed(os.path.join(HERE, "kfdb_traces.npz"), **out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "kfdb":
+        kfdb()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "sim3match":
         sim3match()
         sys.exit(0)

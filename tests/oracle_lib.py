@@ -117,6 +117,21 @@ def lib():
     L.ora_descriptor_distance.argtypes = [u8p, u8p]
     L.ora_search_by_sim3.argtypes = [vp, vp, i32p, f32p, f32p, C.c_float, i32p]
     L.ora_predict_scale.argtypes = [C.c_float, C.c_float, C.c_float, C.c_int]
+    u32p_ = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+    f64p_ = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+    u64p_ = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+    L.ora_kfdb_create.restype = vp
+    L.ora_kfdb_create.argtypes = [C.c_int]
+    L.ora_kfdb_destroy.argtypes = [vp]
+    L.ora_kfdb_add.argtypes = [vp, C.c_int, C.c_int, u32p_, f64p_]
+    L.ora_kfdb_erase.argtypes = [vp, C.c_int]
+    L.ora_kfdb_clear.argtypes = [vp]
+    L.ora_kfdb_set_covisibility.argtypes = [vp, C.c_int, C.c_int, i32p]
+    L.ora_kfdb_detect_relocalization.argtypes = [vp, C.c_uint64, C.c_int, u32p_, f64p_, i32p]
+    L.ora_kfdb_detect_loop.argtypes = [vp, C.c_uint64, C.c_int, u32p_, f64p_, C.c_int, i32p, C.c_float, i32p]
+    L.ora_kfdb_state.argtypes = [vp, C.c_int, u64p_, i32p, f32p]
+    L.ora_l1_score.restype = C.c_double
+    L.ora_l1_score.argtypes = [C.c_int, u32p_, f64p_, C.c_int, u32p_, f64p_]
     L.ora_dm_log.restype = C.c_double
     L.ora_dm_log.argtypes = [C.c_double]
     L.ora_compute_three_maxima.argtypes = [i32p, C.c_int, i32p]
@@ -424,3 +439,60 @@ def search_by_sim3(kf1, kf2, R12, t12, matched12, th=7.5):
                                   np.ascontiguousarray(np.asarray(R12, np.float32).reshape(9)),
                                   np.ascontiguousarray(np.asarray(t12, np.float32).reshape(3)), th, out)
     return nf, out[:kf1.n]
+
+
+class OracleKFDB:
+    """KeyFrameDatabase on the oracle (oracle/kfdb_oracle.h); same interface as
+    rsc.engine.KeyFrameDatabase."""
+
+    def __init__(self, capacity: int):
+        self.capacity = int(capacity)
+        self.h = lib().ora_kfdb_create(self.capacity)
+        self._cand = np.zeros(max(self.capacity, 1), np.int32)
+
+    @staticmethod
+    def _bow(ids, vals):
+        return np.ascontiguousarray(ids, np.uint32), np.ascontiguousarray(vals, np.float64)
+
+    def add(self, kf, ids, vals):
+        i, v = self._bow(ids, vals)
+        lib().ora_kfdb_add(self.h, int(kf), len(i), i, v)
+
+    def erase(self, kf):
+        lib().ora_kfdb_erase(self.h, int(kf))
+
+    def clear(self):
+        lib().ora_kfdb_clear(self.h)
+
+    def set_covisibility(self, kf, best):
+        b = np.ascontiguousarray(best, np.int32)
+        lib().ora_kfdb_set_covisibility(self.h, int(kf), len(b), b)
+
+    def detect_relocalization(self, frame_id, ids, vals):
+        i, v = self._bow(ids, vals)
+        n = lib().ora_kfdb_detect_relocalization(self.h, int(frame_id), len(i), i, v, self._cand)
+        return self._cand[:n].copy()
+
+    def detect_loop(self, kf_id, ids, vals, connected, min_score):
+        i, v = self._bow(ids, vals)
+        c = np.ascontiguousarray(connected, np.int32)
+        n = lib().ora_kfdb_detect_loop(self.h, int(kf_id), len(i), i, v, len(c), c, float(min_score), self._cand)
+        return self._cand[:n].copy()
+
+    def state(self, kf):
+        q = np.zeros(2, np.uint64)
+        w = np.zeros(2, np.int32)
+        s = np.zeros(2, np.float32)
+        lib().ora_kfdb_state(self.h, int(kf), q, w, s)
+        return tuple(int(x) for x in q), tuple(int(x) for x in w), tuple(float(x) for x in s)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ora_kfdb_destroy(self.h)
+            self.h = None
+
+
+def l1_score(ids1, v1, ids2, v2) -> float:
+    a, b = np.ascontiguousarray(ids1, np.uint32), np.ascontiguousarray(ids2, np.uint32)
+    return lib().ora_l1_score(len(a), a, np.ascontiguousarray(v1, np.float64), len(b), b,
+                              np.ascontiguousarray(v2, np.float64))

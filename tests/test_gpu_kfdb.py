@@ -1,0 +1,112 @@
+"""GPU parity of the KeyFrameDatabase candidate queries (KeyFrameDatabase.cpp:52-283) through the
+C ABI (rsc_kfdb_*) against the oracle: candidate lists bit-exact (same slots, same order) and every
+slot's persistent query state (mnLoopQuery/Words/Score, mnRelocQuery/Words/Score) identical after
+each script — on the golden fixture, on random operation scripts, on the hand-built known answers
+of test_cpu_kfdb.py, and on a bench-sized database; plus the ABI's error behaviour."""
+import os
+
+import numpy as np
+import pytest
+
+import kfdb_script as ks
+import oracle_lib as ol
+import test_cpu_kfdb as tk
+from gpu_common import ctx
+from rsc import engine, synth
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def gpu_db(cap, max_words=4096):
+    return engine.KeyFrameDatabase(ctx(), cap, max_words)
+
+
+def states(db, n):
+    return [db.state(k) for k in range(n)]
+
+
+def compare_script(ops, cap):
+    g, o = gpu_db(cap), ol.OracleKFDB(cap)
+    a, b = ks.run_script(g, ops), ks.run_script(o, ops)
+    assert len(a) == len(b)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert list(x) == list(y), i
+    assert states(g, cap) == states(o, cap)
+    return a
+
+
+def test_golden_fixture():
+    z = np.load(os.path.join(ROOT, "tests", "golden", "kfdb_traces.npz"))
+    for c in range(int(z["cases"])):
+        ops = ks.load_script(f"c{c}", z)
+        got = compare_script(ops, int(z[f"c{c}_cap"]))
+        want = [z[f"c{c}_r{i}"] for i in range(int(z[f"c{c}_nr"]))]
+        for g, w in zip(got, want):
+            assert list(g) == list(w)
+
+
+@pytest.mark.parametrize("seed", [4, 5, 6, 7])
+def test_random_scripts(seed):
+    compare_script(ks.make_script(seed, n_kfs=80, n_queries=40, words=400), 96)
+
+
+class GpuTiny:
+    """test_cpu_kfdb's hand-built cases on the device database."""
+
+    def __new__(cls, cap):
+        return gpu_db(cap)
+
+
+@pytest.mark.parametrize("case", ["test_relocalization_known_answers", "test_relocalization_stale_score",
+                                  "test_loop_known_answers", "test_empty_database_and_no_common_words",
+                                  "test_erase_and_order"])
+def test_known_answers(case, monkeypatch):
+    # the CPU known-answer tests iterate over (PyKFDB, OracleKFDB); run them with the device class
+    monkeypatch.setattr(tk.ol, "OracleKFDB", GpuTiny)
+    monkeypatch.setattr(tk, "PyKFDB", GpuTiny)
+    getattr(tk, case)()
+
+
+def test_bench_sized_database():
+    rng = np.random.default_rng(21)
+    n = 2000
+    sc = synth.make_kfdb_scene(rng, n, words_per_kf=600)
+    g, o = gpu_db(n), ol.OracleKFDB(n)
+    for k in range(n):
+        for db in (g, o):
+            db.add(k, *sc.bows[k])
+            db.set_covisibility(k, sc.covis[k])
+    for f in range(1, 25):
+        ids, vals = synth.make_kfdb_query(rng, sc, rng.uniform(0, n - 1))
+        if f % 3:
+            a, b = g.detect_relocalization(f, ids, vals), o.detect_relocalization(f, ids, vals)
+        else:
+            near = int(rng.integers(0, n))
+            conn = sc.covis[near]
+            a, b = g.detect_loop(5000 + f, ids, vals, conn, 0.01), o.detect_loop(5000 + f, ids, vals, conn, 0.01)
+        assert list(a) == list(b), f
+    assert states(g, n) == states(o, n)
+
+
+def test_abi_errors():
+    db = gpu_db(8, max_words=16)
+    ids, vals = np.array([1, 5, 9], np.uint32), np.array([0.2, 0.3, 0.5])
+    db.add(0, ids, vals)
+    with pytest.raises(RuntimeError):
+        db.add(0, ids, vals)  # already present (the reference would list it twice)
+    with pytest.raises(RuntimeError):
+        db.add(1, ids[::-1], vals)  # not a BowVector (ids must ascend)
+    with pytest.raises(RuntimeError):
+        db.add(8, ids, vals)  # slot out of range
+    with pytest.raises(RuntimeError):
+        db.add(2, np.arange(17, dtype=np.uint32), np.ones(17))  # more words than max_words
+    with pytest.raises(RuntimeError):
+        db.add(3, np.array([1, 10 ** 6], np.uint32), np.ones(2))  # not a word of the vocabulary
+    with pytest.raises(RuntimeError):
+        db.detect_relocalization(2, np.array([10 ** 6], np.uint32), np.ones(1))
+    with pytest.raises(RuntimeError):
+        db.set_covisibility(0, np.arange(11, dtype=np.int32) % 8)  # more than 10
+    with pytest.raises(RuntimeError):
+        db.detect_loop(3, ids, vals, np.array([9], np.int32), 0.0)  # connected slot out of range
+    assert list(db.detect_relocalization(1, ids, vals)) == [0]
