@@ -332,6 +332,9 @@ int rsc_kfdb_erase(rsc_kfdb* db, int kf);
 int rsc_kfdb_clear(rsc_kfdb* db);
 /* pKF->GetBestCovisibilityKeyFrames(10) of slot kf (n <= 10 slots, in order). */
 int rsc_kfdb_set_covisibility(rsc_kfdb* db, int kf, int n, const int32_t* best);
+/* The same for count slots at once (kf[c], n[c] <= 10, best[c][10] row-major; one upload). */
+int rsc_kfdb_set_covisibility_many(rsc_kfdb* db, int count, const int32_t* kf, const int32_t* n,
+                                   const int32_t* best);
 /* DetectRelocalizationCandidates(F) (:174-283): frame_id = F->mnId, (word_id, word_value) =
  * F->mBowVec.  candidates (capacity entries): the returned vector's slots in order. */
 int rsc_kfdb_detect_relocalization(rsc_kfdb* db, uint64_t frame_id, int n_words, const uint32_t* word_id,

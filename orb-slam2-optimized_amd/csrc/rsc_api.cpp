@@ -1583,6 +1583,7 @@ struct rsc_kfdb {
     uint32_t vocab = 0;
     uint32_t next_seq = 1;
     std::vector<uint8_t> present;
+    std::vector<int32_t> covis_h, covis_n_h;  // host mirror of the covisibility table
     DevBuf<uint32_t> ids, seq;
     DevBuf<double> vals;
     DevBuf<char> qbuf;  // the query BowVector: ids | vals (8-aligned), one upload per query
@@ -1645,6 +1646,8 @@ int rsc_kfdb_create(rsc_context* C, uint32_t vocab_words, int capacity, int max_
     db->max_words = max_words;
     db->vocab = vocab_words;
     db->present.assign(capacity, 0);
+    db->covis_h.assign((size_t)capacity * kKfdbCovis, 0);
+    db->covis_n_h.assign(capacity, 0);
     RSC_HIP(hipSetDevice(C->device));
     const size_t K = (size_t)capacity;
     int e = 0;
@@ -1724,10 +1727,32 @@ int rsc_kfdb_set_covisibility(rsc_kfdb* db, int kf, int n, const int32_t* best) 
         if (best[i] < 0 || best[i] >= db->cap) return RSC_ERR_ARG;
         row[i] = best[i];
     }
+    std::copy(row, row + kKfdbCovis, db->covis_h.begin() + (size_t)kf * kKfdbCovis);
+    db->covis_n_h[kf] = n;
     RSC_HIP(hipSetDevice(db->ctx->device));
     RSC_HIP(hipStreamSynchronize(db->ctx->stream));
     RSC_HIP(hipMemcpy(db->covis.p + (size_t)kf * kKfdbCovis, row, sizeof(row), hipMemcpyHostToDevice));
     RSC_HIP(hipMemcpy(db->covis_n.p + kf, &n, 4, hipMemcpyHostToDevice));
+    return RSC_OK;
+}
+
+int rsc_kfdb_set_covisibility_many(rsc_kfdb* db, int count, const int32_t* kf, const int32_t* n,
+                                   const int32_t* best) {
+    if (!db || count < 0 || (count && (!kf || !n || !best))) return RSC_ERR_ARG;
+    for (int c = 0; c < count; ++c) {  // validate everything before touching the mirror
+        if (kf[c] < 0 || kf[c] >= db->cap || n[c] < 0 || n[c] > kKfdbCovis) return RSC_ERR_ARG;
+        for (int i = 0; i < n[c]; ++i)
+            if (best[(size_t)c * kKfdbCovis + i] < 0 || best[(size_t)c * kKfdbCovis + i] >= db->cap) return RSC_ERR_ARG;
+    }
+    for (int c = 0; c < count; ++c) {
+        int32_t* row = db->covis_h.data() + (size_t)kf[c] * kKfdbCovis;
+        for (int i = 0; i < kKfdbCovis; ++i) row[i] = i < n[c] ? best[(size_t)c * kKfdbCovis + i] : 0;
+        db->covis_n_h[kf[c]] = n[c];
+    }
+    RSC_HIP(hipSetDevice(db->ctx->device));
+    RSC_HIP(hipStreamSynchronize(db->ctx->stream));
+    RSC_HIP(hipMemcpy(db->covis.p, db->covis_h.data(), 4 * db->covis_h.size(), hipMemcpyHostToDevice));
+    RSC_HIP(hipMemcpy(db->covis_n.p, db->covis_n_h.data(), 4 * db->covis_n_h.size(), hipMemcpyHostToDevice));
     return RSC_OK;
 }
 

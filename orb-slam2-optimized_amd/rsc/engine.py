@@ -42,7 +42,7 @@ EXPORTED = [
     "rsc_search_by_bow_kf_many", "rsc_diag_bow_phase_stamps", "rsc_diag_refine_phase_stamps",
     "rsc_search_by_sim3_many", "rsc_kfview_create", "rsc_kfview_destroy",
     "rsc_kfdb_create", "rsc_kfdb_destroy", "rsc_kfdb_add", "rsc_kfdb_erase", "rsc_kfdb_clear",
-    "rsc_kfdb_set_covisibility", "rsc_kfdb_detect_relocalization", "rsc_kfdb_detect_loop", "rsc_kfdb_state",
+    "rsc_kfdb_set_covisibility", "rsc_kfdb_set_covisibility_many", "rsc_kfdb_detect_relocalization", "rsc_kfdb_detect_loop", "rsc_kfdb_state",
 ]
 
 
@@ -209,6 +209,15 @@ class KeyFrameDatabase:
         b = np.ascontiguousarray(best, np.int32)
         _check(load_library().rsc_kfdb_set_covisibility(self.h, int(kf), len(b), b), "rsc_kfdb_set_covisibility")
 
+    def set_covisibility_many(self, kfs, bests):
+        """set_covisibility for many slots in one upload (bests: sequences of <= 10 slots)."""
+        k = np.ascontiguousarray(kfs, np.int32)
+        n = np.array([len(b) for b in bests], np.int32)
+        tab = np.zeros((max(len(k), 1), 10), np.int32)
+        for i, b in enumerate(bests):
+            tab[i, :len(b)] = b
+        _check(load_library().rsc_kfdb_set_covisibility_many(self.h, len(k), k, n, tab), "set_covisibility_many")
+
     def detect_relocalization(self, frame_id: int, ids, vals) -> np.ndarray:
         """DetectRelocalizationCandidates(F) (:174-283): candidate slots in the reference's order."""
         i, v = self._bow(ids, vals)
@@ -332,6 +341,7 @@ def load_library(path: str = LIB_PATH):
     L.rsc_kfdb_erase.argtypes = [vp, C.c_int]
     L.rsc_kfdb_clear.argtypes = [vp]
     L.rsc_kfdb_set_covisibility.argtypes = [vp, C.c_int, C.c_int, i32p]
+    L.rsc_kfdb_set_covisibility_many.argtypes = [vp, C.c_int, i32p, i32p, i32p]
     L.rsc_kfdb_detect_relocalization.argtypes = [vp, C.c_uint64, C.c_int, u32p_, f64p_, i32p, i32p]
     L.rsc_kfdb_detect_loop.argtypes = [vp, C.c_uint64, C.c_int, u32p_, f64p_, C.c_int, i32p, C.c_float, i32p, i32p]
     L.rsc_kfdb_state.argtypes = [vp, C.c_int, u64p_, i32p, f32p_]

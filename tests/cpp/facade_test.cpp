@@ -11,7 +11,9 @@
 #include "Optimizer.hpp"
 #include "MLPnPsolver.hpp"
 #include "ORBmatcher.hpp"
+#include "KeyFrameDatabase.hpp"
 #include <map>
+#include <set>
 
 struct Vec3 { float v[3]; float operator()(int i) const { return v[i]; } float& operator()(int i) { return v[i]; } };
 struct Mat3 { float m[3][3]; float operator()(int r, int c) const { return m[r][c]; } float& operator()(int r, int c) { return m[r][c]; } };
@@ -51,6 +53,21 @@ struct BowFrame { int N = 0; DescMat mDescriptors; std::vector<KeyPoint> mvKeys;
 // view record: n, desc[n*32], angle[n], valid[n] (u8), nodes, per node (id, count, feats[count])
 template <class V>
 void read_view(FILE* in, V& v, std::vector<KeyPoint>& kps, std::vector<std::shared_ptr<MapPoint>>* mps);
+
+// KeyFrameDatabase mocks: mnId, mBowVec (std::map), covisibility and connections
+struct DBKF {
+    uint64_t mnId = 0;
+    int idx = -1;
+    std::map<unsigned int, double> mBowVec;
+    std::vector<std::shared_ptr<DBKF>> covis;
+    std::set<std::shared_ptr<DBKF>> conn;
+    std::vector<std::shared_ptr<DBKF>> GetBestCovisibilityKeyFrames(int n) const {
+        return std::vector<std::shared_ptr<DBKF>>(covis.begin(), covis.begin() + std::min<size_t>(n, covis.size()));
+    }
+    std::set<std::shared_ptr<DBKF>> GetConnectedKeyFrames() const { return conn; }
+};
+struct DBFrame { uint64_t mnId = 0; std::map<unsigned int, double> mBowVec; };
+struct DBVoc { size_t n; size_t size() const { return n; } };
 
 // Frame as PoseOptimization sees it (include/Frame.hpp:52,131,142,145,153,169)
 struct PFrame {
@@ -204,6 +221,50 @@ int main(int argc, char** argv) {
                 wr<int32_t>(out, nms[c]);
                 for (auto& mp : mm[c]) wr<int32_t>(out, mp ? mp->idx1 : -1);
             }
+        }
+    } else if (mode == 6) {
+        // KeyFrameDatabase through rsc_orb::KeyFrameDatabase: a table of KeyFrames (BowVector,
+        // covisibility), then add / erase / clear / relocalization / loop operations; writes each
+        // query's candidates as KeyFrame table indices
+        auto read_bow = [&](std::map<unsigned int, double>& b) {
+            const int n = rd<int32_t>(in);
+            std::vector<uint32_t> ids(n);
+            for (auto& x : ids) x = rd<uint32_t>(in);
+            for (int i = 0; i < n; ++i) b[ids[i]] = rd<double>(in);
+        };
+        auto voc = std::make_shared<DBVoc>(DBVoc{rd<uint32_t>(in)});
+        const int K = rd<int32_t>(in);
+        std::vector<std::shared_ptr<DBKF>> kfs(K);
+        for (int k = 0; k < K; ++k) { kfs[k] = std::make_shared<DBKF>(); kfs[k]->idx = k; kfs[k]->mnId = 100000 + k; }
+        for (int k = 0; k < K; ++k) {
+            read_bow(kfs[k]->mBowVec);
+            const int nc = rd<int32_t>(in);
+            for (int j = 0; j < nc; ++j) kfs[k]->covis.push_back(kfs[rd<int32_t>(in)]);
+        }
+        rsc_orb::KeyFrameDatabase<std::shared_ptr<DBKF>> db(voc, K + 64);
+        const int nops = rd<int32_t>(in);
+        for (int o = 0; o < nops; ++o) {
+            const int kind = rd<int32_t>(in);
+            std::vector<std::shared_ptr<DBKF>> cands;
+            if (kind == 0) { db.add(kfs[rd<int32_t>(in)]); continue; }
+            if (kind == 1) { db.erase(kfs[rd<int32_t>(in)]); continue; }
+            if (kind == 2) { db.clear(); continue; }
+            if (kind == 4) {
+                DBFrame F;
+                F.mnId = rd<uint64_t>(in);
+                read_bow(F.mBowVec);
+                cands = db.DetectRelocalizationCandidates(&F);
+            } else {
+                auto q = std::make_shared<DBKF>();
+                q->mnId = rd<uint64_t>(in);
+                read_bow(q->mBowVec);
+                const int nc = rd<int32_t>(in);
+                for (int j = 0; j < nc; ++j) q->conn.insert(kfs[rd<int32_t>(in)]);
+                const float ms = rd<float>(in);
+                cands = db.DetectLoopCandidates(q, ms);
+            }
+            wr<int32_t>(out, (int32_t)cands.size());
+            for (auto& c : cands) wr<int32_t>(out, c->idx);
         }
     } else if (mode == 2) {
         auto kf1 = std::make_shared<KeyFrame>(), kf2 = std::make_shared<KeyFrame>();

@@ -230,3 +230,48 @@ def test_orbmatcher_facade_matches_oracle(frame_overload):
         assert np.array_equal(out[pos + 1:pos + 1 + len(m)], m)
         pos += 1 + len(m)
     assert pos == len(out)
+
+
+def _bow_bytes(ids, vals):
+    return struct.pack("<i", len(ids)) + np.asarray(ids, "<u4").tobytes() + np.asarray(vals, "<f8").tobytes()
+
+
+@pytest.mark.parametrize("seed", [3, 8])
+def test_keyframe_database_facade_matches_oracle(seed):
+    """rsc_orb::KeyFrameDatabase (KeyFrameDatabase.cpp) on mock KeyFrames / Frames (std::map
+    BowVectors, GetBestCovisibilityKeyFrames, GetConnectedKeyFrames): an operation script's
+    candidates equal the oracle's, KeyFrame by KeyFrame and in order."""
+    import kfdb_script as ks
+    ops = ks.make_script(seed, n_kfs=50, n_queries=30, words=250)
+    K = 50
+    bows, covis = [None] * K, [np.zeros(0, np.int32)] * K
+    for op in ops:
+        if op[0] == "add" and bows[op[1]] is None:
+            bows[op[1]] = (op[2], op[3])
+        elif op[0] == "covis":
+            covis[op[1]] = op[2]
+    buf = struct.pack("<iIi", 6, 10 ** 6, K)
+    for k in range(K):
+        buf += _bow_bytes(*bows[k]) + struct.pack("<i", len(covis[k])) + np.asarray(covis[k], "<i4").tobytes()
+    body, nops = b"", 0
+    for op in ops:
+        kind = ks.OPS[op[0]]
+        if op[0] == "covis":
+            continue
+        nops += 1
+        body += struct.pack("<i", kind)
+        if op[0] in ("add", "erase"):
+            body += struct.pack("<i", op[1])
+        elif op[0] == "reloc":
+            body += struct.pack("<Q", op[1]) + _bow_bytes(op[2], op[3])
+        elif op[0] == "loop":
+            body += struct.pack("<Q", op[1]) + _bow_bytes(op[2], op[3])
+            body += struct.pack("<i", len(op[4])) + np.asarray(op[4], "<i4").tobytes() + struct.pack("<f", op[5])
+    out = np.frombuffer(run(buf + struct.pack("<i", nops) + body), "<i4")
+    want = ks.run_script(ol.OracleKFDB(K), ops)
+    pos = 0
+    for w in want:
+        n = out[pos]
+        assert list(out[pos + 1:pos + 1 + n]) == list(w)
+        pos += 1 + n
+    assert pos == len(out)
