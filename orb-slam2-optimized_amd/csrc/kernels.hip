@@ -572,14 +572,17 @@ __global__ __launch_bounds__(256) void sim3_scan_kernel(const DevSim3* __restric
         Sim3Pose T;
         RSC_UNROLL for (int k = 0; k < 9; ++k) { T.R12[k] = pp[k]; T.R21[k] = pp[12 + k]; }
         RSC_UNROLL for (int k = 0; k < 3; ++k) { T.t12[k] = pp[9 + k]; T.t21[k] = pp[21 + k]; }
+        // all PPT ballots first, then one predicated store by lanes 0..PPT-1 (as the PnP scan)
+        uint64_t b[PPT];
+        RSC_UNROLL for (int s = 0; s < PPT; ++s)
+            b[s] = __ballot(sim3_inlier(T, K1, K2, A[s], B[s], p1u[s], p1v[s], p2u[s], p2v[s], e1[s], e2[s]));
         int cnt = 0;
-        uint64_t* mw = masks ? masks + (size_t)(lp.out0 + h) * mask_words : nullptr;
+        uint64_t mine = 0;
         RSC_UNROLL for (int s = 0; s < PPT; ++s) {
-            const bool inl = sim3_inlier(T, K1, K2, A[s], B[s], p1u[s], p1v[s], p2u[s], p2v[s], e1[s], e2[s]);
-            const uint64_t b = __ballot(inl);
-            cnt += __popcll(b);
-            if (mw && lane == 0) mw[s * 4 + wave] = b;
+            cnt += __popcll(b[s]);
+            mine = (lane == s) ? b[s] : mine;
         }
+        if (masks && lane < PPT) masks[(size_t)(lp.out0 + h) * mask_words + lane * 4 + wave] = mine;
         if (lane == 0) wave_cnt[wave][j & 63] = cnt;
         if ((j & 63) == 63 || j == wt.z - 1) {
             __syncthreads();
@@ -663,14 +666,17 @@ __global__ __launch_bounds__(256) void mlpnp_scan_kernel(const DevML* __restrict
         double R[9], t[3];
         RSC_UNROLL for (int k = 0; k < 9; ++k) R[k] = pp[k];
         RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = pp[9 + k];
+        // all PPT ballots first, then one predicated store by lanes 0..PPT-1 (as the PnP scan)
+        uint64_t b[PPT];
+        RSC_UNROLL for (int s = 0; s < PPT; ++s)
+            b[s] = __ballot(mlpnp_inlier(R, t, P.fx, P.fy, P.cx, P.cy, X[s], Y[s], Z[s], U[s], V[s], E[s]));
         int cnt = 0;
-        uint64_t* mw = masks ? masks + (size_t)(lp.out0 + h) * mask_words : nullptr;
+        uint64_t mine = 0;
         RSC_UNROLL for (int s = 0; s < PPT; ++s) {
-            const bool inl = mlpnp_inlier(R, t, P.fx, P.fy, P.cx, P.cy, X[s], Y[s], Z[s], U[s], V[s], E[s]);
-            const uint64_t b = __ballot(inl);
-            cnt += __popcll(b);
-            if (mw && lane == 0) mw[s * 4 + wave] = b;
+            cnt += __popcll(b[s]);
+            mine = (lane == s) ? b[s] : mine;
         }
+        if (masks && lane < PPT) masks[(size_t)(lp.out0 + h) * mask_words + lane * 4 + wave] = mine;
         if (lane == 0) wave_cnt[wave][j & 63] = cnt;
         if ((j & 63) == 63 || j == wt.z - 1) {
             __syncthreads();

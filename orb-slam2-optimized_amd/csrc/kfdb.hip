@@ -99,29 +99,61 @@ __global__ __launch_bounds__(1024) void kfdb_finish_kernel(DevKFDB db, KfdbQuery
     __shared__ int s_wcnt[16];
     __shared__ int s_cnt;
     __shared__ unsigned long long s_key[kRankLds];
+    // per-query lists of the scored slots: in LDS when they fit (the usual case: a handful), else
+    // in the global scratch (flat pointers address either)
+    __shared__ int s_tmp[kRankLds], s_scored[kRankLds], s_best[kRankLds];
+    __shared__ float s_sc[kRankLds], s_acc[kRankLds];
     const int t = q.loop ? 0 : 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    // the query words, held for the final table clear (no reload at the end)
+    uint32_t qw[kKfdbMaxWords / 1024];
+#pragma unroll
+    for (int k = 0; k < kKfdbMaxWords / 1024; ++k) {
+        const int i = threadIdx.x + k * 1024;
+        qw[k] = i < q.n ? db.qids[i] : 0u;
+    }
     // ---- select ----
     const int n = db.cap;
+    constexpr int kHeld = 4;  // list entries per thread kept in registers between the two passes
+    int held[kHeld];
     int mx = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x)
+#pragma unroll
+    for (int k = 0; k < kHeld; ++k) {
+        const int i = threadIdx.x + k * 1024;
+        held[k] = (i < n && db.list[i]) ? db.words[t][i] : -1;
+        mx = max(mx, held[k]);
+    }
+    for (int i = threadIdx.x + kHeld * 1024; i < n; i += blockDim.x)
         if (db.list[i]) mx = max(mx, db.words[t][i]);
     const int maxc = block_reduce(mx, s_red, [](int a, int b) { return max(a, b); });
     const int minc = (int)((float)maxc * 0.8f);  // int minCommonWords = maxCommonWords*0.8f
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x)
-        if (db.list[i] && db.words[t][i] > minc) db.tmp[atomicAdd(&s_cnt, 1)] = i;
+    auto keep = [&](int i) {
+        const int c = atomicAdd(&s_cnt, 1);
+        if (c < kRankLds) s_tmp[c] = i;
+        db.tmp[c] = i;
+    };
+#pragma unroll
+    for (int k = 0; k < kHeld; ++k)
+        if (held[k] > minc) keep(threadIdx.x + k * 1024);
+    for (int i = threadIdx.x + kHeld * 1024; i < n; i += blockDim.x)
+        if (db.list[i] && db.words[t][i] > minc) keep(i);
     __syncthreads();
     const int S = s_cnt;
-    if (S <= kRankLds) {
-        for (int i = threadIdx.x; i < S; i += blockDim.x) s_key[i] = db.key[db.tmp[i]];
+    const bool small = S <= kRankLds;
+    int* scored = small ? s_scored : db.scored;
+    float* sc = small ? s_sc : db.sc;
+    float* accs = small ? s_acc : db.acc;
+    int* bests = small ? s_best : db.best;
+    if (small) {
+        for (int i = threadIdx.x; i < S; i += blockDim.x) s_key[i] = db.key[s_tmp[i]];
         __syncthreads();
         for (int i = threadIdx.x; i < S; i += blockDim.x) {
             const unsigned long long k = s_key[i];
             int r = 0;
             for (int j = 0; j < S; ++j) r += s_key[j] < k;
-            db.scored[r] = db.tmp[i];
+            s_scored[r] = s_tmp[i];
         }
     } else {
         for (int i = threadIdx.x; i < S; i += blockDim.x) {
@@ -135,7 +167,7 @@ __global__ __launch_bounds__(1024) void kfdb_finish_kernel(DevKFDB db, KfdbQuery
     __syncthreads();
     // ---- score ----
     for (int e = wave; e < S; e += nw) {
-        const int kf = db.scored[e];
+        const int kf = scored[e];
         const int len = db.len[kf];
         const uint32_t* ids = db.ids + (size_t)kf * db.max_words;
         const double* vals = db.vals + (size_t)kf * db.max_words;
@@ -173,7 +205,7 @@ __global__ __launch_bounds__(1024) void kfdb_finish_kernel(DevKFDB db, KfdbQuery
         score = -score / 2.0;
         const float si = (float)score;  // float si = mpVoc->score(...)
         if (lane == 0) {
-            db.sc[e] = si;
+            sc[e] = si;
             db.score[t][kf] = si;  // mLoopScore / mRelocScore
         }
     }
@@ -181,10 +213,10 @@ __global__ __launch_bounds__(1024) void kfdb_finish_kernel(DevKFDB db, KfdbQuery
     // ---- accumulate ----
     float m = q.loop ? q.min_score : 0.0f;  // bestAccScore's initial value
     for (int i = threadIdx.x; i < S; i += blockDim.x) {
-        const int kf = db.scored[i];
-        const float si = db.sc[i];
+        const int kf = scored[i];
+        const float si = sc[i];
         if (q.loop && !(si >= q.min_score)) {  // not in lScoreAndMatch
-            db.best[i] = -1;
+            bests[i] = -1;
             continue;
         }
         float bestScore = si, accScore = si;
@@ -211,8 +243,8 @@ __global__ __launch_bounds__(1024) void kfdb_finish_kernel(DevKFDB db, KfdbQuery
                 bestScore = s2[k];
             }
         }
-        db.acc[i] = accScore;
-        db.best[i] = bk;
+        accs[i] = accScore;
+        bests[i] = bk;
         if (accScore > m) m = accScore;
     }
     const float bestAcc = block_reduce(m, s_redf, [](float a, float b) { return a > b ? a : b; });
@@ -221,26 +253,28 @@ __global__ __launch_bounds__(1024) void kfdb_finish_kernel(DevKFDB db, KfdbQuery
     int total = 0;
     for (int base = 0; base < S; base += blockDim.x) {
         const int i = base + threadIdx.x;
-        bool keep = false;
-        if (i < S && db.best[i] >= 0 && db.acc[i] > minRetain) {
-            keep = true;
-            const int b = db.best[i];
-            for (int j = 0; j < i && keep; ++j)
-                if (db.best[j] == b && db.acc[j] > minRetain) keep = false;  // already added
+        bool kept = false;
+        if (i < S && bests[i] >= 0 && accs[i] > minRetain) {
+            kept = true;
+            const int b = bests[i];
+            for (int j = 0; j < i && kept; ++j)
+                if (bests[j] == b && accs[j] > minRetain) kept = false;  // already added
         }
-        const unsigned long long bal = __ballot(keep);
+        const unsigned long long bal = __ballot(kept);
         const int before = __popcll(bal & ((1ull << lane) - 1ull));
         __syncthreads();
         if (lane == 0) s_wcnt[wave] = __popcll(bal);
         __syncthreads();
         int off = total;
         for (int w = 0; w < wave; ++w) off += s_wcnt[w];
-        if (keep) db.out[1 + off + before] = db.best[i];
+        if (kept) db.out[1 + off + before] = bests[i];
         for (int w = 0; w < nw; ++w) total += s_wcnt[w];
     }
     if (threadIdx.x == 0) db.out[0] = total;
     // ---- clear the word-position table ----
-    for (int i = threadIdx.x; i < q.n; i += blockDim.x) db.wpos[db.qids[i]] = -1;
+#pragma unroll
+    for (int k = 0; k < kKfdbMaxWords / 1024; ++k)
+        if (threadIdx.x + k * 1024 < q.n) db.wpos[qw[k]] = -1;
 }
 
 }  // namespace
