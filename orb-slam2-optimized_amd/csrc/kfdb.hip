@@ -7,7 +7,8 @@ namespace rsc {
 
 namespace {
 
-constexpr int kBatch = 8;     // words per lane per batch of loads
+constexpr int kBatch = 8;        // words per lane per batch of loads (score phase)
+constexpr int kCountBatch = 16;  // words per lane per batch in the count kernel (1024 per wave)
 constexpr int kRankLds = 1024;  // scored slots ranked from LDS (beyond: from global memory)
 
 // The query's word -> position table (wpos[word] = index in F->mBowVec, -1 elsewhere): scattered
@@ -25,34 +26,37 @@ __global__ __launch_bounds__(256) void kfdb_count_kernel(DevKFDB db, KfdbQuery q
     const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (slot >= db.cap) return;
     if (lane == 0) db.list[slot] = 0;  // in lKFsSharingWords (a flag per slot: no shared counter)
+    const int t = q.loop ? 0 : 1;
+    // independent loads issued together: the slot length, its state, and the first
+    // 64 * kCountBatch word ids (the slot stride is max_words, so the window is in bounds whatever
+    // the length); the table gathers follow, masked by the length
     const int len = db.len[slot];
-    if (len == 0) return;  // not in any list: the walk never touches its state
+    const unsigned long long qb0 = db.query[t][slot];
+    const int w0 = db.words[t][slot];
     const uint32_t* ids = db.ids + (size_t)slot * db.max_words;
     int c = 0, first = INT_MAX;
-    // kBatch words per lane in flight: the id loads, then the dependent table gathers, are issued
-    // back to back (clamped, unconditional) instead of one load-gather round trip per word
-    for (int base = 0; base < len; base += 64 * kBatch) {
-        uint32_t w[kBatch];
-        int p[kBatch];
+    for (int base = 0; base == 0 || base < len; base += 64 * kCountBatch) {
+        uint32_t w[kCountBatch];
+        int p[kCountBatch];
 #pragma unroll
-        for (int b = 0; b < kBatch; ++b) w[b] = ids[min(base + b * 64 + lane, len - 1)];
+        for (int b = 0; b < kCountBatch; ++b) w[b] = ids[min(base + b * 64 + lane, db.max_words - 1)];
 #pragma unroll
-        for (int b = 0; b < kBatch; ++b) p[b] = db.wpos[w[b]];
+        for (int b = 0; b < kCountBatch; ++b) p[b] = db.wpos[base + b * 64 + lane < len ? w[b] : 0u];
 #pragma unroll
-        for (int b = 0; b < kBatch; ++b)
+        for (int b = 0; b < kCountBatch; ++b)
             if (base + b * 64 + lane < len && p[b] >= 0) {
                 c++;
                 first = min(first, p[b]);
             }
     }
+    if (len == 0) return;  // not in any list: the walk never touches its state
     for (int off = 32; off > 0; off >>= 1) {
         c += __shfl_xor(c, off);
         first = min(first, __shfl_xor(first, off));
     }
     if (lane != 0 || c == 0) return;
-    const int t = q.loop ? 0 : 1;
-    unsigned long long qb = db.query[t][slot];
-    int w = db.words[t][slot];
+    unsigned long long qb = qb0;
+    int w = w0;
     bool in_list = false;
     if (qb != q.id) {
         if (q.loop && db.conn[slot]) {
