@@ -176,18 +176,22 @@ __global__ __launch_bounds__(1024) void kfdb_finish_kernel(DevKFDB db, KfdbQuery
         const uint32_t* ids = db.ids + (size_t)kf * db.max_words;
         const double* vals = db.vals + (size_t)kf * db.max_words;
         double score = 0;
-        for (int base = 0; base < len; base += 64 * kBatch) {
+        // the first window is loaded with the length (the slot stride bounds it), not after it
+        for (int base = 0; base == 0 || base < len; base += 64 * kBatch) {
             uint32_t w[kBatch];
             double wv[kBatch], vv[kBatch];
             int p[kBatch];
 #pragma unroll
             for (int b = 0; b < kBatch; ++b) {
-                const int j = min(base + b * 64 + lane, len - 1);
+                const int j = min(base + b * 64 + lane, db.max_words - 1);
                 w[b] = ids[j];
                 wv[b] = vals[j];
             }
 #pragma unroll
-            for (int b = 0; b < kBatch; ++b) p[b] = base + b * 64 + lane < len ? db.wpos[w[b]] : -1;
+            for (int b = 0; b < kBatch; ++b)
+                p[b] = db.wpos[base + b * 64 + lane < len ? w[b] : 0u];
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) p[b] = base + b * 64 + lane < len ? p[b] : -1;
 #pragma unroll
             for (int b = 0; b < kBatch; ++b) vv[b] = db.qvals[max(p[b], 0)];
 #pragma unroll
