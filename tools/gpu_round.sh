@@ -9,7 +9,7 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 if [ -z "$NO_TESTS" ]; then
-  timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/tests.txt 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests.txt 2>&1
 fi
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
 cd /tmp && export TMPDIR=/tmp

@@ -9,7 +9,7 @@ from collections import defaultdict
 
 acc = defaultdict(list)
 for r in csv.DictReader(open(sys.argv[1])):
-    name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "").strip()
+    name = re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", "")).replace("void ", "").strip()
     acc[(name, int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"]))].append(
         (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 rows = sorted(acc.items(), key=lambda kv: -sum(kv[1][1]) if False else -sum(kv[1]))
