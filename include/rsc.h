@@ -106,6 +106,10 @@ int rsc_pnp_set_ransac_parameters_many(rsc_pnp* const* solvers, int count, doubl
 int rsc_pnp_get_state(const rsc_pnp* s, int32_t out[8]);
 /* Debug/parity hook: sample indices (8 per hypothesis) of the last launch for this solver. */
 int rsc_pnp_last_samples(rsc_pnp* s, int32_t* out, int cap);
+/* Parity hook: inlier counts and float poses (R row-major 9 + t 3) of every hypothesis of the last
+ * launch for this solver (PnPsolver.cpp:139-146 mnInliersi / mRi, mti per hypothesis).  Valid until
+ * the context's next launch. */
+int rsc_pnp_last_hypotheses(rsc_pnp* s, int32_t* counts, float* poses, int cap);
 
 /* ---- Sim3Solver (include/Sim3Solver.hpp:16-103, src/Sim3Solver.cpp) --------------------------- */
 /* Raw constructor inputs for one keyframe pair (Sim3Solver.cpp:6-85), per match slot i1 < n1. */
@@ -143,6 +147,9 @@ int rsc_sim3_set_ransac_parameters_many(rsc_sim3* const* solvers, int count, dou
 int rsc_sim3_get_state(const rsc_sim3* s, int32_t out[6]);
 /* Prepared per-correspondence arrays built by the constructor (for parity tests):
  * X1c/X2c [N][3], P1im1/P2im2 [N][2], max_err1/2 [N] (size_t thresholds), indices1 [N]. */
+/* Parity hook: inlier counts and float (R12 9 + t12 3) of every hypothesis of the last launch
+ * (Sim3Solver.cpp:150-153 mnInliersi / mR12i, mt12i). */
+int rsc_sim3_last_hypotheses(rsc_sim3* s, int32_t* counts, float* poses, int cap);
 int rsc_sim3_prepared(const rsc_sim3* s, float* X1c, float* X2c, float* P1im1, float* P2im2, uint64_t* max_err1,
                       uint64_t* max_err2, int32_t* indices1);
 
@@ -170,6 +177,7 @@ int rsc_mlpnp_get_state(const rsc_mlpnp* s, int32_t out[6]);
 /* Parity hooks: double poses (R 9 + t 3) and sample indices (8 per hypothesis) of the last launch. */
 int rsc_mlpnp_last_poses(rsc_mlpnp* s, double* out, int cap);
 int rsc_mlpnp_last_samples(rsc_mlpnp* s, int32_t* out, int cap);
+int rsc_mlpnp_last_counts(rsc_mlpnp* s, int32_t* counts, int cap);
 
 /* ---- Event drivers (BASELINE config 5) -----------------------------------------------------------
  * One relocalization or loop-closure event = the candidate solvers one Tracking::Relocalization() /

@@ -974,6 +974,28 @@ int rsc_pnp_last_samples(rsc_pnp* s, int32_t* out, int cap) {
     return n;
 }
 
+// Parity hook: counts + float poses of the last speculation of this solver.  The counts live in the
+// context's pinned count buffer (valid until the context's next speculation); poses stay in HBM.
+namespace {
+int last_hypotheses(rsc_context* C, int out0, int H, int stride, int32_t* counts, float* poses, int cap) {
+    if (out0 < 0) return 0;
+    const int n = std::min(cap, H);
+    if (counts) std::memcpy(counts, C->h_counts.p + out0, (size_t)n * 4);
+    if (poses) {
+        if (!C->d_poses.p) return RSC_ERR_ARG;
+        std::vector<float> all((size_t)n * stride);
+        RSC_HIP(hipMemcpy(all.data(), C->d_poses.p + (size_t)out0 * stride, all.size() * 4, hipMemcpyDeviceToHost));
+        for (int h = 0; h < n; ++h) std::memcpy(poses + (size_t)h * 12, all.data() + (size_t)h * stride, 48);
+    }
+    return n;
+}
+}  // namespace
+
+int rsc_pnp_last_hypotheses(rsc_pnp* s, int32_t* counts, float* poses, int cap) {
+    if (!s) return RSC_ERR_ARG;
+    return last_hypotheses(s->ctx, s->spec_out0, s->spec_H, 12, counts, poses, cap);
+}
+
 // ---- Sim3 ----
 int rsc_sim3_create(rsc_context* C, const rsc_sim3_input* in, uint32_t seed, rsc_sim3** out) {
     if (!C || !in || !out || in->n1 < 0) return RSC_ERR_ARG;
@@ -1094,6 +1116,11 @@ int rsc_sim3_get_state(const rsc_sim3* s, int32_t out[6]) {
     out[0] = t.mnIterations; out[1] = t.mRansacMaxIts; out[2] = t.mRansacMinInliers; out[3] = t.mnBestInliers;
     out[4] = t.N; out[5] = t.mN1;
     return RSC_OK;
+}
+
+int rsc_sim3_last_hypotheses(rsc_sim3* s, int32_t* counts, float* poses, int cap) {
+    if (!s) return RSC_ERR_ARG;
+    return last_hypotheses(s->ctx, s->spec_out0, s->spec_H, 24, counts, poses, cap);
 }
 
 int rsc_sim3_prepared(const rsc_sim3* s, float* X1c, float* X2c, float* P1im1, float* P2im2, uint64_t* e1,
@@ -2070,6 +2097,11 @@ int rsc_mlpnp_last_poses(rsc_mlpnp* s, double* out, int cap) {
     const int n = std::min(cap, s->spec_H);
     RSC_HIP(hipMemcpy(out, C->d_mposes.p + (size_t)s->spec_out0 * 12, (size_t)n * 96, hipMemcpyDeviceToHost));
     return n;
+}
+
+int rsc_mlpnp_last_counts(rsc_mlpnp* s, int32_t* counts, int cap) {
+    if (!s || !counts) return RSC_ERR_ARG;
+    return last_hypotheses(s->ctx, s->spec_out0, s->spec_H, 12, counts, nullptr, cap);
 }
 
 int rsc_mlpnp_last_samples(rsc_mlpnp* s, int32_t* out, int cap) {

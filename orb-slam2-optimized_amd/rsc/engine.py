@@ -29,7 +29,8 @@ EXPORTED = [
     "rsc_version", "rsc_status_string", "rsc_context_create", "rsc_context_destroy", "rsc_context_set_stream",
     "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_last_kernel_timing", "rsc_diag_host_timing", "rsc_context_enable_timing", "rsc_context_set_solve_mode",
     "rsc_pnp_create", "rsc_pnp_destroy", "rsc_pnp_set_ransac_parameters", "rsc_pnp_iterate", "rsc_pnp_find",
-    "rsc_pnp_iterate_many", "rsc_pnp_reset", "rsc_pnp_get_state", "rsc_pnp_last_samples",
+    "rsc_pnp_iterate_many", "rsc_pnp_reset", "rsc_pnp_get_state", "rsc_pnp_last_samples", "rsc_pnp_last_hypotheses",
+    "rsc_sim3_last_hypotheses", "rsc_mlpnp_last_counts",
     "rsc_sim3_create", "rsc_sim3_destroy", "rsc_sim3_set_ransac_parameters", "rsc_sim3_iterate", "rsc_sim3_find",
     "rsc_sim3_iterate_many", "rsc_sim3_reset", "rsc_sim3_get_state", "rsc_sim3_prepared", "rsc_rand_stream",
     "rsc_pnp_reset_many", "rsc_pnp_set_ransac_parameters_many", "rsc_sim3_reset_many",
@@ -285,6 +286,9 @@ def load_library(path: str = LIB_PATH):
     L.rsc_pnp_reset.argtypes = [vp, C.c_uint32]
     L.rsc_pnp_get_state.argtypes = [vp, i32p]
     L.rsc_pnp_last_samples.argtypes = [vp, i32p, C.c_int]
+    L.rsc_pnp_last_hypotheses.argtypes = [vp, i32p, f32p, C.c_int]
+    L.rsc_sim3_last_hypotheses.argtypes = [vp, i32p, f32p, C.c_int]
+    L.rsc_mlpnp_last_counts.argtypes = [vp, i32p, C.c_int]
     L.rsc_sim3_create.argtypes = [vp, C.POINTER(Sim3Input), C.c_uint32, C.POINTER(vp)]
     L.rsc_sim3_destroy.argtypes = [vp]
     L.rsc_sim3_set_ransac_parameters.argtypes = [vp, C.c_double, C.c_int, C.c_int]
@@ -471,6 +475,15 @@ class PnPSolver:
         n = load_library().rsc_pnp_last_samples(self.h, out.reshape(-1), cap)
         return out[:max(n, 0)]
 
+    def last_hypotheses(self, cap: int = 4096):
+        """(counts [H], float poses [H, 12] = R row-major + t) of the last launch (parity hook)."""
+        cnt = np.zeros(cap, np.int32)
+        pos = np.zeros((cap, 12), np.float32)
+        n = load_library().rsc_pnp_last_hypotheses(self.h, cnt, pos.reshape(-1), cap)
+        if n < 0:
+            _check(n, "last_hypotheses")
+        return cnt[:n], pos[:n]
+
 
 def pnp_iterate_many(solvers, n_iterations, with_masks: bool = True):
     """rsc_pnp_iterate_many: iterate() of every solver in one set of launches."""
@@ -567,6 +580,15 @@ class Sim3Solver:
         _check(load_library().rsc_sim3_prepared(self.h, X1, X2, P1, P2, e1, e2, idx), "prepared")
         return dict(X1c=X1, X2c=X2, P1im1=P1, P2im2=P2, maxerr1=e1, maxerr2=e2, indices=idx)
 
+    def last_hypotheses(self, cap: int = 4096):
+        """(counts [H], float (R12, t12) [H, 12]) of the last launch (parity hook)."""
+        cnt = np.zeros(cap, np.int32)
+        pos = np.zeros((cap, 12), np.float32)
+        n = load_library().rsc_sim3_last_hypotheses(self.h, cnt, pos.reshape(-1), cap)
+        if n < 0:
+            _check(n, "last_hypotheses")
+        return cnt[:n], pos[:n]
+
 
 def sim3_iterate_many(solvers, n_iterations, with_masks: bool = True):
     L = load_library()
@@ -634,6 +656,13 @@ class MLPnPSolver:
         m = L.rsc_mlpnp_last_poses(self.h, pos.reshape(-1), cap)
         assert n == m
         return smp[:n], pos[:n]
+
+    def last_counts(self, cap=4096):
+        cnt = np.zeros(cap, np.int32)
+        n = load_library().rsc_mlpnp_last_counts(self.h, cnt, cap)
+        if n < 0:
+            _check(n, "last_counts")
+        return cnt[:n]
 
 
 class SolverBatch:
