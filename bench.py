@@ -6,16 +6,24 @@ candidates x 2000 correspondences, SetRansacParameters(0.99,10,300,4,0.5,5.991) 
 then iterate(300) on every candidate — 300 hypotheses each (Q1: '||' loop) in exhaustive mode
 (40% inliers, minInliers=1000 unreachable), i.e. 19,200 hypotheses per step, all candidates in one
 rsc_pnp_iterate_many call.  A "step" = reset every solver with a fresh rand() seed + the call above
-(sampling, EPnP solves, inlier scans, selection replay, result records).  With N GPUs (one process
-per GPU, torchrun) every rank runs its own 64-candidate batch (weak scaling) and the per-candidate
-result records are all-gathered over RCCL at the end of each step.
+(sampling, EPnP solves, inlier scans, selection replay, result records) + the RCCL all-gather of the
+per-candidate result records when N > 1.
 
-The Sim3 loop-closure batch (config 3: 32 pairs x 1000 matches, iterate(300)) is measured in the
-same run and reported under "sim3".
+Multi-GPU: one process per GPU.  Under torchrun the ranks come from the
+environment; `python bench.py --gpus N` without WORLD_SIZE starts the N rank processes itself
+(before anything touches the GPU) and exits with their status.  Default = weak scaling (64
+candidates per GPU); `--strong` splits the one 64-candidate batch across the ranks.
+
+Other sections of the same JSON line: sim3 (config 3), mlpnp (config 4 per-GPU share), events
+(config 5), single-event latency, and the SURVEY §8(f) neighbours (PoseOptimization, SearchByBoW,
+SearchBySim3, KeyFrameDatabase).  Every RANSAC section carries a cpu_baseline (the oracle
+restatement on the host's cores: 1 core and all cores, 3 warm-up batches then the median of >= 10).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,11 +33,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import numpy as np  # noqa: E402
 
-RELOC = (0.99, 10, 300, 4, 0.5, 5.991)
-LOOP = (0.99, 20, 300)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec)
-PROFILE_DIR = "profiles/r01"
+PROFILE_DIR = "profiles/r02"
 
 
 def _profile_json(name):
@@ -49,19 +55,54 @@ def parse():
     p.add_argument("--candidates", type=int, default=64)
     p.add_argument("--corrs", type=int, default=2000)
     p.add_argument("--iters", type=int, default=300)
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--strong", action="store_true", help="split one 64-candidate batch across the ranks")
+    p.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-cores CPU baseline (0: auto)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--no-sim3", action="store_true")
-    p.add_argument("--no-mlpnp", action="store_true")
-    p.add_argument("--no-events", action="store_true")
-    p.add_argument("--no-poseopt", action="store_true")
-    p.add_argument("--no-bow", action="store_true")
-    p.add_argument("--no-sim3match", action="store_true")
-    p.add_argument("--no-kfdb", action="store_true")
-    return p.parse_args()
+    for s in ("sim3", "mlpnp", "events", "latency", "poseopt", "bow", "sim3match", "kfdb"):
+        p.add_argument(f"--no-{s}", action="store_true")
+    p.add_argument("--only-headline", action="store_true", help="config 2 only (PMC passes)")
+    p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                   help="nccl (= RCCL over xGMI, the product path) or gloo (host collectives: lets N ranks "
+                        "share fewer GPUs to rehearse the launch and gather on a 1-GPU box)")
+    a = p.parse_args()
+    if a.only_headline:
+        for s in ("sim3", "mlpnp", "events", "latency", "poseopt", "bow", "sim3match", "kfdb"):
+            setattr(a, f"no_{s}", True)
+    return a
+
+
+# ------------------------------------------------------------------------------------------------
+# process launch and distributed setup
+# ------------------------------------------------------------------------------------------------
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` outside torchrun: start N rank processes (RANK/LOCAL_RANK/WORLD_SIZE,
+    rendezvous on 127.0.0.1) and return the worst exit status.  The parent never touches the GPU."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        code = p.wait()
+        if code != 0 and rc == 0:
+            rc = code
+            for q in procs:
+                if q.poll() is None:
+                    q.terminate()
+    return rc
+
+
+COLL_DEV = "cuda"  # device of the collective tensors: cuda for RCCL, cpu for gloo
 
 
 def dist_setup(args):
+    """One process per GPU: rank r drives GPU LOCAL_RANK.  With --dist-backend gloo the ranks may
+    share GPUs (device = LOCAL_RANK mod the visible count) and the collectives run on host tensors."""
+    global COLL_DEV
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -69,8 +110,13 @@ def dist_setup(args):
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            local = local % max(1, torch.cuda.device_count())
+            COLL_DEV = "cpu"
+            dist.init_process_group("gloo")
     return world, rank, local, dist
 
 
@@ -79,36 +125,90 @@ def barrier(dist):
         dist.barrier()
 
 
-def pnp_batch(rng, C, N, ratio):
-    from rsc import synth
-    return [synth.make_pnp_scene(rng, N, ratio) for _ in range(C)]
+def reduce_time_and_count(dist, dt, count):
+    """max over ranks of the timed region, sum of the work units."""
+    if dist is None:
+        return dt, count
+    import torch
+    t = torch.tensor([dt, float(count)], dtype=torch.float64, device=COLL_DEV)
+    mx = t.clone()
+    dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
+    dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+    return float(mx[0]), int(t[1])
 
 
-def run_pnp(engine, ctx, scenes, args, dist, rank, world):
+def cpu_threads(args) -> int:
+    if args.cpu_threads > 0:
+        return args.cpu_threads
+    env = os.environ.get("OMP_NUM_THREADS")
+    n = int(env) if env and env.isdigit() else len(os.sched_getaffinity(0))
+    return max(1, min(n, 16))
+
+
+def median_batches(fn, warmup=3, reps=10):
+    """BASELINE.md §2 timing rule: `warmup` untimed batches, then the median wall time of `reps`
+    timed batches."""
+    for _ in range(warmup):
+        fn()
+    times = []
+    while len(times) < reps:
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    return float(np.median(times)), len(times)
+
+
+def cpu_section(fn_for_threads, units_per_batch, unit, sample, threads, warmup=3, reps=10):
+    """cpu_baseline object: 1 core (the reference's one-thread loop) + all cores (std::thread per
+    shard of the same batch)."""
+    med1, n1 = median_batches(lambda: fn_for_threads(1), warmup, reps)
+    out = dict(value=round(units_per_batch / med1, 2), unit=unit, cores=1, kind="port",
+               sample=f"{sample}; {warmup} warm-up + median of {n1} batches, oracle restatement, 1 thread",
+               median_batch_s=round(med1, 5))
+    if threads > 1:
+        medn, nn = median_batches(lambda: fn_for_threads(threads), warmup, reps)
+        out["all_cores"] = dict(value=round(units_per_batch / medn, 2), unit=unit, cores=threads,
+                                median_batch_s=round(medn, 5),
+                                sample=f"same batch, {warmup} warm-up + median of {nn}, std::thread per shard")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# config 2 (headline)
+# ------------------------------------------------------------------------------------------------
+def run_pnp(engine, ctx, scenes, cand_ids, args, dist, rank, world):
+    from rsc import workloads as wl
     solvers = [engine.PnPSolver(ctx, sc, 1) for sc in scenes]
     batch = engine.SolverBatch(solvers)
     C = len(solvers)
     gather = None
     if dist is not None:
         import torch
-        rec = torch.zeros(C, 20, dtype=torch.float32, device="cuda")
-        gather = (torch, rec, torch.zeros(world * C, 20, dtype=torch.float32, device="cuda"))
-
-    seeds = np.zeros(C, np.uint32)
-    h = np.zeros((C, 20), np.float32)
+        from rsc import dist as rdist
+        maxc = args.candidates  # fixed block per rank (strong-mode shards may differ by one)
+        rec = torch.zeros(maxc, rdist.RECORD, dtype=torch.float32, device=COLL_DEV)
+        allrec = torch.zeros(world * maxc, rdist.RECORD, dtype=torch.float32, device=COLL_DEV)
+        host = np.full((maxc, rdist.RECORD), -1.0, np.float32)
+        gather = (torch, rec, allrec, host)
 
     def step(s):
-        seeds[:] = 1 + np.arange(C) + C * (s + 1000 * rank)
+        if args.strong:
+            seeds = wl.config2_seeds(s, 0, args.candidates)[cand_ids]
+        else:
+            seeds = wl.config2_seeds(s, rank, args.candidates)
         batch.reset(seeds)
-        batch.set_ransac_parameters(*RELOC)
+        batch.set_ransac_parameters(*wl.RELOC)
         outs = batch.iterate_raw(args.iters)
         if gather is not None:
-            torch, rec, allrec = gather
-            h[:, 0], h[:, 1], h[:, 2], h[:, 3] = outs["ok"], outs["no_more"], outs["n_inliers"], outs["iterations"]
-            h[:, 4:20] = outs["T"].reshape(C, 16)
-            rec.copy_(torch.from_numpy(h))
-            dist.all_gather_into_tensor(allrec, rec)  # RCCL over xGMI: winner records of all ranks
-            torch.cuda.synchronize()
+            torch, rec, allrec, host = gather
+            host[:C, 0] = cand_ids
+            host[:C, 1], host[:C, 2], host[:C, 3], host[:C, 4] = (outs["ok"], outs["no_more"], outs["n_inliers"],
+                                                                  outs["iterations"])
+            host[:C, 5:21] = outs["T"].reshape(C, 16)
+            rec.copy_(torch.from_numpy(host))
+            dist.all_gather_into_tensor(allrec, rec)  # RCCL over xGMI: result records of all ranks
+            if COLL_DEV == "cuda":
+                torch.cuda.synchronize()
         return int(outs["iterations"].sum()), outs
 
     for s in range(args.warmup):
@@ -129,8 +229,6 @@ def run_pnp(engine, ctx, scenes, args, dist, rank, world):
     ctx.enable_timing(True)
     solve_ms = scan_ms = eig_ms = 0.0
     launches = 0
-    barrier(dist)
-    ctx.synchronize()
     t1 = time.perf_counter()
     for s in range(args.steps):
         step(args.warmup + args.steps + s)
@@ -140,23 +238,51 @@ def run_pnp(engine, ctx, scenes, args, dist, rank, world):
         eig_ms += tm["eig_ms"]
         launches += tm["solve_launches"]
     ctx.synchronize()
-    barrier(dist)
     dt_inst = time.perf_counter() - t1
     ctx.enable_timing(False)
     return dict(seconds=dt, seconds_instrumented=dt_inst, hyps=hyps, problems=C * args.steps,
-                solve_ms=solve_ms / max(launches, 1),
-                scan_ms=scan_ms / max(launches, 1), eig_ms=eig_ms / max(launches, 1), launches=launches, last=outs)
+                solve_ms=solve_ms / max(launches, 1), scan_ms=scan_ms / max(launches, 1),
+                eig_ms=eig_ms / max(launches, 1), launches=launches, last=outs)
 
 
-def run_sim3(engine, ctx, rng, args):
-    from rsc import synth
-    pairs = [synth.make_sim3_pair(rng, 1000, 15) for _ in range(32)]
+def cpu_baseline_pnp(scenes, args, threads):
+    """Oracle restatement of the same 64-candidate batch (ora_pnp_run_batch)."""
+    import oracle_lib as ol
+    from rsc import workloads as wl
+    L = ol.lib()
+    C = len(scenes)
+    n = np.array([sc.n for sc in scenes], np.int32)
+    off = np.concatenate([[0], np.cumsum(n)[:-1]]).astype(np.int64)
+    p2d = np.ascontiguousarray(np.concatenate([sc.p2d for sc in scenes]), np.float32)
+    p3d = np.ascontiguousarray(np.concatenate([sc.p3dw for sc in scenes]), np.float32)
+    s2 = np.ascontiguousarray(np.concatenate([sc.sigma2 for sc in scenes]), np.float32)
+    out_i4 = np.zeros(4 * C, np.int32)
+    out_T = np.zeros(16 * C, np.float32)
+    sc0 = scenes[0]
+    seeds = wl.config2_seeds(0, 0, C)
+
+    def batch(nt):
+        L.ora_pnp_run_batch(C, n, off, p2d, p3d, s2, sc0.fx, sc0.fy, sc0.cx, sc0.cy, seeds, *wl.RELOC, args.iters,
+                            nt, out_i4, out_T, None)
+    batch(1)
+    hyps = int(out_i4.reshape(C, 4)[:, 3].sum())
+    return cpu_section(batch, hyps, "hypotheses/s",
+                       f"full batch: {C} candidates x {sc0.n} corrs x iterate({args.iters}) = {hyps} hypotheses",
+                       threads)
+
+
+# ------------------------------------------------------------------------------------------------
+# config 3 / 4
+# ------------------------------------------------------------------------------------------------
+def run_sim3(engine, ctx, pairs, args):
+    from rsc import workloads as wl
     solvers = [engine.Sim3Solver(ctx, p, 1) for p in pairs]
     batch = engine.SolverBatch(solvers)
+    C = len(pairs)
 
     def step(s):
-        batch.reset(1 + np.arange(32) + 32 * s)
-        batch.set_ransac_parameters(*LOOP)
+        batch.reset(wl.step_seeds(s, C))
+        batch.set_ransac_parameters(*wl.LOOP)
         return int(batch.iterate_raw(args.iters)["iterations"].sum())
 
     for s in range(args.warmup):
@@ -169,19 +295,49 @@ def run_sim3(engine, ctx, rng, args):
     ctx.synchronize()
     dt = time.perf_counter() - t0
     return dict(hyp_per_s=h / dt, ms_per_step=1e3 * dt / args.steps, hypotheses_per_step=h // args.steps,
-                pairs=32, correspondences=1000)
+                pairs=C, correspondences=pairs[0].n1, solvers=solvers)
 
 
-def run_mlpnp(engine, ctx, rng, args):
-    """Config 4 on one GPU: 32 candidates x 4096 correspondences, MLPnP SetRansacParameters
-    (0.99,10,300,6,0.5,5.991) (commented call Tracking.cpp:1227-1228), iterate(300), exhaustive."""
+def cpu_baseline_sim3(solvers, args, threads):
+    """The Sim3 oracle on the solvers' prepared arrays (ctor output: camera-frame points, size_t
+    thresholds, projections), SetRansacParameters(0.99,20,300) + iterate(300) per pair."""
+    import oracle_lib as ol
+    from rsc import workloads as wl
+    L = ol.lib()
+    preps = [s.prepared() for s in solvers]
+    C = len(preps)
+    n = np.array([len(p["indices"]) for p in preps], np.int32)
+    off = np.concatenate([[0], np.cumsum(n)[:-1]]).astype(np.int64)
+    cat = lambda k, dt: np.ascontiguousarray(np.concatenate([p[k] for p in preps]), dt)
+    X1, X2, P1, P2 = cat("X1c", np.float32), cat("X2c", np.float32), cat("P1im1", np.float32), cat("P2im2", np.float32)
+    e1, e2 = cat("maxerr1", np.uint64), cat("maxerr2", np.uint64)
     from rsc import synth
-    scenes = [synth.make_pnp_scene(rng, 4096, 0.4) for _ in range(32)]
+    K = np.array([synth.FX, synth.FY, synth.CX, synth.CY], np.float32)
+    seeds = wl.step_seeds(0, C)
+    out_i4 = np.zeros(4 * C, np.int32)
+    out_Rt = np.zeros(12 * C, np.float32)
+
+    def batch(nt):
+        L.ora_sim3_run_prepared_batch(C, n, off, X1, X2, P1, P2, e1, e2, K, K, seeds, *wl.LOOP, args.iters, nt,
+                                      out_i4, out_Rt)
+    batch(1)
+    hyps = int(out_i4.reshape(C, 4)[:, 3].sum())
+    return cpu_section(batch, hyps, "hypotheses/s",
+                       f"full batch: {C} pairs x {int(n.mean())} matches x iterate({args.iters}) = {hyps} hypotheses",
+                       threads)
+
+
+def run_mlpnp(engine, ctx, scenes, args):
+    """Config 4 on one GPU: 32 candidates x 4096 correspondences (128 over 4 GPUs), MLPnP
+    SetRansacParameters(0.99,10,300,6,0.5,5.991) (commented call Tracking.cpp:1227-1228),
+    iterate(300), exhaustive."""
+    from rsc import workloads as wl
     batch = engine.SolverBatch([engine.MLPnPSolver(ctx, sc, 1) for sc in scenes])
+    C = len(scenes)
 
     def step(s):
-        batch.reset(1 + np.arange(32) + 32 * s)
-        batch.set_ransac_parameters(0.99, 10, 300, 6, 0.5, 5.991)
+        batch.reset(wl.step_seeds(s, C))
+        batch.set_ransac_parameters(*wl.MLPNP)
         return int(batch.iterate_raw(args.iters)["iterations"].sum())
 
     for s in range(args.warmup):
@@ -194,8 +350,55 @@ def run_mlpnp(engine, ctx, rng, args):
         h += step(args.warmup + s)
     ctx.synchronize()
     dt = time.perf_counter() - t0
-    return dict(hyp_per_s=h / dt, ms_per_step=1e3 * dt / steps, hypotheses_per_step=h // steps, candidates=32,
-                correspondences=4096, steps=steps)
+    return dict(hyp_per_s=h / dt, ms_per_step=1e3 * dt / steps, hypotheses_per_step=h // steps, candidates=C,
+                correspondences=scenes[0].n, steps=steps)
+
+
+def cpu_baseline_mlpnp(scenes, args, threads, sample_cands=4):
+    """The MLPnP oracle on a bounded sample: the first `sample_cands` candidates of the batch per
+    CPU batch (the full 32 x 4096 x 300 batch is ~1 s per core-batch)."""
+    import oracle_lib as ol
+    from rsc import workloads as wl
+    L = ol.lib()
+    sub = scenes[:sample_cands]
+    C = len(sub)
+    n = np.array([sc.n for sc in sub], np.int32)
+    off = np.concatenate([[0], np.cumsum(n)[:-1]]).astype(np.int64)
+    p2d = np.ascontiguousarray(np.concatenate([sc.p2d for sc in sub]), np.float32)
+    p3d = np.ascontiguousarray(np.concatenate([sc.p3dw for sc in sub]), np.float32)
+    s2 = np.ascontiguousarray(np.concatenate([sc.sigma2 for sc in sub]), np.float32)
+    seeds = wl.step_seeds(0, C)
+    out_i4 = np.zeros(4 * C, np.int32)
+    out_T = np.zeros(16 * C, np.float32)
+    sc0 = sub[0]
+
+    def batch(nt):
+        L.ora_mlpnp_run_batch(C, n, off, p2d, p3d, s2, sc0.fx, sc0.fy, sc0.cx, sc0.cy, seeds, *wl.MLPNP,
+                              args.iters, nt, out_i4, out_T)
+    batch(1)
+    hyps = int(out_i4.reshape(C, 4)[:, 3].sum())
+    return cpu_section(batch, hyps, "hypotheses/s",
+                       f"bounded sample: {C} of the {len(scenes)} candidates x {sc0.n} corrs x iterate({args.iters}) "
+                       f"= {hyps} hypotheses per batch", min(threads, C))
+
+
+# ------------------------------------------------------------------------------------------------
+# config 5 (event stream) and single-event latency
+# ------------------------------------------------------------------------------------------------
+def build_event_drivers(engine, ctx, evs, ids):
+    from rsc import events as rev
+    groups = {"reloc": [], "loop": []}
+    for i in ids:
+        ev = evs[i]
+        cls = engine.PnPSolver if ev.kind == "reloc" else engine.Sim3Solver
+        groups[ev.kind].append((ev, [cls(ctx, x, s) for x, s in zip(rev.event_inputs(ev), ev.seeds)]))
+    drivers = []
+    for kind, params in (("reloc", rev.RELOC_PARAMS), ("loop", rev.LOOP_PARAMS)):
+        if groups[kind]:
+            eb = engine.EventBatch([g[1] for g in groups[kind]])
+            seeds = np.array([s for ev, _ in groups[kind] for s in ev.seeds], np.uint32)
+            drivers.append((eb, params, seeds, [ev.eid for ev, _ in groups[kind]]))
+    return drivers
 
 
 def run_events(engine, ctx, args, dist, rank, world):
@@ -206,19 +409,9 @@ def run_events(engine, ctx, args, dist, rank, world):
     A step = reset + SetRansacParameters of every candidate + both drivers + the all-gather."""
     from rsc import events as rev
     evs = rev.make_event_stream()
-    mine = rev.shard_events([ev.cost for ev in evs], world)[rank]
-    groups = {"reloc": [], "loop": []}
-    for i in mine:
-        ev = evs[i]
-        cls = engine.PnPSolver if ev.kind == "reloc" else engine.Sim3Solver
-        groups[ev.kind].append((ev, [cls(ctx, x, s) for x, s in zip(rev.event_inputs(ev), ev.seeds)]))
-    drivers = []
-    for kind, params in (("reloc", rev.RELOC_PARAMS), ("loop", rev.LOOP_PARAMS)):
-        if groups[kind]:
-            eb = engine.EventBatch([g[1] for g in groups[kind]])
-            seeds = np.array([s for ev, _ in groups[kind] for s in ev.seeds], np.uint32)
-            drivers.append((eb, params, seeds, [ev.eid for ev, _ in groups[kind]]))
-    max_per_rank = max(len(p) for p in rev.shard_events([ev.cost for ev in evs], world))
+    shards = rev.shard_events([ev.cost for ev in evs], world)
+    drivers = build_event_drivers(engine, ctx, evs, shards[rank])
+    max_per_rank = max(len(p) for p in shards)
 
     def step():
         recs, hyps = [], 0
@@ -230,7 +423,7 @@ def run_events(engine, ctx, args, dist, rank, world):
             recs.append(rev.pack_events(eids, eb.per_event, eb.winner_poses()))
         rec = np.concatenate(recs) if recs else np.zeros((0, rev.EVENT_RECORD), np.float32)
         if dist is not None:
-            rec = rev.all_gather_events(dist, rec, max_per_rank, device="cuda")
+            rec = rev.all_gather_events(dist, rec, max_per_rank, device=COLL_DEV)
         return hyps, rec
 
     for _ in range(args.warmup):
@@ -245,19 +438,82 @@ def run_events(engine, ctx, args, dist, rank, world):
     ctx.synchronize()
     barrier(dist)
     dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt, float(hyps)], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        dt, hyps = float(t[0]), int(t[1])
+    dt, hyps = reduce_time_and_count(dist, dt, hyps)
     n_ev = len(evs) * args.steps
     return dict(events_per_s=n_ev / dt, ms_per_stream=1e3 * dt / args.steps, hyp_per_s=hyps / dt,
                 events=len(evs), candidates=sum(len(ev.sizes) for ev in evs),
                 resolved=int((rec[:, 1] >= 0).sum()),
-                sharding=f"{world} rank(s), LPT by N*300, RCCL all-gather of {rev.EVENT_RECORD}-float records")
+                sharding=f"{world} rank(s), LPT by N*300, RCCL all-gather of {rev.EVENT_RECORD}-float records"), evs
 
 
+def cpu_baseline_events(evs, threads):
+    """The reference-order event replay of the oracle (ora_reloc/loop_events_batch: per event, the
+    solvers are built from the raw inputs, then iterate(5) rounds until a pose) over the whole stream."""
+    import events_oracle as eo
+    packs = [eo.PackedEvents([ev for ev in evs if ev.kind == k]) for k in ("reloc", "loop")]
+
+    def batch(nt):
+        for p in packs:
+            p.run(nt)
+    return cpu_section(batch, len(evs), "events/s",
+                       f"the whole {len(evs)}-event stream per batch", threads, warmup=1, reps=10)
+
+
+def latency_event(kind: str, seed: int = 4242):
+    """One relocalization event as Tracking::Relocalization sees it (SURVEY H6): C = 15 candidates,
+    N ~ U[300, 900] (mean ~600), candidate quality as the config-5 stream; or one loop event, C = 3
+    pairs x N ~ U[200, 600]."""
+    from rsc import events as rev
+    rng = np.random.default_rng(seed)
+    if kind == "reloc":
+        C = 15
+        sizes = [int(x) for x in rng.integers(300, 901, size=C)]
+        ratios = [float(x) for x in rng.choice([0.05, 0.2, 0.6, 0.8], size=C, p=[0.5, 0.2, 0.15, 0.15])]
+        return rev.Event("reloc", 100000, sizes, ratios, [7 + c for c in range(C)])
+    C = 3
+    sizes = [int(x) for x in rng.integers(200, 601, size=C)]
+    ratios = [float(x) for x in rng.choice([0.02, 0.1, 0.3, 0.6], size=C)]
+    return rev.Event("loop", 100001, sizes, ratios, [9 + c for c in range(C)])
+
+
+def run_latency(engine, ctx, args, with_cpu, reps=50):
+    """Single-event latency: ONE rsc_reloc_events / rsc_loop_events call on one event (reset +
+    SetRansacParameters + the iterate(5) round-robin, result on the host), median over reps calls;
+    CPU: the oracle replay of the same event on one core."""
+    from rsc import events as rev
+    import events_oracle as eo
+    out = {}
+    for kind in ("reloc", "loop"):
+        ev = latency_event(kind)
+        (eb, params, seeds, _), = build_event_drivers(engine, ctx, [ev], [0])
+        times = []
+        for r in range(reps + 5):
+            t0 = time.perf_counter()
+            eb.batch.reset(seeds)
+            eb.batch.set_ransac_parameters(*params)
+            res = eb.run()
+            t = time.perf_counter() - t0
+            if r >= 5:
+                times.append(t)
+        pe = res[0]
+        sec = dict(candidates=len(ev.sizes), mean_corrs=float(np.mean(ev.sizes)), winner=int(pe["winner"]),
+                   round=int(pe["round"]), hypotheses=int(eb.cand["iterations"].sum()),
+                   gpu_ms=round(1e3 * float(np.median(times)), 4), reps=reps)
+        if with_cpu:
+            pk = eo.PackedEvents([ev])
+            med, n = median_batches(lambda: pk.run(1), warmup=3, reps=20)
+            assert np.array_equal(pk.records()[0, 1:5], [pe["winner"], pe["round"], pe["hypothesis"], pe["n_inliers"]])
+            sec["cpu_ms_1core"] = round(1e3 * med, 4)
+            sec["cpu_baseline"] = dict(value=round(1e3 * med, 4), unit="ms/event", cores=1, kind="port",
+                                       sample=f"the same event, 3 warm-up + median of {n}, oracle replay, 1 thread")
+            sec["speedup_vs_cpu_1core"] = round(med / float(np.median(times)), 2)
+        out[kind] = sec
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# SURVEY §8(f) neighbours
+# ------------------------------------------------------------------------------------------------
 def poseopt_frames(rng, F=64, N=2000, ratio=0.8):
     from rsc import synth
     return [synth.make_poseopt_frame(rng, N, ratio) for _ in range(F)]
@@ -528,103 +784,150 @@ def cpu_baseline_poseopt(frames, seconds):
                 sample=f"{done // F} batches of {F} Frames x {f0.n} edges in {dt:.1f} s, oracle restatement, 1 thread")
 
 
-def cpu_baseline(scenes, args):
-    """Oracle restatement (test infrastructure) of the same workload on ONE host core."""
-    import oracle_lib as ol
-    L = ol.lib()
-    C = len(scenes)
-    n = np.array([sc.n for sc in scenes], np.int32)
-    off = np.concatenate([[0], np.cumsum(n)[:-1]]).astype(np.int64)
-    p2d = np.ascontiguousarray(np.concatenate([sc.p2d for sc in scenes]), np.float32)
-    p3d = np.ascontiguousarray(np.concatenate([sc.p3dw for sc in scenes]), np.float32)
-    s2 = np.ascontiguousarray(np.concatenate([sc.sigma2 for sc in scenes]), np.float32)
-    out_i4 = np.zeros(4 * C, np.int32)
-    out_T = np.zeros(16 * C, np.float32)
-    sc0 = scenes[0]
-    hyps = 0
-    batches = 0
-    t0 = time.perf_counter()
-    while True:
-        seeds = (1 + np.arange(C) + C * batches).astype(np.uint32)
-        L.ora_pnp_run_batch(C, n, off, p2d, p3d, s2, sc0.fx, sc0.fy, sc0.cx, sc0.cy, seeds, *RELOC, args.iters,
-                            1, out_i4, out_T, None)
-        hyps += int(out_i4.reshape(C, 4)[:, 3].sum())
-        batches += 1
-        if time.perf_counter() - t0 >= args.cpu_seconds:
-            break
-    dt = time.perf_counter() - t0
-    return dict(value=hyps / dt, unit="hypotheses/s", cores=1, kind="port",
-                sample=f"{batches} full batches ({C} candidates x {sc0.n} corrs x iterate({args.iters})) "
-                       f"= {hyps} hypotheses in {dt:.1f} s, oracle restatement, 1 thread")
+def _rounded(d, nd=4):
+    return {k: (round(v, nd) if isinstance(v, float) else v) for k, v in d.items()}
+
+
+# ------------------------------------------------------------------------------------------------
+# main
+# ------------------------------------------------------------------------------------------------
+def headline_roofline(args, r):
+    """the EPnP launch set is bound by FP64 dependency latency (not HBM, not
+    MFMA): roofline = the algorithmic FP64 work of the solve kernels (S_h flops per hypothesis from
+    the op-counter build of the oracle, profiles/r02/opcount.json) / their HIP-event time, against
+    the FP64 vector peak; measured HBM traffic (PMC) and the effective scan bandwidth beside it."""
+    per_launch_hyps = r["per_launch_hyps"]
+    eig_ms, solve_ms, scan_ms = r["eig_ms"], r["solve_ms"], r["scan_ms"]
+    set_ms = solve_ms + scan_ms
+    B_h = 24 * args.corrs  # SURVEY.md §8(d): PnP scan bytes per hypothesis (p3D 12 + p2D 8 + maxErr 4)
+    scan_bytes = per_launch_hyps * B_h
+    opc = _profile_json("opcount.json")
+    traffic = _profile_json("pmc_traffic.json")
+    S_h = opc["fp64_flops_mean"] if opc else None
+    tf = per_launch_hyps * S_h / (solve_ms * 1e-3) / 1e12 if (S_h and solve_ms > 0) else None
+    meas = traffic["epnp_launch_set_bytes"] if traffic else None
+    roof = {"bound": "fp64-latency",
+            "achieved": round(tf, 4) if tf else None, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP64_PEAK_TFLOPS, 5) if tf else None,
+            "traffic": round(meas) if meas else None,
+            "kernel": "EPnP hypothesis solve: pnp_eig_quad_kernel<4> + pnp_betas_kernel<4> "
+                      f"({per_launch_hyps} hypotheses per launch)",
+            "algorithmic_flops_per_launch": round(per_launch_hyps * S_h) if S_h else None,
+            "S_h_fp64_flops_per_hypothesis": S_h,
+            "ms_per_launch": {"eig": round(eig_ms, 4), "betas": round(solve_ms - eig_ms, 4),
+                              "scan": round(scan_ms, 4), "solve": round(solve_ms, 4), "set": round(set_ms, 4)},
+            "launches": r["launches"],
+            "hbm": {"measured_bytes_per_launch_set": round(meas) if meas else None,
+                    "achieved_GBs": round(meas / (set_ms * 1e-3) / 1e9, 2) if (meas and set_ms) else None,
+                    "frac": round(meas / (set_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if (meas and set_ms) else None,
+                    "peak_GBs": HBM_PEAK_GBS},
+            "effective_scan_bw_frac": round(scan_bytes / (set_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if set_ms else None,
+            "scan_algorithmic_bytes_per_launch": scan_bytes,
+            "timing": "HIP events on the context stream, second pass of the same K steps "
+                      f"({1e3 * r['seconds_instrumented'] / args.steps:.4f} ms/step with events)",
+            "sources": {"S_h": PROFILE_DIR + "/opcount.json (tools/opcount.cpp)",
+                        "traffic": (PROFILE_DIR + "/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE, commit "
+                                    f"{traffic.get('commit')})") if traffic else None}}
+    return roof
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world, rank, local, dist = dist_setup(args)
     from rsc import engine
+    from rsc import dist as rdist
+    from rsc import workloads as wl
     ctx = engine.Context(local)
-    rng = np.random.default_rng(20240 + rank)
-    scenes = pnp_batch(rng, args.candidates, args.corrs, 0.4)
-    r = run_pnp(engine, ctx, scenes, args, dist, rank, world)
-    # max over ranks of the timed region
-    dt = r["seconds"]
-    hyps_total = r["hyps"]
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt, float(r["hyps"])], dtype=torch.float64, device="cuda")
-        mx = t.clone()
-        dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        dt = float(mx[0])
-        hyps_total = int(t[1])
-    events = None if args.no_events else run_events(engine, ctx, args, dist, rank, world)
-    sim3 = mlpnp = None
-    if rank == 0 and not args.no_sim3:
-        sim3 = run_sim3(engine, ctx, np.random.default_rng(77), args)
-    if rank == 0 and not args.no_mlpnp:
-        mlpnp = run_mlpnp(engine, ctx, np.random.default_rng(78), args)
-    poseopt = po_frames = None
-    if rank == 0 and not args.no_poseopt:
-        po_frames = poseopt_frames(np.random.default_rng(79))
-        poseopt = run_poseopt(engine, ctx, po_frames, args)
-    s3m = s3m_probs = None
-    if rank == 0 and not args.no_sim3match:
-        from rsc import synth
-        r3 = np.random.default_rng(81)
-        s3m_probs = [synth.make_sim3match_pair(r3, 1000, 250, 0.3) for _ in range(32)]
-        s3m = run_sim3match(engine, ctx, s3m_probs, args)
-    kfdb = kfdb_sc = kfdb_q = None
-    if rank == 0 and not args.no_kfdb:
-        kfdb_sc, kfdb_q = kfdb_scene()
-        kfdb = run_kfdb(engine, ctx, kfdb_sc, kfdb_q, args)
-    bow = bow_F = bow_K = None
-    if rank == 0 and not args.no_bow:
-        bow_F, bow_K = bow_views(np.random.default_rng(80))
-        bow = run_bow(engine, ctx, bow_F, bow_K, args)
+    if args.strong:
+        all_scenes = wl.config2_scenes(0, args.candidates, args.corrs)
+        lo, hi = rdist.shard_range(args.candidates, world, rank, [sc.n * args.iters for sc in all_scenes])
+        cand_ids = np.arange(lo, hi)
+        scenes = all_scenes[lo:hi]
+    else:
+        scenes = wl.config2_scenes(rank, args.candidates, args.corrs)
+        cand_ids = np.arange(args.candidates)
+    r = run_pnp(engine, ctx, scenes, cand_ids, args, dist, rank, world)
+    r["per_launch_hyps"] = len(scenes) * args.iters
+    dt, hyps_total = reduce_time_and_count(dist, r["seconds"], r["hyps"])
+    _, problems_total = reduce_time_and_count(dist, r["seconds"], r["problems"])
+    events = evs = None
+    if not args.no_events:
+        events, evs = run_events(engine, ctx, args, dist, rank, world)
+    sections = {}
+    threads = cpu_threads(args)
+    with_cpu = (not args.no_cpu) and world == 1
+    if rank == 0:
+        if not args.no_sim3:
+            s3 = run_sim3(engine, ctx, wl.config3_pairs(), args)
+            solvers = s3.pop("solvers")
+            sections["sim3"] = _rounded(s3, 3)
+            if with_cpu:
+                cb = cpu_baseline_sim3(solvers, args, threads)
+                sections["sim3"]["cpu_baseline"] = cb
+                sections["sim3"]["speedup_vs_cpu_1core"] = round(s3["hyp_per_s"] / cb["value"], 1)
+        if not args.no_mlpnp:
+            sc4 = wl.config4_scenes()
+            m = run_mlpnp(engine, ctx, sc4, args)
+            sections["mlpnp"] = _rounded(m, 3)
+            if with_cpu:
+                cb = cpu_baseline_mlpnp(sc4, args, threads)
+                sections["mlpnp"]["cpu_baseline"] = cb
+                sections["mlpnp"]["speedup_vs_cpu_1core"] = round(m["hyp_per_s"] / cb["value"], 1)
+        if events is not None:
+            sections["events"] = _rounded(events, 3)
+            if with_cpu:
+                cb = cpu_baseline_events(evs, threads)
+                sections["events"]["cpu_baseline"] = cb
+                sections["events"]["speedup_vs_cpu_1core"] = round(events["events_per_s"] / cb["value"], 1)
+        if not args.no_latency:
+            sections["single_event_latency"] = run_latency(engine, ctx, args, with_cpu)
+        if not args.no_poseopt:
+            po_frames = poseopt_frames(np.random.default_rng(79))
+            po = run_poseopt(engine, ctx, po_frames, args)
+            sections["poseopt"] = _rounded(po)
+            if with_cpu:
+                cb = cpu_baseline_poseopt(po_frames, 3.0)
+                sections["poseopt"]["cpu_baseline"] = cb
+                sections["poseopt"]["speedup_vs_cpu_1core"] = round(po["poses_per_s"] / cb["value"], 1)
+        if not args.no_sim3match:
+            from rsc import synth
+            r3 = np.random.default_rng(81)
+            s3m_probs = [synth.make_sim3match_pair(r3, 1000, 250, 0.3) for _ in range(32)]
+            s3m = run_sim3match(engine, ctx, s3m_probs, args)
+            sections["search_by_sim3"] = _rounded(s3m, 5)
+            if with_cpu:
+                cb = cpu_baseline_sim3match(s3m_probs, 2.0)
+                sections["search_by_sim3"]["cpu_baseline"] = cb
+                sections["search_by_sim3"]["speedup_vs_cpu_1core"] = round(s3m["pairs_per_s"] / cb["value"], 1)
+        if not args.no_kfdb:
+            kfdb_sc, kfdb_q = kfdb_scene()
+            kf = run_kfdb(engine, ctx, kfdb_sc, kfdb_q, args)
+            sections["kfdb_relocalization"] = _rounded(kf, 5)
+            if with_cpu:
+                cb = cpu_baseline_kfdb(kfdb_sc, kfdb_q, 2.0)
+                sections["kfdb_relocalization"]["cpu_baseline"] = cb
+                sections["kfdb_relocalization"]["speedup_vs_cpu_1core"] = round(kf["queries_per_s"] / cb["value"], 1)
+        if not args.no_bow:
+            bow_F, bow_K = bow_views(np.random.default_rng(80))
+            bw = run_bow(engine, ctx, bow_F, bow_K, args)
+            sections["search_by_bow"] = _rounded(bw, 5)
+            if with_cpu:
+                cb = cpu_baseline_bow(bow_F, bow_K, 3.0)
+                sections["search_by_bow"]["cpu_baseline"] = cb
+                sections["search_by_bow"]["speedup_vs_cpu_1core"] = round(bw["pairs_per_s"] / cb["value"], 1)
     if rank != 0:
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()
         return
     value = hyps_total / dt
-    per_launch_hyps = args.candidates * args.iters
-    B_h = 24 * args.corrs  # SURVEY.md §8(d): PnP scan bytes per hypothesis (p3D 12 + p2D 8 + maxErr 4)
-    algo_bytes = per_launch_hyps * B_h
-    eig_ms, solve_ms, scan_ms = r["eig_ms"], r["solve_ms"], r["scan_ms"]
-    set_ms = solve_ms + scan_ms
-    achieved = algo_bytes / (set_ms * 1e-3) / 1e9 if set_ms > 0 else 0.0
-    opc = _profile_json("opcount.json")
-    traffic = _profile_json("pmc_traffic.json")
-    S_h = opc["fp64_flops_mean"] if opc else None
-    fp64 = None
-    if S_h and solve_ms > 0:
-        tf = per_launch_hyps * S_h / (solve_ms * 1e-3) / 1e12
-        fp64 = {"kernel": "pnp_eig_quad_kernel<4> + pnp_betas_kernel<4> (hypothesis solve)",
-                "achieved": round(tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(tf / FP64_PEAK_TFLOPS, 5), "S_h_fp64_flops_per_hypothesis": S_h,
-                "S_h_source": "tools/opcount.cpp (op-counter build of the oracle EPnP), " + PROFILE_DIR}
+    par = (f"{'strong' if args.strong else 'weak'}: candidates sharded over {world} rank(s) "
+           f"({'64 total' if args.strong else f'{args.candidates} per GPU'}), RCCL all-gather of "
+           f"{rdist.RECORD}-float result records per step")
     out = {
-        "metric": "RANSAC hypotheses/sec (EPnP relocalization batch, 2k corrs x 64 candidates per GPU)",
+        "metric": "RANSAC hypotheses/sec (EPnP relocalization batch, 2k corrs x 64 candidates)",
         "value": round(value, 1),
         "unit": "hypotheses/s",
         "n_gpus": world,
@@ -632,65 +935,33 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * dt / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded EuRoC-shaped scenes; no dataset)",
-        "config": {"workload": "reloc_pnp: candidates x correspondences, iterate(300), exhaustive (40% inliers)",
-                   "candidates_per_gpu": args.candidates, "correspondences": args.corrs,
+        "config": {"workload": "config 2 reloc_pnp: candidates x correspondences, iterate(300), exhaustive "
+                               "(40% inliers)",
+                   "candidates": args.candidates if args.strong else args.candidates * world,
+                   "candidates_per_gpu": len(scenes), "correspondences": args.corrs,
                    "hypotheses_per_candidate": args.iters, "params": "SetRansacParameters(0.99,10,300,4,0.5,5.991)",
-                   "parallelism": f"candidates sharded, {world} rank(s), RCCL all-gather of result records"},
-        "poses_per_s": round(world * r["problems"] / dt, 2),
-        # achieved = effective scan bandwidth of one EPnP launch set
-        # (C*H hypotheses x B_h algorithmic bytes) / (HIP-event time of eig + betas + scan kernels).
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5),
-                     "traffic": round(traffic["epnp_launch_set_bytes"]) if traffic else None,
-                     "kernel": "EPnP launch set: pnp_eig_quad_kernel<4> + pnp_betas_kernel<4> + pnp_scan_kernel<8>",
-                     "ms_per_launch": {"eig": round(eig_ms, 4), "betas": round(solve_ms - eig_ms, 4),
-                                       "scan": round(scan_ms, 4), "set": round(set_ms, 4)},
-                     "launches": r["launches"], "algorithmic_bytes_per_launch": algo_bytes,
-                     "timing": "HIP events on the context stream, second pass of the same K steps "
-                               f"({1e3 * r['seconds_instrumented'] / args.steps:.4f} ms/step with events)",
-                     "traffic_source": (PROFILE_DIR + "/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE)")
-                     if traffic else None},
+                   "parallelism": par},
+        "poses_per_s": round(problems_total / dt, 2),
+        "roofline": headline_roofline(args, r),
     }
-    if fp64 is not None:
-        out["roofline_fp64"] = fp64
-    if sim3 is not None:
-        out["sim3"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in sim3.items()}
-    if events is not None:
-        out["events"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in events.items()}
-    if mlpnp is not None:
-        out["mlpnp"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in mlpnp.items()}
-    if poseopt is not None:
-        out["poseopt"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in poseopt.items()}
-        if not args.no_cpu and world == 1:
-            cb = cpu_baseline_poseopt(po_frames, min(3.0, args.cpu_seconds))
-            out["poseopt"]["cpu_baseline"] = cb
-            out["poseopt"]["speedup_vs_cpu_1core"] = round(poseopt["poses_per_s"] / cb["value"], 1)
-    if bow is not None:
-        out["search_by_bow"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in bow.items()}
-        if not args.no_cpu and world == 1:
-            cb = cpu_baseline_bow(bow_F, bow_K, min(3.0, args.cpu_seconds))
-            out["search_by_bow"]["cpu_baseline"] = cb
-            out["search_by_bow"]["speedup_vs_cpu_1core"] = round(bow["pairs_per_s"] / cb["value"], 1)
-    if s3m is not None:
-        out["search_by_sim3"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in s3m.items()}
-        if not args.no_cpu and world == 1:
-            cb = cpu_baseline_sim3match(s3m_probs, min(2.0, args.cpu_seconds))
-            out["search_by_sim3"]["cpu_baseline"] = cb
-            out["search_by_sim3"]["speedup_vs_cpu_1core"] = round(s3m["pairs_per_s"] / cb["value"], 1)
-    if kfdb is not None:
-        out["kfdb_relocalization"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in kfdb.items()}
-        if not args.no_cpu and world == 1:
-            cb = cpu_baseline_kfdb(kfdb_sc, kfdb_q, min(2.0, args.cpu_seconds))
-            out["kfdb_relocalization"]["cpu_baseline"] = cb
-            out["kfdb_relocalization"]["speedup_vs_cpu_1core"] = round(kfdb["queries_per_s"] / cb["value"], 1)
-    if not args.no_cpu and world == 1:
-        out["cpu_baseline"] = cpu_baseline(scenes, args)
-        out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 1)
-        out["speedup_vs_cpu_1core"] = round(value / out["cpu_baseline"]["value"], 1)
+    if with_cpu:
+        cb = cpu_baseline_pnp(scenes, args, threads)
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu_1core"] = round(value / cb["value"], 1)
+        if "all_cores" in cb:
+            out["speedup_vs_cpu_all_cores"] = round(value / cb["all_cores"]["value"], 1)
+        if "sim3" in sections and "cpu_baseline" in sections["sim3"]:
+            # north_star: ">= 10x the reference CPU PnP+Sim3 RANSAC throughput" — the combined figure
+            g = value + sections["sim3"]["hyp_per_s"]
+            c = cb["value"] + sections["sim3"]["cpu_baseline"]["value"]
+            out["pnp_plus_sim3"] = {"gpu_hyp_per_s": round(g, 1), "cpu_1core_hyp_per_s": round(c, 1),
+                                    "speedup_vs_cpu_1core": round(g / c, 1),
+                                    "note": "sum of the config-2 and config-3 rates (same unit, each on its own batch)"}
+    out.update(sections)
     print(json.dumps(out))
     if dist is not None:
         dist.barrier()

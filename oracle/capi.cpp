@@ -6,6 +6,7 @@
 #include <thread>
 #include <vector>
 #include <atomic>
+#include <memory>
 #include "glibc_rand.h"
 #include "pnp_oracle.h"
 #include "sim3_oracle.h"
@@ -417,6 +418,120 @@ void ora_mlpnp_run_batch(int C, const int32_t* n, const int64_t* off, const floa
         for (int i = 0; i < nthreads; ++i) th.emplace_back(worker);
         for (auto& t : th) t.join();
     }
+}
+
+// ---- Config-5 event stream (CPU baseline and reference-order replay) -------------------------------
+// Tracking::Relocalization (Tracking.cpp:1225-1262) / LoopClosing::ComputeSim3 (LoopClosing.cpp:258-286):
+// every candidate of an event gets its solver (params set once), then rounds of iterate(5) over the
+// candidates not yet discarded; a candidate whose call returns bNoMore is discarded; the event ends at the
+// first candidate (in order) whose call returns a pose.  Event e = candidates [ev_begin[e], ev_begin[e+1]);
+// candidate c = rows [off[c], off[c] + n[c]) of the packed arrays.  Per event: out_rec[4] = winner
+// (index within the event, -1 if none), round, hypothesis (iterations - 1 of the winner), n_inliers;
+// out_T[16] = the winner's Tcw (PnP) or [R12 | t12; 0 0 0 1] (Sim3).  Events run on `nthreads` threads.
+}  // extern "C"
+
+template <typename Solver, typename Make, typename Call>
+static void run_events_generic(int n_events, const int32_t* ev_begin, int nthreads, int32_t* out_rec, float* out_T,
+                               Make make, Call call) {
+    std::atomic<int> next(0);
+    auto worker = [&]() {
+        for (;;) {
+            const int e = next.fetch_add(1);
+            if (e >= n_events) break;
+            const int c0 = ev_begin[e], nc = ev_begin[e + 1] - ev_begin[e];
+            std::vector<std::unique_ptr<Solver>> sv;
+            for (int i = 0; i < nc; ++i) sv.emplace_back(make(c0 + i));
+            std::vector<int> active(nc);
+            for (int i = 0; i < nc; ++i) active[i] = i;
+            int32_t* rec = out_rec + 4 * e;
+            float* T = out_T + 16 * e;
+            rec[0] = rec[1] = rec[2] = -1;
+            rec[3] = 0;
+            std::memset(T, 0, 64);
+            bool done = false;
+            for (int rnd = 0; !active.empty() && !done; ++rnd) {
+                std::vector<int> keep;
+                for (int i : active) {
+                    bool nm = false;
+                    int ni = 0;
+                    if (call(*sv[i], nm, ni, T)) {
+                        rec[0] = i; rec[1] = rnd; rec[2] = sv[i]->iterations() - 1; rec[3] = ni;
+                        done = true;
+                        break;
+                    }
+                    if (!nm) keep.push_back(i);
+                }
+                active.swap(keep);
+            }
+        }
+    };
+    if (nthreads <= 1) {
+        worker();
+    } else {
+        std::vector<std::thread> th;
+        for (int i = 0; i < nthreads; ++i) th.emplace_back(worker);
+        for (auto& t : th) t.join();
+    }
+}
+
+extern "C" {
+
+void ora_reloc_events_batch(int n_events, const int32_t* ev_begin, const int32_t* n, const int64_t* off,
+                            const float* p2d, const float* p3dw, const float* sigma2, float fx, float fy, float cx,
+                            float cy, const uint32_t* seeds, double prob, int min_inliers, int max_its, int min_set,
+                            float eps, float th2, int nthreads, int32_t* out_rec, float* out_T) {
+    run_events_generic<PnPOracle>(
+        n_events, ev_begin, nthreads, out_rec, out_T,
+        [&](int c) {
+            std::vector<int32_t> kp(n[c]);
+            for (int i = 0; i < n[c]; ++i) kp[i] = i;
+            const int64_t o = off[c];
+            auto* s = new PnPOracle(n[c], n[c], p2d + 2 * o, p3dw + 3 * o, sigma2 + o, kp.data(), fx, fy, cx, cy,
+                                    seeds[c]);
+            s->SetRansacParameters(prob, min_inliers, max_its, min_set, eps, th2);
+            return s;
+        },
+        [&](PnPOracle& s, bool& nm, int& ni, float* T) {
+            std::vector<uint8_t> v;
+            return s.iterate(5, nm, v, ni, T);
+        });
+}
+
+// Loop events on the raw KeyFrame-pair inputs (Sim3Solver.cpp:6-85 constructor included, as the
+// reference builds the solvers inside ComputeSim3).  Per candidate: poses[32] = R1 9, t1 3, R2 9, t2 3,
+// K1 4, K2 4.
+void ora_loop_events_batch(int n_events, const int32_t* ev_begin, const int32_t* n1, const int64_t* off,
+                           const uint8_t* valid, const float* Xw1, const float* Xw2, const float* s1, const float* s2,
+                           const float* poses, const uint32_t* seeds, double prob, int min_inliers, int max_its,
+                           int nthreads, int32_t* out_rec, float* out_T) {
+    run_events_generic<Sim3Oracle>(
+        n_events, ev_begin, nthreads, out_rec, out_T,
+        [&](int c) {
+            const int64_t o = off[c];
+            const float* P = poses + 32 * (size_t)c;
+            Sim3Input in;
+            in.n1 = n1[c]; in.valid = valid + o; in.Xw1 = Xw1 + 3 * o; in.Xw2 = Xw2 + 3 * o;
+            in.sigma2_1 = s1 + o; in.sigma2_2 = s2 + o;
+            std::memcpy(in.R1, P, 36); std::memcpy(in.t1, P + 9, 12);
+            std::memcpy(in.R2, P + 12, 36); std::memcpy(in.t2, P + 21, 12);
+            std::memcpy(in.K1, P + 24, 16); std::memcpy(in.K2, P + 28, 16);
+            auto* s = new Sim3Oracle(in, seeds[c]);
+            s->SetRansacParameters(prob, min_inliers, max_its);
+            return s;
+        },
+        [&](Sim3Oracle& s, bool& nm, int& ni, float* T) {
+            std::vector<uint8_t> v;
+            if (!s.iterate(5, nm, v, ni)) return false;
+            float R[9], t[3];
+            s.GetEstimatedRotation(R);
+            s.GetEstimatedTranslation(t);
+            for (int r = 0; r < 3; ++r) {
+                for (int k = 0; k < 3; ++k) T[4 * r + k] = R[3 * r + k];
+                T[4 * r + 3] = t[r];
+            }
+            T[15] = 1.f;
+            return true;
+        });
 }
 
 // deterministic libm (csrc/rsc_math.h) for the accuracy tests

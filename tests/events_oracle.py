@@ -41,3 +41,56 @@ def run_events(evs):
         recs.append(r)
         poses.append(p)
     return rev.pack_events([ev.eid for ev in evs], recs, poses)
+
+
+class PackedEvents:
+    """The inputs of a list of same-kind events packed once for the oracle's C event runners
+    (ora_reloc_events_batch / ora_loop_events_batch): the CPU baseline of config 5 and a second,
+    C-level replay of the reference order."""
+
+    def __init__(self, evs, inputs=None):
+        assert len({ev.kind for ev in evs}) == 1
+        self.kind = evs[0].kind
+        self.eids = [ev.eid for ev in evs]
+        inputs = inputs if inputs is not None else [rev.event_inputs(ev) for ev in evs]
+        flat = [x for xs in inputs for x in xs]
+        self.ev_begin = np.concatenate([[0], np.cumsum([len(ev.sizes) for ev in evs])]).astype(np.int32)
+        self.seeds = np.array([s for ev in evs for s in ev.seeds], np.uint32)
+        if self.kind == "reloc":
+            self.n = np.array([sc.n for sc in flat], np.int32)
+            self.p2d = np.ascontiguousarray(np.concatenate([sc.p2d for sc in flat]), np.float32)
+            self.p3d = np.ascontiguousarray(np.concatenate([sc.p3dw for sc in flat]), np.float32)
+            self.s2 = np.ascontiguousarray(np.concatenate([sc.sigma2 for sc in flat]), np.float32)
+            self.K = (flat[0].fx, flat[0].fy, flat[0].cx, flat[0].cy)
+        else:
+            self.n = np.array([p.n1 for p in flat], np.int32)
+            cat = lambda f, dt: np.ascontiguousarray(np.concatenate([f(p) for p in flat]), dt)
+            self.valid = cat(lambda p: p.valid.astype(np.uint8), np.uint8)
+            self.Xw1 = cat(lambda p: p.Xw1, np.float32)
+            self.Xw2 = cat(lambda p: p.Xw2, np.float32)
+            self.s1 = cat(lambda p: p.sigma2_1, np.float32)
+            self.s2 = cat(lambda p: p.sigma2_2, np.float32)
+            self.poses = np.ascontiguousarray(np.stack([np.concatenate([
+                np.asarray(p.R1, np.float32).ravel(), np.asarray(p.t1, np.float32),
+                np.asarray(p.R2, np.float32).ravel(), np.asarray(p.t2, np.float32),
+                np.asarray(p.K1, np.float32), np.asarray(p.K2, np.float32)]) for p in flat]), np.float32)
+        self.off = np.concatenate([[0], np.cumsum(self.n)[:-1]]).astype(np.int64)
+        self.rec = np.zeros((len(evs), 4), np.int32)
+        self.T = np.zeros((len(evs), 16), np.float32)
+
+    def run(self, nthreads: int = 1):
+        L = ol.lib()
+        ne = len(self.eids)
+        if self.kind == "reloc":
+            L.ora_reloc_events_batch(ne, self.ev_begin, self.n, self.off, self.p2d, self.p3d, self.s2, *self.K,
+                                     self.seeds, *rev.RELOC_PARAMS, nthreads, self.rec.reshape(-1),
+                                     self.T.reshape(-1))
+        else:
+            L.ora_loop_events_batch(ne, self.ev_begin, self.n, self.off, self.valid, self.Xw1, self.Xw2, self.s1,
+                                    self.s2, self.poses.reshape(-1), self.seeds, *rev.LOOP_PARAMS, nthreads,
+                                    self.rec.reshape(-1), self.T.reshape(-1))
+        return self
+
+    def records(self) -> np.ndarray:
+        per = [dict(winner=r[0], round=r[1], hypothesis=r[2], n_inliers=r[3]) for r in self.rec]
+        return rev.pack_events(self.eids, per, self.T)

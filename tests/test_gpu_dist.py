@@ -1,0 +1,116 @@
+"""The N > 1 product path on the GPU: two fresh rank processes (world size 2, both driving device 0,
+gloo collectives — the one-GPU stand-in for RCCL over xGMI) each run their shard THROUGH librsc
+(relocalization candidates by cost-balanced contiguous blocks; config-5 events whole, LPT), then
+all-gather the fixed-size records.  The gathered records must equal a single-process librsc run and
+the oracle bit for bit (sharding changes no arithmetic)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from rsc import dist as rdist
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _scenes():
+    from rsc import synth
+    rng = np.random.default_rng(321)
+    return [synth.make_pnp_scene(rng, int(rng.integers(200, 1500)), float(rng.uniform(0.35, 0.75)))
+            for _ in range(12)]
+
+
+def _events():
+    from rsc import events as rev
+    return rev.make_event_stream(seed=17, n_reloc=10, n_loop=4)
+
+
+def _run_pnp(ctx, scenes, idx):
+    from rsc import engine
+    solvers = [engine.PnPSolver(ctx, scenes[c], 1 + c) for c in idx]
+    if not solvers:
+        return []
+    b = engine.SolverBatch(solvers)
+    b.set_ransac_parameters(0.99, 10, 300, 4, 0.5, 5.991)
+    return b.iterate(300)
+
+
+def _run_events(ctx, evs):
+    from rsc import engine, events as rev
+    out = []
+    for kind in ("reloc", "loop"):
+        sub = [ev for ev in evs if ev.kind == kind]
+        if not sub:
+            continue
+        cls = engine.PnPSolver if kind == "reloc" else engine.Sim3Solver
+        eb = engine.EventBatch([[cls(ctx, x, s) for x, s in zip(rev.event_inputs(ev), ev.seeds)] for ev in sub])
+        eb.batch.set_ransac_parameters(*(rev.RELOC_PARAMS if kind == "reloc" else rev.LOOP_PARAMS))
+        eb.run()
+        out.append(rev.pack_events([ev.eid for ev in sub], eb.per_event, eb.winner_poses()))
+    return np.concatenate(out) if out else np.zeros((0, rev.EVENT_RECORD), np.float32)
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "orb-slam2-optimized_amd"))
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import torch.distributed as dist
+    from rsc import dist as rd, engine, events as rev
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = engine.Context(0)
+    scenes = _scenes()
+    lo, hi = rd.shard_range(len(scenes), world, rank, cost=[s.n for s in scenes])
+    rec = rd.pack_pnp(list(range(lo, hi)), _run_pnp(ctx, scenes, range(lo, hi)))
+    allr = rd.all_gather_records(dist, rec, max_per_rank=len(scenes))
+    evs = _events()
+    mine = rev.shard_events([ev.cost for ev in evs], world)[rank]
+    erec = _run_events(ctx, [evs[i] for i in mine])
+    alle = rev.all_gather_events(dist, erec, max_per_rank=len(evs))
+    q.put((rank, hi - lo, len(mine), allr, alle))
+    dist.barrier()
+    dist.destroy_process_group()
+    ctx.close()
+
+
+def test_world2_librsc_shards_match_single_process_and_oracle():
+    from gpu_common import ctx
+    import events_oracle as eo
+    import oracle_lib as ol
+    sp = mp.get_context("spawn")
+    q = sp.Queue()
+    port = _free_port()
+    procs = [sp.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=240) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    scenes, evs = _scenes(), _events()
+    assert all(g[1] > 0 and g[2] > 0 for g in got)  # both ranks had work
+    single = rdist.pack_pnp(list(range(len(scenes))), _run_pnp(ctx(), scenes, range(len(scenes))))
+    single_ev = _run_events(ctx(), evs)
+    for _, _, _, allr, alle in got:  # every rank holds the full gathered result
+        assert np.array_equal(allr.view(np.uint32), single.view(np.uint32))
+        assert np.array_equal(alle.view(np.uint32), single_ev.view(np.uint32))
+    # and the single-process run is the oracle's
+    ora = []
+    for c, sc in enumerate(scenes):
+        o = ol.OraclePnP(sc, 1 + c)
+        o.set_ransac_parameters(0.99, 10, 300, 4, 0.5, 5.991)
+        ora.append(o.iterate(300))
+    assert np.array_equal(single.view(np.uint32), rdist.pack_pnp(list(range(len(scenes))), ora).view(np.uint32))
+    assert np.array_equal(single_ev.view(np.uint32), eo.run_events(evs).view(np.uint32))
+    assert rdist.reloc_winner(single) == rdist.reloc_winner(got[0][3])

@@ -6,7 +6,7 @@ Corrections (MI355X_MICROARCH.md §HBM): both counters are in KiB; on gfx950 FET
 the bytes of a wide coalesced read, so read bytes = 2 x FETCH_SIZE x 1024 (an upper estimate for
 narrower accesses); WRITE_SIZE x 1024 is exact for 16-B-per-lane stores.
 
-usage: pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv out.json"""
+usage: pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv out.json [commit]"""
 import csv
 import json
 import re
@@ -34,6 +34,7 @@ for k in sorted(set(fetch) | set(write)):
 path = [k for k in kernels if k.replace("rsc::", "").startswith(("pnp_eig_quad_kernel", "pnp_betas_kernel", "pnp_scan_kernel"))]
 out = {"kernels": kernels, "epnp_launch_set": path,
        "epnp_launch_set_bytes": sum(kernels[k]["bytes"] for k in path),
-       "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB"}
+       "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB",
+       "commit": sys.argv[4] if len(sys.argv) > 4 else None}
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 print(json.dumps({k: round(v["bytes"] / 1e6, 3) for k, v in kernels.items()}))
