@@ -514,9 +514,9 @@ def run_latency(engine, ctx, args, with_cpu, reps=50):
 # ------------------------------------------------------------------------------------------------
 # SURVEY §8(f) neighbours
 # ------------------------------------------------------------------------------------------------
-def poseopt_frames(rng, F=64, N=2000, ratio=0.8):
+def poseopt_frames(rng, F=64, N=2000, ratio=0.8, stereo_frac=0.0):
     from rsc import synth
-    return [synth.make_poseopt_frame(rng, N, ratio) for _ in range(F)]
+    return [synth.make_poseopt_frame(rng, N, ratio, stereo_frac=stereo_frac) for _ in range(F)]
 
 
 def run_poseopt(engine, ctx, frames, args):
@@ -767,6 +767,8 @@ def cpu_baseline_poseopt(frames, seconds):
     uv = np.ascontiguousarray(np.concatenate([f.uv for f in frames]), np.float32)
     Xw = np.ascontiguousarray(np.concatenate([f.Xw for f in frames]), np.float32)
     inv = np.ascontiguousarray(np.concatenate([f.inv_sigma2 for f in frames]), np.float32)
+    ur = (np.ascontiguousarray(np.concatenate([f.u_right for f in frames]), np.float32)
+          if frames[0].u_right is not None else None)
     T = np.ascontiguousarray(np.stack([f.Tcw.reshape(16) for f in frames]), np.float32).reshape(-1)
     To = np.zeros(16 * F, np.float32)
     outl = np.zeros(int(off[-1]), np.uint8)
@@ -775,7 +777,8 @@ def cpu_baseline_poseopt(frames, seconds):
     done = 0
     t0 = time.perf_counter()
     while True:
-        L.ora_pose_optimization_batch(F, off, uv, Xw, inv, f0.fx, f0.fy, f0.cx, f0.cy, T, To, outl, good)
+        L.ora_pose_optimization_batch(F, off, uv, Xw, inv, f0.fx, f0.fy, f0.cx, f0.cy, T, To, outl, good,
+                                      None if ur is None else ur.ctypes.data, float(f0.bf))
         done += F
         if time.perf_counter() - t0 >= seconds:
             break
@@ -884,13 +887,18 @@ def main():
         if not args.no_latency:
             sections["single_event_latency"] = run_latency(engine, ctx, args, with_cpu)
         if not args.no_poseopt:
-            po_frames = poseopt_frames(np.random.default_rng(79))
-            po = run_poseopt(engine, ctx, po_frames, args)
-            sections["poseopt"] = _rounded(po)
-            if with_cpu:
-                cb = cpu_baseline_poseopt(po_frames, 3.0)
-                sections["poseopt"]["cpu_baseline"] = cb
-                sections["poseopt"]["speedup_vs_cpu_1core"] = round(po["poses_per_s"] / cb["value"], 1)
+            # stereo first: the reference builds only stereo_euroc / stereo_kitti, whose Frames carry
+            # mvuRight >= 0 on most slots (EdgeStereoSE3ProjectXYZOnlyPose, Optimizer.cpp:290-323)
+            for name, sf in (("poseopt", 0.8), ("poseopt_mono", 0.0)):
+                po_frames = poseopt_frames(np.random.default_rng(79), stereo_frac=sf)
+                po = run_poseopt(engine, ctx, po_frames, args)
+                po["stereo_edge_share"] = (float(np.mean([(f.u_right >= 0).mean() for f in po_frames]))
+                                           if sf > 0 else 0.0)
+                sections[name] = _rounded(po)
+                if with_cpu:
+                    cb = cpu_baseline_poseopt(po_frames, 3.0)
+                    sections[name]["cpu_baseline"] = cb
+                    sections[name]["speedup_vs_cpu_1core"] = round(po["poses_per_s"] / cb["value"], 1)
         if not args.no_sim3match:
             from rsc import synth
             r3 = np.random.default_rng(81)

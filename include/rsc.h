@@ -207,9 +207,9 @@ int rsc_loop_events(rsc_sim3* const* solvers, const int32_t* event_begin, int n_
 /* ---- Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) ------------------------------------
  * The pose-only g2o optimisation every tracking step and Tracking::Relocalization()
  * (Tracking.cpp:1284,1300,1315) run on the RANSAC pose: Levenberg-Marquardt of one VertexSE3Expmap
- * over EdgeSE3ProjectXYZOnlyPose edges with a Huber kernel (delta = sqrt(5.991)), 4 rounds of 10
- * iterations, each restarted from the entry pose, with chi2 > 5.991 outlier re-classification.
- * Monocular edges only (mvuRight < 0, Optimizer.cpp:252); stereo slots -> RSC_ERR_UNSUPPORTED.
+ * over EdgeSE3ProjectXYZOnlyPose (mvuRight < 0) and EdgeStereoSE3ProjectXYZOnlyPose (mvuRight >= 0,
+ * Optimizer.cpp:252-323) edges with Huber kernels (delta sqrt(5.991) / sqrt(7.815)), 4 rounds of 10
+ * iterations, each restarted from the entry pose, with chi2 > 5.991 / 7.815 outlier re-classification.
  * Parity against the reference is unpinned (g2o/Eigen cannot be built here). */
 typedef struct {
     int32_t n;                /* pFrame->N keypoint slots */
@@ -217,9 +217,10 @@ typedef struct {
     const float* uv;          /* [n][2] mvKeysUn[i].pt */
     const float* Xw;          /* [n][3] MapPoint::GetWorldPos() */
     const float* inv_sigma2;  /* [n] mvInvLevelSigma2[kpUn.octave] (information = I * invSigma2) */
-    const float* u_right;     /* [n] mvuRight, or NULL for a monocular Frame */
+    const float* u_right;     /* [n] mvuRight (>= 0: stereo observation), or NULL for a monocular Frame */
     float fx, fy, cx, cy;     /* Frame::fx,fy,cx,cy */
     float Tcw[16];            /* row-major pFrame->mTcw on entry */
+    float bf;                 /* Frame::mbf (stereo baseline * fx; unused without stereo slots) */
 } rsc_poseopt_problem;
 
 typedef struct {

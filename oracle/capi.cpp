@@ -540,12 +540,12 @@ double ora_dm_cos(double x) { return rsc::dm::cos(x); }
 double ora_dm_acos(double x) { return rsc::dm::acos(x); }
 double ora_dm_cbrt(double x) { return rsc::dm::cbrt(x); }
 
-// ---- Optimizer::PoseOptimization (monocular) ----
+// ---- Optimizer::PoseOptimization (mono + stereo edges) ----
 // stats[3] = rounds, LM iterations, LM trials.  Returns nGood.
 int ora_pose_optimization(int n, const uint8_t* has_mp, const float* uv, const float* Xw, const float* inv_sigma2,
                           float fx, float fy, float cx, float cy, const float* Tcw_in, float* Tcw_out,
-                          uint8_t* outlier, int32_t* stats) {
-    PoseOptInput in{n, has_mp, uv, Xw, inv_sigma2, fx, fy, cx, cy, {}};
+                          uint8_t* outlier, int32_t* stats, const float* u_right, float bf) {
+    PoseOptInput in{n, has_mp, uv, Xw, inv_sigma2, fx, fy, cx, cy, {}, u_right, bf};
     std::memcpy(in.Tcw, Tcw_in, sizeof(in.Tcw));
     PoseOptStats st{};
     const int r = pose_optimization(in, Tcw_out, outlier, &st);
@@ -556,11 +556,13 @@ int ora_pose_optimization(int n, const uint8_t* has_mp, const float* uv, const f
 // Batch of problems (bench cpu_baseline): problem c has edges [off[c], off[c+1]) (all with map points).
 void ora_pose_optimization_batch(int count, const int64_t* off, const float* uv, const float* Xw,
                                  const float* inv_sigma2, float fx, float fy, float cx, float cy,
-                                 const float* Tcw_in, float* Tcw_out, uint8_t* outlier, int32_t* n_good) {
+                                 const float* Tcw_in, float* Tcw_out, uint8_t* outlier, int32_t* n_good,
+                                 const float* u_right /* nullable */, float bf) {
     for (int c = 0; c < count; ++c) {
         const int64_t o = off[c];
         const int n = (int)(off[c + 1] - o);
-        PoseOptInput in{n, nullptr, uv + 2 * o, Xw + 3 * o, inv_sigma2 + o, fx, fy, cx, cy, {}};
+        PoseOptInput in{n, nullptr, uv + 2 * o, Xw + 3 * o, inv_sigma2 + o, fx, fy, cx, cy, {},
+                        u_right ? u_right + o : nullptr, bf};
         std::memcpy(in.Tcw, Tcw_in + 16 * c, sizeof(in.Tcw));
         n_good[c] = pose_optimization(in, Tcw_out + 16 * c, outlier + o, nullptr);
     }

@@ -243,34 +243,54 @@ bool ldlt_solve6(double A[6][6], const double b[6], double x[6]) {
     return true;
 }
 
-// ---- EdgeSE3ProjectXYZOnlyPose + RobustKernelHuber ------------------------------------------------
+// ---- EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose + RobustKernelHuber -------------
 struct Edge {
     double Xw[3];
-    double obs[2];
+    double obs[3];
     double inv;      // information = Identity * invSigma2
-    double err[2];   // _error (last computeError)
+    double err[3];   // _error (last computeError)
     int level;
     bool robust;
+    bool stereo;     // EdgeStereoSE3ProjectXYZOnlyPose (3-D error) instead of the 2-D mono edge
     int slot;
 };
 
 struct Cam {
-    double fx, fy, cx, cy;
+    double fx, fy, cx, cy, bf;
 };
 
 void compute_error(Edge& e, const SE3& est, const Cam& K) {
     double p[3];
     se3_map(est, e.Xw, p);
-    const double pr0 = p[0] / p[2], pr1 = p[1] / p[2];
-    const double r0 = pr0 * K.fx + K.cx, r1 = pr1 * K.fy + K.cy;
+    if (!e.stereo) {  // obs - cam_project(map(Xw)), project2d = (x/z, y/z)
+        const double pr0 = p[0] / p[2], pr1 = p[1] / p[2];
+        const double r0 = pr0 * K.fx + K.cx, r1 = pr1 * K.fy + K.cy;
+        e.err[0] = e.obs[0] - r0;
+        e.err[1] = e.obs[1] - r1;
+        e.err[2] = 0.0;
+        return;
+    }
+    // EdgeStereoSE3ProjectXYZOnlyPose::cam_project (types_six_dof_expmap.cpp:299-306):
+    // `const float invz = 1.0f/trans_xyz[2]` — a double division rounded to float
+    const float invz = (float)(1.0 / p[2]);
+    const double r0 = p[0] * (double)invz * K.fx + K.cx;
+    const double r1 = p[1] * (double)invz * K.fy + K.cy;
+    const double r2 = r0 - K.bf * (double)invz;
     e.err[0] = e.obs[0] - r0;
     e.err[1] = e.obs[1] - r1;
+    e.err[2] = e.obs[2] - r2;
 }
 
-double chi2(const Edge& e) {  // _error.dot(information() * _error)
-    const double w0 = e.inv * e.err[0] + 0.0 * e.err[1];
-    const double w1 = 0.0 * e.err[0] + e.inv * e.err[1];
-    return e.err[0] * w0 + e.err[1] * w1;
+double chi2(const Edge& e) {  // _error.dot(information() * _error), Eigen sums left to right
+    if (!e.stereo) {
+        const double w0 = e.inv * e.err[0] + 0.0 * e.err[1];
+        const double w1 = 0.0 * e.err[0] + e.inv * e.err[1];
+        return e.err[0] * w0 + e.err[1] * w1;
+    }
+    const double w0 = (e.inv * e.err[0] + 0.0 * e.err[1]) + 0.0 * e.err[2];
+    const double w1 = (0.0 * e.err[0] + e.inv * e.err[1]) + 0.0 * e.err[2];
+    const double w2 = (0.0 * e.err[0] + 0.0 * e.err[1]) + e.inv * e.err[2];
+    return (e.err[0] * w0 + e.err[1] * w1) + e.err[2] * w2;
 }
 
 struct Huber {
@@ -287,7 +307,8 @@ struct Huber {
     }
 };
 
-void linearize(const Edge& e, const SE3& est, const Cam& K, double J[2][6]) {
+// linearizeOplus: rows 0, 1 (both edges), row 2 (stereo, types_six_dof_expmap.cpp:359-364).
+void linearize(const Edge& e, const SE3& est, const Cam& K, double J[3][6]) {
     double p[3];
     se3_map(est, e.Xw, p);
     const double x = p[0], y = p[1];
@@ -305,12 +326,19 @@ void linearize(const Edge& e, const SE3& est, const Cam& K, double J[2][6]) {
     J[1][3] = 0;
     J[1][4] = -invz * K.fy;
     J[1][5] = y * invz_2 * K.fy;
+    J[2][0] = J[0][0] - K.bf * y * invz_2;
+    J[2][1] = J[0][1] + K.bf * x * invz_2;
+    J[2][2] = J[0][2];
+    J[2][3] = J[0][3];
+    J[2][4] = 0;
+    J[2][5] = J[0][5] - K.bf * invz_2;
 }
 
 struct Problem {
     std::vector<Edge> edges;
     Cam K;
-    Huber huber;
+    Huber huber, huberStereo;
+    const Huber& hub(const Edge& e) const { return e.stereo ? huberStereo : huber; }
     // LM state that lives in the g2o objects across rounds
     double x[6] = {0, 0, 0, 0, 0, 0};  // BlockSolver::_x (zeroed once at allocation, solver.cpp:53-56)
     double lambda = -1.0, ni = 2.0;
@@ -323,7 +351,7 @@ struct Problem {
             if (e.level != 0) continue;
             if (e.robust) {
                 double rho[3];
-                huber.robustify(chi2(e), rho);
+                hub(e).robustify(chi2(e), rho);
                 chi += rho[0];
             } else {
                 chi += chi2(e);
@@ -335,7 +363,8 @@ struct Problem {
         for (Edge& e : edges)
             if (e.level == 0) compute_error(e, est, K);
     }
-    // BlockSolver::buildSystem: H (vertex hessian, full 6x6) and b.
+    // BlockSolver::buildSystem: H (vertex hessian, full 6x6) and b; per edge
+    // BaseUnaryEdge::constructQuadraticForm with D = 2 (mono) or 3 (stereo) error rows.
     void build_system(const SE3& est, double H[6][6], double b[6]) const {
         for (int i = 0; i < 6; ++i) {
             b[i] = 0.0;
@@ -343,31 +372,58 @@ struct Problem {
         }
         for (const Edge& e : edges) {
             if (e.level != 0) continue;
-            double A[2][6];
+            const int D = e.stereo ? 3 : 2;
+            double A[3][6];
             linearize(e, est, K, A);
-            const double om[2][2] = {{e.inv, 0.0}, {0.0, e.inv}};
+            double om[3][3];
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) om[r][c] = (r == c) ? e.inv : 0.0;
             if (e.robust) {
                 double rho[3];
-                huber.robustify(chi2(e), rho);
-                double W[2][2];
-                for (int r = 0; r < 2; ++r)
-                    for (int c = 0; c < 2; ++c) W[r][c] = rho[1] * om[r][c];
-                for (int i = 0; i < 6; ++i) {
-                    double t2[2];
-                    for (int k = 0; k < 2; ++k) t2[k] = (rho[1] * A[0][i]) * om[0][k] + (rho[1] * A[1][i]) * om[1][k];
-                    b[i] -= t2[0] * e.err[0] + t2[1] * e.err[1];
+                hub(e).robustify(chi2(e), rho);
+                double W[3][3];
+                for (int r = 0; r < D; ++r)
+                    for (int c = 0; c < D; ++c) W[r][c] = rho[1] * om[r][c];
+                for (int i = 0; i < 6; ++i) {  // b -= rho1 * A^T * omega * error
+                    double t2[3];
+                    for (int k = 0; k < D; ++k) {
+                        double a = (rho[1] * A[0][i]) * om[0][k];
+                        for (int r = 1; r < D; ++r) a = a + (rho[1] * A[r][i]) * om[r][k];
+                        t2[k] = a;
+                    }
+                    double g = t2[0] * e.err[0];
+                    for (int k = 1; k < D; ++k) g = g + t2[k] * e.err[k];
+                    b[i] -= g;
                 }
-                for (int i = 0; i < 6; ++i) {
-                    double t[2];
-                    for (int k = 0; k < 2; ++k) t[k] = A[0][i] * W[0][k] + A[1][i] * W[1][k];
-                    for (int j = 0; j < 6; ++j) H[i][j] += t[0] * A[0][j] + t[1] * A[1][j];
+                for (int i = 0; i < 6; ++i) {  // H += A^T * (rho1 omega) * A
+                    double t[3];
+                    for (int k = 0; k < D; ++k) {
+                        double a = A[0][i] * W[0][k];
+                        for (int r = 1; r < D; ++r) a = a + A[r][i] * W[r][k];
+                        t[k] = a;
+                    }
+                    for (int j = 0; j < 6; ++j) {
+                        double h = t[0] * A[0][j];
+                        for (int k = 1; k < D; ++k) h = h + t[k] * A[k][j];
+                        H[i][j] += h;
+                    }
                 }
             } else {
                 for (int i = 0; i < 6; ++i) {
-                    double t[2];
-                    for (int k = 0; k < 2; ++k) t[k] = A[0][i] * om[0][k] + A[1][i] * om[1][k];
-                    b[i] -= t[0] * e.err[0] + t[1] * e.err[1];
-                    for (int j = 0; j < 6; ++j) H[i][j] += t[0] * A[0][j] + t[1] * A[1][j];
+                    double t[3];
+                    for (int k = 0; k < D; ++k) {
+                        double a = A[0][i] * om[0][k];
+                        for (int r = 1; r < D; ++r) a = a + A[r][i] * om[r][k];
+                        t[k] = a;
+                    }
+                    double g = t[0] * e.err[0];
+                    for (int k = 1; k < D; ++k) g = g + t[k] * e.err[k];
+                    b[i] -= g;
+                    for (int j = 0; j < 6; ++j) {
+                        double h = t[0] * A[0][j];
+                        for (int k = 1; k < D; ++k) h = h + t[k] * A[k][j];
+                        H[i][j] += h;
+                    }
                 }
             }
         }
@@ -448,10 +504,13 @@ struct Problem {
 
 int pose_optimization(const PoseOptInput& in, float Tcw_out[16], uint8_t* outlier, PoseOptStats* stats) {
     Problem P;
-    P.K = {(double)in.fx, (double)in.fy, (double)in.cx, (double)in.cy};
+    P.K = {(double)in.fx, (double)in.fy, (double)in.cx, (double)in.cy, (double)in.bf};
     const float deltaMono = std::sqrt(5.991);
+    const float deltaStereo = std::sqrt(7.815);
     P.huber.delta = deltaMono;
     P.huber.dsqr = P.huber.delta * P.huber.delta;
+    P.huberStereo.delta = deltaStereo;
+    P.huberStereo.dsqr = P.huberStereo.delta * P.huberStereo.delta;
     for (int i = 0; i < in.n; ++i) {
         if (in.has_mp && !in.has_mp[i]) continue;
         outlier[i] = 0;
@@ -459,8 +518,10 @@ int pose_optimization(const PoseOptInput& in, float Tcw_out[16], uint8_t* outlie
         for (int c = 0; c < 3; ++c) e.Xw[c] = in.Xw[3 * i + c];
         e.obs[0] = in.uv[2 * i];
         e.obs[1] = in.uv[2 * i + 1];
+        e.stereo = in.u_right && in.u_right[i] >= 0.0f;  // Optimizer.cpp:252 (mvuRight[i] < 0: mono)
+        e.obs[2] = e.stereo ? in.u_right[i] : 0.0;
         e.inv = in.inv_sigma2[i];
-        e.err[0] = e.err[1] = 0.0;
+        e.err[0] = e.err[1] = e.err[2] = 0.0;
         e.level = 0;
         e.robust = true;
         e.slot = i;
@@ -478,6 +539,7 @@ int pose_optimization(const PoseOptInput& in, float Tcw_out[16], uint8_t* outlie
     }
     const SE3 init = se3_from_Rt(R0, t0);
     const float chi2Mono[4] = {5.991, 5.991, 5.991, 5.991};
+    const float chi2Stereo[4] = {7.815, 7.815, 7.815, 7.815};
     const int its[4] = {10, 10, 10, 10};
     SE3 est = init;
     int nBad = 0;
@@ -488,8 +550,10 @@ int pose_optimization(const PoseOptInput& in, float Tcw_out[16], uint8_t* outlie
         nBad = 0;
         for (Edge& e : P.edges) {
             if (outlier[e.slot]) compute_error(e, est, P.K);
+            // the mono loop then the stereo loop (Optimizer.cpp:347-398): per-edge decisions only,
+            // nBad is their total, so one pass in edge order is equivalent
             const float c2 = chi2(e);
-            if (c2 > chi2Mono[it]) {
+            if (c2 > (e.stereo ? chi2Stereo[it] : chi2Mono[it])) {
                 outlier[e.slot] = 1;
                 e.level = 1;
                 nBad++;

@@ -1,7 +1,7 @@
 // TEST INFRASTRUCTURE — parity oracle, never linked into the product library.
 //
-// Sequential CPU restatement of Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) for
-// monocular edges, with the parts of the vendored g2o it runs:
+// Sequential CPU restatement of Optimizer::PoseOptimization (src/Optimizer.cpp:205-424), monocular
+// (mvuRight < 0) and stereo (mvuRight >= 0) edges, with the parts of the vendored g2o it runs:
 //   SparseOptimizer::initializeOptimization/optimize/computeActiveErrors/activeRobustChi2
 //     (Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:61-114,199-267,354-414),
 //   OptimizationAlgorithmLevenberg::solve/computeLambdaInit/computeScale
@@ -11,7 +11,9 @@
 //   BaseUnaryEdge::constructQuadraticForm (core/base_unary_edge.hpp:43-71),
 //   RobustKernelHuber (core/robust_kernel_impl.cpp:65-91),
 //   EdgeSE3ProjectXYZOnlyPose::computeError/linearizeOplus (types/types_six_dof_expmap.h:153-157,
-//     types/types_six_dof_expmap.cpp:266-296), VertexSE3Expmap::oplusImpl (types_six_dof_expmap.h:73),
+//     types/types_six_dof_expmap.cpp:266-296), EdgeStereoSE3ProjectXYZOnlyPose::computeError/
+//     cam_project/linearizeOplus (types_six_dof_expmap.h:184-188, .cpp:299-306,335-366),
+//     VertexSE3Expmap::oplusImpl (types_six_dof_expmap.h:73),
 //   SE3Quat (types/se3quat.h: ctor, operator*, map, exp, normalizeRotation),
 //   Converter::toSE3Quat / toIso (src/Converter.cpp:16-29).
 //
@@ -34,6 +36,8 @@ struct PoseOptInput {
     const float* inv_sigma2;  // [n] mvInvLevelSigma2[kpUn.octave]
     float fx, fy, cx, cy;     // Frame::fx..cy
     float Tcw[16];            // row-major pFrame->mTcw
+    const float* u_right = nullptr;  // [n] mvuRight (>= 0: stereo edge, Optimizer.cpp:252,290-323); NULL = mono
+    float bf = 0.0f;                 // Frame::mbf (stereo baseline x fx)
 };
 
 struct PoseOptStats {

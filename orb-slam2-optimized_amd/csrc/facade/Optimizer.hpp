@@ -3,11 +3,12 @@
 // pose-only Levenberg-Marquardt runs on the MI355X (librsc.so), one workgroup per Frame.
 //
 // FrameT needs (include/Frame.hpp): mvpMapPoints (pointer-likes, tested for null), mvuRight,
-// mvKeysUn[i].pt.{x,y} and .octave, mvInvLevelSigma2[], fx, fy, cx, cy, mTcw with operator()(r,c)
+// mvKeysUn[i].pt.{x,y} and .octave, mvInvLevelSigma2[], fx, fy, cx, cy, mbf, mTcw with operator()(r,c)
 // (Eigen::Isometry3f), SetPose(const decltype(mTcw)&), and mvbOutlier (std::vector<bool>).
 // MapPoint::GetWorldPos() must return something indexable with (i).  In the reference tree:
 //     int nGood = rsc_orb::PoseOptimization(&mCurrentFrame);       // Tracking.cpp:621,745,787,1284
-// Monocular observations only: a Frame with a map point on a stereo slot (mvuRight >= 0) throws.
+// Slots with mvuRight >= 0 become EdgeStereoSE3ProjectXYZOnlyPose edges (Optimizer.cpp:290-323), the
+// others monocular edges, exactly as the reference's stereo_euroc / stereo_kitti builds run it.
 #pragma once
 #include <vector>
 #include "rsc_context.hpp"
@@ -51,6 +52,7 @@ struct PoseOptInputs {
         pb.inv_sigma2 = inv.data();
         pb.u_right = ur.data();
         pb.fx = F.fx; pb.fy = F.fy; pb.cx = F.cx; pb.cy = F.cy;
+        pb.bf = F.mbf;
         for (int r = 0; r < 4; ++r)
             for (int c = 0; c < 4; ++c) pb.Tcw[4 * r + c] = F.mTcw(r, c);
     }

@@ -55,29 +55,43 @@ __device__ __forceinline__ double fold_run(double acc, const double* __restrict_
     return acc;
 }
 
-// Error of edge e at `est` (EdgeSE3ProjectXYZOnlyPose::computeError), stored as _error.
-__device__ __forceinline__ double2 po_edge_error(const DevPoseProb& P, int e, const PoSE3& est, const PoCam& K) {
+// Huber kernels of the two edge types (Optimizer.cpp:240-241: float deltas, setDelta(double)).
+struct PoKernels {
+    double dm, dm2, ds, ds2;
+};
+
+__device__ __forceinline__ bool po_is_stereo(const DevPoseProb& P, int e) { return P.ur && P.ur[e] >= 0.0f; }
+
+// Error of edge e at `est` (computeError of its edge type), stored as _error.
+__device__ __forceinline__ double3 po_edge_error(const DevPoseProb& P, int e, const PoSE3& est, const PoCam& K) {
     const float4 xw = P.xw[e];
     const float2 uv = P.uv[e];
+    const bool st = po_is_stereo(P, e);
     const double X[3] = {(double)xw.x, (double)xw.y, (double)xw.z};
-    double e0, e1;
-    po_error(est, K, X, (double)uv.x, (double)uv.y, e0, e1);
-    const double2 er = make_double2(e0, e1);
-    P.err[e] = er;
-    return er;
+    double e0, e1, e2;
+    po_error(est, K, X, (double)uv.x, (double)uv.y, st ? (double)P.ur[e] : 0.0, st, e0, e1, e2);
+    P.err[e] = make_double2(e0, e1);
+    if (st) P.err_r[e] = e2;
+    return make_double3(e0, e1, e2);
+}
+
+__device__ __forceinline__ double3 po_stored_error(const DevPoseProb& P, int e) {
+    const double2 er = P.err[e];
+    return make_double3(er.x, er.y, po_is_stereo(P, e) ? P.err_r[e] : 0.0);
 }
 
 // activeRobustChi2 after computeActiveErrors at `est` (sparse_optimizer.cpp:61-114): errors of the
 // level-0 edges recomputed and stored, their robust chi2 terms (0.0 for inactive edges — an exact
 // identity for a sum that starts at +0.0) folded in edge order by one lane.
 __device__ double po_chi_pass(const DevPoseProb& P, const PoseLds& S, const PoSE3& est, const PoCam& K, bool robust,
-                              double delta, double dsqr) {
+                              const PoKernels& hk) {
     const int tid = threadIdx.x;
     for (int e = tid; e < P.n; e += kPoseChunk) {
         double t = 0.0;
         if (S.lvl[e] == 0) {
-            const double2 er = po_edge_error(P, e, est, K);
-            t = po_chi_term(robust, (double)P.xw[e].w, er.x, er.y, delta, dsqr);
+            const double3 er = po_edge_error(P, e, est, K);
+            const bool st = po_is_stereo(P, e);
+            t = po_chi_term(robust, st, (double)P.xw[e].w, er.x, er.y, er.z, st ? hk.ds : hk.dm, st ? hk.ds2 : hk.dm2);
         }
         S.terms[e] = t;
     }
@@ -93,7 +107,7 @@ __device__ double po_chi_pass(const DevPoseProb& P, const PoseLds& S, const PoSE
 // (block_solver.hpp:502-560) in one pass over kPoseChunk-edge chunks: H lower triangle folded on
 // lanes 0..26 of wave 0 (added) and b (subtracted), both from 0.0; the chi2 column on wave 1.
 __device__ void po_build_pass(const DevPoseProb& P, const PoseLds& S, const PoSE3& est, const PoCam& K, bool robust,
-                              double delta, double dsqr, bool errors, bool chi, double (&H)[6][6], double (&b)[6],
+                              const PoKernels& hk, bool errors, bool chi, double (&H)[6][6], double (&b)[6],
                               double& chi_out) {
     const int tid = threadIdx.x;
     double acc = 0.0;
@@ -103,11 +117,13 @@ __device__ void po_build_pass(const DevPoseProb& P, const PoseLds& S, const PoSE
         RSC_UNROLL for (int k = 0; k < kPoseTerms; ++k) t[k] = 0.0;
         double tc = 0.0;
         if (e < P.n && S.lvl[e] == 0) {
-            const double2 er = errors ? po_edge_error(P, e, est, K) : P.err[e];
+            const double3 er = errors ? po_edge_error(P, e, est, K) : po_stored_error(P, e);
             const float4 xw = P.xw[e];
+            const bool st = po_is_stereo(P, e);
+            const double delta = st ? hk.ds : hk.dm, dsqr = st ? hk.ds2 : hk.dm2;
             const double X[3] = {(double)xw.x, (double)xw.y, (double)xw.z};
-            po_quad_terms(est, K, X, (double)xw.w, er.x, er.y, robust, delta, dsqr, t);
-            if (chi) tc = po_chi_term(robust, (double)xw.w, er.x, er.y, delta, dsqr);
+            po_quad_terms(est, K, X, (double)xw.w, er.x, er.y, er.z, st, robust, delta, dsqr, t);
+            if (chi) tc = po_chi_term(robust, st, (double)xw.w, er.x, er.y, er.z, delta, dsqr);
         }
         RSC_UNROLL for (int k = 0; k < kPoseTerms; ++k) S.terms[k * kPoseCol + tid] = t[k];
         if (chi) S.terms[kPoseTerms * kPoseCol + tid] = tc;
@@ -144,10 +160,15 @@ __global__ __launch_bounds__(kPoseChunk) void poseopt_kernel(const DevPoseProb* 
     const PoseLds S{po_lds, red_sh, reinterpret_cast<uint8_t*>(po_lds + kPoseTermDoubles), &nbad_sh};
     const DevPoseProb& P = probs[blockIdx.x];
     const int tid = threadIdx.x, n = P.n;
-    const PoCam K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
-    const float deltaMono = sqrt(5.991);  // Optimizer.cpp:240
-    const double delta = deltaMono, dsqr = delta * delta;  // RobustKernelHuber::setDelta
-    const float chi2Mono = 5.991f;
+    const PoCam K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy, (double)P.bf};
+    const float deltaMono = sqrt(5.991);    // Optimizer.cpp:240
+    const float deltaStereo = sqrt(7.815);  // Optimizer.cpp:241
+    PoKernels hk;                           // RobustKernelHuber::setDelta
+    hk.dm = deltaMono;
+    hk.dm2 = hk.dm * hk.dm;
+    hk.ds = deltaStereo;
+    hk.ds2 = hk.ds * hk.ds;
+    const float chi2Mono = 5.991f, chi2Stereo = 7.815f;
     double R0[3][3], t0[3];
     RSC_UNROLL for (int r = 0; r < 3; ++r) {
         RSC_UNROLL for (int c = 0; c < 3; ++c) R0[r][c] = (double)P.T[4 * r + c];
@@ -181,7 +202,7 @@ __global__ __launch_bounds__(kPoseChunk) void poseopt_kernel(const DevPoseProb* 
                 lm_its++;
                 double H[6][6], b[6];
                 double chiFold = 0.0;
-                po_build_pass(P, S, est, K, robust, delta, dsqr, !errorsAtEst, !chiKnown, H, b, chiFold);
+                po_build_pass(P, S, est, K, robust, hk, !errorsAtEst, !chiKnown, H, b, chiFold);
                 double currentChi = chiKnown ? chiNow : chiFold;
                 const double iniChi = currentChi;
                 if (i == 0) {
@@ -208,7 +229,7 @@ __global__ __launch_bounds__(kPoseChunk) void poseopt_kernel(const DevPoseProb* 
                     const bool ok2 = po_ldlt_solve6(Hd, b, xs);
                     if (ok2) RSC_UNROLL for (int j = 0; j < 6; ++j) x[j] = xs[j];
                     est = po_mul(po_exp(x), est);
-                    double tempChi = po_chi_pass(P, S, est, K, robust, delta, dsqr);
+                    double tempChi = po_chi_pass(P, S, est, K, robust, hk);
                     if (!ok2) tempChi = DBL_MAX;
                     rho = (currentChi - tempChi);
                     double scale = 0.;
@@ -243,12 +264,13 @@ __global__ __launch_bounds__(kPoseChunk) void poseopt_kernel(const DevPoseProb* 
                 }
             }
         }
-        // re-classification (Optimizer.cpp:347-376)
+        // re-classification (Optimizer.cpp:347-398; mono and stereo loops are per-edge decisions)
         int cnt = 0;
         for (int e = tid; e < n; e += kPoseChunk) {
-            const double2 er = S.lvl[e] ? po_edge_error(P, e, est, K) : P.err[e];
-            const float c2 = (float)po_chi2((double)P.xw[e].w, er.x, er.y);
-            const bool bad = c2 > chi2Mono;
+            const double3 er = S.lvl[e] ? po_edge_error(P, e, est, K) : po_stored_error(P, e);
+            const bool st = po_is_stereo(P, e);
+            const float c2 = (float)po_chi2((double)P.xw[e].w, st, er.x, er.y, er.z);
+            const bool bad = c2 > (st ? chi2Stereo : chi2Mono);
             S.lvl[e] = bad ? 1 : 0;
             P.outlier[e] = bad ? 1 : 0;
             cnt += bad;
@@ -275,14 +297,14 @@ __global__ __launch_bounds__(kPoseChunk) void poseopt_kernel(const DevPoseProb* 
     }
 }
 
+hipError_t poseopt_prepare_device() {
+    // the ~115 KB dynamic-LDS launch needs the per-device attribute raised (rsc_context_create, once
+    // per context: hipFuncSetAttribute applies to the current device)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&poseopt_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPoseLds);
+}
+
 hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&poseopt_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPoseLds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
     poseopt_kernel<<<count, kPoseChunk, kPoseLds, st>>>(probs);
     return hipGetLastError();
 }

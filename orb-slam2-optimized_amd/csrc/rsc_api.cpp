@@ -122,6 +122,7 @@ struct rsc_context {
     // PoseOptimization: packed inputs (problems | xw | uv), edge error scratch, results (outliers | poses)
     DevBuf<char> d_po_in;
     DevBuf<double2> d_po_err;
+    DevBuf<double> d_po_err_r;  // third error component of the stereo edges
     DevBuf<char> d_po_res;
     PinBuf<char> h_po_in;
     PinBuf<char> h_po_res;
@@ -802,6 +803,7 @@ int rsc_context_create(int device, rsc_context** out) {
     if (int e = C->d_table.ensure(C->table.T.size())) return e;
     RSC_HIP(hipMemcpy(C->d_table.p, C->table.T.data(), C->table.T.size() * 4, hipMemcpyHostToDevice));
     for (auto& e : C->ev) RSC_HIP(hipEventCreate(&e));
+    RSC_HIP(poseopt_prepare_device());
     *out = C.release();
     return RSC_OK;
 }
@@ -1152,10 +1154,6 @@ int rsc_pose_optimization_many(rsc_context* C, const rsc_poseopt_problem* P, int
         int ne = 0;
         for (int i = 0; i < q.n; ++i) {
             if (q.has_mp && !q.has_mp[i]) continue;
-            if (q.u_right && q.u_right[i] >= 0) {
-                g_last_error = "stereo observations (mvuRight >= 0) are not supported";
-                return RSC_ERR_UNSUPPORTED;
-            }
             ++ne;
         }
         if (ne > kPoseMaxEdges) {
@@ -1180,7 +1178,8 @@ int rsc_pose_optimization_many(rsc_context* C, const rsc_poseopt_problem* P, int
     RSC_HIP(hipSetDevice(C->device));
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_probs = 0, o_xw = al(sizeof(DevPoseProb) * R), o_uv = o_xw + al(sizeof(float4) * E);
-    const size_t in_bytes = o_uv + al(sizeof(float2) * E);
+    const size_t o_ur = o_uv + al(sizeof(float2) * E);  // mvuRight of the edges (stereo: >= 0)
+    const size_t in_bytes = o_ur + al(sizeof(float) * E);
     const size_t r_out = 0, r_flags = al(sizeof(float) * 16 * R);
     const size_t res_bytes = r_flags + al(E);
     if (int e = C->h_po_in.ensure(in_bytes)) return e;
@@ -1188,6 +1187,7 @@ int rsc_pose_optimization_many(rsc_context* C, const rsc_poseopt_problem* P, int
     if (int e = C->h_po_res.ensure(res_bytes)) return e;
     if (int e = C->d_po_res.ensure(res_bytes)) return e;
     if (int e = C->d_po_err.ensure(E)) return e;
+    if (int e = C->d_po_err_r.ensure(E)) return e;
     // the previous call's copies out of the pinned staging must be complete
     RSC_HIP(hipStreamSynchronize(C->stream));
     char* h = C->h_po_in.p;
@@ -1195,23 +1195,29 @@ int rsc_pose_optimization_many(rsc_context* C, const rsc_poseopt_problem* P, int
     DevPoseProb* hp = reinterpret_cast<DevPoseProb*>(h + o_probs);
     float4* hxw = reinterpret_cast<float4*>(h + o_xw);
     float2* huv = reinterpret_cast<float2*>(h + o_uv);
+    float* hur = reinterpret_cast<float*>(h + o_ur);
     for (int k = 0; k < R; ++k) {
         const rsc_poseopt_problem& q = P[run[k]];
         size_t e = eoff[k];
+        bool stereo = false;
         for (int i = 0; i < q.n; ++i) {
             if (q.has_mp && !q.has_mp[i]) continue;
             hxw[e] = make_float4(q.Xw[3 * i], q.Xw[3 * i + 1], q.Xw[3 * i + 2], q.inv_sigma2[i]);
             huv[e] = make_float2(q.uv[2 * i], q.uv[2 * i + 1]);
+            hur[e] = q.u_right ? q.u_right[i] : -1.0f;
+            stereo |= hur[e] >= 0.0f;
             ++e;
         }
         DevPoseProb& dp = hp[k];
         dp.xw = reinterpret_cast<const float4*>(d + o_xw) + eoff[k];
         dp.uv = reinterpret_cast<const float2*>(d + o_uv) + eoff[k];
+        dp.ur = stereo ? reinterpret_cast<const float*>(d + o_ur) + eoff[k] : nullptr;
         dp.err = C->d_po_err.p + eoff[k];
+        dp.err_r = C->d_po_err_r.p + eoff[k];
         dp.outlier = reinterpret_cast<uint8_t*>(C->d_po_res.p + r_flags) + eoff[k];
         dp.out = reinterpret_cast<float*>(C->d_po_res.p + r_out) + 16 * k;
         dp.n = (int)(eoff[k + 1] - eoff[k]);
-        dp.fx = q.fx; dp.fy = q.fy; dp.cx = q.cx; dp.cy = q.cy;
+        dp.fx = q.fx; dp.fy = q.fy; dp.cx = q.cx; dp.cy = q.cy; dp.bf = q.bf;
         for (int j = 0; j < 12; ++j) dp.T[j] = q.Tcw[j];
     }
     RSC_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, C->stream));

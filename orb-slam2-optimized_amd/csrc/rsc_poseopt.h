@@ -1,6 +1,7 @@
-// rsc_poseopt.h — Optimizer::PoseOptimization (src/Optimizer.cpp:205-424, monocular edges) on the
-// GPU: the g2o Levenberg-Marquardt of one VertexSE3Expmap over EdgeSE3ProjectXYZOnlyPose edges
-// with a Huber kernel, 4 rounds of 10 iterations with inlier/outlier re-classification.
+// rsc_poseopt.h — Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) on the GPU: the g2o
+// Levenberg-Marquardt of one VertexSE3Expmap over EdgeSE3ProjectXYZOnlyPose (mono) and
+// EdgeStereoSE3ProjectXYZOnlyPose (stereo) edges with Huber kernels (delta sqrt(5.991) / sqrt(7.815)),
+// 4 rounds of 10 iterations with inlier/outlier re-classification (chi2 > 5.991 / 7.815).
 //
 // Mapping: one 512-thread workgroup per Frame (problem).  Threads own edges e = tid + 512 k and
 // evaluate the per-edge work of a pass in parallel (error, robust chi2 term, Jacobian and its 27
@@ -29,11 +30,13 @@ constexpr int kPoseTerms = 27;       // 21 lower-triangle H entries + 6 b entrie
 struct DevPoseProb {
     const float4* xw;    // [n] Xw (x, y, z), w = invSigma2 (information = I * invSigma2)
     const float2* uv;    // [n] observation mvKeysUn[i].pt
-    double2* err;        // [n] scratch: the edges' _error
+    const float* ur;     // [n] mvuRight (>= 0: stereo edge), or nullptr: every edge monocular
+    double2* err;        // [n] scratch: the edges' _error (u, v components)
+    double* err_r;       // [n] scratch: third _error component of the stereo edges
     uint8_t* outlier;    // [n] out: mvbOutlier of each edge
     float* out;          // out: [0..11] Tcw rows 0..2 (float), [12] nGood (as float bits of int), [13..15] stats
     int n;               // edges (slots with a map point), >= 3
-    float fx, fy, cx, cy;
+    float fx, fy, cx, cy, bf;
     float T[12];         // initial pFrame->mTcw rows 0..2
 };
 #endif
@@ -198,25 +201,47 @@ RSC_HD PoSE3 po_exp(const double (&u)[6]) {
 }
 
 // ---- edges ---------------------------------------------------------------------------------------
+// EdgeSE3ProjectXYZOnlyPose (mono, 2-D error) and EdgeStereoSE3ProjectXYZOnlyPose (stereo, 3-D error
+// (u, v, u_right)); a Frame slot is stereo iff mvuRight[i] >= 0 (Optimizer.cpp:252,290-323).  The
+// stereo forms below reduce to the mono ones' exact operations when `stereo` is false.
 struct PoCam {
-    double fx, fy, cx, cy;
+    double fx, fy, cx, cy, bf;
 };
 
-// EdgeSE3ProjectXYZOnlyPose::computeError: obs - cam_project(est.map(Xw)).
-RSC_HD void po_error(const PoSE3& est, const PoCam& K, const double (&Xw)[3], double u, double v, double& e0,
-                     double& e1) {
+// computeError: obs - cam_project(est.map(Xw)).  Mono: project2d = (x/z, y/z) in double.  Stereo
+// (types_six_dof_expmap.cpp:299-306): `const float invz = 1.0f/z` — a double division rounded to
+// float — then res0 = x*invz*fx + cx, res1 = y*invz*fy + cy, res2 = res0 - bf*invz.
+RSC_HD void po_error(const PoSE3& est, const PoCam& K, const double (&Xw)[3], double u, double v, double ur,
+                     bool stereo, double& e0, double& e1, double& e2) {
     double p[3];
     po_map(est, Xw, p);
-    const double pr0 = p[0] / p[2], pr1 = p[1] / p[2];
-    e0 = u - (pr0 * K.fx + K.cx);
-    e1 = v - (pr1 * K.fy + K.cy);
+    double r0, r1, r2 = 0.0;
+    if (stereo) {
+        const double invz = (double)(float)(1.0 / p[2]);
+        r0 = p[0] * invz * K.fx + K.cx;
+        r1 = p[1] * invz * K.fy + K.cy;
+        r2 = r0 - K.bf * invz;
+    } else {
+        const double pr0 = p[0] / p[2], pr1 = p[1] / p[2];
+        r0 = pr0 * K.fx + K.cx;
+        r1 = pr1 * K.fy + K.cy;
+    }
+    e0 = u - r0;
+    e1 = v - r1;
+    e2 = stereo ? ur - r2 : 0.0;
 }
 
-// _error.dot(information() * _error), information = I * inv.
-RSC_HD double po_chi2(double inv, double e0, double e1) {
-    const double w0 = inv * e0 + 0.0 * e1;
-    const double w1 = 0.0 * e0 + inv * e1;
-    return e0 * w0 + e1 * w1;
+// _error.dot(information() * _error), information = I * inv, Eigen sums left to right.
+RSC_HD double po_chi2(double inv, bool stereo, double e0, double e1, double e2) {
+    if (!stereo) {
+        const double w0 = inv * e0 + 0.0 * e1;
+        const double w1 = 0.0 * e0 + inv * e1;
+        return e0 * w0 + e1 * w1;
+    }
+    const double w0 = (inv * e0 + 0.0 * e1) + 0.0 * e2;
+    const double w1 = (0.0 * e0 + inv * e1) + 0.0 * e2;
+    const double w2 = (0.0 * e0 + 0.0 * e1) + inv * e2;
+    return (e0 * w0 + e1 * w1) + e2 * w2;
 }
 
 // RobustKernelHuber::robustify (rho[0], rho[1]; rho[2] is unused by g2o's robustInformation).
@@ -231,9 +256,10 @@ RSC_HD void po_huber(double e, double delta, double dsqr, double& rho0, double& 
     }
 }
 
-// Term of activeRobustChi2 for one edge.
-RSC_HD double po_chi_term(bool robust, double inv, double e0, double e1, double delta, double dsqr) {
-    const double c = po_chi2(inv, e0, e1);
+// Term of activeRobustChi2 for one edge (delta / dsqr of the edge's own kernel).
+RSC_HD double po_chi_term(bool robust, bool stereo, double inv, double e0, double e1, double e2, double delta,
+                          double dsqr) {
+    const double c = po_chi2(inv, stereo, e0, e1, e2);
     if (!robust) return c;
     double r0, r1;
     po_huber(c, delta, dsqr, r0, r1);
@@ -241,15 +267,16 @@ RSC_HD double po_chi_term(bool robust, double inv, double e0, double e1, double 
 }
 
 // linearizeOplus + constructQuadraticForm terms of one edge: t[0..20] = lower triangle of
-// J^T W J (row-major i >= j), t[21..26] = the gradient term subtracted from b.
+// J^T W J (row-major i >= j), t[21..26] = the gradient term subtracted from b.  Stereo adds the third
+// Jacobian row (types_six_dof_expmap.cpp:359-364) and a third term to every row/column sum.
 RSC_HD void po_quad_terms(const PoSE3& est, const PoCam& K, const double (&Xw)[3], double inv, double e0, double e1,
-                          bool robust, double delta, double dsqr, double (&t)[kPoseTerms]) {
+                          double e2, bool stereo, bool robust, double delta, double dsqr, double (&t)[kPoseTerms]) {
     double p[3];
     po_map(est, Xw, p);
     const double x = p[0], y = p[1];
     const double invz = 1.0 / p[2];
     const double invz_2 = invz * invz;
-    double A[2][6];
+    double A[3][6];
     A[0][0] = x * y * invz_2 * K.fx;
     A[0][1] = -(1 + (x * x * invz_2)) * K.fx;
     A[0][2] = y * invz * K.fx;
@@ -262,32 +289,49 @@ RSC_HD void po_quad_terms(const PoSE3& est, const PoCam& K, const double (&Xw)[3
     A[1][3] = 0;
     A[1][4] = -invz * K.fy;
     A[1][5] = y * invz_2 * K.fy;
+    A[2][0] = A[0][0] - K.bf * y * invz_2;
+    A[2][1] = A[0][1] + K.bf * x * invz_2;
+    A[2][2] = A[0][2];
+    A[2][3] = A[0][3];
+    A[2][4] = 0;
+    A[2][5] = A[0][5] - K.bf * invz_2;
     double Wd = inv, Wo = 0.0, rho1 = 1.0;
     if (robust) {
         double r0;
-        po_huber(po_chi2(inv, e0, e1), delta, dsqr, r0, rho1);
+        po_huber(po_chi2(inv, stereo, e0, e1, e2), delta, dsqr, r0, rho1);
         Wd = rho1 * inv;
         Wo = rho1 * 0.0;
     }
-    double tm[6][2];
+    double tm[6][3];  // A^T W
     RSC_UNROLL for (int i = 0; i < 6; ++i) {
-        tm[i][0] = A[0][i] * Wd + A[1][i] * Wo;
-        tm[i][1] = A[0][i] * Wo + A[1][i] * Wd;
+        const double a0 = A[0][i] * Wd + A[1][i] * Wo;
+        const double a1 = A[0][i] * Wo + A[1][i] * Wd;
+        tm[i][0] = stereo ? a0 + A[2][i] * Wo : a0;
+        tm[i][1] = stereo ? a1 + A[2][i] * Wo : a1;
+        tm[i][2] = (A[0][i] * Wo + A[1][i] * Wo) + A[2][i] * Wd;
     }
     int k = 0;
     RSC_UNROLL for (int i = 0; i < 6; ++i)
-        RSC_UNROLL for (int j = 0; j <= i; ++j) t[k++] = tm[i][0] * A[0][j] + tm[i][1] * A[1][j];
-    RSC_UNROLL for (int i = 0; i < 6; ++i) {
-        double g0, g1;
-        if (robust) {
-            const double a0 = rho1 * A[0][i], a1 = rho1 * A[1][i];
-            g0 = a0 * inv + a1 * 0.0;
-            g1 = a0 * 0.0 + a1 * inv;
-        } else {
-            g0 = A[0][i] * inv + A[1][i] * 0.0;
-            g1 = A[0][i] * 0.0 + A[1][i] * inv;
+        RSC_UNROLL for (int j = 0; j <= i; ++j) {
+            const double h = tm[i][0] * A[0][j] + tm[i][1] * A[1][j];
+            t[k++] = stereo ? h + tm[i][2] * A[2][j] : h;
         }
-        t[21 + i] = g0 * e0 + g1 * e1;
+    RSC_UNROLL for (int i = 0; i < 6; ++i) {
+        double a0 = A[0][i], a1 = A[1][i], a2 = A[2][i];
+        if (robust) {
+            a0 = rho1 * a0;
+            a1 = rho1 * a1;
+            a2 = rho1 * a2;
+        }
+        double g0 = a0 * inv + a1 * 0.0;
+        double g1 = a0 * 0.0 + a1 * inv;
+        const double g2 = (a0 * 0.0 + a1 * 0.0) + a2 * inv;
+        if (stereo) {
+            g0 = g0 + a2 * 0.0;
+            g1 = g1 + a2 * 0.0;
+        }
+        const double gb = g0 * e0 + g1 * e1;
+        t[21 + i] = stereo ? gb + g2 * e2 : gb;
     }
 }
 
@@ -383,6 +427,7 @@ RSC_HD bool po_ldlt_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[
 
 #if defined(__HIPCC__)
 hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st);
+hipError_t poseopt_prepare_device();
 #endif
 
 }  // namespace rsc

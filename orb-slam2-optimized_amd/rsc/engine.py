@@ -76,7 +76,7 @@ class Sim3Result(C.Structure):
 class PoseOptProblem(C.Structure):
     _fields_ = [("n", C.c_int32), ("has_mp", C.c_void_p), ("uv", C.c_void_p), ("Xw", C.c_void_p),
                 ("inv_sigma2", C.c_void_p), ("u_right", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float),
-                ("cx", C.c_float), ("cy", C.c_float), ("Tcw", C.c_float * 16)]
+                ("cx", C.c_float), ("cy", C.c_float), ("Tcw", C.c_float * 16), ("bf", C.c_float)]
 
 
 class BowFeatures(C.Structure):
@@ -779,11 +779,15 @@ class PoseOptBatch:
             arrs = [np.ascontiguousarray(f.has_mp, np.uint8), np.ascontiguousarray(f.uv, np.float32).reshape(-1),
                     np.ascontiguousarray(f.Xw, np.float32).reshape(-1),
                     np.ascontiguousarray(f.inv_sigma2, np.float32)]
+            ur = getattr(f, "u_right", None)
+            if ur is not None:
+                arrs.append(np.ascontiguousarray(ur, np.float32))
             self.keep.append(arrs)
             p = self.probs[i]
             p.n = f.n
-            p.has_mp, p.uv, p.Xw, p.inv_sigma2 = (a.ctypes.data for a in arrs)
-            p.u_right = None
+            p.has_mp, p.uv, p.Xw, p.inv_sigma2 = (a.ctypes.data for a in arrs[:4])
+            p.u_right = arrs[4].ctypes.data if ur is not None else None
+            p.bf = float(getattr(f, "bf", 0.0))
             p.fx, p.fy, p.cx, p.cy = float(f.fx), float(f.fy), float(f.cx), float(f.cy)
             p.Tcw[:] = [float(v) for v in np.asarray(f.Tcw, np.float32).reshape(16)]
             o = np.full(max(f.n, 1), 255, np.uint8)
@@ -807,7 +811,8 @@ class PoseOptBatch:
 def pose_optimization_many(ctx: Context, frames, with_outliers: bool = True):
     """Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) on every frame in one launch.
 
-    frames: objects with has_mp, uv, Xw, inv_sigma2, Tcw, fx..cy (rsc.synth.PoseOptFrame).  Returns
+    frames: objects with has_mp, uv, Xw, inv_sigma2, Tcw, fx..cy and optionally u_right (mvuRight,
+    >= 0 on stereo slots) + bf (rsc.synth.PoseOptFrame).  Returns
     per frame a dict: n_good (the reference's return value), n_initial, rounds, lm_iterations,
     lm_trials, Tcw float32[4,4] (pFrame->mTcw after the call), outlier uint8[n] (mvbOutlier; 255 on
     slots without a map point)."""

@@ -177,7 +177,8 @@ def make_sim3_pair(rng: np.random.Generator, n1: int, n_inliers: int, invalid_fr
 
 @dataclasses.dataclass
 class PoseOptFrame:
-    """Optimizer::PoseOptimization inputs (Optimizer.cpp:205-318) for one monocular Frame."""
+    """Optimizer::PoseOptimization inputs (Optimizer.cpp:205-325) for one Frame (monocular, or stereo
+    slots where u_right >= 0)."""
     has_mp: np.ndarray      # uint8 [n]   mvpMapPoints[i] != NULL
     uv: np.ndarray          # float32 [n,2] mvKeysUn[i].pt
     Xw: np.ndarray          # float32 [n,3] MapPoint::GetWorldPos() (0 where has_mp == 0)
@@ -190,15 +191,24 @@ class PoseOptFrame:
     fy: np.float32 = FY
     cx: np.float32 = CX
     cy: np.float32 = CY
+    u_right: np.ndarray = None  # float32 [n] mvuRight (-1: monocular slot), None: monocular Frame
+    bf: np.float32 = np.float32(0.0)
 
     @property
     def n(self) -> int:
         return int(self.uv.shape[0])
 
 
+# EuRoC.yaml stereo rig (Camera.bf: baseline 0.110 m x fx)
+EUROC_BF = np.float32(47.90639384423901)
+
+
 def make_poseopt_frame(rng: np.random.Generator, n: int, inlier_ratio: float = 0.8, rot_noise: float = 0.02,
-                       trans_noise: float = 0.05, no_mp_frac: float = 0.0, noise: bool = True) -> PoseOptFrame:
-    """A PnP-shaped scene whose initial Tcw is the true pose perturbed like a RANSAC estimate."""
+                       trans_noise: float = 0.05, no_mp_frac: float = 0.0, noise: bool = True,
+                       stereo_frac: float = 0.0) -> PoseOptFrame:
+    """A PnP-shaped scene whose initial Tcw is the true pose perturbed like a RANSAC estimate.
+    stereo_frac > 0: that share of the slots carries a right-image coordinate mvuRight = u - bf/z
+    (+ the same pixel noise, outliers displaced), the rest are monocular (-1)."""
     sc = make_pnp_scene(rng, n, inlier_ratio, noise=noise)
     dR = random_rotation(rng, rot_noise)
     R0 = dR @ sc.R_true
@@ -212,8 +222,19 @@ def make_poseopt_frame(rng: np.random.Generator, n: int, inlier_ratio: float = 0
     Xw = sc.p3dw.copy()
     Xw[has == 0] = 0.0
     inv = (np.float32(1.0) / sc.sigma2).astype(np.float32)
-    return PoseOptFrame(has_mp=has, uv=sc.p2d, Xw=Xw, inv_sigma2=inv, Tcw=T, R_true=sc.R_true, t_true=sc.t_true,
-                        inlier_true=sc.inlier_true)
+    fr = PoseOptFrame(has_mp=has, uv=sc.p2d, Xw=Xw, inv_sigma2=inv, Tcw=T, R_true=sc.R_true, t_true=sc.t_true,
+                      inlier_true=sc.inlier_true)
+    if stereo_frac > 0:
+        pc = sc.p3dw.astype(np.float64) @ sc.R_true.T + sc.t_true
+        z = np.maximum(pc[:, 2], 1e-3)
+        ur = sc.p2d[:, 0].astype(np.float64) - float(EUROC_BF) / z
+        if noise:
+            ur = ur + rng.normal(size=n) * np.sqrt(sc.sigma2)
+        ur = np.where(sc.inlier_true, ur, ur + rng.uniform(-40, 40, size=n))
+        st = (rng.random(n) < stereo_frac) & (ur >= 0.0)  # no right match off the image: monocular slot
+        fr.u_right = np.where(st, ur, -1.0).astype(np.float32)
+        fr.bf = EUROC_BF
+    return fr
 
 
 @dataclasses.dataclass

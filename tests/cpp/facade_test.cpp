@@ -76,7 +76,7 @@ struct PFrame {
     std::vector<float> mvuRight;
     std::vector<bool> mvbOutlier;
     std::vector<float> mvInvLevelSigma2;
-    float fx, fy, cx, cy;
+    float fx, fy, cx, cy, mbf;
     Mat4 mTcw;
     int set_pose_calls = 0;
     void SetPose(const Mat4& T) { mTcw = T; set_pose_calls++; }
@@ -151,11 +151,12 @@ int main(int argc, char** argv) {
             for (bool v : inl) wr<uint8_t>(out, v ? 1 : 0);
         }
     } else if (mode == 4) {
-        // Optimizer::PoseOptimization on a mock Frame: n slots, fx..cy, Tcw, levels of
+        // Optimizer::PoseOptimization on a mock Frame: n slots, fx..cy, mbf, Tcw, levels of
         // mvInvLevelSigma2, per slot (present, u, v, octave, X, uR)
         PFrame F;
         const int n = rd<int32_t>(in);
         F.fx = rd<float>(in); F.fy = rd<float>(in); F.cx = rd<float>(in); F.cy = rd<float>(in);
+        F.mbf = rd<float>(in);
         for (int r = 0; r < 4; ++r) for (int c = 0; c < 4; ++c) F.mTcw.m[r][c] = rd<float>(in);
         const int nl = rd<int32_t>(in);
         for (int l = 0; l < nl; ++l) F.mvInvLevelSigma2.push_back(rd<float>(in));

@@ -335,12 +335,18 @@ int he_mlpnp_count(const double* R, const double* t, const float* K, float th2, 
 // functions and the same edge-order folds.  xw4 [n][4] = (X, Y, Z, invSigma2), uv [n][2].
 // out[16]: Tcw rows 0..2, then n_good, rounds, lm_iterations, lm_trials (as int bits).
 void he_pose_optimization(int n, const float* xw4, const float* uv, const float* K4, const float* T12, float* out,
-                          uint8_t* outlier) {
+                          uint8_t* outlier, const float* ur /* nullable: all mono */, float bf) {
     using namespace rsc;
-    const PoCam K{(double)K4[0], (double)K4[1], (double)K4[2], (double)K4[3]};
-    const float deltaMono = std::sqrt(5.991);
-    const double delta = deltaMono, dsqr = delta * delta;
-    std::vector<double> err(2 * (size_t)n, 0.0);
+    const PoCam K{(double)K4[0], (double)K4[1], (double)K4[2], (double)K4[3], (double)bf};
+    const float deltaMono = std::sqrt(5.991), deltaStereo = std::sqrt(7.815);
+    const double dm = deltaMono, dm2 = dm * dm, ds = deltaStereo, ds2 = ds * ds;
+    auto stereo = [&](int e) { return ur && ur[e] >= 0.0f; };
+    std::vector<double> err(3 * (size_t)n, 0.0);
+    auto edge_error = [&](const PoSE3& est, int e) {
+        const double X[3] = {xw4[4 * e], xw4[4 * e + 1], xw4[4 * e + 2]};
+        po_error(est, K, X, uv[2 * e], uv[2 * e + 1], stereo(e) ? ur[e] : 0.0, stereo(e), err[3 * e], err[3 * e + 1],
+                 err[3 * e + 2]);
+    };
     std::vector<uint8_t> lvl(n, 0);
     double R0[3][3], t0[3];
     for (int r = 0; r < 3; ++r) {
@@ -355,9 +361,10 @@ void he_pose_optimization(int n, const float* xw4, const float* uv, const float*
         for (int e = 0; e < n; ++e) {
             double t = 0.0;
             if (lvl[e] == 0) {
-                const double X[3] = {xw4[4 * e], xw4[4 * e + 1], xw4[4 * e + 2]};
-                po_error(est, K, X, uv[2 * e], uv[2 * e + 1], err[2 * e], err[2 * e + 1]);
-                t = po_chi_term(robust, xw4[4 * e + 3], err[2 * e], err[2 * e + 1], delta, dsqr);
+                edge_error(est, e);
+                const bool st = stereo(e);
+                t = po_chi_term(robust, st, xw4[4 * e + 3], err[3 * e], err[3 * e + 1], err[3 * e + 2], st ? ds : dm,
+                                st ? ds2 : dm2);
             }
             acc = acc + t;
         }
@@ -371,7 +378,9 @@ void he_pose_optimization(int n, const float* xw4, const float* uv, const float*
             for (int k = 0; k < kPoseTerms; ++k) t[k] = 0.0;
             if (lvl[e] == 0) {
                 const double X[3] = {xw4[4 * e], xw4[4 * e + 1], xw4[4 * e + 2]};
-                po_quad_terms(est, K, X, xw4[4 * e + 3], err[2 * e], err[2 * e + 1], robust, delta, dsqr, t);
+                const bool st = stereo(e);
+                po_quad_terms(est, K, X, xw4[4 * e + 3], err[3 * e], err[3 * e + 1], err[3 * e + 2], st, robust,
+                              st ? ds : dm, st ? ds2 : dm2, t);
             }
             for (int k = 0; k < kPoseTerms; ++k) acc[k] = (k >= 21) ? acc[k] - t[k] : acc[k] + t[k];
         }
@@ -447,12 +456,9 @@ void he_pose_optimization(int n, const float* xw4, const float* uv, const float*
         }
         nBad = 0;
         for (int e = 0; e < n; ++e) {
-            if (lvl[e]) {
-                const double X[3] = {xw4[4 * e], xw4[4 * e + 1], xw4[4 * e + 2]};
-                po_error(est, K, X, uv[2 * e], uv[2 * e + 1], err[2 * e], err[2 * e + 1]);
-            }
-            const float c2 = (float)po_chi2(xw4[4 * e + 3], err[2 * e], err[2 * e + 1]);
-            const bool bad = c2 > 5.991f;
+            if (lvl[e]) edge_error(est, e);
+            const float c2 = (float)po_chi2(xw4[4 * e + 3], stereo(e), err[3 * e], err[3 * e + 1], err[3 * e + 2]);
+            const bool bad = c2 > (stereo(e) ? 7.815f : 5.991f);
             lvl[e] = bad;
             outlier[e] = bad;
             nBad += bad;

@@ -33,7 +33,7 @@ def lib():
         L.he_mlpnp_count.argtypes = [f64p, f64p, f32p, C.c_float, C.c_int, f32p, f32p, u8p]
         L.he_sim3_hypothesis.argtypes = [u32p, C.c_int, C.c_int, C.c_int, f32p, f32p, i32p, f32p]
         L.he_sim3_count.argtypes = [f32p, f32p, f32p, C.c_int, f32p, f32p, f32p, f32p, u64p, u64p, u8p]
-        L.he_pose_optimization.argtypes = [C.c_int, f32p, f32p, f32p, f32p, f32p, u8p]
+        L.he_pose_optimization.argtypes = [C.c_int, f32p, f32p, f32p, f32p, f32p, u8p, C.c_void_p, C.c_float]
         _lib = L
     return _lib
 
@@ -173,8 +173,11 @@ def pose_optimization(frame):
     T12 = np.ascontiguousarray(frame.Tcw[:3], np.float32).reshape(12)
     out = np.zeros(16, np.float32)
     outl = np.zeros(max(n, 1), np.uint8)
+    ur = getattr(frame, "u_right", None)
+    ur = None if ur is None else np.ascontiguousarray(np.asarray(ur, np.float32)[sel])
     lib().he_pose_optimization(n, xw4.reshape(-1) if n else np.zeros(4, np.float32), uv.reshape(-1) if n else
-                               np.zeros(2, np.float32), K, T12, out, outl)
+                               np.zeros(2, np.float32), K, T12, out, outl,
+                               None if ur is None else ur.ctypes.data, float(getattr(frame, "bf", 0.0)))
     ints = out[12:].view(np.int32)
     T = np.eye(4, dtype=np.float32)
     T[:3] = out[:12].reshape(3, 4)

@@ -47,10 +47,10 @@ def lib():
     L = C.CDLL(LIB_PATH)
     vp = C.c_void_p
     L.ora_pose_optimization.argtypes = [C.c_int, u8p, f32p, f32p, f32p, C.c_float, C.c_float, C.c_float,
-                                        C.c_float, f32p, f32p, u8p, i32p]
+                                        C.c_float, f32p, f32p, u8p, i32p, C.c_void_p, C.c_float]
     L.ora_pose_optimization.restype = C.c_int
     L.ora_pose_optimization_batch.argtypes = [C.c_int, i64p, f32p, f32p, f32p, C.c_float, C.c_float, C.c_float,
-                                              C.c_float, f32p, f32p, u8p, i32p]
+                                              C.c_float, f32p, f32p, u8p, i32p, C.c_void_p, C.c_float]
     L.ora_glibc_rand.argtypes = [C.c_uint32, C.c_int, i32p]
     L.ora_sample_stream.argtypes = [C.c_uint32, C.c_int, C.c_int, C.c_int, i32p]
     L.ora_pnp_create.restype = vp
@@ -364,11 +364,14 @@ def pose_optimization(frame):
     T = np.zeros(16, np.float32)
     out = np.full(n, 255, np.uint8)
     st = np.zeros(3, np.int32)
+    ur = getattr(frame, "u_right", None)
+    ur = None if ur is None else np.ascontiguousarray(ur, np.float32)
     r = L.ora_pose_optimization(n, np.ascontiguousarray(frame.has_mp, np.uint8),
                                 np.ascontiguousarray(frame.uv, np.float32),
                                 np.ascontiguousarray(frame.Xw, np.float32),
                                 np.ascontiguousarray(frame.inv_sigma2, np.float32), frame.fx, frame.fy, frame.cx,
-                                frame.cy, np.ascontiguousarray(frame.Tcw, np.float32).reshape(16), T, out, st)
+                                frame.cy, np.ascontiguousarray(frame.Tcw, np.float32).reshape(16), T, out, st,
+                                None if ur is None else ur.ctypes.data, float(getattr(frame, "bf", 0.0)))
     if r == 0 and not T.any():
         T = np.ascontiguousarray(frame.Tcw, np.float32).reshape(16).copy()
     return r, T.reshape(4, 4), out, st

@@ -80,6 +80,67 @@ def test_device_numerics_match_oracle_bitwise(block):
         assert np.array_equal(st, st2)
 
 
+def test_stereo_noise_free_recovers_pose():
+    """Known answer with EdgeStereoSE3ProjectXYZOnlyPose edges (mvuRight >= 0): exact (u, v, u_right)
+    observations, perturbed start -> the true pose, no outliers (Optimizer.cpp:290-323)."""
+    for seed, n, sf in [(11, 300, 1.0), (12, 800, 0.7), (13, 60, 0.5)]:
+        f = frame(seed, n, 1.0, noise=False, rot_noise=0.05, trans_noise=0.1, stereo_frac=sf)
+        assert (f.u_right >= 0).sum() > 0
+        r, T, out, st = ol.pose_optimization(f)
+        assert r == n and not out.any()
+        assert np.abs(T[:3, :3] - f.R_true).max() < 1e-5
+        assert np.abs(T[:3, 3] - f.t_true).max() < 1e-5
+
+
+def test_stereo_outliers_use_7815_threshold():
+    """Stereo edges are classified against chi2 > 7.815 (chi2Stereo), mono edges against 5.991: a
+    stereo edge whose only error is a right-image offset with chi2 between the two thresholds stays an
+    inlier; the same offset on u (mono) is an outlier."""
+    f = frame(14, 200, 1.0, noise=False, rot_noise=0.0, trans_noise=0.0, stereo_frac=1.0)
+    f.Tcw[:3, :3] = f.R_true.astype(np.float32)
+    f.Tcw[:3, 3] = f.t_true.astype(np.float32)
+    k = 5
+    off = np.float32(np.sqrt(6.9 / f.inv_sigma2[k]))  # chi2 = inv * off^2 = 6.9 in (5.991, 7.815]
+    f.u_right[k] += off
+    r, T, out, st = ol.pose_optimization(f)
+    assert out[k] == 0
+    g = frame(14, 200, 1.0, noise=False, rot_noise=0.0, trans_noise=0.0)
+    g.Tcw[:3, :3] = g.R_true.astype(np.float32)
+    g.Tcw[:3, 3] = g.t_true.astype(np.float32)
+    g.uv[k, 0] += off
+    r, T, out, st = ol.pose_optimization(g)
+    assert out[k] == 1
+
+
+def test_stereo_gross_outliers_flagged():
+    f = frame(15, 900, 0.7, stereo_frac=0.8)
+    r, T, out, st = ol.pose_optimization(f)
+    assert (out[~f.inlier_true] == 1).all()
+    assert r == int((out == 0).sum())
+    assert np.abs(T[:3, 3] - f.t_true).max() < 0.01
+
+
+@pytest.mark.parametrize("block", range(3))
+def test_device_numerics_stereo_match_oracle_bitwise(block):
+    """Mixed mono/stereo Frames (stereo share 0..100 %): rsc_poseopt.h host build == the oracle."""
+    rng = np.random.default_rng(950 + block)
+    for _ in range(20):
+        n = int(rng.integers(3, 700))
+        f = synth.make_poseopt_frame(rng, n, float(rng.uniform(0.3, 1.0)), rot_noise=float(rng.uniform(0, 0.15)),
+                                     trans_noise=float(rng.uniform(0, 0.4)),
+                                     no_mp_frac=float(rng.choice([0.0, 0.2])),
+                                     stereo_frac=float(rng.choice([0.3, 0.6, 0.9, 1.0])))
+        if int(f.has_mp.sum()) < 3:
+            continue
+        r, T, out, st = ol.pose_optimization(f)
+        r2, T2, out2, st2 = hl.pose_optimization(f)
+        sel = np.nonzero(f.has_mp)[0]
+        assert r == r2
+        assert np.array_equal(T.view(np.uint32), T2.view(np.uint32))
+        assert np.array_equal(out[sel], out2)
+        assert np.array_equal(st, st2)
+
+
 def test_golden_regression():
     """Committed outputs of the oracle (tests/golden/poseopt_traces.npz, make_golden.py)."""
     import os

@@ -161,17 +161,20 @@ def test_mlpnp_facade_matches_oracle():
             assert ml == 0
 
 
-def test_pose_optimization_facade_matches_oracle():
-    """rsc_orb::PoseOptimization(Frame*) (Optimizer.cpp:205-424) on a mock Frame: slots without a
-    MapPoint keep mvbOutlier, SetPose is called once, nGood / pose / flags equal the oracle."""
+@pytest.mark.parametrize("stereo", [0.0, 0.75])
+def test_pose_optimization_facade_matches_oracle(stereo):
+    """rsc_orb::PoseOptimization(Frame*) (Optimizer.cpp:205-424) on a mock Frame (monocular, or with
+    75 % stereo slots mvuRight >= 0): slots without a MapPoint keep mvbOutlier, SetPose is called once,
+    nGood / pose / flags equal the oracle."""
     rng = np.random.default_rng(31)
-    f = synth.make_poseopt_frame(rng, 900, 0.75, no_mp_frac=0.2)
+    f = synth.make_poseopt_frame(rng, 900, 0.75, no_mp_frac=0.2, stereo_frac=stereo)
+    ur = f.u_right if f.u_right is not None else np.full(f.n, -1.0, np.float32)
     inv_levels = (np.float32(1.0) / synth.level_sigma2()).astype(np.float32)
     oc = np.array([int(np.where(inv_levels == v)[0][0]) for v in f.inv_sigma2])
-    buf = struct.pack("<i", 4) + struct.pack("<i4f", f.n, f.fx, f.fy, f.cx, f.cy)
+    buf = struct.pack("<i", 4) + struct.pack("<i5f", f.n, f.fx, f.fy, f.cx, f.cy, f.bf)
     buf += f.Tcw.astype("<f4").tobytes() + struct.pack("<i", len(inv_levels)) + inv_levels.astype("<f4").tobytes()
     for i in range(f.n):
-        buf += struct.pack("<i2fi3ff", int(f.has_mp[i]), f.uv[i, 0], f.uv[i, 1], oc[i], *f.Xw[i], -1.0)
+        buf += struct.pack("<i2fi3ff", int(f.has_mp[i]), f.uv[i, 0], f.uv[i, 1], oc[i], *f.Xw[i], ur[i])
     out = run(buf)
     n_good, calls = struct.unpack_from("<ii", out, 0)
     T = np.frombuffer(out, "<f4", 16, 8).reshape(4, 4)

@@ -57,3 +57,24 @@ def test_relocalization_batch_64x2000():
     rng = np.random.default_rng(79)
     frames = [synth.make_poseopt_frame(rng, 2000, 0.6) for _ in range(64)]
     check(frames)
+
+
+def test_stereo_frames_bitexact():
+    """EdgeStereoSE3ProjectXYZOnlyPose (Optimizer.cpp:290-323; the reference's stereo_euroc /
+    stereo_kitti builds): Frames with 60-100 % stereo slots, mixed sizes and outlier ratios."""
+    rng = np.random.default_rng(81)
+    frames = []
+    for _ in range(40):
+        n = int(rng.integers(3, 1200))
+        frames.append(synth.make_poseopt_frame(rng, n, float(rng.uniform(0.3, 1.0)),
+                                               rot_noise=float(rng.uniform(0, 0.15)),
+                                               trans_noise=float(rng.uniform(0, 0.4)),
+                                               no_mp_frac=float(rng.choice([0.0, 0.25])),
+                                               stereo_frac=float(rng.uniform(0.6, 1.0))))
+    check(frames)
+
+
+def test_stereo_relocalization_batch_64x2000():
+    rng = np.random.default_rng(82)
+    frames = [synth.make_poseopt_frame(rng, 2000, 0.6, stereo_frac=0.8) for _ in range(64)]
+    check(frames)
