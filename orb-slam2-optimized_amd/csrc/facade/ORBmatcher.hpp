@@ -12,9 +12,21 @@
 //     int nmatches = matcher.SearchByBoW(mpCurrentKF, pKF, vvpMapPointMatches[i]);   // LoopClosing.cpp:251
 // and the batched forms run a whole candidate loop (Tracking.cpp:1207-1232,
 // LoopClosing.cpp:238-265) in one launch with the shared view uploaded once.
+//
+// SearchBySim3 (ORBmatcher.cpp:948-1170, LoopClosing.cpp:309) additionally needs, per KeyFrame,
+// mvKeysUn[i].pt/.octave, mDescriptors, fx..cy, mnMinX..mnMaxY, mfGridElementWidth/HeightInv,
+// mvScaleFactors, mnScaleLevels, mfLogScaleFactor, GetRotation(), GetTranslation(),
+// GetMapPointMatches(); per MapPoint isBad(), GetWorldPos(), GetDescriptor() (one cv::Mat row),
+// GetIndexInKeyFrame(pKF).  Three members the reference keeps protected are read through the
+// customization points below, whose defaults call one-line getters INTEGRATION.md §2 adds to the
+// reference: KeyFrame::GetGrid() (mGrid: the grid cannot be rebuilt from the KeyFrame's integer
+// image bounds, Frame assigned it with float bounds) and MapPoint::GetMaxDistance()/GetMinDistance()
+// (mfMaxDistance/mfMinDistance: GetMaxDistanceInvariance() returns 1.2f*mfMaxDistance, which does
+// not round-trip in float).
 #pragma once
 #include <algorithm>
 #include <memory>
+#include <stdexcept>
 #include <vector>
 #include "rsc_context.hpp"
 
@@ -79,6 +91,93 @@ template <class FrameT>
 BowUpload upload_frame(const FrameT& F) {
     BowUpload u;
     u.build(F, [&](int i) { return (float)F.mvKeys[i].angle; }, [](int) { return true; });
+    return u;
+}
+
+// ---- SearchBySim3 ----------------------------------------------------------------------------------
+// Customization points (specialise for types with other accessors).
+template <class KF>
+const auto& kf_grid(const KF& kf) { return kf.GetGrid(); }                   // KeyFrame::mGrid
+template <class MP>
+float mp_max_distance(MP& mp) { return mp.GetMaxDistance(); }                // MapPoint::mfMaxDistance
+template <class MP>
+float mp_min_distance(MP& mp) { return mp.GetMinDistance(); }                // MapPoint::mfMinDistance
+
+// A KeyFrame's SearchBySim3 inputs uploaded to HBM (rsc_kfview_create).
+struct KFViewUpload {
+    rsc_kfview* h = nullptr;
+    int n = 0;
+    KFViewUpload() = default;
+    KFViewUpload(const KFViewUpload&) = delete;
+    KFViewUpload& operator=(const KFViewUpload&) = delete;
+    KFViewUpload(KFViewUpload&& o) noexcept : h(o.h), n(o.n) { o.h = nullptr; }
+    ~KFViewUpload() { rsc_kfview_destroy(h); }
+};
+
+template <class KFPtr, class MPPtr>
+KFViewUpload upload_kfview(const KFPtr& pKF, const std::vector<MPPtr>& mps) {
+    const auto& K = *pKF;
+    const int n = (int)K.N;
+    std::vector<float> kp(2 * (size_t)n), pos(3 * (size_t)n, 0.f), dmax((size_t)n, 0.f), dmin((size_t)n, 0.f);
+    std::vector<int32_t> oct((size_t)n);
+    std::vector<uint8_t> desc(32 * (size_t)n), state((size_t)n, 0), mdesc(32 * (size_t)n, 0);
+    for (int i = 0; i < n; ++i) {
+        kp[2 * i] = K.mvKeysUn[i].pt.x;
+        kp[2 * i + 1] = K.mvKeysUn[i].pt.y;
+        oct[i] = K.mvKeysUn[i].octave;
+        const uint8_t* row = K.mDescriptors.template ptr<uint8_t>(i);
+        std::copy(row, row + 32, desc.begin() + 32 * (size_t)i);
+        if ((size_t)i >= mps.size() || !mps[i]) continue;  // vpMapPoints[i] NULL
+        auto& mp = *mps[i];
+        if (mp.isBad()) { state[i] = 2; continue; }
+        state[i] = 1;
+        const auto X = mp.GetWorldPos();
+        for (int c = 0; c < 3; ++c) pos[3 * i + c] = X(c);
+        dmax[i] = mp_max_distance(mp);
+        dmin[i] = mp_min_distance(mp);
+        const auto d = mp.GetDescriptor();
+        const uint8_t* dr = d.template ptr<uint8_t>(0);
+        std::copy(dr, dr + 32, mdesc.begin() + 32 * (size_t)i);
+    }
+    const auto& grid = kf_grid(K);  // mGrid[ix][iy] -> CSR over cell = ix * 48 + iy
+    if (grid.size() != 64) throw std::runtime_error("rsc: SearchBySim3: FRAME_GRID_COLS must be 64");
+    std::vector<int32_t> begin(1, 0), feat;
+    for (int ix = 0; ix < 64; ++ix) {
+        if (grid[ix].size() != 48) throw std::runtime_error("rsc: SearchBySim3: FRAME_GRID_ROWS must be 48");
+        for (int iy = 0; iy < 48; ++iy) {
+            for (auto f : grid[ix][iy]) feat.push_back((int32_t)f);
+            begin.push_back((int32_t)feat.size());
+        }
+    }
+    if (feat.empty()) feat.push_back(0);
+    rsc_sim3_kf k;
+    k.n = n;
+    k.kp = kp.data();
+    k.octave = oct.data();
+    k.desc = desc.data();
+    k.cell_begin = begin.data();
+    k.cell_feat = feat.data();
+    k.min_x = (float)K.mnMinX; k.max_x = (float)K.mnMaxX; k.min_y = (float)K.mnMinY; k.max_y = (float)K.mnMaxY;
+    k.grid_w_inv = K.mfGridElementWidthInv;
+    k.grid_h_inv = K.mfGridElementHeightInv;
+    k.fx = K.fx; k.fy = K.fy; k.cx = K.cx; k.cy = K.cy;
+    k.scale_factors = K.mvScaleFactors.data();
+    k.n_levels = (int32_t)K.mnScaleLevels;
+    k.log_scale_factor = K.mfLogScaleFactor;
+    const auto R = pKF->GetRotation();
+    const auto t = pKF->GetTranslation();
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) k.Rcw[3 * r + c] = R(r, c);
+        k.tcw[r] = t(r);
+    }
+    k.mp_state = state.data();
+    k.mp_pos = pos.data();
+    k.mp_dmax = dmax.data();
+    k.mp_dmin = dmin.data();
+    k.mp_desc = mdesc.data();
+    KFViewUpload u;
+    u.n = n;
+    check(rsc_kfview_create(thread_context(), &k, &u.h), "rsc_kfview_create");
     return u;
 }
 
@@ -167,6 +266,77 @@ public:
             for (int i = 0; i < kf1.n && i < n1; ++i)
                 if (idx[c][i] >= 0) out[c][i] = mps[c][idx[c][i]];
         return std::vector<int>(nm.begin(), nm.begin() + C);
+    }
+
+    // SearchBySim3(pKF1, pKF2, vpMatches12, R12, t12, th) (ORBmatcher.cpp:948-1170;
+    // LoopClosing.cpp:309 after a Sim3Solver success): new mutual matches are written into
+    // vpMatches12 (entries already set are kept), returns their number.
+    template <class KFPtr, class MPPtr, class Mat3, class Vec3>
+    int SearchBySim3(KFPtr pKF1, KFPtr pKF2, std::vector<MPPtr>& vpMatches12, const Mat3& R12, const Vec3& t12,
+                     const float th) {
+        std::vector<std::vector<MPPtr>*> m(1, &vpMatches12);
+        std::vector<KFPtr> a(1, pKF1), b(1, pKF2);
+        float R[9], t[3];
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) R[3 * r + c] = R12(r, c);
+            t[r] = t12(r);
+        }
+        return SearchBySim3Many(a, b, m, R, t, th)[0];
+    }
+
+    // SearchBySim3 of several (pKF1[c], pKF2[c]) pairs in one launch; R12 [count][9] row-major,
+    // t12 [count][3].  Each KeyFrame object is uploaded once.
+    template <class KFPtr, class MPPtr>
+    std::vector<int> SearchBySim3Many(const std::vector<KFPtr>& pKF1, const std::vector<KFPtr>& pKF2,
+                                      const std::vector<std::vector<MPPtr>*>& vpMatches12, const float* R12,
+                                      const float* t12, const float th) {
+        const int C = (int)pKF1.size();
+        std::vector<const void*> keys;
+        std::vector<detail::KFViewUpload> views;
+        std::vector<std::vector<MPPtr>> mps;
+        auto view_of = [&](const KFPtr& k) {
+            for (size_t j = 0; j < keys.size(); ++j)
+                if (keys[j] == (const void*)&*k) return (int)j;
+            keys.push_back((const void*)&*k);
+            mps.push_back(k->GetMapPointMatches());
+            views.push_back(detail::upload_kfview(k, mps.back()));
+            return (int)keys.size() - 1;
+        };
+        std::vector<int> v1(C), v2(C);
+        for (int c = 0; c < C; ++c) {
+            v1[c] = view_of(pKF1[c]);
+            v2[c] = view_of(pKF2[c]);
+        }
+        std::vector<rsc_kfview*> h1(C), h2(C);
+        std::vector<std::vector<int32_t>> in(C), out(C);
+        std::vector<const int32_t*> pin(C);
+        std::vector<int32_t*> pout(C);
+        for (int c = 0; c < C; ++c) {
+            h1[c] = views[v1[c]].h;
+            h2[c] = views[v2[c]].h;
+            const int n1 = views[v1[c]].n;
+            const std::vector<MPPtr>& m = *vpMatches12[c];
+            in[c].assign(n1 > 0 ? n1 : 1, -1);
+            out[c].assign(n1 > 0 ? n1 : 1, -1);
+            for (int i = 0; i < n1 && (size_t)i < m.size(); ++i) {  // vbAlreadyMatched1/2 (:980-990)
+                if (!m[i]) continue;
+                const int idx2 = m[i]->GetIndexInKeyFrame(pKF2[c]);
+                in[c][i] = (idx2 >= 0 && idx2 < views[v2[c]].n) ? idx2 : -2;
+            }
+            pin[c] = in[c].data();
+            pout[c] = out[c].data();
+        }
+        std::vector<int32_t> nfound(C > 0 ? C : 1, 0);
+        check(rsc_search_by_sim3_many(thread_context(), h1.data(), h2.data(), C, R12, t12, th, pin.data(), pout.data(),
+                                      nfound.data()),
+              "SearchBySim3");
+        for (int c = 0; c < C; ++c) {  // vpMatches12[i1] = vpMapPoints2[idx2] (:1160-1166)
+            std::vector<MPPtr>& m = *vpMatches12[c];
+            const std::vector<MPPtr>& mp2 = mps[v2[c]];
+            for (int i = 0; i < views[v1[c]].n && (size_t)i < m.size(); ++i)
+                if (out[c][i] >= 0) m[i] = mp2[out[c][i]];
+        }
+        return std::vector<int>(nfound.begin(), nfound.begin() + C);
     }
 
 private:

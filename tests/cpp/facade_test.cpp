@@ -50,6 +50,32 @@ struct BowKF {
 };
 struct BowFrame { int N = 0; DescMat mDescriptors; std::vector<KeyPoint> mvKeys; FeatVec mFeatVec; };
 
+// SearchBySim3 mocks: KeyFrame with the public members ORBmatcher::SearchBySim3 reads plus the
+// GetGrid() getter, MapPoint with GetMaxDistance()/GetMinDistance()
+struct S3KF;
+struct S3MP {
+    bool bad = false; Vec3 X; DescMat d; float dmax = 0, dmin = 0; const S3KF* home = nullptr; int idx = -1;
+    bool isBad() const { return bad; }
+    Vec3 GetWorldPos() const { return X; }
+    DescMat GetDescriptor() const { return d; }
+    float GetMaxDistance() const { return dmax; }
+    float GetMinDistance() const { return dmin; }
+    int GetIndexInKeyFrame(const std::shared_ptr<S3KF>& kf) const { return kf.get() == home ? idx : -1; }
+};
+struct S3KF {
+    int N = 0; std::vector<KeyPoint> mvKeysUn; DescMat mDescriptors;
+    int mnMinX = 0, mnMinY = 0, mnMaxX = 0, mnMaxY = 0;
+    float mfGridElementWidthInv = 0, mfGridElementHeightInv = 0, fx = 0, fy = 0, cx = 0, cy = 0;
+    std::vector<float> mvScaleFactors; int mnScaleLevels = 0; float mfLogScaleFactor = 0;
+    Mat3 R; Vec3 t;
+    std::vector<std::vector<std::vector<size_t>>> grid;
+    std::vector<std::shared_ptr<S3MP>> mps;
+    const std::vector<std::vector<std::vector<size_t>>>& GetGrid() const { return grid; }
+    Mat3 GetRotation() const { return R; }
+    Vec3 GetTranslation() const { return t; }
+    std::vector<std::shared_ptr<S3MP>> GetMapPointMatches() const { return mps; }
+};
+
 // view record: n, desc[n*32], angle[n], valid[n] (u8), nodes, per node (id, count, feats[count])
 template <class V>
 void read_view(FILE* in, V& v, std::vector<KeyPoint>& kps, std::vector<std::shared_ptr<MapPoint>>* mps);
@@ -267,6 +293,60 @@ int main(int argc, char** argv) {
             wr<int32_t>(out, (int32_t)cands.size());
             for (auto& c : cands) wr<int32_t>(out, c->idx);
         }
+    } else if (mode == 7) {
+        // ORBmatcher::SearchBySim3 through the facade: two KeyFrames (keypoints, octaves,
+        // descriptors, CSR grid, bounds, intrinsics, scale pyramid, pose, MapPoints), R12, t12, th,
+        // matched12 (KF2 index / -1 NULL / -2 a MapPoint not in KF2); writes nfound and vpMatches12
+        // after the call as KF2 indices (-1 NULL, -2 the foreign MapPoint)
+        std::shared_ptr<S3KF> kf[2] = {std::make_shared<S3KF>(), std::make_shared<S3KF>()};
+        for (auto& k : kf) {
+            const int n = rd<int32_t>(in);
+            k->N = n;
+            k->mvKeysUn.resize(n);
+            for (int i = 0; i < n; ++i) { k->mvKeysUn[i].pt.x = rd<float>(in); k->mvKeysUn[i].pt.y = rd<float>(in); }
+            for (int i = 0; i < n; ++i) k->mvKeysUn[i].octave = rd<int32_t>(in);
+            k->mDescriptors.d.resize(32 * (size_t)n);
+            if (n && fread(k->mDescriptors.d.data(), 1, 32 * (size_t)n, in) != 32 * (size_t)n) throw std::runtime_error("short read");
+            std::vector<int32_t> begin(64 * 48 + 1);
+            for (auto& b : begin) b = rd<int32_t>(in);
+            k->grid.assign(64, std::vector<std::vector<size_t>>(48));
+            for (int c = 0; c < 64 * 48; ++c)
+                for (int j = begin[c]; j < begin[c + 1]; ++j) k->grid[c / 48][c % 48].push_back((size_t)rd<int32_t>(in));
+            k->mnMinX = rd<int32_t>(in); k->mnMaxX = rd<int32_t>(in); k->mnMinY = rd<int32_t>(in); k->mnMaxY = rd<int32_t>(in);
+            k->mfGridElementWidthInv = rd<float>(in); k->mfGridElementHeightInv = rd<float>(in);
+            k->fx = rd<float>(in); k->fy = rd<float>(in); k->cx = rd<float>(in); k->cy = rd<float>(in);
+            k->mnScaleLevels = rd<int32_t>(in);
+            for (int l = 0; l < k->mnScaleLevels; ++l) k->mvScaleFactors.push_back(rd<float>(in));
+            k->mfLogScaleFactor = rd<float>(in);
+            for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) k->R.m[r][c] = rd<float>(in);
+            for (int r = 0; r < 3; ++r) k->t.v[r] = rd<float>(in);
+            k->mps.resize(n);
+            for (int i = 0; i < n; ++i) {
+                const int st = rd<uint8_t>(in);
+                auto mp = std::make_shared<S3MP>();
+                for (int c = 0; c < 3; ++c) mp->X.v[c] = rd<float>(in);
+                mp->dmax = rd<float>(in); mp->dmin = rd<float>(in);
+                mp->d.d.resize(32);
+                if (fread(mp->d.d.data(), 1, 32, in) != 32) throw std::runtime_error("short read");
+                mp->bad = st == 2; mp->home = k.get(); mp->idx = i;
+                if (st) k->mps[i] = mp;
+            }
+        }
+        Mat3 R12; Vec3 t12;
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) R12.m[r][c] = rd<float>(in);
+        for (int r = 0; r < 3; ++r) t12.v[r] = rd<float>(in);
+        const float th = rd<float>(in);
+        auto foreign = std::make_shared<S3MP>();
+        std::vector<std::shared_ptr<S3MP>> m12(kf[0]->N);
+        for (int i = 0; i < kf[0]->N; ++i) {
+            const int v = rd<int32_t>(in);
+            if (v >= 0) m12[i] = kf[1]->mps[v];
+            else if (v == -2) m12[i] = foreign;
+        }
+        rsc_orb::ORBmatcher matcher;
+        const int nf = matcher.SearchBySim3(kf[0], kf[1], m12, R12, t12, th);
+        wr<int32_t>(out, nf);
+        for (auto& mp : m12) wr<int32_t>(out, !mp ? -1 : (mp == foreign ? -2 : mp->idx));
     } else if (mode == 2) {
         auto kf1 = std::make_shared<KeyFrame>(), kf2 = std::make_shared<KeyFrame>();
         const int n1 = rd<int32_t>(in);

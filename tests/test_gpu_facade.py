@@ -278,3 +278,40 @@ def test_keyframe_database_facade_matches_oracle(seed):
         assert list(out[pos + 1:pos + 1 + n]) == list(w)
         pos += 1 + n
     assert pos == len(out)
+
+
+def _s3kf_bytes(kf):
+    from rsc import synth
+    b = struct.pack("<i", kf.n) + np.ascontiguousarray(kf.kp, "<f4").tobytes()
+    b += np.ascontiguousarray(kf.octave, "<i4").tobytes() + np.ascontiguousarray(kf.desc, np.uint8).tobytes()
+    b += np.ascontiguousarray(kf.cell_begin, "<i4").tobytes() + np.ascontiguousarray(kf.cell_feat, "<i4").tobytes()
+    b += struct.pack("<4i", int(kf.min_x), int(kf.max_x), int(kf.min_y), int(kf.max_y))
+    b += struct.pack("<6f", synth.GRID_W_INV, synth.GRID_H_INV, kf.fx, kf.fy, kf.cx, kf.cy)
+    sf = synth.scale_factors()
+    b += struct.pack("<i", len(sf)) + sf.astype("<f4").tobytes() + struct.pack("<f", synth.LOG_SCALE_FACTOR)
+    b += np.asarray(kf.Rcw, "<f4").tobytes() + np.asarray(kf.tcw, "<f4").tobytes()
+    for i in range(kf.n):
+        b += struct.pack("<B3f2f", int(kf.mp_state[i]), *kf.mp_pos[i], kf.mp_dmax[i], kf.mp_dmin[i])
+        b += np.ascontiguousarray(kf.mp_desc[i], np.uint8).tobytes()
+    return b
+
+
+@pytest.mark.parametrize("seed", [51, 52])
+def test_search_by_sim3_facade_matches_oracle(seed):
+    """rsc_orb::ORBmatcher::SearchBySim3 (ORBmatcher.cpp:948-1170, LoopClosing.cpp:309) on mock
+    KeyFrames / MapPoints (null, bad, already-matched and foreign MapPoints): nfound and vpMatches12
+    after the call equal the oracle."""
+    rng = np.random.default_rng(seed)
+    kf1, kf2, R12, t12, m12 = synth.make_sim3match_pair(rng, 700, 200, 0.3)
+    m12[rng.random(kf1.n) < 0.02] = -2
+    buf = struct.pack("<i", 7) + _s3kf_bytes(kf1) + _s3kf_bytes(kf2)
+    buf += np.asarray(R12, "<f4").tobytes() + np.asarray(t12, "<f4").tobytes() + struct.pack("<f", 7.5)
+    buf += np.asarray(m12, "<i4").tobytes()
+    out = run(buf)
+    nf = struct.unpack_from("<i", out, 0)[0]
+    got = np.frombuffer(out, "<i4", kf1.n, 4)
+    onf, o12 = ol.search_by_sim3(kf1, kf2, R12, t12, m12, 7.5)
+    o12 = o12[:kf1.n]
+    exp = np.where(o12 >= 0, o12, m12)
+    assert nf == onf and nf > 20
+    assert np.array_equal(got, exp)
