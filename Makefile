@@ -27,6 +27,10 @@ $(LIBDIR)/sim3match.o: $(CSRC)/sim3match.hip $(HDRS)
 	mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(LIBDIR)/sim3opt.o: $(CSRC)/sim3opt.hip $(HDRS)
+	mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(LIBDIR)/kfdb.o: $(CSRC)/kfdb.hip $(HDRS)
 	mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -35,7 +39,7 @@ $(LIBDIR)/rsc_api.o: $(CSRC)/rsc_api.cpp $(HDRS)
 	mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIBDIR)/librsc.so: $(LIBDIR)/kernels.o $(LIBDIR)/poseopt.o $(LIBDIR)/orbmatch.o $(LIBDIR)/sim3match.o $(LIBDIR)/kfdb.o $(LIBDIR)/rsc_api.o
+$(LIBDIR)/librsc.so: $(LIBDIR)/kernels.o $(LIBDIR)/poseopt.o $(LIBDIR)/sim3opt.o $(LIBDIR)/orbmatch.o $(LIBDIR)/sim3match.o $(LIBDIR)/kfdb.o $(LIBDIR)/rsc_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 facade_test: $(LIBDIR)/facade_test

@@ -58,7 +58,7 @@ def parse():
     p.add_argument("--strong", action="store_true", help="split one 64-candidate batch across the ranks")
     p.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-cores CPU baseline (0: auto)")
     p.add_argument("--no-cpu", action="store_true")
-    for s in ("sim3", "mlpnp", "events", "latency", "poseopt", "bow", "sim3match", "kfdb"):
+    for s in ("sim3", "mlpnp", "events", "latency", "poseopt", "bow", "sim3match", "sim3opt", "kfdb"):
         p.add_argument(f"--no-{s}", action="store_true")
     p.add_argument("--only-headline", action="store_true", help="config 2 only (PMC passes)")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -66,7 +66,7 @@ def parse():
                         "share fewer GPUs to rehearse the launch and gather on a 1-GPU box)")
     a = p.parse_args()
     if a.only_headline:
-        for s in ("sim3", "mlpnp", "events", "latency", "poseopt", "bow", "sim3match", "kfdb"):
+        for s in ("sim3", "mlpnp", "events", "latency", "poseopt", "bow", "sim3match", "sim3opt", "kfdb"):
             setattr(a, f"no_{s}", True)
     return a
 
@@ -686,6 +686,51 @@ def cpu_baseline_sim3match(probs, seconds):
                        "restatement, 1 thread")
 
 
+def sim3opt_problems(seed=83, pairs=32, n=1000):
+    """SURVEY §8(f) rank 3 (second half): Optimizer::OptimizeSim3 on 32 loop-closure pairs (config-3
+    shape: ~1000 correspondences after SearchBySim3, 25 % outliers, th2 = 10 as LoopClosing.cpp:311)."""
+    from rsc import synth
+    rng = np.random.default_rng(seed)
+    return [synth.make_sim3opt_problem(rng, n, outlier_frac=0.25) for _ in range(pairs)]
+
+
+def run_sim3opt(engine, ctx, probs, args):
+    """One rsc_optimize_sim3_many per step over the 32 pairs (inputs packed and uploaded in the call,
+    as the facade does); kernel time from HIP events in a second pass."""
+    batch = engine.Sim3OptBatch(ctx, probs)
+    for _ in range(args.warmup):
+        batch.run()
+    steps = max(1, args.steps // 2)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        batch.run()
+    dt = time.perf_counter() - t0
+    res = batch.results()
+    ctx.enable_timing(True)
+    kms = 0.0
+    for _ in range(steps):
+        batch.run()
+        kms += ctx.last_timing()["refine_ms"]
+    ctx.enable_timing(False)
+    C = len(probs)
+    return dict(pairs_per_s=C * steps / dt, ms_per_step=1e3 * dt / steps, kernel_ms=kms / steps, pairs=C,
+                correspondences_per_pair=float(np.mean([r["n_correspondences"] for r in res])),
+                mean_inliers=float(np.mean([r["n_inliers"] for r in res])),
+                lm_iterations_per_pair=float(np.mean([r["lm_iterations"] for r in res])), steps=steps)
+
+
+def cpu_baseline_sim3opt(probs):
+    """The OptimizeSim3 oracle on ONE host core over the same pairs."""
+    import oracle_lib as ol
+
+    def batch():
+        for p in probs:
+            ol.optimize_sim3(p)
+    med, n = median_batches(batch, warmup=1, reps=5)
+    return dict(value=round(len(probs) / med, 2), unit="pairs/s", cores=1, kind="port", median_batch_s=round(med, 5),
+                sample=f"{len(probs)} pairs per batch, 1 warm-up + median of {n}, oracle restatement, 1 thread")
+
+
 def kfdb_scene(seed=82, n_kfs=2000, n_queries=64):
     """a 2000-KeyFrame database (600-word BowVectors, a long EuRoC/KITTI map)
     and 64 relocalization queries (Frame BowVectors observed along the trajectory)."""
@@ -909,6 +954,14 @@ def main():
                 cb = cpu_baseline_sim3match(s3m_probs, 2.0)
                 sections["search_by_sim3"]["cpu_baseline"] = cb
                 sections["search_by_sim3"]["speedup_vs_cpu_1core"] = round(s3m["pairs_per_s"] / cb["value"], 1)
+        if not args.no_sim3opt:
+            so_probs = sim3opt_problems()
+            so = run_sim3opt(engine, ctx, so_probs, args)
+            sections["optimize_sim3"] = _rounded(so, 5)
+            if with_cpu:
+                cb = cpu_baseline_sim3opt(so_probs)
+                sections["optimize_sim3"]["cpu_baseline"] = cb
+                sections["optimize_sim3"]["speedup_vs_cpu_1core"] = round(so["pairs_per_s"] / cb["value"], 1)
         if not args.no_kfdb:
             kfdb_sc, kfdb_q = kfdb_scene()
             kf = run_kfdb(engine, ctx, kfdb_sc, kfdb_q, args)

@@ -238,6 +238,43 @@ typedef struct {
 int rsc_pose_optimization_many(rsc_context* ctx, const rsc_poseopt_problem* problems, int count,
                                rsc_poseopt_result* out, uint8_t* const* outlier);
 
+/* ---- Optimizer::OptimizeSim3 (src/Optimizer.cpp:1054-1250) ----------------------------------------
+ * The loop-closure refinement LoopClosing::ComputeSim3 runs on every candidate whose Sim3 RANSAC
+ * succeeded, right after SearchBySim3 (LoopClosing.cpp:309-311): g2o Levenberg-Marquardt of one
+ * VertexSim3Expmap (_fix_scale) over EdgeSim3ProjectXYZ / EdgeInverseSim3ProjectXYZ pairs (numeric
+ * Jacobians) with Huber kernels (delta = sqrt(th2)), optimize(5), outlier removal (chi2 > th2),
+ * optimize(5 or 10).  Parity against the reference is unpinned (g2o/Eigen cannot be built here). */
+typedef struct {
+    int32_t n;               /* vpMatches1.size() = pKF1->N (KeyFrame 1 keypoint slots) */
+    const uint8_t* valid;    /* [n] slot i is a correspondence: vpMatches1[i] and vpMapPoints1[i] set, neither
+                                isBad(), vpMatches1[i]->GetIndexInKeyFrame(pKF2) >= 0 (Optimizer.cpp:1112-1143) */
+    const float* X1w;        /* [n][3] vpMapPoints1[i]->GetWorldPos() */
+    const float* X2w;        /* [n][3] vpMatches1[i]->GetWorldPos() */
+    const float* uv1;        /* [n][2] pKF1->mvKeysUn[i].pt */
+    const float* uv2;        /* [n][2] pKF2->mvKeysUn[i2].pt, i2 = GetIndexInKeyFrame(pKF2) */
+    const float* inv1;       /* [n] pKF1->mvInvLevelSigma2[octave of i] */
+    const float* inv2;       /* [n] pKF2->mvInvLevelSigma2[octave of i2] */
+    float R1w[9], t1w[3];    /* pKF1->GetRotation(), GetTranslation() (row-major) */
+    float R2w[9], t2w[3];    /* pKF2 */
+    float K1[4], K2[4];      /* mK: fx, fy, cx, cy */
+    double S[8];             /* g2oS12 on entry: quaternion (x, y, z, w), t, s */
+    float th2;               /* 10 in LoopClosing.cpp:311 */
+} rsc_sim3opt_problem;
+
+typedef struct {
+    int32_t n_inliers;          /* return value nIn (0 when nCorrespondences - nBad < 10) */
+    int32_t n_correspondences;
+    int32_t n_bad;              /* correspondences removed after the first optimize(5) */
+    int32_t lm_iterations;      /* OptimizationAlgorithmLevenberg::solve calls */
+    int32_t lm_trials;
+    double S[8];                /* g2oS12 after the call (the entry value when n_inliers == 0) */
+} rsc_sim3opt_result;
+
+/* OptimizeSim3 on `count` KeyFrame pairs in one launch (one workgroup per pair).  keep[c] (may be
+ * NULL) receives per slot 0 where vpMatches1[i] is set to NULL (an outlier), 1 elsewhere. */
+int rsc_optimize_sim3_many(rsc_context* ctx, const rsc_sim3opt_problem* problems, int count,
+                           rsc_sim3opt_result* out, uint8_t* const* keep);
+
 /* ---- ORBmatcher::SearchByBoW (src/ORBmatcher.cpp:110-240, :354-488) -----------------------------
  * The producer of every RANSAC correspondence set: Hamming-256 matching of ORB descriptors that
  * share a DBoW2 FeatureVector node, with the nearest-neighbour ratio test and the rotation-histogram

@@ -12,6 +12,7 @@
 #include "sim3_oracle.h"
 #include "mlpnp_oracle.h"
 #include "poseopt_oracle.h"
+#include "sim3opt_oracle.h"
 #include "orbmatch_oracle.h"
 #include "sim3match_oracle.h"
 #include "kfdb_oracle.h"
@@ -566,6 +567,28 @@ void ora_pose_optimization_batch(int count, const int64_t* off, const float* uv,
         std::memcpy(in.Tcw, Tcw_in + 16 * c, sizeof(in.Tcw));
         n_good[c] = pose_optimization(in, Tcw_out + 16 * c, outlier + o, nullptr);
     }
+}
+
+// ---- Optimizer::OptimizeSim3 (Optimizer.cpp:1054-1250) ----
+// poses[24] = R1w 9, t1w 3, R2w 9, t2w 3; K[8] = K1 (fx, fy, cx, cy), K2; S[8] = q (x, y, z, w), t, s
+// in/out; stats[4] = nCorrespondences, nBad, LM iterations, LM trials.  Returns nIn.
+int ora_optimize_sim3(int n, const uint8_t* valid, const float* X1w, const float* X2w, const float* uv1,
+                      const float* uv2, const float* inv1, const float* inv2, const float* poses, const float* K,
+                      float th2, double* S, uint8_t* keep, int32_t* stats) {
+    Sim3OptInput in;
+    in.n = n; in.valid = valid; in.X1w = X1w; in.X2w = X2w; in.uv1 = uv1; in.uv2 = uv2; in.inv1 = inv1;
+    in.inv2 = inv2;
+    std::memcpy(in.R1w, poses, 36); std::memcpy(in.t1w, poses + 9, 12);
+    std::memcpy(in.R2w, poses + 12, 36); std::memcpy(in.t2w, poses + 21, 12);
+    std::memcpy(in.K1, K, 16); std::memcpy(in.K2, K + 4, 16);
+    in.th2 = th2;
+    Sim3Est e;
+    std::memcpy(e.q, S, 32); std::memcpy(e.t, S + 4, 24); e.s = S[7];
+    Sim3OptStats st{};
+    const int r = optimize_sim3(in, e, keep, &st);
+    std::memcpy(S, e.q, 32); std::memcpy(S + 4, e.t, 24); S[7] = e.s;
+    if (stats) { stats[0] = st.n_correspondences; stats[1] = st.n_bad; stats[2] = st.lm_iterations; stats[3] = st.lm_trials; }
+    return r;
 }
 
 // ---- ORBmatcher::SearchByBoW (ORBmatcher.cpp:110-240, :354-488) ----

@@ -18,6 +18,7 @@
 #include "rsc_kernels.h"
 #include "rsc_engine.h"
 #include "rsc_poseopt.h"
+#include "rsc_sim3opt.h"
 #include "rsc_orbmatch.h"
 #include "rsc_sim3match.h"
 #include "rsc_kfdb.h"
@@ -123,6 +124,12 @@ struct rsc_context {
     DevBuf<char> d_po_in;
     DevBuf<double2> d_po_err;
     DevBuf<double> d_po_err_r;  // third error component of the stereo edges
+    // OptimizeSim3: packed inputs (problems | e12 | e21 | uv), edge errors, results (out | keep)
+    DevBuf<char> d_so_in;
+    PinBuf<char> h_so_in;
+    DevBuf<double2> d_so_err;
+    DevBuf<char> d_so_res;
+    PinBuf<char> h_so_res;
     DevBuf<char> d_po_res;
     PinBuf<char> h_po_in;
     PinBuf<char> h_po_res;
@@ -804,6 +811,7 @@ int rsc_context_create(int device, rsc_context** out) {
     RSC_HIP(hipMemcpy(C->d_table.p, C->table.T.data(), C->table.T.size() * 4, hipMemcpyHostToDevice));
     for (auto& e : C->ev) RSC_HIP(hipEventCreate(&e));
     RSC_HIP(poseopt_prepare_device());
+    RSC_HIP(sim3opt_prepare_device());
     *out = C.release();
     return RSC_OK;
 }
@@ -1251,6 +1259,121 @@ int rsc_pose_optimization_many(rsc_context* C, const rsc_poseopt_problem* P, int
                 if (q.has_mp && !q.has_mp[i]) continue;
                 outlier[c][i] = hf[e++];
             }
+        }
+    }
+    return RSC_OK;
+}
+
+// ---- Optimizer::OptimizeSim3 (src/Optimizer.cpp:1054-1250) ----
+int rsc_optimize_sim3_many(rsc_context* C, const rsc_sim3opt_problem* P, int count, rsc_sim3opt_result* out,
+                           uint8_t* const* keep) {
+    if (!C || count < 0 || (count && (!P || !out))) return RSC_ERR_ARG;
+    if (count == 0) return RSC_OK;
+    // compaction of the correspondences (Optimizer.cpp:1108-1171), in slot order
+    std::vector<int> run;
+    std::vector<size_t> moff(1, 0);
+    for (int c = 0; c < count; ++c) {
+        const rsc_sim3opt_problem& q = P[c];
+        if (q.n < 0 || (q.n > 0 && (!q.valid || !q.X1w || !q.X2w || !q.uv1 || !q.uv2 || !q.inv1 || !q.inv2)))
+            return RSC_ERR_ARG;
+        int m = 0;
+        for (int i = 0; i < q.n; ++i) m += q.valid[i] ? 1 : 0;
+        if (m > kSim3OptMaxCorr) {
+            g_last_error = "more than 8192 correspondences in one OptimizeSim3 problem";
+            return RSC_ERR_UNSUPPORTED;
+        }
+        rsc_sim3opt_result& r = out[c];
+        std::memset(&r, 0, sizeof(r));
+        r.n_correspondences = m;
+        std::memcpy(r.S, q.S, sizeof(r.S));
+        if (keep && keep[c]) std::memset(keep[c], 1, (size_t)q.n);
+        if (m > 0) {  // m == 0: optimize() has no vertex to optimise, nCorrespondences - nBad < 10 -> 0
+            run.push_back(c);
+            moff.push_back(moff.back() + (size_t)m);
+        }
+    }
+    const int R = (int)run.size();
+    if (R == 0) return RSC_OK;
+    const size_t M = moff.back();
+    RSC_HIP(hipSetDevice(C->device));
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_e12 = al(sizeof(DevSim3OptProb) * R), o_e21 = o_e12 + al(sizeof(float4) * M);
+    const size_t o_uv = o_e21 + al(sizeof(float4) * M), in_bytes = o_uv + al(sizeof(float4) * M);
+    const size_t r_keep = al(sizeof(double) * 16 * R), res_bytes = r_keep + al(M);
+    if (int e = C->h_so_in.ensure(in_bytes)) return e;
+    if (int e = C->d_so_in.ensure(in_bytes)) return e;
+    if (int e = C->h_so_res.ensure(res_bytes)) return e;
+    if (int e = C->d_so_res.ensure(res_bytes)) return e;
+    if (int e = C->d_so_err.ensure(2 * M)) return e;
+    RSC_HIP(hipStreamSynchronize(C->stream));  // the previous call's copies out of the staging are done
+    char* h = C->h_so_in.p;
+    char* d = C->d_so_in.p;
+    DevSim3OptProb* hp = reinterpret_cast<DevSim3OptProb*>(h);
+    float4* h12 = reinterpret_cast<float4*>(h + o_e12);
+    float4* h21 = reinterpret_cast<float4*>(h + o_e21);
+    float4* huv = reinterpret_cast<float4*>(h + o_uv);
+    for (int k = 0; k < R; ++k) {
+        const rsc_sim3opt_problem& q = P[run[k]];
+        size_t e = moff[k];
+        for (int i = 0; i < q.n; ++i) {
+            if (!q.valid[i]) continue;
+            // P3D1c = R1w*P3D1w + t1w, P3D2c = R2w*P3D2w + t2w (float, Optimizer.cpp:1120-1136)
+            const float* a = q.X1w + 3 * (size_t)i;
+            const float* b = q.X2w + 3 * (size_t)i;
+            float c1[3], c2[3];
+            for (int r = 0; r < 3; ++r) {
+                c1[r] = q.R1w[3 * r] * a[0] + q.R1w[3 * r + 1] * a[1] + q.R1w[3 * r + 2] * a[2] + q.t1w[r];
+                c2[r] = q.R2w[3 * r] * b[0] + q.R2w[3 * r + 1] * b[1] + q.R2w[3 * r + 2] * b[2] + q.t2w[r];
+            }
+            h12[e] = make_float4(c2[0], c2[1], c2[2], q.inv1[i]);
+            h21[e] = make_float4(c1[0], c1[1], c1[2], q.inv2[i]);
+            huv[e] = make_float4(q.uv1[2 * i], q.uv1[2 * i + 1], q.uv2[2 * i], q.uv2[2 * i + 1]);
+            ++e;
+        }
+        DevSim3OptProb& dp = hp[k];
+        dp.e12 = reinterpret_cast<const float4*>(d + o_e12) + moff[k];
+        dp.e21 = reinterpret_cast<const float4*>(d + o_e21) + moff[k];
+        dp.uv = reinterpret_cast<const float4*>(d + o_uv) + moff[k];
+        dp.err = C->d_so_err.p + 2 * moff[k];
+        dp.keep = reinterpret_cast<uint8_t*>(C->d_so_res.p + r_keep) + moff[k];
+        dp.out = reinterpret_cast<double*>(C->d_so_res.p) + 16 * k;
+        dp.m = (int)(moff[k + 1] - moff[k]);
+        dp.th2 = q.th2;
+        const float deltaHuber = std::sqrt(q.th2);  // Optimizer.cpp:1104: float sqrt
+        dp.delta = deltaHuber;
+        std::memcpy(dp.K1, q.K1, sizeof(dp.K1));
+        std::memcpy(dp.K2, q.K2, sizeof(dp.K2));
+        std::memcpy(dp.S0, q.S, sizeof(dp.S0));
+    }
+    RSC_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, C->stream));
+    timing_begin(C, 3);
+    RSC_HIP(launch_sim3opt(R, reinterpret_cast<const DevSim3OptProb*>(d), C->stream));
+    timing_begin(C, 4);
+    RSC_HIP(hipMemcpyAsync(C->h_so_res.p, C->d_so_res.p, res_bytes, hipMemcpyDeviceToHost, C->stream));
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    if (C->timing) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, C->ev[3], C->ev[4]);
+        C->last_ms[2] = ms;
+    }
+    const double* ho = reinterpret_cast<const double*>(C->h_so_res.p);
+    const uint8_t* hk = reinterpret_cast<const uint8_t*>(C->h_so_res.p + r_keep);
+    for (int k = 0; k < R; ++k) {
+        const int c = run[k];
+        const rsc_sim3opt_problem& q = P[c];
+        rsc_sim3opt_result& r = out[c];
+        const double* o = ho + 16 * k;
+        std::memcpy(r.S, o, 64);
+        int32_t st[4];
+        std::memcpy(st, o + 8, 16);
+        r.n_inliers = st[0];
+        r.n_bad = st[1];
+        r.lm_iterations = st[2];
+        r.lm_trials = st[3];
+        if (keep && keep[c]) {
+            size_t e = moff[k];
+            for (int i = 0; i < q.n; ++i)
+                if (q.valid[i]) keep[c][i] = hk[e++];
         }
     }
     return RSC_OK;

@@ -335,14 +335,14 @@ RSC_HD void po_quad_terms(const PoSE3& est, const PoCam& K, const double (&Xw)[3
     }
 }
 
-// Eigen::LDLT<MatrixXd> on the lower triangle of the 6x6 (ldlt_inplace<Lower>::unblocked) and
+// Eigen::LDLT<MatrixXd> on the lower triangle of the n x n (ldlt_inplace<Lower>::unblocked) and
 // _solve_impl; returns isPositive() (x untouched otherwise, as LinearSolverDense::solve).
 // Register arrays with static indices only: the diagonal pivot search and the symmetric
-// transposition are written as value selects.
-RSC_HD bool po_ldlt_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[6]) {
-    constexpr int n = 6;
+// transposition are written as value selects.  n = 6 (PoseOptimization), 7 (OptimizeSim3).
+template <int n>
+RSC_HD bool po_ldlt_solve(double (&A)[n][n], const double (&b)[n], double (&x)[n]) {
     int sign = 0;  // 0 zero, 1 positive semidef, 2 negative semidef, 3 indefinite
-    int tr[6];
+    int tr[n];
     bool stop = false;
     RSC_UNROLL for (int k = 0; k < n; ++k) {
         tr[k] = k;
@@ -362,7 +362,7 @@ RSC_HD bool po_ldlt_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[
                 }
             }
             if (k > 0) {
-                double temp[6];
+                double temp[n];
                 RSC_UNROLL for (int j = 0; j < k; ++j) temp[j] = A[j][j] * A[k][j];
                 double acc = A[k][0] * temp[0];
                 RSC_UNROLL for (int j = 1; j < k; ++j) acc = acc + A[k][j] * temp[j];
@@ -393,7 +393,7 @@ RSC_HD bool po_ldlt_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[
         }
     }
     if (!(sign == 1 || sign == 0)) return false;
-    double y[6];
+    double y[n];
     RSC_UNROLL for (int i = 0; i < n; ++i) y[i] = b[i];
     RSC_UNROLL for (int k = 0; k < n; ++k)
         RSC_UNROLL for (int j = k + 1; j < n; ++j) {
@@ -424,6 +424,8 @@ RSC_HD bool po_ldlt_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[
     RSC_UNROLL for (int i = 0; i < n; ++i) x[i] = y[i];
     return true;
 }
+
+RSC_HD bool po_ldlt_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[6]) { return po_ldlt_solve<6>(A, b, x); }
 
 #if defined(__HIPCC__)
 hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st);

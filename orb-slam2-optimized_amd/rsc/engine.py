@@ -42,6 +42,7 @@ EXPORTED = [
     "rsc_bow_create", "rsc_bow_destroy", "rsc_bow_set_valid", "rsc_search_by_bow_frame_many",
     "rsc_search_by_bow_kf_many", "rsc_diag_bow_phase_stamps", "rsc_diag_refine_phase_stamps",
     "rsc_search_by_sim3_many", "rsc_kfview_create", "rsc_kfview_destroy",
+    "rsc_optimize_sim3_many",
     "rsc_kfdb_create", "rsc_kfdb_destroy", "rsc_kfdb_add", "rsc_kfdb_erase", "rsc_kfdb_clear",
     "rsc_kfdb_set_covisibility", "rsc_kfdb_set_covisibility_many", "rsc_kfdb_detect_relocalization", "rsc_kfdb_detect_loop", "rsc_kfdb_state",
 ]
@@ -77,6 +78,18 @@ class PoseOptProblem(C.Structure):
     _fields_ = [("n", C.c_int32), ("has_mp", C.c_void_p), ("uv", C.c_void_p), ("Xw", C.c_void_p),
                 ("inv_sigma2", C.c_void_p), ("u_right", C.c_void_p), ("fx", C.c_float), ("fy", C.c_float),
                 ("cx", C.c_float), ("cy", C.c_float), ("Tcw", C.c_float * 16), ("bf", C.c_float)]
+
+
+class Sim3OptProblem(C.Structure):
+    _fields_ = [("n", C.c_int32), ("valid", C.c_void_p), ("X1w", C.c_void_p), ("X2w", C.c_void_p),
+                ("uv1", C.c_void_p), ("uv2", C.c_void_p), ("inv1", C.c_void_p), ("inv2", C.c_void_p),
+                ("R1w", C.c_float * 9), ("t1w", C.c_float * 3), ("R2w", C.c_float * 9), ("t2w", C.c_float * 3),
+                ("K1", C.c_float * 4), ("K2", C.c_float * 4), ("S", C.c_double * 8), ("th2", C.c_float)]
+
+
+class Sim3OptResult(C.Structure):
+    _fields_ = [("n_inliers", C.c_int32), ("n_correspondences", C.c_int32), ("n_bad", C.c_int32),
+                ("lm_iterations", C.c_int32), ("lm_trials", C.c_int32), ("S", C.c_double * 8)]
 
 
 class BowFeatures(C.Structure):
@@ -321,6 +334,8 @@ def load_library(path: str = LIB_PATH):
     L.rsc_reloc_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(PnPResult), C.POINTER(EventResult)]
     L.rsc_pose_optimization_many.argtypes = [vp, C.POINTER(PoseOptProblem), C.c_int, C.POINTER(PoseOptResult),
                                              C.POINTER(C.c_void_p)]
+    L.rsc_optimize_sim3_many.argtypes = [vp, C.POINTER(Sim3OptProblem), C.c_int, C.POINTER(Sim3OptResult),
+                                         C.POINTER(C.c_void_p)]
     L.rsc_bow_create.argtypes = [vp, C.POINTER(BowFeatures), C.POINTER(vp)]
     L.rsc_bow_destroy.argtypes = [vp]
     L.rsc_bow_set_valid.argtypes = [vp, u8p]
@@ -806,6 +821,61 @@ class PoseOptBatch:
                         "lm_iterations": r.lm_iterations, "lm_trials": r.lm_trials,
                         "Tcw": np.array(r.Tcw[:], np.float32).reshape(4, 4), "outlier": self.outs[i][:f.n].copy()})
         return out
+
+
+class Sim3OptBatch:
+    """Loop-closure pairs prepared once for repeated rsc_optimize_sim3_many calls
+    (Optimizer::OptimizeSim3, Optimizer.cpp:1054-1250).  problems: rsc.synth.Sim3OptProblem-likes."""
+
+    def __init__(self, ctx: Context, problems):
+        self.ctx = ctx
+        self.problems = list(problems)
+        n = len(self.problems)
+        self.probs = (Sim3OptProblem * max(n, 1))()
+        self.res = (Sim3OptResult * max(n, 1))()
+        self.ptrs = (C.c_void_p * max(n, 1))()
+        self.keep, self.keeps = [], []
+        for i, p in enumerate(self.problems):
+            arrs = [np.ascontiguousarray(p.valid, np.uint8)] + [np.ascontiguousarray(a, np.float32).reshape(-1) for a in
+                                                                (p.X1w, p.X2w, p.uv1, p.uv2, p.inv1, p.inv2)]
+            self.keep.append(arrs)
+            q = self.probs[i]
+            q.n = p.n
+            q.valid, q.X1w, q.X2w, q.uv1, q.uv2, q.inv1, q.inv2 = (a.ctypes.data for a in arrs)
+            q.R1w[:] = [float(v) for v in np.asarray(p.R1w, np.float32).ravel()]
+            q.t1w[:] = [float(v) for v in np.asarray(p.t1w, np.float32)]
+            q.R2w[:] = [float(v) for v in np.asarray(p.R2w, np.float32).ravel()]
+            q.t2w[:] = [float(v) for v in np.asarray(p.t2w, np.float32)]
+            q.K1[:] = [float(v) for v in np.asarray(p.K1, np.float32)]
+            q.K2[:] = [float(v) for v in np.asarray(p.K2, np.float32)]
+            q.S[:] = [float(v) for v in np.asarray(p.S0, np.float64)]
+            q.th2 = float(p.th2)
+            k = np.full(max(p.n, 1), 7, np.uint8)
+            self.keeps.append(k)
+            self.ptrs[i] = k.ctypes.data
+
+    def run(self):
+        _check(load_library().rsc_optimize_sim3_many(self.ctx.h, self.probs, len(self.problems), self.res, self.ptrs),
+               "rsc_optimize_sim3_many")
+
+    def results(self):
+        out = []
+        for i, p in enumerate(self.problems):
+            r = self.res[i]
+            out.append({"n_inliers": r.n_inliers, "n_correspondences": r.n_correspondences, "n_bad": r.n_bad,
+                        "lm_iterations": r.lm_iterations, "lm_trials": r.lm_trials,
+                        "S": np.array(r.S[:], np.float64), "keep": self.keeps[i][:p.n].copy()})
+        return out
+
+
+def optimize_sim3_many(ctx: Context, problems):
+    """Optimizer::OptimizeSim3 on every loop-closure pair in one launch.  Returns per pair a dict:
+    n_inliers (the reference's return value), n_correspondences, n_bad, lm_iterations, lm_trials,
+    S float64[8] (g2oS12 after the call: q x, y, z, w, t, s), keep uint8[n] (0 where vpMatches1[i]
+    is set to NULL)."""
+    b = Sim3OptBatch(ctx, problems)
+    b.run()
+    return b.results()
 
 
 def pose_optimization_many(ctx: Context, frames, with_outliers: bool = True):

@@ -439,6 +439,109 @@ def make_sim3match_pair(rng: np.random.Generator, n_points: int = 1000, n_extra:
     return kf1, kf2, R12, t12, matched12
 
 
+# ---- Optimizer::OptimizeSim3 inputs ----------------------------------------------------------------
+def quat_from_R(m) -> np.ndarray:
+    """Quaterniond(Matrix3d) (Eigen's trace / largest-diagonal algorithm), coefficients (x, y, z, w)."""
+    m = np.asarray(m, np.float64)
+    t = m[0, 0] + m[1, 1] + m[2, 2]
+    if t > 0.0:
+        t = np.sqrt(t + 1.0)
+        w = 0.5 * t
+        t = 0.5 / t
+        return np.array([(m[2, 1] - m[1, 2]) * t, (m[0, 2] - m[2, 0]) * t, (m[1, 0] - m[0, 1]) * t, w])
+    i = 0
+    if m[1, 1] > m[0, 0]:
+        i = 1
+    if m[2, 2] > m[i, i]:
+        i = 2
+    j, k = (i + 1) % 3, (i + 2) % 3
+    c = np.zeros(3)
+    t = np.sqrt(m[i, i] - m[j, j] - m[k, k] + 1.0)
+    c[i] = 0.5 * t
+    t = 0.5 / t
+    w = (m[k, j] - m[j, k]) * t
+    c[j] = (m[j, i] + m[i, j]) * t
+    c[k] = (m[k, i] + m[i, k]) * t
+    return np.array([c[0], c[1], c[2], w])
+
+
+@dataclasses.dataclass
+class Sim3OptProblem:
+    """Optimizer::OptimizeSim3(pKF1, pKF2, vpMatches1, g2oS12, th2) inputs (Optimizer.cpp:1054-1145),
+    per KF1 keypoint slot i: valid (a correspondence: both MapPoints present, not bad, i2 >= 0),
+    X1w = vpMapPoints1[i]->GetWorldPos(), X2w = vpMatches1[i]->GetWorldPos(), uv1 = KF1 mvKeysUn[i],
+    uv2 = KF2 mvKeysUn[i2], inv1/inv2 = mvInvLevelSigma2 of the octaves."""
+    valid: np.ndarray   # uint8 [n]
+    X1w: np.ndarray     # float32 [n,3]
+    X2w: np.ndarray     # float32 [n,3]
+    uv1: np.ndarray     # float32 [n,2]
+    uv2: np.ndarray     # float32 [n,2]
+    inv1: np.ndarray    # float32 [n]
+    inv2: np.ndarray    # float32 [n]
+    R1w: np.ndarray     # float32 [3,3]
+    t1w: np.ndarray     # float32 [3]
+    R2w: np.ndarray
+    t2w: np.ndarray
+    S0: np.ndarray      # float64 [8] g2oS12 on entry: q (x, y, z, w), t, s
+    R12_true: np.ndarray
+    t12_true: np.ndarray
+    inlier_true: np.ndarray  # bool [n]
+    K1: np.ndarray = dataclasses.field(default_factory=lambda: np.array([FX, FY, CX, CY], np.float32))
+    K2: np.ndarray = dataclasses.field(default_factory=lambda: np.array([FX, FY, CX, CY], np.float32))
+    th2: float = 10.0   # LoopClosing.cpp:311
+
+    @property
+    def n(self) -> int:
+        return int(self.valid.shape[0])
+
+    def poses24(self) -> np.ndarray:
+        return np.ascontiguousarray(np.concatenate([np.asarray(self.R1w, np.float32).ravel(),
+                                                    np.asarray(self.t1w, np.float32),
+                                                    np.asarray(self.R2w, np.float32).ravel(),
+                                                    np.asarray(self.t2w, np.float32)]), np.float32)
+
+    def K8(self) -> np.ndarray:
+        return np.ascontiguousarray(np.concatenate([self.K1, self.K2]), np.float32)
+
+
+def make_sim3opt_problem(rng: np.random.Generator, n: int, valid_frac: float = 0.9, outlier_frac: float = 0.1,
+                         pose_noise: float = 0.01, noise: bool = True, drift: float = 0.01) -> Sim3OptProblem:
+    """A loop-closure pair: KF2-camera points X2c, the true relative pose S12 (scale 1, as Sim3Solver
+    fixes it), X1c = S12 X2c (+ map drift noise), both KeyFrames' world poses, observations with
+    pyramid-level pixel noise, outliers displaced, and the initial g2oS12 = a perturbed S12 as
+    Sim3Solver would return it (float R, t -> Sim3(R.cast<double>(), t.cast<double>(), 1))."""
+    s2 = level_sigma2()
+    X2c = np.stack([rng.uniform(-3, 3, n), rng.uniform(-2, 2, n), rng.uniform(1.5, 9, n)], 1)
+    R12 = random_rotation(rng, 0.3)
+    t12 = rng.normal(0, 0.4, 3)
+    X1c = X2c @ R12.T + t12 + (rng.normal(0, drift, (n, 3)) if noise else 0.0)
+    R1w, R2w = random_rotation(rng), random_rotation(rng)
+    t1w, t2w = rng.normal(0, 2, 3), rng.normal(0, 2, 3)
+    X1w = ((X1c - t1w) @ R1w).astype(np.float32)   # R^T (Xc - t)
+    X2w = ((X2c - t2w) @ R2w).astype(np.float32)
+    probs = level_probabilities()
+    o1 = rng.choice(N_LEVELS, size=n, p=probs)
+    o2 = rng.choice(N_LEVELS, size=n, p=probs)
+    uv1 = np.stack([FX * X1c[:, 0] / X1c[:, 2] + CX, FY * X1c[:, 1] / X1c[:, 2] + CY], 1)
+    uv2 = np.stack([FX * X2c[:, 0] / X2c[:, 2] + CX, FY * X2c[:, 1] / X2c[:, 2] + CY], 1)
+    if noise:
+        uv1 = uv1 + rng.normal(size=(n, 2)) * np.sqrt(s2[o1])[:, None]
+        uv2 = uv2 + rng.normal(size=(n, 2)) * np.sqrt(s2[o2])[:, None]
+    inl = rng.random(n) >= outlier_frac
+    bad = ~inl
+    nb = int(bad.sum())
+    uv1[bad] += rng.choice([-1.0, 1.0], (nb, 2)) * rng.uniform(12, 60, (nb, 2))  # gross: >= 12 px
+    valid = (rng.random(n) < valid_frac).astype(np.uint8)
+    Rp = (random_rotation(rng, pose_noise) @ R12).astype(np.float32)
+    tp = (t12 + rng.normal(0, pose_noise, 3)).astype(np.float32)
+    S0 = np.concatenate([quat_from_R(Rp.astype(np.float64)), tp.astype(np.float64), [1.0]])
+    inv = (np.float32(1.0) / s2).astype(np.float32)
+    return Sim3OptProblem(valid=valid, X1w=X1w, X2w=X2w, uv1=uv1.astype(np.float32), uv2=uv2.astype(np.float32),
+                          inv1=inv[o1], inv2=inv[o2], R1w=R1w.astype(np.float32), t1w=t1w.astype(np.float32),
+                          R2w=R2w.astype(np.float32), t2w=t2w.astype(np.float32), S0=S0, R12_true=R12,
+                          t12_true=t12, inlier_true=inl)
+
+
 # ---- KeyFrameDatabase scenes (KeyFrameDatabase.cpp) ---------------------------------------------
 VOCAB_WORDS = 10 ** 6  # ORBvoc.txt: k = 10, L = 6 -> up to 10^6 leaves
 

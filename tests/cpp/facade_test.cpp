@@ -29,7 +29,7 @@ struct MapPoint {
     int GetIndexInKeyFrame(const std::shared_ptr<KeyFrame>& kf) const;
 };
 struct KeyFrame {
-    std::vector<KeyPoint> mvKeysUn; std::vector<float> mvLevelSigma2; Mat3 mK; Mat3 R; Vec3 t;
+    std::vector<KeyPoint> mvKeysUn; std::vector<float> mvLevelSigma2, mvInvLevelSigma2; Mat3 mK; Mat3 R; Vec3 t;
     std::vector<std::shared_ptr<MapPoint>> mps;
     std::vector<std::shared_ptr<MapPoint>> GetMapPointMatches() { return mps; }
     Mat3 GetRotation() const { return R; }
@@ -49,6 +49,17 @@ struct BowKF {
     std::vector<std::shared_ptr<MapPoint>> GetMapPointMatches() const { return mps; }
 };
 struct BowFrame { int N = 0; DescMat mDescriptors; std::vector<KeyPoint> mvKeys; FeatVec mFeatVec; };
+
+// g2o::Sim3 stand-in: rotation().coeffs()[k] (x, y, z, w), translation()[k], scale() as references
+struct MockSim3 {
+    struct V4 { double v[4]; double& operator[](int i) { return v[i]; } };
+    struct Q { V4 c; V4& coeffs() { return c; } };
+    struct V3d { double v[3]; double& operator[](int i) { return v[i]; } };
+    Q q; V3d tr; double s = 1.0;
+    Q& rotation() { return q; }
+    V3d& translation() { return tr; }
+    double& scale() { return s; }
+};
 
 // SearchBySim3 mocks: KeyFrame with the public members ORBmatcher::SearchBySim3 reads plus the
 // GetGrid() getter, MapPoint with GetMaxDistance()/GetMinDistance()
@@ -347,6 +358,53 @@ int main(int argc, char** argv) {
         const int nf = matcher.SearchBySim3(kf[0], kf[1], m12, R12, t12, th);
         wr<int32_t>(out, nf);
         for (auto& mp : m12) wr<int32_t>(out, !mp ? -1 : (mp == foreign ? -2 : mp->idx));
+    } else if (mode == 8) {
+        // Optimizer::OptimizeSim3 through the facade: n1 slots of KF1, n2 of KF2, per KF pose, K,
+        // inverse level sigmas; per KF2 slot (u, v, octave); per KF1 slot (u, v, octave, kind, X1,
+        // X2, i2) with kind 0 = vpMatches1 NULL, 1 = pMP1 NULL, 2 = pMP1 bad, 3 = pMP2 bad, 4 = i2 < 0,
+        // 5 = a correspondence; then S[8], th2.  Writes nIn, S after the call, and per slot whether
+        // vpMatches1[i] is still set.
+        auto kf1 = std::make_shared<KeyFrame>(), kf2 = std::make_shared<KeyFrame>();
+        const int n1 = rd<int32_t>(in), n2 = rd<int32_t>(in);
+        for (auto* kf : {kf1.get(), kf2.get()}) {
+            for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) kf->R.m[r][c] = rd<float>(in);
+            for (int r = 0; r < 3; ++r) kf->t.v[r] = rd<float>(in);
+            float K[4]; for (float& k : K) k = rd<float>(in);
+            std::memset(&kf->mK, 0, sizeof(Mat3));
+            kf->mK.m[0][0] = K[0]; kf->mK.m[1][1] = K[1]; kf->mK.m[0][2] = K[2]; kf->mK.m[1][2] = K[3]; kf->mK.m[2][2] = 1;
+            const int nl = rd<int32_t>(in);
+            for (int l = 0; l < nl; ++l) kf->mvInvLevelSigma2.push_back(rd<float>(in));
+        }
+        kf1->mvKeysUn.resize(n1); kf1->mps.resize(n1);
+        kf2->mvKeysUn.resize(n2); kf2->mps.resize(n2);
+        for (int j = 0; j < n2; ++j) { kf2->mvKeysUn[j].pt.x = rd<float>(in); kf2->mvKeysUn[j].pt.y = rd<float>(in); kf2->mvKeysUn[j].octave = rd<int32_t>(in); }
+        std::vector<std::shared_ptr<MapPoint>> m1(n1);
+        for (int i = 0; i < n1; ++i) {
+            kf1->mvKeysUn[i].pt.x = rd<float>(in); kf1->mvKeysUn[i].pt.y = rd<float>(in); kf1->mvKeysUn[i].octave = rd<int32_t>(in);
+            const int kind = rd<int32_t>(in);
+            Vec3 a, b; for (int r = 0; r < 3; ++r) a.v[r] = rd<float>(in);
+            for (int r = 0; r < 3; ++r) b.v[r] = rd<float>(in);
+            const int i2 = rd<int32_t>(in);
+            if (kind == 0) continue;
+            if (kind != 1) {
+                auto mp1 = std::make_shared<MapPoint>(); mp1->X = a; mp1->bad = kind == 2; mp1->kf1 = kf1.get(); mp1->idx1 = i;
+                kf1->mps[i] = mp1;
+            }
+            auto mp2 = std::make_shared<MapPoint>(); mp2->X = b; mp2->bad = kind == 3; mp2->kf1 = kf1.get();
+            mp2->idx1 = -1; mp2->idx2 = kind == 4 ? -1 : i2;
+            m1[i] = mp2;
+        }
+        MockSim3 S;
+        for (int k = 0; k < 4; ++k) S.q.c.v[k] = rd<double>(in);
+        for (int k = 0; k < 3; ++k) S.tr.v[k] = rd<double>(in);
+        S.s = rd<double>(in);
+        const float th2 = rd<float>(in);
+        const int nIn = rsc_orb::OptimizeSim3(kf1, kf2, m1, S, th2);
+        wr<int32_t>(out, nIn);
+        for (int k = 0; k < 4; ++k) wr<double>(out, S.q.c.v[k]);
+        for (int k = 0; k < 3; ++k) wr<double>(out, S.tr.v[k]);
+        wr<double>(out, S.s);
+        for (int i = 0; i < n1; ++i) wr<uint8_t>(out, m1[i] ? 1 : 0);
     } else if (mode == 2) {
         auto kf1 = std::make_shared<KeyFrame>(), kf2 = std::make_shared<KeyFrame>();
         const int n1 = rd<int32_t>(in);

@@ -11,6 +11,7 @@
 #include "../../orb-slam2-optimized_amd/csrc/rsc_engine.h"
 #include "../../orb-slam2-optimized_amd/csrc/rsc_mlpnp.h"
 #include "../../orb-slam2-optimized_amd/csrc/rsc_poseopt.h"
+#include "../../orb-slam2-optimized_amd/csrc/rsc_sim3opt.h"
 
 using namespace rsc;
 
@@ -474,5 +475,151 @@ void he_pose_optimization(int n, const float* xw4, const float* uv, const float*
     }
     const int ints[4] = {n - nBad, rounds, lm_its, lm_trials};
     std::memcpy(out + 12, ints, 16);
+}
+
+// OptimizeSim3 in the device orchestration (sim3opt.hip), run sequentially: the same per-edge
+// functions, terms in the edge order e12_0, e21_0, ..., the same folds.  Inputs already compacted:
+// e12/e21 [m][4] = (X, invSigma2), uv [m][4]; S[8] in/out; keep[m]; stats[4] = nIn, nBad, its, trials.
+void he_optimize_sim3(int m, const float* e12, const float* e21, const float* uv, const float* K8, float th2,
+                      double* S8, uint8_t* keep, int32_t* stats) {
+    using namespace rsc;
+    const SoCam K1{(double)K8[0], (double)K8[1], (double)K8[2], (double)K8[3]};
+    const SoCam K2{(double)K8[4], (double)K8[5], (double)K8[6], (double)K8[7]};
+    const float deltaHuber = std::sqrt(th2);
+    const double delta = deltaHuber, dsqr = delta * delta;
+    std::vector<double> err(4 * (size_t)m, 0.0);
+    auto load = [&](int c, bool inv_edge, double (&X)[3], double& u, double& v, double& inv) {
+        const float* a = (inv_edge ? e21 : e12) + 4 * (size_t)c;
+        X[0] = a[0]; X[1] = a[1]; X[2] = a[2];
+        inv = a[3];
+        u = uv[4 * c + (inv_edge ? 2 : 0)];
+        v = uv[4 * c + (inv_edge ? 3 : 1)];
+    };
+    auto chi_pass = [&](const SoSim3& S) {
+        const SoSim3 Si = so_inverse(S);
+        double acc = 0.0;
+        for (int c = 0; c < m; ++c) {
+            double t0 = 0.0, t1 = 0.0, r1;
+            if (keep[c]) {
+                double X[3], u, v, inv;
+                load(c, false, X, u, v, inv);
+                so_edge_error(S, K1, X, u, v, err[4 * c], err[4 * c + 1]);
+                po_huber(po_chi2(inv, false, err[4 * c], err[4 * c + 1], 0.0), delta, dsqr, t0, r1);
+                load(c, true, X, u, v, inv);
+                so_edge_error(Si, K2, X, u, v, err[4 * c + 2], err[4 * c + 3]);
+                po_huber(po_chi2(inv, false, err[4 * c + 2], err[4 * c + 3], 0.0), delta, dsqr, t1, r1);
+            }
+            acc = acc + t0;
+            acc = acc + t1;
+        }
+        return acc;
+    };
+    auto build_pass = [&](const SoSim3& S, double (&H)[7][7], double (&b)[7]) {
+        SoPerturbed Pt;
+        so_perturb(S, Pt);
+        double acc[kSim3OptTerms];
+        for (int k = 0; k < kSim3OptTerms; ++k) acc[k] = 0.0;
+        for (int c = 0; c < m; ++c)
+            for (int side = 0; side < 2; ++side) {
+                double t[kSim3OptTerms];
+                for (int k = 0; k < kSim3OptTerms; ++k) t[k] = 0.0;
+                if (keep[c]) {
+                    double X[3], u, v, inv;
+                    load(c, side == 1, X, u, v, inv);
+                    so_quad_terms(Pt, side == 1, side ? K2 : K1, X, u, v, inv, err[4 * c + 2 * side],
+                                  err[4 * c + 2 * side + 1], delta, dsqr, t);
+                }
+                for (int k = 0; k < kSim3OptTerms; ++k) acc[k] = acc[k] + t[k];
+            }
+        int k = 0;
+        for (int i = 0; i < 7; ++i)
+            for (int j = 0; j <= i; ++j) { H[i][j] = acc[k++]; H[j][i] = H[i][j]; }
+        for (int i = 0; i < 7; ++i) b[i] = acc[28 + i];
+    };
+    double x[7] = {0, 0, 0, 0, 0, 0, 0};
+    double lambda = -1.0, ni = 2.0;
+    int nBadLM = 0, its = 0, trials = 0;
+    auto optimize = [&](SoSim3& S, int iterations) {
+        bool ok = true;
+        for (int i = 0; i < iterations && ok; ++i) {
+            its++;
+            double currentChi = chi_pass(S);
+            const double iniChi = currentChi;
+            double H[7][7], b[7];
+            build_pass(S, H, b);
+            if (i == 0) {
+                double maxDiagonal = 0.;
+                for (int j = 0; j < 7; ++j) { const double a = std::fabs(H[j][j]); maxDiagonal = (a < maxDiagonal) ? maxDiagonal : a; }
+                lambda = 1e-5 * maxDiagonal;
+                ni = 2;
+                nBadLM = 0;
+            }
+            double rho = 0;
+            int qmax = 0;
+            do {
+                trials++;
+                const SoSim3 saved = S;
+                double Hd[7][7];
+                for (int r = 0; r < 7; ++r) for (int c = 0; c < 7; ++c) Hd[r][c] = H[r][c];
+                for (int r = 0; r < 7; ++r) Hd[r][r] += lambda;
+                double xs[7];
+                const bool ok2 = po_ldlt_solve<7>(Hd, b, xs);
+                if (ok2) for (int j = 0; j < 7; ++j) x[j] = xs[j];
+                S = so_oplus(x, S);
+                double tempChi = chi_pass(S);
+                if (!ok2) tempChi = DBL_MAX;
+                rho = (currentChi - tempChi);
+                double scale = 0.;
+                for (int j = 0; j < 7; ++j) scale += x[j] * (lambda * x[j] + b[j]);
+                scale += 1e-3;
+                rho /= scale;
+                if (rho > 0 && std::isfinite(tempChi)) {
+                    double alpha = 1. - po_cube(2 * rho - 1);
+                    alpha = (2. / 3. < alpha) ? 2. / 3. : alpha;
+                    const double scaleFactor = (1. / 3. < alpha) ? alpha : 1. / 3.;
+                    lambda *= scaleFactor;
+                    ni = 2;
+                    currentChi = tempChi;
+                } else {
+                    lambda *= ni;
+                    ni *= 2;
+                    S = saved;
+                }
+                qmax++;
+            } while (rho < 0 && qmax < 10);
+            if (qmax == 10 || rho == 0) ok = false;
+            else {
+                if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
+                else nBadLM = 0;
+                ok = nBadLM < 3;
+            }
+        }
+    };
+    auto outlier = [&](int c) {
+        return po_chi2(e12[4 * c + 3], false, err[4 * c], err[4 * c + 1], 0.0) > (double)th2 ||
+               po_chi2(e21[4 * c + 3], false, err[4 * c + 2], err[4 * c + 3], 0.0) > (double)th2;
+    };
+    SoSim3 S;
+    S.r.x = S8[0]; S.r.y = S8[1]; S.r.z = S8[2]; S.r.w = S8[3];
+    S.t[0] = S8[4]; S.t[1] = S8[5]; S.t[2] = S8[6];
+    S.s = S8[7];
+    for (int c = 0; c < m; ++c) keep[c] = 1;
+    optimize(S, 5);
+    int nBad = 0;
+    for (int c = 0; c < m; ++c)
+        if (outlier(c)) { keep[c] = 0; ++nBad; }
+    int nIn = 0;
+    if (m - nBad >= 10) {
+        optimize(S, nBad > 0 ? 10 : 5);
+        for (int c = 0; c < m; ++c) {
+            if (!keep[c]) continue;
+            if (outlier(c)) keep[c] = 0;
+            else ++nIn;
+        }
+        S8[0] = S.r.x; S8[1] = S.r.y; S8[2] = S.r.z; S8[3] = S.r.w;
+        S8[4] = S.t[0]; S8[5] = S.t[1]; S8[6] = S.t[2];
+        S8[7] = S.s;
+    }
+    stats[0] = nIn; stats[1] = nBad; stats[2] = its; stats[3] = trials;
 }
 }  // extern "C"

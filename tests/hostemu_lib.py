@@ -34,6 +34,7 @@ def lib():
         L.he_sim3_hypothesis.argtypes = [u32p, C.c_int, C.c_int, C.c_int, f32p, f32p, i32p, f32p]
         L.he_sim3_count.argtypes = [f32p, f32p, f32p, C.c_int, f32p, f32p, f32p, f32p, u64p, u64p, u8p]
         L.he_pose_optimization.argtypes = [C.c_int, f32p, f32p, f32p, f32p, f32p, u8p, C.c_void_p, C.c_float]
+        L.he_optimize_sim3.argtypes = [C.c_int, f32p, f32p, f32p, f32p, C.c_float, f64p, u8p, i32p]
         _lib = L
     return _lib
 
@@ -182,3 +183,36 @@ def pose_optimization(frame):
     T = np.eye(4, dtype=np.float32)
     T[:3] = out[:12].reshape(3, 4)
     return int(ints[0]), T, outl[:n], ints[1:].copy()
+
+
+def sim3opt_compact(p):
+    """Host compaction of a rsc.synth.Sim3OptProblem as rsc_optimize_sim3_many does it: per
+    correspondence (P3D2c, inv1), (P3D1c, inv2), (uv1, uv2) with the float camera-frame transforms."""
+    sel = np.nonzero(p.valid)[0]
+    f = np.float32
+    R1, t1, R2, t2 = (np.asarray(a, f) for a in (p.R1w, p.t1w, p.R2w, p.t2w))
+    def cam(R, t, X):  # ((R0*x + R1*y) + R2*z) + t in float
+        out = np.zeros((len(X), 3), f)
+        for r in range(3):
+            out[:, r] = ((R[r, 0] * X[:, 0] + R[r, 1] * X[:, 1]) + R[r, 2] * X[:, 2]) + t[r]
+        return out
+    X1 = np.asarray(p.X1w, f)[sel]
+    X2 = np.asarray(p.X2w, f)[sel]
+    e12 = np.concatenate([cam(R2, t2, X2), np.asarray(p.inv1, f)[sel, None]], 1)
+    e21 = np.concatenate([cam(R1, t1, X1), np.asarray(p.inv2, f)[sel, None]], 1)
+    uv = np.concatenate([np.asarray(p.uv1, f)[sel], np.asarray(p.uv2, f)[sel]], 1)
+    return sel, np.ascontiguousarray(e12, f), np.ascontiguousarray(e21, f), np.ascontiguousarray(uv, f)
+
+
+def optimize_sim3(p):
+    """Host build of the device OptimizeSim3 orchestration: (nIn, S[8], keep over the slots, stats[4])."""
+    sel, e12, e21, uv = sim3opt_compact(p)
+    m = len(sel)
+    S = np.ascontiguousarray(p.S0, np.float64).copy()
+    keep_c = np.zeros(max(m, 1), np.uint8)
+    st = np.zeros(4, np.int32)
+    if m:
+        lib().he_optimize_sim3(m, e12.reshape(-1), e21.reshape(-1), uv.reshape(-1), p.K8(), float(p.th2), S, keep_c, st)
+    keep = np.ones(p.n, np.uint8)
+    keep[sel] = keep_c[:m]
+    return int(st[0]), S, keep, st

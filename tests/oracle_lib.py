@@ -51,6 +51,8 @@ def lib():
     L.ora_pose_optimization.restype = C.c_int
     L.ora_pose_optimization_batch.argtypes = [C.c_int, i64p, f32p, f32p, f32p, C.c_float, C.c_float, C.c_float,
                                               C.c_float, f32p, f32p, u8p, i32p, C.c_void_p, C.c_float]
+    L.ora_optimize_sim3.argtypes = [C.c_int, u8p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p, C.c_float,
+                                    np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS"), u8p, i32p]
     L.ora_glibc_rand.argtypes = [C.c_uint32, C.c_int, i32p]
     L.ora_sample_stream.argtypes = [C.c_uint32, C.c_int, C.c_int, C.c_int, i32p]
     L.ora_pnp_create.restype = vp
@@ -504,3 +506,17 @@ def l1_score(ids1, v1, ids2, v2) -> float:
     a, b = np.ascontiguousarray(ids1, np.uint32), np.ascontiguousarray(ids2, np.uint32)
     return lib().ora_l1_score(len(a), a, np.ascontiguousarray(v1, np.float64), len(b), b,
                               np.ascontiguousarray(v2, np.float64))
+
+
+def optimize_sim3(p):
+    """Optimizer::OptimizeSim3 on the oracle for a rsc.synth.Sim3OptProblem: (nIn, S float64[8] = q (x, y,
+    z, w), t, s after the call, keep uint8[n] (0 where vpMatches1[i] is set to NULL), stats[4])."""
+    n = p.n
+    S = np.ascontiguousarray(p.S0, np.float64).copy()
+    keep = np.zeros(max(n, 1), np.uint8)
+    st = np.zeros(4, np.int32)
+    r = lib().ora_optimize_sim3(n, np.ascontiguousarray(p.valid, np.uint8), np.ascontiguousarray(p.X1w, np.float32),
+                                np.ascontiguousarray(p.X2w, np.float32), np.ascontiguousarray(p.uv1, np.float32),
+                                np.ascontiguousarray(p.uv2, np.float32), np.ascontiguousarray(p.inv1, np.float32),
+                                np.ascontiguousarray(p.inv2, np.float32), p.poses24(), p.K8(), float(p.th2), S, keep, st)
+    return r, S, keep[:n], st

@@ -315,3 +315,41 @@ def test_search_by_sim3_facade_matches_oracle(seed):
     exp = np.where(o12 >= 0, o12, m12)
     assert nf == onf and nf > 20
     assert np.array_equal(got, exp)
+
+
+def test_optimize_sim3_facade_matches_oracle():
+    """rsc_orb::OptimizeSim3 (Optimizer.cpp:1054-1250, LoopClosing.cpp:311) on mock KeyFrames /
+    MapPoints / g2o::Sim3: every reason a slot is not a correspondence (NULL match, NULL or bad
+    MapPoint 1, bad MapPoint 2, not in KF2), KF2 keypoints in another order; nIn, g2oS12 and the NULLed
+    vpMatches1 entries equal the oracle."""
+    rng = np.random.default_rng(61)
+    p = synth.make_sim3opt_problem(rng, 600, valid_frac=0.8, outlier_frac=0.2)
+    n1, n2 = p.n, p.n + 50
+    inv_levels = (np.float32(1.0) / synth.level_sigma2()).astype(np.float32)
+    oc1 = np.array([int(np.where(inv_levels == v)[0][0]) for v in p.inv1])
+    oc2 = np.array([int(np.where(inv_levels == v)[0][0]) for v in p.inv2])
+    i2 = rng.permutation(n2)[:n1]
+    kind = np.where(p.valid == 1, 5, rng.integers(0, 5, n1))
+    kp2 = np.zeros((n2, 2), np.float32)
+    o2 = np.zeros(n2, np.int32)
+    kp2[i2] = p.uv2
+    o2[i2] = oc2
+    buf = struct.pack("<iii", 8, n1, n2)
+    for R, t, K in ((p.R1w, p.t1w, p.K1), (p.R2w, p.t2w, p.K2)):
+        buf += np.asarray(R, "<f4").tobytes() + np.asarray(t, "<f4").tobytes() + np.asarray(K, "<f4").tobytes()
+        buf += struct.pack("<i", len(inv_levels)) + inv_levels.astype("<f4").tobytes()
+    for j in range(n2):
+        buf += struct.pack("<2fi", kp2[j, 0], kp2[j, 1], int(o2[j]))
+    for i in range(n1):
+        buf += struct.pack("<2fii3f3fi", p.uv1[i, 0], p.uv1[i, 1], int(oc1[i]), int(kind[i]), *p.X1w[i], *p.X2w[i],
+                           int(i2[i]))
+    buf += np.asarray(p.S0, "<f8").tobytes() + struct.pack("<f", p.th2)
+    out = run(buf)
+    nIn = struct.unpack_from("<i", out, 0)[0]
+    S = np.frombuffer(out, "<f8", 8, 4)
+    still = np.frombuffer(out, np.uint8, n1, 4 + 64)
+    r, So, keep, st = ol.optimize_sim3(p)
+    assert nIn == r and r > 100
+    assert np.array_equal(S.view(np.uint64), So.view(np.uint64))
+    expect = (kind != 0) & (keep == 1)
+    assert np.array_equal(still.astype(bool), expect)
