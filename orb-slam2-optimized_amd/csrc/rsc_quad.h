@@ -185,6 +185,15 @@ struct QuadLdsRows {
     }
 };
 
+// The quad's own three rows of Q (rows q, q+4, q+8 of the row-major 12x12 in T) as the rotation
+// sink of tridiag_qr_events12.
+struct QuadRowsEv {
+    double* T;
+    int q;
+    RSC_HD double load(int r, int col) const { return T[(4 * r + q) * 12 + col]; }
+    RSC_HD void store(int r, int col, double v) { T[(4 * r + q) * 12 + col] = v; }
+};
+
 // Eigenvectors of the four smallest eigenvalues of a symmetric 12x12 (SelfAdjointEigenSolver on
 // MtM, PnPsolver.cpp:379-382) by the four lanes of one quad (q = lane & 3): phases B-D of
 // pnp_eig_quad_body below as a standalone routine (used by the Refine kernel, where one quad of
@@ -245,7 +254,7 @@ __device__ __forceinline__ void quad_eig12_ev4(double* T, double* E, int q, Sync
 // Kernel 1 of the two-kernel hypothesis solve: sample, control points, alphas, MtM, and the 12x12
 // eigenvectors (quad-cooperative).  Writes the stage record (eigenvectors, alphas, cws) and the
 // sample indices.  STOP < 99 truncates (diagnostics only, tools/phase_bench).
-template <int NS, int STOP>
+template <int NS, int STOP, bool EVQR = false>
 __device__ __forceinline__ void pnp_eig_quad_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
                                                   const int2* __restrict__ wg_table, const uint32_t* __restrict__ rng_T,
                                                   double* __restrict__ stage, int32_t* __restrict__ samples,
@@ -355,13 +364,24 @@ __device__ __forceinline__ void pnp_eig_quad_body(const DevPnP* __restrict__ pro
     }
 
     // ---- D: implicit symmetric QR, rotations applied to the own rows ----
-    // The own rows of Q stay in LDS (T, row-major): the rotations' read-modify-writes are off the
-    // Givens chase's dependency chain, and keeping 36 doubles per lane out of the register file
-    // removes the chase's register spills (scratch round trips inside the QR loop).
+    // Sweep form (default): the own rows of Q stay in LDS (T, row-major), so the rotations'
+    // read-modify-writes are off the Givens chase's dependency chain.  The event form
+    // (tridiag_qr_events12, EVQR = true: each quad steps through its own sequence of sweep setups
+    // and single rotations) is bit-identical but measured slower on gfx950 (eig 175 us vs 164 us on
+    // config 2, tools/quad_bench): the union of the 16 quads' sweep windows is only ~12% above the
+    // per-quad event count (tools/qr_stats), less than the event form's extra control flow costs.
     {
-        QuadLdsRows qapply{T, q};
         int perm[12];
-        tridiag_qr<double, 12>(diag, sub, qapply, perm);
+        if (EVQR) {
+            double* ds = E;
+            RSC_UNROLL for (int i = 0; i < 12; ++i) ds[i] = diag[i];
+            RSC_UNROLL for (int i = 0; i < 11; ++i) ds[12 + i] = sub[i];
+            QuadRowsEv rows{T, q};
+            tridiag_qr_events12<3>(ds, rows, perm);
+        } else {
+            QuadLdsRows qapply{T, q};
+            tridiag_qr<double, 12>(diag, sub, qapply, perm);
+        }
         // sorted eigenvector columns 0..3 (the four smallest eigenvalues) of the own rows
         if (active) {
             RSC_UNROLL for (int j = 0; j < 3; ++j) {

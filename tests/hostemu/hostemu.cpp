@@ -622,4 +622,54 @@ void he_optimize_sim3(int m, const float* e12, const float* e21, const float* uv
     }
     stats[0] = nIn; stats[1] = nBad; stats[2] = its; stats[3] = trials;
 }
+
+// 12x12 symmetric eigen-decomposition checks of the event-form implicit QR: A (row-major, lower
+// triangle read) -> Householder tridiagonalisation (sym_eig12_tridiag), then both tridiag_qr and
+// tridiag_qr_events12 on copies.  out_*: diag after the QR (sorted when ok), perm, Q (144), ok.
+void he_qr_compare(const double* A, double* d_ref, int32_t* p_ref, double* q_ref, int32_t* ok_ref, double* d_ev,
+                   int32_t* p_ev, double* q_ev, int32_t* ok_ev) {
+    using namespace rsc;
+    std::vector<double> M(A, A + 144);
+    LaneMat L{M.data(), 1};
+    double diag[12], sub[11];
+    sym_eig12_tridiag(L, diag, sub);
+    std::vector<double> Q1(M), Q2(M);
+    {
+        auto qapply = [&](int k, double c, double s, bool apply) {
+            for (int i = 0; i < 12; ++i) {
+                const double xi = Q1[i * 12 + k], yi = Q1[i * 12 + k + 1];
+                Q1[i * 12 + k] = apply ? c * xi - s * yi : xi;
+                Q1[i * 12 + k + 1] = apply ? s * xi + c * yi : yi;
+            }
+        };
+        double dg[12], sb[11];
+        std::memcpy(dg, diag, sizeof(dg));
+        std::memcpy(sb, sub, sizeof(sb));
+        int perm[12];
+        *ok_ref = tridiag_qr<double, 12>(dg, sb, qapply, perm);
+        for (int i = 0; i < 12; ++i) { d_ref[i] = dg[i]; p_ref[i] = perm[i]; }
+        std::memcpy(q_ref, Q1.data(), 144 * 8);
+    }
+    {
+        struct Rows {
+            double* q;
+            double load(int r, int c) const { return q[r * 12 + c]; }
+            void store(int r, int c, double v) { q[r * 12 + c] = v; }
+        } rows{Q2.data()};
+        double ds[23];
+        std::memcpy(ds, diag, 96);
+        std::memcpy(ds + 12, sub, 88);
+        int perm[12];
+        *ok_ev = tridiag_qr_events12<12>(ds, rows, perm);
+        for (int i = 0; i < 12; ++i) p_ev[i] = perm[i];
+        std::memcpy(q_ev, Q2.data(), 144 * 8);
+        // the event form returns the sorted order via perm and leaves ds[] unsorted; sort a copy the
+        // same way tridiag_qr sorts its diag for the comparison
+        double d2[12];
+        int pp[12];
+        for (int i = 0; i < 12; ++i) { d2[i] = ds[i]; pp[i] = i; }
+        if (*ok_ev) eig_sort<double, 12>(d2, pp);
+        for (int i = 0; i < 12; ++i) d_ev[i] = d2[i];
+    }
+}
 }  // extern "C"

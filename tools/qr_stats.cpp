@@ -59,11 +59,17 @@ int main() {
     for (int h = 0; h < H; ++h) { sw_mean += sweeps[h].size(); rot_mean += rot[h]; }
     printf("per hypothesis: sweeps %.2f, rotations %.2f\n", sw_mean / H, rot_mean / H);
     for (int G : {1, 4, 16, 64}) {
-        double slots = 0, sweeps_w = 0, maxrot = 0;
+        double slots = 0, sweeps_w = 0, maxrot = 0, maxev = 0;
         for (int w = 0; w < H; w += G) {
             size_t ns = 0;
             double mr = 0;
-            for (int l = 0; l < G; ++l) { ns = std::max(ns, sweeps[w + l].size()); mr = std::max(mr, (double)rot[w + l]); }
+            double me = 0;
+            for (int l = 0; l < G; ++l) {
+                ns = std::max(ns, sweeps[w + l].size());
+                mr = std::max(mr, (double)rot[w + l]);
+                me = std::max(me, (double)(rot[w + l] + sweeps[w + l].size() + 1));  // event form: rotations + setups
+            }
+            maxev += me;
             for (size_t i = 0; i < ns; ++i) {
                 int lo = 99, hi = -1;
                 for (int l = 0; l < G; ++l)
@@ -74,8 +80,8 @@ int main() {
             maxrot += mr;
         }
         const double nw = (double)H / G;
-        printf("G=%2d lanes-hyps/wave: sweeps/wave %.2f  union slots/wave %.1f  max lane rotations %.1f\n", G,
-               sweeps_w / nw, slots / nw, maxrot / nw);
+        printf("G=%2d lanes-hyps/wave: sweeps/wave %.2f  union slots/wave %.1f  max lane rotations %.1f  "
+               "event form: max lane events %.1f\n", G, sweeps_w / nw, slots / nw, maxrot / nw, maxev / nw);
     }
     return 0;
 }

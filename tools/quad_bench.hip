@@ -17,11 +17,11 @@ __global__ __launch_bounds__(64) void eig_k(const DevPnP* probs, const LaunchPro
     __shared__ __attribute__((aligned(16))) double smem[kQuadHyps * kQuadRegion];
     pnp_eig_quad_body<4, STOP>(probs, lps, wgt, T, stage, samples, smem);
 }
-template <int STOP>
+template <int STOP, bool EVQR = false>
 __global__ __launch_bounds__(64, 2) void eig_k2(const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                                                 const uint32_t* T, double* stage, int32_t* samples) {
     __shared__ __attribute__((aligned(16))) double smem[kQuadHyps * kQuadRegion];
-    pnp_eig_quad_body<4, STOP>(probs, lps, wgt, T, stage, samples, smem);
+    pnp_eig_quad_body<4, STOP, EVQR>(probs, lps, wgt, T, stage, samples, smem);
 }
 __global__ __launch_bounds__(64) void eig_lane_k(const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                                                   const uint32_t* T, double* stage, int32_t* samples) {
@@ -230,7 +230,8 @@ int main(int argc, char** argv) {
     printf("eig2 A (sample..MtM)  %8.1f us\n", timeit([&] { eig_k2<1><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
     printf("eig2 A+tridiag        %8.1f us\n", timeit([&] { eig_k2<2><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
     printf("eig2 A+tri+accum      %8.1f us\n", timeit([&] { eig_k2<3><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
-    printf("eig2 full (+QR)       %8.1f us\n", timeit([&] { eig_k2<99><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
+    printf("eig2 full event-QR    %8.1f us\n", timeit([&] { eig_k2<99, true><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
+    printf("eig2 full sweep-QR    %8.1f us\n", timeit([&] { eig_k2<99, false><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
     printf("eig lane              %8.1f us\n", timeit([&] { eig_lane_k<<<n64, 64>>>(dprobs, dlps, dw64, dT, dst, dsm); }));
     std::vector<int4> hsv(total);
     for (int i = 0; i < total; ++i) {
