@@ -858,7 +858,7 @@ def headline_roofline(args, r):
             "achieved": round(tf, 4) if tf else None, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / FP64_PEAK_TFLOPS, 5) if tf else None,
             "traffic": round(meas) if meas else None,
-            "kernel": "EPnP hypothesis solve: pnp_eig_quad_kernel<4> + pnp_betas_kernel<4> "
+            "kernel": "EPnP hypothesis solve: pnp_eig_group_kernel<4> + pnp_betas_kernel<4> "
                       f"({per_launch_hyps} hypotheses per launch)",
             "algorithmic_flops_per_launch": round(per_launch_hyps * S_h) if S_h else None,
             "S_h_fp64_flops_per_hypothesis": S_h,

@@ -93,17 +93,17 @@ __global__ __launch_bounds__(64) void pnp_solve_kernel(const DevPnP* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------------
-// PnP hypotheses, two-kernel form (rsc_quad.h): quad-cooperative eigenvectors, then one wave per
-// beta approximation.
+// PnP hypotheses, two-kernel form (rsc_quad.h): lane-group eigenvectors (kEigLanes lanes per
+// hypothesis, kEigHyps per workgroup, one wave per SIMD), then one wave per beta approximation.
 // ------------------------------------------------------------------------------------------------
 template <int NS>
-__global__ __launch_bounds__(64, 2) void pnp_eig_quad_kernel(const DevPnP* __restrict__ probs,
+__global__ __launch_bounds__(64) void pnp_eig_group_kernel(const DevPnP* __restrict__ probs,
                                                           const LaunchProb* __restrict__ lps,
                                                           const int2* __restrict__ wg_table,
                                                           const uint32_t* __restrict__ rng_T,
                                                           double* __restrict__ stage, int32_t* __restrict__ samples) {
-    __shared__ __attribute__((aligned(16))) double smem[kQuadHyps * kQuadRegion];
-    pnp_eig_quad_body<NS, 99>(probs, lps, wg_table, rng_T, stage, samples, smem);
+    __shared__ __attribute__((aligned(16))) double smem[kEigHyps * kQuadRegion];
+    pnp_eig_group_body<NS, 99, kEigLanes, kEigHyps>(probs, lps, wg_table, rng_T, stage, samples, smem);
 }
 
 template <int NS>
@@ -751,7 +751,7 @@ hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchPr
     return hipGetLastError();
 }
 
-hipError_t launch_pnp_solve_split(bool quad, int ns, int nwg16, const int2* wgt16, int nwg64, const int2* wgt64,
+hipError_t launch_pnp_solve_split(bool quad, int ns, int nwgE, const int2* wgtE, int nwg64, const int2* wgt64,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, hipStream_t st, hipEvent_t eig_begin,
                                   hipEvent_t eig_end) {
@@ -761,7 +761,7 @@ hipError_t launch_pnp_solve_split(bool quad, int ns, int nwg16, const int2* wgt1
 #define RSC_CASE(N)                                                                                   \
     case N:                                                                                           \
         if (quad)                                                                                     \
-            pnp_eig_quad_kernel<N><<<nwg16, 64, 0, st>>>(probs, lps, wgt16, T, stage, samples);       \
+            pnp_eig_group_kernel<N><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples);        \
         else                                                                                          \
             pnp_eig_lane_kernel<N><<<nwg64, 64, 0, st>>>(probs, lps, wgt64, T, stage, samples);       \
         if (eig_end) (void)hipEventRecord(eig_end, st);                                               \

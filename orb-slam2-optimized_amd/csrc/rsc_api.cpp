@@ -323,7 +323,7 @@ struct HipPnPBackend : PnPBackend {
             const int g = S[i]->mRansacMinSet - 4;
             for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs[g].push_back(make_int2(i, h0));
             if (quad)
-                for (int h0 = 0; h0 < H[i]; h0 += kQuadHyps) quad_wgs[g].push_back(make_int2(i, h0));
+                for (int h0 = 0; h0 < H[i]; h0 += kEigHyps) quad_wgs[g].push_back(make_int2(i, h0));
             for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
         }
         Blob b;

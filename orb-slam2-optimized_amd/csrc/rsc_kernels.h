@@ -74,13 +74,14 @@ hipError_t launch_rng_stream(const uint32_t* T, const uint32_t* window, int g0, 
 
 hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                             const uint32_t* T, float* poses, int32_t* samples, hipStream_t st);
-constexpr int kQuadHyps = 16;          // hypotheses per workgroup of the quad-cooperative solve
+constexpr int kEigLanes = 2;           // lanes per hypothesis in the eigen-stage kernel (rsc_quad.h)
+constexpr int kEigHyps = 20;           // hypotheses per 64-lane eigen-stage workgroup (960 on config 2)
 constexpr int kAutoSolveMode = 2;      // see rsc_context::solve_mode
 // Per-hypothesis stage record between the two kernels: eigenvectors [12][4], alphas [NS][4], cws [4][3].
 constexpr int kStageDoubles = 48 + 24 + 12;
 // Two-kernel hypothesis solve: eigenvectors (quad-cooperative or lane per hypothesis), then the
 // three beta approximations (one wave each) + selection.
-hipError_t launch_pnp_solve_split(bool quad, int ns, int nwg16, const int2* wgt16, int nwg64, const int2* wgt64,
+hipError_t launch_pnp_solve_split(bool quad, int ns, int nwgE, const int2* wgtE, int nwg64, const int2* wgt64,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, hipStream_t st, hipEvent_t eig_begin = nullptr,
                                   hipEvent_t eig_end = nullptr);

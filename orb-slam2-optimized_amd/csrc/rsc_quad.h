@@ -1,16 +1,18 @@
-// rsc_quad.h — quad-cooperative EPnP hypothesis (4 lanes of a wave per hypothesis).
+// rsc_quad.h — lane-group EPnP hypothesis solve (2 or 4 lanes of a wave per hypothesis).
 //
 // Why: one lane per hypothesis runs PnPsolver::compute_pose as one long dependent FP64 chain, and a
 // relocalization batch (19,200 hypotheses) fills only 300 of the 1,024 SIMDs with one wave each, so
-// the solve is latency-bound.  Four lanes per hypothesis give 4x the waves and split the chain:
-//   * 12x12 Householder tridiagonalisation: lane q owns rows 4j+q (j = 0..2) of the full symmetric
-//     matrix in VGPRs; the Householder vector and A*v are exchanged with DPP quad broadcasts;
-//   * accumulation of the Householder sequence: lane q owns columns 4j+q of Q;
-//   * implicit QR: the Givens chase is computed redundantly by the 4 lanes (bitwise identical),
-//     each lane applies the rotations to its own 3 rows of Q;
+// the solve is latency-bound.  A group of L lanes per hypothesis splits the row work of the chain:
+//   * 12x12 Householder tridiagonalisation: member q owns rows L*j+q of the full symmetric matrix in
+//     VGPRs; the Householder vector and A*v are exchanged with DPP quad_perm broadcasts;
+//   * accumulation of the Householder sequence: member q owns columns L*j+q of Q;
+//   * implicit QR: the Givens chase is computed redundantly by the group (bitwise identical), each
+//     member applying the rotations to its own rows of Q;
 //   * the three beta approximations of PnPsolver.cpp:383-414 (+ Gauss-Newton + compute_R_and_t)
 //     run in a second kernel, one wave per approximation over 64 hypotheses, and the smallest
 //     error wins in the reference's order.
+// The product runs pairs (L = 2, 20 hypotheses per wave: 960 waves for the 1,024 SIMDs on config
+// 2); the Refine kernel's single eigenproblem uses one quad.
 // Every scalar is produced by the same operations on the same operands as the sequential
 // restatement (rsc_core.h / oracle), so results are bitwise identical; the only reorderings are of
 // independent scalars (and of max(), which is order-free for the non-NaN case handled below).
@@ -32,45 +34,54 @@ constexpr int kBetasSmemDoubles = (48 + 66) * 64 + 3 * 64 + 3 * 12 * 64 / 2;
 // Offset of step i's essential Householder vector (entries v[1..10-i]) in the E region.
 RSC_HD constexpr int quad_eoff(int i) { return 10 * i - (i * (i - 1)) / 2; }
 
-template <int SRC>
-__device__ __forceinline__ double qb_(double x) {
-    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), SRC * 0x55, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), SRC * 0x55, 0xF, 0xF, false);
+// Value of x in member SRC of this lane's group of L lanes (L = 4: the quad; L = 2: the pair,
+// lanes {0,1} and {2,3} of each quad) — one DPP quad_perm move per 32-bit half.
+template <int L, int SRC>
+__device__ __forceinline__ double gb_(double x) {
+    static_assert(L == 2 || L == 4, "lane groups of 2 or 4");
+    constexpr int ctrl = (L == 4) ? SRC * 0x55 : (SRC | (SRC << 2) | ((2 + SRC) << 4) | ((2 + SRC) << 6));
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), ctrl, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
 }
-// Value of x in lane `src` of this lane's quad (src is a compile-time constant after unrolling).
-__device__ __forceinline__ double qb(double x, int src) {
-    switch (src & 3) {
-        case 0: return qb_<0>(x);
-        case 1: return qb_<1>(x);
-        case 2: return qb_<2>(x);
-        default: return qb_<3>(x);
+// src is a compile-time constant after unrolling.
+template <int L>
+__device__ __forceinline__ double gb(double x, int src) {
+    switch (src % L) {
+        case 0: return gb_<L, 0>(x);
+        case 1: return gb_<L, 1>(x);
+        case 2: return gb_<L, (L == 4 ? 2 : 0)>(x);
+        default: return gb_<L, (L == 4 ? 3 : 1)>(x);
     }
 }
+template <int SRC>
+__device__ __forceinline__ double qb_(double x) { return gb_<4, SRC>(x); }
 
 // x[base + q] of a register array (static base), 0 outside [0, n).
-template <int n>
-__device__ __forceinline__ double sel4(const double (&x)[n], int base, int q) {
+template <int L, int n>
+__device__ __forceinline__ double seln(const double (&x)[n], int base, int q) {
     double r = 0.0;
-    RSC_UNROLL for (int t = 0; t < 4; ++t) {
+    RSC_UNROLL for (int t = 0; t < L; ++t) {
         const int i = base + t;
         if (i >= 0 && i < n && q == t) r = x[i];
     }
     return r;
 }
 
-// Tridiagonalisation of the scaled 12x12 (sym_eig12_tridiag, Householder part).  A: own rows,
-// full symmetric.  E: this hypothesis' essential-vector region (written by lane 0).
-__device__ __forceinline__ void quad_tridiag(double (&A)[3][12], int q, double* E, double (&diag)[12],
-                                             double (&sub)[11], double (&hC)[11]) {
-    constexpr int n = 12, NN = 11;
+// Tridiagonalisation of the scaled 12x12 (sym_eig12_tridiag, Householder part) by a group of L
+// lanes, member q owning rows L*j + q.  A: own rows, full symmetric.  E: this hypothesis'
+// essential-vector region (written by member 0).
+template <int L>
+__device__ __forceinline__ void group_tridiag(double (&A)[12 / L][12], int q, double* E, double (&diag)[12],
+                                              double (&sub)[11], double (&hC)[11]) {
+    constexpr int n = 12, NN = 11, RJ = 12 / L;
     RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
         const int rs = n - i - 1;
         double v[NN], w2[NN], hcv[NN];
         RSC_UNROLL for (int k = 0; k < NN; ++k) {
             v[k] = 0.0;
             hcv[k] = 0.0;
-            if (k < rs) v[k] = qb(A[(i + 1 + k) >> 2][i], (i + 1 + k) & 3);
+            if (k < rs) v[k] = gb<L>(A[(i + 1 + k) / L][i], (i + 1 + k) % L);
         }
         double tail = 0.0;
         if (rs > 1) {
@@ -96,54 +107,57 @@ __device__ __forceinline__ void quad_tridiag(double (&A)[3][12], int q, double* 
         }
         RSC_UNROLL for (int k = 0; k < NN; ++k) w2[k] = h * v[k];
         // own rows of hc = A_sub * (h v)
-        double hco[3];
-        RSC_UNROLL for (int j = 0; j < 3; ++j) {
+        double hco[RJ];
+        RSC_UNROLL for (int j = 0; j < RJ; ++j) {
             hco[j] = 0.0;
-            if (4 * j + 3 >= i + 1) {
+            if (L * j + L - 1 >= i + 1) {
                 double acc = A[j][i + 1] * w2[0];
                 RSC_UNROLL for (int m = 1; m < NN; ++m) if (m < rs) acc = acc + A[j][i + 1 + m] * w2[m];
                 hco[j] = acc;
             }
         }
-        RSC_UNROLL for (int k = 0; k < NN; ++k) if (k < rs) hcv[k] = qb(hco[(i + 1 + k) >> 2], (i + 1 + k) & 3);
+        RSC_UNROLL for (int k = 0; k < NN; ++k) if (k < rs) hcv[k] = gb<L>(hco[(i + 1 + k) / L], (i + 1 + k) % L);
         double dot = hcv[0] * v[0];
         RSC_UNROLL for (int k = 1; k < NN; ++k) if (k < rs) dot = dot + hcv[k] * v[k];
         const double alpha = (h * -0.5) * dot;
         RSC_UNROLL for (int k = 0; k < NN; ++k) if (k < rs) hcv[k] = hcv[k] + alpha * v[k];
         // rank-2 update of the own rows (both triangles: the mirrored element gets the same bits,
         // the two products are the same and IEEE addition commutes)
-        RSC_UNROLL for (int j = 0; j < 3; ++j) {
-            if (4 * j + 3 >= i + 1) {
-                const int kr = 4 * j + q - (i + 1);
-                const double vo = sel4(v, 4 * j - (i + 1), q);
-                const double ho = sel4(hcv, 4 * j - (i + 1), q);
+        RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+            if (L * j + L - 1 >= i + 1) {
+                const int kr = L * j + q - (i + 1);
+                const double vo = seln<L>(v, L * j - (i + 1), q);
+                const double ho = seln<L>(hcv, L * j - (i + 1), q);
                 if (kr >= 0) {
                     RSC_UNROLL for (int c = 0; c < NN; ++c)
                         if (c < rs) A[j][i + 1 + c] = A[j][i + 1 + c] + ((-v[c]) * ho + (-hcv[c]) * vo);
                 }
             }
         }
-        if (q == ((i + 1) & 3)) A[(i + 1) >> 2][i] = beta;
+        if (q == (i + 1) % L) A[(i + 1) / L][i] = beta;
         hC[i] = h;
     }
-    RSC_UNROLL for (int k = 0; k < n; ++k) diag[k] = qb(A[k >> 2][k], k & 3);
-    RSC_UNROLL for (int k = 0; k < n - 1; ++k) sub[k] = qb(A[(k + 1) >> 2][k], (k + 1) & 3);
+    RSC_UNROLL for (int k = 0; k < n; ++k) diag[k] = gb<L>(A[k / L][k], k % L);
+    RSC_UNROLL for (int k = 0; k < n - 1; ++k) sub[k] = gb<L>(A[(k + 1) / L][k], (k + 1) % L);
 }
 
-// Householder sequence evalTo (sym_eig12_tridiag, accumulation part), own columns 4j+q of Q.
-__device__ __forceinline__ void quad_accumulate(double (&Qc)[3][12], int q, const double* E, const double (&hC)[11]) {
-    RSC_UNROLL for (int j = 0; j < 3; ++j)
-        RSC_UNROLL for (int r = 0; r < 12; ++r) Qc[j][r] = (r == 4 * j + q) ? 1.0 : 0.0;
+// Householder sequence evalTo (sym_eig12_tridiag, accumulation part), own columns L*j + q of Q.
+template <int L>
+__device__ __forceinline__ void group_accumulate(double (&Qc)[12 / L][12], int q, const double* E,
+                                                 const double (&hC)[11]) {
+    constexpr int RJ = 12 / L;
+    RSC_UNROLL for (int j = 0; j < RJ; ++j)
+        RSC_UNROLL for (int r = 0; r < 12; ++r) Qc[j][r] = (r == L * j + q) ? 1.0 : 0.0;
     RSC_UNROLL for (int k = 10; k >= 0; --k) {
         const int cs = 11 - k, b0 = k + 1;
         const double tau = hC[k];
         if (cs == 1) {
-            if (q == 3) Qc[2][11] = Qc[2][11] * (1.0 - tau);
+            if (q == 11 % L) Qc[11 / L][11] = Qc[11 / L][11] * (1.0 - tau);
         } else if (tau != 0.0) {
             double ev[10];
             RSC_UNROLL for (int r = 0; r < 10; ++r) ev[r] = (r < cs - 1) ? E[quad_eoff(k) + r] : 0.0;
-            RSC_UNROLL for (int j = 0; j < 3; ++j) {
-                if (4 * j + 3 >= b0 && 4 * j + q >= b0) {
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                if (L * j + L - 1 >= b0 && L * j + q >= b0) {
                     double acc = ev[0] * Qc[j][b0 + 1];
                     RSC_UNROLL for (int r = 1; r < 10; ++r) if (r < cs - 1) acc = acc + ev[r] * Qc[j][b0 + 1 + r];
                     const double tmp = acc + Qc[j][b0];
@@ -160,33 +174,45 @@ __device__ __forceinline__ void quad_accumulate(double (&Qc)[3][12], int q, cons
     }
 }
 
-// The quad's own three rows of Q (rows q, q+4, q+8 of the row-major 12x12 in T) as the QR's
-// rotation sink: prefetch(k) loads columns k, k+1 at the top of the chase slot so the LDS round
-// trip overlaps the Givens computation; operator() rotates and stores them (tridiag_qr's
-// qapply contract: bit-identical values when !apply).
-struct QuadLdsRows {
+// The group's own rows of Q (rows L*j + q of the row-major 12x12 in T) as the QR's rotation sink:
+// prefetch(k) loads columns k, k+1 at the top of the chase slot so the LDS round trip overlaps the
+// Givens computation; operator() rotates and stores them (tridiag_qr's qapply contract:
+// bit-identical values when !apply).
+template <int L>
+struct GroupLdsRows {
+    static constexpr int RJ = 12 / L;
     double* T;
     int q;
-    double x[3], y[3];
+    double x[RJ], y[RJ];
     RSC_HD void prefetch(int k) {
-        RSC_UNROLL for (int j = 0; j < 3; ++j) {
-            const double* row = T + (4 * j + q) * 12;
+        RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+            const double* row = T + (L * j + q) * 12;
             x[j] = row[k];
             y[j] = row[k + 1];
         }
         __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the rotation's chain
     }
+    // Eigen skips identity rotations (c == 1, s == 0); the chase only produces one when an entry
+    // underflows, so the selects that keep the rows bit-identical then run behind a wave-uniform
+    // branch instead of on every rotation (4 fewer VALU instructions per row, tools/qr_bench).
     RSC_HD void operator()(int k, double c, double s, bool apply) {
-        RSC_UNROLL for (int j = 0; j < 3; ++j) {
-            double* row = T + (4 * j + q) * 12;
-            row[k] = apply ? c * x[j] - s * y[j] : x[j];
-            row[k + 1] = apply ? s * x[j] + c * y[j] : y[j];
+        if (__builtin_expect(__any(!apply), 0)) {
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                double* row = T + (L * j + q) * 12;
+                row[k] = apply ? c * x[j] - s * y[j] : x[j];
+                row[k + 1] = apply ? s * x[j] + c * y[j] : y[j];
+            }
+        } else {
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                double* row = T + (L * j + q) * 12;
+                row[k] = c * x[j] - s * y[j];
+                row[k + 1] = s * x[j] + c * y[j];
+            }
         }
     }
 };
 
-// The quad's own three rows of Q (rows q, q+4, q+8 of the row-major 12x12 in T) as the rotation
-// sink of tridiag_qr_events12.
+// The quad's own three rows of Q as the rotation sink of tridiag_qr_events12 (diagnostic variant).
 struct QuadRowsEv {
     double* T;
     int q;
@@ -194,9 +220,35 @@ struct QuadRowsEv {
     RSC_HD void store(int r, int col, double v) { T[(4 * r + q) * 12 + col] = v; }
 };
 
+// Scale of SelfAdjointEigenSolver = max |lower triangle| over the group's own rows (A: full
+// symmetric own rows, R = L*j + q); a NaN M(0,0) poisons it, as there.
+template <int L>
+__device__ __forceinline__ double group_scale(const double (&A)[12 / L][12], int q) {
+    double m = 0.0;
+    RSC_UNROLL for (int j = 0; j < 12 / L; ++j) {
+        const int R = L * j + q;
+        RSC_UNROLL for (int c = 0; c < 12; ++c) {
+            const double a = fabs(A[j][c]);
+            if (c <= R && a > m) m = a;
+        }
+    }
+    double scale = gb_<L, 0>(m);
+    const double m1 = gb_<L, 1>(m);
+    if (m1 > scale) scale = m1;
+    if (L == 4) {
+        const double m2 = gb_<L, (L == 4 ? 2 : 0)>(m), m3 = gb_<L, (L == 4 ? 3 : 1)>(m);
+        if (m2 > scale) scale = m2;
+        if (m3 > scale) scale = m3;
+    }
+    const double a00 = fabs(gb_<L, 0>(A[0][0]));
+    if (a00 != a00) scale = a00;
+    if (scale == 0.0) scale = 1.0;
+    return scale;
+}
+
 // Eigenvectors of the four smallest eigenvalues of a symmetric 12x12 (SelfAdjointEigenSolver on
 // MtM, PnPsolver.cpp:379-382) by the four lanes of one quad (q = lane & 3): phases B-D of
-// pnp_eig_quad_body below as a standalone routine (used by the Refine kernel, where one quad of
+// pnp_eig_group_body below as a standalone routine (used by the Refine kernel, where one quad of
 // wave 0 serves the workgroup).  T: the quad's 144-double LDS region holding the lower triangle
 // row-major (T[R*12+c], c <= R) on entry; E: 55 doubles of LDS scratch; sync(): an LDS
 // visibility point for the quad.  ev[j][c] = eigenvector column c of row 4j+q, bit-identical to
@@ -206,37 +258,25 @@ __device__ __forceinline__ void quad_eig12_ev4(double* T, double* E, int q, Sync
     double diag[12], sub[11], hC[11];
     {
         double A[3][12];
-        double m = 0.0;
         RSC_UNROLL for (int j = 0; j < 3; ++j) {
             const int R = 4 * j + q;
-            RSC_UNROLL for (int c = 0; c < 12; ++c) {
-                A[j][c] = T[(R >= c) ? R * 12 + c : c * 12 + R];
-                const double a = fabs(A[j][c]);
-                if (c <= R && a > m) m = a;
-            }
+            RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = T[(R >= c) ? R * 12 + c : c * 12 + R];
         }
-        double scale = qb_<0>(m);
-        const double m1 = qb_<1>(m), m2 = qb_<2>(m), m3 = qb_<3>(m);
-        if (m1 > scale) scale = m1;
-        if (m2 > scale) scale = m2;
-        if (m3 > scale) scale = m3;
-        const double a00 = fabs(qb_<0>(A[0][0]));
-        if (a00 != a00) scale = a00;
-        if (scale == 0.0) scale = 1.0;
+        const double scale = group_scale<4>(A, q);
         RSC_UNROLL for (int j = 0; j < 3; ++j)
             RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = A[j][c] / scale;
         sync();  // every lane has read T before phase C overwrites it
-        quad_tridiag(A, q, E, diag, sub, hC);
+        group_tridiag<4>(A, q, E, diag, sub, hC);
     }
     sync();
     {
         double Qc[3][12];
-        quad_accumulate(Qc, q, E, hC);
+        group_accumulate<4>(Qc, q, E, hC);
         RSC_UNROLL for (int j = 0; j < 3; ++j)
             RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + 4 * j + q] = Qc[j][r];
     }
     sync();
-    QuadLdsRows qapply{T, q};
+    GroupLdsRows<4> qapply{T, q};
     int perm[12];
     tridiag_qr<double, 12>(diag, sub, qapply, perm);
     RSC_UNROLL for (int j = 0; j < 3; ++j) {
@@ -252,25 +292,36 @@ __device__ __forceinline__ void quad_eig12_ev4(double* T, double* E, int q, Sync
 }
 
 // Kernel 1 of the two-kernel hypothesis solve: sample, control points, alphas, MtM, and the 12x12
-// eigenvectors (quad-cooperative).  Writes the stage record (eigenvectors, alphas, cws) and the
-// sample indices.  STOP < 99 truncates (diagnostics only, tools/phase_bench).
-template <int NS, int STOP, bool EVQR = false>
-__device__ __forceinline__ void pnp_eig_quad_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
-                                                  const int2* __restrict__ wg_table, const uint32_t* __restrict__ rng_T,
-                                                  double* __restrict__ stage, int32_t* __restrict__ samples,
-                                                  double* smem) {
-    const int lane = threadIdx.x, g = lane >> 2, q = lane & 3;
+// eigenvectors, L lanes per hypothesis (a lane group), HPW hypotheses per 64-lane workgroup
+// (HPW * L <= 64; lanes beyond leave at once).  Writes the stage record (eigenvectors, alphas, cws)
+// and the sample indices.  STOP < 99 truncates (diagnostics only, tools/quad_bench).
+//
+// Why pairs (L = 2, the product's choice): the implicit-QR chase is a serial FP64 chain that every
+// lane of a group computes redundantly, so the wave's instruction stream costs the same whether it
+// serves 16 hypotheses (quads) or 32 (pairs); a group only shares the row work (the rotations on
+// Q, the Householder updates).  A config-2 batch (19,200 hypotheses) is 1,200 quad waves for the
+// 1,024 SIMDs — the last 176 SIMDs run two waves back to back — but 600 pair waves, one per SIMD.
+template <int NS, int STOP, int L, int HPW, bool EVQR = false>
+__device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
+                                                   const int2* __restrict__ wg_table, const uint32_t* __restrict__ rng_T,
+                                                   double* __restrict__ stage, int32_t* __restrict__ samples,
+                                                   double* smem) {
+    static_assert(HPW * L <= 64 && (L == 2 || L == 4), "lane groups of 2 or 4 within one wave");
+    static_assert(!EVQR || L == 4, "event-form QR: quads only");
+    constexpr int RJ = 12 / L;
+    const int lane = threadIdx.x, g = lane / L, q = lane % L;
+    if (g >= HPW) return;  // whole groups only: the DPP broadcasts never read a departed lane
     const int2 wt = wg_table[blockIdx.x];
     const LaunchProb& lp = lps[wt.x];
     const bool active = wt.y + g < lp.H;
-    const int h = active ? wt.y + g : lp.H - 1;  // idle quads repeat the last hypothesis (no writes)
+    const int h = active ? wt.y + g : lp.H - 1;  // idle groups repeat the last hypothesis (no writes)
     const DevPnP& P = probs[lp.prob];
     const size_t rec = (size_t)(lp.out0 + h);
     double* out = stage + rec * kStageDoubles;
     double* T = smem + g * kQuadRegion;
     double* E = T + kQuadT;
 
-    // ---- A: sample, control points, alphas, MtM (all four lanes, identical values) ----
+    // ---- A: sample, control points, alphas, MtM (every lane of the group, identical values) ----
     {
         int idx[NS];
         uint32_t w[31];
@@ -311,28 +362,15 @@ __device__ __forceinline__ void pnp_eig_quad_body(const DevPnP* __restrict__ pro
     // ---- B: scale + tridiagonalise (own rows) ----
     double diag[12], sub[11], hC[11];
     {
-        double A[3][12];
-        double m = 0.0;
-        RSC_UNROLL for (int j = 0; j < 3; ++j) {
-            const int R = 4 * j + q;
-            RSC_UNROLL for (int c = 0; c < 12; ++c) {
-                A[j][c] = T[(R >= c) ? R * 12 + c : c * 12 + R];
-                const double a = fabs(A[j][c]);
-                if (c <= R && a > m) m = a;
-            }
+        double A[RJ][12];
+        RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+            const int R = L * j + q;
+            RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = T[(R >= c) ? R * 12 + c : c * 12 + R];
         }
-        // SelfAdjointEigenSolver scale = max |lower triangle|; a NaN M(0,0) poisons it, as there
-        double scale = qb_<0>(m);
-        const double m1 = qb_<1>(m), m2 = qb_<2>(m), m3 = qb_<3>(m);
-        if (m1 > scale) scale = m1;
-        if (m2 > scale) scale = m2;
-        if (m3 > scale) scale = m3;
-        const double a00 = fabs(qb_<0>(A[0][0]));
-        if (a00 != a00) scale = a00;
-        if (scale == 0.0) scale = 1.0;
-        RSC_UNROLL for (int j = 0; j < 3; ++j)
+        const double scale = group_scale<L>(A, q);
+        RSC_UNROLL for (int j = 0; j < RJ; ++j)
             RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = A[j][c] / scale;
-        quad_tridiag(A, q, E, diag, sub, hC);
+        group_tridiag<L>(A, q, E, diag, sub, hC);
     }
     __syncthreads();
     if (STOP == 2) {
@@ -347,51 +385,51 @@ __device__ __forceinline__ void pnp_eig_quad_body(const DevPnP* __restrict__ pro
 
     // ---- C: accumulate Q (own columns), transpose to row-major Q in this hypothesis' T region ----
     {
-        double Qc[3][12];
-        quad_accumulate(Qc, q, E, hC);
-        RSC_UNROLL for (int j = 0; j < 3; ++j)
-            RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + 4 * j + q] = Qc[j][r];
+        double Qc[RJ][12];
+        group_accumulate<L>(Qc, q, E, hC);
+        RSC_UNROLL for (int j = 0; j < RJ; ++j)
+            RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + L * j + q] = Qc[j][r];
     }
     __syncthreads();
     if (STOP == 3) {
         if (active) {
             double acc = 0.0;
-            RSC_UNROLL for (int j = 0; j < 3; ++j)
-                RSC_UNROLL for (int c = 0; c < 12; ++c) acc += T[(4 * j + q) * 12 + c];
+            RSC_UNROLL for (int j = 0; j < RJ; ++j)
+                RSC_UNROLL for (int c = 0; c < 12; ++c) acc += T[(L * j + q) * 12 + c];
             out[q] = acc + diag[0] + sub[0];
         }
         return;
     }
 
     // ---- D: implicit symmetric QR, rotations applied to the own rows ----
-    // Sweep form (default): the own rows of Q stay in LDS (T, row-major), so the rotations'
-    // read-modify-writes are off the Givens chase's dependency chain.  The event form
-    // (tridiag_qr_events12, EVQR = true: each quad steps through its own sequence of sweep setups
-    // and single rotations) is bit-identical but measured slower on gfx950 (eig 175 us vs 164 us on
-    // config 2, tools/quad_bench): the union of the 16 quads' sweep windows is only ~12% above the
-    // per-quad event count (tools/qr_stats), less than the event form's extra control flow costs.
+    // Sweep form: the own rows of Q stay in LDS (T, row-major), so the rotations' read-modify-
+    // writes are off the Givens chase's dependency chain.  The event form (tridiag_qr_events12,
+    // EVQR = true: each quad steps through its own sequence of sweep setups and single rotations)
+    // is bit-identical but measured slower on gfx950 (eig 175 us vs 164 us on config 2 with quads,
+    // tools/quad_bench): the union of the quads' sweep windows is only ~12% above the per-quad
+    // event count (tools/qr_stats), less than the event form's extra control flow costs.
     {
         int perm[12];
-        if (EVQR) {
+        if constexpr (EVQR) {
             double* ds = E;
             RSC_UNROLL for (int i = 0; i < 12; ++i) ds[i] = diag[i];
             RSC_UNROLL for (int i = 0; i < 11; ++i) ds[12 + i] = sub[i];
             QuadRowsEv rows{T, q};
             tridiag_qr_events12<3>(ds, rows, perm);
         } else {
-            QuadLdsRows qapply{T, q};
+            GroupLdsRows<L> qapply{T, q};
             tridiag_qr<double, 12>(diag, sub, qapply, perm);
         }
         // sorted eigenvector columns 0..3 (the four smallest eigenvalues) of the own rows
         if (active) {
-            RSC_UNROLL for (int j = 0; j < 3; ++j) {
-                const double* row = T + (4 * j + q) * 12;
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                const double* row = T + (L * j + q) * 12;
                 double Qr[12];
                 RSC_UNROLL for (int p = 0; p < 12; ++p) Qr[p] = row[p];
                 RSC_UNROLL for (int c = 0; c < 4; ++c) {
                     double x = Qr[0];
                     RSC_UNROLL for (int p = 1; p < 12; ++p) x = (perm[c] == p) ? Qr[p] : x;
-                    out[kStEv + (4 * j + q) * 4 + c] = x;
+                    out[kStEv + (L * j + q) * 4 + c] = x;
                 }
             }
         }

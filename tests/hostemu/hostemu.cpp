@@ -672,4 +672,36 @@ void he_qr_compare(const double* A, double* d_ref, int32_t* p_ref, double* q_ref
         for (int i = 0; i < 12; ++i) d_ev[i] = d2[i];
     }
 }
+// The split chase (QrChase12 + QrRowApply, rsc_core.h) with the log cut into chunks of `cap`
+// rotations, as the eigen-stage kernel replays it: eigenvalues (sorted), perm, Q, converged flag.
+void he_qr_split(const double* A, int cap, double* d_out, int32_t* p_out, double* q_out, int32_t* ok_out) {
+    using namespace rsc;
+    std::vector<double> M(A, A + 144);
+    LaneMat L{M.data(), 1};
+    double diag[12], sub[11];
+    sym_eig12_tridiag(L, diag, sub);
+    double ds[23];
+    std::memcpy(ds, diag, 96);
+    std::memcpy(ds + 12, sub, 88);
+    auto DS = [&](int i) -> double& { return ds[i]; };
+    QrChase12 ch;
+    ch.init(DS);
+    std::vector<int> lk(cap);
+    std::vector<double> lc(cap), ls(cap);
+    QrRowApply ra[12];
+    while (true) {
+        const int nl = ch.run(DS, [&](int e, int k, double c, double s) { lk[e] = k; lc[e] = c; ls[e] = s; }, cap);
+        for (int e = 0; e < nl; ++e)
+            for (int r = 0; r < 12; ++r) ra[r].step(&M[r * 12], lk[e], lc[e], ls[e]);
+        if (!ch.active) break;
+    }
+    for (int r = 0; r < 12; ++r) ra[r].flush(&M[r * 12]);
+    *ok_out = ch.converged();
+    double d2[12];
+    int pp[12];
+    for (int i = 0; i < 12; ++i) { d2[i] = ds[i]; pp[i] = i; }
+    if (*ok_out) eig_sort<double, 12>(d2, pp);
+    for (int i = 0; i < 12; ++i) { d_out[i] = d2[i]; p_out[i] = pp[i]; }
+    std::memcpy(q_out, M.data(), 144 * 8);
+}
 }  // extern "C"

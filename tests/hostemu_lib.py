@@ -35,6 +35,7 @@ def lib():
         L.he_sim3_count.argtypes = [f32p, f32p, f32p, C.c_int, f32p, f32p, f32p, f32p, u64p, u64p, u8p]
         L.he_pose_optimization.argtypes = [C.c_int, f32p, f32p, f32p, f32p, f32p, u8p, C.c_void_p, C.c_float]
         L.he_qr_compare.argtypes = [f64p, f64p, i32p, f64p, i32p, f64p, i32p, f64p, i32p]
+        L.he_qr_split.argtypes = [f64p, C.c_int, f64p, i32p, f64p, i32p]
         L.he_optimize_sim3.argtypes = [C.c_int, f32p, f32p, f32p, f32p, C.c_float, f64p, u8p, i32p]
         _lib = L
     return _lib

@@ -1,4 +1,5 @@
-"""CPU: the event form of the 12x12 implicit symmetric QR (rsc_core.h tridiag_qr_events12, used by
+"""CPU: the event form and the split chase (QrChase12 + QrRowApply: one lane chases and logs the
+rotations, any lanes replay them on rows of Q, in chunks) of the 12x12 implicit symmetric QR (rsc_core.h tridiag_qr_events12, used by
 the hypothesis eigen-stage kernel) is bit-identical to the sweep form tridiag_qr (the restated
 SelfAdjointEigenSolver) — eigenvalues, sort permutation, eigenvector matrix and the converged flag —
 on EPnP-like spectra (four near-null eigenvalues), wide dynamic ranges, repeated and exactly zero
@@ -17,12 +18,27 @@ def run(A):
     return out
 
 
-def check(A):
-    d1, p1, q1, o1, d2, p2, q2, o2 = run(A)
+def split(A, cap):
+    A = np.ascontiguousarray(A, np.float64).reshape(144)
+    out = [np.zeros(12), np.zeros(12, np.int32), np.zeros(144), np.zeros(1, np.int32)]
+    hl.lib().he_qr_split(A, cap, *out)
+    return out
+
+
+def same(a, b):
+    d1, p1, q1, o1 = a
+    d2, p2, q2, o2 = b
     assert o1[0] == o2[0]
     assert np.array_equal(p1, p2)
     assert np.array_equal(d1.view(np.uint64), d2.view(np.uint64))
     assert np.array_equal(q1.view(np.uint64), q2.view(np.uint64))
+
+
+def check(A):
+    r = run(A)
+    same(r[:4], r[4:])
+    for cap in (1, 7, 32):
+        same(r[:4], split(A, cap))
 
 
 def spd(rng, lams):

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-(kernel, grid size) dispatch statistics from a rocprofv3 kernel_trace.csv, so the launches
-of one bench section (e.g. config 2: pnp_eig_quad_kernel<4> with grid 77824) can be compared with
+of one bench section (e.g. config 2: pnp_eig_group_kernel<4> with grid 61440) can be compared with
 the HIP-event durations bench.py reports.  usage: kernel_stats_by_grid.py trace.csv [out.csv]"""
 import csv
 import re

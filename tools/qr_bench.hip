@@ -1,0 +1,578 @@
+// qr_bench.hip — diagnostic: the implicit-QR stage of the 12x12 EPnP eigen-solver in isolation, on
+// config-2 shaped matrices (64 x 300 hypotheses, tridiagonalised on the host), in three mappings:
+//   quad  : the product's sweep form (4 lanes per hypothesis, 16 per wave, chase computed by all
+//           four lanes, each applying the rotations to its 3 rows of Q in LDS);
+//   split : one lane per hypothesis runs the chase (QrChase12) and logs the rotations to LDS in
+//           chunks of L; LPH lanes per hypothesis replay them on their rows of Q (QrRowApply);
+//   *-null: the chase alone (no Q), to separate the chase from the row updates.
+// Every variant's Q / perm / eigenvalues are checked bit-exact against tridiag_qr on the host.
+// Not part of the product.  Build: make -C tools qr_bench; run: ./build/qr_bench
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <type_traits>
+#include <vector>
+#include "../orb-slam2-optimized_amd/csrc/rsc_epnp.h"
+
+using namespace rsc;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+constexpr int kQS = 145;  // LDS stride of one hypothesis' Q (odd: spreads hypotheses over the banks)
+
+struct NullSink {
+    RSC_HD void operator()(int, double, double, bool) {}
+};
+
+// quad sweep form (as pnp_eig_group_body phase D)
+template <bool APPLY>
+__global__ __launch_bounds__(64, 2) void qr_quad_k(const double* __restrict__ dsub, const double* __restrict__ Qin,
+                                                   double* __restrict__ Qout, double* __restrict__ dout,
+                                                   int* __restrict__ pout, int H) {
+    __shared__ __attribute__((aligned(16))) double T[16 * 144];
+    const int lane = threadIdx.x, g = lane >> 2, q = lane & 3;
+    const int h0 = blockIdx.x * 16;
+    for (int i = lane; i < 16 * 144; i += 64) {
+        const int hh = h0 + i / 144;
+        T[i] = hh < H ? Qin[(size_t)h0 * 144 + i] : 0.0;
+    }
+    const int h = min(h0 + g, H - 1);
+    double diag[12], sub[11];
+    RSC_UNROLL for (int i = 0; i < 12; ++i) diag[i] = dsub[(size_t)h * 23 + i];
+    RSC_UNROLL for (int i = 0; i < 11; ++i) sub[i] = dsub[(size_t)h * 23 + 12 + i];
+    __syncthreads();
+    int perm[12];
+    double* Th = T + g * 144;
+    if (APPLY) {
+        struct Rows {
+            double* T;
+            int q;
+            double x[3], y[3];
+            RSC_HD void prefetch(int k) {
+                RSC_UNROLL for (int j = 0; j < 3; ++j) {
+                    x[j] = T[(4 * j + q) * 12 + k];
+                    y[j] = T[(4 * j + q) * 12 + k + 1];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            RSC_HD void operator()(int k, double c, double s, bool apply) {
+                RSC_UNROLL for (int j = 0; j < 3; ++j) {
+                    T[(4 * j + q) * 12 + k] = apply ? c * x[j] - s * y[j] : x[j];
+                    T[(4 * j + q) * 12 + k + 1] = apply ? s * x[j] + c * y[j] : y[j];
+                }
+            }
+        } rows{Th, q};
+        tridiag_qr<double, 12>(diag, sub, rows, perm);
+    } else {
+        tridiag_qr<double, 12>(diag, sub, NullSink{}, perm);
+    }
+    if (h0 + g < H) {
+        if (APPLY)
+            RSC_UNROLL for (int j = 0; j < 3; ++j)
+                RSC_UNROLL for (int c = 0; c < 12; ++c) Qout[(size_t)(h0 + g) * 144 + (4 * j + q) * 12 + c] = Th[(4 * j + q) * 12 + c];
+        if (q == 0) {
+            RSC_UNROLL for (int i = 0; i < 12; ++i) {
+                dout[(size_t)(h0 + g) * 12 + i] = diag[i];
+                pout[(size_t)(h0 + g) * 12 + i] = perm[i];
+            }
+        }
+    }
+}
+
+// split form: G hypotheses per 64-lane workgroup, lane l < G chases hypothesis l, lanes
+// [LPH*a, LPH*a + LPH) replay hypothesis a's log on rows part + LPH*j.
+template <int G, int LPH, int L, bool APPLY>
+__global__ __launch_bounds__(64) void qr_split_k(const double* __restrict__ dsub, const double* __restrict__ Qin,
+                                                 double* __restrict__ Qout, double* __restrict__ dout,
+                                                 int* __restrict__ pout, int H) {
+    static_assert(G * LPH <= 64 && 12 % LPH == 0, "mapping");
+    constexpr int R = 12 / LPH;
+    __shared__ __attribute__((aligned(16))) double sQ[APPLY ? G * kQS : 1];
+    __shared__ double sds[23 * G];
+    __shared__ double slc[L * G], sls[L * G];
+    __shared__ uint8_t slk[L * G];
+    __shared__ int scount[G];
+    const int lane = threadIdx.x;
+    const int h0 = blockIdx.x * G;
+    if (APPLY)
+        for (int i = lane; i < G * 144; i += 64) {
+            const int a = i / 144, e = i - a * 144;
+            sQ[a * kQS + e] = (h0 + a < H) ? Qin[(size_t)h0 * 144 + i] : 0.0;
+        }
+    for (int i = lane; i < G * 23; i += 64) {
+        const int a = i / 23, e = i - a * 23;
+        sds[e * G + a] = (h0 + a < H) ? dsub[(size_t)h0 * 23 + i] : 0.0;
+    }
+    __syncthreads();
+    const bool chaser = lane < G && h0 + lane < H;
+    auto DS = [&](int i) -> double& { return sds[i * G + lane]; };
+    QrChase12 ch;
+    if (chaser) ch.init(DS);
+    else ch.active = false;
+    const int a = lane / LPH, part = lane - a * LPH;
+    const bool applier = APPLY && a < G && h0 + a < H;
+    QrRowApply ra[R];
+    double* rowb = sQ + a * kQS + part * 12;
+    bool more = true;
+    while (more) {
+        if (chaser) {
+            const int nl = ch.run(DS, [&](int e, int k, double c, double s) {
+                slc[e * G + lane] = c;
+                sls[e * G + lane] = s;
+                slk[e * G + lane] = (uint8_t)k;
+            }, L);
+            scount[lane] = nl;
+        }
+        __syncthreads();
+        if (applier) {
+            const int na = scount[a];
+            for (int e = 0; e < na; ++e) {
+                const int k = slk[e * G + a];
+                const double c = slc[e * G + a], s = sls[e * G + a];
+                RSC_UNROLL for (int r = 0; r < R; ++r) ra[r].step(rowb + r * LPH * 12, k, c, s);
+            }
+        }
+        more = __syncthreads_or(chaser && ch.active);
+    }
+    if (applier) {
+        RSC_UNROLL for (int r = 0; r < R; ++r) ra[r].flush(rowb + r * LPH * 12);
+    }
+    __syncthreads();
+    if (APPLY)
+        for (int i = lane; i < G * 144; i += 64) {
+            const int aa = i / 144, e = i - aa * 144;
+            if (h0 + aa < H) Qout[(size_t)h0 * 144 + i] = sQ[aa * kQS + e];
+        }
+    if (chaser) {
+        double d[12];
+        int perm[12];
+        RSC_UNROLL for (int i = 0; i < 12; ++i) { d[i] = DS(i); perm[i] = i; }
+        if (ch.converged()) eig_sort<double, 12>(d, perm);
+        RSC_UNROLL for (int i = 0; i < 12; ++i) {
+            dout[(size_t)(h0 + lane) * 12 + i] = d[i];
+            pout[(size_t)(h0 + lane) * 12 + i] = perm[i];
+        }
+    }
+}
+
+// ---- device fast paths (candidates for rsc_core.h): the compiler's IEEE f64 sequences without
+// the range scaling / special-case fixups, for operands where those are the identity ----
+// sqrt(x) for x in [1, 2]
+__device__ __forceinline__ double sqrt12(double x) {
+    double g = __builtin_amdgcn_rsq(x);
+    double s = x * g;
+    double h = g * 0.5;
+    const double r = __builtin_fma(-h, s, 0.5);
+    s = __builtin_fma(s, r, s);
+    double d = __builtin_fma(-s, s, x);
+    h = __builtin_fma(h, r, h);
+    s = __builtin_fma(d, h, s);
+    d = __builtin_fma(-s, s, x);
+    return __builtin_fma(d, h, s);
+}
+// n / d for d, n normal within [2^-256, 2^256] (or n == 0)
+__device__ __forceinline__ double div_nr(double n, double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double q = n * r;
+    const double rem = __builtin_fma(-d, q, n);
+    return __builtin_fma(rem, r, q);
+}
+__device__ __forceinline__ bool mid_range(double v) {
+    const unsigned e = (__double2hiint(v) >> 20) & 0x7ff;
+    return e - (1023u - 256u) <= 512u;
+}
+
+__global__ void check_fast(const double* xs, const double* ns, const double* ds, int n, unsigned long long* bad) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double x = xs[i];
+    unsigned long long b = 0;
+    if (__double_as_longlong(sqrt12(x)) != __double_as_longlong(sqrt(x))) b |= 1;
+    if (__double_as_longlong(div_nr(1.0, sqrt(x))) != __double_as_longlong(1.0 / sqrt(x))) b |= 2;
+    const double nn = ns[i], dd = ds[i];
+    if (mid_range(dd) && (nn == 0.0 || mid_range(nn)) &&
+        __double_as_longlong(div_nr(nn, dd)) != __double_as_longlong(nn / dd)) b |= 4;
+    if (b) atomicOr(bad, b);
+}
+
+// makeGivens (rsc_core.h make_givens) with fast paths: OPT & 1 -> sqrt12 + div_nr for 1/u,
+// OPT & 2 -> guarded div_nr for t, OPT & 4 -> one product t*r and fewer selects.
+template <int OPT>
+__device__ __forceinline__ void givens_x(double p, double q, double& c, double& s) {
+    const bool big = fabs(p) > fabs(q);
+    const double nn = big ? q : p, dd = big ? p : q;
+    double t;
+    if (OPT & 2) {
+        t = div_nr(nn, dd);
+        const bool ok = mid_range(dd) && (nn == 0.0 || mid_range(nn));
+        if (!ok) t = nn / dd;
+    } else {
+        t = nn / dd;
+    }
+    double u = (OPT & 1) ? sqrt12(1.0 + t * t) : sqrt(1.0 + t * t);
+    if (dd < 0.0) u = -u;
+    const double r = (OPT & 1) ? div_nr(1.0, u) : 1.0 / u;
+    double cc, ss;
+    if (OPT & 4) {
+        const double m = t * r;  // = (-t) * (-r) of the !big branch
+        cc = big ? r : m;
+        ss = -(big ? m : r);
+        if (p == 0.0) cc = 0.0;
+        if (q == 0.0) { cc = (p < 0.0) ? -1.0 : 1.0; ss = 0.0; }
+    } else {
+        const double sb = -r;
+        cc = big ? r : (-t) * sb;
+        ss = big ? (-t) * r : sb;
+        if (p == 0.0) { cc = 0.0; ss = (q < 0.0) ? 1.0 : -1.0; }
+        if (q == 0.0) { cc = (p < 0.0) ? -1.0 : 1.0; ss = 0.0; }
+    }
+    c = cc;
+    s = ss;
+}
+
+// tridiag_qr<double, 12> (rsc_core.h) with givens_x<OPT>
+template <int OPT, typename QApply>
+__device__ __forceinline__ bool tridiag_qr_x(double (&diag)[12], double (&sub)[11], QApply&& qapply, int (&perm)[12]) {
+    constexpr int n = 12;
+    const int maxIterations = 30;
+    int end = n - 1, start = 0, iter = 0;
+    const double considerAsZero = lim<double>::min();
+    const double precision_inv = 1.0 / lim<double>::eps();
+    bool run = true;
+    while (run) {
+        RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
+            if (i >= start && i < end) {
+                if (fabs(sub[i]) < considerAsZero) {
+                    sub[i] = 0.0;
+                } else {
+                    const double scaled = precision_inv * sub[i];
+                    if (scaled * scaled <= (fabs(diag[i]) + fabs(diag[i + 1]))) sub[i] = 0.0;
+                }
+            }
+        }
+        RSC_UNROLL for (int i = n - 2; i >= 0; --i)
+            if (i == end - 1 && sub[i] == 0.0) end--;
+        run = end > 0;
+        if (run) {
+            iter++;
+            run = iter <= maxIterations * n;
+        }
+        if (!run) continue;
+        start = end - 1;
+        RSC_UNROLL for (int i = n - 2; i >= 0; --i)
+            if (i == start - 1 && sub[i] != 0.0) start--;
+        double dEm1 = 0.0, dE = 0.0, eE = 0.0, dS = 0.0, zS = 0.0;
+        RSC_UNROLL for (int j = 1; j < n; ++j)
+            if (j == end) { dEm1 = diag[j - 1]; dE = diag[j]; eE = sub[j - 1]; }
+        RSC_UNROLL for (int j = 0; j < n - 1; ++j)
+            if (j == start) { dS = diag[j]; zS = sub[j]; }
+        double td = (dEm1 - dE) * 0.5;
+        double e = eE;
+        double mu = dE;
+        if (td == 0.0) {
+            mu -= fabs(e);
+        } else {
+            double e2 = eE * eE;
+            double h = eig_hypot(td, e);
+            if (e2 == 0.0)
+                mu -= (e / (td + (td > 0.0 ? 1.0 : -1.0))) * (e / h);
+            else
+                mu -= e2 / (td + (td > 0.0 ? h : -h));
+        }
+        double x = dS - mu;
+        double z = zS;
+        RSC_UNROLL for (int k = 0; k < n - 1; ++k) {
+            if (k >= start && k < end) {
+                if constexpr (qr_has_prefetch<QApply>::value) qapply.prefetch(k);
+                double c, s;
+                givens_x<OPT>(x, z, c, s);
+                double sdk = s * diag[k] + c * sub[k];
+                double dkp1 = s * sub[k] + c * diag[k + 1];
+                diag[k] = c * (c * diag[k] - s * sub[k]) - s * (c * sub[k] - s * diag[k + 1]);
+                diag[k + 1] = s * sdk + c * dkp1;
+                sub[k] = c * sdk - s * dkp1;
+                if (k > 0 && k > start) sub[k - 1] = c * sub[k - 1] - s * z;
+                x = sub[k];
+                if (k < n - 2 && k < end - 1) {
+                    z = -s * sub[k + 1];
+                    sub[k + 1] = c * sub[k + 1];
+                }
+                qapply(k, c, s, !(c == 1.0 && s == 0.0));
+            }
+        }
+        RSC_LOOP_FENCE();
+    }
+    const bool ok = (iter <= maxIterations * n);
+    RSC_UNROLL for (int i = 0; i < n; ++i) perm[i] = i;
+    if (ok) eig_sort<double, n>(diag, perm);
+    return ok;
+}
+
+// rows in LDS (the product's GroupLdsRows)
+template <int L>
+struct LdsRowsX {
+    static constexpr int RJ = 12 / L;
+    double* T;
+    int q;
+    double x[RJ], y[RJ];
+    RSC_HD void prefetch(int k) {
+        RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+            x[j] = T[(L * j + q) * 12 + k];
+            y[j] = T[(L * j + q) * 12 + k + 1];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    RSC_HD void operator()(int k, double c, double s, bool apply) {
+        RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+            T[(L * j + q) * 12 + k] = apply ? c * x[j] - s * y[j] : x[j];
+            T[(L * j + q) * 12 + k + 1] = apply ? s * x[j] + c * y[j] : y[j];
+        }
+    }
+};
+// rows in LDS, identity-rotation selects only when a lane of the wave has one (uniform branch)
+template <int L>
+struct LdsRowsUni {
+    static constexpr int RJ = 12 / L;
+    double* T;
+    int q;
+    double x[RJ], y[RJ];
+    RSC_HD void prefetch(int k) {
+        RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+            x[j] = T[(L * j + q) * 12 + k];
+            y[j] = T[(L * j + q) * 12 + k + 1];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    RSC_HD void operator()(int k, double c, double s, bool apply) {
+        if (__builtin_expect(__any(!apply), 0)) {
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                T[(L * j + q) * 12 + k] = apply ? c * x[j] - s * y[j] : x[j];
+                T[(L * j + q) * 12 + k + 1] = apply ? s * x[j] + c * y[j] : y[j];
+            }
+        } else {
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                T[(L * j + q) * 12 + k] = c * x[j] - s * y[j];
+                T[(L * j + q) * 12 + k + 1] = s * x[j] + c * y[j];
+            }
+        }
+    }
+};
+// rows in registers (static k after unrolling); UNI: the identity-rotation select only when a lane
+// of the wave has one (wave-uniform branch)
+template <int L, bool UNI>
+struct RegRowsX {
+    static constexpr int RJ = 12 / L;
+    double (&Q)[RJ][12];
+    RSC_HD void operator()(int k, double c, double s, bool apply) {
+        if (UNI) {
+            if (__builtin_expect(__any(!apply), 0)) {
+                RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                    const double a = Q[j][k], b = Q[j][k + 1];
+                    Q[j][k] = apply ? c * a - s * b : a;
+                    Q[j][k + 1] = apply ? s * a + c * b : b;
+                }
+            } else {
+                RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                    const double a = Q[j][k], b = Q[j][k + 1];
+                    Q[j][k] = c * a - s * b;
+                    Q[j][k + 1] = s * a + c * b;
+                }
+            }
+        } else {
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                const double a = Q[j][k], b = Q[j][k + 1];
+                Q[j][k] = apply ? c * a - s * b : a;
+                Q[j][k + 1] = apply ? s * a + c * b : b;
+            }
+        }
+    }
+};
+
+// sweep form in lane groups of L, HPW hypotheses per workgroup; SINK 0 = LDS rows, 1 = register
+// rows, 2 = register rows + uniform identity branch
+template <int L, int HPW, int SINK, int OPT>
+__global__ __launch_bounds__(64) void qr_group_k(const double* __restrict__ dsub, const double* __restrict__ Qin,
+                                                 double* __restrict__ Qout, double* __restrict__ dout,
+                                                 int* __restrict__ pout, int H) {
+    constexpr int RJ = 12 / L;
+    __shared__ __attribute__((aligned(16))) double T[HPW * 144];
+    const int lane = threadIdx.x, g = lane / L, q = lane % L;
+    if (g >= HPW) return;
+    const int h0 = blockIdx.x * HPW;
+    const int h = min(h0 + g, H - 1);
+    double diag[12], sub[11];
+    RSC_UNROLL for (int i = 0; i < 12; ++i) diag[i] = dsub[(size_t)h * 23 + i];
+    RSC_UNROLL for (int i = 0; i < 11; ++i) sub[i] = dsub[(size_t)h * 23 + 12 + i];
+    int perm[12];
+    double* Th = T + g * 144;
+    if constexpr (SINK == 0 || SINK == 3) {
+        RSC_UNROLL for (int j = 0; j < RJ; ++j)
+            RSC_UNROLL for (int c = 0; c < 12; ++c) Th[(L * j + q) * 12 + c] = Qin[(size_t)h * 144 + (L * j + q) * 12 + c];
+        std::conditional_t<SINK == 0, LdsRowsX<L>, LdsRowsUni<L>> rows{Th, q};
+        tridiag_qr_x<OPT>(diag, sub, rows, perm);
+        if (h0 + g < H)
+            RSC_UNROLL for (int j = 0; j < RJ; ++j)
+                RSC_UNROLL for (int c = 0; c < 12; ++c) Qout[(size_t)h * 144 + (L * j + q) * 12 + c] = Th[(L * j + q) * 12 + c];
+    } else {
+        double Qr[RJ][12];
+        RSC_UNROLL for (int j = 0; j < RJ; ++j)
+            RSC_UNROLL for (int c = 0; c < 12; ++c) Qr[j][c] = Qin[(size_t)h * 144 + (L * j + q) * 12 + c];
+        RegRowsX<L, SINK == 2> rows{Qr};
+        tridiag_qr_x<OPT>(diag, sub, rows, perm);
+        if (h0 + g < H)
+            RSC_UNROLL for (int j = 0; j < RJ; ++j)
+                RSC_UNROLL for (int c = 0; c < 12; ++c) Qout[(size_t)h * 144 + (L * j + q) * 12 + c] = Qr[j][c];
+    }
+    if (h0 + g < H && q == 0) {
+        RSC_UNROLL for (int i = 0; i < 12; ++i) {
+            dout[(size_t)h * 12 + i] = diag[i];
+            pout[(size_t)h * 12 + i] = perm[i];
+        }
+    }
+}
+
+int main(int argc, char** argv) {
+    const int n = 2000, NP = 64, Hp = (argc > 1) ? atoi(argv[1]) : 300;
+    const int H = NP * Hp;
+    const double fx = 435.2046959714599, cx = 367.4517211914062, cy = 252.2008514404297;
+    std::mt19937_64 g(7);
+    std::uniform_real_distribution<double> U(0, 1);
+    std::vector<float> P(3 * n), Q2(2 * n);
+    for (int i = 0; i < n; ++i) {
+        const double u = 752 * U(g), v = 480 * U(g), d = 0.5 + 7.5 * U(g);
+        P[3 * i] = (float)((u - cx) / fx * d); P[3 * i + 1] = (float)((v - cy) / fx * d); P[3 * i + 2] = (float)d;
+        const bool in = U(g) < 0.4;
+        Q2[2 * i] = (float)(in ? u + U(g) - 0.5 : 752 * U(g));
+        Q2[2 * i + 1] = (float)(in ? v + U(g) - 0.5 : 480 * U(g));
+    }
+    std::vector<double> dsub((size_t)H * 23), Qin((size_t)H * 144), Qref((size_t)H * 144), dref((size_t)H * 12);
+    std::vector<int> pref((size_t)H * 12);
+    std::uniform_int_distribution<int> pick(0, n - 1);
+    for (int h = 0; h < H; ++h) {
+        HypStore<4> st;
+        int idx[4];
+        for (int k = 0; k < 4; ++k) {
+            bool dup;
+            do { idx[k] = pick(g); dup = false; for (int j = 0; j < k; ++j) dup |= idx[j] == idx[k]; } while (dup);
+            for (int c = 0; c < 3; ++c) st.pw_[k][c] = P[3 * idx[k] + c];
+            st.u_[k][0] = Q2[2 * idx[k]]; st.u_[k][1] = Q2[2 * idx[k] + 1];
+        }
+        st.rows_ = 4; st.spw = nullptr; st.sal = nullptr;
+        const Intrinsics K{fx, fx, cx, cy};
+        double cws[4][3];
+        control_points_and_alphas(st, cws);
+        double slab[160];
+        LaneMat S{slab, 1};
+        build_MtM(st, K, S);
+        double diag[12], sub[11];
+        sym_eig12_tridiag(S, diag, sub);
+        std::memcpy(&dsub[(size_t)h * 23], diag, 96);
+        std::memcpy(&dsub[(size_t)h * 23 + 12], sub, 88);
+        for (int e = 0; e < 144; ++e) Qin[(size_t)h * 144 + e] = slab[e];
+        double* Qh = &Qref[(size_t)h * 144];
+        std::memcpy(Qh, slab, 144 * 8);
+        auto qapply = [&](int k, double c, double s, bool apply) {
+            for (int i = 0; i < 12; ++i) {
+                const double xi = Qh[i * 12 + k], yi = Qh[i * 12 + k + 1];
+                Qh[i * 12 + k] = apply ? c * xi - s * yi : xi;
+                Qh[i * 12 + k + 1] = apply ? s * xi + c * yi : yi;
+            }
+        };
+        int perm[12];
+        tridiag_qr<double, 12>(diag, sub, qapply, perm);
+        for (int i = 0; i < 12; ++i) { dref[(size_t)h * 12 + i] = diag[i]; pref[(size_t)h * 12 + i] = perm[i]; }
+    }
+    double *d_dsub, *d_Qin, *d_Qout, *d_dout;
+    int* d_pout;
+    CK(hipMalloc(&d_dsub, dsub.size() * 8));
+    CK(hipMalloc(&d_Qin, Qin.size() * 8));
+    CK(hipMalloc(&d_Qout, Qin.size() * 8));
+    CK(hipMalloc(&d_dout, dref.size() * 8));
+    CK(hipMalloc(&d_pout, pref.size() * 4));
+    CK(hipMemcpy(d_dsub, dsub.data(), dsub.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_Qin, Qin.data(), Qin.size() * 8, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<double> Qo(Qin.size()), dox(dref.size());
+    std::vector<int> pox(pref.size());
+    auto check = [&](bool withQ) {
+        CK(hipMemcpy(dox.data(), d_dout, dox.size() * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(pox.data(), d_pout, pox.size() * 4, hipMemcpyDeviceToHost));
+        // the quad form returns the sorted diag, the split form sorts a copy: both sorted here
+        long bad = 0;
+        if (memcmp(pox.data(), pref.data(), pox.size() * 4)) bad++;
+        if (memcmp(dox.data(), dref.data(), dox.size() * 8)) bad++;
+        if (withQ) {
+            CK(hipMemcpy(Qo.data(), d_Qout, Qo.size() * 8, hipMemcpyDeviceToHost));
+            if (memcmp(Qo.data(), Qref.data(), Qo.size() * 8)) bad++;
+        }
+        return bad == 0 ? "bit-exact" : "MISMATCH";
+    };
+    auto timeit = [&](const char* name, int wgs, bool withQ, auto launch) {
+        CK(hipMemset(d_Qout, 0, Qin.size() * 8));
+        launch();
+        CK(hipDeviceSynchronize());
+        const char* ok = check(withQ);
+        const int reps = 20;
+        CK(hipEventRecord(e0));
+        for (int r = 0; r < reps; ++r) launch();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("%-34s WGs %5d  %8.1f us  %s\n", name, wgs, 1e3f * ms / reps, ok);
+        fflush(stdout);
+    };
+    printf("H = %d hypotheses\n", H);
+    const int nq = (H + 15) / 16;
+    timeit("quad sweep (product)", nq, true, [&] { qr_quad_k<true><<<nq, 64>>>(d_dsub, d_Qin, d_Qout, d_dout, d_pout, H); });
+    timeit("quad sweep chase-only", nq, false, [&] { qr_quad_k<false><<<nq, 64>>>(d_dsub, d_Qin, d_Qout, d_dout, d_pout, H); });
+    {  // fast-path arithmetic vs IEEE on random operands
+        const int nt = 1 << 22;
+        std::vector<double> xs(nt), ns(nt), dd(nt);
+        std::mt19937_64 r2(11);
+        std::uniform_real_distribution<double> u01(0, 1);
+        for (int i = 0; i < nt; ++i) {
+            xs[i] = (i & 1) ? 1.0 + u01(r2) : 1.0 + std::ldexp(u01(r2), -(int)(r2() % 60));
+            const int ea = (int)(r2() % 500) - 250, eb = (int)(r2() % 500) - 250;
+            ns[i] = std::ldexp(u01(r2) + 0.5, ea) * ((r2() & 1) ? -1 : 1);
+            dd[i] = std::ldexp(u01(r2) + 0.5, eb) * ((r2() & 1) ? -1 : 1);
+            if ((i & 255) == 7) ns[i] = 0.0;
+        }
+        double *a1, *a2, *a3;
+        unsigned long long* bad;
+        CK(hipMalloc(&a1, nt * 8)); CK(hipMalloc(&a2, nt * 8)); CK(hipMalloc(&a3, nt * 8)); CK(hipMalloc(&bad, 8));
+        CK(hipMemcpy(a1, xs.data(), nt * 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(a2, ns.data(), nt * 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(a3, dd.data(), nt * 8, hipMemcpyHostToDevice));
+        CK(hipMemset(bad, 0, 8));
+        check_fast<<<nt / 256, 256>>>(a1, a2, a3, nt, bad);
+        unsigned long long hb = 0;
+        CK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+        printf("fast sqrt/div vs IEEE on %d operand sets: %s (mask %llu)\n", nt, hb ? "MISMATCH" : "bit-exact", hb);
+    }
+#define GROUP(L, HPW, SINK, OPT)                                                                                \
+    {                                                                                                           \
+        const int nw = (H + HPW - 1) / HPW;                                                                     \
+        timeit("group L=" #L " HPW=" #HPW " sink=" #SINK " opt=" #OPT, nw, true,                                \
+               [&] { qr_group_k<L, HPW, SINK, OPT><<<nw, 64>>>(d_dsub, d_Qin, d_Qout, d_dout, d_pout, H); });   \
+    }
+    GROUP(2, 20, 0, 0)
+    GROUP(2, 20, 3, 0)
+    GROUP(2, 20, 3, 7)
+    GROUP(2, 16, 3, 0)
+    GROUP(2, 10, 3, 0)
+    GROUP(2, 8, 3, 0)
+    GROUP(4, 16, 3, 0)
+    GROUP(4, 10, 3, 0)
+    GROUP(4, 8, 3, 0)
+    GROUP(4, 5, 3, 0)
+    return 0;
+}

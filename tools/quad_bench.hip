@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 #include "../orb-slam2-optimized_amd/csrc/rsc_quad.h"
 
@@ -11,17 +12,18 @@ using namespace rsc;
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-template <int STOP>
-__global__ __launch_bounds__(64) void eig_k(const DevPnP* probs, const LaunchProb* lps, const int2* wgt, const uint32_t* T,
+// L lanes per hypothesis, HPW hypotheses per workgroup
+template <int STOP, int L, int HPW, bool EVQR = false>
+__global__ __launch_bounds__(64) void eig_g(const DevPnP* probs, const LaunchProb* lps, const int2* wgt, const uint32_t* T,
                                             double* stage, int32_t* samples) {
-    __shared__ __attribute__((aligned(16))) double smem[kQuadHyps * kQuadRegion];
-    pnp_eig_quad_body<4, STOP>(probs, lps, wgt, T, stage, samples, smem);
+    __shared__ __attribute__((aligned(16))) double smem[HPW * kQuadRegion];
+    pnp_eig_group_body<4, STOP, L, HPW, EVQR>(probs, lps, wgt, T, stage, samples, smem);
 }
 template <int STOP, bool EVQR = false>
 __global__ __launch_bounds__(64, 2) void eig_k2(const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                                                 const uint32_t* T, double* stage, int32_t* samples) {
-    __shared__ __attribute__((aligned(16))) double smem[kQuadHyps * kQuadRegion];
-    pnp_eig_quad_body<4, STOP, EVQR>(probs, lps, wgt, T, stage, samples, smem);
+    __shared__ __attribute__((aligned(16))) double smem[16 * kQuadRegion];
+    pnp_eig_group_body<4, STOP, 4, 16, EVQR>(probs, lps, wgt, T, stage, samples, smem);
 }
 __global__ __launch_bounds__(64) void eig_lane_k(const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                                                   const uint32_t* T, double* stage, int32_t* samples) {
@@ -185,7 +187,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dpo, (size_t)total * 12 * 4));
     std::vector<DevPnP> probs(NP);
     std::vector<LaunchProb> lps(NP);
-    std::vector<int2> w16, w64;
+    std::vector<int2> w16, w64, w32, w20;
     for (int i = 0; i < NP; ++i) {
         DevPnP& d = probs[i];
         d.pts = dp + (size_t)i * N; d.uv = du + (size_t)i * N; d.n = N;
@@ -195,9 +197,15 @@ int main(int argc, char** argv) {
         l.prob = i; l.H = Hp; l.out0 = i * Hp; l.g0 = 0; l.pad = 0;
         for (int j = 0; j < 31; ++j) l.window[j] = (uint32_t)(rnd() * 4294967296.0);
         for (int h0 = 0; h0 < Hp; h0 += 16) w16.push_back(make_int2(i, h0));
+        for (int h0 = 0; h0 < Hp; h0 += 32) w32.push_back(make_int2(i, h0));
+        for (int h0 = 0; h0 < Hp; h0 += 20) w20.push_back(make_int2(i, h0));
         for (int h0 = 0; h0 < Hp; h0 += 64) w64.push_back(make_int2(i, h0));
     }
-    DevPnP* dprobs; LaunchProb* dlps; int2 *dw16, *dw64;
+    DevPnP* dprobs; LaunchProb* dlps; int2 *dw16, *dw64, *dw32, *dw20;
+    CK(hipMalloc(&dw32, w32.size() * sizeof(int2)));
+    CK(hipMalloc(&dw20, w20.size() * sizeof(int2)));
+    CK(hipMemcpy(dw32, w32.data(), w32.size() * sizeof(int2), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw20, w20.data(), w20.size() * sizeof(int2), hipMemcpyHostToDevice));
     CK(hipMalloc(&dprobs, NP * sizeof(DevPnP)));
     CK(hipMalloc(&dlps, NP * sizeof(LaunchProb)));
     CK(hipMalloc(&dw16, w16.size() * sizeof(int2)));
@@ -223,15 +231,41 @@ int main(int argc, char** argv) {
     };
     const int n16 = (int)w16.size(), n64 = (int)w64.size();
     printf("hyps=%d eig WGs=%d betas WGs=%d\n", total, n16, n64);
-    printf("eig A (sample..MtM)   %8.1f us\n", timeit([&] { eig_k<1><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
-    printf("eig A+tridiag         %8.1f us\n", timeit([&] { eig_k<2><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
-    printf("eig A+tri+accum       %8.1f us\n", timeit([&] { eig_k<3><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
-    printf("eig full (+QR)        %8.1f us\n", timeit([&] { eig_k<99><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
+    const int n32 = (int)w32.size(), n20 = (int)w20.size();
+    // reference stage records: the quad sweep form (the round-1/2 product kernel)
+    const size_t nst = (size_t)total * kStageDoubles;
+    std::vector<double> ref(nst), got(nst);
+    std::vector<int32_t> refs((size_t)total * 8), gots((size_t)total * 8);
+    auto snap = [&](std::vector<double>& d, std::vector<int32_t>& sm) {
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(d.data(), dst, nst * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(sm.data(), dsm, sm.size() * 4, hipMemcpyDeviceToHost));
+    };
+    CK(hipMemset(dst, 0, nst * 8));
+    eig_k2<99><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm);
+    snap(ref, refs);
+    auto cmp = [&](const char* name, auto launch) {
+        CK(hipMemset(dst, 0, nst * 8));
+        CK(hipMemset(dsm, 0, gots.size() * 4));
+        launch();
+        snap(got, gots);
+        const bool ok = !memcmp(got.data(), ref.data(), nst * 8) && !memcmp(gots.data(), refs.data(), gots.size() * 4);
+        printf("%-22s %8.1f us  %s\n", name, timeit(launch), ok ? "bit-exact" : "MISMATCH");
+        fflush(stdout);
+    };
     printf("eig2 A (sample..MtM)  %8.1f us\n", timeit([&] { eig_k2<1><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
     printf("eig2 A+tridiag        %8.1f us\n", timeit([&] { eig_k2<2><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
     printf("eig2 A+tri+accum      %8.1f us\n", timeit([&] { eig_k2<3><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
-    printf("eig2 full event-QR    %8.1f us\n", timeit([&] { eig_k2<99, true><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
-    printf("eig2 full sweep-QR    %8.1f us\n", timeit([&] { eig_k2<99, false><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
+    cmp("eig2 quad sweep-QR", [&] { eig_k2<99, false><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); });
+    cmp("eig2 quad event-QR", [&] { eig_k2<99, true><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); });
+    printf("pair32 A              %8.1f us\n", timeit([&] { eig_g<1, 2, 32><<<n32, 64>>>(dprobs, dlps, dw32, dT, dst, dsm); }));
+    printf("pair32 A+tridiag      %8.1f us\n", timeit([&] { eig_g<2, 2, 32><<<n32, 64>>>(dprobs, dlps, dw32, dT, dst, dsm); }));
+    printf("pair32 A+tri+accum    %8.1f us\n", timeit([&] { eig_g<3, 2, 32><<<n32, 64>>>(dprobs, dlps, dw32, dT, dst, dsm); }));
+    cmp("pair32 full", [&] { eig_g<99, 2, 32><<<n32, 64>>>(dprobs, dlps, dw32, dT, dst, dsm); });
+    cmp("pair20 full", [&] { eig_g<99, 2, 20><<<n20, 64>>>(dprobs, dlps, dw20, dT, dst, dsm); });
+    cmp("quad16 (lb64) full", [&] { eig_g<99, 4, 16><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); });
+    printf("WGs: quad16 %d pair32 %d pair20 %d\n", n16, n32, n20);
+    if (argc > 3) return 0;  // eig only
     printf("eig lane              %8.1f us\n", timeit([&] { eig_lane_k<<<n64, 64>>>(dprobs, dlps, dw64, dT, dst, dsm); }));
     std::vector<int4> hsv(total);
     for (int i = 0; i < total; ++i) {
