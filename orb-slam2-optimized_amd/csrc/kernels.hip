@@ -137,7 +137,14 @@ __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict_
                                                        const float* __restrict__ poses,
                                                        int32_t* __restrict__ counts,
                                                        uint64_t* __restrict__ masks, int mask_words) {
-    __shared__ int wave_cnt[4][64];
+    // Hypotheses per flush: the 4 waves' mask words of a batch wait in LDS (16 KB) until the batch's
+    // counts are summed; only hypotheses reaching mRansacMinInliers — the only ones whose inlier
+    // mask the host ever adopts (PnPsolver.cpp:176-195) — are stored.  In exhaustive
+    // relocalization batches almost none qualify, so the 4.8 MB of mask writes per config-2
+    // launch become a few KB.
+    constexpr int B = PPT <= 8 ? 64 : 512 / PPT;
+    __shared__ int wave_cnt[4][B];
+    __shared__ uint64_t mbuf[B][4][PPT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int4 wt = wg_table[blockIdx.x];
     const LaunchProb& lp = lps[wt.x];
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict_
         }
     }
     // The PPT points of a lane are independent: all ballots are taken first and the mask words
-    // are stored by lanes 0..PPT-1 in one predicated store, so the compiler can interleave the
+    // are kept by lanes 0..PPT-1 in one predicated store, so the compiler can interleave the
     // points' arithmetic (a lane-0 branch per point would serialise them).  The next pose is
     // loaded before the current one is used.
     const float* pp = poses + (size_t)(lp.out0 + wt.y) * 12;
@@ -163,7 +170,6 @@ __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict_
     RSC_UNROLL for (int k = 0; k < 9; ++k) Rn[k] = pp[k];
     RSC_UNROLL for (int k = 0; k < 3; ++k) tn[k] = pp[9 + k];
     for (int j = 0; j < wt.z; ++j) {
-        const int h = wt.y + j;
         float R[9], t[3];
         RSC_UNROLL for (int k = 0; k < 9; ++k) R[k] = Rn[k];
         RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = tn[k];
@@ -181,14 +187,24 @@ __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict_
             cnt += __popcll(b[s]);
             mine = (lane == s) ? b[s] : mine;
         }
-        if (masks && lane < PPT) masks[(size_t)(lp.out0 + h) * mask_words + lane * 4 + wave] = mine;
-        if (lane == 0) wave_cnt[wave][j & 63] = cnt;
-        if ((j & 63) == 63 || j == wt.z - 1) {
+        const int jb = j % B;
+        if (lane < PPT) mbuf[jb][wave][lane] = mine;
+        if (lane == 0) wave_cnt[wave][jb] = cnt;
+        if (jb == B - 1 || j == wt.z - 1) {
             __syncthreads();
-            const int base = j & ~63;
-            if (tid <= (j & 63)) {
+            const int base = j - jb;
+            if (tid <= jb) {
                 const int c = wave_cnt[0][tid] + wave_cnt[1][tid] + wave_cnt[2][tid] + wave_cnt[3][tid];
                 counts[lp.out0 + wt.y + base + tid] = c;
+                wave_cnt[0][tid] = c;  // the batch's totals, for the mask stores below
+            }
+            __syncthreads();
+            if (masks) {
+                for (int w = tid; w < (jb + 1) * 4 * PPT; w += 256) {
+                    const int hb = w / (4 * PPT), r = w - hb * (4 * PPT), s = r >> 2, wv = r & 3;
+                    if (wave_cnt[0][hb] >= lp.min_inliers)
+                        masks[(size_t)(lp.out0 + wt.y + base + hb) * mask_words + r] = mbuf[hb][wv][s];
+                }
             }
             __syncthreads();
         }

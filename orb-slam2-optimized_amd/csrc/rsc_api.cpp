@@ -300,7 +300,7 @@ struct HipPnPBackend : PnPBackend {
             lp.out0 = total;
             lp.g0 = S[i]->rng.g;
             std::memcpy(lp.window, S[i]->rng.window, sizeof(lp.window));
-            lp.pad = 0;
+            lp.min_inliers = S[i]->mRansacMinInliers;  // only such hypotheses' masks are ever read
             p->spec_out0 = total;
             p->spec_H = H[i];
             total += H[i];
@@ -517,7 +517,7 @@ struct HipSim3Backend : Sim3Backend {
             std::memcpy(d.K1, p->K1, sizeof(d.K1));
             std::memcpy(d.K2, p->K2, sizeof(d.K2));
             LaunchProb& lp = lps[i];
-            lp.prob = i; lp.H = H[i]; lp.out0 = total; lp.g0 = S[i]->rng.g; lp.pad = 0;
+            lp.prob = i; lp.H = H[i]; lp.out0 = total; lp.g0 = S[i]->rng.g; lp.min_inliers = 0;
             std::memcpy(lp.window, S[i]->rng.window, sizeof(lp.window));
             p->spec_out0 = total;
             p->spec_H = H[i];
@@ -646,7 +646,7 @@ struct HipMLBackend : MLBackend {
             lp.out0 = total;
             lp.g0 = S[i]->rng.g;
             std::memcpy(lp.window, S[i]->rng.window, sizeof(lp.window));
-            lp.pad = 0;
+            lp.min_inliers = S[i]->mRansacMinInliers;  // only such hypotheses' masks are ever read
             p->spec_out0 = total;
             p->spec_H = H[i];
             total += H[i];

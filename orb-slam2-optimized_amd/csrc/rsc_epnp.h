@@ -33,8 +33,21 @@ struct HypStore {
     RSC_HD double u(int i, int c) const { return u_[i][c]; }
     RSC_HD double al(int i, int j) const { return al_[i][j]; }
     RSC_HD void set_al(int i, int j, double v) { al_[i][j] = v; }
+#if defined(__HIP_DEVICE_COMPILE__)
+    // The stale tail is the same for every lane of a workgroup (all its hypotheses belong to one
+    // problem) and read-only within the kernel: read through the constant address space it is
+    // fetched with scalar loads, one broadcast per row, instead of a vector load round trip per
+    // row inside the dependent chain (hundreds of rows after a Refine).
+    RSC_HD double stale_pw(int i, int c) const {
+        return ((const __attribute__((address_space(4))) double*)spw)[3 * i + c];
+    }
+    RSC_HD double stale_al(int i, int j) const {
+        return ((const __attribute__((address_space(4))) double*)sal)[4 * i + j];
+    }
+#else
     RSC_HD double stale_pw(int i, int c) const { return spw[3 * i + c]; }
     RSC_HD double stale_al(int i, int j) const { return sal[4 * i + j]; }
+#endif
 };
 
 struct RowStore {
@@ -52,13 +65,22 @@ struct RowStore {
     RSC_HD double stale_al(int i, int j) const { return als[4 * i + j]; }
 };
 
-// Column sum of pws over ALL allocated rows (current rows first, then stale rows).
+// Column sums of pws over ALL allocated rows (current rows first, then stale rows), each column's
+// additions in row order; the three columns share one pass over the stale tail (Q6: after a
+// Refine the tail holds hundreds of rows, read from global memory).
 template <class St>
-RSC_HD double sum_pw_col(const St& st, int c) {
-    double s = st.pw(0, c);
-    RSC_UNROLL for (int i = 1; i < st.n(); ++i) s = s + st.pw(i, c);
-    for (int i = st.n(); i < st.rows(); ++i) s = s + st.stale_pw(i, c);
-    return s;
+RSC_HD void sum_pw_cols(const St& st, double (&s)[3]) {
+    RSC_UNROLL for (int c = 0; c < 3; ++c) {
+        s[c] = st.pw(0, c);
+        RSC_UNROLL for (int i = 1; i < st.n(); ++i) s[c] = s[c] + st.pw(i, c);
+    }
+#pragma unroll 4
+    for (int i = st.n(); i < st.rows(); ++i) {
+        const double a = st.stale_pw(i, 0), b = st.stale_pw(i, 1), d = st.stale_pw(i, 2);
+        s[0] = s[0] + a;
+        s[1] = s[1] + b;
+        s[2] = s[2] + d;
+    }
 }
 
 // choose_control_points + compute_barycentric_coordinates (PnPsolver.cpp:296-343).
@@ -66,7 +88,7 @@ RSC_HD double sum_pw_col(const St& st, int c) {
 template <class St>
 RSC_HD void control_points_and_alphas(St& st, double (&cws)[4][3]) {
     const int n = st.n();
-    RSC_UNROLL for (int c = 0; c < 3; ++c) cws[0][c] = sum_pw_col(st, c);
+    sum_pw_cols(st, cws[0]);
     RSC_UNROLL for (int c = 0; c < 3; ++c) cws[0][c] = cws[0][c] / n;
     double A[3][3];
     RSC_UNROLL for (int a = 0; a < 3; ++a)
@@ -225,7 +247,12 @@ RSC_HD bool qr_solve_6x4(double (&A)[6][4], double (&b)[6], double (&X)[4]) {
 template <class SV>
 RSC_HD void gauss_newton(const SV& S, double (&betas)[4]) {
     double X[4] = {0.0, 0.0, 0.0, 0.0};
-    RSC_UNROLL for (int it = 0; it < 5; it++) {
+    // Rolled, with a compiler-only memory fence per iteration: unrolled (or with the L reads
+    // hoisted out of the loop) the 60 L entries stay live in VGPRs across all five solves and the
+    // betas kernel spills to scratch; re-read from the view (LDS) they cost 60 loads per iteration.
+#pragma unroll 1
+    for (int it = 0; it < 5; it++) {
+        asm volatile("" ::: "memory");
         double A[6][4], B[6];
         RSC_UNROLL for (int i = 0; i < 6; i++) {
             double l[10];
@@ -373,17 +400,20 @@ RSC_HD double compute_R_and_t(const St& st, const Intrinsics& K, const SV& S, co
     auto pcs = [&](int i, int c) {
         return st.al(i, 0) * ccs[0][c] + st.al(i, 1) * ccs[1][c] + st.al(i, 2) * ccs[2][c] + st.al(i, 3) * ccs[3][c];
     };
-    auto pcs_stale = [&](int i, int c) {
-        return st.stale_al(i, 0) * ccs[0][c] + st.stale_al(i, 1) * ccs[1][c] + st.stale_al(i, 2) * ccs[2][c] +
-               st.stale_al(i, 3) * ccs[3][c];
-    };
     double pc0[3];
     RSC_UNROLL for (int c = 0; c < 3; ++c) {
         double s = pcs(0, c);
         RSC_UNROLL for (int i = 1; i < n; ++i) s = s + pcs(i, c);
-        for (int i = n; i < st.rows(); ++i) s = s + pcs_stale(i, c);
-        pc0[c] = s / n;
+        pc0[c] = s;
     }
+    // stale rows (Q6): one pass, the row's alphas loaded once for the three columns
+#pragma unroll 4
+    for (int i = n; i < st.rows(); ++i) {
+        const double a0 = st.stale_al(i, 0), a1 = st.stale_al(i, 1), a2 = st.stale_al(i, 2), a3 = st.stale_al(i, 3);
+        RSC_UNROLL for (int c = 0; c < 3; ++c)
+            pc0[c] = pc0[c] + (a0 * ccs[0][c] + a1 * ccs[1][c] + a2 * ccs[2][c] + a3 * ccs[3][c]);
+    }
+    RSC_UNROLL for (int c = 0; c < 3; ++c) pc0[c] = pc0[c] / n;
     double M[3][3];
     RSC_UNROLL for (int r = 0; r < 3; ++r)
         RSC_UNROLL for (int c = 0; c < 3; ++c) M[r][c] = 0.0;

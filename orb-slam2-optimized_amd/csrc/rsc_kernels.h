@@ -45,7 +45,7 @@ struct LaunchProb {
     int out0;  // first record index of this problem in the launch's pose/count/mask arrays
     int g0;
     uint32_t window[31];
-    int pad;
+    int min_inliers;  // PnP scan: masks are stored only for counts >= this (mRansacMinInliers)
 };
 
 struct RefineJob {

@@ -509,13 +509,13 @@ __device__ __forceinline__ void pnp_betas_body(const DevPnP* __restrict__ probs,
     double* ERR = LR + 66 * 64;
     float* PZ = reinterpret_cast<float*>(ERR + 3 * 64);
     RSC_UNROLL for (int e = 0; e < 16; ++e) EV[(16 * wave + e) * 64 + lane] = in[kStEv + 16 * wave + e];
-    double cws[4][3];
-    RSC_UNROLL for (int i = 0; i < 4; ++i)
-        RSC_UNROLL for (int c = 0; c < 3; ++c) cws[i][c] = in[kStCws + i * 3 + c];
     __syncthreads();
     const SplitView V{EV + lane, LR + lane, 64};
     if (wave == 0) {
         compute_L_6x10(V);
+        double cws[4][3];
+        RSC_UNROLL for (int i = 0; i < 4; ++i)
+            RSC_UNROLL for (int c = 0; c < 3; ++c) cws[i][c] = in[kStCws + i * 3 + c];
         auto d2 = [&](int a, int b) {
             double x = cws[a][0] - cws[b][0], y = cws[a][1] - cws[b][1], z = cws[a][2] - cws[b][2];
             return x * x + y * y + z * z;
@@ -524,6 +524,13 @@ __device__ __forceinline__ void pnp_betas_body(const DevPnP* __restrict__ probs,
         V.rho(3) = d2(1, 2); V.rho(4) = d2(1, 3); V.rho(5) = d2(2, 3);
     }
     __syncthreads();
+    double betas[4] = {0.0, 0.0, 0.0, 0.0};
+    if (apx == 0) find_betas<1>(V, betas);
+    else if (apx == 1) find_betas<2>(V, betas);
+    else find_betas<3>(V, betas);
+    gauss_newton(V, betas);
+    // the hypothesis' points and alphas are read only now: live across the solves above they
+    // pushed the wave past 256 VGPRs (scratch spills, round 1)
     HypStore<NS> st;
     RSC_UNROLL for (int i = 0; i < NS; ++i) {
         const int id = samples[rec * 8 + i];
@@ -537,12 +544,7 @@ __device__ __forceinline__ void pnp_betas_body(const DevPnP* __restrict__ probs,
     st.spw = P.pws;
     st.sal = P.als;
     const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
-    double betas[4] = {0.0, 0.0, 0.0, 0.0};
-    if (apx == 0) find_betas<1>(V, betas);
-    else if (apx == 1) find_betas<2>(V, betas);
-    else find_betas<3>(V, betas);
-    gauss_newton(V, betas);
-    const double pw0[3] = {cws[0][0], cws[0][1], cws[0][2]};
+    const double pw0[3] = {in[kStCws + 0], in[kStCws + 1], in[kStCws + 2]};
     double R[3][3], t[3];
     ERR[wave * 64 + lane] = compute_R_and_t(st, K, V, betas, pw0, R, t);
     RSC_UNROLL for (int r = 0; r < 3; ++r)

@@ -13,7 +13,9 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "librsc.so")
+# RSC_LIBRSC: another build of the same library (A/B kernel comparisons in tools/); the default is
+# the in-tree build.
+LIB_PATH = os.environ.get("RSC_LIBRSC") or os.path.join(PKG_DIR, "lib", "librsc.so")
 
 RSC_OK = 0
 

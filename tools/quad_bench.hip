@@ -138,6 +138,12 @@ __global__ __launch_bounds__(64) void pb4(const float4* __restrict__ pts, const 
     out[(size_t)h * kStageDoubles] = acc;
 }
 template <int FORCE = -1>
+__global__ __launch_bounds__(192) void betas_k1(const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
+                                               const double* stage, const int32_t* samples, float* poses) {
+    __shared__ __attribute__((aligned(16))) double smem[kBetasSmemDoubles];
+    pnp_betas_body<4, FORCE>(probs, lps, wgt, stage, samples, poses, smem);
+}
+template <int FORCE = -1>
 __global__ __launch_bounds__(192, 2) void betas_k(const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                                                const double* stage, const int32_t* samples, float* poses) {
     __shared__ __attribute__((aligned(16))) double smem[kBetasSmemDoubles];
@@ -194,7 +200,7 @@ int main(int argc, char** argv) {
         d.fx = 435.20468f; d.fy = 435.20468f; d.cx = 367.45172f; d.cy = 252.20085f;
         d.th2 = 5.991f; d.rows = 4; d.pws = nullptr; d.us = nullptr; d.als = nullptr;
         LaunchProb& l = lps[i];
-        l.prob = i; l.H = Hp; l.out0 = i * Hp; l.g0 = 0; l.pad = 0;
+        l.prob = i; l.H = Hp; l.out0 = i * Hp; l.g0 = 0; l.min_inliers = 0;
         for (int j = 0; j < 31; ++j) l.window[j] = (uint32_t)(rnd() * 4294967296.0);
         for (int h0 = 0; h0 < Hp; h0 += 16) w16.push_back(make_int2(i, h0));
         for (int h0 = 0; h0 < Hp; h0 += 32) w32.push_back(make_int2(i, h0));
@@ -265,6 +271,43 @@ int main(int argc, char** argv) {
     cmp("pair20 full", [&] { eig_g<99, 2, 20><<<n20, 64>>>(dprobs, dlps, dw20, dT, dst, dsm); });
     cmp("quad16 (lb64) full", [&] { eig_g<99, 4, 16><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); });
     printf("WGs: quad16 %d pair32 %d pair20 %d\n", n16, n32, n20);
+    {  // eig -> betas back to back (as the product stream): betas time after each eig form
+        hipEvent_t t0, t1, t2;
+        CK(hipEventCreate(&t0)); CK(hipEventCreate(&t1)); CK(hipEventCreate(&t2));
+        for (int form = 0; form < 2; ++form) {
+            float se = 0, sb = 0;
+            for (int r = 0; r < 21; ++r) {
+                CK(hipEventRecord(t0));
+                if (form == 0) eig_k2<99><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm);
+                else eig_g<99, 2, 20><<<n20, 64>>>(dprobs, dlps, dw20, dT, dst, dsm);
+                CK(hipEventRecord(t1));
+                betas_k<<<n64, 192>>>(dprobs, dlps, dw64, dst, dsm, dpo);
+                CK(hipEventRecord(t2));
+                CK(hipEventSynchronize(t2));
+                float a, b2;
+                CK(hipEventElapsedTime(&a, t0, t1));
+                CK(hipEventElapsedTime(&b2, t1, t2));
+                if (r) { se += a; sb += b2; }
+            }
+            printf("%s eig %8.1f us -> betas %8.1f us\n", form ? "pair20" : "quad16", se * 50, sb * 50);
+        }
+        // fresh sample streams per step (as bench.py's reset(seeds) per step)
+        for (int st = 0; st < 6; ++st) {
+            for (auto& l : lps)
+                for (int j = 0; j < 31; ++j) l.window[j] = (uint32_t)(rnd() * 4294967296.0);
+            CK(hipMemcpy(dlps, lps.data(), NP * sizeof(LaunchProb), hipMemcpyHostToDevice));
+            CK(hipEventRecord(t0));
+            eig_g<99, 2, 20><<<n20, 64>>>(dprobs, dlps, dw20, dT, dst, dsm);
+            CK(hipEventRecord(t1));
+            betas_k<<<n64, 192>>>(dprobs, dlps, dw64, dst, dsm, dpo);
+            CK(hipEventRecord(t2));
+            CK(hipEventSynchronize(t2));
+            float a, b2;
+            CK(hipEventElapsedTime(&a, t0, t1));
+            CK(hipEventElapsedTime(&b2, t1, t2));
+            printf("step %d: pair20 eig %8.1f us -> betas %8.1f us\n", st, a * 1e3f, b2 * 1e3f);
+        }
+    }
     if (argc > 3) return 0;  // eig only
     printf("eig lane              %8.1f us\n", timeit([&] { eig_lane_k<<<n64, 64>>>(dprobs, dlps, dw64, dT, dst, dsm); }));
     std::vector<int4> hsv(total);
@@ -296,6 +339,7 @@ int main(int argc, char** argv) {
         printf("pb4 variant %d         %8.1f us\n", v, us);
     }
     printf("betas                 %8.1f us\n", timeit([&] { betas_k<<<n64, 192>>>(dprobs, dlps, dw64, dst, dsm, dpo); }));
+    printf("betas lb(192)         %8.1f us\n", timeit([&] { betas_k1<<<n64, 192>>>(dprobs, dlps, dw64, dst, dsm, dpo); }));
     printf("betas all approx1     %8.1f us\n", timeit([&] { betas_k<0><<<n64, 192>>>(dprobs, dlps, dw64, dst, dsm, dpo); }));
     printf("betas all approx2     %8.1f us\n", timeit([&] { betas_k<1><<<n64, 192>>>(dprobs, dlps, dw64, dst, dsm, dpo); }));
     printf("betas all approx3     %8.1f us\n", timeit([&] { betas_k<2><<<n64, 192>>>(dprobs, dlps, dw64, dst, dsm, dpo); }));
