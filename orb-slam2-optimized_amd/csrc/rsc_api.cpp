@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <string>
@@ -83,6 +84,45 @@ struct PinBuf {
         if (p) (void)hipHostFree(p);
     }
 };
+
+// XCD-aware order of a workgroup table.  The dispatcher deals blocks round-robin over the 8 XCDs
+// (blocks b and b + 8 share one L2; MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"), and
+// every workgroup of a problem reads that problem's correspondences (scan: all of them; solve
+// stages: random samples of them).  Dealt in problem order, each problem's workgroups spread over
+// all 8 XCDs and every L2 fetches the problem's points from HBM again (8x the input bytes, measured
+// with FETCH_SIZE); here the problems are binned onto the 8 residues of b (greedy by workgroup
+// count) so a problem's workgroups share one L2.  Placement only: results do not depend on it.
+template <class T, class Prob>
+void xcd_order(std::vector<T>& wgs, Prob prob_of) {
+    constexpr int X = 8;
+    if (wgs.size() <= (size_t)X) return;
+    std::vector<std::vector<T>> byp;
+    std::vector<int> pid;  // problem id -> index in byp
+    for (const T& w : wgs) {
+        const int p = prob_of(w);
+        if (p >= (int)pid.size()) pid.resize(p + 1, -1);
+        if (pid[p] < 0) { pid[p] = (int)byp.size(); byp.emplace_back(); }
+        byp[pid[p]].push_back(w);
+    }
+    std::vector<int> order(byp.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return byp[a].size() > byp[b].size(); });
+    std::vector<std::vector<T>> bin(X);
+    for (int i : order) {
+        int best = 0;
+        for (int x = 1; x < X; ++x) if (bin[x].size() < bin[best].size()) best = x;
+        bin[best].insert(bin[best].end(), byp[i].begin(), byp[i].end());
+    }
+    std::vector<size_t> next(X, 0);
+    for (size_t b = 0; b < wgs.size(); ++b) {
+        int x = (int)(b % X);
+        if (next[x] == bin[x].size()) {  // this residue's bin is drained: take from the fullest
+            for (int y = 0; y < X; ++y)
+                if (bin[y].size() - next[y] > bin[x].size() - next[x]) x = y;
+        }
+        wgs[b] = bin[x][next[x]++];
+    }
+}
 
 // Hypotheses per scan workgroup: enough workgroups for ~8 waves per SIMD (256 CUs x 4 SIMDs,
 // 4 waves per workgroup) without going below 8 hypotheses per point load.
@@ -326,6 +366,11 @@ struct HipPnPBackend : PnPBackend {
                 for (int h0 = 0; h0 < H[i]; h0 += kEigHyps) quad_wgs[g].push_back(make_int2(i, h0));
             for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
         }
+        for (int g = 0; g < 3; ++g) {
+            xcd_order(solve_wgs[g], [](const int2& w) { return w.x; });
+            xcd_order(quad_wgs[g], [](const int2& w) { return w.x; });
+        }
+        xcd_order(scan_wgs, [](const int4& w) { return w.x; });
         Blob b;
         const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevPnP));
         const size_t o_lps = b.add(lps.data(), lps.size() * sizeof(LaunchProb));
@@ -538,6 +583,8 @@ struct HipSim3Backend : Sim3Backend {
             for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs.push_back(make_int2(i, h0));
             for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
         }
+        xcd_order(solve_wgs, [](const int2& w) { return w.x; });
+        xcd_order(scan_wgs, [](const int4& w) { return w.x; });
         Blob b;
         const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevSim3));
         const size_t o_lps = b.add(lps.data(), lps.size() * sizeof(LaunchProb));
@@ -667,6 +714,8 @@ struct HipMLBackend : MLBackend {
             for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs[g].push_back(make_int2(i, h0));
             for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
         }
+        for (auto& t : solve_wgs) xcd_order(t, [](const int2& w) { return w.x; });
+        xcd_order(scan_wgs, [](const int4& w) { return w.x; });
         Blob b;
         const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevML));
         const size_t o_lps = b.add(lps.data(), lps.size() * sizeof(LaunchProb));
