@@ -48,12 +48,16 @@ int rsc_context_synchronize(rsc_context* ctx);
  * out[0] = hypothesis-solve kernels, out[1] = inlier-scan kernels, out[2] = refine kernels,
  * out[3] = number of solve launches, out[4] = hypotheses solved. */
 int rsc_context_last_timing(rsc_context* ctx, double out[5]);
-/* As above plus out[5] = eigen-stage kernel (pnp_eig_quad/lane_kernel) alone, split solve modes. */
+/* As above plus out[5] = eigen-stage kernel (pnp_eig_group/lane_kernel) alone, split solve modes. */
 int rsc_context_last_kernel_timing(rsc_context* ctx, double out[6]);
 /* Diagnostic: host clock of the last rsc_pnp_iterate_many in microseconds from entry to
  * [0] first launch, [1] kernels enqueued, [2] results back on the host, [3] return. */
 int rsc_diag_host_timing(rsc_context* ctx, double out[4]);
 int rsc_context_enable_timing(rsc_context* ctx, int enable);
+/* Self-test of the device libm restatement (rsc_math.h, used by Sim3 angles, MLPnP, SearchBySim3):
+ * out[i] = f(x[i]) computed ON THE GPU, f = 0 sin, 1 cos, 2 acos, 3 cbrt, 4 log, 5 logf
+ * ((float)x[i] in, float result widened).  Host pointers, n >= 0.  Tests compare it with glibc. */
+int rsc_selftest_math(rsc_context* ctx, int fn, const double* x, int n, double* out);
 /* Hypothesis-solve kernel family for PnP (all produce bit-identical results):
  * 0 = auto, 1 = single kernel (one lane per hypothesis), 2 = quad-cooperative eigenvectors +
  * one wave per beta approximation, 3 = lane-per-hypothesis eigenvectors + per-approximation waves.

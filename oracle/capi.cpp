@@ -536,6 +536,9 @@ void ora_loop_events_batch(int n_events, const int32_t* ev_begin, const int32_t*
 }
 
 // deterministic libm (csrc/rsc_math.h) for the accuracy tests
+void ora_mlpnp_jac(const double* X, const double* nr, const double* ns, const double* x, double* J) {
+    rsc_oracle::mlpnp_jacobian_public(X, nr, ns, x, J);
+}
 double ora_dm_sin(double x) { return rsc::dm::sin(x); }
 double ora_dm_cos(double x) { return rsc::dm::cos(x); }
 double ora_dm_acos(double x) { return rsc::dm::acos(x); }

@@ -755,4 +755,14 @@ bool MLPnPOracle::iterate(int nIterations, bool& bNoMore, std::vector<uint8_t>& 
     return false;
 }
 
+// Test hook: the residual Jacobian above for one correspondence (tests/test_cpu_pins.py compares it
+// with central differences of the reference's residual).
+void mlpnp_jacobian_public(const double X[3], const double nr[3], const double ns[3], const double x[6],
+                           double J[12]) {
+    double Jm[2][6];
+    mlpnp_jac(X, nr, ns, x, x + 3, Jm);
+    for (int r = 0; r < 2; ++r)
+        for (int k = 0; k < 6; ++k) J[6 * r + k] = Jm[r][k];
+}
+
 }  // namespace rsc_oracle

@@ -82,4 +82,8 @@ private:
     GlibcRand rng;
 };
 
+// Residual Jacobian d(r_r, r_s)/d(w, t) of one correspondence at x = (w, t) (test hook).
+void mlpnp_jacobian_public(const double X[3], const double nr[3], const double ns[3], const double x[6],
+                           double J[12]);
+
 }  // namespace rsc_oracle

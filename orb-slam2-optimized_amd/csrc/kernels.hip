@@ -17,6 +17,7 @@
 #include "rsc_epnp.h"
 #include "rsc_sim3.h"
 #include "rsc_quad.h"
+#include "rsc_math.h"
 #include "rsc_mlpnp.h"
 #include "rsc_kernels.h"
 
@@ -787,6 +788,30 @@ hipError_t launch_pnp_solve_split(bool quad, int ns, int nwgE, const int2* wgtE,
 #undef RSC_CASE
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// Device libm restatement self-test (rsc_selftest_math): the functions as the kernels compile them.
+__global__ __launch_bounds__(256) void selftest_math_kernel(int fn, const double* __restrict__ x, int n,
+                                                            double* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double v = x[i];
+    double r;
+    switch (fn) {
+        case 0: r = dm::sin(v); break;
+        case 1: r = dm::cos(v); break;
+        case 2: r = dm::acos(v); break;
+        case 3: r = dm::cbrt(v); break;
+        case 4: r = dm::log(v); break;
+        default: r = (double)dm::logf((float)v); break;
+    }
+    out[i] = r;
+}
+
+hipError_t launch_selftest_math(int fn, const double* x, int n, double* out, hipStream_t st) {
+    if (fn < 0 || fn > 5 || n <= 0) return hipErrorInvalidValue;
+    selftest_math_kernel<<<(n + 255) / 256, 256, 0, st>>>(fn, x, n, out);
     return hipGetLastError();
 }
 

@@ -902,6 +902,20 @@ int rsc_context_enable_timing(rsc_context* C, int enable) {
     return RSC_OK;
 }
 
+int rsc_selftest_math(rsc_context* C, int fn, const double* x, int n, double* out) {
+    if (!C || fn < 0 || fn > 5 || n < 0 || (n > 0 && (!x || !out))) return RSC_ERR_ARG;
+    if (n == 0) return RSC_OK;
+    RSC_HIP(hipSetDevice(C->device));
+    double* d = nullptr;
+    RSC_HIP(hipMalloc(&d, (size_t)n * 16));
+    std::unique_ptr<double, void (*)(double*)> hold(d, [](double* p) { (void)hipFree(p); });
+    RSC_HIP(hipMemcpyAsync(d, x, (size_t)n * 8, hipMemcpyHostToDevice, C->stream));
+    RSC_HIP(launch_selftest_math(fn, d, n, d + n, C->stream));
+    RSC_HIP(hipMemcpyAsync(out, d + n, (size_t)n * 8, hipMemcpyDeviceToHost, C->stream));
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    return RSC_OK;
+}
+
 int rsc_context_last_timing(rsc_context* C, double out[5]) {
     if (!C || !out) return RSC_ERR_ARG;
     for (int i = 0; i < 5; ++i) out[i] = C->last_ms[i];

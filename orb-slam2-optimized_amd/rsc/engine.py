@@ -29,7 +29,7 @@ u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
 # Every symbol declared in include/rsc.h (checked by tests/test_cpu_abi.py).
 EXPORTED = [
     "rsc_version", "rsc_status_string", "rsc_context_create", "rsc_context_destroy", "rsc_context_set_stream",
-    "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_last_kernel_timing", "rsc_diag_host_timing", "rsc_context_enable_timing", "rsc_context_set_solve_mode",
+    "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_last_kernel_timing", "rsc_diag_host_timing", "rsc_context_enable_timing", "rsc_selftest_math", "rsc_context_set_solve_mode",
     "rsc_pnp_create", "rsc_pnp_destroy", "rsc_pnp_set_ransac_parameters", "rsc_pnp_iterate", "rsc_pnp_find",
     "rsc_pnp_iterate_many", "rsc_pnp_reset", "rsc_pnp_get_state", "rsc_pnp_last_samples", "rsc_pnp_last_hypotheses",
     "rsc_sim3_last_hypotheses", "rsc_mlpnp_last_counts",
@@ -285,6 +285,7 @@ def load_library(path: str = LIB_PATH):
     L.rsc_status_string.argtypes = [C.c_int]
     L.rsc_context_create.argtypes = [C.c_int, C.POINTER(vp)]
     L.rsc_context_destroy.argtypes = [vp]
+    L.rsc_selftest_math.argtypes = [vp, C.c_int, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double)]
     L.rsc_context_set_stream.argtypes = [vp, vp]
     L.rsc_context_synchronize.argtypes = [vp]
     L.rsc_context_last_timing.argtypes = [vp, C.POINTER(C.c_double)]
@@ -404,6 +405,17 @@ class Context:
 
     def enable_timing(self, on: bool = True):
         _check(load_library().rsc_context_enable_timing(self.h, int(on)), "enable_timing")
+
+    MATH_FNS = {"sin": 0, "cos": 1, "acos": 2, "cbrt": 3, "log": 4, "logf": 5}
+
+    def selftest_math(self, fn: str, x):
+        """rsc_math.h evaluated on the GPU (f64 array in, f64 array out; logf: float in/out)."""
+        x = np.ascontiguousarray(x, np.float64)
+        out = np.empty_like(x)
+        dp = C.POINTER(C.c_double)
+        _check(load_library().rsc_selftest_math(self.h, self.MATH_FNS[fn], x.ctypes.data_as(dp), int(x.size),
+                                                out.ctypes.data_as(dp)), "selftest_math")
+        return out
 
     SOLVE_MODES = {"auto": 0, "mono": 1, "quad": 2, "split": 3}
 

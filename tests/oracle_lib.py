@@ -110,6 +110,7 @@ def lib():
     for fn in ("ora_dm_sin", "ora_dm_cos", "ora_dm_acos", "ora_dm_cbrt"):
         getattr(L, fn).restype = C.c_double
         getattr(L, fn).argtypes = [C.c_double]
+    L.ora_mlpnp_jac.argtypes = [f64p, f64p, f64p, f64p, f64p]
     L.ora_sym_eig.argtypes = [C.c_int, f64p, f64p, f64p]
     L.ora_sym_eig4f.argtypes = [f32p, f32p, f32p]
     L.ora_svd_solve.argtypes = [C.c_int, f64p, f64p, f64p]
