@@ -378,15 +378,21 @@ void rsc_kfdb_destroy(rsc_kfdb* db);
 int rsc_kfdb_add(rsc_kfdb* db, int kf, int n_words, const uint32_t* word_id, const double* word_value);
 /* erase(pKF) (:23-43); erasing an absent slot is a no-op as in the reference. */
 int rsc_kfdb_erase(rsc_kfdb* db, int kf);
+/* Frees slot kf for reuse by another KeyFrame (not a reference operation): erase + the slot's
+ * query state and covisibility row reset to the fresh-KeyFrame values (KeyFrame.cpp:15).  The
+ * facade calls it when a KeyFrame leaves the database. */
+int rsc_kfdb_release(rsc_kfdb* db, int kf);
 /* clear() (:45-49): empties the inverted file; the per-KeyFrame query state is kept. */
 int rsc_kfdb_clear(rsc_kfdb* db);
 /* pKF->GetBestCovisibilityKeyFrames(10) of slot kf (n <= 10 slots, in order). */
 int rsc_kfdb_set_covisibility(rsc_kfdb* db, int kf, int n, const int32_t* best);
-/* The same for count slots at once (kf[c], n[c] <= 10, best[c][10] row-major; one upload). */
+/* The same for count slots at once (kf[c], n[c] <= 10, best[c][10] row-major); only the span of
+ * rows whose content changed is uploaded. */
 int rsc_kfdb_set_covisibility_many(rsc_kfdb* db, int count, const int32_t* kf, const int32_t* n,
                                    const int32_t* best);
 /* DetectRelocalizationCandidates(F) (:174-283): frame_id = F->mnId, (word_id, word_value) =
- * F->mBowVec.  candidates (capacity entries): the returned vector's slots in order. */
+ * F->mBowVec.  candidates (room for 1 + the highest slot added or referenced so far; capacity
+ * always suffices): the returned vector's slots in order.  Queries sweep only the slots in use. */
 int rsc_kfdb_detect_relocalization(rsc_kfdb* db, uint64_t frame_id, int n_words, const uint32_t* word_id,
                                    const double* word_value, int32_t* candidates, int32_t* n_candidates);
 /* DetectLoopCandidates(pKF, minScore) (:52-172): kf_id = pKF->mnId, connected =

@@ -7,9 +7,13 @@
 // WordValue>), GetBestCovisibilityKeyFrames(10) and GetConnectedKeyFrames(); FrameT needs mnId and
 // mBowVec.  VocT needs size() (mvInvertedFile.resize(voc->size()), KeyFrameDatabase.cpp:11).
 // The per-KeyFrame query state (mnLoopQuery, mnLoopWords, mLoopScore, mnRelocQuery, mnRelocWords,
-// mRelocScore) lives on the device, one slot per KeyFrame seen by this database, so callers must not
-// rely on those KeyFrame members.  The covisibility of every known KeyFrame is refreshed (one
-// upload) before each query, as the reference reads GetBestCovisibilityKeyFrames at query time.
+// mRelocScore) lives on the device, one slot per KeyFrame in the database, so callers must not
+// rely on those KeyFrame members.  Slots (slot 0 is reserved, see kNone) are taken on add() and given
+// back on erase(), with their state reset: a KeyFrame outside the database is never in the inverted
+// file, so its query state can never match a query, and every such KeyFrame met through
+// covisibility or connections is represented by the one never-added slot kNone (same outcome).
+// The covisibility of every KeyFrame in the database is refreshed before each query, as the
+// reference reads GetBestCovisibilityKeyFrames at query time; only rows that changed are uploaded.
 // One mutex serialises the calls, as the reference's mMutex does (Tracking, LocalMapping and
 // LoopClosing threads share the database).  In the reference tree:
 //     mpKeyFrameDatabase = new rsc_orb::KeyFrameDatabase<std::shared_ptr<KeyFrame>>(mpVocabulary);
@@ -17,6 +21,8 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
+#include <string>
 #include <unordered_map>
 #include <vector>
 #include "rsc_context.hpp"
@@ -30,7 +36,8 @@ public:
     template <class VocPtr>
     explicit KeyFrameDatabase(const VocPtr& voc, int capacity = 1 << 16, int max_words = 4096) {
         check(rsc_context_create(device(), &ctx_), "rsc_context_create");
-        check(rsc_kfdb_create(ctx_, (uint32_t)voc->size(), capacity, max_words, &db_), "rsc_kfdb_create");
+        capacity_ = capacity + 1;  // + the kNone slot
+        check(rsc_kfdb_create(ctx_, (uint32_t)voc->size(), capacity_, max_words, &db_), "rsc_kfdb_create");
     }
     KeyFrameDatabase(const KeyFrameDatabase&) = delete;
     KeyFrameDatabase& operator=(const KeyFrameDatabase&) = delete;
@@ -45,17 +52,24 @@ public:
         std::vector<uint32_t> ids;
         std::vector<double> vals;
         bow(pKF->mBowVec, ids, vals);
-        check(rsc_kfdb_add(db_, slot(pKF), (int)ids.size(), ids.data(), vals.data()), "KeyFrameDatabase::add");
+        const bool fresh = slots_.find(pKF.get()) == slots_.end();
+        const int s = take_slot(pKF);
+        const int st = rsc_kfdb_add(db_, s, (int)ids.size(), ids.data(), vals.data());
+        if (st != RSC_OK && fresh) give_back(s);
+        check(st, "KeyFrameDatabase::add");
     }
 
-    // erase(pKF) (:23-43)
+    // erase(pKF) (:23-43): the KeyFrame leaves the inverted file; its slot is reused
     void erase(KeyFramePtr pKF) {
         std::lock_guard<std::mutex> lock(mutex_);
         auto it = slots_.find(pKF.get());
-        if (it != slots_.end()) check(rsc_kfdb_erase(db_, it->second), "KeyFrameDatabase::erase");
+        if (it == slots_.end()) return;
+        const int s = it->second;
+        check(rsc_kfdb_release(db_, s), "KeyFrameDatabase::erase");
+        give_back(s);
     }
 
-    // clear() (:45-49)
+    // clear() (:45-49): empties the inverted file (the KeyFrames keep their query state and slots)
     void clear() {
         std::lock_guard<std::mutex> lock(mutex_);
         check(rsc_kfdb_clear(db_), "KeyFrameDatabase::clear");
@@ -64,13 +78,16 @@ public:
     // DetectLoopCandidates(pKF, minScore) (:52-172)
     std::vector<KeyFramePtr> DetectLoopCandidates(KeyFramePtr pKF, float minScore) {
         std::lock_guard<std::mutex> lock(mutex_);
-        std::vector<int32_t> conn;
-        for (const auto& k : pKF->GetConnectedKeyFrames()) conn.push_back(slot(k));
+        std::vector<int32_t> conn;  // only KeyFrames in the database can be excluded from the walk
+        for (const auto& k : pKF->GetConnectedKeyFrames()) {
+            const int s = slot_of(k);
+            if (s != kNone) conn.push_back(s);
+        }
         std::vector<uint32_t> ids;
         std::vector<double> vals;
         bow(pKF->mBowVec, ids, vals);
         refresh_covisibility();
-        std::vector<int32_t> cand(kfs_.size() + 1);
+        std::vector<int32_t> cand(kfs_.size() + 1);  // one more than the slots in use
         int32_t n = 0;
         check(rsc_kfdb_detect_loop(db_, (uint64_t)pKF->mnId, (int)ids.size(), ids.data(), vals.data(),
                                    (int)conn.size(), conn.data(), minScore, cand.data(), &n),
@@ -108,27 +125,53 @@ private:
         }
     }
 
-    // the KeyFrame's slot (its query state lives there), assigned on first sight
-    int slot(const KeyFramePtr& k) {
+    static constexpr int kNone = 0;  // never added: stands for every KeyFrame outside the database
+
+    int slot_of(const KeyFramePtr& k) const {
+        auto it = slots_.find(k.get());
+        return it == slots_.end() ? kNone : it->second;
+    }
+
+    // the KeyFrame's slot (its query state lives there), taken when it joins the database
+    int take_slot(const KeyFramePtr& k) {
         auto it = slots_.find(k.get());
         if (it != slots_.end()) return it->second;
-        const int s = (int)kfs_.size();
+        int s;
+        if (!free_.empty()) {
+            s = free_.back();
+            free_.pop_back();
+        } else {
+            if ((int)kfs_.size() >= capacity_)
+                throw std::runtime_error("rsc_orb::KeyFrameDatabase: " + std::to_string(capacity_ - 1) +
+                                         " KeyFrames are in the database (its capacity); erase some or "
+                                         "construct it with a larger capacity");
+            s = (int)kfs_.size();
+            kfs_.push_back(nullptr);
+        }
         slots_.emplace(k.get(), s);
-        kfs_.push_back(k);
+        kfs_[s] = k;
         return s;
     }
 
-    // GetBestCovisibilityKeyFrames(10) of every known KeyFrame, one upload
+    void give_back(int s) {
+        slots_.erase(kfs_[s].get());
+        kfs_[s] = nullptr;  // the database no longer holds the KeyFrame alive
+        free_.push_back(s);
+    }
+
+    // GetBestCovisibilityKeyFrames(10) of every KeyFrame in the database; the C ABI uploads only
+    // the rows that changed since the last query
     void refresh_covisibility() {
-        const int n = (int)kfs_.size();
-        std::vector<int32_t> kf(n), cnt(n), best((size_t)n * 10, 0);
-        for (int i = 0; i < n; ++i) {
-            kf[i] = i;
+        std::vector<int32_t> kf, cnt, best;
+        for (int i = 1; i < (int)kfs_.size(); ++i) {
+            if (!kfs_[i]) continue;
             const auto nb = kfs_[i]->GetBestCovisibilityKeyFrames(10);
-            cnt[i] = (int32_t)nb.size();
-            for (int j = 0; j < cnt[i]; ++j) best[(size_t)i * 10 + j] = slot(nb[j]);
+            kf.push_back(i);
+            cnt.push_back((int32_t)nb.size());
+            for (int j = 0; j < 10; ++j) best.push_back(j < (int)nb.size() ? slot_of(nb[j]) : 0);
         }
-        check(rsc_kfdb_set_covisibility_many(db_, n, kf.data(), cnt.data(), best.data()), "covisibility");
+        check(rsc_kfdb_set_covisibility_many(db_, (int)kf.size(), kf.data(), cnt.data(), best.data()),
+              "covisibility");
     }
 
     std::vector<KeyFramePtr> resolve(const std::vector<int32_t>& cand, int n) const {
@@ -141,8 +184,10 @@ private:
     rsc_context* ctx_ = nullptr;
     rsc_kfdb* db_ = nullptr;
     std::mutex mutex_;
+    int capacity_ = 0;
     std::unordered_map<const void*, int> slots_;
-    std::vector<KeyFramePtr> kfs_;
+    std::vector<KeyFramePtr> kfs_{KeyFramePtr()};  // [slot]; slot 0 = kNone
+    std::vector<int> free_;
 };
 
 }  // namespace rsc_orb

@@ -1799,6 +1799,7 @@ int rsc_search_by_sim3_many(rsc_context* C, rsc_kfview* const* kf1, rsc_kfview* 
 struct rsc_kfdb {
     rsc_context* ctx = nullptr;
     int cap = 0, max_words = 0;
+    int hw = 0;  // slots in use: 1 + the highest slot ever added or referenced (queries sweep [0, hw))
     uint32_t vocab = 0;
     uint32_t next_seq = 1;
     std::vector<uint8_t> present;
@@ -1811,9 +1812,10 @@ struct rsc_kfdb {
     DevBuf<float> score, sc, acc;
     DevBuf<uint8_t> conn;
     PinBuf<char> stage;  // query upload | candidates download
+    void touch(int s) { hw = std::max(hw, s + 1); }
     DevKFDB dev() const {
         DevKFDB d;
-        d.cap = cap;
+        d.cap = hw;  // the kernels' sweep bound; the arrays are sized (and strided) by cap
         d.max_words = max_words;
         d.vocab = vocab;
         d.wpos = wpos.p;
@@ -1917,6 +1919,7 @@ int rsc_kfdb_add(rsc_kfdb* db, int kf, int n, const uint32_t* id, const double* 
     RSC_HIP(hipMemcpy(db->seq.p + kf, &s, 4, hipMemcpyHostToDevice));
     RSC_HIP(hipMemcpy(db->len.p + kf, &n, 4, hipMemcpyHostToDevice));
     db->present[kf] = 1;
+    db->touch(kf);
     return RSC_OK;
 }
 
@@ -1926,6 +1929,26 @@ int rsc_kfdb_erase(rsc_kfdb* db, int kf) {
     RSC_HIP(hipSetDevice(db->ctx->device));
     RSC_HIP(hipMemsetAsync(db->len.p + kf, 0, 4, db->ctx->stream));
     RSC_HIP(hipStreamSynchronize(db->ctx->stream));
+    db->present[kf] = 0;
+    return RSC_OK;
+}
+
+int rsc_kfdb_release(rsc_kfdb* db, int kf) {
+    if (!db || kf < 0 || kf >= db->cap) return RSC_ERR_ARG;
+    rsc_context* C = db->ctx;
+    RSC_HIP(hipSetDevice(C->device));
+    const size_t K = (size_t)db->cap;
+    RSC_HIP(hipMemsetAsync(db->len.p + kf, 0, 4, C->stream));
+    for (int t = 0; t < 2; ++t) {
+        RSC_HIP(hipMemsetAsync(db->query.p + t * K + kf, 0, 8, C->stream));
+        RSC_HIP(hipMemsetAsync(db->words.p + t * K + kf, 0, 4, C->stream));
+        RSC_HIP(hipMemsetAsync(db->score.p + t * K + kf, 0, 4, C->stream));
+    }
+    RSC_HIP(hipMemsetAsync(db->covis.p + (size_t)kf * kKfdbCovis, 0, 4 * kKfdbCovis, C->stream));
+    RSC_HIP(hipMemsetAsync(db->covis_n.p + kf, 0, 4, C->stream));
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    std::fill(db->covis_h.begin() + (size_t)kf * kKfdbCovis, db->covis_h.begin() + (size_t)(kf + 1) * kKfdbCovis, 0);
+    db->covis_n_h[kf] = 0;
     db->present[kf] = 0;
     return RSC_OK;
 }
@@ -1948,6 +1971,8 @@ int rsc_kfdb_set_covisibility(rsc_kfdb* db, int kf, int n, const int32_t* best) 
     }
     std::copy(row, row + kKfdbCovis, db->covis_h.begin() + (size_t)kf * kKfdbCovis);
     db->covis_n_h[kf] = n;
+    db->touch(kf);
+    for (int i = 0; i < n; ++i) db->touch(row[i]);
     RSC_HIP(hipSetDevice(db->ctx->device));
     RSC_HIP(hipStreamSynchronize(db->ctx->stream));
     RSC_HIP(hipMemcpy(db->covis.p + (size_t)kf * kKfdbCovis, row, sizeof(row), hipMemcpyHostToDevice));
@@ -1963,15 +1988,31 @@ int rsc_kfdb_set_covisibility_many(rsc_kfdb* db, int count, const int32_t* kf, c
         for (int i = 0; i < n[c]; ++i)
             if (best[(size_t)c * kKfdbCovis + i] < 0 || best[(size_t)c * kKfdbCovis + i] >= db->cap) return RSC_ERR_ARG;
     }
+    // rows whose content changed go up as one span [lo, hi] (the mirror keeps the rest)
+    int lo = INT32_MAX, hi = -1;
     for (int c = 0; c < count; ++c) {
         int32_t* row = db->covis_h.data() + (size_t)kf[c] * kKfdbCovis;
-        for (int i = 0; i < kKfdbCovis; ++i) row[i] = i < n[c] ? best[(size_t)c * kKfdbCovis + i] : 0;
+        bool changed = db->covis_n_h[kf[c]] != n[c];
+        for (int i = 0; i < kKfdbCovis; ++i) {
+            const int32_t v = i < n[c] ? best[(size_t)c * kKfdbCovis + i] : 0;
+            changed |= row[i] != v;
+            row[i] = v;
+            if (i < n[c]) db->touch(v);
+        }
         db->covis_n_h[kf[c]] = n[c];
+        db->touch(kf[c]);
+        if (changed) {
+            lo = std::min(lo, kf[c]);
+            hi = std::max(hi, kf[c]);
+        }
     }
+    if (hi < 0) return RSC_OK;
     RSC_HIP(hipSetDevice(db->ctx->device));
     RSC_HIP(hipStreamSynchronize(db->ctx->stream));
-    RSC_HIP(hipMemcpy(db->covis.p, db->covis_h.data(), 4 * db->covis_h.size(), hipMemcpyHostToDevice));
-    RSC_HIP(hipMemcpy(db->covis_n.p, db->covis_n_h.data(), 4 * db->covis_n_h.size(), hipMemcpyHostToDevice));
+    const size_t rows = (size_t)(hi - lo + 1);
+    RSC_HIP(hipMemcpy(db->covis.p + (size_t)lo * kKfdbCovis, db->covis_h.data() + (size_t)lo * kKfdbCovis,
+                      4 * kKfdbCovis * rows, hipMemcpyHostToDevice));
+    RSC_HIP(hipMemcpy(db->covis_n.p + lo, db->covis_n_h.data() + lo, 4 * rows, hipMemcpyHostToDevice));
     return RSC_OK;
 }
 
@@ -1993,13 +2034,20 @@ int kfdb_query(rsc_kfdb* db, uint64_t qid, int n, const uint32_t* id, const doub
         RSC_HIP(hipMemcpyAsync(db->qbuf.p, h, vo + 8 * (size_t)n, hipMemcpyHostToDevice, C->stream));
     }
     if (loop) {
-        uint8_t* m = reinterpret_cast<uint8_t*>(h + 16 * (size_t)db->max_words + 16);
-        std::memset(m, 0, K);
-        for (int i = 0; i < n_conn; ++i) {
+        for (int i = 0; i < n_conn; ++i)
             if (conn[i] < 0 || conn[i] >= db->cap) return RSC_ERR_ARG;
-            m[conn[i]] = 1;
-        }
-        RSC_HIP(hipMemcpyAsync(db->conn.p, m, K, hipMemcpyHostToDevice, C->stream));
+        for (int i = 0; i < n_conn; ++i) db->touch(conn[i]);
+    }
+    if (db->hw == 0) {  // nothing was ever added: no candidates, no state to update
+        *n_cand = 0;
+        return RSC_OK;
+    }
+    const size_t H = (size_t)db->hw;  // the sweeps and the copies cover the slots in use only
+    if (loop) {
+        uint8_t* m = reinterpret_cast<uint8_t*>(h + 16 * (size_t)db->max_words + 16);
+        std::memset(m, 0, H);
+        for (int i = 0; i < n_conn; ++i) m[conn[i]] = 1;
+        RSC_HIP(hipMemcpyAsync(db->conn.p, m, H, hipMemcpyHostToDevice, C->stream));
     }
     KfdbQuery q;
     q.id = (unsigned long long)qid;
@@ -2011,7 +2059,7 @@ int kfdb_query(rsc_kfdb* db, uint64_t qid, int n, const uint32_t* id, const doub
     d.qvals = reinterpret_cast<const double*>(db->qbuf.p + vo);
     RSC_HIP(launch_kfdb_query(d, q, C->stream));
     timing_begin(C, 4);
-    RSC_HIP(hipMemcpyAsync(h, db->out.p, 4 * (K + 1), hipMemcpyDeviceToHost, C->stream));
+    RSC_HIP(hipMemcpyAsync(h, db->out.p, 4 * (H + 1), hipMemcpyDeviceToHost, C->stream));
     RSC_HIP(hipStreamSynchronize(C->stream));
     if (C->timing) {
         float ms = 0;

@@ -45,7 +45,7 @@ EXPORTED = [
     "rsc_search_by_bow_kf_many", "rsc_diag_bow_phase_stamps", "rsc_diag_refine_phase_stamps",
     "rsc_search_by_sim3_many", "rsc_kfview_create", "rsc_kfview_destroy",
     "rsc_optimize_sim3_many",
-    "rsc_kfdb_create", "rsc_kfdb_destroy", "rsc_kfdb_add", "rsc_kfdb_erase", "rsc_kfdb_clear",
+    "rsc_kfdb_create", "rsc_kfdb_destroy", "rsc_kfdb_add", "rsc_kfdb_erase", "rsc_kfdb_release", "rsc_kfdb_clear",
     "rsc_kfdb_set_covisibility", "rsc_kfdb_set_covisibility_many", "rsc_kfdb_detect_relocalization", "rsc_kfdb_detect_loop", "rsc_kfdb_state",
 ]
 
@@ -218,6 +218,10 @@ class KeyFrameDatabase:
     def erase(self, kf: int):
         _check(load_library().rsc_kfdb_erase(self.h, int(kf)), "rsc_kfdb_erase")
 
+    def release(self, kf: int):
+        """Free slot kf for reuse (erase + fresh query state and covisibility row)."""
+        _check(load_library().rsc_kfdb_release(self.h, int(kf)), "rsc_kfdb_release")
+
     def clear(self):
         _check(load_library().rsc_kfdb_clear(self.h), "rsc_kfdb_clear")
 
@@ -361,6 +365,7 @@ def load_library(path: str = LIB_PATH):
     L.rsc_kfdb_destroy.argtypes = [vp]
     L.rsc_kfdb_add.argtypes = [vp, C.c_int, C.c_int, u32p_, f64p_]
     L.rsc_kfdb_erase.argtypes = [vp, C.c_int]
+    L.rsc_kfdb_release.argtypes = [vp, C.c_int]
     L.rsc_kfdb_clear.argtypes = [vp]
     L.rsc_kfdb_set_covisibility.argtypes = [vp, C.c_int, C.c_int, i32p]
     L.rsc_kfdb_set_covisibility_many.argtypes = [vp, C.c_int, i32p, i32p, i32p]

@@ -110,3 +110,81 @@ def test_abi_errors():
     with pytest.raises(RuntimeError):
         db.detect_loop(3, ids, vals, np.array([9], np.int32), 0.0)  # connected slot out of range
     assert list(db.detect_relocalization(1, ids, vals)) == [0]
+
+
+def test_more_than_4096_slots_in_use():
+    """The finish kernel's select loop beyond its 4 x 1024 register-held list entries (slots in
+    use > 4096), with a sparse high slot added last (the sweeps cover every slot up to it)."""
+    rng = np.random.default_rng(31)
+    n = 4600
+    sc = synth.make_kfdb_scene(rng, n, words_per_kf=60, step=12, n_frequent=8)
+    g, o = gpu_db(n + 300, max_words=128), ol.OracleKFDB(n + 300)
+    order = list(range(n))
+    for k in order:
+        for db in (g, o):
+            db.add(k, *sc.bows[k])
+            db.set_covisibility(k, sc.covis[k])
+    for db in (g, o):
+        db.add(n + 250, *sc.bows[n - 1])
+    for f in range(1, 9):
+        ids, vals = synth.make_kfdb_query(rng, sc, rng.uniform(n - 900, n - 1), words=60)
+        if f % 2:
+            a, b = g.detect_relocalization(f, ids, vals), o.detect_relocalization(f, ids, vals)
+        else:
+            conn = sc.covis[int(rng.integers(n - 900, n))]
+            a, b = g.detect_loop(7000 + f, ids, vals, conn, 0.0), o.detect_loop(7000 + f, ids, vals, conn, 0.0)
+        assert list(a) == list(b), f
+    assert states(g, n + 300) == states(o, n + 300)
+
+
+def test_more_than_1024_scored_slots():
+    """A query every one of 1,500 KeyFrames shares all its words with (all pass minCommonWords):
+    the finish kernel ranks and scores more slots than its LDS ranking holds (1,024)."""
+    rng = np.random.default_rng(32)
+    n = 1500
+    words = np.sort(rng.choice(10 ** 6, 40, replace=False)).astype(np.uint32)
+    g, o = gpu_db(n, max_words=64), ol.OracleKFDB(n)
+    for k in range(n):
+        vals = rng.uniform(0.1, 1.0, 40)
+        vals = vals / vals.sum()
+        extra = np.sort(rng.choice(10 ** 6, 10, replace=False)).astype(np.uint32)
+        ids = np.unique(np.concatenate([words, extra]))
+        v = np.concatenate([vals, rng.uniform(0.01, 0.05, len(ids) - 40)])
+        for db in (g, o):
+            db.add(k, ids, v[:len(ids)])
+            db.set_covisibility(k, np.array([(k + j) % n for j in range(1, 6)], np.int32))
+    qv = rng.uniform(0.1, 1.0, 40)
+    for f in range(1, 4):
+        a, b = g.detect_relocalization(f, words, qv), o.detect_relocalization(f, words, qv)
+        assert list(a) == list(b) and len(a) > 0, f
+        a, b = g.detect_loop(9000 + f, words, qv, np.array([1, 2], np.int32), 0.0), \
+            o.detect_loop(9000 + f, words, qv, np.array([1, 2], np.int32), 0.0)
+        assert list(a) == list(b), f
+    assert states(g, n) == states(o, n)
+
+
+def test_release_resets_the_slot():
+    """rsc_kfdb_release (the facade's erase): the slot leaves the inverted file and its query
+    state and covisibility row return to a fresh KeyFrame's, so another KeyFrame can take it."""
+    rng = np.random.default_rng(33)
+    sc = synth.make_kfdb_scene(rng, 40, words_per_kf=100, step=30)
+    g, o = gpu_db(64, max_words=128), ol.OracleKFDB(64)
+    for k in range(40):
+        for db in (g, o):
+            db.add(k, *sc.bows[k])
+            db.set_covisibility(k, sc.covis[k])
+    ids, vals = synth.make_kfdb_query(rng, sc, 20.0, words=100)
+    assert list(g.detect_relocalization(3, ids, vals)) == list(o.detect_relocalization(3, ids, vals))
+    touched = [k for k in range(40) if g.state(k)[0][1] == 3]
+    assert touched
+    k = touched[0]
+    g.release(k)
+    assert g.state(k) == ((0, 0), (0, 0), (0.0, 0.0))
+    # the slot now hosts another KeyFrame: the database behaves as the oracle with that KeyFrame
+    # in a fresh slot
+    o.erase(k)
+    g.add(k, *sc.bows[39])
+    o.add(50, *sc.bows[39])
+    a = g.detect_relocalization(4, ids, vals)
+    b = o.detect_relocalization(4, ids, vals)
+    assert [50 if x == k else x for x in a] == list(b)
