@@ -731,30 +731,42 @@ def cpu_baseline_sim3opt(probs):
                 sample=f"{len(probs)} pairs per batch, 1 warm-up + median of {n}, oracle restatement, 1 thread")
 
 
-def kfdb_scene(seed=82, n_kfs=2000, n_queries=64):
-    """a 2000-KeyFrame database (600-word BowVectors, a long EuRoC/KITTI map)
-    and 64 relocalization queries (Frame BowVectors observed along the trajectory)."""
+def kfdb_scene(seed=82, n_kfs=2000, n_queries=64, revisits=12):
+    """a 2000-KeyFrame database (600-word BowVectors) built over 12 passes of
+    the same places (a long EuRoC/KITTI-style map with revisits), and 64 relocalization queries
+    (Frame BowVectors observed at those places): the reference returns C ~ 3-16 candidates each."""
     from rsc import synth
     rng = np.random.default_rng(seed)
-    sc = synth.make_kfdb_scene(rng, n_kfs, words_per_kf=600)
-    queries = [synth.make_kfdb_query(rng, sc, rng.uniform(0, n_kfs - 1)) for _ in range(n_queries)]
+    sc = synth.make_kfdb_scene(rng, n_kfs, words_per_kf=600, revisits=revisits)
+    queries = [synth.make_kfdb_query(rng, sc, rng.uniform(0, sc.places - 1)) for _ in range(n_queries)]
     return sc, queries
 
 
+KFDB_CAPACITY = 65537  # the facade's default (1 << 16 KeyFrames + its never-added slot)
+
+
 def run_kfdb(engine, ctx, sc, queries, args):
-    """KeyFrameDatabase::DetectRelocalizationCandidates (KeyFrameDatabase.cpp:174-283) over the
-    resident database: one rsc_kfdb_detect_relocalization per query (query upload, four kernels,
-    candidates back), fresh Frame ids every step so every query walks the full path."""
+    """KeyFrameDatabase::DetectRelocalizationCandidates (KeyFrameDatabase.cpp:174-283) as the C++
+    facade runs it: a database of the facade's default capacity, and per query the covisibility
+    refresh of every KeyFrame (rsc_kfdb_set_covisibility_many: unchanged rows are not uploaded)
+    followed by rsc_kfdb_detect_relocalization (query upload, four kernels over the slots in use,
+    candidates back); fresh Frame ids every step so every query walks the full path."""
     n = len(sc.bows)
-    db = engine.KeyFrameDatabase(ctx, n)
+    db = engine.KeyFrameDatabase(ctx, KFDB_CAPACITY)
     for k in range(n):
         db.add(k, *sc.bows[k])
-        db.set_covisibility(k, sc.covis[k])
+    kfs = np.arange(n, dtype=np.int32)
+    cnt = np.array([len(c) for c in sc.covis], np.int32)
+    tab = np.zeros((n, 10), np.int32)
+    for k, c in enumerate(sc.covis):
+        tab[k, :len(c)] = c
+    db.set_covisibility_table(kfs, cnt, tab)
     fid = [1]
 
     def step():
         nc = 0
         for ids, vals in queries:
+            db.set_covisibility_table(kfs, cnt, tab)
             nc += len(db.detect_relocalization(fid[0], ids, vals))
             fid[0] += 1
         return nc
@@ -776,8 +788,9 @@ def run_kfdb(engine, ctx, sc, queries, args):
     Q = len(queries)
     words = sum(len(b[0]) for b in sc.bows)
     return dict(queries_per_s=Q * steps / dt, ms_per_query=1e3 * dt / (Q * steps), kernel_ms_per_query=kms / Q,
-                keyframes=n, words_per_keyframe=words / n, mean_candidates=nc / (Q * steps),
-                count_kernel_bytes=4 * words, steps=steps)
+                keyframes=n, capacity=KFDB_CAPACITY, words_per_keyframe=words / n, mean_candidates=nc / (Q * steps),
+                count_kernel_bytes=4 * words, steps=steps,
+                path="facade path: covisibility refresh of all KeyFrames + query, per query")
 
 
 def cpu_baseline_kfdb(sc, queries, seconds):

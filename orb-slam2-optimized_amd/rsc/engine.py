@@ -238,6 +238,12 @@ class KeyFrameDatabase:
             tab[i, :len(b)] = b
         _check(load_library().rsc_kfdb_set_covisibility_many(self.h, len(k), k, n, tab), "set_covisibility_many")
 
+    def set_covisibility_table(self, kfs, counts, table):
+        """set_covisibility_many with the rows already packed: kfs int32 [c], counts int32 [c],
+        table int32 [c, 10] (what a C++ caller passes; no per-row Python work)."""
+        _check(load_library().rsc_kfdb_set_covisibility_many(self.h, len(kfs), kfs, counts, table),
+               "set_covisibility_many")
+
     def detect_relocalization(self, frame_id: int, ids, vals) -> np.ndarray:
         """DetectRelocalizationCandidates(F) (:174-283): candidate slots in the reference's order."""
         i, v = self._bow(ids, vals)

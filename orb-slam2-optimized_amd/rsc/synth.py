@@ -558,6 +558,7 @@ class KFDBScene:
     frequent: np.ndarray
     step: int
     span: int
+    places: int = 0  # distinct places (n_kfs / revisits)
 
 
 def _bow_from(rng: np.random.Generator, words: np.ndarray):
@@ -577,13 +578,20 @@ def _place_words(rng, sc: KFDBScene, pos: float, n_words: int, noise_frac: float
 
 
 def make_kfdb_scene(rng: np.random.Generator, n_kfs: int, words_per_kf: int = 600, step: int = 150,
-                    n_frequent: int = 40) -> KFDBScene:
+                    n_frequent: int = 40, revisits: int = 1) -> KFDBScene:
+    """KeyFrames along a trajectory; KeyFrame k observes the words of place k (consecutive places
+    share words).  revisits > 1: the trajectory covers the same n_kfs / revisits places that many
+    times (a map built over repeated passes, as EuRoC's MH / V sequences), with a jittered place per
+    pass, so a relocalization query matches one covisibility group per pass."""
     span = 2 * words_per_kf
-    pools = rng.permutation(VOCAB_WORDS)[: n_kfs * step + span].astype(np.uint32)
+    places = -(-n_kfs // revisits)
+    pools = rng.permutation(VOCAB_WORDS)[: places * step + span].astype(np.uint32)
     frequent = rng.integers(0, VOCAB_WORDS, n_frequent).astype(np.uint32)
     sc = KFDBScene([], [], pools, frequent, step, span)
+    sc.places = places
     for k in range(n_kfs):
-        sc.bows.append(_bow_from(rng, _place_words(rng, sc, k, words_per_kf)))
+        pos = k if revisits == 1 else (k % places) + rng.uniform(-0.3, 0.3)
+        sc.bows.append(_bow_from(rng, _place_words(rng, sc, pos, words_per_kf)))
     for k in range(n_kfs):
         near = sorted((j for j in range(max(0, k - 8), min(n_kfs, k + 9)) if j != k), key=lambda j: (abs(j - k), j))
         sc.covis.append(np.array(near[:10], np.int32))
