@@ -10,6 +10,15 @@ per-event winner record that the ranks all-gather (RCCL over xGMI; gloo in the C
   N~U[20,600] matches (>= 20 per :253), Sim3Solver parameters (0.99,20,300) (:258), the same
   iterate(5) round-robin (:271-286).
 
+Winner semantics: an event ends at the FIRST candidate whose RANSAC iterate() returns a pose.  The
+reference keeps the round-robin going when that pose then fails its later gates —
+PoseOptimization + SearchByProjection reaching nGood >= 50 (Tracking.cpp:1278-1330) for
+relocalization, OptimizeSim3 keeping >= 20 inliers (LoopClosing.cpp:296-312) for loops — so the
+records (and the throughput) equal the reference's only where the first RANSAC success also passes
+those gates.  The stream measures the RANSAC stage the north star names; a caller that needs the
+full gate runs rsc_pose_optimization_many / rsc_optimize_sim3_many on the winner and, if it fails,
+resumes the round-robin with the remaining candidates (INTEGRATION.md "Event streams").
+
 Events are independent, so a rank processes whole events (no data-path collective); the only
 exchange is one all-gather of the per-event records at the end.  Every candidate owns its rand()
 stream (seed fixed by its global id), so the gathered records equal a one-rank run.
