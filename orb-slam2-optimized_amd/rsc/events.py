@@ -16,8 +16,8 @@ PoseOptimization + SearchByProjection reaching nGood >= 50 (Tracking.cpp:1278-13
 relocalization, OptimizeSim3 keeping >= 20 inliers (LoopClosing.cpp:296-312) for loops — so the
 records (and the throughput) equal the reference's only where the first RANSAC success also passes
 those gates.  The stream measures the RANSAC stage the north star names; a caller that needs the
-full gate runs rsc_pose_optimization_many / rsc_optimize_sim3_many on the winner and, if it fails,
-resumes the round-robin with the remaining candidates (INTEGRATION.md "Event streams").
+full gate drives the round-robin with the per-solver iterate calls and the device
+PoseOptimization / OptimizeSim3 (after the event entry points).
 
 Events are independent, so a rank processes whole events (no data-path collective); the only
 exchange is one all-gather of the per-event records at the end.  Every candidate owns its rand()
