@@ -164,6 +164,13 @@ int rsc_sim3_prepared(const rsc_sim3* s, float* X1c, float* X2c, float* P1im1, f
 /* MLPnPsolver::MLPnPsolver (MLPnPsolver.cpp:5-53, includes its SetRansacParameters() call). */
 int rsc_mlpnp_create(rsc_context* ctx, const rsc_pnp_problem* problem, uint32_t seed, rsc_mlpnp** out);
 void rsc_mlpnp_destroy(rsc_mlpnp* s);
+/* computePose's covMats (MLPnPsolver.cpp:321, :375-388, :483-484, :694-695): cov = [n][9] row-major
+ * 3x3 bearing-vector covariance per correspondence (the problem's compacted order), or NULL for the
+ * reference's own configuration (it passes a single-element covMats, so use_cov is false).  With
+ * covariances the hypotheses solve A^T P A and the Gauss-Newton runs on J^T Kll J, P = Kll the
+ * block-diagonal (N^T Sigma N)^-1.  Not reachable from the reference's callers: parity unpinned
+ * (SURVEY.md Q15); checked against the oracle's restatement. */
+int rsc_mlpnp_set_covariances(rsc_mlpnp* s, const double* cov);
 /* MLPnPsolver::SetRansacParameters (MLPnPsolver.cpp:185-220; defaults 0.99, 8, 300, 6, 0.4, 5.991).
  * min_set must be in [6, 8] (computePose asserts n > 5, :324) -> RSC_ERR_UNSUPPORTED otherwise. */
 int rsc_mlpnp_set_ransac_parameters(rsc_mlpnp* s, double probability, int min_inliers, int max_iterations,

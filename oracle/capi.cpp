@@ -339,6 +339,7 @@ void ora_sim3_run_prepared_batch(int C, const int32_t* n, const int64_t* off, co
 
 
 // ---- MLPnPsolver (mlpnp_oracle.h) ----------------------------------------------------------------
+void ora_mlpnp_set_cov(void* h, const double* cov) { static_cast<MLPnPOracle*>(h)->set_covariances(cov); }
 void* ora_mlpnp_create(int n, int n_points, const float* p2d, const float* p3dw, const float* sigma2,
                        const int32_t* kp_index, float fx, float fy, float cx, float cy, uint32_t seed) {
     return new MLPnPOracle(n, n_points, p2d, p3dw, sigma2, kp_index, fx, fy, cx, cy, seed);

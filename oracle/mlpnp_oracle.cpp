@@ -390,8 +390,9 @@ void mlpnp_jac(const double X[3], const double nr[3], const double ns[3], const 
     }
 }
 
-// mlpnp_gn (MLPnPsolver.cpp:659-723), use_cov = false.
-void mlpnp_gn(double x[6], int n, const double (*pts)[3], const double (*Ns)[3][2]) {
+// mlpnp_gn (MLPnPsolver.cpp:659-723).  Pw: the 2x2 blocks of Kll per correspondence (use_cov), or
+// null (use_cov = false: JacTSKll = Jac^T).
+void mlpnp_gn(double x[6], int n, const double (*pts)[3], const double (*Ns)[3][2], const double (*Pw)[4] = nullptr) {
     std::vector<double> r(2 * n), Jm(2 * n * 6), dl(2 * n);
     int it = 0;
     bool stop = false;
@@ -414,14 +415,22 @@ void mlpnp_gn(double x[6], int n, const double (*pts)[3], const double (*Ns)[3][
             for (int k = 0; k < 6; ++k) { Jm[(2 * i) * 6 + k] = J[0][k]; Jm[(2 * i + 1) * 6 + k] = J[1][k]; }
         }
         double A[6][6], g[6], dx[6];
+        // JacTSKll (6 x 2n): Jac^T, or Jac^T * Kll evaluated column by column of the sparse Kll
+        std::vector<double> JtK(6 * 2 * n);
+        for (int a = 0; a < 6; ++a)
+            for (int i = 0; i < n; ++i)
+                for (int q = 0; q < 2; ++q)
+                    JtK[a * 2 * n + 2 * i + q] = Pw ? Jm[(2 * i) * 6 + a] * Pw[i][q] + Jm[(2 * i + 1) * 6 + a] * Pw[i][2 + q]
+                                                    : Jm[(2 * i + q) * 6 + a];
         for (int a = 0; a < 6; ++a) {
+            const double* ja = &JtK[a * 2 * n];
             for (int b = 0; b < 6; ++b) {
-                double s = Jm[a] * Jm[b];
-                for (int q = 1; q < 2 * n; ++q) s = s + Jm[q * 6 + a] * Jm[q * 6 + b];
+                double s = ja[0] * Jm[b];
+                for (int q = 1; q < 2 * n; ++q) s = s + ja[q] * Jm[q * 6 + b];
                 A[a][b] = s;
             }
-            double s = Jm[a] * r[0];
-            for (int q = 1; q < 2 * n; ++q) s = s + Jm[q * 6 + a] * r[q];
+            double s = ja[0] * r[0];
+            for (int q = 1; q < 2 * n; ++q) s = s + ja[q] * r[q];
             g[a] = s;
         }
         ldlt_solve6(A, g, dx);
@@ -569,13 +578,44 @@ void MLPnPOracle::computePose(const int* idx, int n, double Rout[3][3], double t
             }
         }
     }
+    // 2. stochastic model (:368-388): P = I, or the block-diagonal inverse of N^T Sigma N when a
+    // covariance is given for every correspondence
+    const bool use_cov = !mvCov.empty();
+    std::vector<double> Pw(use_cov ? 4 * n : 0);
+    for (int i = 0; use_cov && i < n; ++i) {
+        const double* S = &mvCov[9 * idx[i]];
+        double NtS[2][3], T[2][2];
+        for (int q = 0; q < 2; ++q)
+            for (int c = 0; c < 3; ++c) NtS[q][c] = (Ns[i][0][q] * S[c] + Ns[i][1][q] * S[3 + c]) + Ns[i][2][q] * S[6 + c];
+        for (int q = 0; q < 2; ++q)
+            for (int u = 0; u < 2; ++u) T[q][u] = (NtS[q][0] * Ns[i][0][u] + NtS[q][1] * Ns[i][1][u]) + NtS[q][2] * Ns[i][2][u];
+        const double invdet = 1.0 / (T[0][0] * T[1][1] - T[1][0] * T[0][1]);  // Matrix2d::inverse
+        Pw[4 * i + 0] = T[1][1] * invdet;
+        Pw[4 * i + 1] = -T[0][1] * invdet;
+        Pw[4 * i + 2] = -T[1][0] * invdet;
+        Pw[4 * i + 3] = T[0][0] * invdet;
+    }
     std::vector<double> AtA(colsA * colsA), Vs(colsA * colsA), sv(colsA);
-    for (int a = 0; a < colsA; ++a)
-        for (int b = 0; b < colsA; ++b) {
-            double s = A[a] * A[b];
-            for (int r = 1; r < 2 * n; ++r) s = s + A[r * colsA + a] * A[r * colsA + b];
-            AtA[a * colsA + b] = s;
-        }
+    if (use_cov) {  // A^T P A (:483): (A^T P) first, then the row sums in order
+        std::vector<double> AtP(colsA * 2 * n);
+        for (int a = 0; a < colsA; ++a)
+            for (int i = 0; i < n; ++i)
+                for (int q = 0; q < 2; ++q)
+                    AtP[a * 2 * n + 2 * i + q] = A[(2 * i) * colsA + a] * Pw[4 * i + q] + A[(2 * i + 1) * colsA + a] * Pw[4 * i + 2 + q];
+        for (int a = 0; a < colsA; ++a)
+            for (int b = 0; b < colsA; ++b) {
+                double s = AtP[a * 2 * n] * A[b];
+                for (int r = 1; r < 2 * n; ++r) s = s + AtP[a * 2 * n + r] * A[r * colsA + b];
+                AtA[a * colsA + b] = s;
+            }
+    } else {
+        for (int a = 0; a < colsA; ++a)
+            for (int b = 0; b < colsA; ++b) {
+                double s = A[a] * A[b];
+                for (int r = 1; r < 2 * n; ++r) s = s + A[r * colsA + a] * A[r * colsA + b];
+                AtA[a * colsA + b] = s;
+            }
+    }
     jacobi_svd_square(colsA, AtA.data(), false, nullptr, sv.data(), Vs.data());
     double r1[12];
     for (int k = 0; k < colsA; ++k) r1[k] = Vs[k * colsA + colsA - 1];
@@ -673,9 +713,15 @@ void MLPnPOracle::computePose(const int* idx, int n, double Rout[3][3], double t
     x[3] = t[0]; x[4] = t[1]; x[5] = t[2];
     std::vector<double> pts(3 * n);
     for (int i = 0; i < 3 * n; ++i) pts[i] = P0[i];
-    mlpnp_gn(x, n, reinterpret_cast<const double(*)[3]>(pts.data()), Ns.data());
+    mlpnp_gn(x, n, reinterpret_cast<const double(*)[3]>(pts.data()), Ns.data(),
+             use_cov ? reinterpret_cast<const double(*)[4]>(Pw.data()) : nullptr);
     rodrigues2rot(x, Rout);
     tout[0] = x[3]; tout[1] = x[4]; tout[2] = x[5];
+}
+
+void MLPnPOracle::set_covariances(const double* cov) {
+    if (cov) mvCov.assign(cov, cov + 9 * (size_t)N);
+    else mvCov.clear();
 }
 
 void MLPnPOracle::compute_pose_public(const int* idx, int n, double R[9], double t[3]) {

@@ -40,6 +40,9 @@ public:
     int min_inliers() const { return mRansacMinInliers; }
     int best_inliers() const { return mnBestInliers; }
 
+    // computePose's covMats (MLPnPsolver.cpp:321): cov [N][9] row-major 3x3 per correspondence
+    // (compacted order), or null for the reference's own call (no covariance: use_cov = false).
+    void set_covariances(const double* cov);
     // computePose on correspondences idx[0..n) (hypothesis or any subset); R row-major, t.
     void compute_pose_public(const int* idx, int n, double R[9], double t[3]);
     // Per-hypothesis trace: sample indices, count, double pose.
@@ -61,6 +64,7 @@ private:
     std::vector<double> mvBearing; // [N][3]  ((u-cx)/fx, (v-cy)/fy, 1) in float, then double
     std::vector<double> mvP3Dw;    // [N][3]  float positions widened to double
     std::vector<int32_t> mvKeyPointIndices;
+    std::vector<double> mvCov;     // [N][9] or empty
 
     double mRi[3][3], mti[3];
     std::vector<uint8_t> mvbInliersi;

@@ -646,7 +646,11 @@ __global__ __launch_bounds__(64) void mlpnp_solve_kernel(const DevML* __restrict
         f[i][0] = b.x; f[i][1] = b.y; f[i][2] = 1.0;
     }
     double R[3][3], t[3];
-    mlpnp_compute_pose<NS>(pw, f, LaneMat{slab + lane, 64}, R, t);
+    if (P.cov) {  // covariances supplied: the covMats branch of computePose
+        mlpnp_compute_pose<NS>(pw, f, LaneMat{slab + lane, 64}, R, t, MlIndexedCov{P.cov, idx});
+    } else {
+        mlpnp_compute_pose<NS>(pw, f, LaneMat{slab + lane, 64}, R, t);
+    }
     const size_t rec = (size_t)(lp.out0 + h);
     double* out = poses + rec * 12;
     RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) out[3 * r + c] = R[r][c];

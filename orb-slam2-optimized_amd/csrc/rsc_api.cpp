@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -240,11 +241,13 @@ struct rsc_mlpnp {
     float4* d_pts = nullptr;
     float2* d_uv = nullptr;
     float2* d_brg = nullptr;
+    double* d_cov = nullptr;  // [N][9] when covariances were set
+    bool use_cov = false;
     uint64_t* d_best = nullptr;
     int words = 0;
     int spec_out0 = -1, spec_H = 0;
     ~rsc_mlpnp() {
-        for (void* p : {(void*)d_pts, (void*)d_uv, (void*)d_brg, (void*)d_best})
+        for (void* p : {(void*)d_pts, (void*)d_uv, (void*)d_brg, (void*)d_cov, (void*)d_best})
             if (p) (void)hipFree(p);
     }
 };
@@ -685,7 +688,7 @@ struct HipMLBackend : MLBackend {
             solvers[i] = p;
             S[i]->rng.ensure(C->table, H[i] * S[i]->mRansacMinSet);
             DevML& d = probs[i];
-            d.pts = p->d_pts; d.uv = p->d_uv; d.brg = p->d_brg; d.n = S[i]->N;
+            d.pts = p->d_pts; d.uv = p->d_uv; d.brg = p->d_brg; d.cov = p->use_cov ? p->d_cov : nullptr; d.n = S[i]->N;
             d.fx = p->fx; d.fy = p->fy; d.cx = p->cx; d.cy = p->cy; d.th2 = S[i]->th2;
             LaunchProb& lp = lps[i];
             lp.prob = i;
@@ -2253,6 +2256,23 @@ int rsc_mlpnp_create(rsc_context* C, const rsc_pnp_problem* pb, uint32_t seed, r
 }
 
 void rsc_mlpnp_destroy(rsc_mlpnp* s) { delete s; }
+
+int rsc_mlpnp_set_covariances(rsc_mlpnp* s, const double* cov) {
+    if (!s) return RSC_ERR_ARG;
+    if (!cov) {
+        s->use_cov = false;
+        return RSC_OK;
+    }
+    const int n = s->st.N;
+    for (size_t k = 0; k < 9 * (size_t)n; ++k)
+        if (!std::isfinite(cov[k])) return RSC_ERR_ARG;
+    RSC_HIP(hipSetDevice(s->ctx->device));
+    if (!s->d_cov && n > 0) RSC_HIP(hipMalloc(&s->d_cov, 9 * sizeof(double) * (size_t)n));
+    RSC_HIP(hipStreamSynchronize(s->ctx->stream));
+    if (n > 0) RSC_HIP(hipMemcpy(s->d_cov, cov, 9 * sizeof(double) * (size_t)n, hipMemcpyHostToDevice));
+    s->use_cov = n > 0;
+    return RSC_OK;
+}
 
 int rsc_mlpnp_set_ransac_parameters(rsc_mlpnp* s, double probability, int min_inliers, int max_iterations,
                                     int min_set, float epsilon, float th2) {

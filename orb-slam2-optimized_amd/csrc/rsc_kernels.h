@@ -32,6 +32,7 @@ struct DevML {
     const float4* pts;  // [n] x, y, z (mvP3Dw), w = sigma^2
     const float2* uv;   // [n] mvP2D
     const float2* brg;  // [n] bearing x, y (z = 1), float arithmetic of MLPnPsolver.cpp:32-33
+    const double* cov;  // [n][9] bearing-vector covariances (computePose's covMats), or null
     int n;
     float fx, fy, cx, cy;  // float members (MLPnPsolver.hpp:198)
     float th2;

@@ -544,13 +544,52 @@ RSC_HD void ml_ldlt_solve6(const MlView& L, const double (&g)[6], double (&x)[6]
     RSC_UNROLL for (int i = 0; i < 6; ++i) x[i] = y[i];
 }
 
+// Bearing-vector covariances of computePose's covMats argument (MLPnPsolver.cpp:321, :375-388):
+// cov(i, k) = entry k (row-major) of correspondence i's 3x3 covariance.  MlNoCov: the reference's
+// call (covMats of size 1 != n, so use_cov = false).
+struct MlNoCov {
+    static constexpr bool on = false;
+    RSC_HD double operator()(int, int) const { return 0.0; }
+};
+
+// Covariances of the sampled correspondences idx[i] in a [n][9] table.
+struct MlIndexedCov {
+    static constexpr bool on = true;
+    const double* c;
+    const int* idx;
+    RSC_HD double operator()(int i, int k) const { return c[(size_t)idx[i] * 9 + k]; }
+};
+
+// The 2x2 weight of correspondence i: (N^T Sigma N)^-1 (:380-386; Matrix2d::inverse =
+// adjugate / determinant).  P[0] = P(0,0), P[1] = P(0,1), P[2] = P(1,0), P[3] = P(1,1).
+template <class Cov>
+RSC_HD void ml_cov_weight(const double (&N)[3][2], const Cov& cov, int i, double (&P)[4]) {
+    double NtS[2][3];
+    RSC_UNROLL for (int s = 0; s < 2; ++s)
+        RSC_UNROLL for (int c = 0; c < 3; ++c)
+            NtS[s][c] = (N[0][s] * cov(i, c) + N[1][s] * cov(i, 3 + c)) + N[2][s] * cov(i, 6 + c);
+    double T[2][2];
+    RSC_UNROLL for (int s = 0; s < 2; ++s)
+        RSC_UNROLL for (int q = 0; q < 2; ++q) T[s][q] = (NtS[s][0] * N[0][q] + NtS[s][1] * N[1][q]) + NtS[s][2] * N[2][q];
+    const double invdet = 1.0 / (T[0][0] * T[1][1] - T[1][0] * T[0][1]);
+    P[0] = T[1][1] * invdet;
+    P[1] = -T[0][1] * invdet;
+    P[2] = -T[1][0] * invdet;
+    P[3] = T[0][0] * invdet;
+}
+
 // MLPnPsolver::computePose for NS correspondences (pts world, f bearings), result R (row-major), t.
-// S: the lane slab (kMlSlabDoubles doubles, element stride S.stride).
-template <int NS>
+// S: the lane slab (kMlSlabDoubles doubles, element stride S.stride).  With covariances (Cov::on)
+// the normal equations are A^T P A and the Gauss-Newton system J^T Kll J, J^T Kll r (:483-484,
+// :694-695), P = Kll block-diagonal with the 2x2 weights above; each product restated as
+// (A^T P) first, then the row sums in order.
+template <int NS, class Cov = MlNoCov>
 RSC_HD void mlpnp_compute_pose(const double (&pw)[NS][3], const double (&f)[NS][3], const LaneMat& slab,
-                               double (&Rout)[3][3], double (&tout)[3]) {
+                               double (&Rout)[3][3], double (&tout)[3], const Cov& cov = Cov()) {
     double Ns[NS][3][2];
     RSC_UNROLL for (int i = 0; i < NS; ++i) ml_bearing_nullspace(f[i], Ns[i]);
+    double Pw[Cov::on ? NS : 1][4];
+    if constexpr (Cov::on) RSC_UNROLL for (int i = 0; i < NS; ++i) ml_cov_weight(Ns[i], cov, i, Pw[i]);
     double PPt[3][3];
     RSC_UNROLL for (int a = 0; a < 3; ++a)
         RSC_UNROLL for (int b = 0; b < 3; ++b) {
@@ -593,19 +632,37 @@ RSC_HD void mlpnp_compute_pose(const double (&pw)[NS][3], const double (&f)[NS][
             case 9: return n0; case 10: return n1; default: return n2;
         }
     };
-    RSC_UNROLL for (int a = 0; a < 12; ++a)
-        RSC_UNROLL for (int b = 0; b <= a; ++b) {
-            if (a < colsA) {
-                double s = Aent(0, 0, a) * Aent(0, 0, b);
-                s = s + Aent(0, 1, a) * Aent(0, 1, b);
-                RSC_UNROLL for (int i = 1; i < NS; ++i) {
-                    s = s + Aent(i, 0, a) * Aent(i, 0, b);
-                    s = s + Aent(i, 1, a) * Aent(i, 1, b);
+    if constexpr (Cov::on) {
+        // (A^T P)(a, 2i + q) = A(2i, a) P_i(0, q) + A(2i + 1, a) P_i(1, q); both triangles (P_i
+        // need not be exactly symmetric)
+        auto AtP = [&](int a, int i, int q) { return Aent(i, 0, a) * Pw[i][q] + Aent(i, 1, a) * Pw[i][2 + q]; };
+        RSC_UNROLL for (int a = 0; a < 12; ++a)
+            RSC_UNROLL for (int b = 0; b < 12; ++b) {
+                if (a < colsA && b < colsA) {
+                    double s = AtP(a, 0, 0) * Aent(0, 0, b);
+                    s = s + AtP(a, 0, 1) * Aent(0, 1, b);
+                    RSC_UNROLL for (int i = 1; i < NS; ++i) {
+                        s = s + AtP(a, i, 0) * Aent(i, 0, b);
+                        s = s + AtP(a, i, 1) * Aent(i, 1, b);
+                    }
+                    W.at(a, b) = s;
                 }
-                W.at(a, b) = s;
-                W.at(b, a) = s;
             }
-        }
+    } else {
+        RSC_UNROLL for (int a = 0; a < 12; ++a)
+            RSC_UNROLL for (int b = 0; b <= a; ++b) {
+                if (a < colsA) {
+                    double s = Aent(0, 0, a) * Aent(0, 0, b);
+                    s = s + Aent(0, 1, a) * Aent(0, 1, b);
+                    RSC_UNROLL for (int i = 1; i < NS; ++i) {
+                        s = s + Aent(i, 0, a) * Aent(i, 0, b);
+                        s = s + Aent(i, 1, a) * Aent(i, 1, b);
+                    }
+                    W.at(a, b) = s;
+                    W.at(b, a) = s;
+                }
+            }
+    }
     double r1[12];
     ml_jacobi_svd_lds(W, V, colsA, r1);
 
@@ -691,7 +748,7 @@ RSC_HD void mlpnp_compute_pose(const double (&pw)[NS][3], const double (&f)[NS][
             RSC_UNROLL for (int c = 0; c < 3; ++c) R[r][c] = Ti[0][r][c];
         }
     }
-    // Gauss-Newton (mlpnp_gn, use_cov = false); J rows in the W region, A = J^T J in the V region
+    // Gauss-Newton (mlpnp_gn); J rows in the W region, A = J^T J (or J^T Kll J) in the V region
     double x[6];
     {
         double w3[3];
@@ -726,15 +783,33 @@ RSC_HD void mlpnp_compute_pose(const double (&pw)[NS][3], const double (&f)[NS][
             }
         }
         double g[6];
-        RSC_UNROLL for (int a = 0; a < 6; ++a) {
-            RSC_UNROLL for (int b = 0; b < 6; ++b) {
-                double s = Jv.e(a) * Jv.e(b);
-                RSC_UNROLL for (int q = 1; q < 2 * NS; ++q) s = s + Jv.e(q * 6 + a) * Jv.e(q * 6 + b);
-                Av.at(a, b) = s;
+        if constexpr (Cov::on) {
+            // JacTSKll = J^T Kll: (k, 2i + q) = J(2i, k) P_i(0, q) + J(2i + 1, k) P_i(1, q)
+            RSC_UNROLL for (int a = 0; a < 6; ++a) {
+                double jk[2 * NS];
+                RSC_UNROLL for (int i = 0; i < NS; ++i)
+                    RSC_UNROLL for (int q = 0; q < 2; ++q)
+                        jk[2 * i + q] = Jv.e((2 * i) * 6 + a) * Pw[i][q] + Jv.e((2 * i + 1) * 6 + a) * Pw[i][2 + q];
+                RSC_UNROLL for (int b = 0; b < 6; ++b) {
+                    double s = jk[0] * Jv.e(b);
+                    RSC_UNROLL for (int q = 1; q < 2 * NS; ++q) s = s + jk[q] * Jv.e(q * 6 + b);
+                    Av.at(a, b) = s;
+                }
+                double s = jk[0] * rr[0];
+                RSC_UNROLL for (int q = 1; q < 2 * NS; ++q) s = s + jk[q] * rr[q];
+                g[a] = s;
             }
-            double s = Jv.e(a) * rr[0];
-            RSC_UNROLL for (int q = 1; q < 2 * NS; ++q) s = s + Jv.e(q * 6 + a) * rr[q];
-            g[a] = s;
+        } else {
+            RSC_UNROLL for (int a = 0; a < 6; ++a) {
+                RSC_UNROLL for (int b = 0; b < 6; ++b) {
+                    double s = Jv.e(a) * Jv.e(b);
+                    RSC_UNROLL for (int q = 1; q < 2 * NS; ++q) s = s + Jv.e(q * 6 + a) * Jv.e(q * 6 + b);
+                    Av.at(a, b) = s;
+                }
+                double s = Jv.e(a) * rr[0];
+                RSC_UNROLL for (int q = 1; q < 2 * NS; ++q) s = s + Jv.e(q * 6 + a) * rr[q];
+                g[a] = s;
+            }
         }
         double dx[6];
         ml_ldlt_solve6(Av, g, dx);

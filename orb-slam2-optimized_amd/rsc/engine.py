@@ -37,7 +37,7 @@ EXPORTED = [
     "rsc_sim3_iterate_many", "rsc_sim3_reset", "rsc_sim3_get_state", "rsc_sim3_prepared", "rsc_rand_stream",
     "rsc_pnp_reset_many", "rsc_pnp_set_ransac_parameters_many", "rsc_sim3_reset_many",
     "rsc_sim3_set_ransac_parameters_many",
-    "rsc_mlpnp_create", "rsc_mlpnp_destroy", "rsc_mlpnp_set_ransac_parameters",
+    "rsc_mlpnp_create", "rsc_mlpnp_destroy", "rsc_mlpnp_set_covariances", "rsc_mlpnp_set_ransac_parameters",
     "rsc_mlpnp_set_ransac_parameters_many", "rsc_mlpnp_iterate", "rsc_mlpnp_iterate_many", "rsc_mlpnp_reset",
     "rsc_mlpnp_reset_many", "rsc_mlpnp_get_state", "rsc_mlpnp_last_poses", "rsc_mlpnp_last_samples",
     "rsc_reloc_events", "rsc_loop_events", "rsc_pose_optimization_many",
@@ -334,6 +334,7 @@ def load_library(path: str = LIB_PATH):
     f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
     L.rsc_mlpnp_create.argtypes = [vp, C.POINTER(PnPProblem), C.c_uint32, C.POINTER(vp)]
     L.rsc_mlpnp_destroy.argtypes = [vp]
+    L.rsc_mlpnp_set_covariances.argtypes = [vp, C.POINTER(C.c_double)]
     L.rsc_mlpnp_set_ransac_parameters.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
     L.rsc_mlpnp_set_ransac_parameters_many.argtypes = [C.POINTER(vp), C.c_int, C.c_double, C.c_int, C.c_int,
                                                        C.c_int, C.c_float, C.c_float]
@@ -666,6 +667,15 @@ class MLPnPSolver:
 
     def __del__(self):
         self.close()
+
+    def set_covariances(self, cov):
+        """computePose's covMats: [n, 3, 3] bearing-vector covariances (None: the reference's path)."""
+        if cov is None:
+            _check(load_library().rsc_mlpnp_set_covariances(self.h, None), "rsc_mlpnp_set_covariances")
+            return
+        self._cov = np.ascontiguousarray(np.asarray(cov, np.float64).reshape(self.n, 9))
+        _check(load_library().rsc_mlpnp_set_covariances(self.h, self._cov.ctypes.data_as(C.POINTER(C.c_double))),
+               "rsc_mlpnp_set_covariances")
 
     def set_ransac_parameters(self, probability=0.99, min_inliers=8, max_iterations=300, min_set=6, epsilon=0.4,
                               th2=5.991):

@@ -283,7 +283,7 @@ void he_pnp_state(void* h, int32_t* out) {
 
 template <int NS>
 static void mlpnp_hyp(const uint32_t* window, int g0, int h, int n, const float* pts4, const float* brg2,
-                      int32_t* idx_out, double* R, double* t) {
+                      int32_t* idx_out, double* R, double* t, const double* cov = nullptr) {
     uint32_t w[31];
     std::memcpy(w, window, sizeof(w));
     uint32_t words[NS];
@@ -301,7 +301,11 @@ static void mlpnp_hyp(const uint32_t* window, int g0, int h, int n, const float*
     std::vector<double> slab(kMlSlabDoubles);
     LaneMat S{slab.data(), 1};
     double Rm[3][3], tv[3];
-    mlpnp_compute_pose<NS>(pw, f, S, Rm, tv);
+    if (cov) {
+        mlpnp_compute_pose<NS>(pw, f, S, Rm, tv, MlIndexedCov{cov, idx});
+    } else {
+        mlpnp_compute_pose<NS>(pw, f, S, Rm, tv);
+    }
     for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) R[3 * r + c] = Rm[r][c];
     for (int r = 0; r < 3; ++r) t[r] = tv[r];
 }
@@ -317,6 +321,17 @@ int he_mlpnp_hypothesis(int ns, const uint32_t* window, int g0, int h, int n, co
     }
     return -1;
 }
+// The same with per-correspondence bearing covariances cov [n][9] (computePose's covMats branch).
+int he_mlpnp_hypothesis_cov(int ns, const uint32_t* window, int g0, int h, int n, const float* pts4,
+                            const float* brg2, const double* cov, int32_t* idx, double* R, double* t) {
+    switch (ns) {
+        case 6: mlpnp_hyp<6>(window, g0, h, n, pts4, brg2, idx, R, t, cov); return 0;
+        case 7: mlpnp_hyp<7>(window, g0, h, n, pts4, brg2, idx, R, t, cov); return 0;
+        case 8: mlpnp_hyp<8>(window, g0, h, n, pts4, brg2, idx, R, t, cov); return 0;
+    }
+    return -1;
+}
+
 int he_mlpnp_count(const double* R, const double* t, const float* K, float th2, int n, const float* pts4,
                    const float* uv2, uint8_t* mask) {
     double Rr[9], tt[3];

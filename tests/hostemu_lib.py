@@ -30,6 +30,8 @@ def lib():
         L.he_pnp_rows.restype = C.c_double
         L.he_pnp_rows.argtypes = [C.c_int, C.c_int, f64p, f64p, f64p, f32p, f32p, f32p]
         L.he_mlpnp_hypothesis.argtypes = [C.c_int, u32p, C.c_int, C.c_int, C.c_int, f32p, f32p, i32p, f64p, f64p]
+        L.he_mlpnp_hypothesis_cov.argtypes = [C.c_int, u32p, C.c_int, C.c_int, C.c_int, f32p, f32p, f64p, i32p,
+                                              f64p, f64p]
         L.he_mlpnp_count.argtypes = [f64p, f64p, f32p, C.c_float, C.c_int, f32p, f32p, u8p]
         L.he_sim3_hypothesis.argtypes = [u32p, C.c_int, C.c_int, C.c_int, f32p, f32p, i32p, f32p]
         L.he_sim3_count.argtypes = [f32p, f32p, f32p, C.c_int, f32p, f32p, f32p, f32p, u64p, u64p, u8p]
@@ -89,13 +91,17 @@ def bearings(scene):
     return np.ascontiguousarray(np.stack([(p[:, 0] - cx) / fx, (p[:, 1] - cy) / fy], 1).astype(np.float32))
 
 
-def mlpnp_hypothesis(scene, seed, h, ns=6):
+def mlpnp_hypothesis(scene, seed, h, ns=6, cov=None):
     w, g0 = window(seed)
     pts4, _ = pack_pts(scene)
     idx = np.zeros(8, np.int32)
     R = np.zeros(9)
     t = np.zeros(3)
-    lib().he_mlpnp_hypothesis(ns, w, g0, h, scene.n, pts4, bearings(scene), idx, R, t)
+    if cov is None:
+        lib().he_mlpnp_hypothesis(ns, w, g0, h, scene.n, pts4, bearings(scene), idx, R, t)
+    else:
+        c = np.ascontiguousarray(np.asarray(cov, np.float64).reshape(-1, 9))
+        lib().he_mlpnp_hypothesis_cov(ns, w, g0, h, scene.n, pts4, bearings(scene), c, idx, R, t)
     return idx[:ns], R.reshape(3, 3), t
 
 

@@ -92,6 +92,7 @@ def lib():
     L.ora_mlpnp_create.argtypes = [C.c_int, C.c_int, f32p, f32p, f32p, i32p, C.c_float, C.c_float, C.c_float,
                                    C.c_float, C.c_uint32]
     L.ora_mlpnp_destroy.argtypes = [vp]
+    L.ora_mlpnp_set_cov.argtypes = [vp, C.c_void_p]
     L.ora_mlpnp_set_params.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
     L.ora_mlpnp_iterate.argtypes = [vp, C.c_int, C.POINTER(C.c_int), u8p, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     f32p]
@@ -323,6 +324,14 @@ class OracleMLPnP:
         if getattr(self, "h", None):
             lib().ora_mlpnp_destroy(self.h)
             self.h = None
+
+    def set_covariances(self, cov):
+        """computePose's covMats ([n, 3, 3]) or None."""
+        if cov is None:
+            lib().ora_mlpnp_set_cov(self.h, None)
+            return
+        self._cov = np.ascontiguousarray(np.asarray(cov, np.float64).reshape(-1, 9))
+        lib().ora_mlpnp_set_cov(self.h, self._cov.ctypes.data)
 
     def set_ransac_parameters(self, probability=0.99, min_inliers=8, max_iterations=300, min_set=6, epsilon=0.4,
                               th2=5.991):

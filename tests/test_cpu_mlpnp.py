@@ -101,3 +101,57 @@ def test_device_numerics_planar_bitexact():
         assert idx.tolist() == ints[h, :6].tolist()
         assert np.array_equal(Rh.ravel().view(np.uint64), dbl[h, :9].view(np.uint64)), h
         assert np.array_equal(th.view(np.uint64), dbl[h, 9:].view(np.uint64)), h
+
+
+def bearing_covariances(sc, extra=1e-9):
+    """computePose covMats for the config-4 'with covariances' case: the keypoint's isotropic pixel
+    variance (mvLevelSigma2) pushed through the bearing map ((u - cx) / fx, (v - cy) / fy, 1), plus
+    a tiny isotropic term; [n, 3, 3]."""
+    s2 = np.asarray(sc.sigma2, np.float64)
+    cov = np.zeros((sc.n, 3, 3))
+    cov[:, 0, 0] = s2 / float(sc.fx) ** 2
+    cov[:, 1, 1] = s2 / float(sc.fy) ** 2
+    cov += np.eye(3) * extra
+    return cov
+
+
+@pytest.mark.parametrize("ns", [6, 7, 8])
+def test_covariance_branch_bitexact_vs_oracle(ns):
+    """computePose's covMats branch (MLPnPsolver.cpp:375-388, :483-484, :694-695; dead in the
+    reference's own calls, parity unpinned): the device numerics (host-compiled) against the
+    oracle's restatement, per hypothesis."""
+    rng = np.random.default_rng(40 + ns)
+    sc = synth.make_pnp_scene(rng, 400, 0.6)
+    cov = bearing_covariances(sc)
+    o = ol.OracleMLPnP(sc, 5)
+    o.set_covariances(cov)
+    o.set_ransac_parameters(0.99, 10, 300, ns, 0.5, 5.991)
+    o.enable_trace()
+    o.iterate(40)
+    ints, dbl = o.trace()
+    assert len(ints) >= 10  # iterate returns early once a hypothesis refines
+    for h in range(len(ints)):
+        idx, R, t = he.mlpnp_hypothesis(sc, 5, h, ns, cov=cov)
+        assert idx.tolist() == ints[h, :ns].tolist(), h
+        assert np.array_equal(R.ravel().view(np.uint64), dbl[h, :9].view(np.uint64)), h
+        assert np.array_equal(t.view(np.uint64), dbl[h, 9:].view(np.uint64)), h
+
+
+def test_covariance_branch_known_answer_and_difference():
+    """Noise-free correspondences: the weighted solution is exact; on noisy ones it differs from the
+    unweighted one (the branch is live), and both recover the pose."""
+    rng = np.random.default_rng(44)
+    sc = synth.make_pnp_scene(rng, 80, 1.0, noise=False)
+    o = ol.OracleMLPnP(sc, 1)
+    o.set_covariances(bearing_covariances(sc))
+    for n in (6, 12, 80):
+        R, t = o.compute_pose(np.arange(n))
+        assert np.abs(R - sc.R_true).max() < 2e-6 and np.abs(t - sc.t_true).max() < 2e-5, n
+    sc2 = synth.make_pnp_scene(rng, 80, 1.0)
+    a, b = ol.OracleMLPnP(sc2, 1), ol.OracleMLPnP(sc2, 1)
+    b.set_covariances(bearing_covariances(sc2))
+    Ra, ta = a.compute_pose(np.arange(80))
+    Rb, tb = b.compute_pose(np.arange(80))
+    assert not np.array_equal(Ra, Rb)
+    for R in (Ra, Rb):
+        assert np.abs(R - sc2.R_true).max() < 2e-2

@@ -77,3 +77,37 @@ def test_min_set_out_of_range_is_rejected():
     g = engine.MLPnPSolver(ctx(), synth.make_pnp_scene(rng, 100, 0.5), 1)
     with pytest.raises(RuntimeError):
         g.set_ransac_parameters(0.99, 10, 300, 5, 0.5, 5.991)
+
+
+@pytest.mark.parametrize("ns", [6, 8])
+def test_covariance_branch_bitexact(ns):
+    """computePose's covMats branch (config 4 'with bearing-vector covariances'; never reached by
+    the reference's own calls, parity against the reference unpinned): per-hypothesis double poses
+    and iterate() results bit-exact against the oracle's restatement, and switching the
+    covariances off restores the reference path."""
+    from test_cpu_mlpnp import bearing_covariances
+    rng = np.random.default_rng(60 + ns)
+    sc = synth.make_pnp_scene(rng, 700, 0.4)
+    params = (0.99, 10, 300, ns, 0.5, 5.991)
+    g, o = make(sc, 13, params)
+    cov = bearing_covariances(sc)
+    g.set_covariances(cov)
+    o.set_covariances(cov)
+    o.enable_trace()
+    assert_ml_equal(g.iterate(60), o.iterate(60), "cov exhaustive")
+    smp, pos = g.last_hypotheses()
+    ints, dbl = o.trace()
+    assert len(smp) == len(ints) == 60
+    assert np.array_equal(smp[:, :ns], ints[:, :ns])
+    assert np.array_equal(pos.view(np.uint64), dbl.view(np.uint64))
+    sc2 = synth.make_pnp_scene(rng, 600, 0.65)
+    g2, o2 = make(sc2, 14, params)
+    cov2 = bearing_covariances(sc2)
+    g2.set_covariances(cov2)
+    o2.set_covariances(cov2)
+    for k in range(4):
+        assert_ml_equal(g2.iterate(5), o2.iterate(5), f"cov call {k}")
+    g2.set_covariances(None)
+    o2.set_covariances(None)
+    for k in range(3):
+        assert_ml_equal(g2.iterate(5), o2.iterate(5), f"no-cov call {k}")
