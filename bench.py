@@ -327,12 +327,26 @@ def cpu_baseline_sim3(solvers, args, threads):
                        threads)
 
 
-def run_mlpnp(engine, ctx, scenes, args):
+def mlpnp_covariances(sc):
+    """Bearing-vector covariances for config 4's covariance variant: the keypoint's pixel variance
+    (mvLevelSigma2) through the bearing map ((u - cx) / fx, (v - cy) / fy, 1) + a tiny isotropic term."""
+    s2 = np.asarray(sc.sigma2, np.float64)
+    cov = np.zeros((sc.n, 3, 3))
+    cov[:, 0, 0] = s2 / float(sc.fx) ** 2
+    cov[:, 1, 1] = s2 / float(sc.fy) ** 2
+    return cov + np.eye(3) * 1e-9
+
+
+def run_mlpnp(engine, ctx, scenes, args, with_cov=False):
     """Config 4 on one GPU: 32 candidates x 4096 correspondences (128 over 4 GPUs), MLPnP
     SetRansacParameters(0.99,10,300,6,0.5,5.991) (commented call Tracking.cpp:1227-1228),
-    iterate(300), exhaustive."""
+    iterate(300), exhaustive; with_cov: computePose's bearing-covariance branch (covMats given)."""
     from rsc import workloads as wl
-    batch = engine.SolverBatch([engine.MLPnPSolver(ctx, sc, 1) for sc in scenes])
+    solvers = [engine.MLPnPSolver(ctx, sc, 1) for sc in scenes]
+    if with_cov:
+        for g, sc in zip(solvers, scenes):
+            g.set_covariances(mlpnp_covariances(sc))
+    batch = engine.SolverBatch(solvers)
     C = len(scenes)
 
     def step(s):
@@ -932,6 +946,7 @@ def main():
             sc4 = wl.config4_scenes()
             m = run_mlpnp(engine, ctx, sc4, args)
             sections["mlpnp"] = _rounded(m, 3)
+            sections["mlpnp"]["with_covariances"] = _rounded(run_mlpnp(engine, ctx, sc4, args, with_cov=True), 3)
             if with_cpu:
                 cb = cpu_baseline_mlpnp(sc4, args, threads)
                 sections["mlpnp"]["cpu_baseline"] = cb
