@@ -95,33 +95,35 @@ struct PinBuf {
 // count) so a problem's workgroups share one L2.  Placement only: results do not depend on it.
 template <class T, class Prob>
 void xcd_order(std::vector<T>& wgs, Prob prob_of) {
+    // O(n), no allocation once the scratch has grown (this runs inside every speculation round)
     constexpr int X = 8;
-    if (wgs.size() <= (size_t)X) return;
-    std::vector<std::vector<T>> byp;
-    std::vector<int> pid;  // problem id -> index in byp
-    for (const T& w : wgs) {
-        const int p = prob_of(w);
-        if (p >= (int)pid.size()) pid.resize(p + 1, -1);
-        if (pid[p] < 0) { pid[p] = (int)byp.size(); byp.emplace_back(); }
-        byp[pid[p]].push_back(w);
-    }
-    std::vector<int> order(byp.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return byp[a].size() > byp[b].size(); });
-    std::vector<std::vector<T>> bin(X);
-    for (int i : order) {
+    const size_t n = wgs.size();
+    if (n <= (size_t)X) return;
+    thread_local std::vector<T> src;
+    thread_local std::vector<size_t> rb;  // run r = entries [rb[r], rb[r + 1]) of one problem
+    thread_local std::vector<int> runs[X];
+    src.assign(wgs.begin(), wgs.end());
+    rb.clear();
+    for (size_t i = 0; i < n; ++i)
+        if (i == 0 || prob_of(src[i]) != prob_of(src[i - 1])) rb.push_back(i);
+    rb.push_back(n);
+    size_t left[X] = {};
+    for (int x = 0; x < X; ++x) runs[x].clear();
+    for (size_t r = 0; r + 1 < rb.size(); ++r) {  // each problem to the least loaded residue
         int best = 0;
-        for (int x = 1; x < X; ++x) if (bin[x].size() < bin[best].size()) best = x;
-        bin[best].insert(bin[best].end(), byp[i].begin(), byp[i].end());
+        for (int x = 1; x < X; ++x) if (left[x] < left[best]) best = x;
+        runs[best].push_back((int)r);
+        left[best] += rb[r + 1] - rb[r];
     }
-    std::vector<size_t> next(X, 0);
-    for (size_t b = 0; b < wgs.size(); ++b) {
+    size_t cr[X] = {}, cp[X] = {};
+    for (size_t b = 0; b < n; ++b) {
         int x = (int)(b % X);
-        if (next[x] == bin[x].size()) {  // this residue's bin is drained: take from the fullest
-            for (int y = 0; y < X; ++y)
-                if (bin[y].size() - next[y] > bin[x].size() - next[x]) x = y;
-        }
-        wgs[b] = bin[x][next[x]++];
+        if (!left[x])  // this residue's problems are dealt: take from the one with most left
+            for (int y = 0; y < X; ++y) if (left[y] > left[x]) x = y;
+        const int r = runs[x][cr[x]];
+        wgs[b] = src[rb[r] + cp[x]];
+        if (++cp[x] == rb[r + 1] - rb[r]) { cp[x] = 0; ++cr[x]; }
+        --left[x];
     }
 }
 
