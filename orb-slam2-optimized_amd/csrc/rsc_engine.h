@@ -211,7 +211,7 @@ inline int pnp_iterate_many(PnPBackend& be, PnPState* const* S, int count, const
             int h = std::min(loop_len(i), kMaxSpeculate);
             if (h > 0) { spec.push_back(S[i]); H.push_back(h); who.push_back(i); }
         }
-        std::vector<std::vector<int32_t>> counts;
+        thread_local std::vector<std::vector<int32_t>> counts;  // capacity kept across rounds
         if (!spec.empty()) {
             int st = be.speculate(spec.data(), (int)spec.size(), H.data(), counts);
             if (st) return st;
@@ -553,7 +553,7 @@ inline int mlpnp_iterate_many(MLBackend& be, MLState* const* S, int count, const
             if (h > 0) { spec.push_back(S[i]); H.push_back(h); who.push_back(i); }
         }
         if (spec.empty()) break;
-        std::vector<std::vector<int32_t>> counts;
+        thread_local std::vector<std::vector<int32_t>> counts;  // capacity kept across rounds
         if (int st = be.speculate(spec.data(), (int)spec.size(), H.data(), counts)) return st;
         std::vector<int> pj, pk, pi;
         for (size_t j = 0; j < spec.size(); ++j) {
