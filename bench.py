@@ -97,17 +97,23 @@ def launch_ranks(args) -> int:
 
 
 COLL_DEV = "cuda"  # device of the collective tensors: cuda for RCCL, cpu for gloo
+RESULT_OUT = sys.stdout  # where rank 0 prints the one JSON line
 
 
 def dist_setup(args):
     """One process per GPU: rank r drives GPU LOCAL_RANK.  With --dist-backend gloo the ranks may
-    share GPUs (device = LOCAL_RANK mod the visible count) and the collectives run on host tensors."""
-    global COLL_DEV
+    share GPUs (device = LOCAL_RANK mod the visible count) and the collectives run on host tensors.
+    For world > 1 the process's fd 1 is pointed at stderr (the collective libraries print
+    connection banners on stdout) and the JSON line goes to a saved copy of the original stdout."""
+    global COLL_DEV, RESULT_OUT
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
+        sys.stdout.flush()
+        RESULT_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         import torch
         import torch.distributed as dist
         if args.dist_backend == "nccl":
@@ -1051,7 +1057,7 @@ def main():
                                     "speedup_vs_cpu_1core": round(g / c, 1),
                                     "note": "sum of the config-2 and config-3 rates (same unit, each on its own batch)"}
     out.update(sections)
-    print(json.dumps(out))
+    print(json.dumps(out), file=RESULT_OUT, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

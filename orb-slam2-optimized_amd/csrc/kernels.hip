@@ -118,14 +118,16 @@ __global__ __launch_bounds__(64) void pnp_eig_lane_kernel(const DevPnP* __restri
 }
 
 template <int NS>
-__global__ __launch_bounds__(192, 2) void pnp_betas_kernel(const DevPnP* __restrict__ probs,
-                                                        const LaunchProb* __restrict__ lps,
-                                                        const int2* __restrict__ wg_table,
-                                                        const double* __restrict__ stage,
-                                                        const int32_t* __restrict__ samples,
-                                                        float* __restrict__ poses) {
-    __shared__ __attribute__((aligned(16))) double smem[kBetasSmemDoubles];
-    pnp_betas_body<NS>(probs, lps, wg_table, stage, samples, poses, smem);
+__global__ __launch_bounds__(64) void pnp_betas_kernel(const DevPnP* __restrict__ probs,
+                                                       const LaunchProb* __restrict__ lps,
+                                                       const int2* __restrict__ wg_table, int ngroups,
+                                                       const double* __restrict__ stage,
+                                                       const int32_t* __restrict__ samples,
+                                                       float* __restrict__ poses, double* __restrict__ berr,
+                                                       float* __restrict__ bpose, unsigned* __restrict__ bctr,
+                                                       size_t hcap) {
+    __shared__ __attribute__((aligned(16))) double smem[kBetasWaveSmemDoubles];
+    pnp_betas_wave_body<NS>(probs, lps, wg_table, ngroups, stage, samples, poses, berr, bpose, bctr, hcap, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -774,8 +776,8 @@ hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchPr
 
 hipError_t launch_pnp_solve_split(bool quad, int ns, int nwgE, const int2* wgtE, int nwg64, const int2* wgt64,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
-                                  float* poses, int32_t* samples, hipStream_t st, hipEvent_t eig_begin,
-                                  hipEvent_t eig_end) {
+                                  float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
+                                  hipEvent_t eig_begin, hipEvent_t eig_end) {
     if (ns < 4 || ns > 6) return hipErrorInvalidValue;
     if (eig_begin) (void)hipEventRecord(eig_begin, st);
     switch (ns) {
@@ -786,7 +788,8 @@ hipError_t launch_pnp_solve_split(bool quad, int ns, int nwgE, const int2* wgtE,
         else                                                                                          \
             pnp_eig_lane_kernel<N><<<nwg64, 64, 0, st>>>(probs, lps, wgt64, T, stage, samples);       \
         if (eig_end) (void)hipEventRecord(eig_end, st);                                               \
-        pnp_betas_kernel<N><<<nwg64, 192, 0, st>>>(probs, lps, wgt64, stage, samples, poses);         \
+        pnp_betas_kernel<N><<<3 * nwg64, 64, 0, st>>>(probs, lps, wgt64, nwg64, stage, samples, poses, \
+                                                      bs.err, bs.pose, bs.ctr, bs.hcap);              \
         break;
         RSC_CASE(4) RSC_CASE(5) RSC_CASE(6)
 #undef RSC_CASE

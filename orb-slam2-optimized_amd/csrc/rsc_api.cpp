@@ -156,6 +156,9 @@ struct rsc_context {
     DevBuf<uint64_t> d_masks;
     DevBuf<int32_t> d_samples;
     DevBuf<double> d_stage;  // quad path: per-hypothesis stage records between the two solve kernels
+    DevBuf<double> d_berr;   // pnp_betas_kernel hand-off: error per (approximation, record)
+    DevBuf<float> d_bpose;   //   float pose per (approximation, record)
+    DevBuf<unsigned> d_bctr; //   one arrival counter per 64-hypothesis group (zero between launches)
     DevBuf<float> d_gather;  // gathered pose records (+ their indices)
     DevBuf<double> d_mposes; // MLPnP hypothesis poses, double[12] per record
     DevBuf<char> d_desc;
@@ -391,8 +394,18 @@ struct HipPnPBackend : PnPBackend {
         if (int e = C->d_masks.ensure((size_t)total * mw)) return e;
         if (C->keep_samples || split)
             if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
-        if (split)
+        BetasScratch bs{};
+        if (split) {
             if (int e = C->d_stage.ensure((size_t)total * kStageDoubles)) return e;
+            if (int e = C->d_berr.ensure((size_t)total * 3)) return e;
+            if (int e = C->d_bpose.ensure((size_t)total * 36)) return e;
+            size_t groups = 0;
+            for (int g = 0; g < 3; ++g) groups = std::max(groups, solve_wgs[g].size());
+            const size_t had = C->d_bctr.cap;
+            if (int e = C->d_bctr.ensure(groups)) return e;
+            if (C->d_bctr.cap != had) RSC_HIP(hipMemsetAsync(C->d_bctr.p, 0, C->d_bctr.cap * sizeof(unsigned), C->stream));
+            bs = BetasScratch{C->d_berr.p, C->d_bpose.p, C->d_bctr.p, (size_t)total};
+        }
         const char* base = C->d_desc.p;
         const DevPnP* dprobs = reinterpret_cast<const DevPnP*>(base + o_probs);
         const LaunchProb* dlps = reinterpret_cast<const LaunchProb*>(base + o_lps);
@@ -417,7 +430,7 @@ struct HipPnPBackend : PnPBackend {
                                                   reinterpret_cast<const int2*>(base + o_quad[g]),
                                                   (int)solve_wgs[g].size(),
                                                   reinterpret_cast<const int2*>(base + o_solve[g]), dprobs, dlps,
-                                                  C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p,
+                                                  C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p, bs,
                                                   C->stream, eb, C->timing ? C->ev[7 + 2 * g] : nullptr));
                     first_group = false;
                 } else {

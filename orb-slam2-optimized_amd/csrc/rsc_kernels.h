@@ -83,10 +83,19 @@ constexpr int kAutoSolveMode = 2;      // see rsc_context::solve_mode
 constexpr int kStageDoubles = 48 + 24 + 12;
 // Two-kernel hypothesis solve: eigenvectors (quad-cooperative or lane per hypothesis), then the
 // three beta approximations (one wave each) + selection.
+// Hand-off buffers of pnp_betas_kernel: per record and approximation the error (`err[3][hcap]`)
+// and the float pose (`pose[3][12][hcap]`); one counter per 64-hypothesis group, zero between
+// launches (the kernel resets what it uses).
+struct BetasScratch {
+    double* err;
+    float* pose;
+    unsigned* ctr;
+    size_t hcap;
+};
 hipError_t launch_pnp_solve_split(bool quad, int ns, int nwgE, const int2* wgtE, int nwg64, const int2* wgt64,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
-                                  float* poses, int32_t* samples, hipStream_t st, hipEvent_t eig_begin = nullptr,
-                                  hipEvent_t eig_end = nullptr);
+                                  float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
+                                  hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr);
 hipError_t launch_pnp_solve_stamped(int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                                     const uint32_t* T, float* poses, uint64_t* stamps, hipStream_t st);
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,

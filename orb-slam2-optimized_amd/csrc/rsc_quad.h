@@ -9,8 +9,8 @@
 //   * implicit QR: the Givens chase is computed redundantly by the group (bitwise identical), each
 //     member applying the rotations to its own rows of Q;
 //   * the three beta approximations of PnPsolver.cpp:383-414 (+ Gauss-Newton + compute_R_and_t)
-//     run in a second kernel, one wave per approximation over 64 hypotheses, and the smallest
-//     error wins in the reference's order.
+//     run in a second kernel, one single-wave workgroup per (approximation, 64 hypotheses), and
+//     the smallest error wins in the reference's order.
 // The product runs pairs (L = 2, 20 hypotheses per wave: 960 waves for the 1,024 SIMDs on config
 // 2); the Refine kernel's single eigenproblem uses one quad.
 // Every scalar is produced by the same operations on the same operands as the sequential
@@ -28,8 +28,10 @@ constexpr int kQuadE = 55;   // Householder essential vectors
 constexpr int kQuadRegion = kQuadT + kQuadE + 1;  // 200 doubles per hypothesis
 // stage record offsets (rsc_kernels.h kStageDoubles)
 constexpr int kStEv = 0, kStAl = 48, kStCws = 72;
-// pnp_betas_kernel LDS: eigenvectors [48][64], L+rho [66][64], errors [3][64], poses [3][12][64] f32
+// pnp_betas_body LDS (three-wave form, tools/quad_bench): eigenvectors [48][64], L+rho [66][64],
+// errors [3][64], poses [3][12][64] f32.  pnp_betas_wave_body (product): L+rho [66][64] only.
 constexpr int kBetasSmemDoubles = (48 + 66) * 64 + 3 * 64 + 3 * 12 * 64 / 2;
+constexpr int kBetasWaveSmemDoubles = 66 * 64;
 
 // Offset of step i's essential Householder vector (entries v[1..10-i]) in the E region.
 RSC_HD constexpr int quad_eoff(int i) { return 10 * i - (i * (i - 1)) / 2; }
@@ -558,6 +560,124 @@ __device__ __forceinline__ void pnp_betas_body(const DevPnP* __restrict__ probs,
         if (ERR[128 + lane] < be) { be = ERR[128 + lane]; best = 2; }
         float* o = poses + rec * 12;
         RSC_UNROLL for (int k = 0; k < 12; ++k) o[k] = PZ[(best * 12 + k) * 64 + lane];
+    }
+}
+
+// Eigenvectors read from the stage record in global memory (stride 1), L + rho in LDS
+// (element-major across the wave).
+struct StageEvView {
+    const double* evp;
+    double* Lp;
+    RSC_HD double ev(int r, int c) const { return evp[r * 4 + c]; }
+    RSC_HD double& L(int i, int j) const { return Lp[(i * 10 + j) * 64]; }
+    RSC_HD double& rho(int i) const { return Lp[(60 + i) * 64]; }
+};
+
+// Block -> (64-hypothesis group, approximation) of pnp_betas_kernel: the three waves of a group are
+// blocks b, b+8, b+16 of a run of 24 (one L2: blocks b and b+8 share an XCD), so the group keeps
+// the XCD its wg_table slot was ordered for; the last (ngroups % 8) groups are dealt plainly.
+RSC_HD inline void betas_block(int b, int ngroups, int& g, int& apx) {
+    const int q = ngroups / 8;
+    if (b < 24 * q) {
+        g = (b % 8) + 8 * (b / 24);
+        apx = (b / 8) % 3;
+    } else {
+        const int r = ngroups - 8 * q, rem = b - 24 * q;
+        g = 8 * q + rem % r;
+        apx = rem / r;
+    }
+}
+
+// Kernel 2 (product form): ONE wave per (64 hypotheses, beta approximation), so config 2's 960
+// waves sit one per SIMD instead of 320 three-wave workgroups doubling up on 64 of the 256 CUs.
+// Wave apx runs compute_L_6x10 + find_betas_approx_{apx+1} + gauss_newton + compute_R_and_t
+// (PnPsolver.cpp:383-408) and leaves (error, float pose) in `berr` / `bpose`; the group's last wave
+// to finish (agent-scope counter) keeps the smallest error in the reference's order (:393-414) and
+// writes the pose.  Hand-off: producer stores -> vmcnt(0) -> agent release -> vmcnt(0) -> relaxed
+// agent add; the last adder: agent acquire -> vmcnt(0) -> loads (MI355X_MICROARCH.md, inter-
+// workgroup visibility).  It resets the counter, so every launch starts from zero.
+template <int NS>
+__device__ __forceinline__ void pnp_betas_wave_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
+                                                    const int2* __restrict__ wg_table, int ngroups,
+                                                    const double* __restrict__ stage,
+                                                    const int32_t* __restrict__ samples, float* __restrict__ poses,
+                                                    double* __restrict__ berr, float* __restrict__ bpose,
+                                                    unsigned* __restrict__ bctr, size_t hcap, double* smem) {
+    const int lane = threadIdx.x;
+    int g, apx;
+    betas_block(blockIdx.x, ngroups, g, apx);
+    const int2 wt = wg_table[g];
+    const LaunchProb& lp = lps[wt.x];
+    const bool active = wt.y + lane < lp.H;
+    const int h = active ? wt.y + lane : lp.H - 1;
+    const DevPnP& P = probs[lp.prob];
+    const size_t rec = (size_t)(lp.out0 + h);
+    const double* in = stage + rec * kStageDoubles;
+    const StageEvView V{in + kStEv, smem + lane};
+    compute_L_6x10(V);
+    {
+        double cws[4][3];
+        RSC_UNROLL for (int i = 0; i < 4; ++i)
+            RSC_UNROLL for (int c = 0; c < 3; ++c) cws[i][c] = in[kStCws + i * 3 + c];
+        auto d2 = [&](int a, int b) {
+            double x = cws[a][0] - cws[b][0], y = cws[a][1] - cws[b][1], z = cws[a][2] - cws[b][2];
+            return x * x + y * y + z * z;
+        };
+        V.rho(0) = d2(0, 1); V.rho(1) = d2(0, 2); V.rho(2) = d2(0, 3);
+        V.rho(3) = d2(1, 2); V.rho(4) = d2(1, 3); V.rho(5) = d2(2, 3);
+    }
+    double betas[4] = {0.0, 0.0, 0.0, 0.0};
+    if (apx == 0) find_betas<1>(V, betas);
+    else if (apx == 1) find_betas<2>(V, betas);
+    else find_betas<3>(V, betas);
+    gauss_newton(V, betas);
+    // the hypothesis' points and alphas are read only now (register pressure, see pnp_betas_body)
+    HypStore<NS> st;
+    RSC_UNROLL for (int i = 0; i < NS; ++i) {
+        const int id = samples[rec * 8 + i];
+        const float4 p = P.pts[id];
+        const float2 uv = P.uv[id];
+        st.pw_[i][0] = p.x; st.pw_[i][1] = p.y; st.pw_[i][2] = p.z;
+        st.u_[i][0] = uv.x; st.u_[i][1] = uv.y;
+        RSC_UNROLL for (int j = 0; j < 4; ++j) st.al_[i][j] = in[kStAl + i * 4 + j];
+    }
+    st.rows_ = P.rows;
+    st.spw = P.pws;
+    st.sal = P.als;
+    const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
+    const double pw0[3] = {in[kStCws + 0], in[kStCws + 1], in[kStCws + 2]};
+    double R[3][3], t[3];
+    const double err = compute_R_and_t(st, K, V, betas, pw0, R, t);
+    float pz[12];
+    RSC_UNROLL for (int r = 0; r < 3; ++r)
+        RSC_UNROLL for (int c = 0; c < 3; ++c) pz[3 * r + c] = (float)R[r][c];
+    RSC_UNROLL for (int r = 0; r < 3; ++r) pz[9 + r] = (float)t[r];
+    if (active) {
+        berr[apx * hcap + rec] = err;
+        RSC_UNROLL for (int k = 0; k < 12; ++k) bpose[(apx * 12 + k) * hcap + rec] = pz[k];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add(bctr + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __builtin_amdgcn_readlane(prev, 0);
+    if (prev != 2) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(bctr + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!active) return;
+    double e[3];
+    RSC_UNROLL for (int a = 0; a < 3; ++a) e[a] = (a == apx) ? err : berr[a * hcap + rec];
+    int best = 0;
+    double be = e[0];
+    if (e[1] < be) { be = e[1]; best = 1; }
+    if (e[2] < be) { be = e[2]; best = 2; }
+    float* o = poses + rec * 12;
+    if (best == apx) {
+        RSC_UNROLL for (int k = 0; k < 12; ++k) o[k] = pz[k];
+    } else {
+        RSC_UNROLL for (int k = 0; k < 12; ++k) o[k] = bpose[(best * 12 + k) * hcap + rec];
     }
 }
 
