@@ -99,9 +99,14 @@ void xcd_order(std::vector<T>& wgs, Prob prob_of) {
     constexpr int X = 8;
     const size_t n = wgs.size();
     if (n <= (size_t)X) return;
-    thread_local std::vector<T> src;
-    thread_local std::vector<size_t> rb;  // run r = entries [rb[r], rb[r + 1]) of one problem
-    thread_local std::vector<int> runs[X];
+    // thread_local scratch, addressed once (each access to a thread_local of a shared library is a
+    // __tls_get_addr call)
+    thread_local std::vector<T> src_tl;
+    thread_local std::vector<size_t> rb_tl;  // run r = entries [rb[r], rb[r + 1]) of one problem
+    thread_local std::vector<int> runs_tl[X];
+    std::vector<T>& src = src_tl;
+    std::vector<size_t>& rb = rb_tl;
+    std::vector<int>* runs = runs_tl;
     src.assign(wgs.begin(), wgs.end());
     rb.clear();
     for (size_t i = 0; i < n; ++i)
@@ -262,8 +267,15 @@ namespace {
 // ------------------------------------------------------------------------------------------------
 // Launch-descriptor packing: one pinned blob -> one H2D copy per launch round.
 // ------------------------------------------------------------------------------------------------
+// Descriptor staging of one round.  The byte vector is a per-thread scratch that keeps its capacity
+// across rounds (one Blob is alive at a time per thread), so a round allocates nothing here.
 struct Blob {
-    std::vector<char> bytes;
+    std::vector<char>& bytes;
+    Blob() : bytes(scratch()) { bytes.clear(); }
+    static std::vector<char>& scratch() {
+        thread_local std::vector<char> v;
+        return v;
+    }
     size_t add(const void* p, size_t n) {
         size_t off = (bytes.size() + 15) & ~(size_t)15;
         bytes.resize(off + n);
@@ -331,8 +343,13 @@ struct HipPnPBackend : PnPBackend {
     int speculate(PnPState* const* S, int count, const int* H, std::vector<std::vector<int32_t>>& counts) override {
         // group by min_set (template parameter of the solve kernel)
         int total = 0, maxN = 1;
-        std::vector<DevPnP> probs(count);
-        std::vector<LaunchProb> lps(count);
+        // per-thread scratch that keeps its capacity across rounds (no allocation per round)
+        thread_local std::vector<DevPnP> probs_tl;
+        thread_local std::vector<LaunchProb> lps_tl;
+        std::vector<DevPnP>& probs = probs_tl;
+        std::vector<LaunchProb>& lps = lps_tl;
+        probs.resize(count);
+        lps.resize(count);
         for (int i = 0; i < count; ++i) {
             rsc_pnp* p = of(S[i]);
             if (!p) return RSC_ERR_ARG;
@@ -362,23 +379,47 @@ struct HipPnPBackend : PnPBackend {
         const int mw = ppt * 4;
         C->mask_words = mw;
         // work tables
-        std::vector<std::vector<int2>> solve_wgs(3), quad_wgs(3);
-        std::vector<int4> scan_wgs;
+        thread_local std::vector<int2> solve_wgs_tl[3], quad_wgs_tl[3];
+        thread_local std::vector<int4> scan_wgs_tl;
+        std::vector<int2>* solve_wgs = solve_wgs_tl;
+        std::vector<int2>* quad_wgs = quad_wgs_tl;
+        std::vector<int4>& scan_wgs = scan_wgs_tl;
         const int HC = scan_chunk(total);  // hypotheses per scan workgroup
         const int mode = diag_stamps ? 1 : (C->solve_mode ? C->solve_mode : kAutoSolveMode);
         const bool quad = (mode == 2), split = (mode == 2 || mode == 3);
+        // The tables depend only on the round's shape (count, sample size and H per problem, HC,
+        // mode): a round with the shape of the previous one on this thread reuses them (building
+        // and XCD-ordering ~3.7k entries costs ~10 us of host time per config-2 round).
+        thread_local std::vector<int> shape_tl;
+        std::vector<int>& shape = shape_tl;
+        thread_local std::vector<int> key_tl;
+        std::vector<int>& key = key_tl;
+        key.clear();
+        key.push_back(count);
+        key.push_back(HC);
+        key.push_back(mode);
         for (int i = 0; i < count; ++i) {
-            const int g = S[i]->mRansacMinSet - 4;
-            for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs[g].push_back(make_int2(i, h0));
-            if (quad)
-                for (int h0 = 0; h0 < H[i]; h0 += kEigHyps) quad_wgs[g].push_back(make_int2(i, h0));
-            for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
+            key.push_back(S[i]->mRansacMinSet);
+            key.push_back(H[i]);
         }
-        for (int g = 0; g < 3; ++g) {
-            xcd_order(solve_wgs[g], [](const int2& w) { return w.x; });
-            xcd_order(quad_wgs[g], [](const int2& w) { return w.x; });
+        if (key != shape) {
+            for (int g = 0; g < 3; ++g) { solve_wgs[g].clear(); quad_wgs[g].clear(); }
+            scan_wgs.clear();
+            for (int i = 0; i < count; ++i) {
+                const int g = S[i]->mRansacMinSet - 4;
+                for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs[g].push_back(make_int2(i, h0));
+                if (quad)
+                    for (int h0 = 0; h0 < H[i]; h0 += kEigHyps) quad_wgs[g].push_back(make_int2(i, h0));
+                for (int h0 = 0; h0 < H[i]; h0 += HC)
+                    scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
+            }
+            for (int g = 0; g < 3; ++g) {
+                xcd_order(solve_wgs[g], [](const int2& w) { return w.x; });
+                xcd_order(quad_wgs[g], [](const int2& w) { return w.x; });
+            }
+            xcd_order(scan_wgs, [](const int4& w) { return w.x; });
+            shape.assign(key.begin(), key.end());
         }
-        xcd_order(scan_wgs, [](const int4& w) { return w.x; });
         Blob b;
         const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevPnP));
         const size_t o_lps = b.add(lps.data(), lps.size() * sizeof(LaunchProb));
@@ -468,7 +509,7 @@ struct HipPnPBackend : PnPBackend {
                 }
             }
         }
-        counts.assign(count, {});
+        counts.resize(count);  // keeps the inner vectors' capacity
         for (int i = 0; i < count; ++i)
             counts[i].assign(C->h_counts.p + lps[i].out0, C->h_counts.p + lps[i].out0 + H[i]);
         return 0;
@@ -637,7 +678,7 @@ struct HipSim3Backend : Sim3Backend {
             C->last_ms[3] += 1;
             C->last_ms[4] += total;
         }
-        counts.assign(count, {});
+        counts.resize(count);  // keeps the inner vectors' capacity
         for (int i = 0; i < count; ++i)
             counts[i].assign(C->h_counts.p + lps[i].out0, C->h_counts.p + lps[i].out0 + H[i]);
         return 0;
@@ -773,7 +814,7 @@ struct HipMLBackend : MLBackend {
             C->last_ms[3] += 1;
             C->last_ms[4] += total;
         }
-        counts.assign(count, {});
+        counts.resize(count);  // keeps the inner vectors' capacity
         for (int i = 0; i < count; ++i)
             counts[i].assign(C->h_counts.p + lps[i].out0, C->h_counts.p + lps[i].out0 + H[i]);
         return 0;

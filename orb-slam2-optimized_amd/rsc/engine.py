@@ -281,14 +281,39 @@ class PoseOptResult(C.Structure):
                 ("lm_iterations", C.c_int32), ("lm_trials", C.c_int32), ("Tcw", C.c_float * 16)]
 
 
+_fast = None
+
+
+def _fast_library():
+    """Second handle of librsc.so whose batched reset / iterate prototypes take raw addresses
+    (c_void_p) instead of checked ndarrays; used only by SolverBatch with buffers it owns."""
+    global _fast
+    if _fast is None:
+        F = C.CDLL(_lib_path_loaded)
+        vp = C.c_void_p
+        for kind, rec in (("pnp", PnPResult), ("mlpnp", PnPResult), ("sim3", Sim3Result)):
+            f = getattr(F, f"rsc_{kind}_reset_many")
+            f.argtypes = [C.POINTER(vp), C.c_int, vp]
+            f.restype = C.c_int
+            f = getattr(F, f"rsc_{kind}_iterate_many")
+            f.argtypes = [C.POINTER(vp), C.c_int, vp, C.POINTER(rec), C.POINTER(vp)]
+            f.restype = C.c_int
+        _fast = F
+    return _fast
+
+
+_lib_path_loaded = LIB_PATH
+
+
 def load_library(path: str = LIB_PATH):
     """Load librsc.so (raises if it was not built: no fallback)."""
-    global _lib
+    global _lib, _lib_path_loaded
     if _lib is not None:
         return _lib
     if not os.path.exists(path):
         raise RuntimeError(f"librsc.so not found at {path}: run __graft_entry__.build() / make")
     L = C.CDLL(path)
+    _lib_path_loaded = path
     vp = C.c_void_p
     L.rsc_version.restype = C.c_int
     L.rsc_status_string.restype = C.c_char_p
@@ -724,12 +749,27 @@ class SolverBatch:
         first = self.solvers[0]
         self.kind = "pnp" if isinstance(first, PnPSolver) else ("mlpnp" if isinstance(first, MLPnPSolver) else "sim3")
         self._h = (C.c_void_p * len(self.solvers))(*[s.h.value for s in self.solvers])
+        n = len(self.solvers)
+        # hot-path prototypes with raw addresses (the ndpointer checks cost ~4 us per call): a
+        # second handle of the same library keeps the checked prototypes of load_library() intact
+        load_library()
+        F = _fast_library()
+        self._reset_f = {"pnp": F.rsc_pnp_reset_many, "mlpnp": F.rsc_mlpnp_reset_many,
+                         "sim3": F.rsc_sim3_reset_many}[self.kind]
+        self._iter_f = {"pnp": F.rsc_pnp_iterate_many, "mlpnp": F.rsc_mlpnp_iterate_many,
+                        "sim3": F.rsc_sim3_iterate_many}[self.kind]
+        self._seeds = np.zeros(n, np.uint32)
+        self._seeds_p = self._seeds.ctypes.data
+        rec = Sim3Result if self.kind == "sim3" else PnPResult
+        self._raw = (rec * n)()
+        self._its = np.zeros(n, np.int32)
+        self._its_p = self._its.ctypes.data
+        self._nomask = (C.c_void_p * n)()
+        self._view = np.ctypeslib.as_array(self._raw)
 
     def reset(self, seeds):
-        seeds = np.ascontiguousarray(np.asarray(seeds, np.uint32))
-        L = load_library()
-        f = {"pnp": L.rsc_pnp_reset_many, "mlpnp": L.rsc_mlpnp_reset_many, "sim3": L.rsc_sim3_reset_many}[self.kind]
-        _check(f(self._h, len(self.solvers), seeds), "reset_many")
+        self._seeds[:] = seeds
+        _check(self._reset_f(self._h, len(self.solvers), self._seeds_p), "reset_many")
 
     def set_ransac_parameters(self, *params):
         L = load_library()
@@ -751,17 +791,8 @@ class SolverBatch:
         """iterate() of every solver without inlier vectors; returns the C result records as a
         numpy structured array (fields ok, no_more, n_inliers, iterations, T | R, t) without
         per-solver Python objects (the hot loop of bench.py)."""
-        n = len(self.solvers)
-        if not hasattr(self, "_raw"):
-            rec = Sim3Result if self.kind == "sim3" else PnPResult
-            self._raw = (rec * n)()
-            self._its = np.zeros(n, np.int32)
-            self._nomask = (C.c_void_p * n)()
-            self._view = np.ctypeslib.as_array(self._raw)
         self._its[:] = n_iterations
-        L = load_library()
-        f = {"pnp": L.rsc_pnp_iterate_many, "mlpnp": L.rsc_mlpnp_iterate_many, "sim3": L.rsc_sim3_iterate_many}[self.kind]
-        _check(f(self._h, n, self._its, self._raw, self._nomask), "iterate_many")
+        _check(self._iter_f(self._h, len(self.solvers), self._its_p, self._raw, self._nomask), "iterate_many")
         return self._view
 
     def phase_stamps(self, H):
