@@ -816,6 +816,18 @@ __global__ __launch_bounds__(256) void selftest_math_kernel(int fn, const double
     out[i] = r;
 }
 
+__global__ __launch_bounds__(256) void upload16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n16) dst[i] = src[i];
+}
+
+hipError_t launch_upload16(const void* host_src, void* dev_dst, size_t n16, hipStream_t st) {
+    if (n16 == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)((n16 + 255) / 256);
+    upload16_kernel<<<blocks, 256, 0, st>>>(static_cast<const uint4*>(host_src), static_cast<uint4*>(dev_dst), n16);
+    return hipGetLastError();
+}
+
 hipError_t launch_selftest_math(int fn, const double* x, int n, double* out, hipStream_t st) {
     if (fn < 0 || fn > 5 || n <= 0) return hipErrorInvalidValue;
     selftest_math_kernel<<<(n + 255) / 256, 256, 0, st>>>(fn, x, n, out);

@@ -204,6 +204,7 @@ struct rsc_context {
     // [0] speculation inputs built, [1] kernels enqueued, [2] counts back (sync), [3] return
     double host_us[4] = {0, 0, 0, 0};
     bool direct_counts = true;  // env RSC_DIRECT_COUNTS=0 restores the HBM buffer + D2H copy
+    bool dma_upload = false;    // env RSC_DMA_UPLOAD=1: descriptors by hipMemcpyAsync instead of the copy kernel
     std::chrono::steady_clock::time_point t_entry;
 };
 
@@ -285,12 +286,18 @@ struct Blob {
 };
 
 int upload_blob(rsc_context* C, const Blob& b) {
-    if (int e = C->h_desc.ensure(b.bytes.size())) return e;
-    if (int e = C->d_desc.ensure(b.bytes.size())) return e;
-    // the previous round's H2D copy must be finished before the pinned staging is overwritten
+    const size_t n16 = (b.bytes.size() + 15) / 16;
+    if (int e = C->h_desc.ensure(n16 * 16)) return e;
+    if (int e = C->d_desc.ensure(n16 * 16)) return e;
+    // the previous round's upload must be finished before the pinned staging is overwritten
     RSC_HIP(hipStreamSynchronize(C->stream));
     std::memcpy(C->h_desc.p, b.bytes.data(), b.bytes.size());
-    RSC_HIP(hipMemcpyAsync(C->d_desc.p, C->h_desc.p, b.bytes.size(), hipMemcpyHostToDevice, C->stream));
+    // a copy kernel on the context stream, not hipMemcpyAsync: the DMA engine's start-up and its
+    // completion hand-off to the first kernel cost ~15 us per round (rocprofv3 copy + kernel trace)
+    if (C->dma_upload)
+        RSC_HIP(hipMemcpyAsync(C->d_desc.p, C->h_desc.p, b.bytes.size(), hipMemcpyHostToDevice, C->stream));
+    else
+        RSC_HIP(launch_upload16(C->h_desc.p, C->d_desc.p, n16, C->stream));
     return 0;
 }
 
@@ -914,6 +921,7 @@ int rsc_context_create(int device, rsc_context** out) {
         else if (!std::strcmp(m, "split")) C->solve_mode = 3;
     }
     if (const char* m = std::getenv("RSC_DIRECT_COUNTS")) C->direct_counts = std::strcmp(m, "0") != 0;
+    if (const char* m = std::getenv("RSC_DMA_UPLOAD")) C->dma_upload = std::strcmp(m, "0") != 0;
     C->table.build();
     if (int e = C->d_table.ensure(C->table.T.size())) return e;
     RSC_HIP(hipMemcpy(C->d_table.p, C->table.T.data(), C->table.T.size() * 4, hipMemcpyHostToDevice));
