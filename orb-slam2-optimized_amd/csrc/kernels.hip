@@ -821,6 +821,32 @@ __global__ __launch_bounds__(256) void upload16_kernel(const uint4* __restrict__
     if (i < n16) dst[i] = src[i];
 }
 
+// Byte copy between pinned host memory and HBM (either direction) by one kernel: thread i moves
+// bytes [16 i, 16 i + 16) as one 16-B word, four 4-B words or single bytes (`unit`, by alignment).
+__global__ __launch_bounds__(256) void copy_bytes_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                         size_t n, int unit) {
+    const size_t b = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    if (b >= n) return;
+    if (b + 16 <= n && unit == 16) {
+        *reinterpret_cast<uint4*>(dst + b) = *reinterpret_cast<const uint4*>(src + b);
+    } else if (b + 16 <= n && unit == 4) {
+        RSC_UNROLL for (int k = 0; k < 16; k += 4)
+            *reinterpret_cast<uint32_t*>(dst + b + k) = *reinterpret_cast<const uint32_t*>(src + b + k);
+    } else {
+        const size_t e = (b + 16 < n) ? b + 16 : n;
+        for (size_t k = b; k < e; ++k) dst[k] = src[k];
+    }
+}
+
+hipError_t launch_copy_bytes(const void* src, void* dst, size_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst);
+    const int unit = (a % 16 == 0) ? 16 : (a % 4 == 0 ? 4 : 1);
+    const unsigned blocks = (unsigned)((n + 16 * 256 - 1) / (16 * 256));
+    copy_bytes_kernel<<<blocks, 256, 0, st>>>(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), n, unit);
+    return hipGetLastError();
+}
+
 hipError_t launch_upload16(const void* host_src, void* dev_dst, size_t n16, hipStream_t st) {
     if (n16 == 0) return hipSuccess;
     const unsigned blocks = (unsigned)((n16 + 255) / 256);

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -1870,7 +1871,7 @@ struct rsc_kfdb {
     uint32_t vocab = 0;
     uint32_t next_seq = 1;
     std::vector<uint8_t> present;
-    std::vector<int32_t> covis_h, covis_n_h;  // host mirror of the covisibility table
+    PinBuf<int32_t> covis_h, covis_n_h;  // host mirror of the covisibility table (pinned: the copy kernel reads it)
     DevBuf<uint32_t> ids, seq;
     DevBuf<double> vals;
     DevBuf<char> qbuf;  // the query BowVector: ids | vals (8-aligned), one upload per query
@@ -1934,11 +1935,12 @@ int rsc_kfdb_create(rsc_context* C, uint32_t vocab_words, int capacity, int max_
     db->max_words = max_words;
     db->vocab = vocab_words;
     db->present.assign(capacity, 0);
-    db->covis_h.assign((size_t)capacity * kKfdbCovis, 0);
-    db->covis_n_h.assign(capacity, 0);
     RSC_HIP(hipSetDevice(C->device));
     const size_t K = (size_t)capacity;
     int e = 0;
+    if ((e = db->covis_h.ensure(K * kKfdbCovis)) || (e = db->covis_n_h.ensure(K))) return e;
+    std::memset(db->covis_h.p, 0, K * kKfdbCovis * sizeof(int32_t));
+    std::memset(db->covis_n_h.p, 0, K * sizeof(int32_t));
     if ((e = db->wpos.ensure(vocab_words)) || (e = db->ids.ensure(K * max_words)) || (e = db->vals.ensure(K * max_words)) || (e = db->len.ensure(K)) ||
         (e = db->seq.ensure(K)) || (e = db->covis.ensure(K * kKfdbCovis)) || (e = db->covis_n.ensure(K)) ||
         (e = db->query.ensure(2 * K)) || (e = db->words.ensure(2 * K)) || (e = db->score.ensure(2 * K)) ||
@@ -2014,8 +2016,8 @@ int rsc_kfdb_release(rsc_kfdb* db, int kf) {
     RSC_HIP(hipMemsetAsync(db->covis.p + (size_t)kf * kKfdbCovis, 0, 4 * kKfdbCovis, C->stream));
     RSC_HIP(hipMemsetAsync(db->covis_n.p + kf, 0, 4, C->stream));
     RSC_HIP(hipStreamSynchronize(C->stream));
-    std::fill(db->covis_h.begin() + (size_t)kf * kKfdbCovis, db->covis_h.begin() + (size_t)(kf + 1) * kKfdbCovis, 0);
-    db->covis_n_h[kf] = 0;
+    std::fill(db->covis_h.p + (size_t)kf * kKfdbCovis, db->covis_h.p + (size_t)(kf + 1) * kKfdbCovis, 0);
+    db->covis_n_h.p[kf] = 0;
     db->present[kf] = 0;
     return RSC_OK;
 }
@@ -2029,22 +2031,19 @@ int rsc_kfdb_clear(rsc_kfdb* db) {
     return RSC_OK;
 }
 
+namespace {
+// One covisibility row padded to kKfdbCovis entries (the _many form reads rows of that stride).
+std::array<int32_t, kKfdbCovis> best_row_of(const int32_t* best, int n) {
+    std::array<int32_t, kKfdbCovis> r{};
+    for (int i = 0; i < n; ++i) r[i] = best[i];
+    return r;
+}
+}  // namespace
+
 int rsc_kfdb_set_covisibility(rsc_kfdb* db, int kf, int n, const int32_t* best) {
     if (!db || kf < 0 || kf >= db->cap || n < 0 || n > kKfdbCovis || (n && !best)) return RSC_ERR_ARG;
-    int32_t row[kKfdbCovis] = {};
-    for (int i = 0; i < n; ++i) {
-        if (best[i] < 0 || best[i] >= db->cap) return RSC_ERR_ARG;
-        row[i] = best[i];
-    }
-    std::copy(row, row + kKfdbCovis, db->covis_h.begin() + (size_t)kf * kKfdbCovis);
-    db->covis_n_h[kf] = n;
-    db->touch(kf);
-    for (int i = 0; i < n; ++i) db->touch(row[i]);
-    RSC_HIP(hipSetDevice(db->ctx->device));
-    RSC_HIP(hipStreamSynchronize(db->ctx->stream));
-    RSC_HIP(hipMemcpy(db->covis.p + (size_t)kf * kKfdbCovis, row, sizeof(row), hipMemcpyHostToDevice));
-    RSC_HIP(hipMemcpy(db->covis_n.p + kf, &n, 4, hipMemcpyHostToDevice));
-    return RSC_OK;
+    const int32_t nn = n;
+    return rsc_kfdb_set_covisibility_many(db, 1, &kf, &nn, best_row_of(best, n).data());
 }
 
 int rsc_kfdb_set_covisibility_many(rsc_kfdb* db, int count, const int32_t* kf, const int32_t* n,
@@ -2055,18 +2054,21 @@ int rsc_kfdb_set_covisibility_many(rsc_kfdb* db, int count, const int32_t* kf, c
         for (int i = 0; i < n[c]; ++i)
             if (best[(size_t)c * kKfdbCovis + i] < 0 || best[(size_t)c * kKfdbCovis + i] >= db->cap) return RSC_ERR_ARG;
     }
+    // a copy of the mirror from the previous call may still be in flight
+    RSC_HIP(hipSetDevice(db->ctx->device));
+    RSC_HIP(hipStreamSynchronize(db->ctx->stream));
     // rows whose content changed go up as one span [lo, hi] (the mirror keeps the rest)
     int lo = INT32_MAX, hi = -1;
     for (int c = 0; c < count; ++c) {
-        int32_t* row = db->covis_h.data() + (size_t)kf[c] * kKfdbCovis;
-        bool changed = db->covis_n_h[kf[c]] != n[c];
+        int32_t* row = db->covis_h.p + (size_t)kf[c] * kKfdbCovis;
+        bool changed = db->covis_n_h.p[kf[c]] != n[c];
         for (int i = 0; i < kKfdbCovis; ++i) {
             const int32_t v = i < n[c] ? best[(size_t)c * kKfdbCovis + i] : 0;
             changed |= row[i] != v;
             row[i] = v;
             if (i < n[c]) db->touch(v);
         }
-        db->covis_n_h[kf[c]] = n[c];
+        db->covis_n_h.p[kf[c]] = n[c];
         db->touch(kf[c]);
         if (changed) {
             lo = std::min(lo, kf[c]);
@@ -2074,12 +2076,12 @@ int rsc_kfdb_set_covisibility_many(rsc_kfdb* db, int count, const int32_t* kf, c
         }
     }
     if (hi < 0) return RSC_OK;
-    RSC_HIP(hipSetDevice(db->ctx->device));
-    RSC_HIP(hipStreamSynchronize(db->ctx->stream));
+    // two copy kernels on the context stream (stream order puts them before the next query's
+    // kernels; the next call that rewrites the mirror synchronises first)
     const size_t rows = (size_t)(hi - lo + 1);
-    RSC_HIP(hipMemcpy(db->covis.p + (size_t)lo * kKfdbCovis, db->covis_h.data() + (size_t)lo * kKfdbCovis,
-                      4 * kKfdbCovis * rows, hipMemcpyHostToDevice));
-    RSC_HIP(hipMemcpy(db->covis_n.p + lo, db->covis_n_h.data() + lo, 4 * rows, hipMemcpyHostToDevice));
+    RSC_HIP(launch_copy_bytes(db->covis_h.p + (size_t)lo * kKfdbCovis, db->covis.p + (size_t)lo * kKfdbCovis,
+                              4 * kKfdbCovis * rows, db->ctx->stream));
+    RSC_HIP(launch_copy_bytes(db->covis_n_h.p + lo, db->covis_n.p + lo, 4 * rows, db->ctx->stream));
     return RSC_OK;
 }
 
@@ -2098,7 +2100,7 @@ int kfdb_query(rsc_kfdb* db, uint64_t qid, int n, const uint32_t* id, const doub
     if (n) {
         std::memcpy(h, id, 4 * (size_t)n);
         std::memcpy(h + vo, val, 8 * (size_t)n);
-        RSC_HIP(hipMemcpyAsync(db->qbuf.p, h, vo + 8 * (size_t)n, hipMemcpyHostToDevice, C->stream));
+        RSC_HIP(launch_copy_bytes(h, db->qbuf.p, vo + 8 * (size_t)n, C->stream));
     }
     if (loop) {
         for (int i = 0; i < n_conn; ++i)
@@ -2114,7 +2116,7 @@ int kfdb_query(rsc_kfdb* db, uint64_t qid, int n, const uint32_t* id, const doub
         uint8_t* m = reinterpret_cast<uint8_t*>(h + 16 * (size_t)db->max_words + 16);
         std::memset(m, 0, H);
         for (int i = 0; i < n_conn; ++i) m[conn[i]] = 1;
-        RSC_HIP(hipMemcpyAsync(db->conn.p, m, H, hipMemcpyHostToDevice, C->stream));
+        RSC_HIP(launch_copy_bytes(m, db->conn.p, H, C->stream));
     }
     KfdbQuery q;
     q.id = (unsigned long long)qid;
@@ -2126,7 +2128,7 @@ int kfdb_query(rsc_kfdb* db, uint64_t qid, int n, const uint32_t* id, const doub
     d.qvals = reinterpret_cast<const double*>(db->qbuf.p + vo);
     RSC_HIP(launch_kfdb_query(d, q, C->stream));
     timing_begin(C, 4);
-    RSC_HIP(hipMemcpyAsync(h, db->out.p, 4 * (H + 1), hipMemcpyDeviceToHost, C->stream));
+    RSC_HIP(launch_copy_bytes(db->out.p, h, 4 * (H + 1), C->stream));  // written into pinned memory
     RSC_HIP(hipStreamSynchronize(C->stream));
     if (C->timing) {
         float ms = 0;
