@@ -229,9 +229,25 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// s + col[r] + col[r+1] + ... + col[m-1], left to right.  The LDS loads of 16 rows are issued
+// before their additions, so the fold runs at the FP64 add latency instead of one LDS round trip
+// per row (the refine's folds were LDS-latency-bound: tools/refine_latency_probe.py).
+__device__ __forceinline__ double fold_col(double s, const double* col, int r, int m) {
+    for (; r + 16 <= m; r += 16) {
+        double v[16];
+        RSC_UNROLL for (int k = 0; k < 16; ++k) v[k] = col[r + k];
+        RSC_UNROLL for (int k = 0; k < 16; ++k) s = s + v[k];
+    }
+    for (; r < m; ++r) s = s + col[r];
+    return s;
+}
+
+// Column stride of the fold buffer: 65 doubles, so the K folding lanes read different LDS banks.
+constexpr int kFoldStride = 65;
+
 // Ordered sums of K columns of per-row terms over rows [0, count), by one wave.  term(i, t[K]).
 // from_zero: s = ((0.0 + t0) + t1) + ... (loops starting from 0.0), else s = (t0 + t1) + ...
-// Returns column k's sum in lane k (k < K); buf holds 64*K doubles of this wave.
+// Returns column k's sum in lane k (k < K); buf holds kFoldStride*K doubles of this wave.
 template <int K, class Term>
 __device__ double wave_ordered_sum(int count, double* buf, bool from_zero, Term&& term) {
     const int lane = threadIdx.x & 63;
@@ -241,15 +257,15 @@ __device__ double wave_ordered_sum(int count, double* buf, bool from_zero, Term&
         if (i < count) {
             double t[K];
             term(i, t);
-            RSC_UNROLL for (int k = 0; k < K; ++k) buf[k * 64 + lane] = t[k];
+            RSC_UNROLL for (int k = 0; k < K; ++k) buf[k * kFoldStride + lane] = t[k];
         }
         wave_lds_sync();
         if (lane < K) {
             const int m = min(64, count - base);
-            const double* col = buf + lane * 64;
+            const double* col = buf + lane * kFoldStride;
             int r = 0;
             if (base == 0 && !from_zero) { s = col[0]; r = 1; }
-            for (; r < m; ++r) s = s + col[r];
+            s = fold_col(s, col, r, m);
         }
         wave_lds_sync();
     }
@@ -267,7 +283,7 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
                                                          const RefineJob* __restrict__ jobs,
                                                          int mask_words_out) {
     __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles];
-    __shared__ __attribute__((aligned(16))) double wbuf[4][64 * 9];
+    __shared__ __attribute__((aligned(16))) double wbuf[4][kFoldStride * 9];
     __shared__ int prefix[129];
     __shared__ double cen_sh[3], cws_sh[12], cci_sh[9];
     __shared__ double res_sh[3][13];  // per approximation: R[9], t[3], error
@@ -369,11 +385,11 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     __syncthreads();
     refine_stamp(2);
     // 3. MtM lower triangle, one entry per thread, each folded over the 2*nr rows in order.  The
-    // rows of M are staged through LDS (wbuf, 192 rows x 12 at a time) by all 256 threads, so the
+    // rows of M are staged through LDS (wbuf, 195 rows x 12 at a time) by all 256 threads, so the
     // 78 folding threads read operands from LDS instead of recomputing them from global memory.
     {
         double* Mc = &wbuf[0][0];
-        constexpr int kRows = (4 * 64 * 9) / 12;
+        constexpr int kRows = (4 * kFoldStride * 9) / 12;
         int a = 0, b = tid;
         while (b > a) { b -= a + 1; ++a; }  // tid -> (a,b) with b <= a, row-major lower triangle
         double s = 0.0;
@@ -387,6 +403,12 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
                 if (r0 == 0) {
                     s = Mc[a] * Mc[b];
                     r = 1;
+                }
+                // 8 rows' operands loaded before their products and ordered additions
+                for (; r + 8 <= m; r += 8) {
+                    double x[8], y[8];
+                    RSC_UNROLL for (int k = 0; k < 8; ++k) { x[k] = Mc[(r + k) * 12 + a]; y[k] = Mc[(r + k) * 12 + b]; }
+                    RSC_UNROLL for (int k = 0; k < 8; ++k) s = s + x[k] * y[k];
                 }
                 for (; r < m; ++r) s = s + Mc[r * 12 + a] * Mc[r * 12 + b];
             }

@@ -302,7 +302,9 @@ __device__ __forceinline__ void quad_eig12_ev4(double* T, double* E, int q, Sync
 // lane of a group computes redundantly, so the wave's instruction stream costs the same whether it
 // serves 16 hypotheses (quads) or 32 (pairs); a group only shares the row work (the rotations on
 // Q, the Householder updates).  A config-2 batch (19,200 hypotheses) is 1,200 quad waves for the
-// 1,024 SIMDs — the last 176 SIMDs run two waves back to back — but 600 pair waves, one per SIMD.
+// 1,024 SIMDs — the last 176 SIMDs run two waves back to back — but 960 pair waves of 20
+// hypotheses (kEigHyps), one per SIMD; 32 per pair wave (600 waves) leaves SIMDs idle at the same
+// per-wave latency (tools/qr_bench).
 template <int NS, int STOP, int L, int HPW, bool EVQR = false>
 __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
                                                    const int2* __restrict__ wg_table, const uint32_t* __restrict__ rng_T,

@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase wall-clock of the PnP refine kernel in the single-event latency case
+(bench.py's `single_event_latency` relocalization event: C = 15, N ~ 570), from
+rsc_diag_refine_phase_stamps after one rsc_reloc_events call."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "orb-slam2-optimized_amd"), ROOT]
+import numpy as np  # noqa: E402
+import bench  # noqa: E402
+from rsc import engine  # noqa: E402
+
+ctx = engine.Context(0)
+ev = bench.latency_event("reloc")
+(eb, params, seeds, _), = bench.build_event_drivers(engine, ctx, [ev], [0])
+names = ["compaction", "ctrl pts", "MtM", "eigen", "betas", "check", "exit"]
+for rep in range(5):
+    eb.batch.reset(seeds)
+    eb.batch.set_ransac_parameters(*params)
+    eb.run()
+st = np.zeros(64 * 8, np.uint64)
+engine.load_library().rsc_diag_refine_phase_stamps(ctx.h, st)
+st = st.reshape(64, 8).astype(np.int64)
+ok = st[:, 0] > 0
+d = np.diff(st[ok], axis=1) / 100.0
+print(f"jobs stamped: {ok.sum()}  total us: mean {((st[ok, 6] - st[ok, 0]) / 100.0).mean():.1f} "
+      f"max {((st[ok, 6] - st[ok, 0]) / 100.0).max():.1f}")
+for i, n in enumerate(names[:6]):
+    print(f"  {n:10s} mean {d[:, i].mean():8.1f} us  max {d[:, i].max():8.1f} us")
