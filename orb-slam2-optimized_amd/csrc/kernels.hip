@@ -13,6 +13,7 @@
 //
 // Reference: src/PnPsolver.cpp, src/Sim3Solver.cpp (see rsc_core.h for the arithmetic contract).
 #include <hip/hip_runtime.h>
+#include <climits>
 #include "rsc_core.h"
 #include "rsc_epnp.h"
 #include "rsc_sim3.h"
@@ -586,6 +587,7 @@ __global__ __launch_bounds__(256) void sim3_scan_kernel(const DevSim3* __restric
                                                         const int4* __restrict__ wg_table,
                                                         const float* __restrict__ poses,
                                                         int32_t* __restrict__ counts,
+                                                        int32_t* __restrict__ counts_dev,
                                                         uint64_t* __restrict__ masks, int mask_words) {
     __shared__ int wave_cnt[4][64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -631,6 +633,7 @@ __global__ __launch_bounds__(256) void sim3_scan_kernel(const DevSim3* __restric
             if (tid <= (j & 63)) {
                 const int c = wave_cnt[0][tid] + wave_cnt[1][tid] + wave_cnt[2][tid] + wave_cnt[3][tid];
                 counts[lp.out0 + wt.y + base + tid] = c;
+                if (counts_dev) counts_dev[lp.out0 + wt.y + base + tid] = c;  // for sim3_pick_kernel
             }
             __syncthreads();
         }
@@ -764,6 +767,75 @@ __global__ void gather_records_kernel(const float* __restrict__ src, int stride,
     if (t >= n * take) return;
     const int q = t / take, e = t - q * take;
     dst[t] = src[(size_t)idx[q] * stride + e];
+}
+
+// Sim3Solver::iterate (Sim3Solver.cpp:155-166) keeps the hypothesis with nInliers >= mnBestInliers
+// (later ties win) and returns at the first one with nInliers > mRansacMinInliers.  Evaluated after
+// the scan, one workgroup per solver, so the kept pose comes back with the counts instead of in a
+// second round trip after the host replay (which still decides; the backend serves the pose from
+// here when the replay kept the same index).  In parallel: hypothesis k updates the best iff
+// c_k >= max(best0, c_0..c_k-1) (a prefix maximum over per-thread chunks); the return index r is
+// the first update with c_k > minInliers; the kept index is the last update <= r.
+__global__ __launch_bounds__(256) void sim3_pick_kernel(const LaunchProb* __restrict__ lps,
+                                                        const int32_t* __restrict__ counts,
+                                                        const float* __restrict__ poses, float* __restrict__ pick) {
+    constexpr int T = 256, PER = kPickMaxH / T;
+    __shared__ int pre[T];
+    __shared__ int ret_k, keep_k;
+    const int tid = threadIdx.x;
+    const LaunchProb& lp = lps[blockIdx.x];
+    const int H = lp.H;
+    const int per = (H + T - 1) / T;  // <= PER: contiguous chunk [tid*per, tid*per + per)
+    int c[PER];
+    int mx = INT_MIN;
+    RSC_UNROLL for (int u = 0; u < PER; ++u) {
+        const int k = tid * per + u;
+        c[u] = (u < per && k < H) ? counts[lp.out0 + k] : INT_MIN;
+        mx = max(mx, c[u]);
+    }
+    pre[tid] = mx;
+    if (tid == 0) { ret_k = INT_MAX; keep_k = -1; }
+    __syncthreads();
+    for (int d = 1; d < T; d <<= 1) {  // inclusive prefix maximum of the chunk maxima
+        const int v = (tid >= d) ? pre[tid - d] : INT_MIN;
+        __syncthreads();
+        pre[tid] = max(pre[tid], v);
+        __syncthreads();
+    }
+    int run = max(lp.best0, tid > 0 ? pre[tid - 1] : INT_MIN);  // best before this chunk
+    int my_ret = INT_MAX;
+    RSC_UNROLL for (int u = 0; u < PER; ++u) {
+        const int k = tid * per + u;
+        if (u < per && k < H && c[u] >= run) {
+            run = c[u];
+            if (c[u] > lp.min_inliers) my_ret = min(my_ret, k);
+        }
+    }
+    atomicMin(&ret_k, my_ret);  // LDS atomics
+    __syncthreads();
+    const int r = ret_k;
+    run = max(lp.best0, tid > 0 ? pre[tid - 1] : INT_MIN);
+    int my_keep = -1;
+    RSC_UNROLL for (int u = 0; u < PER; ++u) {
+        const int k = tid * per + u;
+        if (u < per && k < H && k <= r && c[u] >= run) {
+            run = c[u];
+            my_keep = k;
+        }
+    }
+    atomicMax(&keep_k, my_keep);
+    __syncthreads();
+    const int k = keep_k;
+    float* o = pick + (size_t)blockIdx.x * 16;
+    if (tid == 0) reinterpret_cast<int32_t*>(o)[0] = k;
+    if (k >= 0 && tid < 12) o[1 + tid] = poses[(size_t)(lp.out0 + k) * 24 + tid];
+}
+
+hipError_t launch_sim3_pick(int count, const LaunchProb* lps, const int32_t* counts, const float* poses,
+                            float* pick, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    sim3_pick_kernel<<<count, 256, 0, st>>>(lps, counts, poses, pick);
+    return hipGetLastError();
 }
 
 hipError_t launch_gather_records(const float* src, int stride, int take, const int32_t* idx, int n, float* dst,
@@ -910,9 +982,10 @@ hipError_t launch_sim3_solve(int nwg, const DevSim3* probs, const LaunchProb* lp
 }
 
 hipError_t launch_sim3_scan(int ppt, int nwg, const DevSim3* probs, const LaunchProb* lps, const int4* wgt,
-                            const float* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st) {
+                            const float* poses, int32_t* counts, int32_t* counts_dev, uint64_t* masks, int mask_words,
+                            hipStream_t st) {
     switch (ppt) {
-#define RSC_CASE(P) case P: sim3_scan_kernel<P><<<nwg, 256, 0, st>>>(probs, lps, wgt, poses, counts, masks, mask_words); break;
+#define RSC_CASE(P) case P: sim3_scan_kernel<P><<<nwg, 256, 0, st>>>(probs, lps, wgt, poses, counts, counts_dev, masks, mask_words); break;
         RSC_CASE(1) RSC_CASE(2) RSC_CASE(4) RSC_CASE(8) RSC_CASE(16) RSC_CASE(32)
 #undef RSC_CASE
         default: return hipErrorInvalidValue;

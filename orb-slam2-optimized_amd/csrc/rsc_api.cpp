@@ -171,6 +171,7 @@ struct rsc_context {
     PinBuf<char> h_desc;
     PinBuf<int32_t> h_counts;
     PinBuf<float> h_small;
+    PinBuf<float> h_pick;  // Sim3 pick records of the last round, [solver][16]
     DevBuf<char> d_refine;
     // PoseOptimization: packed inputs (problems | xw | uv), edge error scratch, results (outliers | poses)
     DevBuf<char> d_po_in;
@@ -606,6 +607,7 @@ struct HipPnPBackend : PnPBackend {
 struct HipSim3Backend : Sim3Backend {
     rsc_context* C;
     std::vector<rsc_sim3*> solvers;  // slot j of the last speculation
+    bool pick_valid = false;  // C->h_pick holds this round's sim3_pick_kernel records
     explicit HipSim3Backend(rsc_context* c) : C(c) {}
     rsc_sim3* of(Sim3State* s, const std::vector<rsc_sim3*>& all) {
         for (auto* p : all)
@@ -629,7 +631,9 @@ struct HipSim3Backend : Sim3Backend {
             std::memcpy(d.K1, p->K1, sizeof(d.K1));
             std::memcpy(d.K2, p->K2, sizeof(d.K2));
             LaunchProb& lp = lps[i];
-            lp.prob = i; lp.H = H[i]; lp.out0 = total; lp.g0 = S[i]->rng.g; lp.min_inliers = 0;
+            lp.prob = i; lp.H = H[i]; lp.out0 = total; lp.g0 = S[i]->rng.g;
+            lp.min_inliers = S[i]->mRansacMinInliers;  // the pick kernel's return rule
+            lp.best0 = S[i]->mnBestInliers;
             std::memcpy(lp.window, S[i]->rng.window, sizeof(lp.window));
             p->spec_out0 = total;
             p->spec_H = H[i];
@@ -659,8 +663,16 @@ struct HipSim3Backend : Sim3Backend {
         const size_t o_scan = b.add(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
         if (int e = upload_blob(C, b)) return e;
         if (int e = C->d_poses.ensure((size_t)total * 24)) return e;
+        // the kept pose comes back with the counts (sim3_pick_kernel) when every solver's round
+        // fits the pick kernel's LDS
+        pick_valid = true;
+        for (int i = 0; i < count; ++i) pick_valid = pick_valid && H[i] <= kPickMaxH;
         int32_t* cnt_dst = nullptr;
         if (int e = counts_target(C, total, &cnt_dst)) return e;
+        if (pick_valid) {
+            if (int e = C->d_counts.ensure((size_t)total)) return e;
+            if (int e = C->h_pick.ensure((size_t)count * 16)) return e;
+        }
         if (int e = C->d_masks.ensure((size_t)total * mw)) return e;
         if (C->keep_samples)
             if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
@@ -671,9 +683,12 @@ struct HipSim3Backend : Sim3Backend {
         RSC_HIP(launch_sim3_solve((int)solve_wgs.size(), dprobs, dlps, reinterpret_cast<const int2*>(base + o_solve),
                                   C->d_table.p, C->d_poses.p, C->keep_samples ? C->d_samples.p : nullptr, C->stream));
         timing_begin(C, 1);
+        int32_t* cnt_dev = (pick_valid && C->direct_counts) ? C->d_counts.p : nullptr;  // else cnt_dst is HBM
         RSC_HIP(launch_sim3_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
-                                 C->d_poses.p, cnt_dst, C->d_masks.p, mw, C->stream));
+                                 C->d_poses.p, cnt_dst, cnt_dev, C->d_masks.p, mw, C->stream));
         timing_begin(C, 2);
+        if (pick_valid)
+            RSC_HIP(launch_sim3_pick(count, dlps, C->d_counts.p, C->d_poses.p, C->h_pick.p, C->stream));
         if (!C->direct_counts)
             RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
         RSC_HIP(hipStreamSynchronize(C->stream));
@@ -693,6 +708,15 @@ struct HipSim3Backend : Sim3Backend {
     }
 
     int fetch_poses(const int* j, const int* k, int n, float (*pose12)[12]) override {
+        // the poses the pick kernel brought back with the counts, when the replay kept the same
+        // hypotheses (it always does: both apply Sim3Solver.cpp:155-166 to the same counts)
+        bool from_pick = pick_valid;
+        for (int q = 0; q < n && from_pick; ++q)
+            from_pick = reinterpret_cast<const int32_t*>(C->h_pick.p + (size_t)j[q] * 16)[0] == k[q];
+        if (from_pick) {
+            for (int q = 0; q < n; ++q) std::memcpy(pose12[q], C->h_pick.p + (size_t)j[q] * 16 + 1, 48);
+            return 0;
+        }
         // record indices -> one gather kernel -> one D2H copy
         if (int e = C->h_small.ensure((size_t)n * 13)) return e;
         int32_t* hidx = reinterpret_cast<int32_t*>(C->h_small.p + (size_t)n * 12);

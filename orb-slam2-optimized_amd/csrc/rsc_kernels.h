@@ -47,7 +47,11 @@ struct LaunchProb {
     int g0;
     uint32_t window[31];
     int min_inliers;  // PnP scan: masks are stored only for counts >= this (mRansacMinInliers)
+    int best0 = 0;    // Sim3 pick: mnBestInliers when the call started
 };
+
+// Sim3 pick (sim3_pick_kernel): hypotheses per solver it can hold in LDS.
+constexpr int kPickMaxH = 4096;
 
 struct RefineJob {
     int prob;
@@ -111,7 +115,15 @@ hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jo
                              hipStream_t st);
 hipError_t launch_sim3_solve(int nwg, const DevSim3* probs, const LaunchProb* lps, const int2* wgt,
                              const uint32_t* T, float* poses, int32_t* samples, hipStream_t st);
+// counts: where the host reads them (pinned memory or HBM); counts_dev (nullable): an HBM copy for
+// sim3_pick_kernel.
 hipError_t launch_sim3_scan(int ppt, int nwg, const DevSim3* probs, const LaunchProb* lps, const int4* wgt,
-                            const float* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st);
+                            const float* poses, int32_t* counts, int32_t* counts_dev, uint64_t* masks, int mask_words,
+                            hipStream_t st);
+// Sim3Solver::iterate's selection evaluated after the scan (one workgroup per solver, counts from
+// HBM): pick[16 j] = {kept hypothesis index (as int, -1: none), R12[9], t12[3]} — the hypothesis
+// the reference's '>=' rule keeps as mBestRotation / mBestTranslation (pick: pinned host memory).
+hipError_t launch_sim3_pick(int count, const LaunchProb* lps, const int32_t* counts, const float* poses,
+                            float* pick, hipStream_t st);
 
 }  // namespace rsc
