@@ -618,8 +618,13 @@ struct HipSim3Backend : Sim3Backend {
 
     int speculate(Sim3State* const* S, int count, const int* H, std::vector<std::vector<int32_t>>& counts) override {
         int total = 0, maxN = 1;
-        std::vector<DevSim3> probs(count);
-        std::vector<LaunchProb> lps(count);
+        // per-thread scratch that keeps its capacity across rounds (no allocation per round)
+        thread_local std::vector<DevSim3> probs_tl;
+        thread_local std::vector<LaunchProb> lps_tl;
+        std::vector<DevSim3>& probs = probs_tl;
+        std::vector<LaunchProb>& lps = lps_tl;
+        probs.resize(count);
+        lps.resize(count);
         solvers.assign(count, nullptr);
         for (int i = 0; i < count; ++i) {
             rsc_sim3* p = of(S[i], all);
@@ -647,15 +652,26 @@ struct HipSim3Backend : Sim3Backend {
         }
         const int mw = ppt * 4;
         C->mask_words = mw;
-        std::vector<int2> solve_wgs;
-        std::vector<int4> scan_wgs;
+        thread_local std::vector<int2> solve_wgs_tl;
+        thread_local std::vector<int4> scan_wgs_tl;
+        thread_local std::vector<int> shape_tl, key_tl;
+        std::vector<int2>& solve_wgs = solve_wgs_tl;
+        std::vector<int4>& scan_wgs = scan_wgs_tl;
+        std::vector<int>& shape = shape_tl;
+        std::vector<int>& key = key_tl;
         const int HC = 32;
-        for (int i = 0; i < count; ++i) {
-            for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs.push_back(make_int2(i, h0));
-            for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
+        key.assign(H, H + count);  // the tables depend on the per-solver H only (as the PnP tables)
+        if (key != shape) {
+            solve_wgs.clear();
+            scan_wgs.clear();
+            for (int i = 0; i < count; ++i) {
+                for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs.push_back(make_int2(i, h0));
+                for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
+            }
+            xcd_order(solve_wgs, [](const int2& w) { return w.x; });
+            xcd_order(scan_wgs, [](const int4& w) { return w.x; });
+            shape.assign(key.begin(), key.end());
         }
-        xcd_order(solve_wgs, [](const int2& w) { return w.x; });
-        xcd_order(scan_wgs, [](const int4& w) { return w.x; });
         Blob b;
         const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevSim3));
         const size_t o_lps = b.add(lps.data(), lps.size() * sizeof(LaunchProb));

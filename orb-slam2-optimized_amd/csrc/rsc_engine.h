@@ -386,7 +386,7 @@ inline int sim3_iterate_many(Sim3Backend& be, Sim3State* const* S, int count, co
         const int h = std::max(0, std::min(n_its[i], s.mRansacMaxIts - s.mnIterations));
         if (h > 0) { spec.push_back(&s); H.push_back(h); who.push_back(i); }
     }
-    std::vector<std::vector<int32_t>> counts;
+    thread_local std::vector<std::vector<int32_t>> counts;  // capacity kept across calls
     if (!spec.empty()) {
         int st = be.speculate(spec.data(), (int)spec.size(), H.data(), counts);
         if (st) return st;
