@@ -250,7 +250,7 @@ constexpr int kFoldStride = 65;
 // from_zero: s = ((0.0 + t0) + t1) + ... (loops starting from 0.0), else s = (t0 + t1) + ...
 // Returns column k's sum in lane k (k < K); buf holds kFoldStride*K doubles of this wave.
 template <int K, class Term>
-__device__ double wave_ordered_sum(int count, double* buf, bool from_zero, Term&& term) {
+__device__ __forceinline__ double wave_ordered_sum(int count, double* buf, bool from_zero, Term&& term) {
     const int lane = threadIdx.x & 63;
     double s = 0.0;
     for (int base = 0; base < count; base += 64) {
