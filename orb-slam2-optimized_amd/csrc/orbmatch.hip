@@ -155,26 +155,29 @@ __global__ __launch_bounds__(kBowTopkThreads) void bow_topk_kernel(const BowPair
             // stage this segment of the inner node (rows in FeatureVector order + position keys) in
             // the wave's LDS slot: all loads of the segment issued before the first store
             __builtin_amdgcn_wave_barrier();
-            uint4 r0[kBowSeg / 64], r1[kBowSeg / 64];
+            // (descriptor words as plain uint32 arrays: arrays of uint4 were not promoted to
+            // registers and went through scratch)
+            uint32_t r[kBowSeg / 64][8];
             uint32_t fb[kBowSeg / 64];
 #pragma unroll
             for (int u = 0; u < kBowSeg / 64; ++u) {
-                // clamped, unconditional loads (see walk_node); entries past m are not stored
+                // clamped, unconditional loads (see walk_node)
                 const int x = min(lane + 64 * u, m - 1);
-                r0[u] = B.desc_fv[2 * (b0 + s0 + x)];
-                r1[u] = B.desc_fv[2 * (b0 + s0 + x) + 1];
+                const uint4 a = B.desc_fv[2 * (b0 + s0 + x)], b = B.desc_fv[2 * (b0 + s0 + x) + 1];
+                r[u][0] = a.x; r[u][1] = a.y; r[u][2] = a.z; r[u][3] = a.w;
+                r[u][4] = b.x; r[u][5] = b.y; r[u][6] = b.z; r[u][7] = b.w;
                 fb[u] = kFrame ? 0u : B.feat[b0 + s0 + x];
             }
+            // every slot entry is stored, without a branch (entries past m hold copies of row m - 1
+            // and are never read: the insertion below stops at m)
 #pragma unroll
             for (int u = 0; u < kBowSeg / 64; ++u) {
                 const int x = lane + 64 * u;
-                if (x < m) {
-                    sd[2 * x] = r0[u];
-                    sd[2 * x + 1] = r1[u];
-                    // invalid inner features (KeyFrame overload, :404-410) get the empty key, which
-                    // the insertion below leaves out
-                    sk[x] = (kFrame || !(fb[u] & kBowInvalid)) ? (uint32_t)(s0 + x) : kBowNoKey;
-                }
+                sd[2 * x] = make_uint4(r[u][0], r[u][1], r[u][2], r[u][3]);
+                sd[2 * x + 1] = make_uint4(r[u][4], r[u][5], r[u][6], r[u][7]);
+                // invalid inner features (KeyFrame overload, :404-410) get the empty key, which
+                // the insertion below leaves out
+                sk[x] = (kFrame || !(fb[u] & kBowInvalid)) ? (uint32_t)(s0 + x) : kBowNoKey;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
