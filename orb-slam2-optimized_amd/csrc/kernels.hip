@@ -246,6 +246,16 @@ __device__ __forceinline__ double fold_col(double s, const double* col, int r, i
 // Column stride of the fold buffer: 65 doubles, so the K folding lanes read different LDS banks.
 constexpr int kFoldStride = 65;
 
+// Lanes of the Refine's 12x12 eigen-solve group (4: a quad; 2: a pair, as the hypothesis eigen
+// stage).  Both are bit-identical; for the single solve the quad is faster (single-event refine
+// eigen phase 110 us vs 124 us with a pair, tools/refine_latency_probe.py).  RSC_REFINE_EIG_LANES
+// overrides at build time for A/B runs.
+#ifndef RSC_REFINE_EIG_LANES
+#define RSC_REFINE_EIG_LANES 4
+#endif
+constexpr int kRefineEigLanes = RSC_REFINE_EIG_LANES;
+static_assert(kRefineEigLanes == 2 || kRefineEigLanes == 4, "refine eigen group: pair or quad");
+
 // Ordered sums of K columns of per-row terms over rows [0, count), by one wave.  term(i, t[K]).
 // from_zero: s = ((0.0 + t0) + t1) + ... (loops starting from 0.0), else s = (t0 + t1) + ...
 // Returns column k's sum in lane k (k < K); buf holds kFoldStride*K doubles of this wave.
@@ -418,18 +428,20 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     }
     __syncthreads();
     refine_stamp(3);
-    // 4. 12x12 eigenvectors (lanes 0-3 of wave 0 as one quad, quad_eig12_ev4), then L_6x10 and
-    // rho (single lane).  The MtM lower triangle in the slab is the quad's T region; wbuf the E
-    // scratch.  The eigenvector columns 0..3 go back to slab columns 0..3 (SlabView::ev).
-    if (tid < 4) {
-        double ev[3][4];
-        quad_eig12_ev4(slab, &wbuf[0][0], tid, [] {
+    // 4. 12x12 eigenvectors (lanes 0..kRefineEigLanes-1 of wave 0 as one lane group,
+    // group_eig12_ev4), then L_6x10 and rho (single lane).  The MtM lower triangle in the slab is
+    // the group's T region; wbuf the E scratch.  The eigenvector columns 0..3 go back to slab
+    // columns 0..3 (SlabView::ev).
+    if (tid < kRefineEigLanes) {
+        constexpr int L = kRefineEigLanes;
+        double ev[12 / L][4];
+        group_eig12_ev4<L>(slab, &wbuf[0][0], tid, [] {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }, ev);
-        RSC_UNROLL for (int j = 0; j < 3; ++j)
-            RSC_UNROLL for (int c = 0; c < 4; ++c) slab[(4 * j + tid) * 12 + c] = ev[j][c];
+        RSC_UNROLL for (int j = 0; j < 12 / L; ++j)
+            RSC_UNROLL for (int c = 0; c < 4; ++c) slab[(L * j + tid) * 12 + c] = ev[j][c];
     }
     __syncthreads();
     if (tid == 0) {

@@ -249,40 +249,41 @@ __device__ __forceinline__ double group_scale(const double (&A)[12 / L][12], int
 }
 
 // Eigenvectors of the four smallest eigenvalues of a symmetric 12x12 (SelfAdjointEigenSolver on
-// MtM, PnPsolver.cpp:379-382) by the four lanes of one quad (q = lane & 3): phases B-D of
-// pnp_eig_group_body below as a standalone routine (used by the Refine kernel, where one quad of
-// wave 0 serves the workgroup).  T: the quad's 144-double LDS region holding the lower triangle
-// row-major (T[R*12+c], c <= R) on entry; E: 55 doubles of LDS scratch; sync(): an LDS
-// visibility point for the quad.  ev[j][c] = eigenvector column c of row 4j+q, bit-identical to
-// sym_eig12 (rsc_core.h) and to the hypothesis path.
-template <class Sync>
-__device__ __forceinline__ void quad_eig12_ev4(double* T, double* E, int q, Sync sync, double (&ev)[3][4]) {
+// MtM, PnPsolver.cpp:379-382) by the L lanes of one lane group (q = lane index in the group, L = 2:
+// a pair, L = 4: a quad): phases B-D of pnp_eig_group_body below as a standalone routine (used by
+// the Refine kernel, where one group of wave 0 serves the workgroup).  T: the group's 144-double
+// LDS region holding the lower triangle row-major (T[R*12+c], c <= R) on entry; E: 55 doubles of
+// LDS scratch; sync(): an LDS visibility point for the group.  ev[j][c] = eigenvector column c of
+// row L*j+q, bit-identical to sym_eig12 (rsc_core.h) and to the hypothesis path.
+template <int L, class Sync>
+__device__ __forceinline__ void group_eig12_ev4(double* T, double* E, int q, Sync sync, double (&ev)[12 / L][4]) {
+    constexpr int RJ = 12 / L;
     double diag[12], sub[11], hC[11];
     {
-        double A[3][12];
-        RSC_UNROLL for (int j = 0; j < 3; ++j) {
-            const int R = 4 * j + q;
+        double A[RJ][12];
+        RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+            const int R = L * j + q;
             RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = T[(R >= c) ? R * 12 + c : c * 12 + R];
         }
-        const double scale = group_scale<4>(A, q);
-        RSC_UNROLL for (int j = 0; j < 3; ++j)
+        const double scale = group_scale<L>(A, q);
+        RSC_UNROLL for (int j = 0; j < RJ; ++j)
             RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = A[j][c] / scale;
         sync();  // every lane has read T before phase C overwrites it
-        group_tridiag<4>(A, q, E, diag, sub, hC);
+        group_tridiag<L>(A, q, E, diag, sub, hC);
     }
     sync();
     {
-        double Qc[3][12];
-        group_accumulate<4>(Qc, q, E, hC);
-        RSC_UNROLL for (int j = 0; j < 3; ++j)
-            RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + 4 * j + q] = Qc[j][r];
+        double Qc[RJ][12];
+        group_accumulate<L>(Qc, q, E, hC);
+        RSC_UNROLL for (int j = 0; j < RJ; ++j)
+            RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + L * j + q] = Qc[j][r];
     }
     sync();
-    GroupLdsRows<4> qapply{T, q};
+    GroupLdsRows<L> qapply{T, q};
     int perm[12];
     tridiag_qr<double, 12>(diag, sub, qapply, perm);
-    RSC_UNROLL for (int j = 0; j < 3; ++j) {
-        const double* row = T + (4 * j + q) * 12;
+    RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+        const double* row = T + (L * j + q) * 12;
         double Qr[12];
         RSC_UNROLL for (int p = 0; p < 12; ++p) Qr[p] = row[p];
         RSC_UNROLL for (int c = 0; c < 4; ++c) {
