@@ -1,0 +1,60 @@
+"""Regression guard on the gfx950 code objects inside librsc.so (no GPU needed): the latency-bound
+kernels of the hot path must run without scratch (private segment) — a stack round trip inside a
+dependent FP64 chain costs microseconds (DESIGN §9 scratch audit: the Refine's out-of-line
+`wave_ordered_sum` and SearchByBoW's staged uint4 arrays were such cases).  Reads the AMDGPU
+metadata notes with llvm-objdump / llvm-readelf from /opt/rocm; skipped when they are absent."""
+import os
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "orb-slam2-optimized_amd", "lib", "librsc.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+# kernels (demangled-name fragments) that must stay scratch-free
+SCRATCH_FREE = [
+    "pnp_eig_group_kernelILi4E", "pnp_eig_group_kernelILi5E", "pnp_eig_group_kernelILi6E",
+    "pnp_betas_kernelILi4E", "pnp_scan_kernelILi8E", "pnp_refine_kernel",
+    "sim3_solve_kernel", "sim3_scan_kernelILi4E", "sim3_pick_kernel",
+    "sim3opt_kernel", "bow_topk_kernelILb0E", "bow_topk_kernelILb1E", "bow_walk_kernel",
+    "sim3_search_kernel",
+]
+
+
+def _kernels():
+    if not os.path.exists(LIB):
+        pytest.skip("librsc.so not built")
+    objdump, readelf = os.path.join(LLVM, "llvm-objdump"), os.path.join(LLVM, "llvm-readelf")
+    if not (os.path.exists(objdump) and os.path.exists(readelf)):
+        pytest.skip("llvm tools not available")
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        lib = os.path.join(d, "librsc.so")
+        shutil.copy(LIB, lib)
+        subprocess.run([objdump, "--offloading", lib], cwd=d, check=True, capture_output=True)
+        cos = [f for f in os.listdir(d) if "gfx950" in f]
+        assert cos, "no gfx950 code object in librsc.so"
+        for f in cos:
+            txt = subprocess.run([readelf, "--notes", os.path.join(d, f)], check=True, capture_output=True,
+                                 text=True).stdout
+            i = txt.index("---")
+            j = txt.find("\n...", i)
+            doc = yaml.safe_load(txt[i:j if j > 0 else len(txt)].replace("---", "", 1))
+            for k in doc["amdhsa.kernels"]:
+                out[k[".name"]] = k
+    return out
+
+
+def test_hot_path_kernels_have_no_scratch():
+    ks = _kernels()
+    for frag in SCRATCH_FREE:
+        hits = [n for n in ks if frag in n]
+        assert hits, f"kernel {frag} not found in librsc.so"
+        for n in hits:
+            k = ks[n]
+            assert k[".private_segment_fixed_size"] == 0, (n, k[".private_segment_fixed_size"])
+            assert k.get(".vgpr_spill_count", 0) == 0, (n, k[".vgpr_spill_count"])
