@@ -87,7 +87,10 @@ hipError_t launch_rng_stream(const uint32_t* T, const uint32_t* window, int g0, 
 hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                             const uint32_t* T, float* poses, int32_t* samples, hipStream_t st);
 constexpr int kEigLanes = 2;           // lanes per hypothesis in the eigen-stage kernel (rsc_quad.h)
-constexpr int kEigHyps = 20;           // hypotheses per 64-lane eigen-stage workgroup (960 on config 2)
+#ifndef RSC_EIG_HYPS
+#define RSC_EIG_HYPS 20  // build-time override for A/B runs (tools/)
+#endif
+constexpr int kEigHyps = RSC_EIG_HYPS;  // hypotheses per 64-lane eigen-stage workgroup (960 on config 2)
 constexpr int kAutoSolveMode = 2;      // see rsc_context::solve_mode
 // Per-hypothesis stage record between the two kernels: eigenvectors [12][4], alphas [NS][4], cws [4][3].
 constexpr int kStageDoubles = 48 + 24 + 12;
