@@ -313,25 +313,35 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
         for (int wd = tid; wd < nwords; wd += 256) J.adopt_mask[wd] = J.best_mask[wd];
     if (J.adopt_pose && tid < 12) J.out_best_pose[tid] = J.adopt_pose[tid];
     // 1. compaction of the best-inlier set (PnPsolver.cpp:195-214), in index order.
-    if (tid == 0) {
-        int acc = 0;
-        for (int wd = 0; wd < nwords; ++wd) { prefix[wd] = acc; acc += __popcll(J.best_mask[wd]); }
-        prefix[nwords] = acc;
+    // exclusive prefix of the mask words' popcounts by wave 0 (one word per lane, wave scan;
+    // integer sums, so the order is free)
+    if (tid < 64) {
+        int carry = 0;
+        for (int w0 = 0; w0 < nwords; w0 += 64) {
+            const int wd = w0 + lane;
+            const int c = wd < nwords ? __popcll(J.best_mask[wd]) : 0;
+            int x = c;
+            RSC_UNROLL for (int off = 1; off < 64; off <<= 1) {
+                const int y = __shfl_up(x, off);
+                if (lane >= off) x += y;
+            }
+            if (wd < nwords) prefix[wd] = carry + x - c;
+            carry += __shfl(x, 63);
+        }
+        if (lane == 0) prefix[nwords] = carry;
     }
     __syncthreads();
     const int nr = prefix[nwords];
-    for (int wd = tid; wd < nwords; wd += 256) {
-        uint64_t m = J.best_mask[wd];
-        int r = prefix[wd];
-        while (m) {
-            const int b = __ffsll((long long)m) - 1;
-            m &= m - 1;
-            const int i = wd * 64 + b;
+    // one thread per correspondence: its row is the word's prefix + the set bits below it
+    for (int i = tid; i < n; i += 256) {
+        const int wd = i >> 6, b = i & 63;
+        const uint64_t m = J.best_mask[wd];
+        if ((m >> b) & 1ull) {
+            const int r = prefix[wd] + __popcll(m & ((1ull << b) - 1ull));
             const float4 p = P.pts[i];
             const float2 q = P.uv[i];
             P.pws[3 * r + 0] = p.x; P.pws[3 * r + 1] = p.y; P.pws[3 * r + 2] = p.z;
             P.us[2 * r + 0] = q.x; P.us[2 * r + 1] = q.y;
-            ++r;
         }
     }
     // set_maximum_number_of_correspondences(nr): growth zero-fills (the rows beyond nr do not
