@@ -58,11 +58,6 @@ int rsc_context_enable_timing(rsc_context* ctx, int enable);
  * out[i] = f(x[i]) computed ON THE GPU, f = 0 sin, 1 cos, 2 acos, 3 cbrt, 4 log, 5 logf
  * ((float)x[i] in, float result widened).  Host pointers, n >= 0.  Tests compare it with glibc. */
 int rsc_selftest_math(rsc_context* ctx, int fn, const double* x, int n, double* out);
-/* Hypothesis-solve kernel family for PnP (all produce bit-identical results):
- * 0 = auto, 1 = single kernel (one lane per hypothesis), 2 = quad-cooperative eigenvectors +
- * one wave per beta approximation, 3 = lane-per-hypothesis eigenvectors + per-approximation waves.
- * The environment variable RSC_SOLVE_MODE (mono|quad|split) sets the initial value. */
-int rsc_context_set_solve_mode(rsc_context* ctx, int mode);
 
 /* ---- PnPsolver (include/PnPsolver.hpp:21-138, src/PnPsolver.cpp) ------------------------------ */
 typedef struct {

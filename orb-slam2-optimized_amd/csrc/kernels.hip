@@ -1,7 +1,8 @@
 // kernels.hip — gfx950 kernels of the RANSAC pose engine.
 //
-//   pnp_solve_kernel<NS>   one LANE = one EPnP hypothesis (sample -> compute_pose), 64-lane
-//                          workgroups, 80 KiB LDS slab (12x12 eigenproblem per lane).
+//   pnp_eig_group_kernel<NS> / pnp_betas_kernel<NS>   EPnP hypotheses (sample -> compute_pose)
+//                          in two stages: lane pairs per hypothesis for the 12x12 eigenvectors,
+//                          then one wave per (beta approximation, 64 hypotheses) (rsc_quad.h).
 //   pnp_scan_kernel<PPT>   PnPsolver::CheckInliers for a chunk of hypotheses of one problem:
 //                          256 threads hold the problem's correspondences in VGPRs (PPT per
 //                          thread); per hypothesis every lane tests its points, __ballot gives the
@@ -27,73 +28,6 @@ namespace rsc {
 // ------------------------------------------------------------------------------------------------
 // PnP hypotheses
 // ------------------------------------------------------------------------------------------------
-// Diagnostic phase stamps (s_memtime) — only the STAMP=true instantiation executes them; the
-// production kernel passes NoStamp (inlined away).
-struct ClockStamp {
-    uint64_t* out;
-    __device__ void operator()(int k) const {
-        unsigned long long t;
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-        __builtin_amdgcn_sched_barrier(0);
-        out[k] = t;
-    }
-};
-
-template <int NS, bool STAMP>
-__global__ __launch_bounds__(64) void pnp_solve_kernel(const DevPnP* __restrict__ probs,
-                                                       const LaunchProb* __restrict__ lps,
-                                                       const int2* __restrict__ wg_table,
-                                                       const uint32_t* __restrict__ rng_T,
-                                                       float* __restrict__ poses, int32_t* __restrict__ samples,
-                                                       uint64_t* __restrict__ stamps) {
-    __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles * 64];
-    const int lane = threadIdx.x;
-    const int2 wt = wg_table[blockIdx.x];
-    const LaunchProb& lp = lps[wt.x];
-    const int h = wt.y + lane;
-    if (h >= lp.H) return;
-    const DevPnP& P = probs[lp.prob];
-
-    uint64_t st_local[10];
-    ClockStamp cs{st_local};
-    if (STAMP) cs(0);
-    uint32_t w[31];
-    RSC_UNROLL for (int j = 0; j < 31; ++j) w[j] = lp.window[j];
-    uint32_t words[NS];
-    RSC_UNROLL for (int d = 0; d < NS; ++d) words[d] = rng_word(rng_T, w, lp.g0 + h * NS + d);
-    int idx[NS];
-    swap_remove_sample<NS>(words, NS, P.n, idx);
-
-    HypStore<NS> st;
-    RSC_UNROLL for (int i = 0; i < NS; ++i) {
-        const float4 p = P.pts[idx[i]];
-        const float2 q = P.uv[idx[i]];
-        st.pw_[i][0] = p.x; st.pw_[i][1] = p.y; st.pw_[i][2] = p.z;
-        st.u_[i][0] = q.x; st.u_[i][1] = q.y;
-    }
-    st.rows_ = P.rows;
-    st.spw = P.pws;
-    st.sal = P.als;
-    const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
-    LaneMat S{slab + lane, 64};
-    float R[9], t[3];
-    if (STAMP) {
-        epnp_compute_pose(st, K, S, R, t, cs);
-        cs(9);
-        for (int k = 0; k < 10; ++k) stamps[(size_t)(lp.out0 + h) * 10 + k] = st_local[k];
-    } else {
-        epnp_compute_pose(st, K, S, R, t);
-    }
-
-    float* out = poses + (size_t)(lp.out0 + h) * 12;
-    RSC_UNROLL for (int k = 0; k < 9; ++k) out[k] = R[k];
-    RSC_UNROLL for (int k = 0; k < 3; ++k) out[9 + k] = t[k];
-    if (samples) {
-        RSC_UNROLL for (int i = 0; i < NS; ++i) samples[(size_t)(lp.out0 + h) * 8 + i] = idx[i];
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 // PnP hypotheses, two-kernel form (rsc_quad.h): lane-group eigenvectors (kEigLanes lanes per
 // hypothesis, kEigHyps per workgroup, one wave per SIMD), then one wave per beta approximation.
@@ -106,16 +40,6 @@ __global__ __launch_bounds__(64) void pnp_eig_group_kernel(const DevPnP* __restr
                                                           double* __restrict__ stage, int32_t* __restrict__ samples) {
     __shared__ __attribute__((aligned(16))) double smem[kEigHyps * kQuadRegion];
     pnp_eig_group_body<NS, 99, kEigLanes, kEigHyps>(probs, lps, wg_table, rng_T, stage, samples, smem);
-}
-
-template <int NS>
-__global__ __launch_bounds__(64) void pnp_eig_lane_kernel(const DevPnP* __restrict__ probs,
-                                                          const LaunchProb* __restrict__ lps,
-                                                          const int2* __restrict__ wg_table,
-                                                          const uint32_t* __restrict__ rng_T,
-                                                          double* __restrict__ stage, int32_t* __restrict__ samples) {
-    __shared__ __attribute__((aligned(16))) double slab[144 * 64];
-    pnp_eig_lane_body<NS>(probs, lps, wg_table, rng_T, stage, samples, slab);
 }
 
 template <int NS>
@@ -312,14 +236,21 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     if (J.adopt_mask)
         for (int wd = tid; wd < nwords; wd += 256) J.adopt_mask[wd] = J.best_mask[wd];
     if (J.adopt_pose && tid < 12) J.out_best_pose[tid] = J.adopt_pose[tid];
-    // 1. compaction of the best-inlier set (PnPsolver.cpp:195-214), in index order.
+    // 1. compaction of the best-inlier set (PnPsolver.cpp:195-214), in index order.  Bits at or
+    // above n in the last word are cleared, so the popcount prefix and the scatter agree by
+    // construction whatever the mask's padding holds.
+    const uint64_t tail = (n & 63) ? (1ull << (n & 63)) - 1ull : ~0ull;
+    auto best_word = [&](int wd) {
+        const uint64_t m = J.best_mask[wd];
+        return wd == nwords - 1 ? (m & tail) : m;
+    };
     // exclusive prefix of the mask words' popcounts by wave 0 (one word per lane, wave scan;
     // integer sums, so the order is free)
     if (tid < 64) {
         int carry = 0;
         for (int w0 = 0; w0 < nwords; w0 += 64) {
             const int wd = w0 + lane;
-            const int c = wd < nwords ? __popcll(J.best_mask[wd]) : 0;
+            const int c = wd < nwords ? __popcll(best_word(wd)) : 0;
             int x = c;
             RSC_UNROLL for (int off = 1; off < 64; off <<= 1) {
                 const int y = __shfl_up(x, off);
@@ -335,7 +266,7 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     // one thread per correspondence: its row is the word's prefix + the set bits below it
     for (int i = tid; i < n; i += 256) {
         const int wd = i >> 6, b = i & 63;
-        const uint64_t m = J.best_mask[wd];
+        const uint64_t m = best_word(wd);
         if ((m >> b) & 1ull) {
             const int r = prefix[wd] + __popcll(m & ((1ull << b) - 1ull));
             const float4 p = P.pts[i];
@@ -879,18 +810,7 @@ __global__ void rng_stream_kernel(const uint32_t* __restrict__ T, Window31 w, in
 // ------------------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------------------
-hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
-                            const uint32_t* T, float* poses, int32_t* samples, hipStream_t st) {
-    switch (ns) {
-        case 4: pnp_solve_kernel<4, false><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples, nullptr); break;
-        case 5: pnp_solve_kernel<5, false><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples, nullptr); break;
-        case 6: pnp_solve_kernel<6, false><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples, nullptr); break;
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_pnp_solve_split(bool quad, int ns, int nwgE, const int2* wgtE, int nwg64, const int2* wgt64,
+hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwg64, const int2* wgt64,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
                                   hipEvent_t eig_begin, hipEvent_t eig_end) {
@@ -899,10 +819,7 @@ hipError_t launch_pnp_solve_split(bool quad, int ns, int nwgE, const int2* wgtE,
     switch (ns) {
 #define RSC_CASE(N)                                                                                   \
     case N:                                                                                           \
-        if (quad)                                                                                     \
-            pnp_eig_group_kernel<N><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples);        \
-        else                                                                                          \
-            pnp_eig_lane_kernel<N><<<nwg64, 64, 0, st>>>(probs, lps, wgt64, T, stage, samples);       \
+        pnp_eig_group_kernel<N><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples);            \
         if (eig_end) (void)hipEventRecord(eig_end, st);                                               \
         pnp_betas_kernel<N><<<3 * nwg64, 64, 0, st>>>(probs, lps, wgt64, nwg64, stage, samples, poses, \
                                                       bs.err, bs.pose, bs.ctr, bs.hcap);              \
@@ -1019,12 +936,6 @@ hipError_t launch_rng_stream(const uint32_t* T, const uint32_t* window, int g0, 
     Window31 w;
     for (int j = 0; j < 31; ++j) w.w[j] = window[j];
     rng_stream_kernel<<<(n + 255) / 256, 256, 0, st>>>(T, w, g0, n, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_pnp_solve_stamped(int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
-                                    const uint32_t* T, float* poses, uint64_t* stamps, hipStream_t st) {
-    pnp_solve_kernel<4, true><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, nullptr, stamps);
     return hipGetLastError();
 }
 

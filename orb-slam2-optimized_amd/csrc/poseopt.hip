@@ -11,6 +11,7 @@
 // popped to the state currentChi belongs to), so it is reused bit for bit instead of refolded, and
 // the per-edge errors are recomputed only when the last trial was rejected.
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cfloat>
 #include "rsc_poseopt.h"
 #include "rsc_kernels.h"
@@ -276,14 +277,19 @@ __global__ __launch_bounds__(kPoseChunk) void poseopt_kernel(const DevPoseProb* 
     }
 }
 
-hipError_t poseopt_prepare_device() {
-    // the ~115 KB dynamic-LDS launch needs the per-device attribute raised (rsc_context_create, once
-    // per context: hipFuncSetAttribute applies to the current device)
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&poseopt_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPoseLds);
-}
-
 hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st) {
+    // the dynamic-LDS size above 64 KB needs the per-device function attribute: raised lazily at
+    // this kernel's first launch on each device, so only callers of this path depend on it
+    static std::atomic<unsigned long long> raised{0};
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (!((raised.load(std::memory_order_acquire) >> dev) & 1ull)) {
+        if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&poseopt_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPoseLds))
+            return e;
+        raised.fetch_or(1ull << dev, std::memory_order_acq_rel);
+    }
     poseopt_kernel<<<count, kPoseChunk, kPoseLds, st>>>(probs);
     return hipGetLastError();
 }

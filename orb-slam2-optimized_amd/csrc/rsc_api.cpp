@@ -194,10 +194,6 @@ struct rsc_context {
     PinBuf<char> h_bow;
     int mask_words = 0;  // per hypothesis, last speculation
     bool keep_samples = true;
-    // PnP hypothesis kernels ($RSC_SOLVE_MODE): 0 = auto, 1 = "mono" (one kernel, lane per
-    // hypothesis), 2 = "quad" (quad-cooperative eigenvectors + per-approximation waves),
-    // 3 = "split" (lane-per-hypothesis eigenvectors + per-approximation waves).
-    int solve_mode = 0;
     // timing
     bool timing = false;
     hipEvent_t ev[12] = {};  // [0..5] phase marks, [6+2g], [7+2g] eigen-stage kernel of sample-size group g
@@ -274,10 +270,25 @@ namespace {
 // across rounds (one Blob is alive at a time per thread), so a round allocates nothing here.
 struct Blob {
     std::vector<char>& bytes;
-    Blob() : bytes(scratch()) { bytes.clear(); }
+    Blob() : bytes(scratch()) {
+        // one Blob per thread at a time: a nested one would truncate the open one's descriptors
+        if (in_use()) {
+            std::fprintf(stderr, "rsc: nested launch-descriptor Blob on one thread\n");
+            std::abort();
+        }
+        in_use() = true;
+        bytes.clear();
+    }
+    ~Blob() { in_use() = false; }
+    Blob(const Blob&) = delete;
+    Blob& operator=(const Blob&) = delete;
     static std::vector<char>& scratch() {
         thread_local std::vector<char> v;
         return v;
+    }
+    static bool& in_use() {
+        thread_local bool f = false;
+        return f;
     }
     size_t add(const void* p, size_t n) {
         size_t off = (bytes.size() + 15) & ~(size_t)15;
@@ -329,7 +340,6 @@ void timing_begin(rsc_context* C, int slot) {
 // ------------------------------------------------------------------------------------------------
 struct HipPnPBackend : PnPBackend {
     rsc_context* C;
-    uint64_t* diag_stamps = nullptr;  // diagnostic phase-stamp build (rsc_diag_pnp_phase_stamps)
     std::vector<rsc_pnp*> solvers;  // index = state slot in the current call
     explicit HipPnPBackend(rsc_context* c) : C(c) {}
     rsc_pnp* of(PnPState* s) {
@@ -394,11 +404,9 @@ struct HipPnPBackend : PnPBackend {
         std::vector<int2>* quad_wgs = quad_wgs_tl;
         std::vector<int4>& scan_wgs = scan_wgs_tl;
         const int HC = scan_chunk(total);  // hypotheses per scan workgroup
-        const int mode = diag_stamps ? 1 : (C->solve_mode ? C->solve_mode : kAutoSolveMode);
-        const bool quad = (mode == 2), split = (mode == 2 || mode == 3);
-        // The tables depend only on the round's shape (count, sample size and H per problem, HC,
-        // mode): a round with the shape of the previous one on this thread reuses them (building
-        // and XCD-ordering ~3.7k entries costs ~10 us of host time per config-2 round).
+        // The tables depend only on the round's shape (count, sample size and H per problem, HC):
+        // a round with the shape of the previous one on this thread reuses them (building and
+        // XCD-ordering ~3.7k entries costs ~10 us of host time per config-2 round).
         thread_local std::vector<int> shape_tl;
         std::vector<int>& shape = shape_tl;
         thread_local std::vector<int> key_tl;
@@ -406,7 +414,6 @@ struct HipPnPBackend : PnPBackend {
         key.clear();
         key.push_back(count);
         key.push_back(HC);
-        key.push_back(mode);
         for (int i = 0; i < count; ++i) {
             key.push_back(S[i]->mRansacMinSet);
             key.push_back(H[i]);
@@ -417,8 +424,7 @@ struct HipPnPBackend : PnPBackend {
             for (int i = 0; i < count; ++i) {
                 const int g = S[i]->mRansacMinSet - 4;
                 for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs[g].push_back(make_int2(i, h0));
-                if (quad)
-                    for (int h0 = 0; h0 < H[i]; h0 += kEigHyps) quad_wgs[g].push_back(make_int2(i, h0));
+                for (int h0 = 0; h0 < H[i]; h0 += kEigHyps) quad_wgs[g].push_back(make_int2(i, h0));
                 for (int h0 = 0; h0 < H[i]; h0 += HC)
                     scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
             }
@@ -442,53 +448,32 @@ struct HipPnPBackend : PnPBackend {
         int32_t* cnt_dst = nullptr;
         if (int e = counts_target(C, total, &cnt_dst)) return e;
         if (int e = C->d_masks.ensure((size_t)total * mw)) return e;
-        if (C->keep_samples || split)
-            if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
-        BetasScratch bs{};
-        if (split) {
-            if (int e = C->d_stage.ensure((size_t)total * kStageDoubles)) return e;
-            if (int e = C->d_berr.ensure((size_t)total * 3)) return e;
-            if (int e = C->d_bpose.ensure((size_t)total * 36)) return e;
-            size_t groups = 0;
-            for (int g = 0; g < 3; ++g) groups = std::max(groups, solve_wgs[g].size());
-            const size_t had = C->d_bctr.cap;
-            if (int e = C->d_bctr.ensure(groups)) return e;
-            if (C->d_bctr.cap != had) RSC_HIP(hipMemsetAsync(C->d_bctr.p, 0, C->d_bctr.cap * sizeof(unsigned), C->stream));
-            bs = BetasScratch{C->d_berr.p, C->d_bpose.p, C->d_bctr.p, (size_t)total};
-        }
+        if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
+        if (int e = C->d_stage.ensure((size_t)total * kStageDoubles)) return e;
+        if (int e = C->d_berr.ensure((size_t)total * 3)) return e;
+        if (int e = C->d_bpose.ensure((size_t)total * 36)) return e;
+        size_t groups = 0;
+        for (int g = 0; g < 3; ++g) groups = std::max(groups, solve_wgs[g].size());
+        const size_t had = C->d_bctr.cap;
+        if (int e = C->d_bctr.ensure(groups)) return e;
+        if (C->d_bctr.cap != had) RSC_HIP(hipMemsetAsync(C->d_bctr.p, 0, C->d_bctr.cap * sizeof(unsigned), C->stream));
+        const BetasScratch bs{C->d_berr.p, C->d_bpose.p, C->d_bctr.p, (size_t)total};
         const char* base = C->d_desc.p;
         const DevPnP* dprobs = reinterpret_cast<const DevPnP*>(base + o_probs);
         const LaunchProb* dlps = reinterpret_cast<const LaunchProb*>(base + o_lps);
         host_mark(C, 0);
         timing_begin(C, 0);
-        if (diag_stamps) {
-            DevBuf<uint64_t> d;
-            if (int e = d.ensure((size_t)total * 10)) return e;
-            RSC_HIP(launch_pnp_solve_stamped((int)solve_wgs[0].size(), dprobs, dlps,
-                                             reinterpret_cast<const int2*>(base + o_solve[0]), C->d_table.p,
-                                             C->d_poses.p, d.p, C->stream));
-            RSC_HIP(hipMemcpyAsync(diag_stamps, d.p, (size_t)total * 80, hipMemcpyDeviceToHost, C->stream));
-            RSC_HIP(hipStreamSynchronize(C->stream));
-        } else {
-            bool first_group = true;
-            for (int g = 0; g < 3; ++g) {
-                if (solve_wgs[g].empty()) continue;
-                if (split) {
-                    // the first group's eigen stage starts at ev[0]: no extra event in the queue
-                    hipEvent_t eb = (C->timing && !first_group) ? C->ev[6 + 2 * g] : nullptr;
-                    RSC_HIP(launch_pnp_solve_split(quad, 4 + g, (int)quad_wgs[g].size(),
-                                                  reinterpret_cast<const int2*>(base + o_quad[g]),
-                                                  (int)solve_wgs[g].size(),
-                                                  reinterpret_cast<const int2*>(base + o_solve[g]), dprobs, dlps,
-                                                  C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p, bs,
-                                                  C->stream, eb, C->timing ? C->ev[7 + 2 * g] : nullptr));
-                    first_group = false;
-                } else {
-                    RSC_HIP(launch_pnp_solve(4 + g, (int)solve_wgs[g].size(), dprobs, dlps,
-                                             reinterpret_cast<const int2*>(base + o_solve[g]), C->d_table.p,
-                                             C->d_poses.p, C->keep_samples ? C->d_samples.p : nullptr, C->stream));
-                }
-            }
+        bool first_group = true;
+        for (int g = 0; g < 3; ++g) {
+            if (solve_wgs[g].empty()) continue;
+            // the first group's eigen stage starts at ev[0]: no extra event in the queue
+            hipEvent_t eb = (C->timing && !first_group) ? C->ev[6 + 2 * g] : nullptr;
+            RSC_HIP(launch_pnp_solve_split(4 + g, (int)quad_wgs[g].size(),
+                                          reinterpret_cast<const int2*>(base + o_quad[g]), (int)solve_wgs[g].size(),
+                                          reinterpret_cast<const int2*>(base + o_solve[g]), dprobs, dlps,
+                                          C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p, bs, C->stream,
+                                          eb, C->timing ? C->ev[7 + 2 * g] : nullptr));
+            first_group = false;
         }
         timing_begin(C, 1);
         RSC_HIP(launch_pnp_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
@@ -507,15 +492,13 @@ struct HipPnPBackend : PnPBackend {
             C->last_ms[1] += s;
             C->last_ms[3] += 1;
             C->last_ms[4] += total;
-            if (split && !diag_stamps) {
-                bool first_group = true;
-                for (int g = 0; g < 3; ++g) {
-                    if (solve_wgs[g].empty()) continue;
-                    float e = 0;
-                    (void)hipEventElapsedTime(&e, first_group ? C->ev[0] : C->ev[6 + 2 * g], C->ev[7 + 2 * g]);
-                    C->last_ms[5] += e;
-                    first_group = false;
-                }
+            bool first = true;
+            for (int g = 0; g < 3; ++g) {
+                if (solve_wgs[g].empty()) continue;
+                float e = 0;
+                (void)hipEventElapsedTime(&e, first ? C->ev[0] : C->ev[6 + 2 * g], C->ev[7 + 2 * g]);
+                C->last_ms[5] += e;
+                first = false;
             }
         }
         counts.resize(count);  // keeps the inner vectors' capacity
@@ -617,6 +600,7 @@ struct HipSim3Backend : Sim3Backend {
     std::vector<rsc_sim3*> all;
 
     int speculate(Sim3State* const* S, int count, const int* H, std::vector<std::vector<int32_t>>& counts) override {
+        pick_valid = false;  // set again only once this round's pick kernel is enqueued
         int total = 0, maxN = 1;
         // per-thread scratch that keeps its capacity across rounds (no allocation per round)
         thread_local std::vector<DevSim3> probs_tl;
@@ -681,11 +665,11 @@ struct HipSim3Backend : Sim3Backend {
         if (int e = C->d_poses.ensure((size_t)total * 24)) return e;
         // the kept pose comes back with the counts (sim3_pick_kernel) when every solver's round
         // fits the pick kernel's LDS
-        pick_valid = true;
-        for (int i = 0; i < count; ++i) pick_valid = pick_valid && H[i] <= kPickMaxH;
+        bool use_pick = true;
+        for (int i = 0; i < count; ++i) use_pick = use_pick && H[i] <= kPickMaxH;
         int32_t* cnt_dst = nullptr;
         if (int e = counts_target(C, total, &cnt_dst)) return e;
-        if (pick_valid) {
+        if (use_pick) {
             if (int e = C->d_counts.ensure((size_t)total)) return e;
             if (int e = C->h_pick.ensure((size_t)count * 16)) return e;
         }
@@ -699,12 +683,14 @@ struct HipSim3Backend : Sim3Backend {
         RSC_HIP(launch_sim3_solve((int)solve_wgs.size(), dprobs, dlps, reinterpret_cast<const int2*>(base + o_solve),
                                   C->d_table.p, C->d_poses.p, C->keep_samples ? C->d_samples.p : nullptr, C->stream));
         timing_begin(C, 1);
-        int32_t* cnt_dev = (pick_valid && C->direct_counts) ? C->d_counts.p : nullptr;  // else cnt_dst is HBM
+        int32_t* cnt_dev = (use_pick && C->direct_counts) ? C->d_counts.p : nullptr;  // else cnt_dst is HBM
         RSC_HIP(launch_sim3_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
                                  C->d_poses.p, cnt_dst, cnt_dev, C->d_masks.p, mw, C->stream));
         timing_begin(C, 2);
-        if (pick_valid)
+        if (use_pick) {
             RSC_HIP(launch_sim3_pick(count, dlps, C->d_counts.p, C->d_poses.p, C->h_pick.p, C->stream));
+            pick_valid = true;
+        }
         if (!C->direct_counts)
             RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
         RSC_HIP(hipStreamSynchronize(C->stream));
@@ -956,19 +942,12 @@ int rsc_context_create(int device, rsc_context** out) {
     C->device = device;
     RSC_HIP(hipStreamCreateWithFlags(&C->stream, hipStreamNonBlocking));
     C->own_stream = true;
-    if (const char* m = std::getenv("RSC_SOLVE_MODE")) {
-        if (!std::strcmp(m, "mono")) C->solve_mode = 1;
-        else if (!std::strcmp(m, "quad")) C->solve_mode = 2;
-        else if (!std::strcmp(m, "split")) C->solve_mode = 3;
-    }
     if (const char* m = std::getenv("RSC_DIRECT_COUNTS")) C->direct_counts = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_DMA_UPLOAD")) C->dma_upload = std::strcmp(m, "0") != 0;
     C->table.build();
     if (int e = C->d_table.ensure(C->table.T.size())) return e;
     RSC_HIP(hipMemcpy(C->d_table.p, C->table.T.data(), C->table.T.size() * 4, hipMemcpyHostToDevice));
     for (auto& e : C->ev) RSC_HIP(hipEventCreate(&e));
-    RSC_HIP(poseopt_prepare_device());
-    RSC_HIP(sim3opt_prepare_device());
     *out = C.release();
     return RSC_OK;
 }
@@ -995,12 +974,6 @@ int rsc_context_set_stream(rsc_context* C, void* s) {
 int rsc_context_synchronize(rsc_context* C) {
     if (!C) return RSC_ERR_ARG;
     RSC_HIP(hipStreamSynchronize(C->stream));
-    return RSC_OK;
-}
-
-int rsc_context_set_solve_mode(rsc_context* C, int mode) {
-    if (!C || mode < 0 || mode > 3) return RSC_ERR_ARG;
-    C->solve_mode = mode;
     return RSC_OK;
 }
 
@@ -2295,31 +2268,6 @@ int rsc_sim3_set_ransac_parameters_many(rsc_sim3* const* s, int count, double pr
     }
     return RSC_OK;
 }
-
-// ---- diagnostics (not part of the drop-in boundary) ----
-// s_memtime stamps at the phase boundaries of the EPnP solve for H hypotheses of each solver
-// (min_set 4, state unchanged): out[(solver*H + h)*10 + k].
-int rsc_diag_pnp_phase_stamps(rsc_pnp* const* solvers, int count, int H, uint64_t* out) {
-    if (count <= 0 || !solvers || !out || H <= 0) return RSC_ERR_ARG;
-    rsc_context* C = solvers[0]->ctx;
-    RSC_HIP(hipSetDevice(C->device));
-    HipPnPBackend be(C);
-    be.solvers.assign(solvers, solvers + count);
-    be.diag_stamps = out;
-    std::vector<PnPState*> S(count);
-    std::vector<int> Hs(count, H);
-    std::vector<RngStream> keep(count);
-    for (int i = 0; i < count; ++i) {
-        S[i] = &solvers[i]->st;
-        if (S[i]->mRansacMinSet != 4) return RSC_ERR_UNSUPPORTED;
-        keep[i] = S[i]->rng;
-    }
-    std::vector<std::vector<int32_t>> counts;
-    int st = be.speculate(S.data(), count, Hs.data(), counts);
-    for (int i = 0; i < count; ++i) S[i]->rng = keep[i];
-    return st;
-}
-
 
 // ---- MLPnP ----
 int rsc_mlpnp_create(rsc_context* C, const rsc_pnp_problem* pb, uint32_t seed, rsc_mlpnp** out) {

@@ -84,18 +84,15 @@ hipError_t launch_gather_records(const float* src, int stride, int take, const i
                                  hipStream_t st);
 hipError_t launch_rng_stream(const uint32_t* T, const uint32_t* window, int g0, int n, int32_t* out, hipStream_t st);
 
-hipError_t launch_pnp_solve(int ns, int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
-                            const uint32_t* T, float* poses, int32_t* samples, hipStream_t st);
 constexpr int kEigLanes = 2;           // lanes per hypothesis in the eigen-stage kernel (rsc_quad.h)
 #ifndef RSC_EIG_HYPS
 #define RSC_EIG_HYPS 20  // build-time override for A/B runs (tools/)
 #endif
 constexpr int kEigHyps = RSC_EIG_HYPS;  // hypotheses per 64-lane eigen-stage workgroup (960 on config 2)
-constexpr int kAutoSolveMode = 2;      // see rsc_context::solve_mode
 // Per-hypothesis stage record between the two kernels: eigenvectors [12][4], alphas [NS][4], cws [4][3].
 constexpr int kStageDoubles = 48 + 24 + 12;
-// Two-kernel hypothesis solve: eigenvectors (quad-cooperative or lane per hypothesis), then the
-// three beta approximations (one wave each) + selection.
+// Two-kernel hypothesis solve: eigenvectors (lane groups), then the three beta approximations
+// (one wave each) + selection.
 // Hand-off buffers of pnp_betas_kernel: per record and approximation the error (`err[3][hcap]`)
 // and the float pose (`pose[3][12][hcap]`); one counter per 64-hypothesis group, zero between
 // launches (the kernel resets what it uses).
@@ -105,12 +102,10 @@ struct BetasScratch {
     unsigned* ctr;
     size_t hcap;
 };
-hipError_t launch_pnp_solve_split(bool quad, int ns, int nwgE, const int2* wgtE, int nwg64, const int2* wgt64,
+hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwg64, const int2* wgt64,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
                                   hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr);
-hipError_t launch_pnp_solve_stamped(int nwg, const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
-                                    const uint32_t* T, float* poses, uint64_t* stamps, hipStream_t st);
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,
                            const float* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st);
 hipError_t read_refine_stamps(uint64_t* out);  // diagnostic, [64][8]

@@ -429,7 +429,6 @@ RSC_HD bool po_ldlt_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[
 
 #if defined(__HIPCC__)
 hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st);
-hipError_t poseopt_prepare_device();
 #endif
 
 }  // namespace rsc

@@ -28,9 +28,7 @@ constexpr int kQuadE = 55;   // Householder essential vectors
 constexpr int kQuadRegion = kQuadT + kQuadE + 1;  // 200 doubles per hypothesis
 // stage record offsets (rsc_kernels.h kStageDoubles)
 constexpr int kStEv = 0, kStAl = 48, kStCws = 72;
-// pnp_betas_body LDS (three-wave form, tools/quad_bench): eigenvectors [48][64], L+rho [66][64],
-// errors [3][64], poses [3][12][64] f32.  pnp_betas_wave_body (product): L+rho [66][64] only.
-constexpr int kBetasSmemDoubles = (48 + 66) * 64 + 3 * 64 + 3 * 12 * 64 / 2;
+// pnp_betas_wave_body LDS: L + rho [66][64].
 constexpr int kBetasWaveSmemDoubles = 66 * 64;
 
 // Offset of step i's essential Householder vector (entries v[1..10-i]) in the E region.
@@ -214,14 +212,6 @@ struct GroupLdsRows {
     }
 };
 
-// The quad's own three rows of Q as the rotation sink of tridiag_qr_events12 (diagnostic variant).
-struct QuadRowsEv {
-    double* T;
-    int q;
-    RSC_HD double load(int r, int col) const { return T[(4 * r + q) * 12 + col]; }
-    RSC_HD void store(int r, int col, double v) { T[(4 * r + q) * 12 + col] = v; }
-};
-
 // Scale of SelfAdjointEigenSolver = max |lower triangle| over the group's own rows (A: full
 // symmetric own rows, R = L*j + q); a NaN M(0,0) poisons it, as there.
 template <int L>
@@ -306,13 +296,12 @@ __device__ __forceinline__ void group_eig12_ev4(double* T, double* E, int q, Syn
 // 1,024 SIMDs — the last 176 SIMDs run two waves back to back — but 960 pair waves of 20
 // hypotheses (kEigHyps), one per SIMD; 32 per pair wave (600 waves) leaves SIMDs idle at the same
 // per-wave latency (tools/qr_bench).
-template <int NS, int STOP, int L, int HPW, bool EVQR = false>
+template <int NS, int STOP, int L, int HPW>
 __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
                                                    const int2* __restrict__ wg_table, const uint32_t* __restrict__ rng_T,
                                                    double* __restrict__ stage, int32_t* __restrict__ samples,
                                                    double* smem) {
     static_assert(HPW * L <= 64 && (L == 2 || L == 4), "lane groups of 2 or 4 within one wave");
-    static_assert(!EVQR || L == 4, "event-form QR: quads only");
     constexpr int RJ = 12 / L;
     const int lane = threadIdx.x, g = lane / L, q = lane % L;
     if (g >= HPW) return;  // whole groups only: the DPP broadcasts never read a departed lane
@@ -408,23 +397,12 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
 
     // ---- D: implicit symmetric QR, rotations applied to the own rows ----
     // Sweep form: the own rows of Q stay in LDS (T, row-major), so the rotations' read-modify-
-    // writes are off the Givens chase's dependency chain.  The event form (tridiag_qr_events12,
-    // EVQR = true: each quad steps through its own sequence of sweep setups and single rotations)
-    // is bit-identical but measured slower on gfx950 (eig 175 us vs 164 us on config 2 with quads,
-    // tools/quad_bench): the union of the quads' sweep windows is only ~12% above the per-quad
-    // event count (tools/qr_stats), less than the event form's extra control flow costs.
+    // writes are off the Givens chase's dependency chain.  (The event and split-chase forms of the
+    // QR, tools/qr_events.h, are bit-identical and measured slower on gfx950)
     {
         int perm[12];
-        if constexpr (EVQR) {
-            double* ds = E;
-            RSC_UNROLL for (int i = 0; i < 12; ++i) ds[i] = diag[i];
-            RSC_UNROLL for (int i = 0; i < 11; ++i) ds[12 + i] = sub[i];
-            QuadRowsEv rows{T, q};
-            tridiag_qr_events12<3>(ds, rows, perm);
-        } else {
-            GroupLdsRows<L> qapply{T, q};
-            tridiag_qr<double, 12>(diag, sub, qapply, perm);
-        }
+        GroupLdsRows<L> qapply{T, q};
+        tridiag_qr<double, 12>(diag, sub, qapply, perm);
         // sorted eigenvector columns 0..3 (the four smallest eigenvalues) of the own rows
         if (active) {
             RSC_UNROLL for (int j = 0; j < RJ; ++j) {
@@ -438,131 +416,6 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
                 }
             }
         }
-    }
-}
-
-// Kernel 1, lane form: one lane per hypothesis (sample, control points, alphas, MtM, 12x12
-// eigenvectors in the per-lane LDS slab), same stage record as the quad form.
-template <int NS>
-__device__ __forceinline__ void pnp_eig_lane_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
-                                                  const int2* __restrict__ wg_table, const uint32_t* __restrict__ rng_T,
-                                                  double* __restrict__ stage, int32_t* __restrict__ samples,
-                                                  double* slab) {
-    const int lane = threadIdx.x;
-    const int2 wt = wg_table[blockIdx.x];
-    const LaunchProb& lp = lps[wt.x];
-    const int h = wt.y + lane;
-    if (h >= lp.H) return;
-    const DevPnP& P = probs[lp.prob];
-    const size_t rec = (size_t)(lp.out0 + h);
-    double* out = stage + rec * kStageDoubles;
-    int idx[NS];
-    {
-        uint32_t w[31];
-        RSC_UNROLL for (int j = 0; j < 31; ++j) w[j] = lp.window[j];
-        uint32_t words[NS];
-        RSC_UNROLL for (int d = 0; d < NS; ++d) words[d] = rng_word(rng_T, w, lp.g0 + h * NS + d);
-        swap_remove_sample<NS>(words, NS, P.n, idx);
-    }
-    RSC_UNROLL for (int i = 0; i < NS; ++i) samples[rec * 8 + i] = idx[i];
-    const LaneMat S{slab + lane, 64};
-    {
-        HypStore<NS> st;
-        RSC_UNROLL for (int i = 0; i < NS; ++i) {
-            const float4 p = P.pts[idx[i]];
-            const float2 uv = P.uv[idx[i]];
-            st.pw_[i][0] = p.x; st.pw_[i][1] = p.y; st.pw_[i][2] = p.z;
-            st.u_[i][0] = uv.x; st.u_[i][1] = uv.y;
-        }
-        st.rows_ = P.rows;
-        st.spw = P.pws;
-        st.sal = P.als;
-        const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
-        double cws[4][3];
-        control_points_and_alphas(st, cws);
-        RSC_UNROLL for (int i = 0; i < NS; ++i)
-            RSC_UNROLL for (int j = 0; j < 4; ++j) out[kStAl + i * 4 + j] = st.al(i, j);
-        RSC_UNROLL for (int i = 0; i < 4; ++i)
-            RSC_UNROLL for (int c = 0; c < 3; ++c) out[kStCws + i * 3 + c] = cws[i][c];
-        build_MtM(st, K, S);
-    }
-    sym_eig12(S);
-    RSC_UNROLL for (int r = 0; r < 12; ++r)
-        RSC_UNROLL for (int c = 0; c < 4; ++c) out[kStEv + r * 4 + c] = S.at(r, c);
-}
-
-// Kernel 2: 192 threads = 3 waves over the same 64 hypotheses; wave w runs find_betas_approx_{w+1}
-// + gauss_newton + compute_R_and_t (PnPsolver.cpp:383-408), wave 0 keeps the smallest error in the
-// reference's order (:393-414) and writes the float pose.  FORCE >= 0 (diagnostics only,
-// tools/quad_bench) makes every wave run approximation FORCE + 1.
-template <int NS, int FORCE = -1>
-__device__ __forceinline__ void pnp_betas_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
-                                               const int2* __restrict__ wg_table, const double* __restrict__ stage,
-                                               const int32_t* __restrict__ samples, float* __restrict__ poses,
-                                               double* smem) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int apx = FORCE >= 0 ? FORCE : wave;
-    const int2 wt = wg_table[blockIdx.x];
-    const LaunchProb& lp = lps[wt.x];
-    const bool active = wt.y + lane < lp.H;
-    const int h = active ? wt.y + lane : lp.H - 1;
-    const DevPnP& P = probs[lp.prob];
-    const size_t rec = (size_t)(lp.out0 + h);
-    const double* in = stage + rec * kStageDoubles;
-    double* EV = smem;
-    double* LR = EV + 48 * 64;
-    double* ERR = LR + 66 * 64;
-    float* PZ = reinterpret_cast<float*>(ERR + 3 * 64);
-    RSC_UNROLL for (int e = 0; e < 16; ++e) EV[(16 * wave + e) * 64 + lane] = in[kStEv + 16 * wave + e];
-    __syncthreads();
-    const SplitView V{EV + lane, LR + lane, 64};
-    if (wave == 0) {
-        compute_L_6x10(V);
-        double cws[4][3];
-        RSC_UNROLL for (int i = 0; i < 4; ++i)
-            RSC_UNROLL for (int c = 0; c < 3; ++c) cws[i][c] = in[kStCws + i * 3 + c];
-        auto d2 = [&](int a, int b) {
-            double x = cws[a][0] - cws[b][0], y = cws[a][1] - cws[b][1], z = cws[a][2] - cws[b][2];
-            return x * x + y * y + z * z;
-        };
-        V.rho(0) = d2(0, 1); V.rho(1) = d2(0, 2); V.rho(2) = d2(0, 3);
-        V.rho(3) = d2(1, 2); V.rho(4) = d2(1, 3); V.rho(5) = d2(2, 3);
-    }
-    __syncthreads();
-    double betas[4] = {0.0, 0.0, 0.0, 0.0};
-    if (apx == 0) find_betas<1>(V, betas);
-    else if (apx == 1) find_betas<2>(V, betas);
-    else find_betas<3>(V, betas);
-    gauss_newton(V, betas);
-    // the hypothesis' points and alphas are read only now: live across the solves above they
-    // pushed the wave past 256 VGPRs (scratch spills, round 1)
-    HypStore<NS> st;
-    RSC_UNROLL for (int i = 0; i < NS; ++i) {
-        const int id = samples[rec * 8 + i];
-        const float4 p = P.pts[id];
-        const float2 uv = P.uv[id];
-        st.pw_[i][0] = p.x; st.pw_[i][1] = p.y; st.pw_[i][2] = p.z;
-        st.u_[i][0] = uv.x; st.u_[i][1] = uv.y;
-        RSC_UNROLL for (int j = 0; j < 4; ++j) st.al_[i][j] = in[kStAl + i * 4 + j];
-    }
-    st.rows_ = P.rows;
-    st.spw = P.pws;
-    st.sal = P.als;
-    const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
-    const double pw0[3] = {in[kStCws + 0], in[kStCws + 1], in[kStCws + 2]};
-    double R[3][3], t[3];
-    ERR[wave * 64 + lane] = compute_R_and_t(st, K, V, betas, pw0, R, t);
-    RSC_UNROLL for (int r = 0; r < 3; ++r)
-        RSC_UNROLL for (int c = 0; c < 3; ++c) PZ[(wave * 12 + 3 * r + c) * 64 + lane] = (float)R[r][c];
-    RSC_UNROLL for (int r = 0; r < 3; ++r) PZ[(wave * 12 + 9 + r) * 64 + lane] = (float)t[r];
-    __syncthreads();
-    if (wave == 0 && active) {
-        int best = 0;
-        double be = ERR[lane];
-        if (ERR[64 + lane] < be) { be = ERR[64 + lane]; best = 1; }
-        if (ERR[128 + lane] < be) { be = ERR[128 + lane]; best = 2; }
-        float* o = poses + rec * 12;
-        RSC_UNROLL for (int k = 0; k < 12; ++k) o[k] = PZ[(best * 12 + k) * 64 + lane];
     }
 }
 
@@ -634,7 +487,8 @@ __device__ __forceinline__ void pnp_betas_wave_body(const DevPnP* __restrict__ p
     else if (apx == 1) find_betas<2>(V, betas);
     else find_betas<3>(V, betas);
     gauss_newton(V, betas);
-    // the hypothesis' points and alphas are read only now (register pressure, see pnp_betas_body)
+    // the hypothesis' points and alphas are read only now (live across the solves above they pushed
+    // the wave past 256 VGPRs: scratch spills, round 1)
     HypStore<NS> st;
     RSC_UNROLL for (int i = 0; i < NS; ++i) {
         const int id = samples[rec * 8 + i];

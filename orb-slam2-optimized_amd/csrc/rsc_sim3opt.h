@@ -193,7 +193,6 @@ RSC_HD void so_quad_terms(const SoPerturbed& P, bool inverse, const SoCam& K, co
 
 #if defined(__HIPCC__)
 hipError_t launch_sim3opt(int count, const DevSim3OptProb* probs, hipStream_t st);
-hipError_t sim3opt_prepare_device();
 #endif
 
 }  // namespace rsc

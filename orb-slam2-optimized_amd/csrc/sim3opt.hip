@@ -7,6 +7,7 @@
 // wave 1.  The LM control, the 7x7 LDLT and the 14 perturbed estimates of the numeric Jacobian run
 // redundantly in every lane (bit-identical values, no broadcast).
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cfloat>
 #include "rsc_sim3opt.h"
 #include "rsc_fold.h"
@@ -247,12 +248,19 @@ __global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptPro
     if (tid == 0) so_write(P, S, cnt_sh, nBad, L);
 }
 
-hipError_t sim3opt_prepare_device() {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sim3opt_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSoLds);
-}
-
 hipError_t launch_sim3opt(int count, const DevSim3OptProb* probs, hipStream_t st) {
+    // the dynamic-LDS size above 64 KB needs the per-device function attribute: raised lazily at
+    // this kernel's first launch on each device, so only callers of this path depend on it
+    static std::atomic<unsigned long long> raised{0};
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (!((raised.load(std::memory_order_acquire) >> dev) & 1ull)) {
+        if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sim3opt_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSoLds))
+            return e;
+        raised.fetch_or(1ull << dev, std::memory_order_acq_rel);
+    }
     sim3opt_kernel<<<count, kSoThreads, kSoLds, st>>>(probs);
     return hipGetLastError();
 }

@@ -29,7 +29,7 @@ u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
 # Every symbol declared in include/rsc.h (checked by tests/test_cpu_abi.py).
 EXPORTED = [
     "rsc_version", "rsc_status_string", "rsc_context_create", "rsc_context_destroy", "rsc_context_set_stream",
-    "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_last_kernel_timing", "rsc_diag_host_timing", "rsc_context_enable_timing", "rsc_selftest_math", "rsc_context_set_solve_mode",
+    "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_last_kernel_timing", "rsc_diag_host_timing", "rsc_context_enable_timing", "rsc_selftest_math",
     "rsc_pnp_create", "rsc_pnp_destroy", "rsc_pnp_set_ransac_parameters", "rsc_pnp_iterate", "rsc_pnp_find",
     "rsc_pnp_iterate_many", "rsc_pnp_reset", "rsc_pnp_get_state", "rsc_pnp_last_samples", "rsc_pnp_last_hypotheses",
     "rsc_sim3_last_hypotheses", "rsc_mlpnp_last_counts",
@@ -327,7 +327,6 @@ def load_library(path: str = LIB_PATH):
     L.rsc_context_last_kernel_timing.argtypes = [vp, C.POINTER(C.c_double)]
     L.rsc_diag_host_timing.argtypes = [vp, C.POINTER(C.c_double)]
     L.rsc_context_enable_timing.argtypes = [vp, C.c_int]
-    L.rsc_context_set_solve_mode.argtypes = [vp, C.c_int]
     L.rsc_pnp_create.argtypes = [vp, C.POINTER(PnPProblem), C.c_uint32, C.POINTER(vp)]
     L.rsc_pnp_destroy.argtypes = [vp]
     L.rsc_pnp_set_ransac_parameters.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
@@ -405,8 +404,6 @@ def load_library(path: str = LIB_PATH):
     L.rsc_kfdb_detect_loop.argtypes = [vp, C.c_uint64, C.c_int, u32p_, f64p_, C.c_int, i32p, C.c_float, i32p, i32p]
     L.rsc_kfdb_state.argtypes = [vp, C.c_int, u64p_, i32p, f32p_]
     L.rsc_loop_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(Sim3Result), C.POINTER(EventResult)]
-    L.rsc_diag_pnp_phase_stamps.argtypes = [C.POINTER(vp), C.c_int, C.c_int,
-                                            np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
     _lib = L
     return L
 
@@ -453,12 +450,6 @@ class Context:
         _check(load_library().rsc_selftest_math(self.h, self.MATH_FNS[fn], x.ctypes.data_as(dp), int(x.size),
                                                 out.ctypes.data_as(dp)), "selftest_math")
         return out
-
-    SOLVE_MODES = {"auto": 0, "mono": 1, "quad": 2, "split": 3}
-
-    def set_solve_mode(self, mode: str):
-        """PnP hypothesis kernels: auto | mono | quad | split (bit-identical results)."""
-        _check(load_library().rsc_context_set_solve_mode(self.h, self.SOLVE_MODES[mode]), "set_solve_mode")
 
     def last_timing(self):
         out = (C.c_double * 6)()
@@ -794,12 +785,6 @@ class SolverBatch:
         self._its[:] = n_iterations
         _check(self._iter_f(self._h, len(self.solvers), self._its_p, self._raw, self._nomask), "iterate_many")
         return self._view
-
-    def phase_stamps(self, H):
-        """Diagnostic: per-hypothesis s_memtime stamps at the EPnP phase boundaries (PnP only)."""
-        out = np.zeros(len(self.solvers) * H * 10, np.uint64)
-        _check(load_library().rsc_diag_pnp_phase_stamps(self._h, len(self.solvers), H, out), "phase_stamps")
-        return out.reshape(len(self.solvers), H, 10)
 
 
 class EventBatch:

@@ -12,6 +12,7 @@
 #include "../../orb-slam2-optimized_amd/csrc/rsc_mlpnp.h"
 #include "../../orb-slam2-optimized_amd/csrc/rsc_poseopt.h"
 #include "../../orb-slam2-optimized_amd/csrc/rsc_sim3opt.h"
+#include "../../tools/qr_events.h"  // diagnostic QR forms (their bit-equality is tested)
 
 using namespace rsc;
 

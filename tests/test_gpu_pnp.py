@@ -131,13 +131,12 @@ def test_refine_failure_respeculation(case):
         assert g.state()["max_rows"] == o.info()["max_rows"]
 
 
-@pytest.mark.parametrize("mode", ["mono", "quad", "split"])
-def test_solve_modes_bitexact(mode):
-    """Every hypothesis-kernel family against the oracle (samples, counts, poses), min_set 4..6."""
+def test_min_sets_bitexact():
+    """The hypothesis kernels for every supported sample size against the oracle (samples, counts,
+    poses), min_set 4..6."""
     from rsc import engine
     rng = np.random.default_rng(7)
     c = engine.Context(0)
-    c.set_solve_mode(mode)
     for ms in (4, 5, 6):
         sc = synth.make_pnp_scene(rng, 700, 0.5)
         params = (0.99, 10, 300, ms, 0.5, 5.991)
@@ -146,7 +145,7 @@ def test_solve_modes_bitexact(mode):
         o = ol.OraclePnP(sc, 100 + ms)
         o.set_ransac_parameters(*params)
         for k in range(3):
-            assert_pnp_equal(g.iterate(37), o.iterate(37), f"{mode} ms={ms} call {k}")
+            assert_pnp_equal(g.iterate(37), o.iterate(37), f"ms={ms} call {k}")
 
 
 def test_batch_iterate_raw_matches_dicts():

@@ -15,6 +15,7 @@
 #include <type_traits>
 #include <vector>
 #include "../orb-slam2-optimized_amd/csrc/rsc_epnp.h"
+#include "qr_events.h"
 
 using namespace rsc;
 

@@ -6,24 +6,24 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
-#include "../orb-slam2-optimized_amd/csrc/rsc_quad.h"
+#include "quad_variants.h"
 
 using namespace rsc;
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
 // L lanes per hypothesis, HPW hypotheses per workgroup
-template <int STOP, int L, int HPW, bool EVQR = false>
+template <int STOP, int L, int HPW>
 __global__ __launch_bounds__(64) void eig_g(const DevPnP* probs, const LaunchProb* lps, const int2* wgt, const uint32_t* T,
                                             double* stage, int32_t* samples) {
     __shared__ __attribute__((aligned(16))) double smem[HPW * kQuadRegion];
-    pnp_eig_group_body<4, STOP, L, HPW, EVQR>(probs, lps, wgt, T, stage, samples, smem);
+    pnp_eig_group_body<4, STOP, L, HPW>(probs, lps, wgt, T, stage, samples, smem);
 }
-template <int STOP, bool EVQR = false>
+template <int STOP>
 __global__ __launch_bounds__(64, 2) void eig_k2(const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                                                 const uint32_t* T, double* stage, int32_t* samples) {
     __shared__ __attribute__((aligned(16))) double smem[16 * kQuadRegion];
-    pnp_eig_group_body<4, STOP, 4, 16, EVQR>(probs, lps, wgt, T, stage, samples, smem);
+    pnp_eig_group_body<4, STOP, 4, 16>(probs, lps, wgt, T, stage, samples, smem);
 }
 __global__ __launch_bounds__(64) void eig_lane_k(const DevPnP* probs, const LaunchProb* lps, const int2* wgt,
                                                   const uint32_t* T, double* stage, int32_t* samples) {
@@ -262,8 +262,7 @@ int main(int argc, char** argv) {
     printf("eig2 A (sample..MtM)  %8.1f us\n", timeit([&] { eig_k2<1><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
     printf("eig2 A+tridiag        %8.1f us\n", timeit([&] { eig_k2<2><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
     printf("eig2 A+tri+accum      %8.1f us\n", timeit([&] { eig_k2<3><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); }));
-    cmp("eig2 quad sweep-QR", [&] { eig_k2<99, false><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); });
-    cmp("eig2 quad event-QR", [&] { eig_k2<99, true><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); });
+    cmp("eig2 quad sweep-QR", [&] { eig_k2<99><<<n16, 64>>>(dprobs, dlps, dw16, dT, dst, dsm); });
     printf("pair32 A              %8.1f us\n", timeit([&] { eig_g<1, 2, 32><<<n32, 64>>>(dprobs, dlps, dw32, dT, dst, dsm); }));
     printf("pair32 A+tridiag      %8.1f us\n", timeit([&] { eig_g<2, 2, 32><<<n32, 64>>>(dprobs, dlps, dw32, dT, dst, dsm); }));
     printf("pair32 A+tri+accum    %8.1f us\n", timeit([&] { eig_g<3, 2, 32><<<n32, 64>>>(dprobs, dlps, dw32, dT, dst, dsm); }));
