@@ -58,7 +58,8 @@ def parse():
     p.add_argument("--strong", action="store_true", help="split one 64-candidate batch across the ranks")
     p.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-cores CPU baseline (0: auto)")
     p.add_argument("--no-cpu", action="store_true")
-    for s in ("sim3", "mlpnp", "events", "latency", "poseopt", "bow", "sim3match", "sim3opt", "kfdb"):
+    for s in ("sim3", "mlpnp", "events", "latency", "poseopt", "bow", "sim3match", "sim3opt", "kfdb", "config1",
+              "rccl-check"):
         p.add_argument(f"--no-{s}", action="store_true")
     p.add_argument("--only-headline", action="store_true", help="config 2 only (PMC passes)")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -66,7 +67,8 @@ def parse():
                         "share fewer GPUs to rehearse the launch and gather on a 1-GPU box)")
     a = p.parse_args()
     if a.only_headline:
-        for s in ("sim3", "mlpnp", "events", "latency", "poseopt", "bow", "sim3match", "sim3opt", "kfdb"):
+        for s in ("sim3", "mlpnp", "events", "latency", "poseopt", "bow", "sim3match", "sim3opt", "kfdb", "config1",
+                  "rccl_check"):
             setattr(a, f"no_{s}", True)
     return a
 
@@ -98,6 +100,7 @@ def launch_ranks(args) -> int:
 
 COLL_DEV = "cuda"  # device of the collective tensors: cuda for RCCL, cpu for gloo
 RESULT_OUT = sys.stdout  # where rank 0 prints the one JSON line
+RCCL1 = None  # world-1 RCCL process group (torch.distributed) for rccl_check, or the error text
 
 
 def dist_setup(args):
@@ -105,11 +108,29 @@ def dist_setup(args):
     share GPUs (device = LOCAL_RANK mod the visible count) and the collectives run on host tensors.
     For world > 1 the process's fd 1 is pointed at stderr (the collective libraries print
     connection banners on stdout) and the JSON line goes to a saved copy of the original stdout."""
-    global COLL_DEV, RESULT_OUT
+    global COLL_DEV, RESULT_OUT, RCCL1
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if world == 1 and args.dist_backend == "nccl" and not args.no_rccl_check:
+        # A world-1 RCCL process group, created before anything else touches the GPU, so the
+        # product's collective (all_gather_into_tensor of the result records on device) executes on
+        # a 1-GPU box too (rccl_check section, outside the timed regions: at N = 1 the step has no
+        # exchange).  A failure is reported in the JSON line, not fatal.
+        try:
+            import torch
+            import torch.distributed as tdist
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(port))
+            torch.cuda.set_device(local)
+            tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+            RCCL1 = tdist
+        except Exception as e:  # noqa: BLE001
+            RCCL1 = f"{type(e).__name__}: {e}"
     if world > 1:
         sys.stdout.flush()
         RESULT_OUT = os.fdopen(os.dup(1), "w")
@@ -144,11 +165,21 @@ def reduce_time_and_count(dist, dt, count):
 
 
 def cpu_threads(args) -> int:
+    """Threads of the all-cores CPU baseline: every CPU this process may run on
+    (os.sched_getaffinity), unless --cpu-threads or OMP_NUM_THREADS (the GPU box's declared CPU
+    share) set fewer; host_cpus() reports the counts beside it."""
     if args.cpu_threads > 0:
         return args.cpu_threads
+    n = len(os.sched_getaffinity(0))
     env = os.environ.get("OMP_NUM_THREADS")
-    n = int(env) if env and env.isdigit() else len(os.sched_getaffinity(0))
-    return max(1, min(n, 16))
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def host_cpus(threads):
+    return {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "all_cores_threads": threads}
 
 
 def median_batches(fn, warmup=3, reps=10):
@@ -280,28 +311,66 @@ def cpu_baseline_pnp(scenes, args, threads):
 # ------------------------------------------------------------------------------------------------
 # config 3 / 4
 # ------------------------------------------------------------------------------------------------
-def run_sim3(engine, ctx, pairs, args):
+def run_sharded(engine, ctx, batch, lo, hi, total, params, args, dist, world, steps, pack):
+    """One sharded RANSAC section (configs 3 and 4): every rank runs candidates [lo, hi) of the
+    section's `total` (seeds by global candidate index, so any world size gives the same records),
+    then ONE all-gather of the fixed-size result records (RCCL over xGMI) when world > 1.  Timed
+    like the headline: barrier + sync around K steps, max over ranks, hypotheses summed."""
+    from rsc import dist as rdist
     from rsc import workloads as wl
-    solvers = [engine.Sim3Solver(ctx, p, 1) for p in pairs]
-    batch = engine.SolverBatch(solvers)
-    C = len(pairs)
+    gather = None  # records per rank of the all-gather: the largest shard
+    if dist is not None:
+        import torch
+        counts = torch.tensor([hi - lo], dtype=torch.int64, device=COLL_DEV)
+        dist.all_reduce(counts, op=dist.ReduceOp.MAX)
+        gather = max(1, int(counts.item()))
+    ids = list(range(lo, hi))
+    state = {"records": None}
 
     def step(s):
-        batch.reset(wl.step_seeds(s, C))
-        batch.set_ransac_parameters(*wl.LOOP)
-        return int(batch.iterate_raw(args.iters)["iterations"].sum())
+        h = 0
+        rec = np.zeros((0, rdist.RECORD), np.float32)
+        if batch is not None:
+            batch.reset(wl.step_seeds(s, total)[lo:hi])
+            batch.set_ransac_parameters(*params)
+            outs = batch.iterate_raw(args.iters)
+            h = int(outs["iterations"].sum())
+            rec = pack(ids, outs)
+        if gather is not None:
+            rec = rdist.all_gather_records(dist, rec, gather, device=COLL_DEV)
+        state["records"] = rec
+        return h
 
     for s in range(args.warmup):
         step(s)
+    barrier(dist)
     ctx.synchronize()
     t0 = time.perf_counter()
     h = 0
-    for s in range(args.steps):
+    for s in range(steps):
         h += step(args.warmup + s)
     ctx.synchronize()
+    barrier(dist)
     dt = time.perf_counter() - t0
-    return dict(hyp_per_s=h / dt, ms_per_step=1e3 * dt / args.steps, hypotheses_per_step=h // args.steps,
-                pairs=C, correspondences=pairs[0].n1, solvers=solvers)
+    dt, h = reduce_time_and_count(dist, dt, h)
+    return dict(hyp_per_s=h / dt, ms_per_step=1e3 * dt / steps, hypotheses_per_step=h // steps,
+                steps=steps), state["records"]
+
+
+def run_sim3(engine, ctx, pairs, args, dist=None, rank=0, world=1):
+    """Config 3: 32 loop-closure KeyFrame pairs x 1000 matches, SetRansacParameters(0.99,20,300)
+    (LoopClosing.cpp:261) + iterate(300), the pairs (LoopClosing.cpp:238-265's candidates) sharded
+    across the ranks by cost."""
+    from rsc import dist as rdist
+    from rsc import workloads as wl
+    C = len(pairs)
+    lo, hi = rdist.shard_range(C, world, rank, [p.n1 for p in pairs])
+    solvers = [engine.Sim3Solver(ctx, p, 1) for p in pairs[lo:hi]]
+    batch = engine.SolverBatch(solvers) if solvers else None
+    r, rec = run_sharded(engine, ctx, batch, lo, hi, C, wl.LOOP, args, dist, world, args.steps, rdist.pack_sim3)
+    r.update(pairs=C, pairs_per_rank=hi - lo, correspondences=pairs[0].n1,
+             sharding=f"{world} rank(s), contiguous blocks by N, RCCL all-gather of {rdist.RECORD}-float records")
+    return r, solvers, rec
 
 
 def cpu_baseline_sim3(solvers, args, threads):
@@ -343,35 +412,25 @@ def mlpnp_covariances(sc):
     return cov + np.eye(3) * 1e-9
 
 
-def run_mlpnp(engine, ctx, scenes, args, with_cov=False):
-    """Config 4 on one GPU: 32 candidates x 4096 correspondences (128 over 4 GPUs), MLPnP
-    SetRansacParameters(0.99,10,300,6,0.5,5.991) (commented call Tracking.cpp:1227-1228),
-    iterate(300), exhaustive; with_cov: computePose's bearing-covariance branch (covMats given)."""
+def run_mlpnp(engine, ctx, scenes, args, with_cov=False, dist=None, rank=0, world=1):
+    """Config 4: 128 candidates x 4096 correspondences sharded across the ranks (BASELINE: over 4
+    MI355X; here over however many ranks run), MLPnP SetRansacParameters(0.99,10,300,6,0.5,5.991)
+    (commented call Tracking.cpp:1227-1228), iterate(300), exhaustive; with_cov: computePose's
+    bearing-covariance branch (covMats given)."""
+    from rsc import dist as rdist
     from rsc import workloads as wl
-    solvers = [engine.MLPnPSolver(ctx, sc, 1) for sc in scenes]
-    if with_cov:
-        for g, sc in zip(solvers, scenes):
-            g.set_covariances(mlpnp_covariances(sc))
-    batch = engine.SolverBatch(solvers)
     C = len(scenes)
-
-    def step(s):
-        batch.reset(wl.step_seeds(s, C))
-        batch.set_ransac_parameters(*wl.MLPNP)
-        return int(batch.iterate_raw(args.iters)["iterations"].sum())
-
-    for s in range(args.warmup):
-        step(s)
-    ctx.synchronize()
-    steps = max(1, args.steps // 4)
-    t0 = time.perf_counter()
-    h = 0
-    for s in range(steps):
-        h += step(args.warmup + s)
-    ctx.synchronize()
-    dt = time.perf_counter() - t0
-    return dict(hyp_per_s=h / dt, ms_per_step=1e3 * dt / steps, hypotheses_per_step=h // steps, candidates=C,
-                correspondences=scenes[0].n, steps=steps)
+    lo, hi = rdist.shard_range(C, world, rank, [sc.n for sc in scenes])
+    solvers = [engine.MLPnPSolver(ctx, sc, 1) for sc in scenes[lo:hi]]
+    if with_cov:
+        for g, sc in zip(solvers, scenes[lo:hi]):
+            g.set_covariances(mlpnp_covariances(sc))
+    batch = engine.SolverBatch(solvers) if solvers else None
+    r, rec = run_sharded(engine, ctx, batch, lo, hi, C, wl.MLPNP, args, dist, world, max(1, args.steps // 4),
+                         rdist.pack_pnp)
+    r.update(candidates=C, candidates_per_rank=hi - lo, correspondences=scenes[0].n,
+             sharding=f"{world} rank(s), contiguous blocks by N, RCCL all-gather of {rdist.RECORD}-float records")
+    return r, rec
 
 
 def cpu_baseline_mlpnp(scenes, args, threads, sample_cands=4):
@@ -529,6 +588,85 @@ def run_latency(engine, ctx, args, with_cpu, reps=50):
             sec["speedup_vs_cpu_1core"] = round(med / float(np.median(times)), 2)
         out[kind] = sec
     return out
+
+
+def run_config1(engine, ctx, with_cpu, reps=50):
+    """BASELINE config 1: ONE PnPsolver::iterate(300) call at N = 500 (Tracking.cpp:1226 parameters,
+    exhaustive: 40 % inliers, minInliers 250 unreachable -> 300 hypotheses).  GPU: reset +
+    SetRansacParameters + iterate on the resident solver, median of `reps` calls.  CPU: the oracle's
+    SetRansacParameters + iterate on a fresh solver (construction outside the clock), median of
+    `reps` calls on one core.  Both must return the same result."""
+    import oracle_lib as ol
+    from rsc import synth
+    from rsc import workloads as wl
+    sc = synth.make_pnp_scene(np.random.default_rng(500), 500, 0.4)
+    b = engine.SolverBatch([engine.PnPSolver(ctx, sc, 1)])
+    times = []
+    for r in range(reps + 5):
+        t0 = time.perf_counter()
+        b.reset(np.array([1], np.uint32))
+        b.set_ransac_parameters(*wl.RELOC)
+        out = b.iterate_raw(300)
+        t = time.perf_counter() - t0
+        if r >= 5:
+            times.append(t)
+    g = out[0]
+    sec = dict(correspondences=sc.n, hypotheses=int(g["iterations"]), ok=bool(g["ok"]),
+               gpu_ms=round(1e3 * float(np.median(times)), 4), reps=reps,
+               note="one iterate() call: the latency a single caller sees (CPU plumbing case of BASELINE config 1)")
+    if with_cpu:
+        ct = []
+        res = None
+        for r in range(reps + 3):
+            o = ol.OraclePnP(sc, 1)
+            t0 = time.perf_counter()
+            o.set_ransac_parameters(*wl.RELOC)
+            res = o.iterate(300)
+            t = time.perf_counter() - t0
+            if r >= 3:
+                ct.append(t)
+        assert res["iterations"] == int(g["iterations"]) and bool(res["ok"]) == bool(g["ok"])
+        med = float(np.median(ct))
+        sec["cpu_baseline"] = dict(value=round(1e3 * med, 4), unit="ms/call", cores=1, kind="port",
+                                   sample=f"the same call, 3 warm-up + median of {reps}, oracle restatement, 1 thread")
+        sec["cpu_hyp_per_s_1core"] = round(int(g["iterations"]) / med, 1)
+        sec["gpu_hyp_per_s"] = round(int(g["iterations"]) / float(np.median(times)), 1)
+        sec["speedup_vs_cpu_1core"] = round(med / float(np.median(times)), 2)
+    return sec
+
+
+def rccl_check(engine, ctx, args):
+    """The product's collective on THIS box at world 1: the config-2 result records of one step go
+    through all_gather_into_tensor on device tensors (RCCL, backend "nccl") and must come back
+    bit-equal; reports the collective's time.  Outside every timed region."""
+    if args.dist_backend != "nccl" or args.no_rccl_check:
+        return None
+    if not hasattr(RCCL1, "all_gather_into_tensor"):
+        return {"executed": False, "error": RCCL1}
+    import torch
+    from rsc import dist as rdist
+    from rsc import workloads as wl
+    scenes = wl.config2_scenes(0, 8, args.corrs)
+    b = engine.SolverBatch([engine.PnPSolver(ctx, sc, 1) for sc in scenes])
+    b.reset(wl.config2_seeds(0, 0, len(scenes)))
+    b.set_ransac_parameters(*wl.RELOC)
+    rec = rdist.pack_pnp(list(range(len(scenes))), b.iterate_raw(args.iters))
+    t = torch.from_numpy(rec).cuda()
+    out = torch.empty_like(t)
+    times = []
+    for _ in range(25):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        RCCL1.all_gather_into_tensor(out, t)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    got = out.cpu().numpy()
+    return {"executed": True, "backend": RCCL1.get_backend(), "world": RCCL1.get_world_size(),
+            "records": int(rec.shape[0]), "bytes": int(rec.nbytes),
+            "records_bitequal": bool(np.array_equal(got.view(np.uint32), rec.view(np.uint32))),
+            "all_gather_us_median": round(1e6 * float(np.median(times[5:])), 2),
+            "note": "all_gather_into_tensor of the config-2 result records on device, world 1 (RCCL); "
+                    "multi-GPU curves come from the driver's N=2/4/8 runs"}
 
 
 # ------------------------------------------------------------------------------------------------
@@ -939,24 +1077,27 @@ def main():
     sections = {}
     threads = cpu_threads(args)
     with_cpu = (not args.no_cpu) and world == 1
+    # configs 3 and 4: candidates sharded across the ranks (every rank runs its block)
+    s3 = s3_solvers = m4 = None
+    if not args.no_sim3:
+        s3, s3_solvers, _ = run_sim3(engine, ctx, wl.config3_pairs(), args, dist, rank, world)
+    if not args.no_mlpnp:
+        sc4 = wl.config4_scenes(candidates=wl.CONFIG4["candidates"])
+        m4, _ = run_mlpnp(engine, ctx, sc4, args, False, dist, rank, world)
+        m4["with_covariances"] = _rounded(run_mlpnp(engine, ctx, sc4, args, True, dist, rank, world)[0], 3)
     if rank == 0:
-        if not args.no_sim3:
-            s3 = run_sim3(engine, ctx, wl.config3_pairs(), args)
-            solvers = s3.pop("solvers")
+        if s3 is not None:
             sections["sim3"] = _rounded(s3, 3)
             if with_cpu:
-                cb = cpu_baseline_sim3(solvers, args, threads)
+                cb = cpu_baseline_sim3(s3_solvers, args, threads)
                 sections["sim3"]["cpu_baseline"] = cb
                 sections["sim3"]["speedup_vs_cpu_1core"] = round(s3["hyp_per_s"] / cb["value"], 1)
-        if not args.no_mlpnp:
-            sc4 = wl.config4_scenes()
-            m = run_mlpnp(engine, ctx, sc4, args)
-            sections["mlpnp"] = _rounded(m, 3)
-            sections["mlpnp"]["with_covariances"] = _rounded(run_mlpnp(engine, ctx, sc4, args, with_cov=True), 3)
+        if m4 is not None:
+            sections["mlpnp"] = _rounded(m4, 3)
             if with_cpu:
                 cb = cpu_baseline_mlpnp(sc4, args, threads)
                 sections["mlpnp"]["cpu_baseline"] = cb
-                sections["mlpnp"]["speedup_vs_cpu_1core"] = round(m["hyp_per_s"] / cb["value"], 1)
+                sections["mlpnp"]["speedup_vs_cpu_1core"] = round(m4["hyp_per_s"] / cb["value"], 1)
         if events is not None:
             sections["events"] = _rounded(events, 3)
             if with_cpu:
@@ -965,6 +1106,12 @@ def main():
                 sections["events"]["speedup_vs_cpu_1core"] = round(events["events_per_s"] / cb["value"], 1)
         if not args.no_latency:
             sections["single_event_latency"] = run_latency(engine, ctx, args, with_cpu)
+        if not args.no_config1:
+            sections["config1"] = run_config1(engine, ctx, with_cpu)
+        if world == 1:
+            rc = rccl_check(engine, ctx, args)
+            if rc is not None:
+                sections["rccl_check"] = rc
         if not args.no_poseopt:
             # stereo first: the reference builds only stereo_euroc / stereo_kitti, whose Frames carry
             # mvuRight >= 0 on most slots (EdgeStereoSE3ProjectXYZOnlyPose, Optimizer.cpp:290-323)
@@ -1045,6 +1192,7 @@ def main():
     }
     if with_cpu:
         cb = cpu_baseline_pnp(scenes, args, threads)
+        cb["host"] = host_cpus(threads)
         out["cpu_baseline"] = cb
         out["speedup_vs_cpu_1core"] = round(value / cb["value"], 1)
         if "all_cores" in cb:
@@ -1061,6 +1209,8 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    elif hasattr(RCCL1, "destroy_process_group"):
+        RCCL1.destroy_process_group()
 
 
 if __name__ == "__main__":

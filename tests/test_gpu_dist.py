@@ -1,7 +1,8 @@
 """The N > 1 product path on the GPU: two fresh rank processes (world size 2, both driving device 0,
 gloo collectives — the one-GPU stand-in for RCCL over xGMI) each run their shard THROUGH librsc
-(relocalization candidates by cost-balanced contiguous blocks; config-5 events whole, LPT), then
-all-gather the fixed-size records.  The gathered records must equal a single-process librsc run and
+(relocalization candidates, config-3 Sim3 pairs and config-4 MLPnP candidates by cost-balanced
+contiguous blocks; config-5 events whole, LPT), then all-gather the fixed-size records.  A world-1
+process group with the nccl backend (RCCL) runs the same all-gather on device tensors.  The gathered records must equal a single-process librsc run and
 the oracle bit for bit (sharding changes no arithmetic)."""
 import os
 import socket
@@ -28,6 +29,38 @@ def _scenes():
     rng = np.random.default_rng(321)
     return [synth.make_pnp_scene(rng, int(rng.integers(200, 1500)), float(rng.uniform(0.35, 0.75)))
             for _ in range(12)]
+
+
+def _pairs():
+    from rsc import synth
+    rng = np.random.default_rng(654)
+    return [synth.make_sim3_pair(rng, int(rng.integers(150, 700)), int(rng.integers(10, 200))) for _ in range(6)]
+
+
+def _ml_scenes():
+    from rsc import synth
+    rng = np.random.default_rng(987)
+    return [synth.make_pnp_scene(rng, int(rng.integers(100, 900)), float(rng.uniform(0.3, 0.8))) for _ in range(6)]
+
+
+def _run_sim3(ctx, pairs, idx):
+    from rsc import engine
+    solvers = [engine.Sim3Solver(ctx, pairs[c], 1 + c) for c in idx]
+    if not solvers:
+        return []
+    b = engine.SolverBatch(solvers)
+    b.set_ransac_parameters(0.99, 20, 300)
+    return b.iterate(300)
+
+
+def _run_mlpnp(ctx, scenes, idx):
+    from rsc import engine
+    solvers = [engine.MLPnPSolver(ctx, scenes[c], 1 + c) for c in idx]
+    if not solvers:
+        return []
+    b = engine.SolverBatch(solvers)
+    b.set_ransac_parameters(0.99, 10, 300, 6, 0.5, 5.991)
+    return b.iterate(300)
 
 
 def _events():
@@ -78,7 +111,16 @@ def _worker(rank, world, port, q):
     mine = rev.shard_events([ev.cost for ev in evs], world)[rank]
     erec = _run_events(ctx, [evs[i] for i in mine])
     alle = rev.all_gather_events(dist, erec, max_per_rank=len(evs))
-    q.put((rank, hi - lo, len(mine), allr, alle))
+    # configs 3 and 4 (bench.py run_sim3 / run_mlpnp): contiguous blocks by N, one all-gather each
+    pairs = _pairs()
+    lo3, hi3 = rd.shard_range(len(pairs), world, rank, cost=[p.n1 for p in pairs])
+    s3 = rd.all_gather_records(dist, rd.pack_sim3(list(range(lo3, hi3)), _run_sim3(ctx, pairs, range(lo3, hi3))),
+                               max_per_rank=len(pairs))
+    mls = _ml_scenes()
+    lo4, hi4 = rd.shard_range(len(mls), world, rank, cost=[m.n for m in mls])
+    m4 = rd.all_gather_records(dist, rd.pack_pnp(list(range(lo4, hi4)), _run_mlpnp(ctx, mls, range(lo4, hi4))),
+                               max_per_rank=len(mls))
+    q.put((rank, hi - lo, len(mine), allr, alle, hi3 - lo3, s3, hi4 - lo4, m4))
     dist.barrier()
     dist.destroy_process_group()
     ctx.close()
@@ -102,7 +144,7 @@ def test_world2_librsc_shards_match_single_process_and_oracle():
     assert all(g[1] > 0 and g[2] > 0 for g in got)  # both ranks had work
     single = rdist.pack_pnp(list(range(len(scenes))), _run_pnp(ctx(), scenes, range(len(scenes))))
     single_ev = _run_events(ctx(), evs)
-    for _, _, _, allr, alle in got:  # every rank holds the full gathered result
+    for _, _, _, allr, alle, _, _, _, _ in got:  # every rank holds the full gathered result
         assert np.array_equal(allr.view(np.uint32), single.view(np.uint32))
         assert np.array_equal(alle.view(np.uint32), single_ev.view(np.uint32))
     # and the single-process run is the oracle's
@@ -114,3 +156,56 @@ def test_world2_librsc_shards_match_single_process_and_oracle():
     assert np.array_equal(single.view(np.uint32), rdist.pack_pnp(list(range(len(scenes))), ora).view(np.uint32))
     assert np.array_equal(single_ev.view(np.uint32), eo.run_events(evs).view(np.uint32))
     assert rdist.reloc_winner(single) == rdist.reloc_winner(got[0][3])
+    # configs 3 / 4: both ranks ran a block, every rank holds all records, equal to one process and
+    # to the oracle
+    pairs, mls = _pairs(), _ml_scenes()
+    assert all(g[5] > 0 and g[7] > 0 for g in got)
+    s3_single = rdist.pack_sim3(list(range(len(pairs))), _run_sim3(ctx(), pairs, range(len(pairs))))
+    m4_single = rdist.pack_pnp(list(range(len(mls))), _run_mlpnp(ctx(), mls, range(len(mls))))
+    for g in got:
+        assert np.array_equal(g[6].view(np.uint32), s3_single.view(np.uint32))
+        assert np.array_equal(g[8].view(np.uint32), m4_single.view(np.uint32))
+    o3, o4 = [], []
+    for c, p in enumerate(pairs):
+        o = ol.OracleSim3(p, 1 + c)
+        o.set_ransac_parameters(0.99, 20, 300)
+        o3.append(o.iterate(300))
+    for c, sc in enumerate(mls):
+        o = ol.OracleMLPnP(sc, 1 + c)
+        o.set_ransac_parameters(0.99, 10, 300, 6, 0.5, 5.991)
+        o4.append(o.iterate(300))
+    assert np.array_equal(s3_single.view(np.uint32), rdist.pack_sim3(list(range(len(pairs))), o3).view(np.uint32))
+    assert np.array_equal(m4_single.view(np.uint32), rdist.pack_pnp(list(range(len(mls))), o4).view(np.uint32))
+
+
+def _rccl_worker(port, q):
+    """World-1 RCCL (backend "nccl"): the config-2 result records through all_gather_into_tensor on
+    device tensors, as bench.py's N > 1 step does over xGMI."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "orb-slam2-optimized_amd"))
+    import torch
+    import torch.distributed as dist
+    from rsc import dist as rd, engine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    ctx = engine.Context(0)
+    scenes = _scenes()
+    rec = rd.pack_pnp(list(range(len(scenes))), _run_pnp(ctx, scenes, range(len(scenes))))
+    allr = rd.all_gather_records(dist, rec, max_per_rank=len(scenes) + 3, device="cuda")
+    q.put((dist.get_backend(), allr, rec))
+    dist.destroy_process_group()
+    ctx.close()
+
+
+def test_world1_rccl_all_gather_of_records():
+    sp = mp.get_context("spawn")
+    q = sp.Queue()
+    p = sp.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    backend, allr, rec = q.get(timeout=240)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert backend == "nccl"
+    assert np.array_equal(allr.view(np.uint32), rec.view(np.uint32))
