@@ -118,6 +118,9 @@ def dist_setup(args):
         # product's collective (all_gather_into_tensor of the result records on device) executes on
         # a 1-GPU box too (rccl_check section, outside the timed regions: at N = 1 the step has no
         # exchange).  A failure is reported in the JSON line, not fatal.
+        sys.stdout.flush()
+        RESULT_OUT = os.fdopen(os.dup(1), "w")  # RCCL prints its banner on fd 1
+        os.dup2(2, 1)
         try:
             import torch
             import torch.distributed as tdist
@@ -335,7 +338,8 @@ def run_sharded(engine, ctx, batch, lo, hi, total, params, args, dist, world, st
             batch.set_ransac_parameters(*params)
             outs = batch.iterate_raw(args.iters)
             h = int(outs["iterations"].sum())
-            rec = pack(ids, outs)
+            if gather is not None:
+                rec = pack(ids, outs)
         if gather is not None:
             rec = rdist.all_gather_records(dist, rec, gather, device=COLL_DEV)
         state["records"] = rec

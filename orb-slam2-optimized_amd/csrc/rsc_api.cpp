@@ -404,6 +404,9 @@ struct HipPnPBackend : PnPBackend {
         std::vector<int2>* quad_wgs = quad_wgs_tl;
         std::vector<int4>& scan_wgs = scan_wgs_tl;
         const int HC = scan_chunk(total);  // hypotheses per scan workgroup
+        int eig_shape = 0, hb = 64;         // launch shapes of the two solve stages (rsc_kernels.h)
+        pnp_round_shape(total, eig_shape, hb);
+        const int eig_step = kEigShapes[eig_shape].hyps;
         // The tables depend only on the round's shape (count, sample size and H per problem, HC):
         // a round with the shape of the previous one on this thread reuses them (building and
         // XCD-ordering ~3.7k entries costs ~10 us of host time per config-2 round).
@@ -414,6 +417,8 @@ struct HipPnPBackend : PnPBackend {
         key.clear();
         key.push_back(count);
         key.push_back(HC);
+        key.push_back(eig_shape);
+        key.push_back(hb);
         for (int i = 0; i < count; ++i) {
             key.push_back(S[i]->mRansacMinSet);
             key.push_back(H[i]);
@@ -423,8 +428,8 @@ struct HipPnPBackend : PnPBackend {
             scan_wgs.clear();
             for (int i = 0; i < count; ++i) {
                 const int g = S[i]->mRansacMinSet - 4;
-                for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs[g].push_back(make_int2(i, h0));
-                for (int h0 = 0; h0 < H[i]; h0 += kEigHyps) quad_wgs[g].push_back(make_int2(i, h0));
+                for (int h0 = 0; h0 < H[i]; h0 += hb) solve_wgs[g].push_back(make_int2(i, h0));
+                for (int h0 = 0; h0 < H[i]; h0 += eig_step) quad_wgs[g].push_back(make_int2(i, h0));
                 for (int h0 = 0; h0 < H[i]; h0 += HC)
                     scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
             }
@@ -468,8 +473,9 @@ struct HipPnPBackend : PnPBackend {
             if (solve_wgs[g].empty()) continue;
             // the first group's eigen stage starts at ev[0]: no extra event in the queue
             hipEvent_t eb = (C->timing && !first_group) ? C->ev[6 + 2 * g] : nullptr;
-            RSC_HIP(launch_pnp_solve_split(4 + g, (int)quad_wgs[g].size(),
-                                          reinterpret_cast<const int2*>(base + o_quad[g]), (int)solve_wgs[g].size(),
+            RSC_HIP(launch_pnp_solve_split(4 + g, eig_shape, (int)quad_wgs[g].size(),
+                                          reinterpret_cast<const int2*>(base + o_quad[g]), hb,
+                                          (int)solve_wgs[g].size(),
                                           reinterpret_cast<const int2*>(base + o_solve[g]), dprobs, dlps,
                                           C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p, bs, C->stream,
                                           eb, C->timing ? C->ev[7 + 2 * g] : nullptr));

@@ -452,9 +452,11 @@ RSC_HD inline void betas_block(int b, int ngroups, int& g, int& apx) {
 // writes the pose.  Hand-off: producer stores -> vmcnt(0) -> agent release -> vmcnt(0) -> relaxed
 // agent add; the last adder: agent acquire -> vmcnt(0) -> loads (MI355X_MICROARCH.md, inter-
 // workgroup visibility).  It resets the counter, so every launch starts from zero.
+// hb: hypotheses per wave (64 for large rounds; fewer for small ones, so a wave carries the union
+// of fewer data-dependent chains): lanes >= hb mirror lane % hb (same control flow, no writes).
 template <int NS>
 __device__ __forceinline__ void pnp_betas_wave_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
-                                                    const int2* __restrict__ wg_table, int ngroups,
+                                                    const int2* __restrict__ wg_table, int ngroups, int hb,
                                                     const double* __restrict__ stage,
                                                     const int32_t* __restrict__ samples, float* __restrict__ poses,
                                                     double* __restrict__ berr, float* __restrict__ bpose,
@@ -464,8 +466,9 @@ __device__ __forceinline__ void pnp_betas_wave_body(const DevPnP* __restrict__ p
     betas_block(blockIdx.x, ngroups, g, apx);
     const int2 wt = wg_table[g];
     const LaunchProb& lp = lps[wt.x];
-    const bool active = wt.y + lane < lp.H;
-    const int h = active ? wt.y + lane : lp.H - 1;
+    const bool active = lane < hb && wt.y + lane < lp.H;
+    const int hm = wt.y + lane % hb;
+    const int h = active ? wt.y + lane : (hm < lp.H ? hm : wt.y);
     const DevPnP& P = probs[lp.prob];
     const size_t rec = (size_t)(lp.out0 + h);
     const double* in = stage + rec * kStageDoubles;

@@ -30,23 +30,38 @@ def shard_range(n_items: int, world: int, rank: int, cost=None) -> tuple[int, in
     return bounds[rank], bounds[rank + 1]
 
 
-def pack_pnp(cand_ids, results) -> np.ndarray:
-    out = np.zeros((len(results), RECORD), np.float32)
-    for i, (c, r) in enumerate(zip(cand_ids, results)):
-        out[i, 0] = c
-        out[i, 1:5] = [r["ok"], r["no_more"], r["n_inliers"], r["iterations"]]
-        out[i, 5:21] = np.asarray(r["T"], np.float32).ravel()
+def _fields(results, names):
+    """Columns of per-candidate results: a numpy structured array (SolverBatch.iterate_raw, read
+    without a Python loop) or a list of result dicts."""
+    if isinstance(results, np.ndarray) and results.dtype.names:
+        return [np.asarray(results[n]) for n in names]
+    return [np.asarray([r[n] for r in results]) for n in names]
+
+
+def _pack(cand_ids, results, pose_cols):
+    n = len(results)
+    out = np.zeros((n, RECORD), np.float32)
+    if n == 0:
+        return out
+    ok, nm, ni, it = _fields(results, ("ok", "no_more", "n_inliers", "iterations"))
+    out[:, 0] = np.asarray(cand_ids, np.float32)
+    out[:, 1], out[:, 2], out[:, 3], out[:, 4] = ok, nm, ni, it
+    col = 5
+    for name, width in pose_cols:
+        (v,) = _fields(results, (name,))
+        out[:, col:col + width] = v.reshape(n, width)
+        col += width
     return out
+
+
+def pack_pnp(cand_ids, results) -> np.ndarray:
+    """PnP / MLPnP records: [candidate, ok, no_more, n_inliers, iterations, T[16]]."""
+    return _pack(cand_ids, results, (("T", 16),))
 
 
 def pack_sim3(cand_ids, results) -> np.ndarray:
-    out = np.zeros((len(results), RECORD), np.float32)
-    for i, (c, r) in enumerate(zip(cand_ids, results)):
-        out[i, 0] = c
-        out[i, 1:5] = [r["ok"], r["no_more"], r["n_inliers"], r["iterations"]]
-        out[i, 5:14] = np.asarray(r["R"], np.float32).ravel()
-        out[i, 14:17] = np.asarray(r["t"], np.float32)
-    return out
+    """Sim3 records: [candidate, ok, no_more, n_inliers, iterations, R[9], t[3], 0 0 0 0]."""
+    return _pack(cand_ids, results, (("R", 9), ("t", 3)))
 
 
 def all_gather_records(dist, records: np.ndarray, max_per_rank: int, device=None) -> np.ndarray:
