@@ -28,6 +28,7 @@ extern "C" {
 #define RSC_ERR_OOM (-3)
 #define RSC_ERR_UNSUPPORTED (-4)
 #define RSC_ERR_NODEVICE (-5)
+#define RSC_ERR_INTERNAL (-6) /* an engine invariant failed (a bug; rsc_status_string says which) */
 
 typedef struct rsc_context rsc_context;
 typedef struct rsc_pnp rsc_pnp;

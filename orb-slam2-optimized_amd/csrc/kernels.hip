@@ -67,6 +67,7 @@ __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict_
                                                        const int4* __restrict__ wg_table,  // lp, hyp0, count
                                                        const float* __restrict__ poses,
                                                        int32_t* __restrict__ counts,
+                                                       int32_t* __restrict__ counts_dev,
                                                        uint64_t* __restrict__ masks, int mask_words) {
     // Hypotheses per flush: the 4 waves' mask words of a batch wait in LDS (16 KB) until the batch's
     // counts are summed; only hypotheses reaching mRansacMinInliers — the only ones whose inlier
@@ -127,6 +128,7 @@ __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict_
             if (tid <= jb) {
                 const int c = wave_cnt[0][tid] + wave_cnt[1][tid] + wave_cnt[2][tid] + wave_cnt[3][tid];
                 counts[lp.out0 + wt.y + base + tid] = c;
+                if (counts_dev) counts_dev[lp.out0 + wt.y + base + tid] = c;  // pnp_select_refine_kernel
                 wave_cnt[0][tid] = c;  // the batch's totals, for the mask stores below
             }
             __syncthreads();
@@ -217,9 +219,7 @@ __device__ __forceinline__ void refine_stamp(int slot) {
     if (blockIdx.x < 64 && threadIdx.x == 0) g_refine_stamps[blockIdx.x][slot] = wall_clock64();
 }
 
-__global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restrict__ probs,
-                                                         const RefineJob* __restrict__ jobs,
-                                                         int mask_words_out) {
+__device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs, const RefineJob& J) {
     __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles];
     __shared__ __attribute__((aligned(16))) double wbuf[4][kFoldStride * 9];
     __shared__ int prefix[129];
@@ -228,7 +228,6 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     __shared__ float pose_sh[12];
     __shared__ int cnt_sh[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const RefineJob& J = jobs[blockIdx.x];
     const DevPnP& P = probs[J.prob];
     const int n = P.n;
     const int nwords = (n + 63) / 64;
@@ -477,6 +476,8 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
     RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = pose_sh[9 + k];
     int cnt = 0;
     const double fx = P.fx, fy = P.fy, cx = P.cx, cy = P.cy;
+    // the solver's own mask words only (a launch can hold solvers of different N)
+    const int mask_words_out = J.out_words;
     for (int base = 0; base < mask_words_out * 64; base += 256) {
         const int i = base + tid;
         bool inl = false;
@@ -496,6 +497,69 @@ __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restric
         *J.out_count = cnt_sh[0] + cnt_sh[1] + cnt_sh[2] + cnt_sh[3];
         RSC_UNROLL for (int k = 0; k < 12; ++k) J.out_pose[k] = pose_sh[k];
     }
+}
+
+__global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restrict__ probs,
+                                                         const RefineJob* __restrict__ jobs) {
+    const RefineJob J = jobs[blockIdx.x];
+    pnp_refine_body(probs, J);
+}
+
+// The host replay's first pause of a speculation round, evaluated on the device right after the scan
+// (one workgroup per solver of the round), and its Refine() run at once — no host round trip between
+// the scan and the Refine.  PnPsolver.cpp:139-157 for the round's hypotheses [0, H): the first k with
+// nInliers >= mRansacMinInliers pauses the loop; it becomes the new best when nInliers > mnBestInliers
+// (best0: the value when the round was launched), and Refine() runs on mvbBestInliers with
+// set_maximum_number_of_correspondences(max(rows0, mnBestInliers)).  The host replay applies the
+// same rules to the same counts and takes these results (RefineSelOut) instead of launching the
+// refine itself; a solver without a qualifying hypothesis leaves k = -1 and touches nothing.
+__global__ __launch_bounds__(256) void pnp_select_refine_kernel(const DevPnP* __restrict__ probs,
+                                                                const RefineSel* __restrict__ sels,
+                                                                const int32_t* __restrict__ counts,
+                                                                uint64_t* __restrict__ masks, int mask_words,
+                                                                const float* __restrict__ poses,
+                                                                RefineSelOut* __restrict__ out) {
+    __shared__ int k_sh;
+    const RefineSel S = sels[blockIdx.x];
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        int k = -1;
+        for (int base = 0; base < S.H && k < 0; base += 64) {  // wave-uniform loop
+            const int idx = base + tid;
+            const bool q = idx < S.H && counts[S.out0 + idx] >= S.min_inliers;
+            const uint64_t b = __ballot(q);
+            if (b) k = base + __ffsll((unsigned long long)b) - 1;
+        }
+        if (tid == 0) k_sh = k;
+    }
+    __syncthreads();
+    const int k = k_sh;
+    RefineSelOut& o = out[blockIdx.x];
+    if (k < 0) {
+        if (tid == 0) o.k = -1;
+        return;
+    }
+    const size_t rec = (size_t)(S.out0 + k);
+    const int c = counts[rec];
+    const bool adopt = c > S.best0;
+    const int nr = adopt ? c : S.best0;
+    RefineJob J;
+    J.prob = S.prob;
+    J.rows_after = max(S.rows0, nr);
+    J.best_mask = adopt ? masks + rec * mask_words : S.best;
+    J.adopt_mask = adopt ? S.best : nullptr;
+    J.adopt_pose = adopt ? poses + rec * 12 : nullptr;
+    J.out_best_pose = o.best_pose;
+    J.out_pose = o.pose;
+    J.out_count = &o.count;
+    J.out_mask = S.refined;
+    J.out_words = S.words;
+    if (tid == 0) {
+        o.k = k;
+        o.adopt = adopt ? 1 : 0;
+        o.rows_after = J.rows_after;
+    }
+    pnp_refine_body(probs, J);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -901,9 +965,10 @@ hipError_t launch_selftest_math(int fn, const double* x, int n, double* out, hip
 }
 
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,
-                           const float* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st) {
+                           const float* poses, int32_t* counts, int32_t* counts_dev, uint64_t* masks, int mask_words,
+                           hipStream_t st) {
     switch (ppt) {
-#define RSC_CASE(P) case P: pnp_scan_kernel<P><<<nwg, 256, 0, st>>>(probs, lps, wgt, poses, counts, masks, mask_words); break;
+#define RSC_CASE(P) case P: pnp_scan_kernel<P><<<nwg, 256, 0, st>>>(probs, lps, wgt, poses, counts, counts_dev, masks, mask_words); break;
         RSC_CASE(1) RSC_CASE(2) RSC_CASE(4) RSC_CASE(8) RSC_CASE(16) RSC_CASE(32)
 #undef RSC_CASE
         default: return hipErrorInvalidValue;
@@ -915,9 +980,16 @@ hipError_t read_refine_stamps(uint64_t* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_refine_stamps), sizeof(uint64_t) * 64 * 8, 0, hipMemcpyDeviceToHost);
 }
 
-hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, int mask_words_out,
-                             hipStream_t st) {
-    pnp_refine_kernel<<<njobs, 256, 0, st>>>(probs, jobs, mask_words_out);
+hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, hipStream_t st) {
+    pnp_refine_kernel<<<njobs, 256, 0, st>>>(probs, jobs);
+    return hipGetLastError();
+}
+
+hipError_t launch_pnp_select_refine(int nsel, const DevPnP* probs, const RefineSel* sels, const int32_t* counts,
+                                    uint64_t* masks, int mask_words, const float* poses, RefineSelOut* out,
+                                    hipStream_t st) {
+    if (nsel <= 0) return hipSuccess;
+    pnp_select_refine_kernel<<<nsel, 256, 0, st>>>(probs, sels, counts, masks, mask_words, poses, out);
     return hipGetLastError();
 }
 

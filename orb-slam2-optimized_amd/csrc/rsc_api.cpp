@@ -173,6 +173,8 @@ struct rsc_context {
     PinBuf<float> h_small;
     PinBuf<float> h_pick;  // Sim3 pick records of the last round, [solver][16]
     DevBuf<char> d_refine;
+    DevBuf<RefineSelOut> d_selout;  // pnp_select_refine_kernel results of the last fused round
+    PinBuf<RefineSelOut> h_selout;
     // PoseOptimization: packed inputs (problems | xw | uv), edge error scratch, results (outliers | poses)
     DevBuf<char> d_po_in;
     DevBuf<double2> d_po_err;
@@ -202,6 +204,7 @@ struct rsc_context {
     // [0] speculation inputs built, [1] kernels enqueued, [2] counts back (sync), [3] return
     double host_us[4] = {0, 0, 0, 0};
     bool direct_counts = true;  // env RSC_DIRECT_COUNTS=0 restores the HBM buffer + D2H copy
+    bool fused_refine = true;   // env RSC_FUSED_REFINE=0: the replay's Refine always as its own launch
     bool dma_upload = false;    // env RSC_DMA_UPLOAD=1: descriptors by hipMemcpyAsync instead of the copy kernel
     std::chrono::steady_clock::time_point t_entry;
 };
@@ -341,6 +344,7 @@ void timing_begin(rsc_context* C, int slot) {
 struct HipPnPBackend : PnPBackend {
     rsc_context* C;
     std::vector<rsc_pnp*> solvers;  // index = state slot in the current call
+    int fused_count = 0;  // > 0: the last speculation ran pnp_select_refine_kernel over this many slots
     explicit HipPnPBackend(rsc_context* c) : C(c) {}
     rsc_pnp* of(PnPState* s) {
         for (auto* p : solvers)
@@ -397,6 +401,25 @@ struct HipPnPBackend : PnPBackend {
         }
         const int mw = ppt * 4;
         C->mask_words = mw;
+        // the replay's first Refine of every solver runs on the device with the round (small rounds)
+        fused_count = 0;
+        const bool fused = C->fused_refine && total <= kFusedRefineMaxHyps;
+        thread_local std::vector<RefineSel> sels_tl;
+        std::vector<RefineSel>& sels = sels_tl;
+        sels.resize(fused ? count : 0);
+        for (int i = 0; fused && i < count; ++i) {
+            rsc_pnp* p = of(S[i]);
+            RefineSel& r = sels[i];
+            r.prob = i;
+            r.out0 = lps[i].out0;
+            r.H = H[i];
+            r.min_inliers = S[i]->mRansacMinInliers;
+            r.best0 = S[i]->mnBestInliers;
+            r.rows0 = S[i]->max_rows;
+            r.best = p->d_best;
+            r.refined = p->d_refined;
+            r.words = p->words;
+        }
         // work tables
         thread_local std::vector<int2> solve_wgs_tl[3], quad_wgs_tl[3];
         thread_local std::vector<int4> scan_wgs_tl;
@@ -448,10 +471,20 @@ struct HipPnPBackend : PnPBackend {
         for (int g = 0; g < 3; ++g) o_solve[g] = b.add(solve_wgs[g].data(), solve_wgs[g].size() * sizeof(int2));
         for (int g = 0; g < 3; ++g) o_quad[g] = b.add(quad_wgs[g].data(), quad_wgs[g].size() * sizeof(int2));
         const size_t o_scan = b.add(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
+        const size_t o_sel = fused ? b.add(sels.data(), sels.size() * sizeof(RefineSel)) : 0;
         if (int e = upload_blob(C, b)) return e;
         if (int e = C->d_poses.ensure((size_t)total * 12)) return e;
         int32_t* cnt_dst = nullptr;
         if (int e = counts_target(C, total, &cnt_dst)) return e;
+        int32_t* cnt_dev = nullptr;  // HBM copy of the counts for the device-side selection
+        if (fused) {
+            if (C->direct_counts) {
+                if (int e = C->d_counts.ensure((size_t)total)) return e;
+                cnt_dev = C->d_counts.p;
+            }
+            if (int e = C->d_selout.ensure((size_t)count)) return e;
+            if (int e = C->h_selout.ensure((size_t)count)) return e;
+        }
         if (int e = C->d_masks.ensure((size_t)total * mw)) return e;
         if (int e = C->d_samples.ensure((size_t)total * 8)) return e;
         if (int e = C->d_stage.ensure((size_t)total * kStageDoubles)) return e;
@@ -483,8 +516,17 @@ struct HipPnPBackend : PnPBackend {
         }
         timing_begin(C, 1);
         RSC_HIP(launch_pnp_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
-                                C->d_poses.p, cnt_dst, C->d_masks.p, mw, C->stream));
+                                C->d_poses.p, cnt_dst, cnt_dev, C->d_masks.p, mw, C->stream));
         timing_begin(C, 2);
+        if (fused) {
+            timing_begin(C, 3);
+            RSC_HIP(launch_pnp_select_refine(count, dprobs, reinterpret_cast<const RefineSel*>(base + o_sel),
+                                             cnt_dev ? cnt_dev : cnt_dst, C->d_masks.p, mw, C->d_poses.p,
+                                             C->d_selout.p, C->stream));
+            timing_begin(C, 4);
+            RSC_HIP(hipMemcpyAsync(C->h_selout.p, C->d_selout.p, sizeof(RefineSelOut) * count, hipMemcpyDeviceToHost,
+                                   C->stream));
+        }
         if (!C->direct_counts)
             RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
         host_mark(C, 1);
@@ -506,15 +548,41 @@ struct HipPnPBackend : PnPBackend {
                 C->last_ms[5] += e;
                 first = false;
             }
+            if (fused) {
+                float r = 0;
+                (void)hipEventElapsedTime(&r, C->ev[3], C->ev[4]);
+                C->last_ms[2] += r;
+            }
         }
         counts.resize(count);  // keeps the inner vectors' capacity
         for (int i = 0; i < count; ++i)
             counts[i].assign(C->h_counts.p + lps[i].out0, C->h_counts.p + lps[i].out0 + H[i]);
+        if (fused) fused_count = count;
         return 0;
     }
 
-    int refine(PnPState* const* S, int count, const int* spec_j, const int* adopt_k, const int* rows_after,
-               int* rcount, float (*rpose)[12]) override {
+    int refine(PnPState* const* S, int count, const int* spec_j, const int* pause_k, const int* adopt_k,
+               const int* rows_after, int* rcount, float (*rpose)[12]) override {
+        if (fused_count > 0) {
+            // the device ran exactly these Refines with the round (pnp_select_refine_kernel applies the
+            // replay's rules to the same counts); anything else is an engine bug, reported loudly
+            const int nslots = fused_count;
+            fused_count = 0;
+            for (int i = 0; i < count; ++i) {
+                const RefineSelOut* o = spec_j[i] >= 0 && spec_j[i] < nslots ? &C->h_selout.p[spec_j[i]] : nullptr;
+                if (!o || o->k != pause_k[i] || (o->adopt != 0) != (adopt_k[i] >= 0) || o->rows_after != rows_after[i]) {
+                    g_last_error = "device-side Refine selection disagrees with the host replay";
+                    return RSC_ERR_INTERNAL;
+                }
+            }
+            for (int i = 0; i < count; ++i) {
+                const RefineSelOut& o = C->h_selout.p[spec_j[i]];
+                rcount[i] = o.count;
+                std::memcpy(rpose[i], o.pose, 48);
+                if (adopt_k[i] >= 0) pose12_to_T(o.best_pose, S[i]->mBestTcw);
+            }
+            return 0;
+        }
         std::vector<DevPnP> probs(count);
         std::vector<RefineJob> jobs(count);
         // out: refined poses [count][12] | counts [count] | adopted best poses [count][12]
@@ -522,7 +590,6 @@ struct HipPnPBackend : PnPBackend {
         float* d_out_pose = reinterpret_cast<float*>(C->d_refine.p);
         int32_t* d_out_cnt = reinterpret_cast<int32_t*>(C->d_refine.p + (size_t)count * 48);
         float* d_out_best = reinterpret_cast<float*>(C->d_refine.p + (size_t)count * 52);
-        int maxw = 1;
         for (int i = 0; i < count; ++i) {
             rsc_pnp* p = of(S[i]);
             probs[i] = dev_of(p);
@@ -543,16 +610,15 @@ struct HipPnPBackend : PnPBackend {
             jobs[i].out_pose = d_out_pose + 12 * i;
             jobs[i].out_count = d_out_cnt + i;
             jobs[i].out_mask = p->d_refined;
-            maxw = std::max(maxw, p->words);
+            jobs[i].out_words = p->words;
         }
         Blob b;
         const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevPnP));
         const size_t o_jobs = b.add(jobs.data(), jobs.size() * sizeof(RefineJob));
         if (int e = upload_blob(C, b)) return e;
         timing_begin(C, 3);
-        // refined masks are written with a per-solver word count: launch per distinct width
         RSC_HIP(launch_pnp_refine(count, reinterpret_cast<const DevPnP*>(C->d_desc.p + o_probs),
-                                  reinterpret_cast<const RefineJob*>(C->d_desc.p + o_jobs), maxw, C->stream));
+                                  reinterpret_cast<const RefineJob*>(C->d_desc.p + o_jobs), C->stream));
         timing_begin(C, 4);
         if (int e = C->h_small.ensure((size_t)count * 25)) return e;
         RSC_HIP(hipMemcpyAsync(C->h_small.p, C->d_refine.p, (size_t)count * 100, hipMemcpyDeviceToHost, C->stream));
@@ -933,6 +999,7 @@ const char* rsc_status_string(int status) {
         case RSC_ERR_OOM: return g_last_error.empty() ? "out of device memory" : g_last_error.c_str();
         case RSC_ERR_UNSUPPORTED: return g_last_error.empty() ? "unsupported" : g_last_error.c_str();
         case RSC_ERR_NODEVICE: return "no HIP device";
+        case RSC_ERR_INTERNAL: return g_last_error.empty() ? "internal error" : g_last_error.c_str();
         default: return "unknown status";
     }
 }
@@ -949,6 +1016,7 @@ int rsc_context_create(int device, rsc_context** out) {
     RSC_HIP(hipStreamCreateWithFlags(&C->stream, hipStreamNonBlocking));
     C->own_stream = true;
     if (const char* m = std::getenv("RSC_DIRECT_COUNTS")) C->direct_counts = std::strcmp(m, "0") != 0;
+    if (const char* m = std::getenv("RSC_FUSED_REFINE")) C->fused_refine = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_DMA_UPLOAD")) C->dma_upload = std::strcmp(m, "0") != 0;
     C->table.build();
     if (int e = C->d_table.ensure(C->table.T.size())) return e;

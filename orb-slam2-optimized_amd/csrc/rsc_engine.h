@@ -156,12 +156,15 @@ struct PnPBackend {
     // Speculate hypotheses [0, H[i]) for solver states[i] (from their current rng position and
     // EPnP buffer rows).  Fills counts[i][0..H[i]).
     virtual int speculate(PnPState* const* states, int count, const int* H, std::vector<std::vector<int32_t>>& counts) = 0;
-    // Refine() for each listed solver, preceded (adopt_k[q] >= 0) by the new-best bookkeeping of
-    // PnPsolver.cpp:147-156: mvbBestInliers/mBestTcw := hypothesis adopt_k[q] of speculation slot
-    // spec_j[q] (the backend writes states[q]->mBestTcw).  Uses the best mask and rows_after; writes
-    // the refined count and pose (the caller decides success) into the out arrays.
-    virtual int refine(PnPState* const* states, int count, const int* spec_j, const int* adopt_k,
-                       const int* rows_after, int* refined_count, float (*refined_pose)[12]) = 0;
+    // Refine() for each listed solver, paused at hypothesis pause_k[q] of speculation slot
+    // spec_j[q], preceded (adopt_k[q] >= 0) by the new-best bookkeeping of PnPsolver.cpp:147-156:
+    // mvbBestInliers/mBestTcw := that hypothesis (the backend writes states[q]->mBestTcw).  Uses the
+    // best mask and rows_after; writes the refined count and pose (the caller decides success) into
+    // the out arrays.  A backend may have run exactly this Refine already on the device with the
+    // round (the first pause of each solver); it then only hands back the results.
+    virtual int refine(PnPState* const* states, int count, const int* spec_j, const int* pause_k,
+                       const int* adopt_k, const int* rows_after, int* refined_count,
+                       float (*refined_pose)[12]) = 0;
     // vbInliers: scatter best (kind 2) or refined (kind 1) mask through kp_index into n_points bytes.
     virtual int fetch_mask(PnPState* const* states, int count, const int* kind, uint8_t* const* out) = 0;
     virtual ~PnPBackend() {}
@@ -241,7 +244,7 @@ inline int pnp_iterate_many(PnPBackend& be, PnPState* const* S, int count, const
         }
         // Refine() for every paused solver
         std::vector<PnPState*> rs;
-        std::vector<int> rows_after, rj, rk;
+        std::vector<int> rows_after, rj, rk, rp;
         for (size_t j = 0; j < spec.size(); ++j)
             if (pause_k[j] >= 0) {
                 PnPState& s = *spec[j];
@@ -250,13 +253,14 @@ inline int pnp_iterate_many(PnPBackend& be, PnPState* const* S, int count, const
                 rs.push_back(&s);
                 rows_after.push_back(ra);
                 rj.push_back((int)j);
+                rp.push_back(pause_k[j]);
                 rk.push_back(adopt_k[j]);
             }
         std::vector<int> rcount(rs.size());
         std::vector<float> rpose(rs.size() * 12);
         if (!rs.empty()) {
-            int st = be.refine(rs.data(), (int)rs.size(), rj.data(), rk.data(), rows_after.data(), rcount.data(),
-                               reinterpret_cast<float(*)[12]>(rpose.data()));
+            int st = be.refine(rs.data(), (int)rs.size(), rj.data(), rp.data(), rk.data(), rows_after.data(),
+                               rcount.data(), reinterpret_cast<float(*)[12]>(rpose.data()));
             if (st) return st;
         }
         for (size_t q = 0; q < rs.size(); ++q) {

@@ -63,6 +63,28 @@ struct RefineJob {
     float* out_pose;            // 12 floats
     int32_t* out_count;
     uint64_t* out_mask;         // mvbRefinedInliers as bits
+    int out_words;              // words of out_mask (the solver's ceil(N/64))
+};
+
+// pnp_select_refine_kernel: one speculation round's solver (the replay's state at launch) and what
+// the kernel leaves for the host replay.
+struct RefineSel {
+    int prob;          // index into the round's DevPnP table
+    int out0, H;       // the solver's hypothesis records in the round
+    int min_inliers;   // mRansacMinInliers
+    int best0;         // mnBestInliers when the round was launched
+    int rows0;         // maximum_number_of_correspondences when the round was launched
+    uint64_t* best;    // the solver's mvbBestInliers bits
+    uint64_t* refined; // mvbRefinedInliers bits
+    int words;         // words of best / refined (ceil(N/64))
+};
+struct RefineSelOut {
+    int k;           // first hypothesis with nInliers >= mRansacMinInliers, -1: none (nothing ran)
+    int adopt;       // it became the new best (mask + pose adopted on the device)
+    int rows_after;  // set_maximum_number_of_correspondences(max(rows0, mnBestInliers))
+    int count;       // mnRefinedInliers
+    float pose[12];      // refined R (9) + t (3)
+    float best_pose[12]; // adopted hypothesis pose (when adopt)
 };
 
 struct Window31 {
@@ -120,11 +142,20 @@ hipError_t launch_pnp_solve_split(int ns, int eig_shape, int nwgE, const int2* w
                                   const int2* wgtB, const DevPnP* probs, const LaunchProb* lps, const uint32_t* T,
                                   double* stage, float* poses, int32_t* samples, const BetasScratch& bs,
                                   hipStream_t st, hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr);
+// counts: where the host reads them (pinned memory or HBM); counts_dev (nullable): an HBM copy for
+// pnp_select_refine_kernel.
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,
-                           const float* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st);
+                           const float* poses, int32_t* counts, int32_t* counts_dev, uint64_t* masks, int mask_words,
+                           hipStream_t st);
+hipError_t launch_pnp_select_refine(int nsel, const DevPnP* probs, const RefineSel* sels, const int32_t* counts,
+                                    uint64_t* masks, int mask_words, const float* poses, RefineSelOut* out,
+                                    hipStream_t st);
+// Rounds up to this many hypotheses run the replay's first Refine on the device right after the
+// scan (pnp_select_refine_kernel): latency-bound rounds lose a host round trip; large exhaustive
+// rounds (config 2), where no hypothesis qualifies, keep their launch set unchanged.
+constexpr int kFusedRefineMaxHyps = 4096;
 hipError_t read_refine_stamps(uint64_t* out);  // diagnostic, [64][8]
-hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, int mask_words_out,
-                             hipStream_t st);
+hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, hipStream_t st);
 hipError_t launch_sim3_solve(int nwg, const DevSim3* probs, const LaunchProb* lps, const int2* wgt,
                              const uint32_t* T, float* poses, int32_t* samples, hipStream_t st);
 // counts: where the host reads them (pinned memory or HBM); counts_dev (nullable): an HBM copy for

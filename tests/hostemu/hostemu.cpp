@@ -189,8 +189,8 @@ struct EmuPnPBackend : PnPBackend {
         }
         return 0;
     }
-    int refine(PnPState* const* S, int count, const int* spec_j, const int* adopt_k, const int* rows_after,
-               int* rcount, float (*rpose)[12]) override {
+    int refine(PnPState* const* S, int count, const int* spec_j, const int* /*pause_k*/, const int* adopt_k,
+               const int* rows_after, int* rcount, float (*rpose)[12]) override {
         for (int i = 0; i < count; ++i) {
             EmuPnP* p = of(S[i]);
             PnPState& s = *S[i];
