@@ -205,6 +205,8 @@ struct rsc_context {
     double host_us[4] = {0, 0, 0, 0};
     bool direct_counts = true;  // env RSC_DIRECT_COUNTS=0 restores the HBM buffer + D2H copy
     bool fused_refine = true;   // env RSC_FUSED_REFINE=0: the replay's Refine always as its own launch
+    int eig_shape_force = -1;   // env RSC_EIG_SHAPE (0..2): fixed eigen-stage shape (A/B runs, tools/)
+    int betas_hb_force = 0;     // env RSC_BETAS_HB (1..64): fixed betas hypotheses per wave (A/B runs)
     bool dma_upload = false;    // env RSC_DMA_UPLOAD=1: descriptors by hipMemcpyAsync instead of the copy kernel
     std::chrono::steady_clock::time_point t_entry;
 };
@@ -429,6 +431,8 @@ struct HipPnPBackend : PnPBackend {
         const int HC = scan_chunk(total);  // hypotheses per scan workgroup
         int eig_shape = 0, hb = 64;         // launch shapes of the two solve stages (rsc_kernels.h)
         pnp_round_shape(total, eig_shape, hb);
+        if (C->eig_shape_force >= 0) eig_shape = C->eig_shape_force;
+        if (C->betas_hb_force > 0) hb = C->betas_hb_force;
         const int eig_step = kEigShapes[eig_shape].hyps;
         // The tables depend only on the round's shape (count, sample size and H per problem, HC):
         // a round with the shape of the previous one on this thread reuses them (building and
@@ -1017,6 +1021,8 @@ int rsc_context_create(int device, rsc_context** out) {
     C->own_stream = true;
     if (const char* m = std::getenv("RSC_DIRECT_COUNTS")) C->direct_counts = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_FUSED_REFINE")) C->fused_refine = std::strcmp(m, "0") != 0;
+    if (const char* m = std::getenv("RSC_EIG_SHAPE")) C->eig_shape_force = std::min(2, std::max(-1, std::atoi(m)));
+    if (const char* m = std::getenv("RSC_BETAS_HB")) C->betas_hb_force = std::min(64, std::max(0, std::atoi(m)));
     if (const char* m = std::getenv("RSC_DMA_UPLOAD")) C->dma_upload = std::strcmp(m, "0") != 0;
     C->table.build();
     if (int e = C->d_table.ensure(C->table.T.size())) return e;
