@@ -32,30 +32,27 @@ namespace rsc {
 // PnP hypotheses, two-kernel form (rsc_quad.h): lane-group eigenvectors (kEigLanes lanes per
 // hypothesis, kEigHyps per workgroup, one wave per SIMD), then one wave per beta approximation.
 // ------------------------------------------------------------------------------------------------
-// L lanes per hypothesis, HPW hypotheses per wave: (2, kEigHyps) for large rounds (config 2: 960
-// waves, one per SIMD); (4, 4) and (4, 1) for rounds that cannot fill the SIMDs anyway, where a wave
-// holding fewer hypotheses pays the union of fewer QR sweep windows (kEigShapes, rsc_kernels.h).
-template <int NS, int L, int HPW>
+template <int NS>
 __global__ __launch_bounds__(64) void pnp_eig_group_kernel(const DevPnP* __restrict__ probs,
                                                           const LaunchProb* __restrict__ lps,
                                                           const int2* __restrict__ wg_table,
                                                           const uint32_t* __restrict__ rng_T,
                                                           double* __restrict__ stage, int32_t* __restrict__ samples) {
-    __shared__ __attribute__((aligned(16))) double smem[HPW * kQuadRegion];
-    pnp_eig_group_body<NS, 99, L, HPW>(probs, lps, wg_table, rng_T, stage, samples, smem);
+    __shared__ __attribute__((aligned(16))) double smem[kEigHyps * kQuadRegion];
+    pnp_eig_group_body<NS, 99, kEigLanes, kEigHyps>(probs, lps, wg_table, rng_T, stage, samples, smem);
 }
 
 template <int NS>
 __global__ __launch_bounds__(64) void pnp_betas_kernel(const DevPnP* __restrict__ probs,
                                                        const LaunchProb* __restrict__ lps,
-                                                       const int2* __restrict__ wg_table, int ngroups, int hb,
+                                                       const int2* __restrict__ wg_table, int ngroups,
                                                        const double* __restrict__ stage,
                                                        const int32_t* __restrict__ samples,
                                                        float* __restrict__ poses, double* __restrict__ berr,
                                                        float* __restrict__ bpose, unsigned* __restrict__ bctr,
                                                        size_t hcap) {
     __shared__ __attribute__((aligned(16))) double smem[kBetasWaveSmemDoubles];
-    pnp_betas_wave_body<NS>(probs, lps, wg_table, ngroups, hb, stage, samples, poses, berr, bpose, bctr, hcap, smem);
+    pnp_betas_wave_body<NS>(probs, lps, wg_table, ngroups, kBetasHyps, stage, samples, poses, berr, bpose, bctr, hcap, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -877,26 +874,22 @@ __global__ void rng_stream_kernel(const uint32_t* __restrict__ T, Window31 w, in
 // ------------------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------------------
-hipError_t launch_pnp_solve_split(int ns, int eig_shape, int nwgE, const int2* wgtE, int hb, int nwgB,
-                                  const int2* wgtB, const DevPnP* probs, const LaunchProb* lps, const uint32_t* T,
-                                  double* stage, float* poses, int32_t* samples, const BetasScratch& bs,
-                                  hipStream_t st, hipEvent_t eig_begin, hipEvent_t eig_end) {
-    if (ns < 4 || ns > 6 || eig_shape < 0 || eig_shape > 2 || hb < 1 || hb > 64) return hipErrorInvalidValue;
+hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, const int2* wgtB,
+                                  const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
+                                  float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
+                                  hipEvent_t eig_begin, hipEvent_t eig_end) {
+    if (ns < 4 || ns > 6) return hipErrorInvalidValue;
     if (eig_begin) (void)hipEventRecord(eig_begin, st);
     switch (ns) {
-#define RSC_EIG(N, L, HPW) pnp_eig_group_kernel<N, L, HPW><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples)
 #define RSC_CASE(N)                                                                                   \
     case N:                                                                                           \
-        if (eig_shape == 0) RSC_EIG(N, kEigLanes, kEigHyps);                                          \
-        else if (eig_shape == 1) RSC_EIG(N, 4, 4);                                                    \
-        else RSC_EIG(N, 4, 1);                                                                        \
+        pnp_eig_group_kernel<N><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples);            \
         if (eig_end) (void)hipEventRecord(eig_end, st);                                               \
-        pnp_betas_kernel<N><<<3 * nwgB, 64, 0, st>>>(probs, lps, wgtB, nwgB, hb, stage, samples, poses,  \
+        pnp_betas_kernel<N><<<3 * nwgB, 64, 0, st>>>(probs, lps, wgtB, nwgB, stage, samples, poses,   \
                                                      bs.err, bs.pose, bs.ctr, bs.hcap);               \
         break;
         RSC_CASE(4) RSC_CASE(5) RSC_CASE(6)
 #undef RSC_CASE
-#undef RSC_EIG
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

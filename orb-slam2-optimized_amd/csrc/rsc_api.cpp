@@ -205,8 +205,6 @@ struct rsc_context {
     double host_us[4] = {0, 0, 0, 0};
     bool direct_counts = true;  // env RSC_DIRECT_COUNTS=0 restores the HBM buffer + D2H copy
     bool fused_refine = true;   // env RSC_FUSED_REFINE=0: the replay's Refine always as its own launch
-    int eig_shape_force = -1;   // env RSC_EIG_SHAPE (0..2): fixed eigen-stage shape (A/B runs, tools/)
-    int betas_hb_force = 0;     // env RSC_BETAS_HB (1..64): fixed betas hypotheses per wave (A/B runs)
     bool dma_upload = false;    // env RSC_DMA_UPLOAD=1: descriptors by hipMemcpyAsync instead of the copy kernel
     std::chrono::steady_clock::time_point t_entry;
 };
@@ -429,11 +427,7 @@ struct HipPnPBackend : PnPBackend {
         std::vector<int2>* quad_wgs = quad_wgs_tl;
         std::vector<int4>& scan_wgs = scan_wgs_tl;
         const int HC = scan_chunk(total);  // hypotheses per scan workgroup
-        int eig_shape = 0, hb = 64;         // launch shapes of the two solve stages (rsc_kernels.h)
-        pnp_round_shape(total, eig_shape, hb);
-        if (C->eig_shape_force >= 0) eig_shape = C->eig_shape_force;
-        if (C->betas_hb_force > 0) hb = C->betas_hb_force;
-        const int eig_step = kEigShapes[eig_shape].hyps;
+
         // The tables depend only on the round's shape (count, sample size and H per problem, HC):
         // a round with the shape of the previous one on this thread reuses them (building and
         // XCD-ordering ~3.7k entries costs ~10 us of host time per config-2 round).
@@ -444,8 +438,6 @@ struct HipPnPBackend : PnPBackend {
         key.clear();
         key.push_back(count);
         key.push_back(HC);
-        key.push_back(eig_shape);
-        key.push_back(hb);
         for (int i = 0; i < count; ++i) {
             key.push_back(S[i]->mRansacMinSet);
             key.push_back(H[i]);
@@ -455,8 +447,8 @@ struct HipPnPBackend : PnPBackend {
             scan_wgs.clear();
             for (int i = 0; i < count; ++i) {
                 const int g = S[i]->mRansacMinSet - 4;
-                for (int h0 = 0; h0 < H[i]; h0 += hb) solve_wgs[g].push_back(make_int2(i, h0));
-                for (int h0 = 0; h0 < H[i]; h0 += eig_step) quad_wgs[g].push_back(make_int2(i, h0));
+                for (int h0 = 0; h0 < H[i]; h0 += kBetasHyps) solve_wgs[g].push_back(make_int2(i, h0));
+                for (int h0 = 0; h0 < H[i]; h0 += kEigHyps) quad_wgs[g].push_back(make_int2(i, h0));
                 for (int h0 = 0; h0 < H[i]; h0 += HC)
                     scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
             }
@@ -510,9 +502,8 @@ struct HipPnPBackend : PnPBackend {
             if (solve_wgs[g].empty()) continue;
             // the first group's eigen stage starts at ev[0]: no extra event in the queue
             hipEvent_t eb = (C->timing && !first_group) ? C->ev[6 + 2 * g] : nullptr;
-            RSC_HIP(launch_pnp_solve_split(4 + g, eig_shape, (int)quad_wgs[g].size(),
-                                          reinterpret_cast<const int2*>(base + o_quad[g]), hb,
-                                          (int)solve_wgs[g].size(),
+            RSC_HIP(launch_pnp_solve_split(4 + g, (int)quad_wgs[g].size(),
+                                          reinterpret_cast<const int2*>(base + o_quad[g]), (int)solve_wgs[g].size(),
                                           reinterpret_cast<const int2*>(base + o_solve[g]), dprobs, dlps,
                                           C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p, bs, C->stream,
                                           eb, C->timing ? C->ev[7 + 2 * g] : nullptr));
@@ -1021,8 +1012,6 @@ int rsc_context_create(int device, rsc_context** out) {
     C->own_stream = true;
     if (const char* m = std::getenv("RSC_DIRECT_COUNTS")) C->direct_counts = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_FUSED_REFINE")) C->fused_refine = std::strcmp(m, "0") != 0;
-    if (const char* m = std::getenv("RSC_EIG_SHAPE")) C->eig_shape_force = std::min(2, std::max(-1, std::atoi(m)));
-    if (const char* m = std::getenv("RSC_BETAS_HB")) C->betas_hb_force = std::min(64, std::max(0, std::atoi(m)));
     if (const char* m = std::getenv("RSC_DMA_UPLOAD")) C->dma_upload = std::strcmp(m, "0") != 0;
     C->table.build();
     if (int e = C->d_table.ensure(C->table.T.size())) return e;

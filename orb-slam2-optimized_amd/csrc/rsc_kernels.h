@@ -124,24 +124,15 @@ struct BetasScratch {
     unsigned* ctr;
     size_t hcap;
 };
-// Launch shapes of the two stages, chosen per round from its hypothesis count: the eigen stage in
-// (lanes, hypotheses per wave) = (kEigLanes, kEigHyps) | (4, 4) | (4, 1) (eig_shape 0 | 1 | 2), the
-// betas stage with hb hypotheses per wave (64 for large rounds).  A wave of a latency-bound round
-// then carries the union of fewer hypotheses' data-dependent chains; results are bit-identical.
-struct EigShape {
-    int lanes, hyps;
-};
-constexpr EigShape kEigShapes[3] = {{kEigLanes, kEigHyps}, {4, 4}, {4, 1}};
-inline void pnp_round_shape(int total_hyps, int& eig_shape, int& hb) {
-    // eigen stage: one wave per SIMD at most (1,024 SIMDs); betas: 3 waves per group of hb
-    eig_shape = total_hyps <= 1024 ? 2 : (total_hyps <= 4096 ? 1 : 0);
-    hb = 64;
-    while (hb > 1 && 3 * ((total_hyps + hb - 1) / hb) * 2 <= 1024) hb >>= 1;
-}
-hipError_t launch_pnp_solve_split(int ns, int eig_shape, int nwgE, const int2* wgtE, int hb, int nwgB,
-                                  const int2* wgtB, const DevPnP* probs, const LaunchProb* lps, const uint32_t* T,
-                                  double* stage, float* poses, int32_t* samples, const BetasScratch& bs,
-                                  hipStream_t st, hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr);
+// Hypotheses per betas wave: 64.  Smaller waves for small (latency-bound) rounds, and eigen-stage
+// waves of quads x 4 or quads x 1 instead of pairs x 20, were measured slower on the single-event
+// case (tools/latency_ab.py, profiles/r03/latency_ab_r3_c.txt): the stage time is not the union of
+// a wave's hypotheses' chains but the per-wave latency, which more, narrower waves do not shorten.
+constexpr int kBetasHyps = 64;
+hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, const int2* wgtB,
+                                  const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
+                                  float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
+                                  hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr);
 // counts: where the host reads them (pinned memory or HBM); counts_dev (nullable): an HBM copy for
 // pnp_select_refine_kernel.
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostic A/B of the single-event latency (bench.py's relocalization event) across engine
-variants set through the environment at context creation (RSC_EIG_SHAPE, RSC_BETAS_HB,
-RSC_FUSED_REFINE): one context + solver set per variant in ONE process, the GPU first kept busy for
+variants set through the environment at context creation (e.g. RSC_FUSED_REFINE; the round-3
+RSC_EIG_SHAPE / RSC_BETAS_HB shapes were measured with it and removed): one context + solver set per variant in ONE process, the GPU first kept busy for
 ~1 s with the config-2 batch, then the variants measured in rotation (clock state shared).
     python3 tools/latency_ab.py "base:" "eig1:RSC_EIG_SHAPE=1" "hb64:RSC_BETAS_HB=64" ...
 Each argument is name:VAR=val,VAR=val.  Prints the median per variant."""
@@ -15,11 +15,13 @@ import numpy as np  # noqa: E402
 import bench  # noqa: E402
 from rsc import engine, workloads as wl  # noqa: E402
 
-KEYS = ("RSC_EIG_SHAPE", "RSC_BETAS_HB", "RSC_FUSED_REFINE")
-variants = []
+specs = []
 for arg in sys.argv[1:] or ["base:"]:
     name, _, spec = arg.partition(":")
-    env = dict(kv.split("=") for kv in spec.split(",") if kv)
+    specs.append((name, dict(kv.split("=") for kv in spec.split(",") if kv)))
+KEYS = sorted({k for _, env in specs for k in env})
+variants = []
+for name, env in specs:
     for k in KEYS:
         os.environ.pop(k, None)
     os.environ.update(env)
