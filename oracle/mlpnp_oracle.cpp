@@ -1,6 +1,7 @@
 // TEST INFRASTRUCTURE — parity oracle, never linked into the product library.
 // Restatement of src/MLPnPsolver.cpp (reference) — see mlpnp_oracle.h.  Line numbers cite the reference.
 #include "mlpnp_oracle.h"
+#include "ora_libm.h"
 #include "ora_linalg.h"
 #include "../orb-slam2-optimized_amd/csrc/rsc_math.h"
 #include <cassert>
@@ -322,8 +323,8 @@ void rodrigues2rot(const double w[3], double R[3][3]) {
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) R[i][j] = (i == j) ? 1.0 : 0.0;
     if (nrm > kEps) {
-        const double a = rsc::dm::sin(nrm) / nrm;
-        const double b = (1.0 - rsc::dm::cos(nrm)) / (nrm * nrm);
+        const double a = ora_libm::sin(nrm) / nrm;
+        const double b = (1.0 - ora_libm::cos(nrm)) / (nrm * nrm);
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) {
                 const double ss = S[i][0] * S[0][j] + S[i][1] * S[1][j] + S[i][2] * S[2][j];
@@ -336,12 +337,12 @@ void rodrigues2rot(const double w[3], double R[3][3]) {
 void rot2rodrigues(const double R[3][3], double w[3]) {
     w[0] = w[1] = w[2] = 0.0;
     const double trace = ((R[0][0] + R[1][1]) + R[2][2]) - 1.0;
-    const double wnorm = rsc::dm::acos(trace / 2.0);
+    const double wnorm = ora_libm::acos(trace / 2.0);
     if (wnorm > kEps) {
         w[0] = R[2][1] - R[1][2];
         w[1] = R[0][2] - R[2][0];
         w[2] = R[1][0] - R[0][1];
-        const double sc = wnorm / (2.0 * rsc::dm::sin(wnorm));
+        const double sc = wnorm / (2.0 * ora_libm::sin(wnorm));
         for (int k = 0; k < 3; ++k) w[k] *= sc;
     }
 }
@@ -354,8 +355,8 @@ void mlpnp_jac(const double X[3], const double nr[3], const double ns[3], const 
                double J[2][6]) {
     const double th2 = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
     const double th = std::sqrt(th2);
-    const double a = rsc::dm::sin(th) / th;
-    const double b = (1.0 - rsc::dm::cos(th)) / th2;
+    const double a = ora_libm::sin(th) / th;
+    const double b = (1.0 - ora_libm::cos(th)) / th2;
     const double S[3][3] = {{0.0, -w[2], w[1]}, {w[2], 0.0, -w[0]}, {-w[1], w[0], 0.0}};
     double R[3][3];
     for (int i = 0; i < 3; ++i)
@@ -674,7 +675,7 @@ void MLPnPOracle::computePose(const int* idx, int n, double Rout[3][3], double t
         double tmp[3][3] = {{r1[0], r1[3], r1[6]}, {r1[1], r1[4], r1[7]}, {r1[2], r1[5], r1[8]}};
         const double c0[3] = {tmp[0][0], tmp[1][0], tmp[2][0]}, c1[3] = {tmp[0][1], tmp[1][1], tmp[2][1]},
                      c2[3] = {tmp[0][2], tmp[1][2], tmp[2][2]};
-        const double scale = 1.0 / rsc::dm::cbrt(std::fabs(norm3(c0) * norm3(c1) * norm3(c2)));
+        const double scale = 1.0 / ora_libm::cbrt_pow(std::fabs(norm3(c0) * norm3(c1) * norm3(c2)));
         double U3[9], S3[3], V3[9];
         jacobi_svd_square(3, &tmp[0][0], true, U3, S3, V3);
         for (int r = 0; r < 3; ++r)

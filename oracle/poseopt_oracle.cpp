@@ -1,6 +1,7 @@
 // TEST INFRASTRUCTURE — parity oracle, never linked into the product library.
 // Sequential restatement of Optimizer::PoseOptimization + the g2o code it runs (see header).
 #include "poseopt_oracle.h"
+#include "ora_libm.h"
 
 #include <algorithm>
 #include <cfloat>
@@ -153,7 +154,7 @@ SE3 se3_exp(const double u[6]) {
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) V[i][j] = R[i][j];
     } else {
-        const double st = rsc::dm::sin(theta), ct = rsc::dm::cos(theta);
+        const double st = ora_libm::sin(theta), ct = ora_libm::cos(theta);
         const double a = st / theta;
         const double b = (1.0 - ct) / (theta * theta);
         const double c = (theta - st) / cube(theta);

@@ -1,5 +1,6 @@
 // TEST INFRASTRUCTURE — parity oracle (see sim3match_oracle.h).
 #include "sim3match_oracle.h"
+#include "ora_libm.h"
 
 #include <algorithm>
 #include <climits>
@@ -85,7 +86,7 @@ void search_direction(const Sim3KF& src, const Sim3KF& dst, const float* Rsd, co
 
 int predict_scale(float dmax, float current_dist, float log_scale_factor, int n_levels) {
     const float ratio = dmax / current_dist;
-    int nScale = (int)std::ceil(rsc::dm::logf(ratio) / log_scale_factor);
+    int nScale = (int)std::ceil(ora_libm::logf(ratio) / log_scale_factor);
     if (nScale < 0) nScale = 0;
     else if (nScale >= n_levels) nScale = n_levels - 1;
     return nScale;

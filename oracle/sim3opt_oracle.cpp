@@ -1,6 +1,7 @@
 // TEST INFRASTRUCTURE — parity oracle, never linked into the product library.
 // Sequential restatement of Optimizer::OptimizeSim3 + the g2o code it runs (see the header).
 #include "sim3opt_oracle.h"
+#include "ora_libm.h"
 
 #include <cfloat>
 #include <cmath>
@@ -132,7 +133,7 @@ Sim3 sim3_exp(const double u[7]) {
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j) R[i][j] = ((i == j ? 1.0 : 0.0) + Om[i][j]) + Om2[i][j];
         } else {
-            const double st = rsc::dm::sin(theta), ct = rsc::dm::cos(theta);
+            const double st = ora_libm::sin(theta), ct = ora_libm::cos(theta);
             const double theta2 = theta * theta;
             A = (1 - ct) / (theta2);
             B = (theta - st) / (theta2 * theta);
@@ -149,7 +150,7 @@ Sim3 sim3_exp(const double u[7]) {
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j) R[i][j] = ((i == j ? 1.0 : 0.0) + Om[i][j]) + Om2[i][j];
         } else {
-            const double st = rsc::dm::sin(theta), ct = rsc::dm::cos(theta);
+            const double st = ora_libm::sin(theta), ct = ora_libm::cos(theta);
             const double ra = st / theta, rb = (1 - ct) / (theta * theta);
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j) R[i][j] = ((i == j ? 1.0 : 0.0) + ra * Om[i][j]) + rb * Om2[i][j];

@@ -10,7 +10,11 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(ROOT, "oracle", "build", "librsc_oracle.so")
+# RSC_ORACLE_LIBM=glibc selects the build whose transcendental functions are host glibc's (the
+# reference's), for tests/test_cpu_libm_choice.py; the default build is the checker.
+LIB_PATH = os.path.join(ROOT, "oracle", "build",
+                        "librsc_oracle_glibc.so" if os.environ.get("RSC_ORACLE_LIBM") == "glibc"
+                        else "librsc_oracle.so")
 
 _lib = None
 
@@ -25,7 +29,7 @@ u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
 def build_oracle() -> str:
     if not os.path.exists(LIB_PATH) or _stale():
         import subprocess
-        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "all"])
     return LIB_PATH
 
 
