@@ -15,6 +15,10 @@ $(LIBDIR)/kernels.o: $(CSRC)/kernels.hip $(HDRS)
 	mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(LIBDIR)/mlpnp.o: $(CSRC)/mlpnp.hip $(HDRS)
+	mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(LIBDIR)/poseopt.o: $(CSRC)/poseopt.hip $(HDRS)
 	mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -39,7 +43,7 @@ $(LIBDIR)/rsc_api.o: $(CSRC)/rsc_api.cpp $(HDRS)
 	mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIBDIR)/librsc.so: $(LIBDIR)/kernels.o $(LIBDIR)/poseopt.o $(LIBDIR)/sim3opt.o $(LIBDIR)/orbmatch.o $(LIBDIR)/sim3match.o $(LIBDIR)/kfdb.o $(LIBDIR)/rsc_api.o
+$(LIBDIR)/librsc.so: $(LIBDIR)/kernels.o $(LIBDIR)/mlpnp.o $(LIBDIR)/poseopt.o $(LIBDIR)/sim3opt.o $(LIBDIR)/orbmatch.o $(LIBDIR)/sim3match.o $(LIBDIR)/kfdb.o $(LIBDIR)/rsc_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 facade_test: $(LIBDIR)/facade_test

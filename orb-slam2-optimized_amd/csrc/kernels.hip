@@ -11,6 +11,7 @@
 //                          EPnP buffers, EPnP over n_r rows (MtM built block-parallel), then the
 //                          block-parallel CheckInliers of the refined pose.
 //   sim3_solve_kernel / sim3_scan_kernel   the same split for Sim3Solver (Horn, float).
+//   (MLPnPsolver's kernels are in mlpnp.hip.)
 //
 // Reference: src/PnPsolver.cpp, src/Sim3Solver.cpp (see rsc_core.h for the arithmetic contract).
 #include <hip/hip_runtime.h>
@@ -20,7 +21,6 @@
 #include "rsc_sim3.h"
 #include "rsc_quad.h"
 #include "rsc_math.h"
-#include "rsc_mlpnp.h"
 #include "rsc_kernels.h"
 
 namespace rsc {
@@ -655,126 +655,6 @@ __global__ __launch_bounds__(256) void sim3_scan_kernel(const DevSim3* __restric
             __syncthreads();
         }
     }
-}
-
-// ------------------------------------------------------------------------------------------------
-// MLPnP hypotheses (one lane each, W/V of the 12x12 JacobiSVD in a 288-double LDS slab per lane)
-// and the MLPnP CheckInliers scan.
-// ------------------------------------------------------------------------------------------------
-template <int NS>
-__global__ __launch_bounds__(64) void mlpnp_solve_kernel(const DevML* __restrict__ probs,
-                                                         const LaunchProb* __restrict__ lps,
-                                                         const int2* __restrict__ wg_table,
-                                                         const uint32_t* __restrict__ rng_T,
-                                                         double* __restrict__ poses, int32_t* __restrict__ samples) {
-    __shared__ __attribute__((aligned(16))) double slab[kMlSlabDoubles * 64];
-    const int lane = threadIdx.x;
-    const int2 wt = wg_table[blockIdx.x];
-    const LaunchProb& lp = lps[wt.x];
-    const int h = wt.y + lane;
-    if (h >= lp.H) return;
-    const DevML& P = probs[lp.prob];
-    int idx[NS];
-    {
-        uint32_t w[31];
-        RSC_UNROLL for (int j = 0; j < 31; ++j) w[j] = lp.window[j];
-        uint32_t words[NS];
-        RSC_UNROLL for (int d = 0; d < NS; ++d) words[d] = rng_word(rng_T, w, lp.g0 + h * NS + d);
-        swap_remove_sample<NS>(words, NS, P.n, idx);
-    }
-    double pw[NS][3], f[NS][3];
-    RSC_UNROLL for (int i = 0; i < NS; ++i) {
-        const float4 p = P.pts[idx[i]];
-        const float2 b = P.brg[idx[i]];
-        pw[i][0] = p.x; pw[i][1] = p.y; pw[i][2] = p.z;
-        f[i][0] = b.x; f[i][1] = b.y; f[i][2] = 1.0;
-    }
-    double R[3][3], t[3];
-    if (P.cov) {  // covariances supplied: the covMats branch of computePose
-        mlpnp_compute_pose<NS>(pw, f, LaneMat{slab + lane, 64}, R, t, MlIndexedCov{P.cov, idx});
-    } else {
-        mlpnp_compute_pose<NS>(pw, f, LaneMat{slab + lane, 64}, R, t);
-    }
-    const size_t rec = (size_t)(lp.out0 + h);
-    double* out = poses + rec * 12;
-    RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) out[3 * r + c] = R[r][c];
-    RSC_UNROLL for (int r = 0; r < 3; ++r) out[9 + r] = t[r];
-    if (samples) RSC_UNROLL for (int i = 0; i < NS; ++i) samples[rec * 8 + i] = idx[i];
-}
-
-template <int PPT>
-__global__ __launch_bounds__(256) void mlpnp_scan_kernel(const DevML* __restrict__ probs,
-                                                         const LaunchProb* __restrict__ lps,
-                                                         const int4* __restrict__ wg_table,
-                                                         const double* __restrict__ poses,
-                                                         int32_t* __restrict__ counts,
-                                                         uint64_t* __restrict__ masks, int mask_words) {
-    __shared__ int wave_cnt[4][64];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int4 wt = wg_table[blockIdx.x];
-    const LaunchProb& lp = lps[wt.x];
-    const DevML& P = probs[lp.prob];
-    float X[PPT], Y[PPT], Z[PPT], U[PPT], V[PPT], E[PPT];
-    RSC_UNROLL for (int s = 0; s < PPT; ++s) {
-        const int i = s * 256 + tid;
-        if (i < P.n) {
-            const float4 p = P.pts[i];
-            const float2 q = P.uv[i];
-            X[s] = p.x; Y[s] = p.y; Z[s] = p.z; E[s] = p.w * P.th2; U[s] = q.x; V[s] = q.y;
-        } else {
-            X[s] = 0.f; Y[s] = 0.f; Z[s] = 1.f; E[s] = -1.f; U[s] = 0.f; V[s] = 0.f;
-        }
-    }
-    for (int j = 0; j < wt.z; ++j) {
-        const int h = wt.y + j;
-        const double* pp = poses + (size_t)(lp.out0 + h) * 12;
-        double R[9], t[3];
-        RSC_UNROLL for (int k = 0; k < 9; ++k) R[k] = pp[k];
-        RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = pp[9 + k];
-        // all PPT ballots first, then one predicated store by lanes 0..PPT-1 (as the PnP scan)
-        uint64_t b[PPT];
-        RSC_UNROLL for (int s = 0; s < PPT; ++s)
-            b[s] = __ballot(mlpnp_inlier(R, t, P.fx, P.fy, P.cx, P.cy, X[s], Y[s], Z[s], U[s], V[s], E[s]));
-        int cnt = 0;
-        uint64_t mine = 0;
-        RSC_UNROLL for (int s = 0; s < PPT; ++s) {
-            cnt += __popcll(b[s]);
-            mine = (lane == s) ? b[s] : mine;
-        }
-        if (masks && lane < PPT) masks[(size_t)(lp.out0 + h) * mask_words + lane * 4 + wave] = mine;
-        if (lane == 0) wave_cnt[wave][j & 63] = cnt;
-        if ((j & 63) == 63 || j == wt.z - 1) {
-            __syncthreads();
-            const int base = j & ~63;
-            if (tid <= (j & 63)) {
-                const int c = wave_cnt[0][tid] + wave_cnt[1][tid] + wave_cnt[2][tid] + wave_cnt[3][tid];
-                counts[lp.out0 + wt.y + base + tid] = c;
-            }
-            __syncthreads();
-        }
-    }
-}
-
-hipError_t launch_mlpnp_solve(int ns, int nwg, const DevML* probs, const LaunchProb* lps, const int2* wgt,
-                              const uint32_t* T, double* poses, int32_t* samples, hipStream_t st) {
-    switch (ns) {
-        case 6: mlpnp_solve_kernel<6><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples); break;
-        case 7: mlpnp_solve_kernel<7><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples); break;
-        case 8: mlpnp_solve_kernel<8><<<nwg, 64, 0, st>>>(probs, lps, wgt, T, poses, samples); break;
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_mlpnp_scan(int ppt, int nwg, const DevML* probs, const LaunchProb* lps, const int4* wgt,
-                             const double* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st) {
-    switch (ppt) {
-#define RSC_CASE(P) case P: mlpnp_scan_kernel<P><<<nwg, 256, 0, st>>>(probs, lps, wgt, poses, counts, masks, mask_words); break;
-        RSC_CASE(1) RSC_CASE(2) RSC_CASE(4) RSC_CASE(8) RSC_CASE(16) RSC_CASE(32)
-#undef RSC_CASE
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
 }
 
 // Gather `take` floats of records idx[q] (record stride `stride` floats) into dst[q][take].

@@ -866,12 +866,12 @@ struct HipMLBackend : MLBackend {
         }
         const int mw = ppt * 4;
         C->mask_words = mw;
-        std::vector<std::vector<int2>> solve_wgs(3);
+        std::vector<std::vector<int2>> solve_wgs(6);  // by (min_set, covariances given)
         std::vector<int4> scan_wgs;
         const int HC = 32;
         for (int i = 0; i < count; ++i) {
-            const int g = S[i]->mRansacMinSet - 6;
-            for (int h0 = 0; h0 < H[i]; h0 += 64) solve_wgs[g].push_back(make_int2(i, h0));
+            const int g = 2 * (S[i]->mRansacMinSet - 6) + (probs[i].cov ? 1 : 0);
+            for (int h0 = 0; h0 < H[i]; h0 += kMlQuadHyps) solve_wgs[g].push_back(make_int2(i, h0));
             for (int h0 = 0; h0 < H[i]; h0 += HC) scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
         }
         for (auto& t : solve_wgs) xcd_order(t, [](const int2& w) { return w.x; });
@@ -879,8 +879,8 @@ struct HipMLBackend : MLBackend {
         Blob b;
         const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevML));
         const size_t o_lps = b.add(lps.data(), lps.size() * sizeof(LaunchProb));
-        size_t o_solve[3];
-        for (int g = 0; g < 3; ++g) o_solve[g] = b.add(solve_wgs[g].data(), solve_wgs[g].size() * sizeof(int2));
+        size_t o_solve[6];
+        for (int g = 0; g < 6; ++g) o_solve[g] = b.add(solve_wgs[g].data(), solve_wgs[g].size() * sizeof(int2));
         const size_t o_scan = b.add(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
         if (int e = upload_blob(C, b)) return e;
         if (int e = C->d_mposes.ensure((size_t)total * 12)) return e;
@@ -893,9 +893,9 @@ struct HipMLBackend : MLBackend {
         const DevML* dprobs = reinterpret_cast<const DevML*>(base + o_probs);
         const LaunchProb* dlps = reinterpret_cast<const LaunchProb*>(base + o_lps);
         timing_begin(C, 0);
-        for (int g = 0; g < 3; ++g) {
+        for (int g = 0; g < 6; ++g) {
             if (solve_wgs[g].empty()) continue;
-            RSC_HIP(launch_mlpnp_solve(6 + g, (int)solve_wgs[g].size(), dprobs, dlps,
+            RSC_HIP(launch_mlpnp_solve(6 + g / 2, (g & 1) != 0, (int)solve_wgs[g].size(), dprobs, dlps,
                                        reinterpret_cast<const int2*>(base + o_solve[g]), C->d_table.p, C->d_mposes.p,
                                        C->keep_samples ? C->d_samples.p : nullptr, C->stream));
         }

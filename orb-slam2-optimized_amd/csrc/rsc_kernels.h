@@ -90,8 +90,11 @@ struct RefineSelOut {
 struct Window31 {
     uint32_t w[31];
 };
-// MLPnP: one lane per hypothesis (min_set 6..8), poses as double[12] records (R row-major, t).
-hipError_t launch_mlpnp_solve(int ns, int nwg, const DevML* probs, const LaunchProb* lps, const int2* wgt,
+// MLPnP: one quad per hypothesis, kMlQuadHyps per workgroup (min_set 6..8), poses as double[12]
+// records (R row-major, t).
+constexpr int kMlQuadHyps = 16;  // MLPnP hypotheses (quads) per 64-lane workgroup (rsc_mlpnp_quad.h)
+// cov: the workgroups' problems carry bearing covariances (DevML::cov != null)
+hipError_t launch_mlpnp_solve(int ns, bool cov, int nwg, const DevML* probs, const LaunchProb* lps, const int2* wgt,
                               const uint32_t* T, double* poses, int32_t* samples, hipStream_t st);
 hipError_t launch_mlpnp_scan(int ppt, int nwg, const DevML* probs, const LaunchProb* lps, const int4* wgt,
                              const double* poses, int32_t* counts, uint64_t* masks, int mask_words, hipStream_t st);

@@ -578,18 +578,22 @@ RSC_HD void ml_cov_weight(const double (&N)[3][2], const Cov& cov, int i, double
     P[3] = T[0][0] * invdet;
 }
 
-// MLPnPsolver::computePose for NS correspondences (pts world, f bearings), result R (row-major), t.
-// S: the lane slab (kMlSlabDoubles doubles, element stride S.stride).  With covariances (Cov::on)
-// the normal equations are A^T P A and the Gauss-Newton system J^T Kll J, J^T Kll r (:483-484,
-// :694-695), P = Kll block-diagonal with the 2x2 weights above; each product restated as
-// (A^T P) first, then the row sums in order.
-template <int NS, class Cov = MlNoCov>
-RSC_HD void mlpnp_compute_pose(const double (&pw)[NS][3], const double (&f)[NS][3], const LaneMat& slab,
-                               double (&Rout)[3][3], double (&tout)[3], const Cov& cov = Cov()) {
+// Phase 1 of MLPnPsolver::computePose (:321-416): bearing nullspaces, covariance weights (covMats),
+// the planarity test (FullPivHouseholderQR rank of P P^T) and the points P (rotated into the plane's
+// eigenbasis when planar).  Shared by the lane form (mlpnp_compute_pose) and the quad kernel.
+template <int NS, class Cov>
+struct MlPrep {
     double Ns[NS][3][2];
-    RSC_UNROLL for (int i = 0; i < NS; ++i) ml_bearing_nullspace(f[i], Ns[i]);
     double Pw[Cov::on ? NS : 1][4];
-    if constexpr (Cov::on) RSC_UNROLL for (int i = 0; i < NS; ++i) ml_cov_weight(Ns[i], cov, i, Pw[i]);
+    double eigenRot[3][3];
+    double P[NS][3];
+    bool planar;
+};
+
+template <int NS, class Cov>
+RSC_HD void mlpnp_prepare(const double (&pw)[NS][3], const double (&f)[NS][3], const Cov& cov, MlPrep<NS, Cov>& m) {
+    RSC_UNROLL for (int i = 0; i < NS; ++i) ml_bearing_nullspace(f[i], m.Ns[i]);
+    if constexpr (Cov::on) RSC_UNROLL for (int i = 0; i < NS; ++i) ml_cov_weight(m.Ns[i], cov, i, m.Pw[i]);
     double PPt[3][3];
     RSC_UNROLL for (int a = 0; a < 3; ++a)
         RSC_UNROLL for (int b = 0; b < 3; ++b) {
@@ -597,75 +601,77 @@ RSC_HD void mlpnp_compute_pose(const double (&pw)[NS][3], const double (&f)[NS][
             RSC_UNROLL for (int i = 1; i < NS; ++i) s = s + pw[i][a] * pw[i][b];
             PPt[a][b] = s;
         }
-    const bool planar = ml_fullpiv_rank3(PPt) == 2;
-    double eigenRot[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
-    double P[NS][3];
-    RSC_UNROLL for (int i = 0; i < NS; ++i) RSC_UNROLL for (int c = 0; c < 3; ++c) P[i][c] = pw[i][c];
-    if (planar) {
+    m.planar = ml_fullpiv_rank3(PPt) == 2;
+    RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) m.eigenRot[r][c] = (r == c) ? 1.0 : 0.0;
+    RSC_UNROLL for (int i = 0; i < NS; ++i) RSC_UNROLL for (int c = 0; c < 3; ++c) m.P[i][c] = pw[i][c];
+    if (m.planar) {
         double Ve[3][3], we[3];
         sym_eig_reg<double, 3>(PPt, Ve, we);
-        RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) eigenRot[r][c] = Ve[c][r];
+        RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) m.eigenRot[r][c] = Ve[c][r];
         RSC_UNROLL for (int i = 0; i < NS; ++i) {
             double q[3];
             RSC_UNROLL for (int r = 0; r < 3; ++r)
-                q[r] = eigenRot[r][0] * P[i][0] + eigenRot[r][1] * P[i][1] + eigenRot[r][2] * P[i][2];
-            RSC_UNROLL for (int r = 0; r < 3; ++r) P[i][r] = q[r];
+                q[r] = m.eigenRot[r][0] * m.P[i][0] + m.eigenRot[r][1] * m.P[i][1] + m.eigenRot[r][2] * m.P[i][2];
+            RSC_UNROLL for (int r = 0; r < 3; ++r) m.P[i][r] = q[r];
         }
     }
-    const int colsA = planar ? 9 : 12;
-    const MlView W{slab.base, slab.stride, 0}, V{slab.base, slab.stride, 144};
-    // A^T A (A built on the fly; lower triangle computed, upper mirrored — exact symmetry)
-    auto Aent = [&](int i, int s, int col) -> double {
-        const double n0 = Ns[i][0][s], n1 = Ns[i][1][s], n2 = Ns[i][2][s];
-        if (planar) {
-            switch (col) {
-                case 0: return n0 * P[i][1]; case 1: return n0 * P[i][2];
-                case 2: return n1 * P[i][1]; case 3: return n1 * P[i][2];
-                case 4: return n2 * P[i][1]; case 5: return n2 * P[i][2];
-                case 6: return n0; case 7: return n1; default: return n2;
-            }
-        }
-        switch (col) {
-            case 0: return n0 * P[i][0]; case 1: return n0 * P[i][1]; case 2: return n0 * P[i][2];
-            case 3: return n1 * P[i][0]; case 4: return n1 * P[i][1]; case 5: return n1 * P[i][2];
-            case 6: return n2 * P[i][0]; case 7: return n2 * P[i][1]; case 8: return n2 * P[i][2];
-            case 9: return n0; case 10: return n1; default: return n2;
-        }
-    };
-    if constexpr (Cov::on) {
-        // (A^T P)(a, 2i + q) = A(2i, a) P_i(0, q) + A(2i + 1, a) P_i(1, q); both triangles (P_i
-        // need not be exactly symmetric)
-        auto AtP = [&](int a, int i, int q) { return Aent(i, 0, a) * Pw[i][q] + Aent(i, 1, a) * Pw[i][2 + q]; };
-        RSC_UNROLL for (int a = 0; a < 12; ++a)
-            RSC_UNROLL for (int b = 0; b < 12; ++b) {
-                if (a < colsA && b < colsA) {
-                    double s = AtP(a, 0, 0) * Aent(0, 0, b);
-                    s = s + AtP(a, 0, 1) * Aent(0, 1, b);
-                    RSC_UNROLL for (int i = 1; i < NS; ++i) {
-                        s = s + AtP(a, i, 0) * Aent(i, 0, b);
-                        s = s + AtP(a, i, 1) * Aent(i, 1, b);
-                    }
-                    W.at(a, b) = s;
-                }
-            }
-    } else {
-        RSC_UNROLL for (int a = 0; a < 12; ++a)
-            RSC_UNROLL for (int b = 0; b <= a; ++b) {
-                if (a < colsA) {
-                    double s = Aent(0, 0, a) * Aent(0, 0, b);
-                    s = s + Aent(0, 1, a) * Aent(0, 1, b);
-                    RSC_UNROLL for (int i = 1; i < NS; ++i) {
-                        s = s + Aent(i, 0, a) * Aent(i, 0, b);
-                        s = s + Aent(i, 1, a) * Aent(i, 1, b);
-                    }
-                    W.at(a, b) = s;
-                    W.at(b, a) = s;
-                }
-            }
-    }
-    double r1[12];
-    ml_jacobi_svd_lds(W, V, colsA, r1);
+}
 
+// Row (2i + s) of the design matrix A (:418-470), column col (< 9 planar, < 12 general).
+template <int NS, class Cov>
+RSC_HD double mlpnp_A(const MlPrep<NS, Cov>& m, int i, int s, int col) {
+    const double n0 = m.Ns[i][0][s], n1 = m.Ns[i][1][s], n2 = m.Ns[i][2][s];
+    if (m.planar) {
+        switch (col) {
+            case 0: return n0 * m.P[i][1]; case 1: return n0 * m.P[i][2];
+            case 2: return n1 * m.P[i][1]; case 3: return n1 * m.P[i][2];
+            case 4: return n2 * m.P[i][1]; case 5: return n2 * m.P[i][2];
+            case 6: return n0; case 7: return n1; default: return n2;
+        }
+    }
+    switch (col) {
+        case 0: return n0 * m.P[i][0]; case 1: return n0 * m.P[i][1]; case 2: return n0 * m.P[i][2];
+        case 3: return n1 * m.P[i][0]; case 4: return n1 * m.P[i][1]; case 5: return n1 * m.P[i][2];
+        case 6: return n2 * m.P[i][0]; case 7: return n2 * m.P[i][1]; case 8: return n2 * m.P[i][2];
+        case 9: return n0; case 10: return n1; default: return n2;
+    }
+}
+
+// Entry (a, b) of the normal matrix A^T A (:471-478), or A^T P A with covariances (:483-484,
+// evaluated as (A^T P) then the row sums in order).  ra[i][s] / rb[i][s]: A(2i + s, a) / A(2i + s, b).
+// Without covariances the value is symmetric bit for bit (the products commute).
+template <int NS, class Cov>
+RSC_HD double mlpnp_normal_entry(const MlPrep<NS, Cov>& m, const double (&ra)[NS][2], const double (&rb)[NS][2]) {
+    if constexpr (Cov::on) {
+        auto AtP = [&](int i, int q) { return ra[i][0] * m.Pw[i][q] + ra[i][1] * m.Pw[i][2 + q]; };
+        double s = AtP(0, 0) * rb[0][0];
+        s = s + AtP(0, 1) * rb[0][1];
+        RSC_UNROLL for (int i = 1; i < NS; ++i) {
+            s = s + AtP(i, 0) * rb[i][0];
+            s = s + AtP(i, 1) * rb[i][1];
+        }
+        return s;
+    } else {
+        double s = ra[0][0] * rb[0][0];
+        s = s + ra[0][1] * rb[0][1];
+        RSC_UNROLL for (int i = 1; i < NS; ++i) {
+            s = s + ra[i][0] * rb[i][0];
+            s = s + ra[i][1] * rb[i][1];
+        }
+        return s;
+    }
+}
+
+// Phase 3 of computePose (:480-623): pose recovery from the null vector r1 (the V column of the
+// smallest singular value of the normal matrix) and the Gauss-Newton refinement (mlpnp_gn,
+// :659-723).  slab: kMlSlabDoubles doubles (element stride slab.stride) for J and the LDLT system.
+template <int NS, class Cov>
+RSC_HD void mlpnp_finish_pose(const double (&pw)[NS][3], const double (&f)[NS][3], const MlPrep<NS, Cov>& m,
+                              const double (&r1)[12], const LaneMat& slab, double (&Rout)[3][3], double (&tout)[3]) {
+    const bool planar = m.planar;
+    const auto& eigenRot = m.eigenRot;
+    const auto& Ns = m.Ns;
+    const auto& Pw = m.Pw;
     double R[3][3], t[3];
     if (planar) {
         double tmp[3][3] = {{0.0, r1[0], r1[1]}, {0.0, r1[2], r1[3]}, {0.0, r1[4], r1[5]}};
@@ -840,6 +846,34 @@ RSC_HD void mlpnp_compute_pose(const double (&pw)[NS][3], const double (&f)[NS][
     tout[0] = x[3];
     tout[1] = x[4];
     tout[2] = x[5];
+}
+
+// MLPnPsolver::computePose for NS correspondences (pts world, f bearings), result R (row-major), t,
+// one lane (the sequential composition; the host emulation tests it and the quad kernel runs the same
+// phases with the 12x12 SVD spread over four lanes).  S: the lane slab (kMlSlabDoubles doubles,
+// element stride S.stride): the normal matrix and V of the JacobiSVD, then J and the LDLT system.
+template <int NS, class Cov = MlNoCov>
+RSC_HD void mlpnp_compute_pose(const double (&pw)[NS][3], const double (&f)[NS][3], const LaneMat& slab,
+                               double (&Rout)[3][3], double (&tout)[3], const Cov& cov = Cov()) {
+    MlPrep<NS, Cov> m;
+    mlpnp_prepare<NS, Cov>(pw, f, cov, m);
+    const int colsA = m.planar ? 9 : 12;
+    const MlView W{slab.base, slab.stride, 0}, V{slab.base, slab.stride, 144};
+    RSC_UNROLL for (int a = 0; a < 12; ++a)
+        RSC_UNROLL for (int b = 0; b < 12; ++b) {
+            if (a < colsA && b < colsA) {
+                double ra[NS][2], rb[NS][2];
+                RSC_UNROLL for (int i = 0; i < NS; ++i)
+                    RSC_UNROLL for (int s2 = 0; s2 < 2; ++s2) {
+                        ra[i][s2] = mlpnp_A<NS, Cov>(m, i, s2, a);
+                        rb[i][s2] = mlpnp_A<NS, Cov>(m, i, s2, b);
+                    }
+                W.at(a, b) = mlpnp_normal_entry<NS, Cov>(m, ra, rb);
+            }
+        }
+    double r1[12];
+    ml_jacobi_svd_lds(W, V, colsA, r1);
+    mlpnp_finish_pose<NS, Cov>(pw, f, m, r1, slab, Rout, tout);
 }
 
 // MLPnPsolver::CheckInliers for one correspondence (MLPnPsolver.cpp:222-255).
