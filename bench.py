@@ -56,6 +56,7 @@ def parse():
     p.add_argument("--corrs", type=int, default=2000)
     p.add_argument("--iters", type=int, default=300)
     p.add_argument("--strong", action="store_true", help="split one 64-candidate batch across the ranks")
+    p.add_argument("--mlpnp-candidates", type=int, default=128, help="config-4 candidates (sharded over the ranks)")
     p.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-cores CPU baseline (0: auto)")
     p.add_argument("--no-cpu", action="store_true")
     for s in ("sim3", "mlpnp", "events", "latency", "poseopt", "bow", "sim3match", "sim3opt", "kfdb", "config1",
@@ -1086,7 +1087,7 @@ def main():
     if not args.no_sim3:
         s3, s3_solvers, _ = run_sim3(engine, ctx, wl.config3_pairs(), args, dist, rank, world)
     if not args.no_mlpnp:
-        sc4 = wl.config4_scenes(candidates=wl.CONFIG4["candidates"])
+        sc4 = wl.config4_scenes(candidates=args.mlpnp_candidates)
         m4, _ = run_mlpnp(engine, ctx, sc4, args, False, dist, rank, world)
         m4["with_covariances"] = _rounded(run_mlpnp(engine, ctx, sc4, args, True, dist, rank, world)[0], 3)
     if rank == 0:
