@@ -662,16 +662,29 @@ RSC_HD double mlpnp_normal_entry(const MlPrep<NS, Cov>& m, const double (&ra)[NS
     }
 }
 
+// Read access to a hypothesis' correspondences and phase-1 state for mlpnp_finish_pose: from
+// registers (MlRegs, the sequential form) or from the quad kernel's parked LDS copy (MlParked in
+// rsc_mlpnp_quad.h), so that kernel does not hold them in VGPRs through the Gauss-Newton loop.
+template <int NS, class Cov>
+struct MlRegs {
+    const double (&pw_)[NS][3];
+    const double (&f_)[NS][3];
+    const MlPrep<NS, Cov>& m;
+    RSC_HD double pw(int i, int c) const { return pw_[i][c]; }
+    RSC_HD double f(int i, int c) const { return f_[i][c]; }
+    RSC_HD double ns(int i, int r, int s) const { return m.Ns[i][r][s]; }
+    RSC_HD double pwgt(int i, int e) const { return m.Pw[Cov::on ? i : 0][e]; }
+    RSC_HD double eig(int r, int c) const { return m.eigenRot[r][c]; }
+    RSC_HD bool planar() const { return m.planar; }
+};
+
 // Phase 3 of computePose (:480-623): pose recovery from the null vector r1 (the V column of the
 // smallest singular value of the normal matrix) and the Gauss-Newton refinement (mlpnp_gn,
 // :659-723).  slab: kMlSlabDoubles doubles (element stride slab.stride) for J and the LDLT system.
-template <int NS, class Cov>
-RSC_HD void mlpnp_finish_pose(const double (&pw)[NS][3], const double (&f)[NS][3], const MlPrep<NS, Cov>& m,
-                              const double (&r1)[12], const LaneMat& slab, double (&Rout)[3][3], double (&tout)[3]) {
-    const bool planar = m.planar;
-    const auto& eigenRot = m.eigenRot;
-    const auto& Ns = m.Ns;
-    const auto& Pw = m.Pw;
+template <int NS, class Cov, class View>
+RSC_HD void mlpnp_finish_pose(const View& in, const double (&r1)[12], const LaneMat& slab, double (&Rout)[3][3],
+                              double (&tout)[3]) {
+    const bool planar = in.planar();
     double R[3][3], t[3];
     if (planar) {
         double tmp[3][3] = {{0.0, r1[0], r1[1]}, {0.0, r1[2], r1[3]}, {0.0, r1[4], r1[5]}};
@@ -691,7 +704,7 @@ RSC_HD void mlpnp_finish_pose(const double (&pw)[NS][3], const double (&f)[NS][3
         double R2[3][3];
         RSC_UNROLL for (int r = 0; r < 3; ++r)
             RSC_UNROLL for (int c = 0; c < 3; ++c)
-                R2[r][c] = eigenRot[0][r] * R1[0][c] + eigenRot[1][r] * R1[1][c] + eigenRot[2][r] * R1[2][c];
+                R2[r][c] = in.eig(0, r) * R1[0][c] + in.eig(1, r) * R1[1][c] + in.eig(2, r) * R1[2][c];
         const double tv[3] = {scale * r1[6], scale * r1[7], scale * r1[8]};
         double Ro[3][3];
         RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) Ro[r][c] = -R2[c][r];
@@ -709,10 +722,10 @@ RSC_HD void mlpnp_finish_pose(const double (&pw)[NS][3], const double (&f)[NS][3
             RSC_UNROLL for (int p = 0; p < 6; ++p) {
                 double v[3];
                 RSC_UNROLL for (int r = 0; r < 3; ++r)
-                    v[r] = (Rc[r][0] * pw[p][0] + Rc[r][1] * pw[p][1] + Rc[r][2] * pw[p][2]) + Tc[r];
+                    v[r] = (Rc[r][0] * in.pw(p, 0) + Rc[r][1] * in.pw(p, 1) + Rc[r][2] * in.pw(p, 2)) + Tc[r];
                 const double nv = ml_norm3(v);
                 RSC_UNROLL for (int r = 0; r < 3; ++r) v[r] = v[r] / nv;
-                norms += (1.0 - ml_dot3(v, f[p]));
+                { const double fp[3] = {in.f(p, 0), in.f(p, 1), in.f(p, 2)}; norms += (1.0 - ml_dot3(v, fp)); }
             }
             const bool take = (k == 0) || (norms < best_val);
             best_val = take ? norms : best_val;
@@ -742,10 +755,10 @@ RSC_HD void mlpnp_finish_pose(const double (&pw)[NS][3], const double (&f)[NS][3
             RSC_UNROLL for (int p = 0; p < 6; ++p) {
                 double v[3];
                 RSC_UNROLL for (int r = 0; r < 3; ++r)
-                    v[r] = (Ti[s][r][0] * pw[p][0] + Ti[s][r][1] * pw[p][1] + Ti[s][r][2] * pw[p][2]) + Ti[s][r][3];
+                    v[r] = (Ti[s][r][0] * in.pw(p, 0) + Ti[s][r][1] * in.pw(p, 1) + Ti[s][r][2] * in.pw(p, 2)) + Ti[s][r][3];
                 const double nv = ml_norm3(v);
                 RSC_UNROLL for (int r = 0; r < 3; ++r) v[r] = v[r] / nv;
-                err[s] += (1.0 - ml_dot3(v, f[p]));
+                { const double fp[3] = {in.f(p, 0), in.f(p, 1), in.f(p, 2)}; err[s] += (1.0 - ml_dot3(v, fp)); }
             }
         }
         const bool k0 = err[0] < err[1];
@@ -774,28 +787,33 @@ RSC_HD void mlpnp_finish_pose(const double (&pw)[NS][3], const double (&f)[NS][3
         RSC_UNROLL for (int i = 0; i < NS; ++i) {
             double pc[3];
             RSC_UNROLL for (int k = 0; k < 3; ++k)
-                pc[k] = (Rg[k][0] * pw[i][0] + Rg[k][1] * pw[i][1] + Rg[k][2] * pw[i][2]) + x[3 + k];
+                pc[k] = (Rg[k][0] * in.pw(i, 0) + Rg[k][1] * in.pw(i, 1) + Rg[k][2] * in.pw(i, 2)) + x[3 + k];
             const double nrm = ml_norm3(pc);
             RSC_UNROLL for (int k = 0; k < 3; ++k) pc[k] = pc[k] / nrm;
-            const double nr[3] = {Ns[i][0][0], Ns[i][1][0], Ns[i][2][0]};
-            const double ns[3] = {Ns[i][0][1], Ns[i][1][1], Ns[i][2][1]};
+            const double nr[3] = {in.ns(i, 0, 0), in.ns(i, 1, 0), in.ns(i, 2, 0)};
+            const double ns[3] = {in.ns(i, 0, 1), in.ns(i, 1, 1), in.ns(i, 2, 1)};
             rr[2 * i] = ml_dot3(nr, pc);
             rr[2 * i + 1] = ml_dot3(ns, pc);
             double J[2][6];
-            ml_jac(pw[i], nr, ns, x, x + 3, J);
+            const double pwi[3] = {in.pw(i, 0), in.pw(i, 1), in.pw(i, 2)};
+            ml_jac(pwi, nr, ns, x, x + 3, J);
             RSC_UNROLL for (int k = 0; k < 6; ++k) {
                 Jv.e((2 * i) * 6 + k) = J[0][k];
                 Jv.e((2 * i + 1) * 6 + k) = J[1][k];
             }
         }
-        double g[6];
-        if constexpr (Cov::on) {
-            // JacTSKll = J^T Kll: (k, 2i + q) = J(2i, k) P_i(0, q) + J(2i + 1, k) P_i(1, q)
-            RSC_UNROLL for (int a = 0; a < 6; ++a) {
+        // J^T J (or J^T Kll J) and J^T r one row a at a time: a rolled loop keeps J in the slab instead
+        // of 2 NS x 6 doubles of registers; g[a] waits in the J region's spare rows (e >= 2 NS * 6)
+        constexpr int kG = 120;
+        static_assert(2 * NS * 6 <= kG, "g rows after J");
+#pragma unroll 1
+        for (int a = 0; a < 6; ++a) {
+            if constexpr (Cov::on) {
+                // JacTSKll = J^T Kll: (k, 2i + q) = J(2i, k) P_i(0, q) + J(2i + 1, k) P_i(1, q)
                 double jk[2 * NS];
                 RSC_UNROLL for (int i = 0; i < NS; ++i)
                     RSC_UNROLL for (int q = 0; q < 2; ++q)
-                        jk[2 * i + q] = Jv.e((2 * i) * 6 + a) * Pw[i][q] + Jv.e((2 * i + 1) * 6 + a) * Pw[i][2 + q];
+                        jk[2 * i + q] = Jv.e((2 * i) * 6 + a) * in.pwgt(i, q) + Jv.e((2 * i + 1) * 6 + a) * in.pwgt(i, 2 + q);
                 RSC_UNROLL for (int b = 0; b < 6; ++b) {
                     double s = jk[0] * Jv.e(b);
                     RSC_UNROLL for (int q = 1; q < 2 * NS; ++q) s = s + jk[q] * Jv.e(q * 6 + b);
@@ -803,10 +821,8 @@ RSC_HD void mlpnp_finish_pose(const double (&pw)[NS][3], const double (&f)[NS][3
                 }
                 double s = jk[0] * rr[0];
                 RSC_UNROLL for (int q = 1; q < 2 * NS; ++q) s = s + jk[q] * rr[q];
-                g[a] = s;
-            }
-        } else {
-            RSC_UNROLL for (int a = 0; a < 6; ++a) {
+                Jv.e(kG + a) = s;
+            } else {
                 RSC_UNROLL for (int b = 0; b < 6; ++b) {
                     double s = Jv.e(a) * Jv.e(b);
                     RSC_UNROLL for (int q = 1; q < 2 * NS; ++q) s = s + Jv.e(q * 6 + a) * Jv.e(q * 6 + b);
@@ -814,9 +830,11 @@ RSC_HD void mlpnp_finish_pose(const double (&pw)[NS][3], const double (&f)[NS][3
                 }
                 double s = Jv.e(a) * rr[0];
                 RSC_UNROLL for (int q = 1; q < 2 * NS; ++q) s = s + Jv.e(q * 6 + a) * rr[q];
-                g[a] = s;
+                Jv.e(kG + a) = s;
             }
         }
+        double g[6];
+        RSC_UNROLL for (int a = 0; a < 6; ++a) g[a] = Jv.e(kG + a);
         double dx[6];
         ml_ldlt_solve6(Av, g, dx);
         double mx = rabs(dx[0]), mn = rabs(dx[0]);
@@ -873,7 +891,7 @@ RSC_HD void mlpnp_compute_pose(const double (&pw)[NS][3], const double (&f)[NS][
         }
     double r1[12];
     ml_jacobi_svd_lds(W, V, colsA, r1);
-    mlpnp_finish_pose<NS, Cov>(pw, f, m, r1, slab, Rout, tout);
+    mlpnp_finish_pose<NS, Cov>(MlRegs<NS, Cov>{pw, f, m}, r1, slab, Rout, tout);
 }
 
 // MLPnPsolver::CheckInliers for one correspondence (MLPnPsolver.cpp:222-255).

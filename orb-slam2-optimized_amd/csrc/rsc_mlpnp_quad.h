@@ -209,7 +209,7 @@ __device__ __forceinline__ void ml_quad_jacobi_svd(double (&Wc)[3][12], double (
     }
 }
 
-// Park / restore the phase-1 state (and the hypothesis' points and bearings) in the hypothesis' LDS
+// Park the phase-1 state (and the hypothesis' points and bearings) in the hypothesis' LDS
 // region while the SVD holds W and V in VGPRs.  All four lanes write the same values.
 template <int NS, class Cov>
 __device__ __forceinline__ void ml_park(double* st, const double (&pw)[NS][3], const double (&f)[NS][3],
@@ -223,18 +223,20 @@ __device__ __forceinline__ void ml_park(double* st, const double (&pw)[NS][3], c
     RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) st[k++] = m.eigenRot[r][c];
     st[k++] = m.planar ? 1.0 : 0.0;
 }
-template <int NS, class Cov>
-__device__ __forceinline__ void ml_unpark(const double* st, double (&pw)[NS][3], double (&f)[NS][3], MlPrep<NS, Cov>& m) {
-    int k = 0;
-    RSC_UNROLL for (int i = 0; i < NS; ++i) RSC_UNROLL for (int c = 0; c < 3; ++c) pw[i][c] = st[k++];
-    RSC_UNROLL for (int i = 0; i < NS; ++i) RSC_UNROLL for (int c = 0; c < 3; ++c) f[i][c] = st[k++];
-    RSC_UNROLL for (int i = 0; i < NS; ++i) RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int s = 0; s < 2; ++s)
-        m.Ns[i][r][s] = st[k++];
-    if constexpr (Cov::on) RSC_UNROLL for (int i = 0; i < NS; ++i) RSC_UNROLL for (int e = 0; e < 4; ++e) m.Pw[i][e] = st[k++];
-    RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) m.eigenRot[r][c] = st[k++];
-    m.planar = st[k++] != 0.0;
-}
 static_assert(kMlQuadRegion - kMlQuadGN >= 8 * 6 + 8 * 6 + 8 * 4 + 9 + 1, "parked state fits the region");
+
+// The parked state (ml_park layout) read in place by mlpnp_finish_pose.
+template <int NS, class Cov>
+struct MlParked {
+    const double* st;
+    static constexpr int kF = 3 * NS, kNs = 6 * NS, kPw = 12 * NS, kEig = 12 * NS + (Cov::on ? 4 * NS : 0);
+    __device__ double pw(int i, int c) const { return st[3 * i + c]; }
+    __device__ double f(int i, int c) const { return st[kF + 3 * i + c]; }
+    __device__ double ns(int i, int r, int s) const { return st[kNs + 6 * i + 2 * r + s]; }
+    __device__ double pwgt(int i, int e) const { return st[kPw + 4 * i + e]; }
+    __device__ double eig(int r, int c) const { return st[kEig + 3 * r + c]; }
+    __device__ bool planar() const { return st[kEig + 9] != 0.0; }
+};
 
 // One MLPnP hypothesis per quad: sample, computePose (MLPnPsolver.cpp:321-623), pose record.
 template <int NS, class Cov>
@@ -287,10 +289,7 @@ __device__ __forceinline__ void mlpnp_quad_hypothesis(const DevML& P, const int 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double pw[NS][3], f[NS][3];
-    MlPrep<NS, Cov> m;
-    ml_unpark<NS, Cov>(stash, pw, f, m);
-    mlpnp_finish_pose<NS, Cov>(pw, f, m, r1, LaneMat{region, 1}, Rout, tout);
+    mlpnp_finish_pose<NS, Cov>(MlParked<NS, Cov>{stash}, r1, LaneMat{region, 1}, Rout, tout);
 }
 
 }  // namespace rsc
