@@ -1,4 +1,4 @@
-// poseopt.hip — Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) kernel: one 512-thread
+// poseopt.hip — Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) kernel: one 256-thread
 // workgroup per Frame.  See rsc_poseopt.h for the mapping and the arithmetic contract.
 //
 // Where the time goes: every g2o reduction is a sequential sum over the edges, and only its
@@ -21,11 +21,17 @@ namespace rsc {
 
 namespace {
 
-constexpr int kPoseChunk = 512;                 // edges per build chunk = threads per workgroup
+// Edges per build chunk = threads per workgroup.  256 (one wave per SIMD of a CU): the per-thread
+// LM control state and an edge's 27 H/b terms fit the 512-VGPR budget of a 4-wave workgroup without
+// scratch (512 threads capped a wave at 256 VGPRs and spilled 35 of them, round 2).
+#ifndef RSC_POSE_CHUNK
+#define RSC_POSE_CHUNK 256
+#endif
+constexpr int kPoseChunk = RSC_POSE_CHUNK;
 constexpr int kPoseCol = kPoseChunk + 2;        // padded column stride (doubles): 16 B bank shift per column
 constexpr int kPoseCols = kPoseTerms + 1;       // 27 H/b columns + the chi2 column
-constexpr int kPoseTermDoubles = kPoseCols * kPoseCol;
-static_assert(kPoseTermDoubles >= kPoseMaxEdges, "chi2 terms of a whole pass must fit the term buffer");
+// term buffer: the build pass's columns, or the chi2 terms of a whole pass (n <= kPoseMaxEdges)
+constexpr int kPoseTermDoubles = (kPoseCols * kPoseCol > kPoseMaxEdges) ? kPoseCols * kPoseCol : kPoseMaxEdges;
 constexpr size_t kPoseLds = sizeof(double) * kPoseTermDoubles + kPoseMaxEdges;
 
 struct PoseLds {

@@ -3,7 +3,7 @@
 // EdgeStereoSE3ProjectXYZOnlyPose (stereo) edges with Huber kernels (delta sqrt(5.991) / sqrt(7.815)),
 // 4 rounds of 10 iterations with inlier/outlier re-classification (chi2 > 5.991 / 7.815).
 //
-// Mapping: one 512-thread workgroup per Frame (problem).  Threads own edges e = tid + 512 k and
+// Mapping: one 256-thread workgroup per Frame (problem).  Threads own edges e = tid + 256 k and
 // evaluate the per-edge work of a pass in parallel (error, robust chi2 term, Jacobian and its 27
 // Hessian/gradient terms); the reductions g2o performs as sequential loops over the active edges
 // (activeRobustChi2, buildSystem's H += J^T W J, b -= ...) are folded in edge order on one lane
