@@ -54,7 +54,8 @@ __global__ __launch_bounds__(256) void kfdb_count_kernel(DevKFDB db, KfdbQuery q
         c += __shfl_xor(c, off);
         first = min(first, __shfl_xor(first, off));
     }
-    if (lane != 0 || c == 0) return;
+    if (c == 0) return;
+    // the walk's state rules (every lane: the inputs are wave-uniform)
     unsigned long long qb = qb0;
     int w = w0;
     bool in_list = false;
@@ -69,12 +70,54 @@ __global__ __launch_bounds__(256) void kfdb_count_kernel(DevKFDB db, KfdbQuery q
     } else {
         w += c;  // already met by an earlier query with the same id: counts accumulate, not listed
     }
-    db.query[t][slot] = qb;
-    db.words[t][slot] = w;
-    if (in_list) {
-        db.list[slot] = 1;
-        db.key[slot] = ((unsigned long long)first << 32) | db.seq[slot];
+    if (lane == 0) {
+        db.query[t][slot] = qb;
+        db.words[t][slot] = w;
+        if (in_list) {
+            db.list[slot] = 1;
+            db.key[slot] = ((unsigned long long)first << 32) | db.seq[slot];
+        }
     }
+    if (!in_list) return;
+    // L1Scoring::score(F->mBowVec, pKFi->mBowVec) (ScoringObject.cpp:23-67): per-word terms in
+    // parallel, the sum in ascending word order on the wave's scalar path; finish keeps it only if
+    // the slot is scored (mLoopScore / mRelocScore are written there)
+    const double* vals = db.vals + (size_t)slot * db.max_words;
+    double score = 0;
+    for (int base = 0; base < len; base += 64 * kBatch) {
+        uint32_t wd[kBatch];
+        double wv[kBatch], vv[kBatch];
+        int p[kBatch];
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) {
+            const int j = min(base + b * 64 + lane, db.max_words - 1);
+            wd[b] = ids[j];
+            wv[b] = vals[j];
+        }
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) p[b] = db.wpos[base + b * 64 + lane < len ? wd[b] : 0u];
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) p[b] = base + b * 64 + lane < len ? p[b] : -1;
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) vv[b] = db.qvals[max(p[b], 0)];
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) {
+            const double vi = vv[b], wi = wv[b];
+            const double term = fabs(vi - wi) - fabs(vi) - fabs(wi);
+            const long long tb = __double_as_longlong(term);
+            const int lo = (int)(tb & 0xffffffff), hi = (int)(tb >> 32);
+            unsigned long long m = __ballot(p[b] >= 0);
+            while (m) {  // ascending word order: batch b, then lane (uniform lane index)
+                const int src = __builtin_amdgcn_readfirstlane(__ffsll((long long)m) - 1);
+                const unsigned long long v = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(hi, src) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readlane(lo, src);
+                score += __longlong_as_double((long long)v);
+                m &= m - 1;
+            }
+        }
+    }
+    score = -score / 2.0;
+    if (lane == 0) db.tscore[slot] = (float)score;  // float si = mpVoc->score(...)
 }
 
 template <typename T, typename Op>
@@ -92,8 +135,8 @@ __device__ T block_reduce(T v, T* s_red, Op op) {
 // The rest of the query in one workgroup (16 waves), phases separated by barriers:
 //   select:     maxCommonWords / minCommonWords (:86-93, :201-207) and the scored slots in
 //               lKFsSharingWords order (rank by the walk's first meeting);
-//   score:      L1Scoring::score(F->mBowVec, pKFi->mBowVec) (ScoringObject.cpp:23-67), one wave per
-//               scored slot: per-word terms in parallel, the sum in ascending word order;
+//   scores:     the scored slots' L1 scores from the count kernel (ScoringObject.cpp:23-67), stored
+//               as mLoopScore / mRelocScore;
 //   accumulate: covisibility accumulation (:118-147, :233-259), retain (> 0.75 * best) and
 //               first-occurrence de-duplication (:150-168, :262-279);
 //   and the word-position table is cleared for the next query.
@@ -169,53 +212,12 @@ __global__ __launch_bounds__(1024) void kfdb_finish_kernel(DevKFDB db, KfdbQuery
         }
     }
     __syncthreads();
-    // ---- score ----
-    for (int e = wave; e < S; e += nw) {
+    // ---- scores (computed by the count kernel for every listed slot) ----
+    for (int e = threadIdx.x; e < S; e += blockDim.x) {
         const int kf = scored[e];
-        const int len = db.len[kf];
-        const uint32_t* ids = db.ids + (size_t)kf * db.max_words;
-        const double* vals = db.vals + (size_t)kf * db.max_words;
-        double score = 0;
-        // the first window is loaded with the length (the slot stride bounds it), not after it
-        for (int base = 0; base == 0 || base < len; base += 64 * kBatch) {
-            uint32_t w[kBatch];
-            double wv[kBatch], vv[kBatch];
-            int p[kBatch];
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b) {
-                const int j = min(base + b * 64 + lane, db.max_words - 1);
-                w[b] = ids[j];
-                wv[b] = vals[j];
-            }
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b)
-                p[b] = db.wpos[base + b * 64 + lane < len ? w[b] : 0u];
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b) p[b] = base + b * 64 + lane < len ? p[b] : -1;
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b) vv[b] = db.qvals[max(p[b], 0)];
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b) {
-                const double vi = vv[b], wi = wv[b];
-                const double term = fabs(vi - wi) - fabs(vi) - fabs(wi);
-                const long long tb = __double_as_longlong(term);
-                const int lo = (int)(tb & 0xffffffff), hi = (int)(tb >> 32);
-                unsigned long long m = __ballot(p[b] >= 0);
-                while (m) {  // ascending word order: batch b, then lane (uniform lane index)
-                    const int src = __builtin_amdgcn_readfirstlane(__ffsll((long long)m) - 1);
-                    const unsigned long long v = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(hi, src) << 32) |
-                                                 (uint32_t)__builtin_amdgcn_readlane(lo, src);
-                    score += __longlong_as_double((long long)v);
-                    m &= m - 1;
-                }
-            }
-        }
-        score = -score / 2.0;
-        const float si = (float)score;  // float si = mpVoc->score(...)
-        if (lane == 0) {
-            sc[e] = si;
-            db.score[t][kf] = si;  // mLoopScore / mRelocScore
-        }
+        const float si = db.tscore[kf];
+        sc[e] = si;
+        db.score[t][kf] = si;  // mLoopScore / mRelocScore
     }
     __syncthreads();
     // ---- accumulate ----

@@ -1959,7 +1959,7 @@ struct rsc_kfdb {
     DevBuf<char> qbuf;  // the query BowVector: ids | vals (8-aligned), one upload per query
     DevBuf<int32_t> wpos, len, covis, covis_n, words, list, scored, best, tmp, counters, out;
     DevBuf<unsigned long long> query, key;
-    DevBuf<float> score, sc, acc;
+    DevBuf<float> score, sc, acc, tscore;
     DevBuf<uint8_t> conn;
     PinBuf<char> stage;  // query upload | candidates download
     void touch(int s) { hw = std::max(hw, s + 1); }
@@ -1980,6 +1980,7 @@ struct rsc_kfdb {
             d.words[t] = words.p + (size_t)t * cap;
             d.score[t] = score.p + (size_t)t * cap;
         }
+        d.tscore = tscore.p;
         d.list = list.p;
         d.key = key.p;
         d.scored = scored.p;
@@ -2027,7 +2028,7 @@ int rsc_kfdb_create(rsc_context* C, uint32_t vocab_words, int capacity, int max_
         (e = db->seq.ensure(K)) || (e = db->covis.ensure(K * kKfdbCovis)) || (e = db->covis_n.ensure(K)) ||
         (e = db->query.ensure(2 * K)) || (e = db->words.ensure(2 * K)) || (e = db->score.ensure(2 * K)) ||
         (e = db->list.ensure(K)) || (e = db->key.ensure(K)) || (e = db->scored.ensure(K)) || (e = db->sc.ensure(K)) ||
-        (e = db->acc.ensure(K)) || (e = db->best.ensure(K)) || (e = db->tmp.ensure(K)) || (e = db->counters.ensure(4)) ||
+        (e = db->acc.ensure(K)) || (e = db->tscore.ensure(K)) || (e = db->best.ensure(K)) || (e = db->tmp.ensure(K)) || (e = db->counters.ensure(4)) ||
         (e = db->out.ensure(K + 1)) || (e = db->qbuf.ensure(16 * (size_t)max_words + 16)) ||
         (e = db->conn.ensure(K)))
         return e;

@@ -9,12 +9,14 @@
 //   scatter:    the query's word -> position table (a vocabulary-sized int array, -1 elsewhere).
 //   count:      one wave per slot — one table gather per slot word gives the common-word count
 //               (the number of times the reference's inverted-file walk meets the slot) and the
-//               first query word it meets (the list position); the lane-0 state update reproduces
-//               the walk's per-occurrence rules exactly.
+//               first query word it meets (the list position); the state update reproduces the
+//               walk's per-occurrence rules exactly; a slot that enters lKFsSharingWords also gets
+//               its DBoW2 L1 score here (terms in parallel, summed in ascending word order through
+//               the wave's shuffles), while its words are in cache and off the finish kernel's
+//               single-workgroup critical path (kept only for the slots finish scores).
 //   finish:     one workgroup — maxCommonWords, minCommonWords = int(max * 0.8f), the scored slots
-//               in lKFsSharingWords order (rank by (first query word, seq)); DBoW2 L1 scores (one
-//               wave per scored slot, terms in parallel, summed in ascending word order through
-//               the wave's shuffles); covisibility accumulation, 0.75 * best retain,
+//               in lKFsSharingWords order (rank by (first query word, seq)) and their scores;
+//               covisibility accumulation, 0.75 * best retain,
 //               first-occurrence de-duplication; candidates in the reference's vector order; the
 //               table is cleared for the next query.
 // Integer/latency-bound work (a few bytes per BowVector entry, no MFMA); the HBM stream is the
@@ -43,6 +45,7 @@ struct DevKFDB {
     int32_t* words[2];
     float* score[2];
     // per-query scratch
+    float* tscore;           // [cap] L1 score of every listed slot (count kernel), kept for the scored ones
     int32_t* list;           // [cap] 1 = in lKFsSharingWords this query
     unsigned long long* key; // [cap] (first query word << 32) | seq
     int32_t* scored;         // [cap] scored slots in list order
