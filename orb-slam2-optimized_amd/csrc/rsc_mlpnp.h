@@ -802,12 +802,12 @@ RSC_HD void mlpnp_finish_pose(const View& in, const double (&r1)[12], const Lane
                 Jv.e((2 * i + 1) * 6 + k) = J[1][k];
             }
         }
-        // J^T J (or J^T Kll J) and J^T r one row a at a time: a rolled loop keeps J in the slab instead
-        // of 2 NS x 6 doubles of registers; g[a] waits in the J region's spare rows (e >= 2 NS * 6)
+        // J^T J (or J^T Kll J) and J^T r one row a at a time; where registers are short (covariances,
+        // NS > 6) the row loop stays rolled, so J stays in the slab instead of 2 NS x 6 doubles of
+        // VGPRs; g[a] waits in the J region's spare rows (e >= 2 NS * 6)
         constexpr int kG = 120;
         static_assert(2 * NS * 6 <= kG, "g rows after J");
-#pragma unroll 1
-        for (int a = 0; a < 6; ++a) {
+        auto row = [&](int a) {
             if constexpr (Cov::on) {
                 // JacTSKll = J^T Kll: (k, 2i + q) = J(2i, k) P_i(0, q) + J(2i + 1, k) P_i(1, q)
                 double jk[2 * NS];
@@ -832,6 +832,12 @@ RSC_HD void mlpnp_finish_pose(const View& in, const double (&r1)[12], const Lane
                 RSC_UNROLL for (int q = 1; q < 2 * NS; ++q) s = s + Jv.e(q * 6 + a) * rr[q];
                 Jv.e(kG + a) = s;
             }
+        };
+        if constexpr (Cov::on || NS > 6) {
+#pragma unroll 1
+            for (int a = 0; a < 6; ++a) row(a);
+        } else {
+            RSC_UNROLL for (int a = 0; a < 6; ++a) row(a);
         }
         double g[6];
         RSC_UNROLL for (int a = 0; a < 6; ++a) g[a] = Jv.e(kG + a);
