@@ -35,16 +35,43 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec)
-PROFILE_DIR = "profiles/r02"
+FP32_PEAK_TFLOPS = 157.3   # MI355X vector FP32 (spec)
+PROFILE_DIRS = ("profiles/r03", "profiles/r02")  # newest first
 
 
 def _profile_json(name):
-    """Committed measurement side files (op-count, PMC traffic) of this round, or None."""
-    path = os.path.join(ROOT, PROFILE_DIR, name)
-    if not os.path.exists(path):
+    """Committed measurement side file (op counts, PMC traffic), from the newest round that has it;
+    returns (data, relative path) or (None, None)."""
+    for d in PROFILE_DIRS:
+        path = os.path.join(ROOT, d, name)
+        if os.path.exists(path):
+            with open(path) as f:
+                return json.load(f), os.path.join(d, name)
+    return None, None
+
+
+def op_count(key):
+    """FP64 flops per unit of section `key` from tools/opcount_report.py's opcount.json (None if absent)."""
+    opc, _ = _profile_json("opcount.json")
+    if not opc:
         return None
-    with open(path) as f:
-        return json.load(f)
+    if key in opc and isinstance(opc[key], dict):
+        return opc[key].get("fp64_flops_mean")
+    return opc.get("fp64_flops_mean") if key == "pnp" else None
+
+
+def fp64_roofline(kernel, units, flops_per_unit, ms, unit_desc):
+    """Roofline object of an FP64-latency-bound solver kernel: algorithmic flops (op-counter build
+    of the oracle) per launch / the kernel's HIP-event time, against the FP64 vector peak."""
+    if not flops_per_unit or not ms:
+        return None
+    tf = units * flops_per_unit / (ms * 1e-3) / 1e12
+    _, src = _profile_json("opcount.json")
+    return {"bound": "fp64-latency", "achieved": round(tf, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP64_PEAK_TFLOPS, 5), "traffic": None, "kernel": kernel,
+            "algorithmic_flops_per_launch": round(units * flops_per_unit), "flops_per_unit": flops_per_unit,
+            "unit_of_work": unit_desc, "kernel_ms_per_launch": round(ms, 4),
+            "sources": {"flops_per_unit": f"{src} (tools/opcount_report.py)", "time": "HIP events, second pass"}}
 
 
 def parse():
@@ -331,13 +358,16 @@ def run_sharded(engine, ctx, batch, lo, hi, total, params, args, dist, world, st
     ids = list(range(lo, hi))
     state = {"records": None}
 
+    def local(s):
+        batch.reset(wl.step_seeds(s, total)[lo:hi])
+        batch.set_ransac_parameters(*params)
+        return batch.iterate_raw(args.iters)
+
     def step(s):
         h = 0
         rec = np.zeros((0, rdist.RECORD), np.float32)
         if batch is not None:
-            batch.reset(wl.step_seeds(s, total)[lo:hi])
-            batch.set_ransac_parameters(*params)
-            outs = batch.iterate_raw(args.iters)
+            outs = local(s)
             h = int(outs["iterations"].sum())
             if gather is not None:
                 rec = pack(ids, outs)
@@ -358,8 +388,23 @@ def run_sharded(engine, ctx, batch, lo, hi, total, params, args, dist, world, st
     barrier(dist)
     dt = time.perf_counter() - t0
     dt, h = reduce_time_and_count(dist, dt, h)
-    return dict(hyp_per_s=h / dt, ms_per_step=1e3 * dt / steps, hypotheses_per_step=h // steps,
-                steps=steps), state["records"]
+    # second pass (this rank's launches only, not the metric): HIP events around the solve and scan
+    # kernels on the context stream
+    kt = dict(solve_ms=0.0, scan_ms=0.0, launches=0, hyps=0)
+    if batch is not None:
+        ctx.enable_timing(True)
+        for s in range(steps):
+            local(args.warmup + steps + s)
+            tm = ctx.last_timing()
+            kt["solve_ms"] += tm["solve_ms"]
+            kt["scan_ms"] += tm["scan_ms"]
+            kt["launches"] += tm["solve_launches"]
+            kt["hyps"] += tm["hypotheses"]
+        ctx.enable_timing(False)
+    n = max(kt["launches"], 1)
+    return dict(hyp_per_s=h / dt, ms_per_step=1e3 * dt / steps, hypotheses_per_step=h // steps, steps=steps,
+                kernel_ms_per_launch={"solve": round(kt["solve_ms"] / n, 4), "scan": round(kt["scan_ms"] / n, 4)},
+                hypotheses_per_launch=kt["hyps"] // n), state["records"]
 
 
 def run_sim3(engine, ctx, pairs, args, dist=None, rank=0, world=1):
@@ -375,6 +420,19 @@ def run_sim3(engine, ctx, pairs, args, dist=None, rank=0, world=1):
     r, rec = run_sharded(engine, ctx, batch, lo, hi, C, wl.LOOP, args, dist, world, args.steps, rdist.pack_sim3)
     r.update(pairs=C, pairs_per_rank=hi - lo, correspondences=pairs[0].n1,
              sharding=f"{world} rank(s), contiguous blocks by N, RCCL all-gather of {rdist.RECORD}-float records")
+    # config 3 is scan-bound (Horn on 3 points is tiny): FP32 VALU roofline of the scan kernel with
+    # SURVEY §8(d)'s F_h = 62 N flops and B_h = 48 N bytes per hypothesis
+    scan_ms = r["kernel_ms_per_launch"]["scan"]
+    hl = r["hypotheses_per_launch"]
+    nc = float(np.mean([p.n1 for p in pairs[lo:hi]])) if hi > lo else 0.0
+    if scan_ms and hl:
+        tf = hl * 62 * nc / (scan_ms * 1e-3) / 1e12
+        r["roofline"] = {"bound": "valu-fp32", "achieved": round(tf, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tf / FP32_PEAK_TFLOPS, 5), "traffic": None,
+                         "kernel": f"sim3_scan_kernel ({hl} hypotheses x {nc:.0f} correspondences per launch)",
+                         "algorithmic_flops_per_launch": round(hl * 62 * nc),
+                         "effective_scan_bw_frac": round(hl * 48 * nc / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                         "sources": {"per_unit": "SURVEY.md §8(d): F_h = 62 N, B_h = 48 N", "time": "HIP events"}}
     return r, solvers, rec
 
 
@@ -435,6 +493,11 @@ def run_mlpnp(engine, ctx, scenes, args, with_cov=False, dist=None, rank=0, worl
                          rdist.pack_pnp)
     r.update(candidates=C, candidates_per_rank=hi - lo, correspondences=scenes[0].n,
              sharding=f"{world} rank(s), contiguous blocks by N, RCCL all-gather of {rdist.RECORD}-float records")
+    roof = fp64_roofline("mlpnp_quad_kernel<6>" + ("<MlIndexedCov>" if with_cov else ""), r["hypotheses_per_launch"],
+                         op_count("mlpnp"), r["kernel_ms_per_launch"]["solve"],
+                         "MLPnP computePose on a 6-point sample")
+    if roof:
+        r["roofline"] = roof
     return r, rec
 
 
@@ -710,9 +773,15 @@ def run_poseopt(engine, ctx, frames, args):
     its = sum(r["lm_iterations"] for r in res)
     trials = sum(r["lm_trials"] for r in res)
     F = len(frames)
-    return dict(poses_per_s=F * steps / dt, ms_per_step=1e3 * dt / steps, kernel_ms=kms / steps, frames=F,
-                edges_per_frame=frames[0].n, lm_iterations_per_frame=its / F, lm_trials_per_frame=trials / F,
-                steps=steps)
+    out = dict(poses_per_s=F * steps / dt, ms_per_step=1e3 * dt / steps, kernel_ms=kms / steps, frames=F,
+               edges_per_frame=frames[0].n, lm_iterations_per_frame=its / F, lm_trials_per_frame=trials / F,
+               steps=steps)
+    stereo = any((getattr(f, "u_right", None) is not None and (np.asarray(f.u_right) >= 0).any()) for f in frames)
+    roof = fp64_roofline("poseopt_kernel", F, op_count("poseopt" if stereo else "poseopt_mono"), kms / steps,
+                         "one PoseOptimization call (one Frame)")
+    if roof:
+        out["roofline"] = roof
+    return out
 
 
 def bow_views(rng, C=64, N=2000):
@@ -876,10 +945,15 @@ def run_sim3opt(engine, ctx, probs, args):
         kms += ctx.last_timing()["refine_ms"]
     ctx.enable_timing(False)
     C = len(probs)
-    return dict(pairs_per_s=C * steps / dt, ms_per_step=1e3 * dt / steps, kernel_ms=kms / steps, pairs=C,
-                correspondences_per_pair=float(np.mean([r["n_correspondences"] for r in res])),
-                mean_inliers=float(np.mean([r["n_inliers"] for r in res])),
-                lm_iterations_per_pair=float(np.mean([r["lm_iterations"] for r in res])), steps=steps)
+    out = dict(pairs_per_s=C * steps / dt, ms_per_step=1e3 * dt / steps, kernel_ms=kms / steps, pairs=C,
+               correspondences_per_pair=float(np.mean([r["n_correspondences"] for r in res])),
+               mean_inliers=float(np.mean([r["n_inliers"] for r in res])),
+               lm_iterations_per_pair=float(np.mean([r["lm_iterations"] for r in res])), steps=steps)
+    roof = fp64_roofline("sim3opt_kernel", C, op_count("optimize_sim3"), kms / steps,
+                         "one OptimizeSim3 call (one KeyFrame pair)")
+    if roof:
+        out["roofline"] = roof
+    return out
 
 
 def cpu_baseline_sim3opt(probs):
@@ -1025,9 +1099,9 @@ def headline_roofline(args, r):
     set_ms = solve_ms + scan_ms
     B_h = 24 * args.corrs  # PnP scan bytes per hypothesis (p3D 12 + p2D 8 + maxErr 4)
     scan_bytes = per_launch_hyps * B_h
-    opc = _profile_json("opcount.json")
-    traffic = _profile_json("pmc_traffic.json")
-    S_h = opc["fp64_flops_mean"] if opc else None
+    _, opc_src = _profile_json("opcount.json")
+    traffic, traffic_src = _profile_json("pmc_traffic.json")
+    S_h = op_count("pnp")
     tf = per_launch_hyps * S_h / (solve_ms * 1e-3) / 1e12 if (S_h and solve_ms > 0) else None
     meas = traffic["epnp_launch_set_bytes"] if traffic else None
     roof = {"bound": "fp64-latency",
@@ -1049,8 +1123,8 @@ def headline_roofline(args, r):
             "scan_algorithmic_bytes_per_launch": scan_bytes,
             "timing": "HIP events on the context stream, second pass of the same K steps "
                       f"({1e3 * r['seconds_instrumented'] / args.steps:.4f} ms/step with events)",
-            "sources": {"S_h": PROFILE_DIR + "/opcount.json (tools/opcount.cpp)",
-                        "traffic": (PROFILE_DIR + "/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE, commit "
+            "sources": {"S_h": f"{opc_src} (tools/opcount_report.py)",
+                        "traffic": (f"{traffic_src} (2 x FETCH_SIZE + WRITE_SIZE, commit "
                                     f"{traffic.get('commit')})") if traffic else None}}
     return roof
 

@@ -553,7 +553,7 @@ int pose_optimization(const PoseOptInput& in, float Tcw_out[16], uint8_t* outlie
             if (outlier[e.slot]) compute_error(e, est, P.K);
             // the mono loop then the stereo loop (Optimizer.cpp:347-398): per-edge decisions only,
             // nBad is their total, so one pass in edge order is equivalent
-            const float c2 = chi2(e);
+            const float c2 = (float)chi2(e);  // float chi2 = e->chi2()
             if (c2 > (e.stereo ? chi2Stereo[it] : chi2Mono[it])) {
                 outlier[e.slot] = 1;
                 e.level = 1;

@@ -1,0 +1,23 @@
+// opcount_libm.h — the oracle's transcendental calls on the counting scalar (one flop per call).
+#pragma once
+#include "opcount_scalar.h"
+#include "../orb-slam2-optimized_amd/csrc/rsc_math.h"
+#include "../oracle/ora_libm.h"
+
+namespace ora_libm {
+inline CntD sin(CntD x) { ++g_flops; return CntD(sin(x.v)); }
+inline CntD cos(CntD x) { ++g_flops; return CntD(cos(x.v)); }
+inline CntD acos(CntD x) { ++g_flops; return CntD(acos(x.v)); }
+inline CntD cbrt_pow(CntD x) { ++g_flops; return CntD(cbrt_pow(x.v)); }
+}  // namespace ora_libm
+namespace std {
+inline bool isfinite(CntD x) { return std::isfinite(x.v); }
+inline bool isnan(CntD x) { return std::isnan(x.v); }
+inline CntD exp(CntD x) { ++g_flops; return CntD(::exp(x.v)); }
+inline CntD sin(CntD x) { ++g_flops; return CntD(::sin(x.v)); }
+inline CntD cos(CntD x) { ++g_flops; return CntD(::cos(x.v)); }
+inline CntD acos(CntD x) { ++g_flops; return CntD(::acos(x.v)); }
+inline CntD fma(CntD a, CntD b, CntD c) { g_flops += 2; return CntD(::fma(a.v, b.v, c.v)); }
+inline CntD min(CntD a, double b) { return (b < a.v) ? CntD(b) : a; }  // std::min(a, b): b < a ? b : a
+inline CntD max(double a, CntD b) { return a < b.v ? b : CntD(a); }  // std::max(a, b): a < b ? b : a
+}  // namespace std

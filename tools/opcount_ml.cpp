@@ -1,35 +1,34 @@
-// opcount — FP64 operation counter build of the CPU restatement (SURVEY.md §8(d) "Solve FLOPs S_h":
-// "measure it by an op-counter build of the CPU restatement and report mean ± σ per config").
-//
-// The oracle's EPnP (oracle/pnp_oracle.cpp, test infrastructure) is compiled a second time with
-// `double` replaced by a counting scalar, then compute_pose() is run on the minimal 4-point samples
-// of a config-2 scene.  Counted: +, -, *, / (1 flop each), sqrt (1 flop, also counted apart),
-// comparisons are not flops.  Output: one JSON line {mean, std, min, max, sqrt, div, samples}.
-// Measurement tooling only; the product never links this.
-#include <algorithm>
-#include <cfloat>
-#include <cmath>
-#include <cstdint>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <limits>
+// opcount_ml — FP64 operation count of MLPnPsolver::computePose (SURVEY.md §8(d) "Solve FLOPs S_h"
+// for config 4): the oracle restatement (oracle/mlpnp_oracle.cpp) compiled with `double` replaced by
+// the counting scalar (opcount_scalar.h), computePose run on 6-point samples of a config-4 shaped
+// scene (4096 correspondences, 40 % inliers).  sin / cos / acos / cbrt count one flop per call.
+// Output: one JSON line.  Measurement tooling only.
 #include <random>
-#include <type_traits>
 #include <vector>
-
 #include "opcount_scalar.h"
+#include "../orb-slam2-optimized_amd/csrc/rsc_math.h"
+#include "../oracle/ora_libm.h"
+
+namespace ora_libm {
+inline CntD sin(CntD x) { ++g_flops; return CntD(sin(x.v)); }
+inline CntD cos(CntD x) { ++g_flops; return CntD(cos(x.v)); }
+inline CntD acos(CntD x) { ++g_flops; return CntD(acos(x.v)); }
+inline CntD cbrt_pow(CntD x) { ++g_flops; return CntD(cbrt_pow(x.v)); }
+}  // namespace ora_libm
+namespace std {
+inline bool isfinite(CntD x) { return std::isfinite(x.v); }
+inline bool isnan(CntD x) { return std::isnan(x.v); }
+}  // namespace std
 
 #define double CntD
-#include "../oracle/pnp_oracle.cpp"
+#include "../oracle/mlpnp_oracle.cpp"
 #undef double
 
 int main(int argc, char** argv) {
-    const int n = argc > 1 ? atoi(argv[1]) : 2000;
-    const int samples = argc > 2 ? atoi(argv[2]) : 20000;
-    // Config-2 shaped scene: frustum points at depth [0.5, 8] m, EuRoC intrinsics, 40% inliers.
+    const int n = argc > 1 ? atoi(argv[1]) : 4096;
+    const int samples = argc > 2 ? atoi(argv[2]) : 5000;
     const float fx = 435.2046959714599f, fy = 435.2046959714599f, cx = 367.4517211914062f, cy = 252.2008514404297f;
-    std::mt19937_64 g(2024);
+    std::mt19937_64 g(2025);
     std::uniform_real_distribution<double> U(0.0, 1.0);
     std::normal_distribution<double> G(0.0, 1.0);
     std::vector<float> p2d(2 * n), p3d(3 * n), s2(n, 1.f);
@@ -38,7 +37,6 @@ int main(int argc, char** argv) {
     for (int i = 0; i < n; ++i) {
         const double u = 752 * U(g), v = 480 * U(g), d = 0.5 + 7.5 * U(g);
         const double xc = (u - cx) / fx * d, yc = (v - cy) / fy * d, zc = d;
-        // Xw = R^T (Xc - t), R = rot_z(ang), t = (0.3, -0.2, 0.5)
         const double a = xc - 0.3, b = yc + 0.2, c = zc - 0.5;
         p3d[3 * i] = (float)(ca * a + sa * b);
         p3d[3 * i + 1] = (float)(-sa * a + ca * b);
@@ -48,13 +46,13 @@ int main(int argc, char** argv) {
         p2d[2 * i + 1] = (float)(inl ? v + G(g) : 480 * U(g));
         kp[i] = i;
     }
-    rsc_oracle::PnPOracle o(n, n, p2d.data(), p3d.data(), s2.data(), kp.data(), fx, fy, cx, cy, 1);
+    rsc_oracle::MLPnPOracle o(n, n, p2d.data(), p3d.data(), s2.data(), kp.data(), fx, fy, cx, cy, 1);
     std::vector<double> f(samples);
     uint64_t sq = 0, dv = 0;
     std::uniform_int_distribution<int> pick(0, n - 1);
     for (int s = 0; s < samples; ++s) {
-        int idx[4];
-        for (int k = 0; k < 4; ++k) {
+        int idx[6];
+        for (int k = 0; k < 6; ++k) {
             bool dup;
             do {
                 idx[k] = pick(g);
@@ -62,9 +60,9 @@ int main(int argc, char** argv) {
                 for (int j = 0; j < k; ++j) dup |= idx[j] == idx[k];
             } while (dup);
         }
-        float R[9], t[3];
+        CntD R[9], t[3];
         g_flops = g_sqrt = g_div = 0;
-        o.compute_pose_public(idx, 4, R, t);
+        o.compute_pose_public(idx, 6, R, t);
         f[s] = (double)g_flops;
         sq += g_sqrt;
         dv += g_div;
@@ -73,8 +71,8 @@ int main(int argc, char** argv) {
     for (double x : f) { mean += x; mn = std::min(mn, x); mx = std::max(mx, x); }
     mean /= samples;
     for (double x : f) var += (x - mean) * (x - mean);
-    printf("{\"config\": \"pnp_epnp_compute_pose (4-point sample)\", \"fp64_flops_mean\": %.1f, \"std\": %.1f, "
+    printf("{\"config\": \"mlpnp_compute_pose (6-point sample, N = %d)\", \"fp64_flops_mean\": %.1f, \"std\": %.1f, "
            "\"min\": %.0f, \"max\": %.0f, \"sqrt_mean\": %.2f, \"div_mean\": %.2f, \"samples\": %d}\n",
-           mean, std::sqrt(var / samples), mn, mx, (double)sq / samples, (double)dv / samples, samples);
+           n, mean, std::sqrt(var / samples), mn, mx, (double)sq / samples, (double)dv / samples, samples);
     return 0;
 }
