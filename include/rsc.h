@@ -410,6 +410,10 @@ int rsc_kfdb_state(rsc_kfdb* db, int kf, uint64_t* q, int32_t* w, float* s);
 /* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP refine launch, [job < 64][8]:
  * entry, compaction, control points, MtM, eigen, betas, check, exit. */
 int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out);
+/* Diagnostic: wall-clock (100 MHz) ticks of the last PoseOptimization launch, [frame < 64][8]:
+ * fused passes (ticks), number of passes + (their active edges << 24), re-classification, whole kernel,
+ * 4 unused. */
+int rsc_diag_poseopt_phases(rsc_context* ctx, uint64_t* out);
 /* Diagnostic: wall-clock (100 MHz) phase stamps of the last SearchByBoW launch, [pair < 64][96]. */
 int rsc_diag_bow_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
 

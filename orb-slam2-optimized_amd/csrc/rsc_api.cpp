@@ -2114,19 +2114,13 @@ int rsc_kfdb_clear(rsc_kfdb* db) {
     return RSC_OK;
 }
 
-namespace {
-// One covisibility row padded to kKfdbCovis entries (the _many form reads rows of that stride).
-std::array<int32_t, kKfdbCovis> best_row_of(const int32_t* best, int n) {
-    std::array<int32_t, kKfdbCovis> r{};
-    for (int i = 0; i < n; ++i) r[i] = best[i];
-    return r;
-}
-}  // namespace
-
 int rsc_kfdb_set_covisibility(rsc_kfdb* db, int kf, int n, const int32_t* best) {
     if (!db || kf < 0 || kf >= db->cap || n < 0 || n > kKfdbCovis || (n && !best)) return RSC_ERR_ARG;
     const int32_t nn = n;
-    return rsc_kfdb_set_covisibility_many(db, 1, &kf, &nn, best_row_of(best, n).data());
+    // one covisibility row padded to kKfdbCovis entries (the _many form reads rows of that stride)
+    std::array<int32_t, kKfdbCovis> row{};
+    for (int i = 0; i < n && i < kKfdbCovis; ++i) row[i] = best[i];
+    return rsc_kfdb_set_covisibility_many(db, 1, &kf, &nn, row.data());
 }
 
 int rsc_kfdb_set_covisibility_many(rsc_kfdb* db, int count, const int32_t* kf, const int32_t* n,
@@ -2246,6 +2240,14 @@ int rsc_kfdb_state(rsc_kfdb* db, int kf, uint64_t* q, int32_t* w, float* s) {
         RSC_HIP(hipMemcpy(&w[t], db->words.p + (size_t)t * db->cap + kf, 4, hipMemcpyDeviceToHost));
         RSC_HIP(hipMemcpy(&s[t], db->score.p + (size_t)t * db->cap + kf, 4, hipMemcpyDeviceToHost));
     }
+    return RSC_OK;
+}
+
+int rsc_diag_poseopt_phases(rsc_context* C, uint64_t* out) {
+    if (!C || !out) return RSC_ERR_ARG;
+    RSC_HIP(hipSetDevice(C->device));
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    RSC_HIP(read_poseopt_phases(out));
     return RSC_OK;
 }
 

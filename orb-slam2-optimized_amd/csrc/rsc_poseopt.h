@@ -3,13 +3,14 @@
 // EdgeStereoSE3ProjectXYZOnlyPose (stereo) edges with Huber kernels (delta sqrt(5.991) / sqrt(7.815)),
 // 4 rounds of 10 iterations with inlier/outlier re-classification (chi2 > 5.991 / 7.815).
 //
-// Mapping: one 256-thread workgroup per Frame (problem).  Threads own edges e = tid + 256 k and
-// evaluate the per-edge work of a pass in parallel (error, robust chi2 term, Jacobian and its 27
-// Hessian/gradient terms); the reductions g2o performs as sequential loops over the active edges
-// (activeRobustChi2, buildSystem's H += J^T W J, b -= ...) are folded in edge order on one lane
-// per accumulator, so every sum has the reference's evaluation order.  The LM control (6x6 LDLT,
-// exp map, lambda schedule, stop rules) is tiny and runs redundantly in every lane from the
-// folded values in LDS, so no further broadcast is needed.
+// Mapping: one 256-thread workgroup per Frame (problem).  A pass (computeActiveErrors +
+// activeRobustChi2 + buildSystem at one estimate) walks the round's active edges in slabs of 192:
+// waves 1..3 evaluate one edge per lane (error, robust chi2 term, Jacobian and its 27 Hessian /
+// gradient terms) into an LDS slab buffer while wave 0 folds the previous slab, one lane per
+// accumulator, so every sum g2o performs as a sequential loop over the active edges has the
+// reference's evaluation order.  The LM control (6x6 LDLT, exp map, lambda schedule, stop rules) is
+// tiny and runs redundantly in every lane from the folded values in LDS, so no further broadcast is
+// needed.
 //
 // g2o source followed (Thirdparty/g2o/g2o): optimization_algorithm_levenberg.cpp:59-172,
 // sparse_optimizer.cpp:61-114,354-414, block_solver.hpp:502-604, solvers/linear_solver_dense.h,
@@ -428,6 +429,7 @@ RSC_HD bool po_ldlt_solve(double (&A)[n][n], const double (&b)[n], double (&x)[n
 RSC_HD bool po_ldlt_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[6]) { return po_ldlt_solve<6>(A, b, x); }
 
 #if defined(__HIPCC__)
+hipError_t read_poseopt_phases(uint64_t* out);  // diagnostic, [64][4] (poseopt.hip)
 hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st);
 #endif
 

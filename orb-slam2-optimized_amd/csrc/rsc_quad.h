@@ -432,7 +432,7 @@ struct StageEvView {
 // Block -> (64-hypothesis group, approximation) of pnp_betas_kernel: the three waves of a group are
 // blocks b, b+8, b+16 of a run of 24 (one L2: blocks b and b+8 share an XCD), so the group keeps
 // the XCD its wg_table slot was ordered for; the last (ngroups % 8) groups are dealt plainly.
-RSC_HD inline void betas_block(int b, int ngroups, int& g, int& apx) {
+RSC_HD void betas_block(int b, int ngroups, int& g, int& apx) {
     const int q = ngroups / 8;
     if (b < 24 * q) {
         g = (b % 8) + 8 * (b / 24);

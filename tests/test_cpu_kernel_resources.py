@@ -21,7 +21,8 @@ SCRATCH_FREE = [
     "pnp_betas_kernelILi4E", "pnp_scan_kernelILi8E", "pnp_refine_kernel",
     "sim3_solve_kernel", "sim3_scan_kernelILi4E", "sim3_pick_kernel",
     "sim3opt_kernel", "bow_topk_kernelILb0E", "bow_topk_kernelILb1E", "bow_walk_kernel",
-    "sim3_search_kernel",
+    "sim3_search_kernel", "poseopt_kernel",
+    "mlpnp_quad_kernelILi6ENS_7MlNoCov", "mlpnp_quad_kernelILi6ENS_12MlIndexedCov",
 ]
 
 
