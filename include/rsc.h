@@ -414,6 +414,9 @@ int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out);
  * fused passes (ticks), number of passes + (their active edges << 24), re-classification, whole kernel,
  * 4 unused. */
 int rsc_diag_poseopt_phases(rsc_context* ctx, uint64_t* out);
+/* Diagnostic: wall clock (100 MHz) of KeyFrameDatabase slots 0..4095 in the last count launch,
+ * [slot][4] = entry, staged, counted, exit (zeros unless built with RSC_KFDB_STAMPS=1). */
+int rsc_diag_kfdb_stamps(rsc_context* ctx, uint64_t* out);
 /* Diagnostic: wall-clock (100 MHz) phase stamps of the last SearchByBoW launch, [pair < 64][96]. */
 int rsc_diag_bow_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
 

@@ -1957,7 +1957,7 @@ struct rsc_kfdb {
     DevBuf<uint32_t> ids, seq;
     DevBuf<double> vals;
     DevBuf<char> qbuf;  // the query BowVector: ids | vals (8-aligned), one upload per query
-    DevBuf<int32_t> wpos, len, covis, covis_n, words, list, scored, best, tmp, counters, out;
+    DevBuf<int32_t> len, covis, covis_n, words, list, scored, best, tmp, counters, out;
     DevBuf<unsigned long long> query, key;
     DevBuf<float> score, sc, acc, tscore;
     DevBuf<uint8_t> conn;
@@ -1968,7 +1968,6 @@ struct rsc_kfdb {
         d.cap = hw;  // the kernels' sweep bound; the arrays are sized (and strided) by cap
         d.max_words = max_words;
         d.vocab = vocab;
-        d.wpos = wpos.p;
         d.ids = ids.p;
         d.vals = vals.p;
         d.len = len.p;
@@ -2024,7 +2023,7 @@ int rsc_kfdb_create(rsc_context* C, uint32_t vocab_words, int capacity, int max_
     if ((e = db->covis_h.ensure(K * kKfdbCovis)) || (e = db->covis_n_h.ensure(K))) return e;
     std::memset(db->covis_h.p, 0, K * kKfdbCovis * sizeof(int32_t));
     std::memset(db->covis_n_h.p, 0, K * sizeof(int32_t));
-    if ((e = db->wpos.ensure(vocab_words)) || (e = db->ids.ensure(K * max_words)) || (e = db->vals.ensure(K * max_words)) || (e = db->len.ensure(K)) ||
+    if ((e = db->ids.ensure(K * max_words)) || (e = db->vals.ensure(K * max_words)) || (e = db->len.ensure(K)) ||
         (e = db->seq.ensure(K)) || (e = db->covis.ensure(K * kKfdbCovis)) || (e = db->covis_n.ensure(K)) ||
         (e = db->query.ensure(2 * K)) || (e = db->words.ensure(2 * K)) || (e = db->score.ensure(2 * K)) ||
         (e = db->list.ensure(K)) || (e = db->key.ensure(K)) || (e = db->scored.ensure(K)) || (e = db->sc.ensure(K)) ||
@@ -2036,7 +2035,6 @@ int rsc_kfdb_create(rsc_context* C, uint32_t vocab_words, int capacity, int max_
     if ((e = db->stage.ensure(stage))) return e;
     // KeyFrame.cpp:15: query ids and word counts start at 0; the scores (uninitialised in the
     // reference) are defined as 0
-    RSC_HIP(hipMemsetAsync(db->wpos.p, 0xFF, 4 * (size_t)vocab_words, C->stream));  // -1: no query word
     RSC_HIP(hipMemsetAsync(db->counters.p, 0, 16, C->stream));  // the finish kernel re-zeroes n_list
     RSC_HIP(hipMemsetAsync(db->len.p, 0, 4 * K, C->stream));
     RSC_HIP(hipMemsetAsync(db->covis_n.p, 0, 4 * K, C->stream));
@@ -2240,6 +2238,14 @@ int rsc_kfdb_state(rsc_kfdb* db, int kf, uint64_t* q, int32_t* w, float* s) {
         RSC_HIP(hipMemcpy(&w[t], db->words.p + (size_t)t * db->cap + kf, 4, hipMemcpyDeviceToHost));
         RSC_HIP(hipMemcpy(&s[t], db->score.p + (size_t)t * db->cap + kf, 4, hipMemcpyDeviceToHost));
     }
+    return RSC_OK;
+}
+
+int rsc_diag_kfdb_stamps(rsc_context* C, uint64_t* out) {
+    if (!C || !out) return RSC_ERR_ARG;
+    RSC_HIP(hipSetDevice(C->device));
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    RSC_HIP(read_kfdb_stamps(out));
     return RSC_OK;
 }
 

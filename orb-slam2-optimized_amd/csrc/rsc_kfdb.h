@@ -5,11 +5,11 @@
 // TF-IDF values) at [k * max_words, k * max_words + len[k]), its add order seq[k] (the position
 // the reference's inverted-file lists give it: add() appends to every word's list, erase() removes
 // without reordering, so each list is in ascending seq), its best-10 covisibility list and the
-// per-KeyFrame query state (KeyFrame.hpp:129-134).  A query runs three kernels:
-//   scatter:    the query's word -> position table (a vocabulary-sized int array, -1 elsewhere).
-//   count:      one wave per slot — one table gather per slot word gives the common-word count
-//               (the number of times the reference's inverted-file walk meets the slot) and the
-//               first query word it meets (the list position); the state update reproduces the
+// per-KeyFrame query state (KeyFrame.hpp:129-134).  A query runs two kernels:
+//   count:      one wave per slot, the query BowVector staged in each workgroup's LDS as a hash —
+//               a probe per slot word gives the common-word count (the number of times the
+//               reference's inverted-file walk meets the slot) and the first query word it meets
+//               (the list position); the state update reproduces the
 //               walk's per-occurrence rules exactly; a slot that enters lKFsSharingWords also gets
 //               its DBoW2 L1 score here (terms in parallel, summed in ascending word order through
 //               the wave's shuffles), while its words are in cache and off the finish kernel's
@@ -17,10 +17,9 @@
 //   finish:     one workgroup — maxCommonWords, minCommonWords = int(max * 0.8f), the scored slots
 //               in lKFsSharingWords order (rank by (first query word, seq)) and their scores;
 //               covisibility accumulation, 0.75 * best retain,
-//               first-occurrence de-duplication; candidates in the reference's vector order; the
-//               table is cleared for the next query.
+//               first-occurrence de-duplication; candidates in the reference's vector order.
 // Integer/latency-bound work (a few bytes per BowVector entry, no MFMA); the HBM stream is the
-// slots' word ids (4 B per word) plus one 4-B table gather per word in `count`.
+// slots' word ids (4 B per word) in `count`, plus the values of the common words.
 #pragma once
 #include <cstdint>
 #include <hip/hip_runtime.h>
@@ -33,7 +32,6 @@ constexpr int kKfdbCovis = 10;       // GetBestCovisibilityKeyFrames(10)
 struct DevKFDB {
     int cap, max_words;
     uint32_t vocab;          // word ids < vocab (KeyFrameDatabase(voc): mvInvertedFile sized voc->size())
-    int32_t* wpos;           // [vocab] query word -> position in F->mBowVec, -1 elsewhere
     const uint32_t* ids;     // [cap][max_words]
     const double* vals;      // [cap][max_words]
     const int32_t* len;      // [cap] 0 = not in the inverted file
@@ -55,7 +53,7 @@ struct DevKFDB {
     int32_t* tmp;            // [cap]
     int32_t* counters;       // [0] n_list, [1] n_scored, [2] min_common, [3] n_tmp
     int32_t* out;            // [1 + cap]: n_candidates, candidates
-    const uint32_t* qids;    // [max_words] query BowVector
+    const uint32_t* qids;    // [max_words] query BowVector (ids strictly ascending)
     const double* qvals;
     const uint8_t* conn;     // [cap] connected-KeyFrame mask (loop query)
 };
@@ -68,5 +66,6 @@ struct KfdbQuery {
 };
 
 hipError_t launch_kfdb_query(const DevKFDB& db, const KfdbQuery& q, hipStream_t st);
+hipError_t read_kfdb_stamps(uint64_t* out);  // diagnostic, [4096][4] (kfdb.hip, RSC_KFDB_STAMPS=1 builds)
 
 }  // namespace rsc

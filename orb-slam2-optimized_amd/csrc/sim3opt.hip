@@ -1,11 +1,15 @@
 // sim3opt.hip — Optimizer::OptimizeSim3 (src/Optimizer.cpp:1054-1250) kernel: one 256-thread
-// workgroup per KeyFrame pair.  See rsc_sim3opt.h for the mapping and the arithmetic contract.
+// workgroup per KeyFrame pair.  See rsc_sim3opt.h for the arithmetic contract.
 //
-// A pass computes the per-edge terms of all correspondences in parallel (thread = correspondence,
-// both of its edges) into LDS columns in g2o's edge order, then folds every column in that order on
-// its own lane: H lower triangle (28) and b (7) on lanes 0..34 of wave 0, the robust chi2 column on
-// wave 1.  The LM control, the 7x7 LDLT and the 14 perturbed estimates of the numeric Jacobian run
-// redundantly in every lane (bit-identical values, no broadcast).
+// The pass structure is PoseOptimization's (poseopt.hip): every pass is the fused
+// computeActiveErrors + activeRobustChi2 + buildSystem at one estimate — the LM trial's chi2 pass
+// builds the system at the trial estimate, which is the next iteration's system when the trial is
+// accepted (optimization_algorithm_levenberg.cpp:63-75,108-112) — over the active edges in g2o's
+// order (e12_c, e21_c of every kept correspondence c, ascending), in slabs of 192 edges: waves 1..3
+// evaluate one edge per lane (error, robust chi2 term, the 14-estimate numeric Jacobian and its 35
+// H/b terms) into one of two LDS slab buffers while lanes 0..35 of wave 0 fold the previous slab.
+// The 14 perturbed estimates of a pass (and their inverses) are built once, one per lane, into LDS
+// and read from there by every edge.  The 7x7 LDLT and the LM control run redundantly in every lane.
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <cfloat>
@@ -16,99 +20,163 @@ namespace rsc {
 
 namespace {
 
-constexpr int kSoThreads = 256;                  // correspondences per chunk
-constexpr int kSoChunkEdges = 2 * kSoThreads;    // 512 edge terms per chunk
-constexpr int kSoCol = kSoChunkEdges + 2;        // padded column stride (doubles)
+constexpr int kSoThreads = 256;                  // one wave per SIMD of a CU
+constexpr int kSoFoldLanes = 64;                 // wave 0 folds
+constexpr int kSoSlab = kSoThreads - kSoFoldLanes;  // active edges per slab (waves 1..3)
+constexpr int kSoCol = kSoSlab + 2;              // padded column stride (doubles)
 constexpr int kSoCols = kSim3OptTerms + 1;       // 35 H/b columns + the chi2 column
-constexpr int kSoTermDoubles = kSoCols * kSoCol;
-static_assert(kSoTermDoubles >= 2 * kSim3OptMaxCorr, "chi2 terms of a whole pass must fit the term buffer");
-constexpr size_t kSoLds = sizeof(double) * kSoTermDoubles;
+constexpr int kSoBuf = kSoCols * kSoCol;         // one slab buffer
+constexpr size_t kSoPt = sizeof(SoPerturbed);
+constexpr size_t kSoLds = sizeof(double) * 2 * kSoBuf + kSoPt + sizeof(uint16_t) * kSim3OptMaxCorr;
+static_assert(kSoCol % 2 == 0, "fold_fixed reads 16-byte aligned columns");
+static_assert(kSoPt % 16 == 0, "the active list follows the perturbed estimates");
+static_assert(kSim3OptMaxCorr <= 65536, "active list is uint16");
+
+// The problem's arrays as global-address-space pointers (global, not flat, accesses: a pending
+// flat access would turn every LDS wait of the folds into a full lgkmcnt(0)).
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* so_g(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
+__device__ __forceinline__ float4 so_ld(const float4* p, int e) {
+    using V = float __attribute__((ext_vector_type(4)));
+    const V v = so_g(reinterpret_cast<const V*>(p))[e];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ double2 so_ld(const double2* p, int e) {
+    using V = double __attribute__((ext_vector_type(2)));
+    const V v = so_g(reinterpret_cast<const V*>(p))[e];
+    return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ void so_st(double2* p, int e, double a, double b) {
+    using V = double __attribute__((ext_vector_type(2)));
+    V v;
+    v.x = a;
+    v.y = b;
+    so_g(reinterpret_cast<V*>(p))[e] = v;
+}
 
 struct SoCtx {
     const DevSim3OptProb& P;
-    double* terms;
-    double* red;  // [36]
+    double* terms;       // [2][kSoCols][kSoCol] slab buffers
+    SoPerturbed* pt;     // the pass's perturbed estimates
+    uint16_t* list;      // kept correspondences in order
+    double* red;         // [36] a pass's folded sums
+    double* cur;         // [35] the current system (H lower triangle, b), kept in LDS across passes
+    int* cnt;            // scan / count scratch
     SoCam K1, K2;
     double delta, dsqr, th2;
 };
 
-__device__ __forceinline__ void so_load(const SoCtx& C, int c, bool inverse, double (&X)[3], double& u, double& v,
-                                        double& inv) {
-    const float4 a = inverse ? C.P.e21[c] : C.P.e12[c];
-    const float4 o = C.P.uv[c];
-    X[0] = a.x; X[1] = a.y; X[2] = a.z;
-    inv = a.w;
-    u = inverse ? o.z : o.x;
-    v = inverse ? o.w : o.y;
+// Inputs of one edge (side 0: e12 of correspondence c, side 1: e21), loaded a slab ahead.
+struct SoEdgeIn {
+    float4 a;  // point (camera of the other KeyFrame), w = invSigma2
+    float4 o;  // observations (kpUn1, kpUn2)
+    int c, side;
+};
+
+__device__ __forceinline__ SoEdgeIn so_load_edge(const SoCtx& C, int pos) {
+    SoEdgeIn in;
+    in.c = C.list[pos >> 1];
+    in.side = pos & 1;
+    in.a = so_ld(in.side ? C.P.e21 : C.P.e12, in.c);
+    in.o = so_ld(C.P.uv, in.c);
+    return in;
 }
 
-// computeActiveErrors at S + activeRobustChi2 (sparse_optimizer.cpp:61-114): errors of the active
-// edges stored as _error, robust chi2 terms (0.0 for inactive edges: an exact identity of a sum that
-// starts at +0.0) folded in edge order by one lane.
-__device__ double so_chi_pass(const SoCtx& C, const SoSim3& S) {
-    const DevSim3OptProb& P = C.P;
-    const int tid = threadIdx.x;
+// The kept correspondences in order (the edges initializeOptimization() keeps, in the order
+// Optimizer.cpp:1106-1160 added them); returns their count.
+__device__ int so_list_kept(const SoCtx& C) {
+    const int m = C.P.m, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int per = (m + kSoThreads - 1) / kSoThreads;
+    const int lo = min(m, tid * per), hi = min(m, lo + per);
+    int c = 0;
+    for (int i = lo; i < hi; ++i) c += so_g(C.P.keep)[i] != 0;
+    int inc = c;
+    RSC_UNROLL for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) C.cnt[w] = inc;
+    __syncthreads();
+    int pos = inc - c, total = 0;
+    RSC_UNROLL for (int q = 0; q < kSoThreads / 64; ++q) {
+        const int t = C.cnt[q];
+        if (q < w) pos += t;
+        total += t;
+    }
+    for (int i = lo; i < hi; ++i)
+        if (so_g(C.P.keep)[i]) C.list[pos++] = (uint16_t)i;
+    __syncthreads();
+    return total;
+}
+
+// BaseBinaryEdge::linearizeOplus's 14 perturbed estimates of S and their inverses (so_perturb),
+// one per lane of wave 1, into LDS.
+__device__ void so_build_perturbed(const SoCtx& C, const SoSim3& S) {
+    const int tid = threadIdx.x - kSoFoldLanes;
+    if (tid >= 0 && tid < 14) {
+        const int d = tid % 7;
+        double u[7];
+        RSC_UNROLL for (int i = 0; i < 7; ++i) u[i] = (i == d) ? (tid < 7 ? 1e-9 : -1e-9) : 0.0;  // static indices
+        const SoSim3 e = so_oplus(u, S);
+        const SoSim3 ei = so_inverse(e);
+        SoSim3* dst = tid < 7 ? C.pt->p : C.pt->m;
+        SoSim3* dsti = tid < 7 ? C.pt->pi : C.pt->mi;
+        dst[d] = e;
+        dsti[d] = ei;
+    }
+    __syncthreads();
+}
+
+// One pass at S over the 2 mk active edges: computeActiveErrors (errors stored),
+// activeRobustChi2 (sparse_optimizer.cpp:61-114) and BlockSolverX::buildSystem
+// (block_solver.hpp:502-560: H lower triangle and b added from 0.0), every sum folded in edge order.
+// The folded sums are left in C.red (H lower triangle row-major, b, chi2); C.red is next written at
+// the end of the next pass, so they can be read until then.
+__device__ double so_pass(const SoCtx& C, int mk, const SoSim3& S) {
+    so_build_perturbed(C, S);
+    const int tid = threadIdx.x, me = 2 * mk;
+    const int nslab = (me + kSoSlab - 1) / kSoSlab;
+    const int j = tid - kSoFoldLanes;
     const SoSim3 Si = so_inverse(S);
-    for (int c = tid; c < P.m; c += kSoThreads) {
-        double t0 = 0.0, t1 = 0.0;
-        if (P.keep[c]) {
-            double X[3], u, v, inv, e0, e1;
-            so_load(C, c, false, X, u, v, inv);
-            so_edge_error(S, C.K1, X, u, v, e0, e1);
-            P.err[2 * c] = make_double2(e0, e1);
-            double r1;
-            po_huber(po_chi2(inv, false, e0, e1, 0.0), C.delta, C.dsqr, t0, r1);
-            so_load(C, c, true, X, u, v, inv);
-            so_edge_error(Si, C.K2, X, u, v, e0, e1);
-            P.err[2 * c + 1] = make_double2(e0, e1);
-            po_huber(po_chi2(inv, false, e0, e1, 0.0), C.delta, C.dsqr, t1, r1);
-        }
-        C.terms[2 * c] = t0;
-        C.terms[2 * c + 1] = t1;
-    }
-    __syncthreads();
-    if (tid == 0) C.red[0] = fold_run<false>(0.0, C.terms, 2 * P.m);
-    __syncthreads();
-    const double chi = C.red[0];
-    __syncthreads();
-    return chi;
-}
-
-// BlockSolverX::buildSystem (block_solver.hpp:502-560) with the stored errors at S.
-__device__ void so_build_pass(const SoCtx& C, const SoSim3& S, double (&H)[7][7], double (&b)[7]) {
-    const DevSim3OptProb& P = C.P;
-    const int tid = threadIdx.x;
-    SoPerturbed Pt;
-    so_perturb(S, Pt);
+    SoEdgeIn nx{};
+    if (j >= 0 && j < me) nx = so_load_edge(C, j);
     double acc = 0.0;
-    for (int base = 0; base < P.m; base += kSoThreads) {
-        const int c = base + tid;
-        RSC_UNROLL for (int side = 0; side < 2; ++side) {
-            double t[kSim3OptTerms];
-            RSC_UNROLL for (int k = 0; k < kSim3OptTerms; ++k) t[k] = 0.0;
-            if (c < P.m && P.keep[c]) {
-                double X[3], u, v, inv;
-                so_load(C, c, side == 1, X, u, v, inv);
-                const double2 er = P.err[2 * c + side];
-                so_quad_terms(Pt, side == 1, side == 1 ? C.K2 : C.K1, X, u, v, inv, er.x, er.y, C.delta, C.dsqr, t);
+    for (int k = 0; k <= nslab; ++k) {
+        if (j >= 0) {
+            const int pos = k * kSoSlab + j;
+            double* buf = C.terms + (k & 1) * kSoBuf + j;
+            if (k < nslab && pos < me) {
+                const SoEdgeIn in = nx;
+                if (pos + kSoSlab < me) nx = so_load_edge(C, pos + kSoSlab);
+                const bool inv_edge = in.side == 1;
+                const double X[3] = {(double)in.a.x, (double)in.a.y, (double)in.a.z};
+                const double inv = in.a.w;
+                const double u = inv_edge ? in.o.z : in.o.x, v = inv_edge ? in.o.w : in.o.y;
+                const SoCam& K = inv_edge ? C.K2 : C.K1;
+                double e0, e1;
+                so_edge_error(inv_edge ? Si : S, K, X, u, v, e0, e1);
+                so_st(C.P.err, 2 * in.c + in.side, e0, e1);
+                double tc, r1;
+                po_huber(po_chi2(inv, false, e0, e1, 0.0), C.delta, C.dsqr, tc, r1);
+                double t[kSim3OptTerms];
+                so_quad_terms(*C.pt, inv_edge, K, X, u, v, inv, e0, e1, C.delta, C.dsqr, t);
+                RSC_UNROLL for (int q = 0; q < kSim3OptTerms; ++q) buf[q * kSoCol] = t[q];
+                buf[kSim3OptTerms * kSoCol] = tc;
+            } else if (k < nslab) {
+                // padding of the last slab: +0.0 terms are exact identities of these folds (an
+                // accumulator that starts at +0.0 never becomes -0.0 under round-to-nearest)
+                RSC_UNROLL for (int q = 0; q < kSoCols; ++q) buf[q * kSoCol] = 0.0;
             }
-            RSC_UNROLL for (int k = 0; k < kSim3OptTerms; ++k) C.terms[k * kSoCol + 2 * tid + side] = t[k];
+        } else if (k > 0 && tid < kSoCols) {
+            acc = fold_fixed<kSoSlab>(acc, C.terms + ((k - 1) & 1) * kSoBuf + tid * kSoCol);
         }
-        __syncthreads();
-        const int m = 2 * min(kSoThreads, P.m - base);
-        if (tid < kSim3OptTerms) acc = fold_run<false>(acc, C.terms + tid * kSoCol, m);
         __syncthreads();
     }
-    if (tid < kSim3OptTerms) C.red[tid] = acc;
+    if (tid < kSoCols) C.red[tid] = acc;
     __syncthreads();
-    int k = 0;
-    RSC_UNROLL for (int i = 0; i < 7; ++i)
-        RSC_UNROLL for (int j = 0; j <= i; ++j) {
-            H[i][j] = C.red[k++];
-            H[j][i] = H[i][j];
-        }
-    RSC_UNROLL for (int i = 0; i < 7; ++i) b[i] = C.red[28 + i];
-    __syncthreads();
+    return C.red[kSim3OptTerms];
 }
 
 struct SoLM {
@@ -120,17 +188,24 @@ struct SoLM {
 // initializeOptimization() + optimize(iterations) (sparse_optimizer.cpp:354-414) with
 // OptimizationAlgorithmLevenberg::solve (optimization_algorithm_levenberg.cpp:59-151).
 __device__ void so_optimize(const SoCtx& C, SoLM& L, SoSim3& S, int iterations) {
+    const int mk = so_list_kept(C);
+    if (mk == 0) return;
+    // the system at S (C.cur: lower triangle row-major, then b) and the chi2 solve() computes there
+    double chiS = so_pass(C, mk, S);
+    auto adopt = [&]() {  // C.cur = the last pass's system
+        if (threadIdx.x < kSim3OptTerms) C.cur[threadIdx.x] = C.red[threadIdx.x];
+        __syncthreads();
+    };
+    adopt();
     bool ok = true;
     for (int i = 0; i < iterations && ok; ++i) {
         L.its++;
-        double currentChi = so_chi_pass(C, S);
+        double currentChi = chiS;
         const double iniChi = currentChi;
-        double H[7][7], b[7];
-        so_build_pass(C, S, H, b);
         if (i == 0) {
             double maxDiagonal = 0.;
             RSC_UNROLL for (int j = 0; j < 7; ++j) {  // std::max(fabs(H(j,j)), maxDiagonal)
-                const double a = rabs(H[j][j]);
+                const double a = rabs(C.cur[j * (j + 1) / 2 + j]);
                 maxDiagonal = (a < maxDiagonal) ? maxDiagonal : a;
             }
             L.lambda = 1e-5 * maxDiagonal;
@@ -141,17 +216,20 @@ __device__ void so_optimize(const SoCtx& C, SoLM& L, SoSim3& S, int iterations) 
         int qmax = 0;
         do {
             L.trials++;
-            const SoSim3 saved = S;
             double Hd[7][7];
-            RSC_UNROLL for (int r = 0; r < 7; ++r)
-                RSC_UNROLL for (int c = 0; c < 7; ++c) Hd[r][c] = H[r][c];
+            double b[7];
+            RSC_UNROLL for (int r = 0; r < 7; ++r) {
+                RSC_UNROLL for (int c = 0; c < 7; ++c)
+                    Hd[r][c] = r >= c ? C.cur[r * (r + 1) / 2 + c] : C.cur[c * (c + 1) / 2 + r];
+                b[r] = C.cur[28 + r];
+            }
             RSC_UNROLL for (int r = 0; r < 7; ++r) Hd[r][r] += L.lambda;
             double xs[7];
             const bool ok2 = po_ldlt_solve<7>(Hd, b, xs);
             if (ok2) RSC_UNROLL for (int j = 0; j < 7; ++j) L.x[j] = xs[j];
-            S = so_oplus(L.x, S);
-            double tempChi = so_chi_pass(C, S);
-            if (!ok2) tempChi = DBL_MAX;
+            const SoSim3 trial = so_oplus(L.x, S);
+            const double chiT = so_pass(C, mk, trial);
+            const double tempChi = ok2 ? chiT : DBL_MAX;
             rho = (currentChi - tempChi);
             double scale = 0.;
             RSC_UNROLL for (int j = 0; j < 7; ++j) scale += L.x[j] * (L.lambda * L.x[j] + b[j]);
@@ -164,10 +242,13 @@ __device__ void so_optimize(const SoCtx& C, SoLM& L, SoSim3& S, int iterations) 
                 L.lambda *= scaleFactor;
                 L.ni = 2;
                 currentChi = tempChi;
+                S = trial;
+                adopt();  // the trial's system
+                chiS = chiT;
             } else {
+                // pop: the edges keep the rejected trial's errors (no recompute in g2o)
                 L.lambda *= L.ni;
                 L.ni *= 2;
-                S = saved;  // pop: the edges keep the rejected trial's errors (no recompute in g2o)
             }
             qmax++;
         } while (rho < 0 && qmax < 10);
@@ -183,16 +264,17 @@ __device__ void so_optimize(const SoCtx& C, SoLM& L, SoSim3& S, int iterations) 
 
 // chi2 > th2 test of correspondence c on its stored errors (Optimizer.cpp:1184, :1216).
 __device__ __forceinline__ bool so_outlier(const SoCtx& C, int c) {
-    const double2 a = C.P.err[2 * c], b = C.P.err[2 * c + 1];
-    const float4 p = C.P.e12[c], q = C.P.e21[c];
+    const double2 a = so_ld(C.P.err, 2 * c), b = so_ld(C.P.err, 2 * c + 1);
+    const float4 p = so_ld(C.P.e12, c), q = so_ld(C.P.e21, c);
     return po_chi2((double)p.w, false, a.x, a.y, 0.0) > C.th2 || po_chi2((double)q.w, false, b.x, b.y, 0.0) > C.th2;
 }
 
 __device__ void so_write(const DevSim3OptProb& P, const SoSim3& S, int nIn, int nBad, const SoLM& L) {
-    P.out[0] = S.r.x; P.out[1] = S.r.y; P.out[2] = S.r.z; P.out[3] = S.r.w;
-    P.out[4] = S.t[0]; P.out[5] = S.t[1]; P.out[6] = S.t[2];
-    P.out[7] = S.s;
-    int* o = reinterpret_cast<int*>(P.out + 8);
+    auto out = so_g(P.out);
+    out[0] = S.r.x; out[1] = S.r.y; out[2] = S.r.z; out[3] = S.r.w;
+    out[4] = S.t[0]; out[5] = S.t[1]; out[6] = S.t[2];
+    out[7] = S.s;
+    auto o = so_g(reinterpret_cast<int*>(P.out + 8));
     o[0] = nIn; o[1] = nBad; o[2] = L.its; o[3] = L.trials;
 }
 
@@ -201,10 +283,14 @@ __device__ void so_write(const DevSim3OptProb& P, const SoSim3& S, int nIn, int 
 __global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptProb* __restrict__ probs) {
     extern __shared__ __attribute__((aligned(16))) double so_lds[];
     __shared__ double red_sh[kSoCols];
-    __shared__ int cnt_sh;
+    __shared__ double cur_sh[kSim3OptTerms];
+    __shared__ int cnt_sh[kSoThreads / 64];
+    __shared__ int tot_sh;
     const DevSim3OptProb& P = probs[blockIdx.x];
     const int tid = threadIdx.x;
-    SoCtx C{P, so_lds, red_sh, {}, {}, 0.0, 0.0, (double)P.th2};
+    SoPerturbed* pt = reinterpret_cast<SoPerturbed*>(so_lds + 2 * kSoBuf);
+    uint16_t* list = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(pt) + kSoPt);
+    SoCtx C{P, so_lds, pt, list, red_sh, cur_sh, cnt_sh, {}, {}, 0.0, 0.0, (double)P.th2};
     C.K1 = SoCam{(double)P.K1[0], (double)P.K1[1], (double)P.K1[2], (double)P.K1[3]};
     C.K2 = SoCam{(double)P.K2[0], (double)P.K2[1], (double)P.K2[2], (double)P.K2[3]};
     C.delta = P.delta;
@@ -214,8 +300,8 @@ __global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptPro
     S.t[0] = P.S0[4]; S.t[1] = P.S0[5]; S.t[2] = P.S0[6];
     S.s = P.S0[7];
     const SoSim3 S_in = S;
-    for (int c = tid; c < P.m; c += kSoThreads) P.keep[c] = 1;
-    if (tid == 0) cnt_sh = 0;
+    for (int c = tid; c < P.m; c += kSoThreads) so_g(P.keep)[c] = 1;
+    if (tid == 0) tot_sh = 0;
     __syncthreads();
     SoLM L;
     so_optimize(C, L, S, 5);
@@ -223,29 +309,29 @@ __global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptPro
     int bad = 0;
     for (int c = tid; c < P.m; c += kSoThreads) {
         if (so_outlier(C, c)) {
-            P.keep[c] = 0;
+            so_g(P.keep)[c] = 0;
             ++bad;
         }
     }
-    if (bad) atomicAdd(&cnt_sh, bad);
+    if (bad) atomicAdd(&tot_sh, bad);
     __syncthreads();
-    const int nBad = cnt_sh;
+    const int nBad = tot_sh;
     __syncthreads();
     if (P.m - nBad < 10) {  // return 0, g2oS12 untouched (:1201-1202)
         if (tid == 0) so_write(P, S_in, 0, nBad, L);
         return;
     }
-    if (tid == 0) cnt_sh = 0;
+    if (tid == 0) tot_sh = 0;
     so_optimize(C, L, S, nBad > 0 ? 10 : 5);
     int in = 0;
     for (int c = tid; c < P.m; c += kSoThreads) {
-        if (!P.keep[c]) continue;
-        if (so_outlier(C, c)) P.keep[c] = 0;
+        if (!so_g(P.keep)[c]) continue;
+        if (so_outlier(C, c)) so_g(P.keep)[c] = 0;
         else ++in;
     }
-    if (in) atomicAdd(&cnt_sh, in);
+    if (in) atomicAdd(&tot_sh, in);
     __syncthreads();
-    if (tid == 0) so_write(P, S, cnt_sh, nBad, L);
+    if (tid == 0) so_write(P, S, tot_sh, nBad, L);
 }
 
 hipError_t launch_sim3opt(int count, const DevSim3OptProb* probs, hipStream_t st) {

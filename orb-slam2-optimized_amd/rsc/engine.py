@@ -42,7 +42,7 @@ EXPORTED = [
     "rsc_mlpnp_reset_many", "rsc_mlpnp_get_state", "rsc_mlpnp_last_poses", "rsc_mlpnp_last_samples",
     "rsc_reloc_events", "rsc_loop_events", "rsc_pose_optimization_many",
     "rsc_bow_create", "rsc_bow_destroy", "rsc_bow_set_valid", "rsc_search_by_bow_frame_many",
-    "rsc_search_by_bow_kf_many", "rsc_diag_bow_phase_stamps", "rsc_diag_refine_phase_stamps", "rsc_diag_poseopt_phases",
+    "rsc_search_by_bow_kf_many", "rsc_diag_bow_phase_stamps", "rsc_diag_refine_phase_stamps", "rsc_diag_poseopt_phases", "rsc_diag_kfdb_stamps",
     "rsc_search_by_sim3_many", "rsc_kfview_create", "rsc_kfview_destroy",
     "rsc_optimize_sim3_many",
     "rsc_kfdb_create", "rsc_kfdb_destroy", "rsc_kfdb_add", "rsc_kfdb_erase", "rsc_kfdb_release", "rsc_kfdb_clear",
@@ -385,6 +385,7 @@ def load_library(path: str = LIB_PATH):
                                             C.c_int]
     L.rsc_diag_refine_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
     L.rsc_diag_poseopt_phases.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
+    L.rsc_diag_kfdb_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
     f32p_ = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
     L.rsc_kfview_create.argtypes = [vp, C.POINTER(Sim3KFStruct), C.POINTER(vp)]
     L.rsc_kfview_destroy.argtypes = [vp]
