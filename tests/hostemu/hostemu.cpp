@@ -349,7 +349,9 @@ int he_mlpnp_count(const double* R, const double* t, const float* K, float th2, 
 }
 
 // PoseOptimization in the device orchestration (poseopt.hip), run sequentially: the same per-edge
-// functions and the same edge-order folds.  xw4 [n][4] = (X, Y, Z, invSigma2), uv [n][2].
+// functions, the same fused passes (errors + robust chi2 + system at one estimate, the trial's
+// system adopted when the trial is accepted) and the same edge-order folds over the active edges —
+// the CPU tests check it against the oracle's literal g2o control flow.  xw4 [n][4] = (X, Y, Z, invSigma2), uv [n][2].
 // out[16]: Tcw rows 0..2, then n_good, rounds, lm_iterations, lm_trials (as int bits).
 void he_pose_optimization(int n, const float* xw4, const float* uv, const float* K4, const float* T12, float* out,
                           uint8_t* outlier, const float* ur /* nullable: all mono */, float bf) {
@@ -373,38 +375,29 @@ void he_pose_optimization(int n, const float* xw4, const float* uv, const float*
     const PoSE3 init = po_from_Rt(R0, t0);
     for (int e = 0; e < n; ++e) outlier[e] = 0;
     bool robust = true;
-    auto chi_pass = [&](const PoSE3& est) {
-        double acc = 0.0;
+    // one fused pass at est over the active edges in edge order (poseopt.hip po_pass): errors stored,
+    // the 27 H/b terms (b's negated) and the robust chi2 term folded; returns chi2
+    auto pass = [&](const PoSE3& est, double (&H)[6][6], double (&b)[6]) {
+        double acc[kPoseTerms + 1];
+        for (int k = 0; k <= kPoseTerms; ++k) acc[k] = 0.0;
         for (int e = 0; e < n; ++e) {
-            double t = 0.0;
-            if (lvl[e] == 0) {
-                edge_error(est, e);
-                const bool st = stereo(e);
-                t = po_chi_term(robust, st, xw4[4 * e + 3], err[3 * e], err[3 * e + 1], err[3 * e + 2], st ? ds : dm,
-                                st ? ds2 : dm2);
-            }
-            acc = acc + t;
-        }
-        return acc;
-    };
-    auto build_pass = [&](const PoSE3& est, double (&H)[6][6], double (&b)[6]) {
-        double acc[kPoseTerms];
-        for (int k = 0; k < kPoseTerms; ++k) acc[k] = 0.0;
-        for (int e = 0; e < n; ++e) {
+            if (lvl[e]) continue;
+            edge_error(est, e);
+            const double X[3] = {xw4[4 * e], xw4[4 * e + 1], xw4[4 * e + 2]};
+            const bool st = stereo(e);
             double t[kPoseTerms];
-            for (int k = 0; k < kPoseTerms; ++k) t[k] = 0.0;
-            if (lvl[e] == 0) {
-                const double X[3] = {xw4[4 * e], xw4[4 * e + 1], xw4[4 * e + 2]};
-                const bool st = stereo(e);
-                po_quad_terms(est, K, X, xw4[4 * e + 3], err[3 * e], err[3 * e + 1], err[3 * e + 2], st, robust,
-                              st ? ds : dm, st ? ds2 : dm2, t);
-            }
-            for (int k = 0; k < kPoseTerms; ++k) acc[k] = (k >= 21) ? acc[k] - t[k] : acc[k] + t[k];
+            po_quad_terms(est, K, X, xw4[4 * e + 3], err[3 * e], err[3 * e + 1], err[3 * e + 2], st, robust,
+                          st ? ds : dm, st ? ds2 : dm2, t);
+            const double tc = po_chi_term(robust, st, xw4[4 * e + 3], err[3 * e], err[3 * e + 1], err[3 * e + 2],
+                                          st ? ds : dm, st ? ds2 : dm2);
+            for (int k = 0; k < kPoseTerms; ++k) acc[k] = acc[k] + ((k >= 21) ? -t[k] : t[k]);
+            acc[kPoseTerms] = acc[kPoseTerms] + tc;
         }
         int k = 0;
         for (int i = 0; i < 6; ++i)
             for (int j = 0; j <= i; ++j) { H[i][j] = acc[k++]; H[j][i] = H[i][j]; }
         for (int i = 0; i < 6; ++i) b[i] = acc[21 + i];
+        return acc[kPoseTerms];
     };
     double x[6] = {0, 0, 0, 0, 0, 0};
     double lambda = -1.0, ni = 2.0;
@@ -416,13 +409,13 @@ void he_pose_optimization(int n, const float* xw4, const float* uv, const float*
         bool any = false;
         for (int e = 0; e < n; ++e) any |= (lvl[e] == 0);
         if (any) {
+            double H[6][6], b[6];
+            double chiEst = pass(est, H, b);
             bool ok = true;
             for (int i = 0; i < 10 && ok; ++i) {
                 lm_its++;
-                double currentChi = chi_pass(est);
+                double currentChi = chiEst;
                 const double iniChi = currentChi;
-                double H[6][6], b[6];
-                build_pass(est, H, b);
                 if (i == 0) {
                     double maxDiagonal = 0.;
                     for (int j = 0; j < 6; ++j) { const double a = std::fabs(H[j][j]); maxDiagonal = (a < maxDiagonal) ? maxDiagonal : a; }
@@ -434,16 +427,16 @@ void he_pose_optimization(int n, const float* xw4, const float* uv, const float*
                 int qmax = 0;
                 do {
                     lm_trials++;
-                    const PoSE3 saved = est;
                     double Hd[6][6];
                     for (int r = 0; r < 6; ++r) for (int c = 0; c < 6; ++c) Hd[r][c] = H[r][c];
                     for (int r = 0; r < 6; ++r) Hd[r][r] += lambda;
                     double xs[6];
                     const bool ok2 = po_ldlt_solve6(Hd, b, xs);
                     if (ok2) for (int j = 0; j < 6; ++j) x[j] = xs[j];
-                    est = po_mul(po_exp(x), est);
-                    double tempChi = chi_pass(est);
-                    if (!ok2) tempChi = DBL_MAX;
+                    const PoSE3 trial = po_mul(po_exp(x), est);
+                    double Ht[6][6], bt[6];
+                    const double chiT = pass(trial, Ht, bt);
+                    const double tempChi = ok2 ? chiT : DBL_MAX;
                     rho = (currentChi - tempChi);
                     double scale = 0.;
                     for (int j = 0; j < 6; ++j) scale += x[j] * (lambda * x[j] + b[j]);
@@ -456,10 +449,13 @@ void he_pose_optimization(int n, const float* xw4, const float* uv, const float*
                         lambda *= scaleFactor;
                         ni = 2;
                         currentChi = tempChi;
+                        est = trial;
+                        std::memcpy(H, Ht, sizeof(H));
+                        std::memcpy(b, bt, sizeof(b));
+                        chiEst = chiT;
                     } else {
                         lambda *= ni;
                         ni *= 2;
-                        est = saved;
                     }
                     qmax++;
                 } while (rho < 0 && qmax < 10);
@@ -494,7 +490,7 @@ void he_pose_optimization(int n, const float* xw4, const float* uv, const float*
 }
 
 // OptimizeSim3 in the device orchestration (sim3opt.hip), run sequentially: the same per-edge
-// functions, terms in the edge order e12_0, e21_0, ..., the same folds.  Inputs already compacted:
+// functions, the same fused passes, terms in the edge order e12_0, e21_0, ..., the same folds.  Inputs already compacted:
 // e12/e21 [m][4] = (X, invSigma2), uv [m][4]; S[8] in/out; keep[m]; stats[4] = nIn, nBad, its, trials.
 void he_optimize_sim3(int m, const float* e12, const float* e21, const float* uv, const float* K8, float th2,
                       double* S8, uint8_t* keep, int32_t* stats) {
@@ -511,58 +507,49 @@ void he_optimize_sim3(int m, const float* e12, const float* e21, const float* uv
         u = uv[4 * c + (inv_edge ? 2 : 0)];
         v = uv[4 * c + (inv_edge ? 3 : 1)];
     };
-    auto chi_pass = [&](const SoSim3& S) {
-        const SoSim3 Si = so_inverse(S);
-        double acc = 0.0;
-        for (int c = 0; c < m; ++c) {
-            double t0 = 0.0, t1 = 0.0, r1;
-            if (keep[c]) {
-                double X[3], u, v, inv;
-                load(c, false, X, u, v, inv);
-                so_edge_error(S, K1, X, u, v, err[4 * c], err[4 * c + 1]);
-                po_huber(po_chi2(inv, false, err[4 * c], err[4 * c + 1], 0.0), delta, dsqr, t0, r1);
-                load(c, true, X, u, v, inv);
-                so_edge_error(Si, K2, X, u, v, err[4 * c + 2], err[4 * c + 3]);
-                po_huber(po_chi2(inv, false, err[4 * c + 2], err[4 * c + 3], 0.0), delta, dsqr, t1, r1);
-            }
-            acc = acc + t0;
-            acc = acc + t1;
-        }
-        return acc;
-    };
-    auto build_pass = [&](const SoSim3& S, double (&H)[7][7], double (&b)[7]) {
+    // one fused pass at S over the kept correspondences' edges in g2o's order (sim3opt.hip so_pass):
+    // errors stored, the 35 H/b terms and the robust chi2 term folded; returns chi2
+    auto pass = [&](const SoSim3& S, double (&H)[7][7], double (&b)[7]) {
         SoPerturbed Pt;
         so_perturb(S, Pt);
-        double acc[kSim3OptTerms];
-        for (int k = 0; k < kSim3OptTerms; ++k) acc[k] = 0.0;
-        for (int c = 0; c < m; ++c)
+        const SoSim3 Si = so_inverse(S);
+        double acc[kSim3OptTerms + 1];
+        for (int k = 0; k <= kSim3OptTerms; ++k) acc[k] = 0.0;
+        for (int c = 0; c < m; ++c) {
+            if (!keep[c]) continue;
             for (int side = 0; side < 2; ++side) {
+                double X[3], u, v, inv, r0, r1;
+                load(c, side == 1, X, u, v, inv);
+                double& e0 = err[4 * c + 2 * side];
+                double& e1 = err[4 * c + 2 * side + 1];
+                so_edge_error(side ? Si : S, side ? K2 : K1, X, u, v, e0, e1);
+                po_huber(po_chi2(inv, false, e0, e1, 0.0), delta, dsqr, r0, r1);
                 double t[kSim3OptTerms];
-                for (int k = 0; k < kSim3OptTerms; ++k) t[k] = 0.0;
-                if (keep[c]) {
-                    double X[3], u, v, inv;
-                    load(c, side == 1, X, u, v, inv);
-                    so_quad_terms(Pt, side == 1, side ? K2 : K1, X, u, v, inv, err[4 * c + 2 * side],
-                                  err[4 * c + 2 * side + 1], delta, dsqr, t);
-                }
+                so_quad_terms(Pt, side == 1, side ? K2 : K1, X, u, v, inv, e0, e1, delta, dsqr, t);
                 for (int k = 0; k < kSim3OptTerms; ++k) acc[k] = acc[k] + t[k];
+                acc[kSim3OptTerms] = acc[kSim3OptTerms] + r0;
             }
+        }
         int k = 0;
         for (int i = 0; i < 7; ++i)
             for (int j = 0; j <= i; ++j) { H[i][j] = acc[k++]; H[j][i] = H[i][j]; }
         for (int i = 0; i < 7; ++i) b[i] = acc[28 + i];
+        return acc[kSim3OptTerms];
     };
     double x[7] = {0, 0, 0, 0, 0, 0, 0};
     double lambda = -1.0, ni = 2.0;
     int nBadLM = 0, its = 0, trials = 0;
     auto optimize = [&](SoSim3& S, int iterations) {
+        bool any = false;
+        for (int c = 0; c < m; ++c) any |= keep[c] != 0;
+        if (!any) return;
+        double H[7][7], b[7];
+        double chiS = pass(S, H, b);
         bool ok = true;
         for (int i = 0; i < iterations && ok; ++i) {
             its++;
-            double currentChi = chi_pass(S);
+            double currentChi = chiS;
             const double iniChi = currentChi;
-            double H[7][7], b[7];
-            build_pass(S, H, b);
             if (i == 0) {
                 double maxDiagonal = 0.;
                 for (int j = 0; j < 7; ++j) { const double a = std::fabs(H[j][j]); maxDiagonal = (a < maxDiagonal) ? maxDiagonal : a; }
@@ -574,16 +561,16 @@ void he_optimize_sim3(int m, const float* e12, const float* e21, const float* uv
             int qmax = 0;
             do {
                 trials++;
-                const SoSim3 saved = S;
                 double Hd[7][7];
                 for (int r = 0; r < 7; ++r) for (int c = 0; c < 7; ++c) Hd[r][c] = H[r][c];
                 for (int r = 0; r < 7; ++r) Hd[r][r] += lambda;
                 double xs[7];
                 const bool ok2 = po_ldlt_solve<7>(Hd, b, xs);
                 if (ok2) for (int j = 0; j < 7; ++j) x[j] = xs[j];
-                S = so_oplus(x, S);
-                double tempChi = chi_pass(S);
-                if (!ok2) tempChi = DBL_MAX;
+                const SoSim3 trial = so_oplus(x, S);
+                double Ht[7][7], bt[7];
+                const double chiT = pass(trial, Ht, bt);
+                const double tempChi = ok2 ? chiT : DBL_MAX;
                 rho = (currentChi - tempChi);
                 double scale = 0.;
                 for (int j = 0; j < 7; ++j) scale += x[j] * (lambda * x[j] + b[j]);
@@ -596,10 +583,13 @@ void he_optimize_sim3(int m, const float* e12, const float* e21, const float* uv
                     lambda *= scaleFactor;
                     ni = 2;
                     currentChi = tempChi;
+                    S = trial;
+                    std::memcpy(H, Ht, sizeof(H));
+                    std::memcpy(b, bt, sizeof(b));
+                    chiS = chiT;
                 } else {
                     lambda *= ni;
                     ni *= 2;
-                    S = saved;
                 }
                 qmax++;
             } while (rho < 0 && qmax < 10);
