@@ -22,7 +22,8 @@ __global__ __launch_bounds__(64) void mlpnp_quad_kernel(const DevML* __restrict_
                                                         const int2* __restrict__ wg_table,
                                                         const uint32_t* __restrict__ rng_T,
                                                         double* __restrict__ poses, int32_t* __restrict__ samples) {
-    __shared__ __attribute__((aligned(16))) double smem[kMlQuadHyps * kMlQuadRegion];
+    constexpr int kRegion = ml_quad_region<NS, Cov>();
+    __shared__ __attribute__((aligned(16))) double smem[kMlQuadHyps * kRegion];
     const int lane = threadIdx.x, g = lane >> 2, q = lane & 3;
     const int2 wt = wg_table[blockIdx.x];
     const LaunchProb& lp = lps[wt.x];
@@ -38,7 +39,7 @@ __global__ __launch_bounds__(64) void mlpnp_quad_kernel(const DevML* __restrict_
         swap_remove_sample<NS>(words, NS, P.n, idx);
     }
     double R[3][3], t[3];
-    double* region = smem + g * kMlQuadRegion;
+    double* region = smem + g * kRegion;
     if constexpr (Cov::on) {  // covariances supplied: the covMats branch of computePose
         mlpnp_quad_hypothesis<NS>(P, idx, MlIndexedCov{P.cov, idx}, q, region, R, t);
     } else {

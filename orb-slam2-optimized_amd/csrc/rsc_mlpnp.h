@@ -678,6 +678,12 @@ struct MlRegs {
     RSC_HD bool planar() const { return m.planar; }
 };
 
+// Doubles of the Gauss-Newton slab: J (2 NS x 6), g (6), the 6x6 system + its temp row (stride 12).
+template <int NS>
+constexpr int ml_gn_slab() {
+    return 12 * NS + 6 + 6 * 12 + 6;
+}
+
 // Phase 3 of computePose (:480-623): pose recovery from the null vector r1 (the V column of the
 // smallest singular value of the normal matrix) and the Gauss-Newton refinement (mlpnp_gn,
 // :659-723).  slab: kMlSlabDoubles doubles (element stride slab.stride) for J and the LDLT system.
@@ -775,8 +781,10 @@ RSC_HD void mlpnp_finish_pose(const View& in, const double (&r1)[12], const Lane
         x[0] = w3[0]; x[1] = w3[1]; x[2] = w3[2];
         x[3] = t[0]; x[4] = t[1]; x[5] = t[2];
     }
-    const MlView Jv{slab.base, slab.stride, 0};   // J(r, k) = e(r*6 + k), r < 2*NS
-    const MlView Av{slab.base, slab.stride, 144};  // 6x6 (+ temp row 6)
+    // J(r, k) = e(r*6 + k), r < 2*NS; g right after J; the 6x6 system (+ temp row 6) after g: the
+    // Gauss-Newton slab is ml_gn_slab<NS>() doubles
+    const MlView Jv{slab.base, slab.stride, 0};
+    const MlView Av{slab.base, slab.stride, 12 * NS + 6};
     int it = 0;
     bool stop = false;
     while (it < 5 && !stop) {
@@ -805,8 +813,7 @@ RSC_HD void mlpnp_finish_pose(const View& in, const double (&r1)[12], const Lane
         // J^T J (or J^T Kll J) and J^T r one row a at a time; where registers are short (covariances,
         // NS > 6) the row loop stays rolled, so J stays in the slab instead of 2 NS x 6 doubles of
         // VGPRs; g[a] waits in the J region's spare rows (e >= 2 NS * 6)
-        constexpr int kG = 120;
-        static_assert(2 * NS * 6 <= kG, "g rows after J");
+        constexpr int kG = 12 * NS;
         auto row = [&](int a) {
             if constexpr (Cov::on) {
                 // JacTSKll = J^T Kll: (k, 2i + q) = J(2i, k) P_i(0, q) + J(2i + 1, k) P_i(1, q)

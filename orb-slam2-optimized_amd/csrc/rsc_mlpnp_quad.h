@@ -19,10 +19,23 @@
 
 namespace rsc {
 
-constexpr int kMlQuadGN = 222;    // doubles of the Gauss-Newton slab (J rows, then the 6x6 system)
-// per-hypothesis LDS region: GN slab + the parked phase-1 state (<= 138 doubles at NS = 8); odd modulo
-// 32 so the quads of a wave start on different LDS banks
-constexpr int kMlQuadRegion = 361;
+// Per-hypothesis LDS region: a slab shared by the phase-1 design matrix A (2 NS x 12) and the
+// Gauss-Newton system (ml_gn_slab), then the parked phase-1 state of the variant; rounded up to an
+// odd number of doubles so the quads of a wave start on different LDS banks.  The common variant
+// (NS = 6, no covariances) takes 239 doubles, 30 KB per 16-hypothesis workgroup: LDS no longer caps
+// the CU at three workgroups (it did at 361 doubles), one wave per SIMD is the VGPR bound.
+template <int NS>
+constexpr int ml_quad_slab() {
+    return (24 * NS > ml_gn_slab<NS>()) ? 24 * NS : ml_gn_slab<NS>();
+}
+template <int NS, class Cov>
+constexpr int ml_quad_parked() {
+    return 3 * NS + 3 * NS + 6 * NS + (Cov::on ? 4 * NS : 0) + 9 + 1;
+}
+template <int NS, class Cov>
+constexpr int ml_quad_region() {
+    return (ml_quad_slab<NS>() + ml_quad_parked<NS, Cov>()) | 1;
+}
 
 // DPP quad_perm control that swaps lanes a and b of every quad (others read themselves).
 __host__ __device__ constexpr int quad_swap_ctrl(int a, int b) {
@@ -234,7 +247,7 @@ __device__ __forceinline__ void ml_unpark(const double* st, double (&pw)[NS][3],
     RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) m.eigenRot[r][c] = st[k++];
     m.planar = st[k++] != 0.0;
 }
-static_assert(kMlQuadRegion - kMlQuadGN >= 8 * 6 + 8 * 6 + 8 * 4 + 9 + 1, "parked state fits the region");
+static_assert(ml_quad_region<8, MlIndexedCov>() * kMlQuadHyps * 8 <= 48 * 1024, "the largest region");
 
 // The parked state (ml_park layout) read in place by mlpnp_finish_pose.
 template <int NS, class Cov>
@@ -253,7 +266,7 @@ struct MlParked {
 template <int NS, class Cov>
 __device__ __forceinline__ void mlpnp_quad_hypothesis(const DevML& P, const int (&idx)[NS], const Cov& cov, int q,
                                                       double* region, double (&Rout)[3][3], double (&tout)[3]) {
-    double* stash = region + kMlQuadGN;
+    double* stash = region + ml_quad_slab<NS>();
     double Wc[3][12], Vc[3][12];
     bool planar;
     {
