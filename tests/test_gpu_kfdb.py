@@ -188,3 +188,35 @@ def test_release_resets_the_slot():
     a = g.detect_relocalization(4, ids, vals)
     b = o.detect_relocalization(4, ids, vals)
     assert [50 if x == k else x for x in a] == list(b)
+
+
+def test_long_bow_vectors_and_queries():
+    """BowVectors over 1,024 words (the count kernel's second batch of ids: counts and the L1 score
+    carried across batches) and queries up to the 4,096-word bound (the largest LDS hash, 8,192
+    entries, above the default 64 KB of dynamic LDS)."""
+    rng = np.random.default_rng(34)
+    n = 60
+    sc = synth.make_kfdb_scene(rng, n, words_per_kf=1800, step=300, n_frequent=40)
+    g, o = gpu_db(n + 4), ol.OracleKFDB(n + 4)
+    for k in range(n):
+        for db in (g, o):
+            db.add(k, *sc.bows[k])
+            db.set_covisibility(k, sc.covis[k])
+    # one KeyFrame at the 4,096-word bound, sharing its words with the long queries below
+    big = np.unique(np.concatenate([sc.bows[30][0], rng.choice(10 ** 6, 3000, replace=False).astype(np.uint32)]))[:4096]
+    bv = rng.uniform(0.01, 1.0, len(big))
+    for db in (g, o):
+        db.add(n, big, bv / bv.sum())
+    assert max(len(b[0]) for b in sc.bows) > 1024
+    for f, words in enumerate((1200, 2500, 4096, 3000), 1):
+        if words == 4096:
+            ids, vals = big, rng.uniform(0.01, 1.0, len(big))
+        else:
+            ids, vals = synth.make_kfdb_query(rng, sc, rng.uniform(10, n - 10), words=words)
+        assert len(ids) > 1024
+        a, b = g.detect_relocalization(f, ids, vals), o.detect_relocalization(f, ids, vals)
+        assert list(a) == list(b) and len(a) > 0, f
+        conn = sc.covis[int(rng.integers(0, n))]
+        a, b = g.detect_loop(100 + f, ids, vals, conn, 0.0), o.detect_loop(100 + f, ids, vals, conn, 0.0)
+        assert list(a) == list(b), f
+    assert states(g, n + 4) == states(o, n + 4)
