@@ -407,8 +407,9 @@ int rsc_kfdb_detect_loop(rsc_kfdb* db, uint64_t kf_id, int n_words, const uint32
  * mnRelocWords}, s[2] = {mLoopScore, mRelocScore}. */
 int rsc_kfdb_state(rsc_kfdb* db, int kf, uint64_t* q, int32_t* w, float* s);
 
-/* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP refine launch, [job < 64][8]:
- * entry, compaction, control points, MtM, eigen, betas, check, exit. */
+/* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP refine launch, [job < 64][12]:
+ * entry, compaction, control points, MtM, eigen, betas, check, exit, then inside the eigen phase:
+ * tridiagonal, Q accumulated, QR chase, eigenvectors (zeros unless built with RSC_REFINE_STAMPS=1). */
 int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out);
 /* Diagnostic: wall-clock (100 MHz) ticks of the last PoseOptimization launch, [frame < 64][8]:
  * fused passes (ticks), number of passes + (their active edges << 24), re-classification, whole kernel,

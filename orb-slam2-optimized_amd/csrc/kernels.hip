@@ -19,6 +19,22 @@
 #include "rsc_core.h"
 #include "rsc_epnp.h"
 #include "rsc_sim3.h"
+
+// Diagnostic phase stamps of the refine kernel (rsc_diag_refine_phase_stamps), compiled in only with
+// RSC_REFINE_STAMPS=1: [job][0..7] = entry, compaction, control points, MtM, eigen, betas, check,
+// exit; [8..11] inside the eigen phase = scaled + tridiagonal, Q accumulated, QR chase, eigenvectors.
+#ifndef RSC_REFINE_STAMPS
+#define RSC_REFINE_STAMPS 0
+#endif
+namespace rsc {
+__device__ uint64_t g_refine_stamps[64][12];
+}
+#if RSC_REFINE_STAMPS
+#define RSC_EIG_PHASE(k)                                                                               \
+    do {                                                                                               \
+        if (blockIdx.x < 64 && threadIdx.x == 0) ::rsc::g_refine_stamps[blockIdx.x][8 + (k)] = wall_clock64(); \
+    } while (0)
+#endif
 #include "rsc_quad.h"
 #include "rsc_math.h"
 #include "rsc_kernels.h"
@@ -209,11 +225,8 @@ __device__ __forceinline__ double wave_ordered_sum(int count, double* buf, bool 
     return s;
 }
 
-// Diagnostic phase stamps of the refine kernel (wall clock, 100 MHz): job 0..63 of the last
-// launch, [job][0..7] = entry, compaction, control points, MtM, eigen, betas, check, exit.
-__device__ uint64_t g_refine_stamps[64][8];
 __device__ __forceinline__ void refine_stamp(int slot) {
-    if (blockIdx.x < 64 && threadIdx.x == 0) g_refine_stamps[blockIdx.x][slot] = wall_clock64();
+    if (RSC_REFINE_STAMPS && blockIdx.x < 64 && threadIdx.x == 0) g_refine_stamps[blockIdx.x][slot] = wall_clock64();
 }
 
 __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs, const RefineJob& J) {
@@ -368,20 +381,14 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
     }
     __syncthreads();
     refine_stamp(3);
-    // 4. 12x12 eigenvectors (lanes 0..kRefineEigLanes-1 of wave 0 as one lane group,
-    // group_eig12_ev4), then L_6x10 and rho (single lane).  The MtM lower triangle in the slab is
-    // the group's T region; wbuf the E scratch.  The eigenvector columns 0..3 go back to slab
-    // columns 0..3 (SlabView::ev).
-    if (tid < kRefineEigLanes) {
-        constexpr int L = kRefineEigLanes;
-        double ev[12 / L][4];
-        group_eig12_ev4<L>(slab, &wbuf[0][0], tid, [] {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }, ev);
-        RSC_UNROLL for (int j = 0; j < 12 / L; ++j)
-            RSC_UNROLL for (int c = 0; c < 4; ++c) slab[(L * j + tid) * 12 + c] = ev[j][c];
+    // 4. 12x12 eigenvectors (rows_eig12_ev4: Householder phases on lanes 0..kRefineEigLanes-1 of
+    // wave 0 as one lane group, the QR chase on lanes 0..11 with one row of Q in each lane's VGPRs),
+    // then L_6x10 and rho (single lane).  The MtM lower triangle in the slab is the group's T region;
+    // wbuf the E scratch.  The eigenvector columns 0..3 go back to slab columns 0..3 (SlabView::ev).
+    if (wave == 0) {
+        double ev[4];
+        rows_eig12_ev4<kRefineEigLanes>(slab, &wbuf[0][0], lane, [] { wave_lds_sync(); }, ev);
+        if (lane < 12) RSC_UNROLL for (int c = 0; c < 4; ++c) slab[lane * 12 + c] = ev[c];
     }
     __syncthreads();
     if (tid == 0) {
@@ -850,7 +857,7 @@ hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchPr
 }
 
 hipError_t read_refine_stamps(uint64_t* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_refine_stamps), sizeof(uint64_t) * 64 * 8, 0, hipMemcpyDeviceToHost);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_refine_stamps), sizeof(uint64_t) * 64 * 12, 0, hipMemcpyDeviceToHost);
 }
 
 hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, hipStream_t st) {

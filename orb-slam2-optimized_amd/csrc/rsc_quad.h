@@ -21,6 +21,12 @@
 #include "rsc_epnp.h"
 #include "rsc_kernels.h"
 
+#ifndef RSC_EIG_PHASE
+#define RSC_EIG_PHASE(k) \
+    do {                 \
+    } while (0)
+#endif
+
 namespace rsc {
 
 constexpr int kQuadT = 144;  // MtM lower triangle, then the Q transpose
@@ -262,6 +268,7 @@ __device__ __forceinline__ void group_eig12_ev4(double* T, double* E, int q, Syn
         group_tridiag<L>(A, q, E, diag, sub, hC);
     }
     sync();
+    RSC_EIG_PHASE(0);
     {
         double Qc[RJ][12];
         group_accumulate<L>(Qc, q, E, hC);
@@ -269,9 +276,11 @@ __device__ __forceinline__ void group_eig12_ev4(double* T, double* E, int q, Syn
             RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + L * j + q] = Qc[j][r];
     }
     sync();
+    RSC_EIG_PHASE(1);
     GroupLdsRows<L> qapply{T, q};
     int perm[12];
     tridiag_qr<double, 12>(diag, sub, qapply, perm);
+    RSC_EIG_PHASE(2);
     RSC_UNROLL for (int j = 0; j < RJ; ++j) {
         const double* row = T + (L * j + q) * 12;
         double Qr[12];
@@ -282,6 +291,74 @@ __device__ __forceinline__ void group_eig12_ev4(double* T, double* E, int q, Syn
             ev[j][c] = x;
         }
     }
+    RSC_EIG_PHASE(3);
+}
+
+// Q = Q * G on columns k, k+1 of one row held in VGPRs (tridiag_qr's qapply contract).
+struct RegRowQ {
+    double (&row)[12];
+    RSC_HD void operator()(int k, double c, double s, bool apply) {
+        const double x = row[k], y = row[k + 1];
+        row[k] = apply ? c * x - s * y : x;
+        row[k + 1] = apply ? s * x + c * y : y;
+    }
+};
+
+// The Refine's 12x12 eigenvectors (one problem per workgroup): phases B-C (scale, Householder
+// tridiagonalisation, Q accumulation) on lanes 0..L-1 of the calling wave exactly as
+// group_eig12_ev4, then the implicit-QR chase on lanes 0..11, lane r holding row r of Q in VGPRs: the
+// chase is computed redundantly (identical values) and each lane rotates its own row — no LDS round
+// trip and no Q-row traffic in the rotation chain, which is what bounds one lone problem.  T: the
+// 144-double LDS region (MtM lower triangle on entry, Q after phase C); E: LDS scratch of at least
+// 90 doubles; sync(): an LDS visibility point of the wave.  Lanes 0..11 return the four eigenvector
+// entries of their row, bit-identical to group_eig12_ev4.
+template <int L, class Sync>
+__device__ __forceinline__ void rows_eig12_ev4(double* T, double* E, int lane, Sync sync, double (&ev)[4]) {
+    constexpr int RJ = 12 / L;
+    constexpr int kDiag = 64, kSub = 76;  // diag / sub hand-off in E, after the Householder vectors
+    if (lane < L) {
+        double diag[12], sub[11], hC[11];
+        {
+            double A[RJ][12];
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                const int R = L * j + lane;
+                RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = T[(R >= c) ? R * 12 + c : c * 12 + R];
+            }
+            const double scale = group_scale<L>(A, lane);
+            RSC_UNROLL for (int j = 0; j < RJ; ++j)
+                RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = A[j][c] / scale;
+            sync();  // every lane has read T before phase C overwrites it
+            group_tridiag<L>(A, lane, E, diag, sub, hC);
+        }
+        sync();
+        RSC_EIG_PHASE(0);
+        double Qc[RJ][12];
+        group_accumulate<L>(Qc, lane, E, hC);
+        RSC_UNROLL for (int j = 0; j < RJ; ++j)
+            RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + L * j + lane] = Qc[j][r];
+        if (lane == 0) {
+            RSC_UNROLL for (int i = 0; i < 12; ++i) E[kDiag + i] = diag[i];
+            RSC_UNROLL for (int i = 0; i < 11; ++i) E[kSub + i] = sub[i];
+        }
+    }
+    sync();
+    RSC_EIG_PHASE(1);
+    if (lane < 12) {
+        double diag[12], sub[11], row[12];
+        RSC_UNROLL for (int i = 0; i < 12; ++i) diag[i] = E[kDiag + i];
+        RSC_UNROLL for (int i = 0; i < 11; ++i) sub[i] = E[kSub + i];
+        RSC_UNROLL for (int c = 0; c < 12; ++c) row[c] = T[lane * 12 + c];
+        RegRowQ qapply{row};
+        int perm[12];
+        tridiag_qr<double, 12>(diag, sub, qapply, perm);
+        RSC_EIG_PHASE(2);
+        RSC_UNROLL for (int c = 0; c < 4; ++c) {
+            double x = row[0];
+            RSC_UNROLL for (int p = 1; p < 12; ++p) x = (perm[c] == p) ? row[p] : x;
+            ev[c] = x;
+        }
+    }
+    RSC_EIG_PHASE(3);
 }
 
 // Kernel 1 of the two-kernel hypothesis solve: sample, control points, alphas, MtM, and the 12x12
