@@ -57,7 +57,9 @@ int rsc_diag_host_timing(rsc_context* ctx, double out[4]);
 int rsc_context_enable_timing(rsc_context* ctx, int enable);
 /* Self-test of the device libm restatement (rsc_math.h, used by Sim3 angles, MLPnP, SearchBySim3):
  * out[i] = f(x[i]) computed ON THE GPU, f = 0 sin, 1 cos, 2 acos, 3 cbrt, 4 log, 5 logf
- * ((float)x[i] in, float result widened).  Host pointers, n >= 0.  Tests compare it with glibc. */
+ * ((float)x[i] in, float result widened); and the eigen-solver chase's short-chain forms
+ * (rsc_core.h): 6 sqrt for x in [1,4), 7 1/x for |x| in [1,2), 8 / 9 make_givens(x[i],
+ * x[(i+n/2)%n]) c / s.  Host pointers, n >= 0.  Tests compare with glibc / IEEE numpy. */
 int rsc_selftest_math(rsc_context* ctx, int fn, const double* x, int n, double* out);
 
 /* ---- PnPsolver (include/PnPsolver.hpp:21-138, src/PnPsolver.cpp) ------------------------------ */
@@ -407,9 +409,11 @@ int rsc_kfdb_detect_loop(rsc_kfdb* db, uint64_t kf_id, int n_words, const uint32
  * mnRelocWords}, s[2] = {mLoopScore, mRelocScore}. */
 int rsc_kfdb_state(rsc_kfdb* db, int kf, uint64_t* q, int32_t* w, float* s);
 
-/* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP refine launch, [job < 64][12]:
+/* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP refine launch, [job < 64][24]:
  * entry, compaction, control points, MtM, eigen, betas, check, exit, then inside the eigen phase:
- * tridiagonal, Q accumulated, QR chase, eigenvectors (zeros unless built with RSC_REFINE_STAMPS=1). */
+ * tridiagonal, Q accumulated, QR chase, eigenvectors, then [12 + 4w + j] inside the betas phase of
+ * wave w: betas + Gauss-Newton, pc0 sum, M sum + Horn, error sum (zeros unless built with
+ * RSC_REFINE_STAMPS=1). */
 int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out);
 /* Diagnostic: wall-clock (100 MHz) ticks of the last PoseOptimization launch, [frame < 64][8]:
  * fused passes (ticks), number of passes + (their active edges << 24), re-classification, whole kernel,

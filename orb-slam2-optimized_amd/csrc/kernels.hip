@@ -22,12 +22,14 @@
 
 // Diagnostic phase stamps of the refine kernel (rsc_diag_refine_phase_stamps), compiled in only with
 // RSC_REFINE_STAMPS=1: [job][0..7] = entry, compaction, control points, MtM, eigen, betas, check,
-// exit; [8..11] inside the eigen phase = scaled + tridiagonal, Q accumulated, QR chase, eigenvectors.
+// exit; [8..11] inside the eigen phase = scaled + tridiagonal, Q accumulated, QR chase, eigenvectors;
+// [12 + 4w + j] inside the betas phase, wave w (approximation w + 1): j = 0 betas + Gauss-Newton + ccs,
+// 1 pc0 sum, 2 M sum + Horn, 3 reprojection-error sum.
 #ifndef RSC_REFINE_STAMPS
 #define RSC_REFINE_STAMPS 0
 #endif
 namespace rsc {
-__device__ uint64_t g_refine_stamps[64][12];
+__device__ uint64_t g_refine_stamps[64][24];
 }
 #if RSC_REFINE_STAMPS
 #define RSC_EIG_PHASE(k)                                                                               \
@@ -228,6 +230,10 @@ __device__ __forceinline__ double wave_ordered_sum(int count, double* buf, bool 
 __device__ __forceinline__ void refine_stamp(int slot) {
     if (RSC_REFINE_STAMPS && blockIdx.x < 64 && threadIdx.x == 0) g_refine_stamps[blockIdx.x][slot] = wall_clock64();
 }
+__device__ __forceinline__ void refine_wave_stamp(int wave, int j) {
+    if (RSC_REFINE_STAMPS && blockIdx.x < 64 && (threadIdx.x & 63) == 0)
+        g_refine_stamps[blockIdx.x][12 + 4 * wave + j] = wall_clock64();
+}
 
 __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs, const RefineJob& J) {
     __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles];
@@ -420,6 +426,7 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
                 RSC_UNROLL for (int c = 0; c < 3; ++c) ccs_sh[wave][3 * i + c] = ccs[i][c];
         }
         wave_lds_sync();
+        refine_wave_stamp(wave, 0);
         double ccs[4][3];
         RSC_UNROLL for (int i = 0; i < 4; ++i)
             RSC_UNROLL for (int c = 0; c < 3; ++c) ccs[i][c] = ccs_sh[wave][3 * i + c];
@@ -432,6 +439,7 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
         __shared__ double pc0_sh[3][3];
         if (lane < 3) pc0_sh[wave][lane] = ps / nr;
         wave_lds_sync();
+        refine_wave_stamp(wave, 1);
         const double pc0[3] = {pc0_sh[wave][0], pc0_sh[wave][1], pc0_sh[wave][2]};
         const double ms = wave_ordered_sum<9>(nr, buf, true, [&](int i, double (&t)[9]) {
             const double al4[4] = {als[4 * i], als[4 * i + 1], als[4 * i + 2], als[4 * i + 3]};
@@ -453,6 +461,7 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
             RSC_UNROLL for (int k = 0; k < 3; ++k) rt_sh[wave][9 + k] = t[k];
         }
         wave_lds_sync();
+        refine_wave_stamp(wave, 2);
         double R[3][3], t[3];
         RSC_UNROLL for (int k = 0; k < 9; ++k) R[k / 3][k % 3] = rt_sh[wave][k];
         RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = rt_sh[wave][9 + k];
@@ -463,6 +472,7 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
             RSC_UNROLL for (int k = 0; k < 12; ++k) res_sh[wave][k] = rt_sh[wave][k];
             res_sh[wave][12] = es / nr;
         }
+        refine_wave_stamp(wave, 3);
     }
     __syncthreads();
     refine_stamp(5);
@@ -795,7 +805,17 @@ __global__ __launch_bounds__(256) void selftest_math_kernel(int fn, const double
         case 2: r = dm::acos(v); break;
         case 3: r = dm::cbrt(v); break;
         case 4: r = dm::log(v); break;
-        default: r = (double)dm::logf((float)v); break;
+        case 5: r = (double)dm::logf((float)v); break;
+        // the chase's short-chain IEEE forms (rsc_core.h) and make_givens built from them;
+        // make_givens pairs x[i] with x[(i + n/2) % n]
+        case 6: r = sqrt_unit(v); break;
+        case 7: r = recip_unit(v); break;
+        default: {
+            double c, s;
+            make_givens(v, x[(i + n / 2) % n], c, s);
+            r = fn == 8 ? c : s;
+            break;
+        }
     }
     out[i] = r;
 }
@@ -839,7 +859,7 @@ hipError_t launch_upload16(const void* host_src, void* dev_dst, size_t n16, hipS
 }
 
 hipError_t launch_selftest_math(int fn, const double* x, int n, double* out, hipStream_t st) {
-    if (fn < 0 || fn > 5 || n <= 0) return hipErrorInvalidValue;
+    if (fn < 0 || fn > 9 || n <= 0) return hipErrorInvalidValue;
     selftest_math_kernel<<<(n + 255) / 256, 256, 0, st>>>(fn, x, n, out);
     return hipGetLastError();
 }
@@ -857,7 +877,7 @@ hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchPr
 }
 
 hipError_t read_refine_stamps(uint64_t* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_refine_stamps), sizeof(uint64_t) * 64 * 12, 0, hipMemcpyDeviceToHost);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_refine_stamps), sizeof(uint64_t) * 64 * 24, 0, hipMemcpyDeviceToHost);
 }
 
 hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, hipStream_t st) {

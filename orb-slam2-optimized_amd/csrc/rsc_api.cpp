@@ -1053,7 +1053,7 @@ int rsc_context_enable_timing(rsc_context* C, int enable) {
 }
 
 int rsc_selftest_math(rsc_context* C, int fn, const double* x, int n, double* out) {
-    if (!C || fn < 0 || fn > 5 || n < 0 || (n > 0 && (!x || !out))) return RSC_ERR_ARG;
+    if (!C || fn < 0 || fn > 9 || n < 0 || (n > 0 && (!x || !out))) return RSC_ERR_ARG;
     if (n == 0) return RSC_OK;
     RSC_HIP(hipSetDevice(C->device));
     double* d = nullptr;

@@ -50,6 +50,45 @@ template <> struct lim<float> {
 };
 
 RSC_HD double rsqrt_(double x) { return sqrt(x); }
+
+// sqrt(x) for x in [1, 4) and 1/u for |u| in [1, 2), correctly rounded, with shorter chains (device).
+// The compiler's IEEE expansions add range handling around the core: sqrt scales x below 2^-767
+// (v_cmp -> s_cselect -> v_ldexp, a VALU-SALU-VALU round trip) and fixes up +-0 / inf after it;
+// 1/u pre-scales with v_div_scale and post-fixes with v_div_fixup.  In these ranges every one of
+// those steps returns its input (and v_div_fmas is a plain fma), so the core instructions issued
+// directly give the same bits with 3-4 fewer dependent steps each: make_givens' 1 + t^2 in [1, 2]
+// and sqrt(1 + t^2) in [1, sqrt 2] are exactly these cases.  tests/test_gpu_math.py checks both
+// against IEEE numpy over their ranges.
+RSC_HD double sqrt_unit(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+#else
+    return sqrt(x);
+#endif
+}
+RSC_HD double recip_unit(double u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(u);
+    double e = __builtin_fma(-u, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-u, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-u, r, 1.0);  // q = 1 * r = r: the expansion's residual and correction
+    return __builtin_fma(e, r, r);
+#else
+    return 1.0 / u;
+#endif
+}
+RSC_HD float sqrt_unit(float x) { return sqrtf(x); }
+RSC_HD float recip_unit(float u) { return 1.0f / u; }
 RSC_HD float rsqrt_(float x) { return sqrtf(x); }
 RSC_HD double rabs(double x) { return fabs(x); }
 RSC_HD float rabs(float x) { return fabsf(x); }
@@ -73,25 +112,29 @@ template <typename S> RSC_HD S eig_hypot(S x, S y) {
     const S ax = rabs(x), ay = rabs(y);
     const bool gx = ax > ay;
     const S p = gx ? ax : ay;
-    const S qp = (gx ? ay : ax) / p;
-    const S r = p * rsqrt_(S(1) + qp * qp);
+    const S qp = (gx ? ay : ax) / p;  // in [0, 1] (p == 0 is overridden below)
+    const S r = p * sqrt_unit(S(1) + qp * qp);
     return (p == S(0)) ? S(0) : r;
 }
 
 // JacobiRotation::makeGivens (real case).
+// |t| <= 1, so 1 + t^2 is in [1, 2] and |u| in [1, sqrt 2] (the *_unit forms above).  The two special
+// cases (p == 0; q == 0, which wins) are one select on values computed from p and q alone, so the
+// chain after 1/u is a multiply and two selects.
 template <typename S> RSC_HD void make_givens(S p, S q, S& c, S& s) {
     const bool big = rabs(p) > rabs(q);
     const S t = (big ? q : p) / (big ? p : q);
-    S u = rsqrt_(S(1) + t * t);
+    S u = sqrt_unit(S(1) + t * t);
     if ((big ? p : q) < S(0)) u = -u;
-    const S r = S(1) / u;  // big: c = 1/u, s = -t*c;  else: s = -1/u (= -(1/u)), c = -t*s
+    const S r = recip_unit(u);  // big: c = 1/u, s = -t*c;  else: s = -1/u (= -(1/u)), c = -t*s
     const S sb = -r;
-    S cc = big ? r : (-t) * sb;
-    S ss = big ? (-t) * r : sb;
-    if (p == S(0)) { cc = S(0); ss = (q < S(0)) ? S(1) : S(-1); }
-    if (q == S(0)) { cc = (p < S(0)) ? S(-1) : S(1); ss = S(0); }
-    c = cc;
-    s = ss;
+    const S cc = big ? r : (-t) * sb;
+    const S ss = big ? (-t) * r : sb;
+    const bool qz = q == S(0), sp = (p == S(0)) | qz;
+    const S c_sp = qz ? ((p < S(0)) ? S(-1) : S(1)) : S(0);
+    const S s_sp = qz ? S(0) : ((q < S(0)) ? S(1) : S(-1));
+    c = sp ? c_sp : cc;
+    s = sp ? s_sp : ss;
 }
 
 // Ascending selection sort of the eigenvalues (end of computeFromTridiagonal_impl): the same
@@ -140,50 +183,56 @@ RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, int (&per
     int end = n - 1, start = 0, iter = 0;
     const S considerAsZero = lim<S>::min();
     const S precision_inv = S(1) / lim<S>::eps();
+    // Branch-free sweep bookkeeping.  Each `if` of Eigen's loop (deflation test, end/start
+    // searches, shift cases, the chase's edge updates) compiled to a branch — a scalar branch when
+    // the group's values are uniform, an exec-mask region otherwise — and the sweep's ~100 branches
+    // cost more than its rotations (one 12x12 Refine chase: 156 rotations, 23 sweeps, 221 k shader
+    // clocks, 3x the make_givens chains; tools/eig_probe.hip).  Here every test is a value select on
+    // the same operands (same results, bit for bit); the only branches left are the loop exit and
+    // the chase's per-slot range guard, which skips slots outside [start, end).  Conditions are
+    // combined with the non-short-circuit & and | (a short-circuit || is a branch again).
     // Single-exit loop (Eigen's two `break`s folded into `run`): with several exits the CFG
     // structurizer nests the loop and every lane pays for the extra control flow.
     bool run = true;
     while (run) {
+        // for (i = start; i < end; ++i): |sub| < considerAsZero, or (sub/eps)^2 <= |d_i| + |d_i+1|
         RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
-            if (i >= start && i < end) {
-                if (rabs(sub[i]) < considerAsZero) {
-                    sub[i] = S(0);
-                } else {
-                    const S scaled = precision_inv * sub[i];
-                    if (scaled * scaled <= (rabs(diag[i]) + rabs(diag[i + 1]))) sub[i] = S(0);
-                }
-            }
+            const S scaled = precision_inv * sub[i];
+            const bool z = (rabs(sub[i]) < considerAsZero) | (scaled * scaled <= (rabs(diag[i]) + rabs(diag[i + 1])));
+            sub[i] = (z & (i >= start) & (i < end)) ? S(0) : sub[i];
         }
-        RSC_UNROLL for (int i = n - 2; i >= 0; --i)
-            if (i == end - 1 && sub[i] == S(0)) end--;
+        // while (end > 0 && sub[end-1] == 0) end--;
+        RSC_UNROLL for (int i = n - 2; i >= 0; --i) end = ((i == end - 1) & (sub[i] == S(0))) ? i : end;
         run = end > 0;
-        if (run) {
-            iter++;
-            run = iter <= maxIterations * n;
-        }
+        iter = run ? iter + 1 : iter;
+        run = run & (iter <= maxIterations * n);
         if (!run) continue;
+        // start = end - 1; while (start > 0 && sub[start-1] != 0) start--;
         start = end - 1;
-        RSC_UNROLL for (int i = n - 2; i >= 0; --i)
-            if (i == start - 1 && sub[i] != S(0)) start--;
+        RSC_UNROLL for (int i = n - 2; i >= 0; --i) start = ((i == start - 1) & (sub[i] != S(0))) ? i : start;
         // ---- tridiagonal_qr_step(diag, sub, start, end) ----
         S dEm1 = S(0), dE = S(0), eE = S(0), dS = S(0), zS = S(0);
-        RSC_UNROLL for (int j = 1; j < n; ++j)
-            if (j == end) { dEm1 = diag[j - 1]; dE = diag[j]; eE = sub[j - 1]; }
-        RSC_UNROLL for (int j = 0; j < n - 1; ++j)
-            if (j == start) { dS = diag[j]; zS = sub[j]; }
-        S td = (dEm1 - dE) * S(0.5);
-        S e = eE;
-        S mu = dE;
-        if (td == S(0)) {
-            mu -= rabs(e);
-        } else {
-            S e2 = eE * eE;
-            S h = eig_hypot(td, e);
-            if (e2 == S(0))
-                mu -= (e / (td + (td > S(0) ? S(1) : S(-1)))) * (e / h);
-            else
-                mu -= e2 / (td + (td > S(0) ? h : -h));
+        RSC_UNROLL for (int j = 1; j < n; ++j) {
+            const bool m = j == end;
+            dEm1 = m ? diag[j - 1] : dEm1;
+            dE = m ? diag[j] : dE;
+            eE = m ? sub[j - 1] : eE;
         }
+        RSC_UNROLL for (int j = 0; j < n - 1; ++j) {
+            const bool m = j == start;
+            dS = m ? diag[j] : dS;
+            zS = m ? sub[j] : zS;
+        }
+        // Wilkinson shift; the three cases of Eigen are evaluated side by side and selected
+        // (td == 0: mu - |e|; e^2 underflows: the two-quotient form; otherwise e^2/(td +- h))
+        const S td = (dEm1 - dE) * S(0.5);
+        const S e = eE;
+        const S e2 = eE * eE;
+        const S h = eig_hypot(td, e);
+        const S mu_z = dE - rabs(e);
+        const S mu_u = dE - (e / (td + (td > S(0) ? S(1) : S(-1)))) * (e / h);
+        const S mu_n = dE - e2 / (td + (td > S(0) ? h : -h));
+        const S mu = (td == S(0)) ? mu_z : ((e2 == S(0)) ? mu_u : mu_n);
         S x = dS - mu;
         S z = zS;
         RSC_UNROLL for (int k = 0; k < n - 1; ++k) {
@@ -196,11 +245,12 @@ RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, int (&per
                 diag[k] = c * (c * diag[k] - s * sub[k]) - s * (c * sub[k] - s * diag[k + 1]);
                 diag[k + 1] = s * sdk + c * dkp1;
                 sub[k] = c * sdk - s * dkp1;
-                if (k > 0 && k > start) sub[k - 1] = c * sub[k - 1] - s * z;
+                if (k > 0) sub[k - 1] = (k > start) ? c * sub[k - 1] - s * z : sub[k - 1];
                 x = sub[k];
-                if (k < n - 2 && k < end - 1) {
-                    z = -s * sub[k + 1];
-                    sub[k + 1] = c * sub[k + 1];
+                if (k < n - 2) {
+                    const bool m = k < end - 1;
+                    z = m ? -s * sub[k + 1] : z;
+                    sub[k + 1] = m ? c * sub[k + 1] : sub[k + 1];
                 }
                 // Eigen skips identity rotations; qapply receives the flag and selects (a
                 // conditional call here gets tail-duplicated into the loop latch, which turns

@@ -442,7 +442,8 @@ class Context:
     def enable_timing(self, on: bool = True):
         _check(load_library().rsc_context_enable_timing(self.h, int(on)), "enable_timing")
 
-    MATH_FNS = {"sin": 0, "cos": 1, "acos": 2, "cbrt": 3, "log": 4, "logf": 5}
+    MATH_FNS = {"sin": 0, "cos": 1, "acos": 2, "cbrt": 3, "log": 4, "logf": 5, "sqrt_unit": 6, "recip_unit": 7,
+                "givens_c": 8, "givens_s": 9}
 
     def selftest_math(self, fn: str, x):
         """rsc_math.h evaluated on the GPU (f64 array in, f64 array out; logf: float in/out)."""

@@ -55,3 +55,55 @@ def test_device_libm_matches_host_restatement_and_glibc(name):
             assert abs(di - gi) <= math.ulp(np.float32(gi)) + 1e-300, (name, xi, di, gi)
         else:
             assert _ulp_close(di, gi, k), (name, xi, di, gi)
+
+
+# ---- the QR chase's short-chain forms (rsc_core.h sqrt_unit / recip_unit, and make_givens built
+# from them) against IEEE numpy, bit for bit ----
+
+def _givens_ieee(p, q):
+    """JacobiRotation::makeGivens (real case) with IEEE operations (numpy), as rsc_core.h."""
+    with np.errstate(all="ignore"):
+        big = np.abs(p) > np.abs(q)
+        t = np.where(big, q, p) / np.where(big, p, q)
+        u = np.sqrt(1.0 + t * t)
+        u = np.where(np.where(big, p, q) < 0, -u, u)
+        r = 1.0 / u
+        sb = -r
+        c = np.where(big, r, (-t) * sb)
+        s = np.where(big, (-t) * r, sb)
+        c = np.where(p == 0, 0.0, c)
+        s = np.where(p == 0, np.where(q < 0, 1.0, -1.0), s)
+        c = np.where(q == 0, np.where(p < 0, -1.0, 1.0), c)
+        s = np.where(q == 0, 0.0, s)
+    return c, s
+
+
+def _same_bits(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return (a.view(np.uint64) == b.view(np.uint64)) | (np.isnan(a) & np.isnan(b))
+
+
+@pytest.mark.parametrize("name", ["sqrt_unit", "recip_unit", "givens_c", "givens_s"])
+def test_chase_arithmetic_is_ieee(name):
+    rng = np.random.default_rng(11)
+    if name == "sqrt_unit":
+        x = np.concatenate([rng.uniform(1.0, 4.0, 300000), 1.0 + rng.uniform(0, 1, 100000) ** 2,
+                            [1.0, 2.0, 3.0, np.nextafter(4.0, 0), np.nextafter(1.0, 2), 2.0 - 2**-52]])
+        want = np.sqrt(x)
+    elif name == "recip_unit":
+        x = rng.uniform(1.0, 2.0, 300000) * rng.choice([-1.0, 1.0], 300000)
+        x = np.concatenate([x, [1.0, -1.0, np.nextafter(2.0, 0), -np.nextafter(2.0, 0), 2.0**0.5, -(2.0**0.5),
+                                np.nextafter(1.0, 2)]])
+        want = 1.0 / x
+    else:
+        n = 200000
+        mags = 10.0 ** rng.uniform(-300, 300, n) * rng.choice([-1.0, 1.0], n)
+        mid = rng.standard_normal(n) * 10.0 ** rng.integers(-20, 3, n)
+        special = np.array([0.0, -0.0, 1.0, -1.0, 5e-324, -5e-324, np.inf, -np.inf, np.nan, 1e-300, -1e-300] * 10)
+        x = np.concatenate([mags, mid, special])
+        x = x[rng.permutation(x.size)]
+        c, s = _givens_ieee(x, x[(np.arange(x.size) + x.size // 2) % x.size])
+        want = c if name == "givens_c" else s
+    dev = gpu_ctx().selftest_math(name, x)
+    bad = np.flatnonzero(~_same_bits(dev, want))
+    assert bad.size == 0, [(float(x[i]), float(dev[i]), float(want[i])) for i in bad[:8]]
