@@ -320,7 +320,10 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
         });
         if (lane < 6) buf[lane] = as;
         wave_lds_sync();
-        if (lane == 0) {
+        // the 3x3 eigensolver, control points and C^-1 on every lane of the wave (identical values
+        // and writes): a uniform chain runs with scalar branches, about twice as fast as the same
+        // chain on one lane under an exec mask (tools/eig_probe.hip refine_betas_like)
+        {
             double cws[4][3];
             cws[0][0] = c0; cws[0][1] = c1; cws[0][2] = c2;
             const double A[3][3] = {{buf[0], buf[1], buf[2]}, {buf[1], buf[3], buf[4]}, {buf[2], buf[4], buf[5]}};
@@ -397,7 +400,7 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
         if (lane < 12) RSC_UNROLL for (int c = 0; c < 4; ++c) slab[lane * 12 + c] = ev[c];
     }
     __syncthreads();
-    if (tid == 0) {
+    if (wave == 0) {  // every lane of wave 0, identical values and writes
         compute_L_6x10(SlabView{S});
         auto d2 = [&](int a, int b) {
             double x = cws_sh[3 * a] - cws_sh[3 * b], y = cws_sh[3 * a + 1] - cws_sh[3 * b + 1],
@@ -414,7 +417,7 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
     if (wave < 3) {
         const SlabView SV{S};
         __shared__ double ccs_sh[3][12];
-        if (lane == 0) {
+        {  // every lane of the wave (identical values and writes; see the control points above)
             double betas[4] = {0.0, 0.0, 0.0, 0.0};
             if (wave == 0) find_betas<1>(SV, betas);
             else if (wave == 1) find_betas<2>(SV, betas);
@@ -452,7 +455,7 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
         if (lane < 9) m_sh[wave][lane] = ms;
         wave_lds_sync();
         __shared__ double rt_sh[3][12];
-        if (lane == 0) {
+        {  // every lane of the wave, as above
             double M[3][3], R[3][3], t[3];
             RSC_UNROLL for (int r = 0; r < 3; ++r)
                 RSC_UNROLL for (int c = 0; c < 3; ++c) M[r][c] = m_sh[wave][3 * r + c];

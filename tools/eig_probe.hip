@@ -14,6 +14,7 @@
 #include <cmath>
 #include <vector>
 #include <random>
+#include <cstring>
 
 __device__ unsigned long long g_st[8][16];
 __device__ unsigned long long g_clk[8][16];
@@ -396,6 +397,80 @@ __global__ __launch_bounds__(64) void chase_stamped(const double* __restrict__ d
     out[lane] = a + perm[0];
 }
 
+
+// The Refine kernel's betas structure: 256 threads, the slab (eigenvectors, L, rho) in LDS read
+// through SlabView, lane 0 of waves 0..2 running find_betas<w+1> + gauss_newton (MODE 0) — or all 64
+// lanes of the wave running it redundantly (MODE 1).
+template <int MODE>
+__global__ __launch_bounds__(256) void refine_betas_like(const double* __restrict__ slab_in, double* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int e = tid; e < kSlabDoubles; e += 256) slab[e] = slab_in[e];
+    __syncthreads();
+    wstamp(wave, 0);
+    if (wave < 3) {
+        // MODE 2: the same slab through a base the compiler sees as lane-varying (an inline-asm VGPR
+        // zero), so the values read are divergent and data-dependent ifs stay selects / exec masks
+        int z = 0;
+        if (MODE == 2) asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        const SlabView SV{LaneMat{slab + z, 1}};
+        if (MODE >= 1 || lane == 0) {
+            double betas[4] = {0.0, 0.0, 0.0, 0.0};
+            if (wave == 0) find_betas<1>(SV, betas);
+            else if (wave == 1) find_betas<2>(SV, betas);
+            else find_betas<3>(SV, betas);
+            wstamp(wave, 1);
+            gauss_newton(SV, betas);
+            wstamp(wave, 2);
+            if (lane == 0) for (int k = 0; k < 4; ++k) out[wave * 4 + k] = betas[k];
+        }
+    }
+    __syncthreads();
+}
+
+
+// Which factor makes the Refine-shaped betas slow: (a) 64-thread workgroups, SlabView over a
+// shared slab (wave = blockIdx); (b) 256-thread workgroup, SplitView per lane (stride 64).
+__global__ __launch_bounds__(64) void slab_betas_64(const double* __restrict__ slab_in, double* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles];
+    const int lane = threadIdx.x, wave = blockIdx.x;
+    for (int e = lane; e < kSlabDoubles; e += 64) slab[e] = slab_in[e];
+    __syncthreads();
+    wstamp(wave, 0);
+    const SlabView SV{LaneMat{slab, 1}};
+    double betas[4] = {0.0, 0.0, 0.0, 0.0};
+    if (wave == 0) find_betas<1>(SV, betas);
+    else if (wave == 1) find_betas<2>(SV, betas);
+    else find_betas<3>(SV, betas);
+    wstamp(wave, 1);
+    gauss_newton(SV, betas);
+    wstamp(wave, 2);
+    if (lane == 0) for (int k = 0; k < 4; ++k) out[wave * 4 + k] = betas[k];
+}
+__global__ __launch_bounds__(256) void split_betas_256(const double* __restrict__ slab_in, double* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) double Lsh[3][66 * 64];
+    __shared__ double ev[48];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 48) ev[tid] = slab_in[(tid / 4) * 12 + tid % 4];
+    if (wave < 3) {
+        for (int q = 0; q < 66; ++q) Lsh[wave][q * 64 + lane] = slab_in[slab_free(q)];
+    }
+    __syncthreads();
+    wstamp(wave, 0);
+    if (wave < 3) {
+        const SplitView V{ev, Lsh[wave] + lane, 64};
+        double betas[4] = {0.0, 0.0, 0.0, 0.0};
+        if (wave == 0) find_betas<1>(V, betas);
+        else if (wave == 1) find_betas<2>(V, betas);
+        else find_betas<3>(V, betas);
+        wstamp(wave, 1);
+        gauss_newton(V, betas);
+        wstamp(wave, 2);
+        if (lane == 0) for (int k = 0; k < 4; ++k) out[wave * 4 + k] = betas[k];
+    }
+    __syncthreads();
+}
+
 // The betas kernel's cross-workgroup hand-off (stores, agent release, atomic, agent acquire, loads).
 __global__ __launch_bounds__(64) void fence_probe(double* buf, unsigned* ctr) {
     const int lane = threadIdx.x;
@@ -498,6 +573,16 @@ __global__ void setup_refine_hyp(double* pws, const double* us, double* als, int
         for (int c = 0; c < 4; ++c) hp->ev[r * 4 + c] = M[r * 12 + c];
     for (int i = 0; i < 4; ++i)
         for (int c = 0; c < 3; ++c) hp->cws[3 * i + c] = cws[i][c];
+    {
+        const SlabView SV{LaneMat{M, 1}};
+        compute_L_6x10(SV);
+        auto d2 = [&](int a, int b) {
+            double x = cws[a][0] - cws[b][0], y = cws[a][1] - cws[b][1], z = cws[a][2] - cws[b][2];
+            return x * x + y * y + z * z;
+        };
+        SV.rho(0) = d2(0, 1); SV.rho(1) = d2(0, 2); SV.rho(2) = d2(0, 3);
+        SV.rho(3) = d2(1, 2); SV.rho(4) = d2(1, 3); SV.rho(5) = d2(2, 3);
+    }
     for (int i = 0; i < 4; ++i) {
         for (int c = 0; c < 3; ++c) hp->pw[3 * i + c] = pws[3 * i + c];
         for (int c = 0; c < 2; ++c) hp->u[2 * i + c] = us[2 * i + c];
@@ -645,6 +730,34 @@ int main() {
         report("one 3-wave WG, apx 1", 0, 5, bph);
         report("one 3-wave WG, apx 2", 1, 5, bph);
         report("one 3-wave WG, apx 3", 2, 5, bph);
+        {
+            const char* rph[] = {"find_betas", "gauss_newton"};
+            double* slab_g = d_mtm + 21 * 160;
+            for (int rep = 0; rep < 3; ++rep) { refine_betas_like<0><<<1, 256>>>(slab_g, d_out + 3000); CK(hipDeviceSynchronize()); }
+            report("refine-like lane 0, w0", 0, 2, rph);
+            report("refine-like lane 0, w1", 1, 2, rph);
+            report("refine-like lane 0, w2", 2, 2, rph);
+            for (int rep = 0; rep < 3; ++rep) { refine_betas_like<1><<<1, 256>>>(slab_g, d_out + 3000); CK(hipDeviceSynchronize()); }
+            report("refine-like 64 lanes, w0", 0, 2, rph);
+            report("refine-like 64 lanes, w1", 1, 2, rph);
+            report("refine-like 64 lanes, w2", 2, 2, rph);
+            for (int rep = 0; rep < 3; ++rep) { refine_betas_like<2><<<1, 256>>>(slab_g, d_out + 3000); CK(hipDeviceSynchronize()); }
+            report("refine-like divergent, w0", 0, 2, rph);
+            report("refine-like divergent, w1", 1, 2, rph);
+            report("refine-like divergent, w2", 2, 2, rph);
+            for (int rep = 0; rep < 3; ++rep) { slab_betas_64<<<3, 64>>>(slab_g, d_out + 3000); CK(hipDeviceSynchronize()); }
+            report("slab view, 64-thread WGs, w0", 0, 2, rph);
+            report("slab view, 64-thread WGs, w2", 2, 2, rph);
+            for (int rep = 0; rep < 3; ++rep) { split_betas_256<<<1, 256>>>(slab_g, d_out + 3000); CK(hipDeviceSynchronize()); }
+            report("split view, 256-thread WG, w0", 0, 2, rph);
+            report("split view, 256-thread WG, w2", 2, 2, rph);
+            double bo[12], bo2[12];
+            CK(hipMemcpy(bo, d_out + 3000, sizeof(bo), hipMemcpyDeviceToHost));
+            refine_betas_like<0><<<1, 256>>>(slab_g, d_out + 3000);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(bo2, d_out + 3000, sizeof(bo2), hipMemcpyDeviceToHost));
+            printf("    divergent-form betas bit-equal to lane-0 form: %s\n", memcmp(bo, bo2, sizeof(bo)) == 0 ? "yes" : "NO");
+        }
         // instruction-cache effect: the same launch right after other large kernels (cold) and
         // then again (warm)
         for (int rep = 0; rep < 2; ++rep) {
