@@ -741,40 +741,39 @@ RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6]
             RSC_UNROLL for (int q = 0; q < p; ++q) {
                 double pt = precision * maxDiag;
                 double threshold = (considerAsZero < pt) ? pt : considerAsZero;
-                if (rabs(W[p][q]) > threshold || rabs(W[q][p]) > threshold) {
+                if ((rabs(W[p][q]) > threshold) | (rabs(W[q][p]) > threshold)) {
                     finished = false;
+                    // real_2x2_jacobi_svd.  Its inner ifs are value selects on the same operands
+                    // (a divergent if is an exec-mask region, a uniform one a scalar branch; both cost
+                    // more than the selects, tools/eig_probe.hip), and |tt| <= 1 puts tt^2 + 1 in
+                    // [1, 2] and its root in [1, sqrt 2] (the short-chain *_unit forms).
                     double m00 = W[p][p], m01 = W[p][q], m10 = W[q][p], m11 = W[q][q];
-                    double c1, s1;
-                    double t = m00 + m11;
-                    double d = m10 - m01;
-                    if (rabs(d) < considerAsZero) {
-                        s1 = 0.0; c1 = 1.0;
-                    } else {
-                        double u = t / d;
-                        double tmp = sqrt(1.0 + u * u);
-                        s1 = 1.0 / tmp;
-                        c1 = u / tmp;
-                    }
-                    if (!(c1 == 1.0 && s1 == 0.0)) {
-                        double x0 = m00, y0 = m10, x1 = m01, y1 = m11;
-                        m00 = c1 * x0 + s1 * y0; m10 = -s1 * x0 + c1 * y0;
-                        m01 = c1 * x1 + s1 * y1; m11 = -s1 * x1 + c1 * y1;
+                    const double t = m00 + m11;
+                    const double d = m10 - m01;
+                    const bool dz = rabs(d) < considerAsZero;
+                    const double u = t / d;
+                    const double tmp = sqrt(1.0 + u * u);
+                    const double s1 = dz ? 0.0 : 1.0 / tmp;
+                    const double c1 = dz ? 1.0 : u / tmp;
+                    {
+                        const bool rot = !((c1 == 1.0) & (s1 == 0.0));
+                        const double x0 = m00, y0 = m10, x1 = m01, y1 = m11;
+                        m00 = rot ? c1 * x0 + s1 * y0 : x0;
+                        m10 = rot ? -s1 * x0 + c1 * y0 : y0;
+                        m01 = rot ? c1 * x1 + s1 * y1 : x1;
+                        m11 = rot ? -s1 * x1 + c1 * y1 : y1;
                     }
                     double cr, sr;
                     {
-                        double deno = 2.0 * rabs(m01);
-                        if (deno < considerAsZero) {
-                            cr = 1.0; sr = 0.0;
-                        } else {
-                            double tau = (m00 - m11) / deno;
-                            double w = sqrt(tau * tau + 1.0);
-                            double tt;
-                            if (tau > 0.0) tt = 1.0 / (tau + w); else tt = 1.0 / (tau - w);
-                            double sign_t = tt > 0.0 ? 1.0 : -1.0;
-                            double nn = 1.0 / sqrt(tt * tt + 1.0);
-                            sr = -sign_t * (m01 / rabs(m01)) * rabs(tt) * nn;
-                            cr = nn;
-                        }
+                        const double deno = 2.0 * rabs(m01);
+                        const bool nz = deno < considerAsZero;
+                        const double tau = (m00 - m11) / deno;
+                        const double w = sqrt(tau * tau + 1.0);
+                        const double tt = 1.0 / (tau > 0.0 ? tau + w : tau - w);
+                        const double sign_t = tt > 0.0 ? 1.0 : -1.0;
+                        const double nn = recip_unit(sqrt_unit(tt * tt + 1.0));
+                        sr = nz ? 0.0 : -sign_t * (m01 / rabs(m01)) * rabs(tt) * nn;
+                        cr = nz ? 1.0 : nn;
                     }
                     double crt = cr, srt = -sr;
                     double cl = c1 * crt - s1 * srt;
