@@ -43,7 +43,8 @@ __device__ bool tridiag_qr_st(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, in
     // cost more than its rotations (one 12x12 Refine chase: 156 rotations, 23 sweeps, 221 k shader
     // clocks, 3x the make_givens chains; tools/eig_probe.hip).  Here every test is a value select on
     // the same operands (same results, bit for bit); the only branches left are the loop exit and
-    // the chase's per-slot range guard, which skips slots outside [start, end).
+    // the chase's per-slot range guard, which skips slots outside [start, end).  Conditions are
+    // combined with the non-short-circuit & and | (a short-circuit || is a branch again).
     // Single-exit loop (Eigen's two `break`s folded into `run`): with several exits the CFG
     // structurizer nests the loop and every lane pays for the extra control flow.
     bool run = true;
@@ -55,15 +56,21 @@ __device__ bool tridiag_qr_st(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, in
             const bool z = (rabs(sub[i]) < considerAsZero) | (scaled * scaled <= (rabs(diag[i]) + rabs(diag[i + 1])));
             sub[i] = (z & (i >= start) & (i < end)) ? S(0) : sub[i];
         }
-        // while (end > 0 && sub[end-1] == 0) end--;
-        RSC_UNROLL for (int i = n - 2; i >= 0; --i) end = ((i == end - 1) & (sub[i] == S(0))) ? i : end;
+        // The two searches on a bit mask of the nonzero sub-diagonal entries (a find-last-set instead
+        // of an 11-step select chain each):
+        // while (end > 0 && sub[end-1] == 0) end--;  ->  end = 1 + last nonzero index below end, or 0
+        unsigned nz = 0u;
+        RSC_UNROLL for (int i = 0; i < n - 1; ++i) nz |= (sub[i] != S(0)) ? (1u << i) : 0u;
+        const unsigned live = nz & ((1u << end) - 1u);
+        end = live ? 32 - __builtin_clz(live) : 0;
         run = end > 0;
         iter = run ? iter + 1 : iter;
         run = run & (iter <= maxIterations * n);
         if (!run) continue;
         // start = end - 1; while (start > 0 && sub[start-1] != 0) start--;
-        start = end - 1;
-        RSC_UNROLL for (int i = n - 2; i >= 0; --i) start = ((i == start - 1) & (sub[i] != S(0))) ? i : start;
+        //   ->  start = 1 + last zero index below end - 1, or 0
+        const unsigned zero = ~nz & ((1u << (end - 1)) - 1u);
+        start = zero ? 32 - __builtin_clz(zero) : 0;
         // ---- tridiagonal_qr_step(diag, sub, start, end) ----
         S dEm1 = S(0), dE = S(0), eE = S(0), dS = S(0), zS = S(0);
         RSC_UNROLL for (int j = 1; j < n; ++j) {
