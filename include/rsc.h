@@ -59,7 +59,9 @@ int rsc_context_enable_timing(rsc_context* ctx, int enable);
  * out[i] = f(x[i]) computed ON THE GPU, f = 0 sin, 1 cos, 2 acos, 3 cbrt, 4 log, 5 logf
  * ((float)x[i] in, float result widened); and the eigen-solver chase's short-chain forms
  * (rsc_core.h): 6 sqrt for x in [1,4), 7 1/x for |x| in [1,2), 8 / 9 make_givens(x[i],
- * x[(i+n/2)%n]) c / s.  Host pointers, n >= 0.  Tests compare with glibc / IEEE numpy. */
+ * x[(i+n/2)%n]) c / s; 10 qr_solve_6x4 (PnPsolver.cpp:693-796) on records of 34 doubles
+ * (A[6][4] row-major, b[6], previous X[4]) -> X in out[0..3], 1/0 success in out[4] of each record
+ * (n a multiple of 34).  Host pointers, n >= 0.  Tests compare with glibc / IEEE numpy / the oracle. */
 int rsc_selftest_math(rsc_context* ctx, int fn, const double* x, int n, double* out);
 
 /* ---- PnPsolver (include/PnPsolver.hpp:21-138, src/PnPsolver.cpp) ------------------------------ */
@@ -409,19 +411,21 @@ int rsc_kfdb_detect_loop(rsc_kfdb* db, uint64_t kf_id, int n_words, const uint32
  * mnRelocWords}, s[2] = {mLoopScore, mRelocScore}. */
 int rsc_kfdb_state(rsc_kfdb* db, int kf, uint64_t* q, int32_t* w, float* s);
 
-/* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP refine launch, [job < 64][24]:
+/* Diagnostics below: `cap` = number of uint64 slots at `out`; RSC_ERR_ARG when it is smaller than
+ * the layout (64*24, 64*8, 4096*4 and at most 64*96 words).
+ * Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP refine launch, [job < 64][24]:
  * entry, compaction, control points, MtM, eigen, betas, check, exit, then inside the eigen phase:
  * tridiagonal, Q accumulated, QR chase, eigenvectors, then [12 + 4w + j] inside the betas phase of
  * wave w: betas + Gauss-Newton, pc0 sum, M sum + Horn, error sum (zeros unless built with
  * RSC_REFINE_STAMPS=1). */
-int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out);
+int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
 /* Diagnostic: wall-clock (100 MHz) ticks of the last PoseOptimization launch, [frame < 64][8]:
  * fused passes (ticks), number of passes + (their active edges << 24), re-classification, whole kernel,
  * 4 unused. */
-int rsc_diag_poseopt_phases(rsc_context* ctx, uint64_t* out);
+int rsc_diag_poseopt_phases(rsc_context* ctx, uint64_t* out, int cap);
 /* Diagnostic: wall clock (100 MHz) of KeyFrameDatabase slots 0..4095 in the last count launch,
  * [slot][4] = entry, staged, counted, exit (zeros unless built with RSC_KFDB_STAMPS=1). */
-int rsc_diag_kfdb_stamps(rsc_context* ctx, uint64_t* out);
+int rsc_diag_kfdb_stamps(rsc_context* ctx, uint64_t* out, int cap);
 /* Diagnostic: wall-clock (100 MHz) phase stamps of the last SearchByBoW launch, [pair < 64][96]. */
 int rsc_diag_bow_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
 

@@ -536,6 +536,16 @@ void ora_loop_events_batch(int n_events, const int32_t* ev_begin, const int32_t*
         });
 }
 
+// qr_solve (PnPsolver.cpp:693-796) on one 6x4 system: A row-major (modified in place as the
+// reference does), b, X = the previous X (kept on the singular bail-out).  Returns 1 / 0 (singular).
+int ora_qr_solve(double* A, double* b, double* X) {
+    double Am[6][4];
+    for (int i = 0; i < 6; ++i) for (int j = 0; j < 4; ++j) Am[i][j] = A[4 * i + j];
+    const bool ok = rsc_oracle::PnPOracle::qr_solve(Am, b, X);
+    for (int i = 0; i < 6; ++i) for (int j = 0; j < 4; ++j) A[4 * i + j] = Am[i][j];
+    return ok ? 1 : 0;
+}
+
 // deterministic libm (csrc/rsc_math.h) for the accuracy tests
 void ora_mlpnp_jac(const double* X, const double* nr, const double* ns, const double* x, double* J) {
     rsc_oracle::mlpnp_jacobian_public(X, nr, ns, x, J);

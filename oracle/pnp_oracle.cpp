@@ -519,18 +519,39 @@ void PnPOracle::gauss_newton(const double L[6][10], const double rho[6], double 
 }
 
 // PnPsolver.cpp:693-796 — Householder QR solve of the 6x4 system, verbatim structure.
-void PnPOracle::qr_solve(double A[6][4], double b[6], double X[4]) {
+#ifdef ORA_QR_STATS
+// tools/q19_stats.py: how often the last row is a column's strict maximum (the scans where Q19's eta
+// differs from a six-row eta).  Only in the instrumented build (-DORA_QR_STATS).
+static long g_qr_calls = 0, g_qr_row5[4] = {0, 0, 0, 0};
+extern "C" void ora_qr_stats(long* o) {
+    o[0] = g_qr_calls;
+    for (int k = 0; k < 4; ++k) o[1 + k] = g_qr_row5[k];
+}
+#endif
+bool PnPOracle::qr_solve(double A[6][4], double b[6], double X[4]) {
     const int nr = 6, nc = 4;
+#ifdef ORA_QR_STATS
+    ++g_qr_calls;
+#endif
     double A1[4], A2[4];
     for (int k = 0; k < nc; k++) {
+        // :714-720 — `elt = fabs(*ppAik)` is read BEFORE `ppAik += nc`, so iteration i reads row
+        // i-1: eta = max |A[k..nr-2][k]| (row k twice, the last row never) (Q19).
+#ifdef ORA_QR_STATS
+        {
+            double m = 0.0;
+            for (int i = k; i < nr - 1; ++i) m = std::max(m, ab(A[i][k]));
+            if (ab(A[nr - 1][k]) > m) ++g_qr_row5[k];
+        }
+#endif
         double eta = ab(A[k][k]);
         for (int i = k + 1; i < nr; i++) {
-            double elt = ab(A[i][k]);
+            double elt = ab(A[i - 1][k]);
             if (eta < elt) eta = elt;
         }
         if (eta == 0) {
             A1[k] = A2[k] = 0.0;
-            return;  // "A is singular" (:722-726)
+            return false;  // "A is singular" (:722-726)
         }
         double sum = 0.0, inv_eta = 1. / eta;
         for (int i = k; i < nr; i++) {
@@ -561,6 +582,7 @@ void PnPOracle::qr_solve(double A[6][4], double b[6], double X[4]) {
         for (int j = i + 1; j < nc; j++) s += A[i][j] * X[j];
         X[i] = (b[i] - s) / A2[i];
     }
+    return true;
 }
 
 // ---- test hooks ----

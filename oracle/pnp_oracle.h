@@ -44,6 +44,8 @@ public:
     // Exposed pieces for known-answer tests.
     double compute_pose_public(const int* idx, int n, float R[9], float t[3]);
     void check_inliers_public(const float R[9], const float t[3], std::vector<uint8_t>& inl, int& count);
+    // qr_solve (PnPsolver.cpp:693-796); false on the singular bail-out (X untouched).
+    static bool qr_solve(double A[6][4], double b[6], double X[4]);
 
 private:
     void CheckInliers();
@@ -61,7 +63,6 @@ private:
     void find_betas_approx_1(const double L[6][10], const double rho[6], double betas[4]);
     void find_betas_approx_2(const double L[6][10], const double rho[6], double betas[4]);
     void find_betas_approx_3(const double L[6][10], const double rho[6], double betas[4]);
-    void qr_solve(double A[6][4], double b[6], double X[4]);
     void compute_rho(double rho[6]);
     void compute_L_6x10(const double (*U)[12], double L[6][10]);
     void gauss_newton(const double L[6][10], const double rho[6], double betas[4]);

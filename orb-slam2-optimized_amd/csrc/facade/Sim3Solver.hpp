@@ -3,15 +3,29 @@
 // mvKeysUn, mvLevelSigma2 and a static/instance mK with (r,c) access (KeyFrame.hpp:149-174);
 // MapPointT needs isBad(), GetWorldPos() and GetIndexInKeyFrame(pKF) (MapPoint.cpp:297-304).
 // Rotation/translation types need (r,c) / (i) access and a default constructor.
+//
+// GetEstimatedRotation() / GetEstimatedTranslation() return Mat3 / Vec3, by default the types of
+// KeyFrameT::GetRotation() / GetTranslation() — Eigen::Matrix3f / Eigen::Vector3f for the reference's
+// KeyFrame (KeyFrame.hpp:42-43), the types include/Sim3Solver.hpp:29-30 declares — so the call sites
+// `Eigen::Matrix3f R = vpSim3Solvers[i]->GetEstimatedRotation();` (LoopClosing.cpp:307-308) compile
+// unchanged.
 #pragma once
 #include <cstring>
 #include <memory>
+#include <type_traits>
+#include <utility>
 #include <vector>
 #include "rsc_context.hpp"
 
 namespace rsc_orb {
 
-template <class KeyFrameT, class MapPointT, class Mat3 = void, class Vec3 = void>
+template <class KeyFrameT>
+using kf_rotation_t = typename std::decay<decltype(std::declval<KeyFrameT&>().GetRotation())>::type;
+template <class KeyFrameT>
+using kf_translation_t = typename std::decay<decltype(std::declval<KeyFrameT&>().GetTranslation())>::type;
+
+template <class KeyFrameT, class MapPointT, class Mat3 = kf_rotation_t<KeyFrameT>,
+          class Vec3 = kf_translation_t<KeyFrameT>>
 class Sim3Solver {
 public:
     // Sim3Solver::Sim3Solver (Sim3Solver.cpp:6-85): the match validity / keypoint lookup is done
@@ -87,7 +101,12 @@ public:
         return r.ok != 0;
     }
 
-    // GetEstimatedRotation / GetEstimatedTranslation (Sim3Solver.cpp:296-304)
+    // GetEstimatedRotation / GetEstimatedTranslation (Sim3Solver.hpp:29-30, Sim3Solver.cpp:296-304):
+    // the reference signatures, returning the best hypothesis' R12 / t12 of the last iterate().
+    Mat3 GetEstimatedRotation() const { return GetEstimatedRotation<Mat3>(); }
+    Vec3 GetEstimatedTranslation() const { return GetEstimatedTranslation<Vec3>(); }
+
+    // The same into any type with (r,c) / (i) access.
     template <class M3>
     M3 GetEstimatedRotation() const {
         M3 R;

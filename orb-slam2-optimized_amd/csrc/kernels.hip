@@ -823,6 +823,27 @@ __global__ __launch_bounds__(256) void selftest_math_kernel(int fn, const double
     out[i] = r;
 }
 
+// qr_solve_6x4 self-test (rsc_selftest_math fn 10): record r = x[34 r ..] holds A[6][4] row-major,
+// b[6] and the previous X[4]; out[34 r + 0..3] = X after the solve, out[34 r + 4] = 1 on success,
+// 0 on the singular bail-out (Q9 / Q19).
+__global__ __launch_bounds__(256) void selftest_qr_kernel(const double* __restrict__ x, int nrec,
+                                                          double* __restrict__ out) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= nrec) return;
+    const double* in = x + 34 * (size_t)r;
+    double A[6][4], b[6], X[4];
+    RSC_UNROLL for (int i = 0; i < 6; ++i) {
+        RSC_UNROLL for (int j = 0; j < 4; ++j) A[i][j] = in[4 * i + j];
+        b[i] = in[24 + i];
+    }
+    RSC_UNROLL for (int j = 0; j < 4; ++j) X[j] = in[30 + j];
+    const bool ok = qr_solve_6x4(A, b, X);
+    double* o = out + 34 * (size_t)r;
+    RSC_UNROLL for (int j = 0; j < 4; ++j) o[j] = X[j];
+    o[4] = ok ? 1.0 : 0.0;
+    for (int j = 5; j < 34; ++j) o[j] = 0.0;
+}
+
 __global__ __launch_bounds__(256) void upload16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16) {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n16) dst[i] = src[i];
@@ -862,7 +883,13 @@ hipError_t launch_upload16(const void* host_src, void* dev_dst, size_t n16, hipS
 }
 
 hipError_t launch_selftest_math(int fn, const double* x, int n, double* out, hipStream_t st) {
-    if (fn < 0 || fn > 9 || n <= 0) return hipErrorInvalidValue;
+    if (fn < 0 || fn > 10 || n <= 0) return hipErrorInvalidValue;
+    if (fn == 10) {
+        if (n % 34) return hipErrorInvalidValue;
+        const int nrec = n / 34;
+        selftest_qr_kernel<<<(nrec + 255) / 256, 256, 0, st>>>(x, nrec, out);
+        return hipGetLastError();
+    }
     selftest_math_kernel<<<(n + 255) / 256, 256, 0, st>>>(fn, x, n, out);
     return hipGetLastError();
 }

@@ -563,9 +563,25 @@ struct HipPnPBackend : PnPBackend {
             // replay's rules to the same counts); anything else is an engine bug, reported loudly
             const int nslots = fused_count;
             fused_count = 0;
+            // every slot: the device refined exactly the listed slots (o.k >= 0) and no other one
+            // (an unlisted device Refine would have overwritten that solver's best / refined masks)
+            thread_local std::vector<int> listed_tl;
+            std::vector<int>& listed = listed_tl;
+            listed.assign((size_t)nslots, -1);
             for (int i = 0; i < count; ++i) {
-                const RefineSelOut* o = spec_j[i] >= 0 && spec_j[i] < nslots ? &C->h_selout.p[spec_j[i]] : nullptr;
-                if (!o || o->k != pause_k[i] || (o->adopt != 0) != (adopt_k[i] >= 0) || o->rows_after != rows_after[i]) {
+                if (spec_j[i] < 0 || spec_j[i] >= nslots || listed[spec_j[i]] >= 0) {
+                    g_last_error = "device-side Refine selection disagrees with the host replay";
+                    return RSC_ERR_INTERNAL;
+                }
+                listed[spec_j[i]] = i;
+            }
+            for (int j = 0; j < nslots; ++j) {
+                const RefineSelOut& o = C->h_selout.p[j];
+                const int i = listed[j];
+                const bool agree = i < 0 ? o.k < 0
+                                         : o.k == pause_k[i] && (o.adopt != 0) == (adopt_k[i] >= 0) &&
+                                               o.rows_after == rows_after[i];
+                if (!agree) {
                     g_last_error = "device-side Refine selection disagrees with the host replay";
                     return RSC_ERR_INTERNAL;
                 }
@@ -578,6 +594,7 @@ struct HipPnPBackend : PnPBackend {
             }
             return 0;
         }
+        if (count == 0) return 0;
         std::vector<DevPnP> probs(count);
         std::vector<RefineJob> jobs(count);
         // out: refined poses [count][12] | counts [count] | adopted best poses [count][12]
@@ -1053,7 +1070,7 @@ int rsc_context_enable_timing(rsc_context* C, int enable) {
 }
 
 int rsc_selftest_math(rsc_context* C, int fn, const double* x, int n, double* out) {
-    if (!C || fn < 0 || fn > 9 || n < 0 || (n > 0 && (!x || !out))) return RSC_ERR_ARG;
+    if (!C || fn < 0 || fn > 10 || n < 0 || (n > 0 && (!x || !out)) || (fn == 10 && n % 34)) return RSC_ERR_ARG;
     if (n == 0) return RSC_OK;
     RSC_HIP(hipSetDevice(C->device));
     double* d = nullptr;
@@ -2241,24 +2258,24 @@ int rsc_kfdb_state(rsc_kfdb* db, int kf, uint64_t* q, int32_t* w, float* s) {
     return RSC_OK;
 }
 
-int rsc_diag_kfdb_stamps(rsc_context* C, uint64_t* out) {
-    if (!C || !out) return RSC_ERR_ARG;
+int rsc_diag_kfdb_stamps(rsc_context* C, uint64_t* out, int cap) {
+    if (!C || !out || cap < 4096 * 4) return RSC_ERR_ARG;
     RSC_HIP(hipSetDevice(C->device));
     RSC_HIP(hipStreamSynchronize(C->stream));
     RSC_HIP(read_kfdb_stamps(out));
     return RSC_OK;
 }
 
-int rsc_diag_poseopt_phases(rsc_context* C, uint64_t* out) {
-    if (!C || !out) return RSC_ERR_ARG;
+int rsc_diag_poseopt_phases(rsc_context* C, uint64_t* out, int cap) {
+    if (!C || !out || cap < 64 * 8) return RSC_ERR_ARG;
     RSC_HIP(hipSetDevice(C->device));
     RSC_HIP(hipStreamSynchronize(C->stream));
     RSC_HIP(read_poseopt_phases(out));
     return RSC_OK;
 }
 
-int rsc_diag_refine_phase_stamps(rsc_context* C, uint64_t* out) {
-    if (!C || !out) return RSC_ERR_ARG;
+int rsc_diag_refine_phase_stamps(rsc_context* C, uint64_t* out, int cap) {
+    if (!C || !out || cap < 64 * 24) return RSC_ERR_ARG;
     RSC_HIP(hipStreamSynchronize(C->stream));
     RSC_HIP(read_refine_stamps(out));
     return RSC_OK;

@@ -161,7 +161,8 @@ struct PnPBackend {
     // mvbBestInliers/mBestTcw := that hypothesis (the backend writes states[q]->mBestTcw).  Uses the
     // best mask and rows_after; writes the refined count and pose (the caller decides success) into
     // the out arrays.  A backend may have run exactly this Refine already on the device with the
-    // round (the first pause of each solver); it then only hands back the results.
+    // round (the first pause of each solver); it then only hands back the results.  Called after
+    // every speculation, with count == 0 when no solver paused.
     virtual int refine(PnPState* const* states, int count, const int* spec_j, const int* pause_k,
                        const int* adopt_k, const int* rows_after, int* refined_count,
                        float (*refined_pose)[12]) = 0;
@@ -258,7 +259,9 @@ inline int pnp_iterate_many(PnPBackend& be, PnPState* const* S, int count, const
             }
         std::vector<int> rcount(rs.size());
         std::vector<float> rpose(rs.size() * 12);
-        if (!rs.empty()) {
+        // called after every speculation, with an empty list when no solver paused, so that a
+        // backend that selected Refines on the device checks it selected none
+        if (!spec.empty()) {
             int st = be.refine(rs.data(), (int)rs.size(), rj.data(), rp.data(), rk.data(), rows_after.data(),
                                rcount.data(), reinterpret_cast<float(*)[12]>(rpose.data()));
             if (st) return st;

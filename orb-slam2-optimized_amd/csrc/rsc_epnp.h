@@ -194,15 +194,18 @@ RSC_HD void compute_L_6x10(const SV& S) {
     }
 }
 
-// qr_solve (PnPsolver.cpp:693-796).  Returns false on the singular bail-out (X left unchanged).
+// qr_solve (PnPsolver.cpp:693-796).  Returns false on the singular bail-out (X left unchanged):
+// rows k..4 of column k all zero (Q19: row 5 is not looked at, :714-726).
 RSC_HD bool qr_solve_6x4(double (&A)[6][4], double (&b)[6], double (&X)[4]) {
     double A1[4], A2[4];
     bool singular = false;
     RSC_UNROLL for (int k = 0; k < 4; k++) {
         if (!singular) {
+            // Q19: the reference's pointer loop (:714-720) reads *ppAik before advancing it, so
+            // eta is the largest |A[i][k]| over rows k..4 (row k twice, row 5 never).
             double eta = rabs(A[k][k]);
             RSC_UNROLL for (int i = k + 1; i < 6; i++) {
-                double elt = rabs(A[i][k]);
+                double elt = rabs(A[i - 1][k]);
                 if (eta < elt) eta = elt;
             }
             if (eta == 0) {

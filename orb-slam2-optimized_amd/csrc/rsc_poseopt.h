@@ -429,7 +429,7 @@ RSC_HD bool po_ldlt_solve(double (&A)[n][n], const double (&b)[n], double (&x)[n
 RSC_HD bool po_ldlt_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[6]) { return po_ldlt_solve<6>(A, b, x); }
 
 #if defined(__HIPCC__)
-hipError_t read_poseopt_phases(uint64_t* out);  // diagnostic, [64][4] (poseopt.hip)
+hipError_t read_poseopt_phases(uint64_t* out);  // diagnostic, [64][8] (poseopt.hip)
 hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st);
 #endif
 

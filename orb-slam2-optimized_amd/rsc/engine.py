@@ -383,9 +383,10 @@ def load_library(path: str = LIB_PATH):
                                             C.POINTER(C.c_void_p), i32p]
     L.rsc_diag_bow_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"),
                                             C.c_int]
-    L.rsc_diag_refine_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
-    L.rsc_diag_poseopt_phases.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
-    L.rsc_diag_kfdb_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")]
+    L.rsc_diag_refine_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"),
+                                               C.c_int]
+    L.rsc_diag_poseopt_phases.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"), C.c_int]
+    L.rsc_diag_kfdb_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"), C.c_int]
     f32p_ = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
     L.rsc_kfview_create.argtypes = [vp, C.POINTER(Sim3KFStruct), C.POINTER(vp)]
     L.rsc_kfview_destroy.argtypes = [vp]
@@ -443,7 +444,7 @@ class Context:
         _check(load_library().rsc_context_enable_timing(self.h, int(on)), "enable_timing")
 
     MATH_FNS = {"sin": 0, "cos": 1, "acos": 2, "cbrt": 3, "log": 4, "logf": 5, "sqrt_unit": 6, "recip_unit": 7,
-                "givens_c": 8, "givens_s": 9}
+                "givens_c": 8, "givens_s": 9, "qr_solve": 10}
 
     def selftest_math(self, fn: str, x):
         """rsc_math.h evaluated on the GPU (f64 array in, f64 array out; logf: float in/out)."""
@@ -453,6 +454,18 @@ class Context:
         _check(load_library().rsc_selftest_math(self.h, self.MATH_FNS[fn], x.ctypes.data_as(dp), int(x.size),
                                                 out.ctypes.data_as(dp)), "selftest_math")
         return out
+
+    def qr_solve(self, A, b, X0):
+        """PnPsolver::qr_solve (the kernels' qr_solve_6x4) ON THE GPU for a batch of 6x4 systems:
+        A [k,6,4], b [k,6], X0 [k,4] (kept on the singular bail-out) -> (X [k,4], ok [k] bool)."""
+        A = np.asarray(A, np.float64).reshape(-1, 24)
+        k = A.shape[0]
+        rec = np.zeros((k, 34))
+        rec[:, :24] = A
+        rec[:, 24:30] = np.asarray(b, np.float64).reshape(k, 6)
+        rec[:, 30:34] = np.asarray(X0, np.float64).reshape(k, 4)
+        out = self.selftest_math("qr_solve", rec.ravel()).reshape(k, 34)
+        return out[:, :4].copy(), out[:, 4] == 1.0
 
     def last_timing(self):
         out = (C.c_double * 6)()

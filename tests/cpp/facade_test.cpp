@@ -440,14 +440,23 @@ int main(int argc, char** argv) {
         const double prob = rd<double>(in);
         const int mi = rd<int32_t>(in), mx = rd<int32_t>(in);
         const int ncalls = rd<int32_t>(in);
-        rsc_orb::Sim3Solver<KeyFrame, MapPoint> solver(kf1, kf2, matched, seed);
+        // LoopClosing::ComputeSim3's own expressions (LoopClosing.cpp:260-261,286,307-308): the
+        // solvers live behind pointers and the getters are called without template arguments.
+        std::vector<std::shared_ptr<rsc_orb::Sim3Solver<KeyFrame, MapPoint>>> vpSim3Solvers(1);
+        vpSim3Solvers[0] = std::make_shared<rsc_orb::Sim3Solver<KeyFrame, MapPoint>>(kf1, kf2, matched, seed);
+        auto& solver = *vpSim3Solvers[0];
         solver.SetRansacParameters(prob, mi, mx);
         for (int c = 0; c < ncalls; ++c) {
             const int its = rd<int32_t>(in);
             bool nm = false; std::vector<bool> inl; int ni = -1;
-            bool ok = its < 0 ? solver.find(inl, ni) : solver.iterate(its, nm, inl, ni);
-            Mat3 R = solver.GetEstimatedRotation<Mat3>();
-            Vec3 t = solver.GetEstimatedTranslation<Vec3>();
+            bool ok = its < 0 ? solver.find(inl, ni) : vpSim3Solvers[0]->iterate(its, nm, inl, ni);
+            Mat3 R = vpSim3Solvers[0]->GetEstimatedRotation();
+            Vec3 t = vpSim3Solvers[0]->GetEstimatedTranslation();
+            {   // the explicit-type form gives the same values
+                Mat3 R2 = solver.GetEstimatedRotation<Mat3>();
+                Vec3 t2 = solver.GetEstimatedTranslation<Vec3>();
+                if (std::memcmp(&R2, &R, sizeof(R)) || std::memcmp(&t2, &t, sizeof(t))) return 3;
+            }
             wr<int32_t>(out, ok); wr<int32_t>(out, nm); wr<int32_t>(out, ni);
             for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) wr<float>(out, R.m[a][b]);
             for (int a = 0; a < 3; ++a) wr<float>(out, t.v[a]);

@@ -15,6 +15,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(ROOT, "oracle", "build",
                         "librsc_oracle_glibc.so" if os.environ.get("RSC_ORACLE_LIBM") == "glibc"
                         else "librsc_oracle.so")
+# RSC_ORACLE_LIB=<path>: another build of the restatement (tools/oracle_ab.py compares two builds,
+# e.g. an arithmetic-order variant or the previous round's oracle).
+LIB_PATH = os.environ.get("RSC_ORACLE_LIB", LIB_PATH)
 
 _lib = None
 
@@ -27,6 +30,8 @@ u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
 
 
 def build_oracle() -> str:
+    if "RSC_ORACLE_LIB" in os.environ:
+        return LIB_PATH
     if not os.path.exists(LIB_PATH) or _stale():
         import subprocess
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "all"])
@@ -116,6 +121,9 @@ def lib():
         getattr(L, fn).restype = C.c_double
         getattr(L, fn).argtypes = [C.c_double]
     L.ora_mlpnp_jac.argtypes = [f64p, f64p, f64p, f64p, f64p]
+    if hasattr(L, "ora_qr_solve"):  # absent from round-3 builds compared by tools/oracle_ab.py
+        L.ora_qr_solve.argtypes = [f64p, f64p, f64p]
+        L.ora_qr_solve.restype = C.c_int
     L.ora_sym_eig.argtypes = [C.c_int, f64p, f64p, f64p]
     L.ora_sym_eig4f.argtypes = [f32p, f32p, f32p]
     L.ora_svd_solve.argtypes = [C.c_int, f64p, f64p, f64p]
@@ -173,6 +181,15 @@ def svd_solve(A, b):
     x = np.zeros(k)
     lib().ora_svd_solve(k, A.ravel(), np.ascontiguousarray(b, np.float64), x)
     return x
+
+
+def qr_solve(A, b, X0):
+    """PnPsolver::qr_solve (PnPsolver.cpp:693-796) as restated: (X, ok)."""
+    A = np.array(A, np.float64).reshape(24)
+    b = np.array(b, np.float64).reshape(6)
+    X = np.array(X0, np.float64).reshape(4)
+    ok = lib().ora_qr_solve(A, b, X)
+    return X, bool(ok)
 
 
 def random_int(seed, maxes):

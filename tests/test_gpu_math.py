@@ -107,3 +107,22 @@ def test_chase_arithmetic_is_ieee(name):
     dev = gpu_ctx().selftest_math(name, x)
     bad = np.flatnonzero(~_same_bits(dev, want))
     assert bad.size == 0, [(float(x[i]), float(dev[i]), float(want[i])) for i in bad[:8]]
+
+
+def test_device_qr_solve_q19_matches_oracle():
+    """Q19 (PnPsolver.cpp:714-720): the kernels' qr_solve_6x4 on the GPU — eta over rows k..4,
+    the singular bail-out keeping X — bit-for-bit equal to the oracle (itself equal to a literal
+    pointer-walk transcription, tests/test_cpu_q19.py)."""
+    from test_cpu_q19 import q19_cases
+    cases = q19_cases(seed=1919, n_random=2000)
+    A = np.stack([c[0] for c in cases])
+    b = np.stack([c[1] for c in cases])
+    X0 = np.stack([c[2] for c in cases])
+    X, ok = gpu_ctx().qr_solve(A, b, X0)
+    n_singular = 0
+    for i, (Ai, bi, Xi) in enumerate(cases):
+        want, ok_want = ol.qr_solve(Ai, bi, Xi)
+        assert ok[i] == ok_want, i
+        assert np.array_equal(X[i].view(np.uint64), want.view(np.uint64)), (i, X[i], want)
+        n_singular += not ok_want
+    assert n_singular >= 4

@@ -161,3 +161,39 @@ def test_batch_iterate_raw_matches_dicts():
         assert raw["iterations"][i] == o["iterations"] and raw["no_more"][i] == o["no_more"]
         if o["ok"]:
             assert bits(raw["T"][i].reshape(4, 4)).tolist() == bits(o["T"]).tolist()
+
+
+@pytest.mark.parametrize("mode", ["fused", "large_round", "unfused"])
+def test_iterate_many_mixed_n_refines(mode, monkeypatch):
+    """Solvers of very different N whose Refines land in the same launch: the device-side
+    selection + Refine (rounds <= 4,096 hypotheses, `fused`), the two-launch form for a larger round
+    (`large_round`: 16 solvers x 300) and with RSC_FUSED_REFINE=0 (`unfused`).  Every solver's
+    result, mask and EPnP row count must equal its own sequential oracle run: a Refine writing past a
+    shorter solver's bitsets, or one the host did not ask for, shows up as a neighbour's mask."""
+    from rsc import engine
+    if mode == "unfused":
+        monkeypatch.setenv("RSC_FUSED_REFINE", "0")
+    c = engine.Context(0)
+    sizes = [100, 3000, 240, 1800, 64, 2500, 130, 900]
+    if mode == "large_round":
+        sizes = sizes * 2
+    rng = np.random.default_rng({"fused": 5, "large_round": 6, "unfused": 7}[mode])
+    scenes = [synth.make_pnp_scene(rng, n, float(rng.uniform(0.55, 0.8)), n_points=n + 11) for n in sizes]
+    gs, os_ = [], []
+    for i, sc in enumerate(scenes):
+        g = engine.PnPSolver(c, sc, 500 + i)
+        g.set_ransac_parameters(*RELOC)
+        o = ol.OraclePnP(sc, 500 + i)
+        o.set_ransac_parameters(*RELOC)
+        gs.append(g)
+        os_.append(o)
+    its = 300 if mode == "large_round" else 5
+    n_ok = 0
+    for rnd in range(4):
+        outs = engine.pnp_iterate_many(gs, its)
+        for i, (g, o) in enumerate(zip(gs, os_)):
+            ro = o.iterate(its)
+            assert_pnp_equal(outs[i], ro, f"{mode} round {rnd} solver {i} (N={sizes[i]})")
+            assert g.state()["max_rows"] == o.info()["max_rows"]
+            n_ok += ro["ok"]
+    assert n_ok >= len(sizes) // 2

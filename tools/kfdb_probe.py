@@ -27,7 +27,7 @@ st = np.zeros(4096 * 4, np.uint64)
 rows = []
 for i, (ids, vals) in enumerate(queries[:16]):
     db.detect_relocalization(100 + i, ids, vals)
-    engine.load_library().rsc_diag_kfdb_stamps(ctx.h, st)
+    engine._check(engine.load_library().rsc_diag_kfdb_stamps(ctx.h, st, st.size), "kfdb stamps")
     s = st.reshape(4096, 4)[:n].astype(np.int64)
     t0 = s[:, 0].min()
     rows.append([(s[:, 0] - t0).max(), (s[:, 1] - s[:, 0]).mean(), (s[:, 2] - s[:, 1]).mean(),

@@ -19,7 +19,7 @@ for sf in (0.8, 0.0):
     for _ in range(5):
         b.run()
     ph = np.zeros(64 * 8, np.uint64)
-    engine.load_library().rsc_diag_poseopt_phases(ctx.h, ph)
+    engine._check(engine.load_library().rsc_diag_poseopt_phases(ctx.h, ph, ph.size), "poseopt phases")
     ph = ph.reshape(64, 8).astype(np.float64)
     npass = (ph[:, 1].astype(np.uint64) & np.uint64(0xFFFFFF)).astype(np.float64)
     summ = (ph[:, 1].astype(np.uint64) >> np.uint64(24)).astype(np.float64)

@@ -23,7 +23,7 @@ for rep in range(5):
     eb.batch.set_ransac_parameters(*params)
     eb.run()
 st = np.zeros(64 * 24, np.uint64)
-engine.load_library().rsc_diag_refine_phase_stamps(ctx.h, st)
+engine._check(engine.load_library().rsc_diag_refine_phase_stamps(ctx.h, st, st.size), "refine stamps")
 st = st.reshape(64, 24).astype(np.int64)
 ok = st[:, 0] > 0
 d = np.diff(st[ok][:, :8], axis=1) / 100.0

@@ -20,9 +20,9 @@ for rep in range(2):
     eb.batch.reset(seeds)
     eb.batch.set_ransac_parameters(*rev.RELOC_PARAMS)
     eb.run()
-st = np.zeros(64 * 12, np.uint64)
-engine.load_library().rsc_diag_refine_phase_stamps(ctx.h, st)
-st = st.reshape(64, 12).astype(np.int64)
+st = np.zeros(64 * 24, np.uint64)
+engine._check(engine.load_library().rsc_diag_refine_phase_stamps(ctx.h, st, st.size), "refine stamps")
+st = st.reshape(64, 24).astype(np.int64)
 ok = st[:, 0] > 0
 d = np.diff(st[ok][:, :8], axis=1) / 100.0
 print(f"jobs stamped: {ok.sum()}  total us: mean {((st[ok, 6] - st[ok, 0]) / 100.0).mean():.1f} "
