@@ -13,9 +13,16 @@
 //   * Quaternion::toRotationMatrix — PnPsolver.cpp:478, Sim3Solver.cpp:248.
 //
 // ARITHMETIC CONTRACT (shared with the HIP kernels; see DESIGN.md §"Arithmetic contract"):
-// Eigen's association order inside sums depends on SIMD packet width and alignment and cannot be
-// reproduced without Eigen, so every sum here is evaluated strictly left to right in index order,
-// starting from the first term (or from 0.0 where the reference itself starts from setZero()).
+// Sums are evaluated left to right in index order, starting from the first term (or from 0.0
+// where the reference itself starts from setZero()) — EXCEPT the 3-term reductions of fixed-size
+// Eigen expressions, which follow Eigen 3.3's evaluation on the reference's x86-64 SSE2 build
+// (round 4, profiles/r04/order_choice.json): a reduction that cannot use packets (a dot / squared
+// norm / product coefficient over a row of a column-major matrix, or any float 3-vector: 3 < 4
+// lanes) is redux_novec_unroller's halving tree a0 + (a1 + a2) (`ered3`); a Matrix3d * Vector3d
+// assigned to a Vector3d evaluates rows 0-1 as one Packet2d multiply-add chain in index order and
+// row 2 by the coefficient path (halving).  Dynamic-size reductions (column sums, M^T M) stay left
+// to right: their order depends on the run-time alignment and GEMM blocking.
+// -DORA_LTR_ORDER restores the rounds 1-3 left-to-right order everywhere (tools/oracle_ab.py A/B).
 // No FMA contraction (-ffp-contract=off), IEEE division and sqrt.
 #pragma once
 #include <cmath>
@@ -31,6 +38,15 @@ template <> struct Lim<double> { static double eps() { return DBL_EPSILON; } sta
 template <> struct Lim<float>  { static float eps() { return FLT_EPSILON; }  static float min() { return FLT_MIN; } };
 
 template <typename S> static inline S ab(S x) { return std::fabs(x); }
+
+// 3-term reduction of a non-vectorisable fixed-size Eigen expression (see the contract above).
+#ifndef ORA_LTR_ORDER
+template <typename S> static inline S ered3(S a0, S a1, S a2) { return a0 + (a1 + a2); }
+#else
+template <typename S> static inline S ered3(S a0, S a1, S a2) { return a0 + a1 + a2; }
+#endif
+// Row r of Matrix3d * Vector3d into a Vector3d: rows 0-1 one Packet2d chain, row 2 coefficient-wise.
+template <typename S> static inline S emv3d_row(int r, S a0, S a1, S a2) { return r < 2 ? (a0 + a1) + a2 : ered3(a0, a1, a2); }
 template <typename S> static inline S sq(S x) { return x * x; }
 
 // Eigen numext::hypot (MathFunctions.h, hypot_impl) for real scalars.

@@ -165,9 +165,10 @@ void PnPOracle::CheckInliers() {
     for (int i = 0; i < N; i++) {
         const float* P = &mvP3Dw[3 * i];
         const float* p = &mvP2D[2 * i];
-        float Xc = mRi[0][0] * P[0] + mRi[0][1] * P[1] + mRi[0][2] * P[2] + mti[0];
-        float Yc = mRi[1][0] * P[0] + mRi[1][1] * P[1] + mRi[1][2] * P[2] + mti[1];
-        float Zc = mRi[2][0] * P[0] + mRi[2][1] * P[1] + mRi[2][2] * P[2] + mti[2];
+        // :250 Matrix3f * Vector3f: three coefficient-path reductions (ered3), then + mti
+        float Xc = ered3(mRi[0][0] * P[0], mRi[0][1] * P[1], mRi[0][2] * P[2]) + mti[0];
+        float Yc = ered3(mRi[1][0] * P[0], mRi[1][1] * P[1], mRi[1][2] * P[2]) + mti[1];
+        float Zc = ered3(mRi[2][0] * P[0], mRi[2][1] * P[1], mRi[2][2] * P[2]) + mti[2];
         float invZc = 1 / Zc;
         float ue = (float)(cx + fx * Xc * invZc);
         float ve = (float)(cy + fy * Yc * invZc);
@@ -239,7 +240,8 @@ void PnPOracle::compute_barycentric_coordinates() {
         double d0 = pws[3 * i + 0] - cws[0][0];
         double d1 = pws[3 * i + 1] - cws[0][1];
         double d2 = pws[3 * i + 2] - cws[0][2];
-        for (int j = 0; j < 3; j++) alphas[4 * i + j + 1] = CC_inv[j][0] * d0 + CC_inv[j][1] * d1 + CC_inv[j][2] * d2;
+        // :338 row(j).dot(...) over rows of column-major 3x3 / dynamic matrices: halving redux
+        for (int j = 0; j < 3; j++) alphas[4 * i + j + 1] = ered3(CC_inv[j][0] * d0, CC_inv[j][1] * d1, CC_inv[j][2] * d2);
         alphas[4 * i + 0] = 1.0 - alphas[4 * i + 1] - alphas[4 * i + 2] - alphas[4 * i + 3];
     }
 }
@@ -327,9 +329,10 @@ double PnPOracle::reprojection_error(const double R[3][3], const double t[3]) {
     double sum2 = 0.0;
     for (int i = 0; i < number_of_correspondences; i++) {
         const double* P = &pws[3 * i];
-        double X = R[0][0] * P[0] + R[0][1] * P[1] + R[0][2] * P[2] + t[0];
-        double Y = R[1][0] * P[0] + R[1][1] * P[1] + R[1][2] * P[2] + t[1];
-        double Z = R[2][0] * P[0] + R[2][1] * P[1] + R[2][2] * P[2] + t[2];
+        // :423 Matrix3d * Vector3d + t into a Vector3d (emv3d_row)
+        double X = emv3d_row(0, R[0][0] * P[0], R[0][1] * P[1], R[0][2] * P[2]) + t[0];
+        double Y = emv3d_row(1, R[1][0] * P[0], R[1][1] * P[1], R[1][2] * P[2]) + t[1];
+        double Z = emv3d_row(2, R[2][0] * P[0], R[2][1] * P[1], R[2][2] * P[2]) + t[2];
         double inv_Zc = 1.0 / Z;
         double u = cx + fx * X * inv_Zc;
         double v = cy + fy * Y * inv_Zc;
@@ -377,7 +380,8 @@ void PnPOracle::estimate_R_and_t(double R[3][3], double t[3]) {
     quat_to_R(qw, qx, qy, qz, R);
     if (det3(R) < 0)
         for (int c = 0; c < 3; ++c) R[2][c] = -R[2][c];
-    for (int r = 0; r < 3; ++r) t[r] = pc0[r] - (R[r][0] * pw0[0] + R[r][1] * pw0[1] + R[r][2] * pw0[2]);
+    // :492 pc0 - Matrix3d * pw0 into a Vector3d (emv3d_row)
+    for (int r = 0; r < 3; ++r) t[r] = pc0[r] - emv3d_row(r, R[r][0] * pw0[0], R[r][1] * pw0[1], R[r][2] * pw0[2]);
 }
 
 // PnPsolver.cpp:495-502 — negates ALL allocated rows of pcs.
@@ -464,7 +468,8 @@ void PnPOracle::compute_L_6x10(const double (*U)[12], double l[6][10]) {
             if (b > 3) { a++; b = a + 1; }
         }
     }
-    auto dot = [](const double* x, const double* y) { return x[0] * y[0] + x[1] * y[1] + x[2] * y[2]; };
+    // rows of column-major Matrix<double,6,3>: halving redux (ered3)
+    auto dot = [](const double* x, const double* y) { return ered3(x[0] * y[0], x[1] * y[1], x[2] * y[2]); };
     for (int i = 0; i < 6; i++) {
         l[i][0] = dot(dv[0][i], dv[0][i]);
         l[i][1] = 2.0 * dot(dv[0][i], dv[1][i]);
@@ -483,7 +488,7 @@ void PnPOracle::compute_L_6x10(const double (*U)[12], double l[6][10]) {
 void PnPOracle::compute_rho(double rho[6]) {
     auto d2 = [&](int a, int b) {
         double x = cws[a][0] - cws[b][0], y = cws[a][1] - cws[b][1], z = cws[a][2] - cws[b][2];
-        return x * x + y * y + z * z;
+        return ered3(x * x, y * y, z * z);  // squaredNorm of a row of Matrix<double,4,3>
     };
     rho[0] = d2(0, 1); rho[1] = d2(0, 2); rho[2] = d2(0, 3);
     rho[3] = d2(1, 2); rho[4] = d2(1, 3); rho[5] = d2(2, 3);

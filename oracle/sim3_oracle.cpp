@@ -7,9 +7,9 @@
 
 namespace rsc_oracle {
 
-// X3Dc = Rcw * Xw + tcw (float; left-to-right sums)
+// X3Dc = Rcw * Xw + tcw (:58, :62; Matrix3f * Vector3f: coefficient-path reductions, ered3)
 static inline void xform(const float R[9], const float t[3], const float* X, float* out) {
-    for (int r = 0; r < 3; ++r) out[r] = R[3 * r + 0] * X[0] + R[3 * r + 1] * X[1] + R[3 * r + 2] * X[2] + t[r];
+    for (int r = 0; r < 3; ++r) out[r] = ered3(R[3 * r + 0] * X[0], R[3 * r + 1] * X[1], R[3 * r + 2] * X[2]) + t[r];
 }
 
 // Sim3Solver.cpp:6-85
@@ -135,8 +135,8 @@ bool Sim3Oracle::find(std::vector<uint8_t>& vbInliers12, int& nInliers) {
 void Sim3Oracle::ComputeSim3(const float P1[3][3], const float P2[3][3]) {
     float O1[3], O2[3], Pr1[3][3], Pr2[3][3];
     for (int r = 0; r < 3; ++r) {
-        O1[r] = P1[r][0] + P1[r][1] + P1[r][2];
-        O2[r] = P2[r][0] + P2[r][1] + P2[r][2];
+        O1[r] = ered3(P1[r][0], P1[r][1], P1[r][2]);  // P.rowwise().sum() (:188)
+        O2[r] = ered3(P2[r][0], P2[r][1], P2[r][2]);
     }
     for (int r = 0; r < 3; ++r) { O1[r] = O1[r] / 3.f; O2[r] = O2[r] / 3.f; }
     for (int i = 0; i < 3; ++i)
@@ -144,7 +144,7 @@ void Sim3Oracle::ComputeSim3(const float P1[3][3], const float P2[3][3]) {
     // M = Pr2 * Pr1^T
     float M[3][3];
     for (int a = 0; a < 3; ++a)
-        for (int b = 0; b < 3; ++b) M[a][b] = Pr2[a][0] * Pr1[b][0] + Pr2[a][1] * Pr1[b][1] + Pr2[a][2] * Pr1[b][2];
+        for (int b = 0; b < 3; ++b) M[a][b] = ered3(Pr2[a][0] * Pr1[b][0], Pr2[a][1] * Pr1[b][1], Pr2[a][2] * Pr1[b][2]);
     float N11 = M[0][0] + M[1][1] + M[2][2];
     float N12 = M[1][2] - M[2][1];
     float N13 = M[2][0] - M[0][2];
@@ -160,11 +160,11 @@ void Sim3Oracle::ComputeSim3(const float P1[3][3], const float P2[3][3]) {
     // q = (w,x,y,z) = eigenvector of the largest eigenvalue, NOT conjugated (:243-246)
     quat_to_R(es.V[0][3], es.V[1][3], es.V[2][3], es.V[3][3], mR12i);
     // scale fixed to 1 (:250); t12 = O1 - R12*O2 (:253)
-    for (int r = 0; r < 3; ++r) mt12i[r] = O1[r] - (mR12i[r][0] * O2[0] + mR12i[r][1] * O2[1] + mR12i[r][2] * O2[2]);
+    for (int r = 0; r < 3; ++r) mt12i[r] = O1[r] - ered3(mR12i[r][0] * O2[0], mR12i[r][1] * O2[1], mR12i[r][2] * O2[2]);
     // T21 = T12.inverse() for an Isometry: R^T, -(R^T t)
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) mR21i[r][c] = mR12i[c][r];
-    for (int r = 0; r < 3; ++r) mt21i[r] = -(mR21i[r][0] * mt12i[0] + mR21i[r][1] * mt12i[1] + mR21i[r][2] * mt12i[2]);
+    for (int r = 0; r < 3; ++r) mt21i[r] = -ered3(mR21i[r][0] * mt12i[0], mR21i[r][1] * mt12i[1], mR21i[r][2] * mt12i[2]);
 }
 
 // Sim3Solver.cpp:306-327 (rotation() taken as linear(), Q14)
@@ -174,9 +174,9 @@ void Sim3Oracle::Project(const std::vector<float>& X, std::vector<float>& P2D, c
     P2D.resize(2 * n);
     for (size_t i = 0; i < n; ++i) {
         const float* p = &X[3 * i];
-        float x3 = R[0][0] * p[0] + R[0][1] * p[1] + R[0][2] * p[2] + t[0];
-        float y3 = R[1][0] * p[0] + R[1][1] * p[1] + R[1][2] * p[2] + t[1];
-        float z3 = R[2][0] * p[0] + R[2][1] * p[1] + R[2][2] * p[2] + t[2];
+        float x3 = ered3(R[0][0] * p[0], R[0][1] * p[1], R[0][2] * p[2]) + t[0];  // :320
+        float y3 = ered3(R[1][0] * p[0], R[1][1] * p[1], R[1][2] * p[2]) + t[1];
+        float z3 = ered3(R[2][0] * p[0], R[2][1] * p[1], R[2][2] * p[2]) + t[2];
         const float invz = 1 / z3;
         const float x = x3 * invz;
         const float y = y3 * invz;
@@ -223,7 +223,7 @@ void Sim3Oracle::compute_sim3_public(const int idx[3], float R[9], float t[3]) {
 int Sim3Oracle::check_inliers_public(const float R[9], const float t[3], std::vector<uint8_t>& inl) {
     for (int r = 0; r < 3; ++r) { mt12i[r] = t[r]; for (int c = 0; c < 3; ++c) mR12i[r][c] = R[3 * r + c]; }
     for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) mR21i[r][c] = mR12i[c][r];
-    for (int r = 0; r < 3; ++r) mt21i[r] = -(mR21i[r][0] * mt12i[0] + mR21i[r][1] * mt12i[1] + mR21i[r][2] * mt12i[2]);
+    for (int r = 0; r < 3; ++r) mt21i[r] = -ered3(mR21i[r][0] * mt12i[0], mR21i[r][1] * mt12i[1], mR21i[r][2] * mt12i[2]);
     CheckInliers();
     inl = mvbInliersi;
     return mnInliersi;

@@ -346,9 +346,9 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
     __syncthreads();
     for (int i = tid; i < nr; i += 256) {
         const double d0 = pws[3 * i] - cws_sh[0], d1 = pws[3 * i + 1] - cws_sh[1], d2 = pws[3 * i + 2] - cws_sh[2];
-        const double a1 = cci_sh[0] * d0 + cci_sh[1] * d1 + cci_sh[2] * d2;
-        const double a2 = cci_sh[3] * d0 + cci_sh[4] * d1 + cci_sh[5] * d2;
-        const double a3 = cci_sh[6] * d0 + cci_sh[7] * d1 + cci_sh[8] * d2;
+        const double a1 = ered3(cci_sh[0] * d0, cci_sh[1] * d1, cci_sh[2] * d2);  // :338, ered3
+        const double a2 = ered3(cci_sh[3] * d0, cci_sh[4] * d1, cci_sh[5] * d2);
+        const double a3 = ered3(cci_sh[6] * d0, cci_sh[7] * d1, cci_sh[8] * d2);
         als[4 * i + 1] = a1;
         als[4 * i + 2] = a2;
         als[4 * i + 3] = a3;
@@ -405,7 +405,7 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
         auto d2 = [&](int a, int b) {
             double x = cws_sh[3 * a] - cws_sh[3 * b], y = cws_sh[3 * a + 1] - cws_sh[3 * b + 1],
                    z = cws_sh[3 * a + 2] - cws_sh[3 * b + 2];
-            return x * x + y * y + z * z;
+            return ered3(x * x, y * y, z * z);  // squaredNorm of a row of cws (:640-645)
         };
         const SlabView SV{S};
         SV.rho(0) = d2(0, 1); SV.rho(1) = d2(0, 2); SV.rho(2) = d2(0, 3);

@@ -1253,10 +1253,11 @@ int rsc_sim3_create(rsc_context* C, const rsc_sim3_input* in, uint32_t seed, rsc
         s.indices1.push_back(i1);
         const float* a = &in->Xw1[3 * i1];
         const float* b = &in->Xw2[3 * i1];
+        // Rcw*X3Dw + tcw (Sim3Solver.cpp:58,62): Matrix3f * Vector3f, coefficient-path reductions
         for (int r = 0; r < 3; ++r)
-            S->X1c.push_back(in->R1[3 * r] * a[0] + in->R1[3 * r + 1] * a[1] + in->R1[3 * r + 2] * a[2] + in->t1[r]);
+            S->X1c.push_back(ered3(in->R1[3 * r] * a[0], in->R1[3 * r + 1] * a[1], in->R1[3 * r + 2] * a[2]) + in->t1[r]);
         for (int r = 0; r < 3; ++r)
-            S->X2c.push_back(in->R2[3 * r] * b[0] + in->R2[3 * r + 1] * b[1] + in->R2[3 * r + 2] * b[2] + in->t2[r]);
+            S->X2c.push_back(ered3(in->R2[3 * r] * b[0], in->R2[3 * r + 1] * b[1], in->R2[3 * r + 2] * b[2]) + in->t2[r]);
     }
     s.N = (int)s.indices1.size();
     std::memcpy(S->K1, in->K1, sizeof(S->K1));

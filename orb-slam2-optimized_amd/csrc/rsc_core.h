@@ -9,8 +9,10 @@
 //
 // Algorithms follow the reference solvers (src/PnPsolver.cpp, src/Sim3Solver.cpp) and the Eigen
 // routines they call (SelfAdjointEigenSolver, JacobiSVD+ColPivHouseholderQR, Matrix3d::inverse,
-// Quaternion::toRotationMatrix).  Arithmetic contract: every sum left to right in index
-// order, no FMA contraction (compiled with -ffp-contract=off), IEEE-correct division and sqrt.
+// Quaternion::toRotationMatrix).  Arithmetic contract: sums left to right in index
+// order except the 3-term reductions of fixed-size Eigen expressions, which follow Eigen 3.3 on the
+// reference's x86-64 SSE2 build (`ered3`, `emv3d_row` below); no FMA contraction (compiled with
+// -ffp-contract=off), IEEE-correct division and sqrt.
 //
 // The header is also compiled for the host by the test-only emulation library
 // (tests/hostemu/), so the device arithmetic can be checked against the oracle on a CPU.
@@ -50,6 +52,14 @@ template <> struct lim<float> {
 };
 
 RSC_HD double rsqrt_(double x) { return sqrt(x); }
+
+// 3-term reduction of a fixed-size Eigen expression that cannot use SIMD packets — a coefficient of
+// a product / dot / squared norm over a row of a column-major matrix, or any float 3-vector (3 < 4
+// lanes): Eigen's redux_novec_unroller halves the index range, a0 + (a1 + a2).
+template <typename S> RSC_HD S ered3(S a0, S a1, S a2) { return a0 + (a1 + a2); }
+// Row r of a Matrix3d * Vector3d assigned to a Vector3d: rows 0-1 are one Packet2d multiply-add
+// chain in index order, row 2 is the coefficient path.
+template <typename S> RSC_HD S emv3d_row(int r, S a0, S a1, S a2) { return r < 2 ? (a0 + a1) + a2 : ered3(a0, a1, a2); }
 
 // sqrt(x) for x in [1, 4) and 1/u for |u| in [1, 2), correctly rounded, with shorter chains (device).
 // The compiler's IEEE expansions add range handling around the core: sqrt scales x below 2^-767
@@ -955,9 +965,10 @@ RSC_HD void swap_remove_sample(const uint32_t* words, int ms, int N, int (&out)[
 // ---------------------------------------------------------------------------------------------
 RSC_HD bool pnp_inlier(const float (&R)[9], const float (&t)[3], double fx, double fy, double cx, double cy,
                        float X, float Y, float Z, float u, float v, float maxErr) {
-    float Xc = R[0] * X + R[1] * Y + R[2] * Z + t[0];
-    float Yc = R[3] * X + R[4] * Y + R[5] * Z + t[1];
-    float Zc = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    // mRi*p3Dw + mti (:250): Matrix3f * Vector3f, coefficient-path reductions
+    float Xc = ered3(R[0] * X, R[1] * Y, R[2] * Z) + t[0];
+    float Yc = ered3(R[3] * X, R[4] * Y, R[5] * Z) + t[1];
+    float Zc = ered3(R[6] * X, R[7] * Y, R[8] * Z) + t[2];
     float invZc = 1.0f / Zc;
     float ue = (float)(cx + fx * (double)Xc * (double)invZc);
     float ve = (float)(cy + fy * (double)Yc * (double)invZc);

@@ -111,9 +111,10 @@ RSC_HD void control_points_and_alphas(St& st, double (&cws)[4][3]) {
         double d0 = st.pw(i, 0) - cws[0][0];
         double d1 = st.pw(i, 1) - cws[0][1];
         double d2 = st.pw(i, 2) - cws[0][2];
-        double a1 = CCi[0][0] * d0 + CCi[0][1] * d1 + CCi[0][2] * d2;
-        double a2 = CCi[1][0] * d0 + CCi[1][1] * d1 + CCi[1][2] * d2;
-        double a3 = CCi[2][0] * d0 + CCi[2][1] * d1 + CCi[2][2] * d2;
+        // CC_inv.row(j).dot(pws.row(i) - cws.row(0)) (:338): rows of column-major matrices, ered3
+        double a1 = ered3(CCi[0][0] * d0, CCi[0][1] * d1, CCi[0][2] * d2);
+        double a2 = ered3(CCi[1][0] * d0, CCi[1][1] * d1, CCi[1][2] * d2);
+        double a3 = ered3(CCi[2][0] * d0, CCi[2][1] * d1, CCi[2][2] * d2);
         st.set_al(i, 1, a1);
         st.set_al(i, 2, a2);
         st.set_al(i, 3, a3);
@@ -180,7 +181,8 @@ RSC_HD void compute_L_6x10(const SV& S) {
         double dv[4][3];
         RSC_UNROLL for (int i = 0; i < 4; ++i)
             RSC_UNROLL for (int c = 0; c < 3; ++c) dv[i][c] = S.ev(3 * a + c, i) - S.ev(3 * b + c, i);
-        auto dot = [&](int x, int y) { return dv[x][0] * dv[y][0] + dv[x][1] * dv[y][1] + dv[x][2] * dv[y][2]; };
+        // dv[i].row(j).dot(...) (:626-635): rows of Matrix<double,6,3>, ered3
+        auto dot = [&](int x, int y) { return ered3(dv[x][0] * dv[y][0], dv[x][1] * dv[y][1], dv[x][2] * dv[y][2]); };
         S.L(j, 0) = dot(0, 0);
         S.L(j, 1) = 2.0 * dot(0, 1);
         S.L(j, 2) = dot(1, 1);
@@ -375,15 +377,17 @@ RSC_HD void horn_from_M(const double (&M)[3][3], const double (&pc0)[3], const d
     if (det3(R) < 0) {
         RSC_UNROLL for (int c = 0; c < 3; ++c) R[2][c] = -R[2][c];
     }
-    RSC_UNROLL for (int r = 0; r < 3; ++r) t[r] = pc0[r] - (R[r][0] * pw0[0] + R[r][1] * pw0[1] + R[r][2] * pw0[2]);
+    // t = pc0 - R*pw0 (:492) into a Vector3d: emv3d_row
+    RSC_UNROLL for (int r = 0; r < 3; ++r) t[r] = pc0[r] - emv3d_row(r, R[r][0] * pw0[0], R[r][1] * pw0[1], R[r][2] * pw0[2]);
 }
 
 // One term of reprojection_error (:417-431).
 RSC_HD double reproj_term(const double (&R)[3][3], const double (&t)[3], const Intrinsics& K, double P0, double P1,
                           double P2, double u0, double u1) {
-    double X = R[0][0] * P0 + R[0][1] * P1 + R[0][2] * P2 + t[0];
-    double Y = R[1][0] * P0 + R[1][1] * P1 + R[1][2] * P2 + t[1];
-    double Z = R[2][0] * P0 + R[2][1] * P1 + R[2][2] * P2 + t[2];
+    // R*pws.row(i).transpose() + t (:423) into a Vector3d: emv3d_row
+    double X = emv3d_row(0, R[0][0] * P0, R[0][1] * P1, R[0][2] * P2) + t[0];
+    double Y = emv3d_row(1, R[1][0] * P0, R[1][1] * P1, R[1][2] * P2) + t[1];
+    double Z = emv3d_row(2, R[2][0] * P0, R[2][1] * P1, R[2][2] * P2) + t[2];
     double inv_Zc = 1.0 / Z;
     double u = K.cx + K.fx * X * inv_Zc;
     double v = K.cy + K.fy * Y * inv_Zc;
@@ -457,7 +461,7 @@ RSC_HD double epnp_betas_and_pose(const St& st, const Intrinsics& K, const SV& S
     {
         auto d2 = [&](int a, int b) {
             double x = cws[a][0] - cws[b][0], y = cws[a][1] - cws[b][1], z = cws[a][2] - cws[b][2];
-            return x * x + y * y + z * z;
+            return ered3(x * x, y * y, z * z);  // squaredNorm of a row of cws (:640-645)
         };
         S.rho(0) = d2(0, 1); S.rho(1) = d2(0, 2); S.rho(2) = d2(0, 3);
         S.rho(3) = d2(1, 2); S.rho(4) = d2(1, 3); S.rho(5) = d2(2, 3);

@@ -557,7 +557,7 @@ __device__ __forceinline__ void pnp_betas_wave_body(const DevPnP* __restrict__ p
             RSC_UNROLL for (int c = 0; c < 3; ++c) cws[i][c] = in[kStCws + i * 3 + c];
         auto d2 = [&](int a, int b) {
             double x = cws[a][0] - cws[b][0], y = cws[a][1] - cws[b][1], z = cws[a][2] - cws[b][2];
-            return x * x + y * y + z * z;
+            return ered3(x * x, y * y, z * z);  // squaredNorm of a row of cws (:640-645)
         };
         V.rho(0) = d2(0, 1); V.rho(1) = d2(0, 2); V.rho(2) = d2(0, 3);
         V.rho(3) = d2(1, 2); V.rho(4) = d2(1, 3); V.rho(5) = d2(2, 3);

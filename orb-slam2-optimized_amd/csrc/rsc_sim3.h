@@ -15,15 +15,15 @@ struct Sim3Pose {
 RSC_HD void sim3_compute(const float (&P1)[3][3], const float (&P2)[3][3], Sim3Pose& T) {
     float O1[3], O2[3], Pr1[3][3], Pr2[3][3];
     RSC_UNROLL for (int r = 0; r < 3; ++r) {
-        O1[r] = P1[r][0] + P1[r][1] + P1[r][2];
-        O2[r] = P2[r][0] + P2[r][1] + P2[r][2];
+        O1[r] = ered3(P1[r][0], P1[r][1], P1[r][2]);  // P.rowwise().sum() (:188)
+        O2[r] = ered3(P2[r][0], P2[r][1], P2[r][2]);
     }
     RSC_UNROLL for (int r = 0; r < 3; ++r) { O1[r] = O1[r] / 3.f; O2[r] = O2[r] / 3.f; }
     RSC_UNROLL for (int i = 0; i < 3; ++i)
         RSC_UNROLL for (int r = 0; r < 3; ++r) { Pr1[r][i] = P1[r][i] - O1[r]; Pr2[r][i] = P2[r][i] - O2[r]; }
     float M[3][3];
     RSC_UNROLL for (int a = 0; a < 3; ++a)
-        RSC_UNROLL for (int b = 0; b < 3; ++b) M[a][b] = Pr2[a][0] * Pr1[b][0] + Pr2[a][1] * Pr1[b][1] + Pr2[a][2] * Pr1[b][2];
+        RSC_UNROLL for (int b = 0; b < 3; ++b) M[a][b] = ered3(Pr2[a][0] * Pr1[b][0], Pr2[a][1] * Pr1[b][1], Pr2[a][2] * Pr1[b][2]);
     const float N11 = M[0][0] + M[1][1] + M[2][2];
     const float N12 = M[1][2] - M[2][1];
     const float N13 = M[2][0] - M[0][2];
@@ -40,19 +40,19 @@ RSC_HD void sim3_compute(const float (&P1)[3][3], const float (&P2)[3][3], Sim3P
     float R[3][3];
     quat_to_R<float>(V[0][3], V[1][3], V[2][3], V[3][3], R);  // not conjugated (:243-246)
     RSC_UNROLL for (int r = 0; r < 3; ++r) {
-        T.t12[r] = O1[r] - (R[r][0] * O2[0] + R[r][1] * O2[1] + R[r][2] * O2[2]);
+        T.t12[r] = O1[r] - ered3(R[r][0] * O2[0], R[r][1] * O2[1], R[r][2] * O2[2]);
         RSC_UNROLL for (int c = 0; c < 3; ++c) { T.R12[3 * r + c] = R[r][c]; T.R21[3 * c + r] = R[r][c]; }
     }
     RSC_UNROLL for (int r = 0; r < 3; ++r)
-        T.t21[r] = -(T.R21[3 * r + 0] * T.t12[0] + T.R21[3 * r + 1] * T.t12[1] + T.R21[3 * r + 2] * T.t12[2]);
+        T.t21[r] = -ered3(T.R21[3 * r + 0] * T.t12[0], T.R21[3 * r + 1] * T.t12[1], T.R21[3 * r + 2] * T.t12[2]);
 }
 
 // Sim3Solver::Project of one point (Rcw = Tcw.rotation() taken as linear(), Q14).
 RSC_HD void sim3_project(const float (&R)[9], const float (&t)[3], float fx, float fy, float cx, float cy,
                          float X, float Y, float Z, float& u, float& v) {
-    float x3 = R[0] * X + R[1] * Y + R[2] * Z + t[0];
-    float y3 = R[3] * X + R[4] * Y + R[5] * Z + t[1];
-    float z3 = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    float x3 = ered3(R[0] * X, R[1] * Y, R[2] * Z) + t[0];  // Rcw*P3Dw + tcw (:320)
+    float y3 = ered3(R[3] * X, R[4] * Y, R[5] * Z) + t[1];
+    float z3 = ered3(R[6] * X, R[7] * Y, R[8] * Z) + t[2];
     const float invz = 1.0f / z3;
     const float x = x3 * invz;
     const float y = y3 * invz;

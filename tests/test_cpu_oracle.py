@@ -97,7 +97,29 @@ def test_svd_solve_vs_numpy(k):
     assert np.allclose(ol.svd_solve(A, b), np.linalg.pinv(A) @ b, atol=1e-10)
 
 
-@pytest.mark.parametrize("n", [4, 5, 6, 10, 50, 500])
+def test_epnp_known_answer_minimal_is_basis_dependent():
+    """n = 4 (the RANSAC sample): M is 8 x 12, so MtM has an exact 4-dimensional null space whose
+    eigenvector basis is fixed by rounding alone, and find_betas_approx_1/2/3 keep only
+    some of the 10 beta products — whether Gauss-Newton then reaches the true pose depends on that
+    basis.  Over 200 noise-free scenes the restatement recovers it about 45 % of the time (the rounds
+    1-3 left-to-right order: about 42 %), so the known answer is a rate, not a per-sample property;
+    n >= 5 recovers it always (test_epnp_known_answer)."""
+    ok = 0
+    for k in range(200):
+        rng = np.random.default_rng(4000 + k)
+        sc = synth.make_pnp_scene(rng, 60, 1.0, noise=False)
+        o = ol.OraclePnP(sc, 1)
+        o.set_ransac_parameters(0.99, 10, 300, 4, 0.5, 5.991)
+        idx = np.sort(rng.choice(sc.n, 4, replace=False)).astype(np.int32)
+        R, t, err = o.compute_pose(idx)
+        good = np.abs(R - sc.R_true).max() < 2e-5 and np.abs(t - sc.t_true).max() < 2e-4
+        ok += good
+        if good:
+            assert err < 0.05  # pixels; float-rounded inputs
+    assert 0.3 < ok / 200 < 0.7
+
+
+@pytest.mark.parametrize("n", [5, 6, 10, 50, 500])
 def test_epnp_known_answer(n):
     """Noise-free correspondences: EPnP (compute_pose, PnPsolver.cpp:359-415) recovers Tcw."""
     rng = np.random.default_rng(100 + n)
@@ -201,8 +223,11 @@ def test_q8_refine_strictness_and_q12_first_success():
                 assert row[8] >= mi and row[11] == (row[10] > mi)
             else:
                 assert row[8] < mi
-        if r["ok"]:
-            assert ints[-1, 11] == 1 and r["n_inliers"] == ints[-1, 10]
+        if r["ok"] and ints[-1, 11] == 1:  # returned by a successful Refine (:159-166)
+            assert r["n_inliers"] == ints[-1, 10]
+        elif r["ok"]:  # budget exhausted, best >= minInliers returned (:173-188)
+            assert r["no_more"] and len(ints) == o.info()["max_iterations"] or len(ints) == 300
+            assert r["n_inliers"] == o.info()["best_inliers"] >= mi
     pair = synth.make_sim3_pair(rng, 500, 200)
     s = ol.OracleSim3(pair, 3)
     s.set_ransac_parameters(0.99, 20, 300)

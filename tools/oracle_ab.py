@@ -114,8 +114,12 @@ def compare(a_path, b_path):
         same_count = ia[..., -1] == ib[..., -1] if tag == "c2x" else ia[..., 3] == ib[..., 3]
         finite = np.isfinite(pa).all(-1) & np.isfinite(pb).all(-1)
         dpose = np.abs(pa.astype(np.float64) - pb.astype(np.float64)).max(-1)
+        cc = np.argwhere(~same_count)
         rep[tag] = dict(hypotheses=int(same_bits.size), pose_bits_changed=int((~same_bits).sum()),
                         count_changed=int((~same_count).sum()),
+                        count_changed_first50=[[int(a), int(b)] for a, b in cc[:50]],  # (problem, hypothesis)
+                        max_abs_count_diff=int(np.abs(ia[..., -1 if tag == "c2x" else 3].astype(np.int64)
+                                                      - ib[..., -1 if tag == "c2x" else 3]).max()),
                         max_abs_pose_diff=float(dpose[finite].max()) if finite.any() else 0.0,
                         pose_within_1em4=float(np.mean(dpose[finite] <= 1e-4)) if finite.any() else 1.0,
                         count_agreement=float(np.mean(same_count)))
@@ -123,10 +127,16 @@ def compare(a_path, b_path):
         ra, rb = A[tag + "_rec"], B[tag + "_rec"]
         ma, mb = A[tag + "_masks"], B[tag + "_masks"]
         d = dict(problems=int(len(ra)), outcome_agreement=_agree(ra, rb), mask_agreement=_agree(ma, mb))
+        bad = ~np.all(ra == rb, axis=1) | ~np.all(ma.reshape(len(ma), -1) == mb.reshape(len(mb), -1), axis=1)
+        d["mismatching_problems"] = [int(i) for i in np.flatnonzero(bad)]
+        d["records_a_b"] = {int(i): [ra[i].tolist(), rb[i].tolist()] for i in np.flatnonzero(bad)}
         if tag == "c2p":
             Ta, Tb = A["c2p_T"], B["c2p_T"]
+            dT = np.abs(Ta.astype(np.float64) - Tb).max(-1)
             d["pose_bits_agreement"] = _agree(Ta.view(np.uint32), Tb.view(np.uint32))
-            d["pose_within_1em4"] = float(np.mean(np.abs(Ta - Tb).max(-1) <= 1e-4))
+            d["pose_within_1em4"] = float(np.mean(dT <= 1e-4))
+            d["max_abs_pose_diff"] = float(dT.max())
+            d["median_abs_pose_diff_of_mismatches"] = float(np.median(dT[bad])) if bad.any() else 0.0
         rep[tag] = d
     ea, eb = A["c5_records"], B["c5_records"]
     same = np.all(ea[:, :5] == eb[:, :5], axis=1)
