@@ -527,10 +527,11 @@ void PnPOracle::gauss_newton(const double L[6][10], const double rho[6], double 
 #ifdef ORA_QR_STATS
 // tools/q19_stats.py: how often the last row is a column's strict maximum (the scans where Q19's eta
 // differs from a six-row eta).  Only in the instrumented build (-DORA_QR_STATS).
-static long g_qr_calls = 0, g_qr_row5[4] = {0, 0, 0, 0};
+static long g_qr_calls = 0, g_qr_row5[4] = {0, 0, 0, 0}, g_qr_singular = 0;
 extern "C" void ora_qr_stats(long* o) {
     o[0] = g_qr_calls;
     for (int k = 0; k < 4; ++k) o[1 + k] = g_qr_row5[k];
+    o[5] = g_qr_singular;
 }
 #endif
 bool PnPOracle::qr_solve(double A[6][4], double b[6], double X[4]) {
@@ -556,6 +557,9 @@ bool PnPOracle::qr_solve(double A[6][4], double b[6], double X[4]) {
         }
         if (eta == 0) {
             A1[k] = A2[k] = 0.0;
+#ifdef ORA_QR_STATS
+            ++g_qr_singular;
+#endif
             return false;  // "A is singular" (:722-726)
         }
         double sum = 0.0, inv_eta = 1. / eta;

@@ -226,6 +226,21 @@ RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, int (&per
         //   ->  start = 1 + last zero index below end - 1, or 0
         const unsigned zero = ~nz & ((1u << (end - 1)) - 1u);
         start = zero ? 32 - __builtin_clz(zero) : 0;
+#ifndef RSC_NO_NAN_EXIT
+        // Non-finite block (Q4: a coplanar sample's NaN control points): when diag[start..end] and
+        // sub[start..end-1] are all NaN, no entry deflates and Eigen's loop runs to maxIterations*n
+        // sweeps (360 at n = 12).  This sweep's rotations are all NaN (make_givens(NaN, NaN)), so it
+        // turns Q's columns start..end into NaN; every later sweep maps that state onto itself
+        // (NaN in, NaN out; the block cannot change: its sub-diagonal never reads 0).  Ending after
+        // this sweep with Eigen's NoConvergence (no sort) therefore returns Eigen's final state.
+        unsigned dnan = 0u, snan = 0u;
+        RSC_UNROLL for (int i = 0; i < n; ++i) dnan |= (diag[i] != diag[i]) ? (1u << i) : 0u;
+        RSC_UNROLL for (int i = 0; i < n - 1; ++i) snan |= (sub[i] != sub[i]) ? (1u << i) : 0u;
+        const unsigned lo = (1u << start) - 1u;
+        const unsigned blk_d = ((2u << end) - 1u) & ~lo, blk_s = ((1u << end) - 1u) & ~lo;
+        const bool dead = ((dnan & blk_d) == blk_d) & ((snan & blk_s) == blk_s);
+        iter = dead ? maxIterations * n : iter;  // the next loop test ends it, not converged
+#endif
         // ---- tridiagonal_qr_step(diag, sub, start, end) ----
         S dEm1 = S(0), dE = S(0), eE = S(0), dS = S(0), zS = S(0);
         RSC_UNROLL for (int j = 1; j < n; ++j) {

@@ -109,6 +109,90 @@ def make_pnp_scene(rng: np.random.Generator, n: int, inlier_ratio: float, noise:
                     n_points=int(n_points), R_true=R, t_true=t, inlier_true=inl)
 
 
+def _observe(rng, R, t, Xw, inlier_ratio, noise, n_points):
+    """Projections of world points Xw (float64 [n,3]) by Tcw = (R, t) as a PnPScene: inliers noisy
+    by sigma(level), outliers uniform in the image (as make_pnp_scene)."""
+    n = len(Xw)
+    Xc = Xw @ R.T + t
+    fx, fy, cx, cy = float(FX), float(FY), float(CX), float(CY)
+    u = fx * Xc[:, 0] / Xc[:, 2] + cx
+    v = fy * Xc[:, 1] / Xc[:, 2] + cy
+    levels = rng.choice(N_LEVELS, size=n, p=level_probabilities())
+    s2 = level_sigma2()[levels]
+    n_in = int(round(inlier_ratio * n))
+    inl = np.zeros(n, dtype=bool)
+    inl[rng.permutation(n)[:n_in]] = True
+    if noise:
+        sig = np.sqrt(s2.astype(np.float64))
+        u[inl] += rng.normal(size=n_in) * sig[inl]
+        v[inl] += rng.normal(size=n_in) * sig[inl]
+    u[~inl] = rng.uniform(0, WIDTH, size=n - n_in)
+    v[~inl] = rng.uniform(0, HEIGHT, size=n - n_in)
+    n_points = n if n_points is None else n_points
+    kp = np.sort(rng.choice(n_points, size=n, replace=False)).astype(np.int32) if n_points > n \
+        else np.arange(n, dtype=np.int32)
+    return PnPScene(p2d=np.stack([u, v], 1).astype(np.float32), p3dw=Xw.astype(np.float32),
+                    sigma2=s2.astype(np.float32), kp_index=kp, n_points=int(n_points), R_true=R, t_true=t,
+                    inlier_true=inl)
+
+
+def make_planar_pnp_scene(rng: np.random.Generator, n: int, inlier_ratio: float, plane: str = "floor",
+                          noise: bool = True, n_points: int | None = None) -> PnPScene:
+    """Relocalization candidate whose map points lie on one plane — the walls and floors of EuRoC's
+    rooms, which make_pnp_scene avoids by drawing a frustum volume.
+
+    plane = "floor": world Y = 1.5 exactly (representable), so every 4-point sample is exactly
+            coplanar in float: the PCA's smallest eigenvalue is 0 (or a rounding residue of either
+            sign), sqrt(lambda / n) and the 3x3 inverse of the control points give NaN or inf, and
+            the hypothesis ends with NaN poses and 0 inliers (Q4, PnPsolver.cpp:311-331);
+    plane = "wall":  world Z = 6 exactly (the same, facing the camera);
+    plane = "tilted": a random plane through the view, coplanar up to float rounding (ill-conditioned
+            but mostly finite samples);
+    plane = "duplicates": a frustum scene in which 25 % of the correspondences repeat another one
+            exactly (3D and 2D), so samples with repeated points are rank-deficient.
+    The camera looks at the plane from 1.5-9 m; points outside the image are redrawn."""
+    if plane == "duplicates":
+        sc = make_pnp_scene(rng, n, inlier_ratio, noise=noise, n_points=n_points)
+        k = n // 4
+        src = rng.choice(n - k, size=k)
+        dst = n - k + np.arange(k)
+        for a in (sc.p2d, sc.p3dw, sc.sigma2):
+            a[dst] = a[src]
+        sc.inlier_true[dst] = sc.inlier_true[src]
+        return sc
+    R = random_rotation(rng, 0.25)
+    t = rng.uniform(-0.5, 0.5, size=3)
+    if plane == "tilted":
+        nrm = np.array([0.0, -1.0, -0.4]) + rng.normal(size=3) * 0.3
+        nrm /= np.linalg.norm(nrm)
+        e1 = np.cross(nrm, [1.0, 0.0, 0.0])
+        e1 /= np.linalg.norm(e1)
+        e2 = np.cross(nrm, e1)
+        p0 = R.T @ (np.array([0.0, 0.5, 5.0]) - t)
+    pts = []
+    while sum(len(p) for p in pts) < n:
+        m = 4 * n
+        if plane == "floor":
+            W = np.stack([rng.uniform(-6, 6, m), np.full(m, 1.5), rng.uniform(0.5, 12, m)], 1)
+        elif plane == "wall":
+            W = np.stack([rng.uniform(-6, 6, m), rng.uniform(-4, 4, m), np.full(m, 6.0)], 1)
+        elif plane == "tilted":
+            a, b = rng.uniform(-6, 6, m), rng.uniform(-6, 6, m)
+            W = p0 + a[:, None] * e1 + b[:, None] * e2
+        else:
+            raise ValueError(plane)
+        W = W.astype(np.float32).astype(np.float64)
+        Xc = W @ R.T + t
+        z = Xc[:, 2]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            u = float(FX) * Xc[:, 0] / z + float(CX)
+            v = float(FY) * Xc[:, 1] / z + float(CY)
+        ok = (z > 1.5) & (z < 9.0) & (u >= 0) & (u < WIDTH) & (v >= 0) & (v < HEIGHT)
+        pts.append(W[ok])
+    Xw = np.concatenate(pts)[:n]
+    return _observe(rng, R, t, Xw, inlier_ratio, noise, n_points)
+
+
 @dataclasses.dataclass
 class Sim3Pair:
     """Raw Sim3Solver constructor inputs (Sim3Solver.cpp:6-85) for one keyframe pair."""
@@ -131,12 +215,17 @@ class Sim3Pair:
 
 
 def make_sim3_pair(rng: np.random.Generator, n1: int, n_inliers: int, invalid_frac: float = 0.0,
-                   noise3d: float = 0.01) -> Sim3Pair:
+                   noise3d: float = 0.01, degenerate: str | None = None) -> Sim3Pair:
     """Two keyframes seeing the same points; map 2 carries a rigid loop drift (Rd, td).
 
     Physical point P: Xw1 = P (+noise), Xw2 = Rd P + td (+noise).  KF1: Xc1 = R1 P + t1.
     KF2 is displaced by (Rrel, trel) from KF1, expressed in map-2 coordinates, so that
     Xc2 = Rrel Xc1 + trel for inliers.  Outliers of map 2 are unrelated points in front of KF2.
+
+    degenerate = "collinear": 40 % of the matches lie on one 3D line (a pole, a door edge) in
+    both maps, so 3-point samples drawn from them are collinear (Horn's M has rank 1, the 4x4 N
+    repeated eigenvalues: Sim3Solver.cpp:139-151, :196-266); "duplicates": 30 % of the matches
+    repeat another match exactly, so samples can hold the same point twice.
     """
     R1 = random_rotation(rng, 0.3)
     t1 = rng.uniform(-1, 1, size=3)
@@ -152,8 +241,22 @@ def make_sim3_pair(rng: np.random.Generator, n1: int, n_inliers: int, invalid_fr
     d = rng.uniform(1.0, 8.0, size=n1)
     Xc1 = np.stack([(u - cx) / fx * d, (v - cy) / fy * d, d], axis=1)
     P = (Xc1 - t1) @ R1
+    if degenerate == "collinear":
+        k = (2 * n1) // 5
+        a = P[0]
+        dirn = rng.normal(size=3)
+        dirn /= np.linalg.norm(dirn)
+        P[:k] = a + rng.uniform(-1.0, 1.0, size=k)[:, None] * dirn
     Xw1 = P + rng.normal(size=P.shape) * noise3d
     Xw2 = P @ Rd.T + td + rng.normal(size=P.shape) * noise3d
+    if degenerate == "collinear":  # exactly collinear in both maps (no 3D noise on the line)
+        Xw1[:k] = P[:k]
+        Xw2[:k] = P[:k] @ Rd.T + td
+    if degenerate == "duplicates":
+        k = (3 * n1) // 10
+        src = rng.choice(n1 - k, size=k)
+        Xw1[n1 - k:] = Xw1[src]
+        Xw2[n1 - k:] = Xw2[src]
     inl = np.zeros(n1, dtype=bool)
     inl[rng.permutation(n1)[:n_inliers]] = True
     nout = int((~inl).sum())

@@ -50,6 +50,38 @@ def test_hypotheses_bitexact(ms, k):
             break  # the oracle's Refine changes the EPnP buffers for later hypotheses
 
 
+def _nan_equal(a, b):
+    a = np.ascontiguousarray(a, np.float32).ravel()
+    b = np.ascontiguousarray(b, np.float32).ravel()
+    na, nb = np.isnan(a), np.isnan(b)
+    return np.array_equal(na, nb) and np.array_equal(a.view(np.uint32)[~na], b.view(np.uint32)[~nb])
+
+
+@pytest.mark.parametrize("plane", ["floor", "wall", "tilted"])
+def test_planar_hypotheses_nan_exit_bitexact(plane):
+    """Coplanar samples (Q4): NaN control points, a 12x12 / 4x4 eigen-solve that never deflates.
+    The product's QR sweep ends after the first all-NaN sweep (rsc_core.h tridiag_qr), the oracle
+    runs Eigen's full 30 n sweeps: the poses must agree (NaN as NaN) and the counts exactly."""
+    rng = np.random.default_rng({"floor": 1, "wall": 2, "tilted": 3}[plane])
+    sc = synth.make_planar_pnp_scene(rng, 300, 0.7, plane)
+    o = ol.OraclePnP(sc, 7)
+    o.set_ransac_parameters(*RELOC)
+    o.enable_trace()
+    o.iterate(40)
+    ints, fl = o.trace()
+    n_nan = 0
+    for h in range(len(ints)):
+        idx, R, t = he.pnp_hypothesis(sc, 7, h)
+        assert np.array_equal(idx, ints[h, :4]), h
+        assert _nan_equal(np.concatenate([R.ravel(), t]), fl[h]), h
+        c, _ = he.pnp_count(sc, R, t)
+        assert c == ints[h, 8], h
+        n_nan += bool(np.isnan(fl[h]).any())
+        if ints[h, 9]:
+            break
+    assert n_nan > 0
+
+
 def test_refine_rows_and_stale_rows_bitexact():
     rng = np.random.default_rng(5)
     sc = synth.make_pnp_scene(rng, 400, 0.6)

@@ -31,21 +31,29 @@ def main(r3, r4, out):
     L = ol.lib()
     L.ora_qr_stats.argtypes = [ctypes.POINTER(ctypes.c_long)]
     rep = {}
-    prev = [0] * 5
-    for name, ratio in (("config2_exhaustive", 0.4), ("config2_parity", 0.6)):
-        scenes = W.config2_scenes(ratio=ratio)
-        for sc, s in zip(scenes, W.config2_seeds(0)):
+    from rsc import synth
+    import numpy as np
+    prev = [0] * 6
+    work = [("config2_exhaustive", lambda: W.config2_scenes(ratio=0.4)),
+            ("config2_parity", lambda: W.config2_scenes(ratio=0.6))]
+    for plane in ("floor", "wall", "tilted", "duplicates"):
+        work.append((f"planar_{plane}_16x2000", lambda p=plane: [
+            synth.make_planar_pnp_scene(np.random.default_rng(300 + i), 2000, 0.6, p) for i in range(16)]))
+    for name, make in work:
+        scenes = make()
+        for sc, s in zip(scenes, W.config2_seeds(0, candidates=len(scenes))):
             o = ol.OraclePnP(sc, int(s))
             o.set_ransac_parameters(*W.RELOC)
             o.iterate(300)
-        c = (ctypes.c_long * 5)()
+        c = (ctypes.c_long * 6)()
         L.ora_qr_stats(c)
         cur = list(c)
         d = [a - b for a, b in zip(cur, prev)]
         prev = cur
         rep[name] = dict(qr_solve_calls=d[0], column_scans=4 * d[0],
-                         scans_row5_strict_max=sum(d[1:]), by_column=d[1:],
-                         fraction_of_scans=sum(d[1:]) / max(1, 4 * d[0]))
+                         scans_row5_strict_max=sum(d[1:5]), by_column=d[1:5],
+                         fraction_of_scans=sum(d[1:5]) / max(1, 4 * d[0]),
+                         singular_bailouts=d[5])
     rep["round3_vs_round4_oracle"] = oracle_ab.compare(r3, r4)
     rep["note"] = ("Q19 changes the double-precision Gauss-Newton iterates whenever row 5 is a column's "
                    "strict maximum; the float poses returned by compute_pose (cast at PnPsolver.cpp:411-412) "
