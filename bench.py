@@ -254,10 +254,15 @@ def run_pnp(engine, ctx, scenes, cand_ids, args, dist, rank, world):
         import torch
         from rsc import dist as rdist
         maxc = args.candidates  # fixed block per rank (strong-mode shards may differ by one)
-        rec = torch.zeros(maxc, rdist.RECORD, dtype=torch.float32, device=COLL_DEV)
-        allrec = torch.zeros(world * maxc, rdist.RECORD, dtype=torch.float32, device=COLL_DEV)
-        host = np.full((maxc, rdist.RECORD), -1.0, np.float32)
-        gather = (torch, rec, allrec, host)
+        # one int32 payload per rank (rsc.dist.all_gather_records_and_mask's layout): the result
+        # records, then the candidate of this rank that can win and its vbInliers as a bitset
+        words = (max(sc.n_points for sc in scenes) + 31) // 32
+        per = maxc * rdist.RECORD + 1 + words
+        rec = torch.zeros(per, dtype=torch.int32, device=COLL_DEV)
+        allrec = torch.zeros(world * per, dtype=torch.int32, device=COLL_DEV)
+        host = np.full(per, -1, np.int32)
+        hrec = host[:maxc * rdist.RECORD].view(np.float32).reshape(maxc, rdist.RECORD)
+        gather = (torch, rec, allrec, host, hrec, maxc * rdist.RECORD, rdist)
 
     def step(s):
         if args.strong:
@@ -268,13 +273,21 @@ def run_pnp(engine, ctx, scenes, cand_ids, args, dist, rank, world):
         batch.set_ransac_parameters(*wl.RELOC)
         outs = batch.iterate_raw(args.iters)
         if gather is not None:
-            torch, rec, allrec, host = gather
-            host[:C, 0] = cand_ids
-            host[:C, 1], host[:C, 2], host[:C, 3], host[:C, 4] = (outs["ok"], outs["no_more"], outs["n_inliers"],
+            torch, rec, allrec, host, hrec, mo, rdist = gather
+            hrec[:C, 0] = cand_ids
+            hrec[:C, 1], hrec[:C, 2], hrec[:C, 3], hrec[:C, 4] = (outs["ok"], outs["no_more"], outs["n_inliers"],
                                                                   outs["iterations"])
-            host[:C, 5:21] = outs["T"].reshape(C, 16)
+            hrec[:C, 5:21] = outs["T"].reshape(C, 16)
+            ok = np.flatnonzero(outs["ok"])
+            host[mo] = cand_ids[ok[0]] if len(ok) else -1  # rsc.dist.local_reloc_candidate
+            host[mo + 1:] = 0
+            if len(ok):  # the winner's vbInliers (exhaustive mode never has one)
+                m = np.zeros((len(host) - mo - 1) * 32, np.uint8)
+                v = solvers[ok[0]].last_inliers()
+                m[:len(v)] = v
+                host[mo + 1:] = np.packbits(m, bitorder="little").view(np.int32)
             rec.copy_(torch.from_numpy(host))
-            dist.all_gather_into_tensor(allrec, rec)  # RCCL over xGMI: result records of all ranks
+            dist.all_gather_into_tensor(allrec, rec)  # RCCL over xGMI: records + winner mask of all ranks
             if COLL_DEV == "cuda":
                 torch.cuda.synchronize()
         return int(outs["iterations"].sum()), outs
@@ -729,9 +742,23 @@ def rccl_check(engine, ctx, args):
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     got = out.cpu().numpy()
+    # the records + winner-mask exchange (rsc.dist.all_gather_records_and_mask) on device, with a
+    # parity-mode batch so that a winner exists
+    ps = wl.config2_scenes(0, 8, args.corrs, ratio=0.7, seed=4242)
+    sol = [engine.PnPSolver(ctx, sc, 1 + i) for i, sc in enumerate(ps)]
+    b2 = engine.SolverBatch(sol)
+    b2.set_ransac_parameters(*wl.RELOC)
+    rec2 = rdist.pack_pnp(list(range(len(ps))), b2.iterate_raw(args.iters))
+    c = rdist.local_reloc_candidate(rec2)
+    mask = sol[c].last_inliers() if c >= 0 else None
+    r2, m2 = rdist.all_gather_records_and_mask(RCCL1, rec2, len(ps), c, mask, ps[0].n_points, device="cuda")
+    mask_ok = bool(np.array_equal(r2.view(np.uint32), rec2.view(np.uint32)) and
+                   (c < 0 or (c in m2 and np.array_equal(m2[c], mask))))
     return {"executed": True, "backend": RCCL1.get_backend(), "world": RCCL1.get_world_size(),
             "records": int(rec.shape[0]), "bytes": int(rec.nbytes),
             "records_bitequal": bool(np.array_equal(got.view(np.uint32), rec.view(np.uint32))),
+            "winner_mask_exchange": {"winner": int(c), "bitequal": mask_ok,
+                                     "inliers": int(mask.sum()) if mask is not None else 0},
             "all_gather_us_median": round(1e6 * float(np.median(times[5:])), 2),
             "note": "all_gather_into_tensor of the config-2 result records on device, world 1 (RCCL); "
                     "multi-GPU curves come from the driver's N=2/4/8 runs"}

@@ -94,6 +94,11 @@ int rsc_pnp_set_ransac_parameters(rsc_pnp* s, double probability, int min_inlier
 int rsc_pnp_iterate(rsc_pnp* s, int n_iterations, rsc_pnp_result* out, uint8_t* inliers);
 /* PnPsolver::find (PnPsolver.cpp:96-100). */
 int rsc_pnp_find(rsc_pnp* s, rsc_pnp_result* out, uint8_t* inliers);
+/* vbInliers of the last iterate() / find() of this solver (n_points bytes; mvbRefinedInliers or
+ * mvbBestInliers scattered through the keypoint indices, PnPsolver.cpp:159-166, :176-186), fetched
+ * after the call — e.g. for the candidate a rank contributes to the multi-GPU winner exchange.
+ * Returns 1, or 0 with all-zero bytes when that call returned false (vbInliers empty, :105). */
+int rsc_pnp_last_inliers(rsc_pnp* s, uint8_t* out);
 /* iterate() on `count` solvers of ONE context at once (the relocalization candidates of
  * Tracking.cpp:1239-1334); all hypotheses of all solvers run in the same kernel launches.
  * Results are identical to calling rsc_pnp_iterate on each solver in order. */

@@ -220,6 +220,7 @@ struct rsc_pnp {
     uint64_t* d_best = nullptr;
     uint64_t* d_refined = nullptr;
     int words = 0;
+    int last_kind = 0;  // vbInliers of the last iterate(): 0 empty, 1 refined mask, 2 best mask
     // position in the last speculation of its context
     int spec_out0 = -1, spec_H = 0;
     ~rsc_pnp() {
@@ -1168,7 +1169,10 @@ int rsc_pnp_iterate_many(rsc_pnp* const* solvers, int count, const int32_t* n_it
     std::vector<PnPResult> res(count);
     int st = pnp_iterate_many(be, S.data(), count, its.data(), res.data(), inliers);
     if (st) return st;
-    for (int i = 0; i < count; ++i) to_result(res[i], &out[i]);
+    for (int i = 0; i < count; ++i) {
+        to_result(res[i], &out[i]);
+        solvers[i]->last_kind = res[i].mask_kind;
+    }
     host_mark(C, 3);
     return RSC_OK;
 }
@@ -1189,6 +1193,20 @@ int rsc_pnp_iterate(rsc_pnp* s, int n_its, rsc_pnp_result* out, uint8_t* inliers
 int rsc_pnp_find(rsc_pnp* s, rsc_pnp_result* out, uint8_t* inliers) {
     if (!s) return RSC_ERR_ARG;
     return rsc_pnp_iterate(s, s->st.mRansacMaxIts, out, inliers);
+}
+
+int rsc_pnp_last_inliers(rsc_pnp* s, uint8_t* out) {
+    if (!s || !out) return RSC_ERR_ARG;
+    const PnPState& t = s->st;
+    std::memset(out, 0, (size_t)t.N_points);
+    if (s->last_kind == 0) return 0;
+    std::vector<uint64_t> w((size_t)s->words);
+    RSC_HIP(hipMemcpyAsync(w.data(), s->last_kind == 1 ? s->d_refined : s->d_best, (size_t)s->words * 8,
+                           hipMemcpyDeviceToHost, s->ctx->stream));
+    RSC_HIP(hipStreamSynchronize(s->ctx->stream));
+    for (int j = 0; j < t.N; ++j)
+        if ((w[j >> 6] >> (j & 63)) & 1ull) out[t.kp_index[j]] = 1;
+    return 1;
 }
 
 int rsc_pnp_reset(rsc_pnp* s, uint32_t seed) {

@@ -83,6 +83,67 @@ def all_gather_records(dist, records: np.ndarray, max_per_rank: int, device=None
     return allr[np.argsort(allr[:, 0], kind="stable")]
 
 
+def local_reloc_candidate(records: np.ndarray) -> int:
+    """The only candidate of this rank's contiguous block that can be the relocalization winner:
+    its lowest-index successful one (Tracking.cpp:1241-1265), or -1."""
+    ok = records[records[:, 1] > 0] if len(records) else records
+    return int(ok[0, 0]) if len(ok) else -1
+
+
+def local_loop_candidate(records: np.ndarray) -> int:
+    """The loop-closure winner among this rank's candidates: smallest (round, c) with round =
+    (hypothesis of the first success) // 5 (LoopClosing.cpp:271-327), or -1."""
+    ok = records[records[:, 1] > 0] if len(records) else records
+    return loop_winner({int(r[0]): int(r[4]) - 1 for r in ok}) if len(ok) else -1
+
+
+def all_gather_records_and_mask(dist, records: np.ndarray, max_per_rank: int, local_cand: int, local_mask,
+                                mask_len: int, device=None):
+    """The records all-gather of all_gather_records plus the winner's inlier vector in the SAME
+    collective (the winner's bitset as the optional second payload).
+
+    Every rank appends the vbInliers of its own candidate that can win (local_reloc_candidate /
+    local_loop_candidate; -1 for none) as a bitset of mask_len bits — the length is common to all
+    candidates of an event: F.N for relocalization (PnPsolver vbInliers, PnPsolver.hpp:31), mN1 for
+    loop closure (Sim3Solver.cpp:116).  After the gather every rank holds the global winner's
+    vbInliers and can run PoseOptimization (Tracking.cpp:1271-1284) or SearchBySim3
+    (LoopClosing.cpp:300-309) itself.  One fixed-size int32 payload per rank:
+    [max_per_rank x RECORD float32 bit patterns | candidate | words of the bitset].
+
+    Returns (records sorted by candidate, {candidate: bool[mask_len]} for every rank's entry)."""
+    import torch
+    world = dist.get_world_size()
+    words = (mask_len + 31) // 32
+    per = max_per_rank * RECORD + 1 + words
+    buf = np.full(per, -1, np.int32)
+    pad = np.full((max_per_rank, RECORD), -1.0, np.float32)
+    pad[:len(records)] = records
+    buf[:max_per_rank * RECORD] = pad.view(np.int32).ravel()
+    buf[max_per_rank * RECORD] = local_cand
+    bits = np.zeros(words * 32, np.uint8)
+    if local_cand >= 0:
+        m = np.asarray(local_mask, bool)
+        assert len(m) == mask_len
+        bits[:mask_len] = m
+    buf[max_per_rank * RECORD + 1:] = np.packbits(bits, bitorder="little").view(np.int32)
+    t = torch.from_numpy(buf)
+    if device is not None:
+        t = t.to(device)
+    out = torch.empty(world * per, dtype=torch.int32, device=t.device)
+    dist.all_gather_into_tensor(out, t)
+    allb = out.cpu().numpy().reshape(world, per)
+    recs = allb[:, :max_per_rank * RECORD].copy().view(np.float32).reshape(-1, RECORD)
+    recs = recs[recs[:, 0] >= 0]
+    recs = recs[np.argsort(recs[:, 0], kind="stable")]
+    masks = {}
+    for r in range(world):
+        c = int(allb[r, max_per_rank * RECORD])
+        if c >= 0:
+            w = allb[r, max_per_rank * RECORD + 1:].copy().view(np.uint8)
+            masks[c] = np.unpackbits(w, bitorder="little")[:mask_len].astype(bool)
+    return recs, masks
+
+
 def reloc_winner(records: np.ndarray) -> int:
     """Lowest candidate index whose iterate() returned true (Tracking.cpp:1241-1265), or -1."""
     ok = records[records[:, 1] > 0]

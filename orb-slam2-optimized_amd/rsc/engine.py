@@ -31,6 +31,7 @@ EXPORTED = [
     "rsc_version", "rsc_status_string", "rsc_context_create", "rsc_context_destroy", "rsc_context_set_stream",
     "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_last_kernel_timing", "rsc_diag_host_timing", "rsc_context_enable_timing", "rsc_selftest_math",
     "rsc_pnp_create", "rsc_pnp_destroy", "rsc_pnp_set_ransac_parameters", "rsc_pnp_iterate", "rsc_pnp_find",
+    "rsc_pnp_last_inliers",
     "rsc_pnp_iterate_many", "rsc_pnp_reset", "rsc_pnp_get_state", "rsc_pnp_last_samples", "rsc_pnp_last_hypotheses",
     "rsc_sim3_last_hypotheses", "rsc_mlpnp_last_counts",
     "rsc_sim3_create", "rsc_sim3_destroy", "rsc_sim3_set_ransac_parameters", "rsc_sim3_iterate", "rsc_sim3_find",
@@ -332,6 +333,8 @@ def load_library(path: str = LIB_PATH):
     L.rsc_pnp_set_ransac_parameters.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
     L.rsc_pnp_iterate.argtypes = [vp, C.c_int, C.POINTER(PnPResult), C.c_void_p]
     L.rsc_pnp_find.argtypes = [vp, C.POINTER(PnPResult), C.c_void_p]
+    L.rsc_pnp_last_inliers.argtypes = [vp, C.c_void_p]
+    L.rsc_pnp_last_inliers.restype = C.c_int
     L.rsc_pnp_iterate_many.argtypes = [C.POINTER(vp), C.c_int, i32p, C.POINTER(PnPResult), C.POINTER(C.c_void_p)]
     L.rsc_pnp_reset.argtypes = [vp, C.c_uint32]
     L.rsc_pnp_get_state.argtypes = [vp, i32p]
@@ -532,6 +535,15 @@ class PnPSolver:
         mask = np.zeros(max(self.n_points, 1), np.uint8)
         _check(load_library().rsc_pnp_find(self.h, C.byref(r), mask.ctypes.data), "find")
         return _pnp_out(r, mask[:self.n_points])
+
+    def last_inliers(self):
+        """vbInliers of the last iterate()/find() (bool[n_points]; None when it returned false),
+        fetched after the call (rsc_pnp_last_inliers) — e.g. after SolverBatch.iterate_raw."""
+        mask = np.zeros(max(self.n_points, 1), np.uint8)
+        st = load_library().rsc_pnp_last_inliers(self.h, mask.ctypes.data)
+        if st < 0:
+            _check(st, "last_inliers")
+        return mask[:self.n_points].astype(bool) if st == 1 else None
 
     def reset(self, seed: int):
         _check(load_library().rsc_pnp_reset(self.h, seed), "reset")

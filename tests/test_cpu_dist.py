@@ -144,3 +144,89 @@ def test_gloo_world2_events_match_single_process():
     assert 0 < len(mine) < len(evs)
     single = eo.run_events(evs)
     assert np.array_equal(allr.view(np.uint32), single.view(np.uint32))
+
+
+F_N = 1300  # keypoints of the current Frame: the common length of every candidate's vbInliers
+
+
+def _mask_scenes():
+    from rsc import synth
+    rng = np.random.default_rng(77)
+    # parity mode (>= 60 % inliers): several candidates succeed, with Refine
+    return [synth.make_pnp_scene(rng, int(rng.integers(300, 1200)), float(rng.uniform(0.65, 0.85)), n_points=F_N)
+            for _ in range(7)]
+
+
+def _mask_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "orb-slam2-optimized_amd"))
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import torch.distributed as dist
+    from rsc import dist as rd
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    scenes = _mask_scenes()
+    lo, hi = rd.shard_range(len(scenes), world, rank, cost=[s.n for s in scenes])
+    res = _solve(range(lo, hi), scenes)
+    rec = rd.pack_pnp(list(range(lo, hi)), res)
+    c = rd.local_reloc_candidate(rec)
+    mask = res[c - lo]["inliers"] if c >= 0 else None
+    allr, masks = rd.all_gather_records_and_mask(dist, rec, len(scenes), c, mask, F_N)
+    q.put((rank, c, allr, masks))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_winner_mask_in_the_exchange():
+    """The winner's vbInliers travels in the records all-gather: after it, EVERY rank
+    holds the relocalization winner's mask, equal to the single-process run's (Tracking.cpp:1271-1284
+    can run on any rank)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mask_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=120) for _ in range(2)], key=lambda g: g[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    scenes = _mask_scenes()
+    res = _solve(range(len(scenes)), scenes)
+    single = rdist.pack_pnp(list(range(len(scenes))), res)
+    win = rdist.reloc_winner(single)
+    assert win >= 0
+    for rank, c, allr, masks in got:
+        assert np.array_equal(allr, single)
+        assert rdist.reloc_winner(allr) == win
+        assert win in masks and np.array_equal(masks[win], res[win]["inliers"])
+        assert masks[win].sum() == res[win]["n_inliers"]
+    assert sum(g[1] >= 0 for g in got) >= 1
+
+
+def test_mask_exchange_packing_round_trip():
+    """Single process, world 1 gloo: odd mask lengths, no local candidate, all-ones masks."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        rng = np.random.default_rng(3)
+        for n in (1, 31, 32, 33, 1999, 2000):
+            rec = np.zeros((3, rdist.RECORD), np.float32)
+            rec[:, 0] = [4, 5, 6]
+            rec[1, 1] = 1
+            m = rng.random(n) < 0.5
+            allr, masks = rdist.all_gather_records_and_mask(dist, rec, 5, 5, m, n)
+            assert np.array_equal(allr, rec) and np.array_equal(masks[5], m)
+            allr, masks = rdist.all_gather_records_and_mask(dist, rec, 5, -1, None, n)
+            assert masks == {}
+            allr, masks = rdist.all_gather_records_and_mask(dist, rec, 5, 6, np.ones(n, bool), n)
+            assert masks[6].all() and len(masks[6]) == n
+        assert rdist.local_reloc_candidate(rec) == 5
+        rec2 = rec.copy()
+        rec2[:, 1] = 1
+        rec2[:, 4] = [12, 4, 9]  # first successes at hypotheses 11, 3, 8 -> rounds 2, 0, 1
+        assert rdist.local_loop_candidate(rec2) == 5
+    finally:
+        dist.destroy_process_group()

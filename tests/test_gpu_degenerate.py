@@ -39,8 +39,10 @@ def nan_equal(a, b):
 @pytest.mark.parametrize("plane", ["floor", "wall", "tilted", "duplicates"])
 def test_pnp_degenerate_every_hypothesis(plane):
     from rsc import engine
+    # exhaustive: at most 45 % inliers, so minInliers = N/2 is unreachable and the 300 speculated
+    # hypotheses are the 300 the reference evaluates (Refine paths: the round-robin test below)
     scenes = [synth.make_planar_pnp_scene(np.random.default_rng(700 + i), n, r, plane)
-              for i, (n, r) in enumerate([(600, 0.7), (1500, 0.6), (250, 0.8), (2000, 0.5)])]
+              for i, (n, r) in enumerate([(600, 0.45), (1500, 0.4), (250, 0.45), (2000, 0.3)])]
     seeds = [11, 12, 13, 14]
     gs = [engine.PnPSolver(ctx(), sc, s) for sc, s in zip(scenes, seeds)]
     b = engine.SolverBatch(gs)
@@ -53,6 +55,7 @@ def test_pnp_degenerate_every_hypothesis(plane):
         o.enable_trace()
         ro = o.iterate(300)
         assert_pnp_equal(outs[i], ro, f"{plane} cand {i}")
+        assert not ro["ok"] and ro["iterations"] == 300
         ints, fl = o.trace()
         cnt, pos = gs[i].last_hypotheses(400)
         smp = gs[i].last_samples(400)
@@ -108,9 +111,11 @@ def test_sim3_degenerate_every_hypothesis(kind):
         assert_sim3_equal(outs[i], ro, f"{kind} pair {i}")
         ints, fl = o.trace()
         cnt, pos = gs[i].last_hypotheses(400)
-        assert len(cnt) == len(ints)
-        assert np.array_equal(cnt, ints[:, 3]), f"{kind} pair {i} counts"
-        assert nan_equal(pos, fl), f"{kind} pair {i} poses"
+        # one speculation of all 300; the reference stops at its first success (Q12)
+        h = len(ints)
+        assert len(cnt) >= h
+        assert np.array_equal(cnt[:h], ints[:, 3]), f"{kind} pair {i} counts"
+        assert nan_equal(pos[:h], fl), f"{kind} pair {i} poses"
 
 
 @pytest.mark.parametrize("plane", ["floor", "wall", "tilted"])
@@ -131,8 +136,9 @@ def test_mlpnp_planar_branch_on_device(plane):
         assert np.array_equal(rg["inliers"], ro["inliers"])
     ints, dbl = o.trace()
     smp, pos = g.last_hypotheses()
-    assert len(smp) == len(ints)
-    assert np.array_equal(smp[:, :6], ints[:, :6])
-    da, db = pos.astype(np.float64), dbl.astype(np.float64)
+    h = len(ints)
+    assert len(smp) >= h
+    assert np.array_equal(smp[:h, :6], ints[:, :6])
+    da, db = pos[:h].astype(np.float64), dbl.astype(np.float64)
     na, nb = np.isnan(da), np.isnan(db)
     assert np.array_equal(na, nb) and np.array_equal(da.view(np.uint64)[~na], db.view(np.uint64)[~nb])

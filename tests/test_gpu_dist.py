@@ -68,6 +68,22 @@ def _events():
     return rev.make_event_stream(seed=17, n_reloc=10, n_loop=4)
 
 
+F_N, N1 = 1300, 600  # common vbInliers lengths: the Frame's keypoints / the KeyFrame's matches
+
+
+def _mask_scenes():
+    from rsc import synth
+    rng = np.random.default_rng(77)
+    return [synth.make_pnp_scene(rng, int(rng.integers(300, 1200)), float(rng.uniform(0.65, 0.85)), n_points=F_N)
+            for _ in range(7)]
+
+
+def _mask_pairs():
+    from rsc import synth
+    rng = np.random.default_rng(78)
+    return [synth.make_sim3_pair(rng, N1, int(rng.integers(15, 120))) for _ in range(6)]
+
+
 def _run_pnp(ctx, scenes, idx):
     from rsc import engine
     solvers = [engine.PnPSolver(ctx, scenes[c], 1 + c) for c in idx]
@@ -120,7 +136,26 @@ def _worker(rank, world, port, q):
     lo4, hi4 = rd.shard_range(len(mls), world, rank, cost=[m.n for m in mls])
     m4 = rd.all_gather_records(dist, rd.pack_pnp(list(range(lo4, hi4)), _run_mlpnp(ctx, mls, range(lo4, hi4))),
                                max_per_rank=len(mls))
-    q.put((rank, hi - lo, len(mine), allr, alle, hi3 - lo3, s3, hi4 - lo4, m4))
+    # the winner's vbInliers in the same all-gather: relocalization candidates in
+    # parity mode (Refine successes) — the mask of the rank's local candidate fetched after a raw
+    # iterate with rsc_pnp_last_inliers — and loop-closure pairs (masks from iterate)
+    ps = _mask_scenes()
+    lo5, hi5 = rd.shard_range(len(ps), world, rank, cost=[s.n for s in ps])
+    sol = [engine.PnPSolver(ctx, ps[c], 1 + c) for c in range(lo5, hi5)]
+    b = engine.SolverBatch(sol)
+    b.set_ransac_parameters(0.99, 10, 300, 4, 0.5, 5.991)
+    rec5 = rd.pack_pnp(list(range(lo5, hi5)), b.iterate_raw(300))
+    c5 = rd.local_reloc_candidate(rec5)
+    r5, k5 = rd.all_gather_records_and_mask(dist, rec5, len(ps), c5,
+                                            sol[c5 - lo5].last_inliers() if c5 >= 0 else None, F_N)
+    pp = _mask_pairs()
+    lo6, hi6 = rd.shard_range(len(pp), world, rank)
+    res6 = _run_sim3(ctx, pp, range(lo6, hi6))
+    rec6 = rd.pack_sim3(list(range(lo6, hi6)), res6)
+    c6 = rd.local_loop_candidate(rec6)
+    r6, k6 = rd.all_gather_records_and_mask(dist, rec6, len(pp), c6,
+                                            res6[c6 - lo6]["inliers"] if c6 >= 0 else None, N1)
+    q.put((rank, hi - lo, len(mine), allr, alle, hi3 - lo3, s3, hi4 - lo4, m4, r5, k5, r6, k6))
     dist.barrier()
     dist.destroy_process_group()
     ctx.close()
@@ -144,7 +179,8 @@ def test_world2_librsc_shards_match_single_process_and_oracle():
     assert all(g[1] > 0 and g[2] > 0 for g in got)  # both ranks had work
     single = rdist.pack_pnp(list(range(len(scenes))), _run_pnp(ctx(), scenes, range(len(scenes))))
     single_ev = _run_events(ctx(), evs)
-    for _, _, _, allr, alle, _, _, _, _ in got:  # every rank holds the full gathered result
+    for g in got:  # every rank holds the full gathered result
+        allr, alle = g[3], g[4]
         assert np.array_equal(allr.view(np.uint32), single.view(np.uint32))
         assert np.array_equal(alle.view(np.uint32), single_ev.view(np.uint32))
     # and the single-process run is the oracle's
@@ -176,6 +212,31 @@ def test_world2_librsc_shards_match_single_process_and_oracle():
         o4.append(o.iterate(300))
     assert np.array_equal(s3_single.view(np.uint32), rdist.pack_sim3(list(range(len(pairs))), o3).view(np.uint32))
     assert np.array_equal(m4_single.view(np.uint32), rdist.pack_pnp(list(range(len(mls))), o4).view(np.uint32))
+    # the winner's mask in the exchange: every rank holds it, equal to one process and the oracle
+    ps, pp = _mask_scenes(), _mask_pairs()
+    ora5 = []
+    for c, sc in enumerate(ps):
+        o = ol.OraclePnP(sc, 1 + c)
+        o.set_ransac_parameters(0.99, 10, 300, 4, 0.5, 5.991)
+        ora5.append(o.iterate(300))
+    w5 = rdist.reloc_winner(rdist.pack_pnp(list(range(len(ps))), ora5))
+    ora6 = []
+    for c, p in enumerate(pp):
+        o = ol.OracleSim3(p, 1 + c)
+        o.set_ransac_parameters(0.99, 20, 300)
+        ora6.append(o.iterate(300))
+    rec6_ora = rdist.pack_sim3(list(range(len(pp))), ora6)
+    w6 = rdist.local_loop_candidate(rec6_ora)
+    assert w5 >= 0 and w6 >= 0
+    single5 = _run_pnp(ctx(), ps, range(len(ps)))
+    for g in got:
+        r5, k5, r6, k6 = g[9], g[10], g[11], g[12]
+        assert np.array_equal(r5.view(np.uint32), rdist.pack_pnp(list(range(len(ps))), ora5).view(np.uint32))
+        assert rdist.reloc_winner(r5) == w5
+        assert np.array_equal(k5[w5], ora5[w5]["inliers"]) and np.array_equal(k5[w5], single5[w5]["inliers"])
+        assert np.array_equal(r6.view(np.uint32), rec6_ora.view(np.uint32))
+        assert rdist.local_loop_candidate(r6) == w6
+        assert np.array_equal(k6[w6], ora6[w6]["inliers"])
 
 
 def _rccl_worker(port, q):
