@@ -554,6 +554,8 @@ double ora_dm_sin(double x) { return rsc::dm::sin(x); }
 double ora_dm_cos(double x) { return rsc::dm::cos(x); }
 double ora_dm_acos(double x) { return rsc::dm::acos(x); }
 double ora_dm_cbrt(double x) { return rsc::dm::cbrt(x); }
+double ora_dm_pow13(double x) { return rsc::dm::pow_1_3(x); }
+double ora_dm_pow32(double x) { return rsc::dm::pow_3_2(x); }
 
 // ---- Optimizer::PoseOptimization (mono + stereo edges) ----
 // stats[3] = rounds, LM iterations, LM trials.  Returns nGood.

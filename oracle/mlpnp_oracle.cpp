@@ -4,6 +4,7 @@
 #include "ora_libm.h"
 #include "ora_linalg.h"
 #include "../orb-slam2-optimized_amd/csrc/rsc_math.h"
+#include "../orb-slam2-optimized_amd/csrc/rsc_mlpnp_jac.h"
 #include <cassert>
 #include <cmath>
 #include <cstring>
@@ -347,48 +348,16 @@ void rot2rodrigues(const double R[3][3], double w[3]) {
     }
 }
 
-// Residual Jacobian of r = n^T (R(w) X + t) / |R(w) X + t| for n in {n_r, n_s}
-// (replaces mlpnpJacs, MLPnPsolver.cpp:773-1020 — same function, analytic form):
-//   dr/dy = (n - (n.u) u) / |y|,  dy/dt = I,
-//   dy/dw_k = (w_k (w x z) + c_k x z) / |w|^2 with z = R X, c_k = w x (e_k - R e_k).
+// mlpnpJacs (MLPnPsolver.cpp:773-1020): the reference's generated Jacobian, operation for operation
+// (csrc/rsc_mlpnp_jac.h, shared with the kernels; sin / cos / pow(., 3/2) through ora_libm).
 void mlpnp_jac(const double X[3], const double nr[3], const double ns[3], const double w[3], const double t[3],
                double J[2][6]) {
-    const double th2 = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
-    const double th = std::sqrt(th2);
-    const double a = ora_libm::sin(th) / th;
-    const double b = (1.0 - ora_libm::cos(th)) / th2;
-    const double S[3][3] = {{0.0, -w[2], w[1]}, {w[2], 0.0, -w[0]}, {-w[1], w[0], 0.0}};
-    double R[3][3];
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-            const double ss = S[i][0] * S[0][j] + S[i][1] * S[1][j] + S[i][2] * S[2][j];
-            R[i][j] = (((i == j) ? 1.0 : 0.0) + a * S[i][j]) + b * ss;
-        }
-    double z[3], y[3], u[3];
-    for (int i = 0; i < 3; ++i) {
-        z[i] = R[i][0] * X[0] + R[i][1] * X[1] + R[i][2] * X[2];
-        y[i] = z[i] + t[i];
-    }
-    const double ny = norm3(y);
-    for (int i = 0; i < 3; ++i) u[i] = y[i] / ny;
-    double wz[3], dy[3][3];
-    cross3(w, z, wz);
-    for (int k = 0; k < 3; ++k) {
-        double v[3], ck[3], cz[3];
-        for (int i = 0; i < 3; ++i) v[i] = ((i == k) ? 1.0 : 0.0) - R[i][k];
-        cross3(w, v, ck);
-        cross3(ck, z, cz);
-        for (int i = 0; i < 3; ++i) dy[k][i] = (w[k] * wz[i] + cz[i]) / th2;
-    }
-    const double* nv[2] = {nr, ns};
-    for (int row = 0; row < 2; ++row) {
-        const double* n = nv[row];
-        const double nu = dot3(n, u);
-        double g[3];
-        for (int i = 0; i < 3; ++i) g[i] = (n[i] - nu * u[i]) / ny;
-        for (int k = 0; k < 3; ++k) J[row][k] = dot3(g, dy[k]);
-        for (int i = 0; i < 3; ++i) J[row][3 + i] = g[i];
-    }
+    rsc::MlJacWArr W;
+    rsc::mlpnp_jac_w<ora_libm::JacLibm>(w, W);
+    double Jm[2][6];
+    rsc::mlpnp_jac_pt<ora_libm::JacLibm>(W, X, nr, ns, t, w, Jm);
+    for (int r = 0; r < 2; ++r)
+        for (int c = 0; c < 6; ++c) J[r][c] = Jm[r][c];
 }
 
 // mlpnp_gn (MLPnPsolver.cpp:659-723).  Pw: the 2x2 blocks of Kll per correspondence (use_cov), or
@@ -675,7 +644,7 @@ void MLPnPOracle::computePose(const int* idx, int n, double Rout[3][3], double t
         double tmp[3][3] = {{r1[0], r1[3], r1[6]}, {r1[1], r1[4], r1[7]}, {r1[2], r1[5], r1[8]}};
         const double c0[3] = {tmp[0][0], tmp[1][0], tmp[2][0]}, c1[3] = {tmp[0][1], tmp[1][1], tmp[2][1]},
                      c2[3] = {tmp[0][2], tmp[1][2], tmp[2][2]};
-        const double scale = 1.0 / ora_libm::cbrt_pow(std::fabs(norm3(c0) * norm3(c1) * norm3(c2)));
+        const double scale = 1.0 / ora_libm::pow_1_3(std::fabs(norm3(c0) * norm3(c1) * norm3(c2)));
         double U3[9], S3[3], V3[9];
         jacobi_svd_square(3, &tmp[0][0], true, U3, S3, V3);
         for (int r = 0; r < 3; ++r)

@@ -5,7 +5,8 @@
 // both use these restatements of the classic fdlibm algorithms (Cody-Waite reduction by pi/2 in
 // three parts, the minimax kernels __kernel_sin / __kernel_cos, the rational acos of e_acos.c, and
 // the bit-seeded Newton cbrt of s_cbrt.c).  Accuracy < 1 ulp over the arguments MLPnP produces;
-// tests/test_cpu_math.py checks them against glibc.  Only +, -, *, / and IEEE sqrt are used, so
+// tests/test_cpu_math.py checks them against glibc.  Only +, -, *, / and IEEE sqrt are used — and,
+// in the two pow restatements, fma (correctly rounded on both sides: v_fma_f64, glibc fma) — so
 // with -ffp-contract=off the host and gfx950 builds return identical bits.
 //
 // Arguments beyond |x| = 2^19 * pi/2 are reduced with the same three-part scheme (fdlibm switches to
@@ -310,6 +311,37 @@ RSCM_HD double log(double x) {
 
 // logf as the float rounding of the double log above.
 RSCM_HD float logf(float x) { return (float)log((double)x); }
+
+// pow(x, 3.0/2.0) of mlpnpJacs' 1.0/pow(t8,3.0/2.0) and 1.0/pow(t63,3.0/2.0)
+// (MLPnPsolver.cpp:839,:901; glibc pow in the reference), correctly rounded up to a 2^-104 relative
+// band around the rounding midpoints: s = sqrt(x) rounded, r = x - s^2 and x*s - fl(x*s) exact by
+// fma, x^1.5 = x*s + x*r/(2s) to second order.  pow's special cases for x = +-0, +inf, < 0, NaN.
+RSCM_HD double pow_3_2(double x) {
+    if (!(x > 0.0)) return (x == 0.0) ? 0.0 : (x - x) / (x - x);
+    const double s = sqrt(x);
+    const double p = x * s;
+    if (p > 1.7976931348623157e308) return p;  // overflow (and x = +inf)
+    const double r = fma(-s, s, x);
+    const double e = fma(x, s, -p);
+    return p + (e + x * (r / (s + s)));
+}
+
+// pow(x, 1.0/3.0) of computePose's scale (MLPnPsolver.cpp:567; glibc pow in the reference, not cbrt:
+// the exponent is the double nearest 1/3, 1/3 - 2^-54/3).  x^y = cbrt(x) * x^-(2^-54/3), i.e. the
+// cube root in double-double — one Newton step on fdlibm's cbrt with the residual x - c^3 formed
+// exactly by fma — times 1 - (2^-54/3) ln x (the dropped square term is below 2^-100).  Correctly
+// rounded up to a 2^-100 band around the midpoints; x >= 0 here (the argument is an abs()).
+RSCM_HD double pow_1_3(double x) {
+    if (!(x > 0.0)) return (x == 0.0) ? 0.0 : (x - x) / (x - x);
+    if (x > 1.7976931348623157e308) return x;
+    const double c = cbrt(x);
+    const double c2 = c * c, c2l = fma(c, c, -c2);           // c^2 = c2 + c2l exactly
+    const double c3 = c2 * c, c3l = fma(c2, c, -c3);         // c2 * c = c3 + c3l exactly
+    const double res = ((x - c3) - c3l) - c2l * c;           // x - c^3 (x - c3 exact: Sterbenz)
+    const double corr = res / (3.0 * c2);                    // cbrt(x) = c + corr + O(corr^2)
+    const double delta = 1.8503717077085941e-17;             // 1/3 - fl(1/3) = 2^-54 / 3
+    return c + (corr - c * (delta * log(x)));
+}
 
 }  // namespace dm
 }  // namespace rsc

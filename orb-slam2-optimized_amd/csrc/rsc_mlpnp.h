@@ -1,7 +1,8 @@
 // rsc_mlpnp.h — per-lane MLPnP hypothesis (MLPnPsolver::computePose, src/MLPnPsolver.cpp:321-623)
 // for one hypothesis per lane.  Same arithmetic as the oracle restatement (oracle/mlpnp_oracle.cpp):
-// every sum left to right, fdlibm transcendentals (rsc_math.h), cbrt for pow(x, 1/3), analytic
-// residual Jacobian, generic cofactor 4x4 inverse.
+// every sum left to right, fdlibm transcendentals (rsc_math.h), correctly rounded restatements of
+// glibc's pow(x, 1.0/3.0) and pow(x, 3.0/2.0) (rsc_math.h), the reference's own generated residual
+// Jacobian mlpnpJacs operation for operation (rsc_mlpnp_jac.h), generic cofactor 4x4 inverse.
 //
 // Storage: small matrices in VGPRs with static indices; the 12x12 (or 9x9) JacobiSVD work matrix W
 // and its V accumulate in a per-lane LDS slab (LaneMat, element-major across the wave, 288 doubles
@@ -9,6 +10,7 @@
 #pragma once
 #include "rsc_core.h"
 #include "rsc_math.h"
+#include "rsc_mlpnp_jac.h"
 
 namespace rsc {
 
@@ -419,46 +421,6 @@ RSC_HD void ml_rot2rodrigues(const double (&R)[3][3], double (&w)[3]) {
     }
 }
 
-// Residual Jacobian rows (see oracle mlpnp_jac).
-RSC_HD void ml_jac(const double (&X)[3], const double (&nr)[3], const double (&ns)[3], const double* w,
-                   const double* t, double (&J)[2][6]) {
-    const double th2 = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
-    const double th = sqrt(th2);
-    const double a = dm::sin(th) / th;
-    const double b = (1.0 - dm::cos(th)) / th2;
-    const double S[3][3] = {{0.0, -w[2], w[1]}, {w[2], 0.0, -w[0]}, {-w[1], w[0], 0.0}};
-    double R[3][3];
-    RSC_UNROLL for (int i = 0; i < 3; ++i)
-        RSC_UNROLL for (int j = 0; j < 3; ++j) {
-            const double ss = S[i][0] * S[0][j] + S[i][1] * S[1][j] + S[i][2] * S[2][j];
-            R[i][j] = (((i == j) ? 1.0 : 0.0) + a * S[i][j]) + b * ss;
-        }
-    double z[3], y[3], u[3];
-    RSC_UNROLL for (int i = 0; i < 3; ++i) {
-        z[i] = R[i][0] * X[0] + R[i][1] * X[1] + R[i][2] * X[2];
-        y[i] = z[i] + t[i];
-    }
-    const double ny = ml_norm3(y);
-    RSC_UNROLL for (int i = 0; i < 3; ++i) u[i] = y[i] / ny;
-    double wz[3], dy[3][3];
-    ml_cross3(w, z, wz);
-    RSC_UNROLL for (int k = 0; k < 3; ++k) {
-        double v[3], ck[3], cz[3];
-        RSC_UNROLL for (int i = 0; i < 3; ++i) v[i] = ((i == k) ? 1.0 : 0.0) - R[i][k];
-        ml_cross3(w, v, ck);
-        ml_cross3(ck, z, cz);
-        RSC_UNROLL for (int i = 0; i < 3; ++i) dy[k][i] = (w[k] * wz[i] + cz[i]) / th2;
-    }
-    RSC_UNROLL for (int row = 0; row < 2; ++row) {
-        const double* n = row == 0 ? nr : ns;
-        const double nu = ml_dot3(n, u);
-        double g[3];
-        RSC_UNROLL for (int i = 0; i < 3; ++i) g[i] = (n[i] - nu * u[i]) / ny;
-        RSC_UNROLL for (int k = 0; k < 3; ++k) J[row][k] = ml_dot3(g, dy[k]);
-        RSC_UNROLL for (int i = 0; i < 3; ++i) J[row][3 + i] = g[i];
-    }
-}
-
 // LDLT<MatrixXd>(A).solve(g), 6x6, A in LDS view L (rows/cols 0..5), pivoted as Eigen.
 RSC_HD void ml_ldlt_solve6(const MlView& L, const double (&g)[6], double (&x)[6]) {
     const int n = 6;
@@ -679,17 +641,22 @@ struct MlRegs {
 };
 
 // Doubles of the Gauss-Newton slab: J (2 NS x 6), g (6), the 6x6 system + its temp row (stride 12).
+// While the Jacobian rows are evaluated, mlpnpJacs' stored w-only temporaries (kMlJacStored doubles)
+// occupy the space of g and the system, which are written only after the last row.
 template <int NS>
 constexpr int ml_gn_slab() {
     return 12 * NS + 6 + 6 * 12 + 6;
 }
+static_assert(12 * 6 + kMlJacStored <= ml_gn_slab<6>(), "mlpnpJacs temporaries do not fit the system's space");
 
 // Phase 3 of computePose (:480-623): pose recovery from the null vector r1 (the V column of the
 // smallest singular value of the normal matrix) and the Gauss-Newton refinement (mlpnp_gn,
 // :659-723).  slab: kMlSlabDoubles doubles (element stride slab.stride) for J and the LDLT system.
-template <int NS, class Cov, class View>
-RSC_HD void mlpnp_finish_pose(const View& in, const double (&r1)[12], const LaneMat& slab, double (&Rout)[3][3],
-                              double (&tout)[3]) {
+// jin: the correspondences again, read with a run-time index by the Jacobian loop (the parked LDS
+// copy in the quad kernel, so no register array is indexed dynamically).
+template <int NS, class Cov, class View, class JView>
+RSC_HD void mlpnp_finish_pose(const View& in, const JView& jin, const double (&r1)[12], const LaneMat& slab,
+                              double (&Rout)[3][3], double (&tout)[3]) {
     const bool planar = in.planar();
     double R[3][3], t[3];
     if (planar) {
@@ -744,7 +711,7 @@ RSC_HD void mlpnp_finish_pose(const View& in, const double (&r1)[12], const Lane
     } else {
         const double tmp[3][3] = {{r1[0], r1[3], r1[6]}, {r1[1], r1[4], r1[7]}, {r1[2], r1[5], r1[8]}};
         const double c0[3] = {r1[0], r1[1], r1[2]}, c1[3] = {r1[3], r1[4], r1[5]}, c2[3] = {r1[6], r1[7], r1[8]};
-        const double scale = 1.0 / dm::cbrt(rabs(ml_norm3(c0) * ml_norm3(c1) * ml_norm3(c2)));
+        const double scale = 1.0 / dm::pow_1_3(rabs(ml_norm3(c0) * ml_norm3(c1) * ml_norm3(c2)));  // :567
         ml_nearest_rotation(tmp, R);
         if (ml_det3(R) < 0) RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) R[r][c] *= -1.0;
         const double ts[3] = {scale * r1[9], scale * r1[10], scale * r1[11]};
@@ -791,24 +758,38 @@ RSC_HD void mlpnp_finish_pose(const View& in, const double (&r1)[12], const Lane
         double Rg[3][3];
         const double w3[3] = {x[0], x[1], x[2]};
         ml_rodrigues2rot(w3, Rg);
+        // mlpnpJacs' w-only temporaries, once per iteration, parked after the system (rsc_mlpnp_jac.h)
+        const MlJacWStrided JW{{slab.base + 12 * NS * slab.stride, slab.stride}};
+        {
+            MlJacWStrided JWw = JW;
+            mlpnp_jac_w<MlJacDeviceLibm>(x, JWw);
+        }
         double rr[2 * NS];
         RSC_UNROLL for (int i = 0; i < NS; ++i) {
             double pc[3];
             RSC_UNROLL for (int k = 0; k < 3; ++k)
-                pc[k] = (Rg[k][0] * in.pw(i, 0) + Rg[k][1] * in.pw(i, 1) + Rg[k][2] * in.pw(i, 2)) + x[3 + k];
+                pc[k] = (Rg[k][0] * jin.pw(i, 0) + Rg[k][1] * jin.pw(i, 1) + Rg[k][2] * jin.pw(i, 2)) + x[3 + k];
             const double nrm = ml_norm3(pc);
             RSC_UNROLL for (int k = 0; k < 3; ++k) pc[k] = pc[k] / nrm;
-            const double nr[3] = {in.ns(i, 0, 0), in.ns(i, 1, 0), in.ns(i, 2, 0)};
-            const double ns[3] = {in.ns(i, 0, 1), in.ns(i, 1, 1), in.ns(i, 2, 1)};
+            const double nr[3] = {jin.ns(i, 0, 0), jin.ns(i, 1, 0), jin.ns(i, 2, 0)};
+            const double ns[3] = {jin.ns(i, 0, 1), jin.ns(i, 1, 1), jin.ns(i, 2, 1)};
             rr[2 * i] = ml_dot3(nr, pc);
             rr[2 * i + 1] = ml_dot3(ns, pc);
+        }
+        // the Jacobian rows (mlpnpJacs, MLPnPsolver.cpp:749-767), one correspondence at a time: its
+        // ~200 temporaries are live for that correspondence only
+#pragma unroll 1
+        for (int i = 0; i < NS; ++i) {
+            const double nr[3] = {jin.ns(i, 0, 0), jin.ns(i, 1, 0), jin.ns(i, 2, 0)};
+            const double ns[3] = {jin.ns(i, 0, 1), jin.ns(i, 1, 1), jin.ns(i, 2, 1)};
+            const double pwi[3] = {jin.pw(i, 0), jin.pw(i, 1), jin.pw(i, 2)};
             double J[2][6];
-            const double pwi[3] = {in.pw(i, 0), in.pw(i, 1), in.pw(i, 2)};
-            ml_jac(pwi, nr, ns, x, x + 3, J);
+            mlpnp_jac_pt<MlJacDeviceLibm>(JW, pwi, nr, ns, x + 3, x, J);
             RSC_UNROLL for (int k = 0; k < 6; ++k) {
                 Jv.e((2 * i) * 6 + k) = J[0][k];
                 Jv.e((2 * i + 1) * 6 + k) = J[1][k];
             }
+            RSC_LOOP_FENCE();
         }
         // J^T J (or J^T Kll J) and J^T r one row a at a time; where registers are short (covariances,
         // NS > 6) the row loop stays rolled, so J stays in the slab instead of 2 NS x 6 doubles of
@@ -904,7 +885,8 @@ RSC_HD void mlpnp_compute_pose(const double (&pw)[NS][3], const double (&f)[NS][
         }
     double r1[12];
     ml_jacobi_svd_lds(W, V, colsA, r1);
-    mlpnp_finish_pose<NS, Cov>(MlRegs<NS, Cov>{pw, f, m}, r1, slab, Rout, tout);
+    const MlRegs<NS, Cov> in{pw, f, m};
+    mlpnp_finish_pose<NS, Cov>(in, in, r1, slab, Rout, tout);
 }
 
 // MLPnPsolver::CheckInliers for one correspondence (MLPnPsolver.cpp:222-255).

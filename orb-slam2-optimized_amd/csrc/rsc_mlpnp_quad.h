@@ -319,9 +319,11 @@ __device__ __forceinline__ void mlpnp_quad_hypothesis(const DevML& P, const int 
         double pw[NS][3], f[NS][3];
         MlPrep<NS, Cov> m;
         ml_unpark<NS, Cov>(stash, pw, f, m);
-        mlpnp_finish_pose<NS, Cov>(MlRegs<NS, Cov>{pw, f, m}, r1, LaneMat{region, 1}, Rout, tout);
+        mlpnp_finish_pose<NS, Cov>(MlRegs<NS, Cov>{pw, f, m}, MlParked<NS, Cov>{stash}, r1, LaneMat{region, 1}, Rout,
+                                   tout);
     } else {
-        mlpnp_finish_pose<NS, Cov>(MlParked<NS, Cov>{stash}, r1, LaneMat{region, 1}, Rout, tout);
+        mlpnp_finish_pose<NS, Cov>(MlParked<NS, Cov>{stash}, MlParked<NS, Cov>{stash}, r1, LaneMat{region, 1}, Rout,
+                                   tout);
     }
 }
 

@@ -117,7 +117,8 @@ def lib():
                                          C.c_float, C.c_float, C.c_int, i32p, f32p]
     L.ora_loop_events_batch.argtypes = [C.c_int, i32p, i32p, i64p, u8p, f32p, f32p, f32p, f32p, f32p, u32p,
                                         C.c_double, C.c_int, C.c_int, C.c_int, i32p, f32p]
-    for fn in ("ora_dm_sin", "ora_dm_cos", "ora_dm_acos", "ora_dm_cbrt"):
+    for fn in ("ora_dm_sin", "ora_dm_cos", "ora_dm_acos", "ora_dm_cbrt") + \
+            tuple(f for f in ("ora_dm_pow13", "ora_dm_pow32") if hasattr(L, f)):
         getattr(L, fn).restype = C.c_double
         getattr(L, fn).argtypes = [C.c_double]
     L.ora_mlpnp_jac.argtypes = [f64p, f64p, f64p, f64p, f64p]

@@ -228,7 +228,10 @@ def test_world2_librsc_shards_match_single_process_and_oracle():
     rec6_ora = rdist.pack_sim3(list(range(len(pp))), ora6)
     w6 = rdist.local_loop_candidate(rec6_ora)
     assert w5 >= 0 and w6 >= 0
-    single5 = _run_pnp(ctx(), ps, range(len(ps)))
+    from rsc import engine
+    b5 = engine.SolverBatch([engine.PnPSolver(ctx(), sc, 1 + c) for c, sc in enumerate(ps)])
+    b5.set_ransac_parameters(0.99, 10, 300, 4, 0.5, 5.991)
+    single5 = b5.iterate(300, with_masks=True)
     for g in got:
         r5, k5, r6, k6 = g[9], g[10], g[11], g[12]
         assert np.array_equal(r5.view(np.uint32), rdist.pack_pnp(list(range(len(ps))), ora5).view(np.uint32))

@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
-"""Writes profiles/r03/libm_choice.json: (1) how often the fdlibm restatement (csrc/rsc_math.h, what
-the kernels compile) returns a different double than host glibc on random arguments of each
-function's working range, and (2) the outcome comparison of tests/test_cpu_libm_choice.py (the oracle
-built with each libm on the MLPnP / PoseOptimization / SearchBySim3 / OptimizeSim3 workloads)."""
+"""Writes profiles/r04/libm_choice.json: (1) how often the restatements the kernels compile
+(csrc/rsc_math.h: fdlibm sin / cos / acos / log, the correctly rounded pow(x, 1/3) and pow(x, 3/2))
+return a different double than host glibc on random arguments of each function's working range —
+beside the round-3 forms cbrt and x*sqrt(x) for contrast; (2) the outcome comparison of
+tests/test_cpu_libm_choice.py (the oracle built with each libm on the MLPnP / PoseOptimization /
+SearchBySim3 / OptimizeSim3 workloads); (3) VERDICT r3 "Next round" 1c: the same outcome comparison
+between the round-3 MLPnP restatement (analytic Jacobian, x*sqrt(x), cbrt) and the round-4 one
+(mlpnpJacs as written, pow restatements) — pass the round-3 oracle build as argv[1]."""
 import ctypes
 import json
 import os
@@ -18,7 +22,7 @@ import test_cpu_libm_choice as t  # noqa: E402
 
 L = ol.lib()
 libm = ctypes.CDLL("libm.so.6")
-for name in ("sin", "cos", "acos", "cbrt", "log"):
+for name in ("sin", "cos", "acos", "cbrt", "log", "pow13", "pow32"):
     f = getattr(L, "ora_dm_" + name)
     f.restype, f.argtypes = ctypes.c_double, [ctypes.c_double]
 for name in ("sin", "cos", "acos", "pow", "log"):
@@ -33,7 +37,12 @@ cases = {
     "sin (|x| <= pi)": (L.ora_dm_sin, libm.sin, rng.uniform(-np.pi, np.pi, n)),
     "cos (|x| <= pi)": (L.ora_dm_cos, libm.cos, rng.uniform(-np.pi, np.pi, n)),
     "acos ([-1, 1])": (L.ora_dm_acos, libm.acos, rng.uniform(-1, 1, n)),
-    "cbrt vs pow(x, 1/3) ([1e-6, 1e3])": (L.ora_dm_cbrt, lambda x: libm.pow(x, 1.0 / 3.0), 10 ** rng.uniform(-6, 3, n)),
+    "cbrt vs pow(x, 1/3) ([1e-6, 1e3]) (round-3 form)": (L.ora_dm_cbrt, lambda x: libm.pow(x, 1.0 / 3.0),
+                                                          10 ** rng.uniform(-6, 3, n)),
+    "pow_1_3 vs pow(x, 1/3) ([1e-6, 1e3])": (L.ora_dm_pow13, lambda x: libm.pow(x, 1.0 / 3.0), 10 ** rng.uniform(-6, 3, n)),
+    "x*sqrt(x) vs pow(x, 3/2) ([1e-6, 1e6]) (round-3 form)": (lambda x: x * np.sqrt(x), lambda x: libm.pow(x, 1.5),
+                                                              10 ** rng.uniform(-6, 6, n)),
+    "pow_3_2 vs pow(x, 3/2) ([1e-6, 1e6])": (L.ora_dm_pow32, lambda x: libm.pow(x, 1.5), 10 ** rng.uniform(-6, 6, n)),
 }
 funcs = {}
 for k, (f, g, xs) in cases.items():
@@ -47,11 +56,24 @@ with tempfile.TemporaryDirectory() as td:
     a = t._run(pathlib.Path(td), "fdlibm")
     b = t._run(pathlib.Path(td), "glibc")
     stats, bad = t.compare(a, b)
+    jac = None
+    if len(sys.argv) > 1:  # round-3 oracle build: its MLPnP differs only in the Jacobian and pow forms
+        path = os.path.join(td, "r3.npz")
+        env = dict(os.environ, RSC_ORACLE_LIB=os.path.abspath(sys.argv[1]))
+        env.pop("RSC_ORACLE_LIBM", None)
+        subprocess.run([sys.executable, os.path.join(ROOT, "tests", "libm_workload.py"), path], env=env, check=True)
+        r3 = np.load(path)
+        js, jbad = t.compare(r3, a)
+        jac = dict(outcomes=js["mlpnp"], mismatching_problems=[list(map(str, x)) for x in jbad if x[0].startswith("mlpnp")],
+                   note="round-3 MLPnP restatement (analytic Gallego-Yezzi Jacobian, x*sqrt(x) for pow(., 3/2), cbrt "
+                        "for pow(., 1/3)) vs round 4 (mlpnpJacs of MLPnPsolver.cpp:773-1020 operation for operation, "
+                        "rsc_math.h pow_3_2 / pow_1_3), both with the fdlibm sin / cos / acos")
 head = subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=ROOT, capture_output=True, text=True).stdout.strip()
 out = dict(commit=head, function_differences=funcs, outcomes=stats, mismatching_problems=[list(map(str, x)) for x in bad],
+           jacobian_and_pow_forms=jac,
            note="outcome = discrete results (ok / counts / iterations, inlier, outlier, match and keep decisions) "
                 "identical and pose within 1e-4; the GPU is bit-exact to the fdlibm build")
-os.makedirs(os.path.join(ROOT, "profiles", "r03"), exist_ok=True)
-with open(os.path.join(ROOT, "profiles", "r03", "libm_choice.json"), "w") as f:
+os.makedirs(os.path.join(ROOT, "profiles", "r04"), exist_ok=True)
+with open(os.path.join(ROOT, "profiles", "r04", "libm_choice.json"), "w") as f:
     json.dump(out, f, indent=1)
 print(json.dumps(out, indent=1))
