@@ -479,13 +479,8 @@ def cpu_baseline_sim3(solvers, args, threads):
 
 
 def mlpnp_covariances(sc):
-    """Bearing-vector covariances for config 4's covariance variant: the keypoint's pixel variance
-    (mvLevelSigma2) through the bearing map ((u - cx) / fx, (v - cy) / fy, 1) + a tiny isotropic term."""
-    s2 = np.asarray(sc.sigma2, np.float64)
-    cov = np.zeros((sc.n, 3, 3))
-    cov[:, 0, 0] = s2 / float(sc.fx) ** 2
-    cov[:, 1, 1] = s2 / float(sc.fy) ** 2
-    return cov + np.eye(3) * 1e-9
+    from rsc import workloads as wl
+    return wl.config4_covariances(sc)
 
 
 def run_mlpnp(engine, ctx, scenes, args, with_cov=False, dist=None, rank=0, world=1):

@@ -46,5 +46,16 @@ def config4_scenes(candidates: int = 32, corrs: int = 4096, ratio: float = 0.4, 
     return [synth.make_pnp_scene(rng, corrs, ratio) for _ in range(candidates)]
 
 
+def config4_covariances(sc):
+    """Bearing-vector covariances of config 4's "with bearing-vector covariances" variant: the
+    keypoint's pixel variance (mvLevelSigma2) through the bearing map ((u - cx) / fx, (v - cy) / fy, 1)
+    plus a tiny isotropic term — computePose's covMats (MLPnPsolver.cpp:375-388)."""
+    s2 = np.asarray(sc.sigma2, np.float64)
+    cov = np.zeros((sc.n, 3, 3))
+    cov[:, 0, 0] = s2 / float(sc.fx) ** 2
+    cov[:, 1, 1] = s2 / float(sc.fy) ** 2
+    return cov + np.eye(3) * 1e-9
+
+
 def step_seeds(step: int, count: int) -> np.ndarray:
     return (1 + np.arange(count) + count * step).astype(np.uint32)

@@ -140,6 +140,39 @@ def test_config4_mlpnp_4096_batch_every_hypothesis():
         assert np.array_equal(pos.view(np.uint64), dbl.view(np.uint64)), f"cand {i} poses"
 
 
+def test_config4_mlpnp_4096_covariances_every_hypothesis():
+    """Config 4 "with bearing-vector covariances" at the per-GPU share (32 candidates x 4096, the
+    bench's covariance section): computePose's covMats branch (MLPnPsolver.cpp:375-388, 483-484,
+    694-695; mlpnp_quad_kernel<6, MlIndexedCov>) — samples, counts, double poses bit-exact against the
+    oracle's restatement (parity with the reference unpinned: it never reaches this branch, Q15)."""
+    from rsc import engine
+    scenes = wl.config4_scenes()
+    seeds = wl.step_seeds(0, len(scenes))
+    gs = [engine.MLPnPSolver(ctx(), sc, int(s)) for sc, s in zip(scenes, seeds)]
+    for g, sc in zip(gs, scenes):
+        g.set_covariances(wl.config4_covariances(sc))
+    b = engine.SolverBatch(gs)
+    b.set_ransac_parameters(*wl.MLPNP)
+    outs = b.iterate(300, with_masks=True)
+    hyp = [g.last_hypotheses(400) for g in gs]
+    cnts = [g.last_counts(400) for g in gs]
+    for i, (sc, s) in enumerate(zip(scenes, seeds)):
+        o = ol.OracleMLPnP(sc, int(s))
+        o.set_covariances(wl.config4_covariances(sc))
+        o.set_ransac_parameters(*wl.MLPNP)
+        o.enable_trace()
+        ro = o.iterate(300)
+        assert outs[i]["ok"] == ro["ok"] and outs[i]["n_inliers"] == ro["n_inliers"], f"cand {i}"
+        assert outs[i]["iterations"] == ro["iterations"] == 300
+        assert np.array_equal(bits(outs[i]["T"]), bits(ro["T"])), f"cand {i} T"
+        ints, dbl = o.trace()
+        smp, pos = hyp[i]
+        assert len(smp) == len(ints) == 300
+        assert np.array_equal(smp[:, :6], ints[:, :6]), f"cand {i} samples"
+        assert np.array_equal(cnts[i], ints[:, 8]), f"cand {i} counts"
+        assert np.array_equal(pos.view(np.uint64), dbl.view(np.uint64)), f"cand {i} poses"
+
+
 def test_config5_full_event_stream():
     """The bench's 150 + 20 event stream (rsc.events.make_event_stream() defaults) through
     rsc_reloc_events / rsc_loop_events against the sequential round-robin replay."""
