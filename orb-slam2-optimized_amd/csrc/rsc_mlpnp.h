@@ -550,12 +550,12 @@ struct MlPrep {
     double eigenRot[3][3];
     double P[NS][3];
     bool planar;
+    RSC_HD double pwgt(int i, int e) const { return Pw[Cov::on ? i : 0][e]; }
 };
 
-template <int NS, class Cov>
-RSC_HD void mlpnp_prepare(const double (&pw)[NS][3], const double (&f)[NS][3], const Cov& cov, MlPrep<NS, Cov>& m) {
-    RSC_UNROLL for (int i = 0; i < NS; ++i) ml_bearing_nullspace(f[i], m.Ns[i]);
-    if constexpr (Cov::on) RSC_UNROLL for (int i = 0; i < NS; ++i) ml_cov_weight(m.Ns[i], cov, i, m.Pw[i]);
+// The planarity test (:346-364): rank of P P^T == 2, and the plane's eigenbasis (identity otherwise).
+template <int NS>
+RSC_HD bool ml_planarity(const double (&pw)[NS][3], double (&eigenRot)[3][3]) {
     double PPt[3][3];
     RSC_UNROLL for (int a = 0; a < 3; ++a)
         RSC_UNROLL for (int b = 0; b < 3; ++b) {
@@ -563,49 +563,60 @@ RSC_HD void mlpnp_prepare(const double (&pw)[NS][3], const double (&f)[NS][3], c
             RSC_UNROLL for (int i = 1; i < NS; ++i) s = s + pw[i][a] * pw[i][b];
             PPt[a][b] = s;
         }
-    m.planar = ml_fullpiv_rank3(PPt) == 2;
-    RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) m.eigenRot[r][c] = (r == c) ? 1.0 : 0.0;
-    RSC_UNROLL for (int i = 0; i < NS; ++i) RSC_UNROLL for (int c = 0; c < 3; ++c) m.P[i][c] = pw[i][c];
-    if (m.planar) {
+    const bool planar = ml_fullpiv_rank3(PPt) == 2;
+    RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) eigenRot[r][c] = (r == c) ? 1.0 : 0.0;
+    if (planar) {
         double Ve[3][3], we[3];
         sym_eig_reg<double, 3>(PPt, Ve, we);
-        RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) m.eigenRot[r][c] = Ve[c][r];
-        RSC_UNROLL for (int i = 0; i < NS; ++i) {
-            double q[3];
-            RSC_UNROLL for (int r = 0; r < 3; ++r)
-                q[r] = m.eigenRot[r][0] * m.P[i][0] + m.eigenRot[r][1] * m.P[i][1] + m.eigenRot[r][2] * m.P[i][2];
-            RSC_UNROLL for (int r = 0; r < 3; ++r) m.P[i][r] = q[r];
-        }
+        RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) eigenRot[r][c] = Ve[c][r];
     }
+    return planar;
+}
+
+// Point i of the design matrix: pw (general) or eigenRot * pw (planar).
+RSC_HD void ml_design_point(bool planar, const double (&eigenRot)[3][3], const double* pw, double (&P)[3]) {
+    double q[3];
+    RSC_UNROLL for (int r = 0; r < 3; ++r) q[r] = eigenRot[r][0] * pw[0] + eigenRot[r][1] * pw[1] + eigenRot[r][2] * pw[2];
+    RSC_UNROLL for (int r = 0; r < 3; ++r) P[r] = planar ? q[r] : pw[r];
+}
+
+template <int NS, class Cov>
+RSC_HD void mlpnp_prepare(const double (&pw)[NS][3], const double (&f)[NS][3], const Cov& cov, MlPrep<NS, Cov>& m) {
+    RSC_UNROLL for (int i = 0; i < NS; ++i) ml_bearing_nullspace(f[i], m.Ns[i]);
+    if constexpr (Cov::on) RSC_UNROLL for (int i = 0; i < NS; ++i) ml_cov_weight(m.Ns[i], cov, i, m.Pw[i]);
+    m.planar = ml_planarity<NS>(pw, m.eigenRot);
+    RSC_UNROLL for (int i = 0; i < NS; ++i) ml_design_point(m.planar, m.eigenRot, pw[i], m.P[i]);
 }
 
 // Row (2i + s) of the design matrix A (:418-470), column col (< 9 planar, < 12 general).
-template <int NS, class Cov>
-RSC_HD double mlpnp_A(const MlPrep<NS, Cov>& m, int i, int s, int col) {
-    const double n0 = m.Ns[i][0][s], n1 = m.Ns[i][1][s], n2 = m.Ns[i][2][s];
-    if (m.planar) {
+RSC_HD double mlpnp_A_entry(bool planar, double n0, double n1, double n2, const double (&P)[3], int col) {
+    if (planar) {
         switch (col) {
-            case 0: return n0 * m.P[i][1]; case 1: return n0 * m.P[i][2];
-            case 2: return n1 * m.P[i][1]; case 3: return n1 * m.P[i][2];
-            case 4: return n2 * m.P[i][1]; case 5: return n2 * m.P[i][2];
+            case 0: return n0 * P[1]; case 1: return n0 * P[2];
+            case 2: return n1 * P[1]; case 3: return n1 * P[2];
+            case 4: return n2 * P[1]; case 5: return n2 * P[2];
             case 6: return n0; case 7: return n1; default: return n2;
         }
     }
     switch (col) {
-        case 0: return n0 * m.P[i][0]; case 1: return n0 * m.P[i][1]; case 2: return n0 * m.P[i][2];
-        case 3: return n1 * m.P[i][0]; case 4: return n1 * m.P[i][1]; case 5: return n1 * m.P[i][2];
-        case 6: return n2 * m.P[i][0]; case 7: return n2 * m.P[i][1]; case 8: return n2 * m.P[i][2];
+        case 0: return n0 * P[0]; case 1: return n0 * P[1]; case 2: return n0 * P[2];
+        case 3: return n1 * P[0]; case 4: return n1 * P[1]; case 5: return n1 * P[2];
+        case 6: return n2 * P[0]; case 7: return n2 * P[1]; case 8: return n2 * P[2];
         case 9: return n0; case 10: return n1; default: return n2;
     }
+}
+template <int NS, class Cov>
+RSC_HD double mlpnp_A(const MlPrep<NS, Cov>& m, int i, int s, int col) {
+    return mlpnp_A_entry(m.planar, m.Ns[i][0][s], m.Ns[i][1][s], m.Ns[i][2][s], m.P[i], col);
 }
 
 // Entry (a, b) of the normal matrix A^T A (:471-478), or A^T P A with covariances (:483-484,
 // evaluated as (A^T P) then the row sums in order).  ra[i][s] / rb[i][s]: A(2i + s, a) / A(2i + s, b).
 // Without covariances the value is symmetric bit for bit (the products commute).
-template <int NS, class Cov>
-RSC_HD double mlpnp_normal_entry(const MlPrep<NS, Cov>& m, const double (&ra)[NS][2], const double (&rb)[NS][2]) {
+template <int NS, class Cov, class M>
+RSC_HD double mlpnp_normal_entry(const M& m, const double (&ra)[NS][2], const double (&rb)[NS][2]) {
     if constexpr (Cov::on) {
-        auto AtP = [&](int i, int q) { return ra[i][0] * m.Pw[i][q] + ra[i][1] * m.Pw[i][2 + q]; };
+        auto AtP = [&](int i, int q) { return ra[i][0] * m.pwgt(i, q) + ra[i][1] * m.pwgt(i, 2 + q); };
         double s = AtP(0, 0) * rb[0][0];
         s = s + AtP(0, 1) * rb[0][1];
         RSC_UNROLL for (int i = 1; i < NS; ++i) {

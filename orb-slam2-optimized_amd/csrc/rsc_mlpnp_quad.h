@@ -277,18 +277,56 @@ __device__ __forceinline__ void mlpnp_quad_hypothesis(const DevML& P, const int 
             pw[i][0] = p.x; pw[i][1] = p.y; pw[i][2] = p.z;
             f[i][0] = b.x; f[i][1] = b.y; f[i][2] = 1.0;
         }
-        MlPrep<NS, Cov> m;
-        mlpnp_prepare<NS, Cov>(pw, f, cov, m);
-        planar = m.planar;
-        ml_park<NS, Cov>(stash, pw, f, m);
         // the design matrix A (2 NS x 12, columns beyond colsA zero) through the GN slab: every lane
         // writes all of it (identical values, static indices), then reads its own columns back
-        const int colsA = planar ? 9 : 12;
         double* At = region;
-        RSC_UNROLL for (int i = 0; i < NS; ++i)
-            RSC_UNROLL for (int s = 0; s < 2; ++s)
-                RSC_UNROLL for (int c = 0; c < 12; ++c)
-                    At[(2 * i + s) * 12 + c] = (c < colsA) ? mlpnp_A<NS, Cov>(m, i, s, c) : 0.0;
+        constexpr bool kParkAsYouGo = Cov::on || NS > 6;
+        // phase-1 state: in registers (NS = 6 without covariances), or — where the nullspaces, the
+        // covariance weights and the points do not fit beside each other (19 NS + 9 doubles) —
+        // parked correspondence by correspondence as it is produced (ml_park's layout) and read back
+        MlPrep<NS, Cov> m;
+        if constexpr (!kParkAsYouGo) {
+            mlpnp_prepare<NS, Cov>(pw, f, cov, m);
+            planar = m.planar;
+            ml_park<NS, Cov>(stash, pw, f, m);
+        } else {
+            using PV = MlParked<NS, Cov>;
+            RSC_UNROLL for (int i = 0; i < NS; ++i) {
+                double Ns[3][2];
+                ml_bearing_nullspace(f[i], Ns);
+                RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int s = 0; s < 2; ++s) stash[PV::kNs + 6 * i + 2 * r + s] = Ns[r][s];
+                if constexpr (Cov::on) {
+                    double Pw4[4];
+                    ml_cov_weight(Ns, cov, i, Pw4);
+                    RSC_UNROLL for (int e = 0; e < 4; ++e) stash[PV::kPw + 4 * i + e] = Pw4[e];
+                }
+                RSC_UNROLL for (int c = 0; c < 3; ++c) { stash[3 * i + c] = pw[i][c]; stash[PV::kF + 3 * i + c] = f[i][c]; }
+            }
+            double eigenRot[3][3];
+            planar = ml_planarity<NS>(pw, eigenRot);
+            RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) stash[PV::kEig + 3 * r + c] = eigenRot[r][c];
+            stash[PV::kEig + 9] = planar ? 1.0 : 0.0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            RSC_UNROLL for (int i = 0; i < NS; ++i) {
+                double Pi[3];
+                ml_design_point(planar, eigenRot, pw[i], Pi);
+                RSC_UNROLL for (int s = 0; s < 2; ++s) {
+                    const double n0 = stash[PV::kNs + 6 * i + s], n1 = stash[PV::kNs + 6 * i + 2 + s],
+                                 n2 = stash[PV::kNs + 6 * i + 4 + s];
+                    RSC_UNROLL for (int c = 0; c < 12; ++c)
+                        At[(2 * i + s) * 12 + c] = (c < (planar ? 9 : 12)) ? mlpnp_A_entry(planar, n0, n1, n2, Pi, c) : 0.0;
+                }
+            }
+        }
+        const int colsA = planar ? 9 : 12;
+        if constexpr (!kParkAsYouGo) {
+            RSC_UNROLL for (int i = 0; i < NS; ++i)
+                RSC_UNROLL for (int s = 0; s < 2; ++s)
+                    RSC_UNROLL for (int c = 0; c < 12; ++c)
+                        At[(2 * i + s) * 12 + c] = (c < colsA) ? mlpnp_A<NS, Cov>(m, i, s, c) : 0.0;
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -302,7 +340,9 @@ __device__ __forceinline__ void mlpnp_quad_hypothesis(const DevML& P, const int 
             RSC_UNROLL for (int i = 0; i < NS; ++i)
                 RSC_UNROLL for (int s = 0; s < 2; ++s) ra[i][s] = At[(2 * i + s) * 12 + r];
             RSC_UNROLL for (int j = 0; j < 3; ++j) {
-                const double v = mlpnp_normal_entry<NS, Cov>(m, ra, rb[j]);
+                double v;
+                if constexpr (Cov::on || NS > 6) v = mlpnp_normal_entry<NS, Cov>(MlParked<NS, Cov>{stash}, ra, rb[j]);
+                else v = mlpnp_normal_entry<NS, Cov>(m, ra, rb[j]);
                 Wc[j][r] = (r < colsA && 4 * j + q < colsA) ? v : 0.0;
             }
         }

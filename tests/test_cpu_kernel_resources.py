@@ -23,6 +23,9 @@ SCRATCH_FREE = [
     "sim3opt_kernel", "bow_topk_kernelILb0E", "bow_topk_kernelILb1E", "bow_walk_kernel",
     "sim3_search_kernel", "poseopt_kernel",
     "mlpnp_quad_kernelILi6ENS_7MlNoCov", "mlpnp_quad_kernelILi6ENS_12MlIndexedCov",
+    # round 4: the NS = 7 / 8 variants too (their phase-1 state is parked as it is produced)
+    "mlpnp_quad_kernelILi7ENS_7MlNoCov", "mlpnp_quad_kernelILi7ENS_12MlIndexedCov",
+    "mlpnp_quad_kernelILi8ENS_7MlNoCov", "mlpnp_quad_kernelILi8ENS_12MlIndexedCov",
 ]
 
 
@@ -56,7 +59,7 @@ def _kernels():
 # the 256 architectural VGPRs of a wave; since round 4 both MLPnP NS = 6 variants evaluate the
 # reference's generated Jacobian (mlpnpJacs, ~200 temporaries per correspondence, rsc_mlpnp_jac.h);
 # their private segments must still be empty
-AGPR_SPILL_OK = ["sim3opt_kernel", "mlpnp_quad_kernelILi6ENS_12MlIndexedCov", "mlpnp_quad_kernelILi6ENS_7MlNoCov"]
+AGPR_SPILL_OK = ["sim3opt_kernel", "mlpnp_quad_kernel"]
 
 
 def test_hot_path_kernels_have_no_scratch():

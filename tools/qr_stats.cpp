@@ -58,7 +58,7 @@ int main() {
     double sw_mean = 0, rot_mean = 0;
     for (int h = 0; h < H; ++h) { sw_mean += sweeps[h].size(); rot_mean += rot[h]; }
     printf("per hypothesis: sweeps %.2f, rotations %.2f\n", sw_mean / H, rot_mean / H);
-    for (int G : {1, 4, 16, 64}) {
+    for (int G : {1, 4, 16, 20, 64}) {
         double slots = 0, sweeps_w = 0, maxrot = 0, maxev = 0;
         for (int w = 0; w < H; w += G) {
             size_t ns = 0;
