@@ -5,6 +5,9 @@
 #include "ora_linalg.h"
 #include "../orb-slam2-optimized_amd/csrc/rsc_math.h"
 #include "../orb-slam2-optimized_amd/csrc/rsc_mlpnp_jac.h"
+#ifndef ORA_JAC_LIBM
+#define ORA_JAC_LIBM ora_libm::JacLibm  // the op-counter build (tools/opcount_libm.h) passes a counting policy
+#endif
 #include <cassert>
 #include <cmath>
 #include <cstring>
@@ -353,9 +356,9 @@ void rot2rodrigues(const double R[3][3], double w[3]) {
 void mlpnp_jac(const double X[3], const double nr[3], const double ns[3], const double w[3], const double t[3],
                double J[2][6]) {
     rsc::MlJacWArr W;
-    rsc::mlpnp_jac_w<ora_libm::JacLibm>(w, W);
+    rsc::mlpnp_jac_w<ORA_JAC_LIBM>(w, W);
     double Jm[2][6];
-    rsc::mlpnp_jac_pt<ora_libm::JacLibm>(W, X, nr, ns, t, w, Jm);
+    rsc::mlpnp_jac_pt<ORA_JAC_LIBM>(W, X, nr, ns, t, w, Jm);
     for (int r = 0; r < 2; ++r)
         for (int c = 0; c < 6; ++c) J[r][c] = Jm[r][c];
 }

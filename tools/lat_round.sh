@@ -15,7 +15,6 @@ RSC_FUSED_REFINE=0 timeout -k 10 120 python tools/latency_trace.py reloc 100 > $
 timeout -k 10 120 python tools/latency_trace.py reloc 100 >> $OUT/lat_fused.txt 2>&1
 timeout -k 10 120 python tools/latency_trace.py loop 100 > $OUT/lat_loop.txt 2>&1
 timeout -k 10 120 python tools/refine_latency_probe.py tools/bin/librsc_stamps.so > $OUT/refine_probe.txt 2>&1
-timeout -k 10 60 ./tools/bin/eig_probe > $OUT/eig_probe.txt 2>&1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_lat -o lat --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/latency_trace.py reloc 50 > $OUT/prof_lat.txt 2>&1
 echo done > $OUT/done

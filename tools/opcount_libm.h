@@ -8,8 +8,24 @@ namespace ora_libm {
 inline CntD sin(CntD x) { ++g_flops; return CntD(sin(x.v)); }
 inline CntD cos(CntD x) { ++g_flops; return CntD(cos(x.v)); }
 inline CntD acos(CntD x) { ++g_flops; return CntD(acos(x.v)); }
-inline CntD cbrt_pow(CntD x) { ++g_flops; return CntD(cbrt_pow(x.v)); }
+inline CntD pow_1_3(CntD x) { ++g_flops; return CntD(pow_1_3(x.v)); }
+inline CntD pow_3_2(CntD x) { ++g_flops; return CntD(pow_3_2(x.v)); }
 }  // namespace ora_libm
+namespace rsc {
+namespace dm {
+inline CntD sin(CntD x) { ++g_flops; return CntD(sin(x.v)); }
+inline CntD cos(CntD x) { ++g_flops; return CntD(cos(x.v)); }
+inline CntD pow_3_2(CntD x) { ++g_flops; return CntD(pow_3_2(x.v)); }
+}  // namespace dm
+}  // namespace rsc
+inline CntD sqrt(CntD x) { return std::sqrt(x); }  // unqualified sqrt of rsc_mlpnp_jac.h (ADL)
+// the shared mlpnpJacs restatement's libm policy on the counting scalar (oracle ORA_JAC_LIBM)
+struct OpcJacLibm {
+    static CntD sin(CntD x) { return ora_libm::sin(x); }
+    static CntD cos(CntD x) { return ora_libm::cos(x); }
+    static CntD pow_3_2(CntD x) { return ora_libm::pow_3_2(x); }
+};
+#define ORA_JAC_LIBM OpcJacLibm
 namespace std {
 inline bool isfinite(CntD x) { return std::isfinite(x.v); }
 inline bool isnan(CntD x) { return std::isnan(x.v); }

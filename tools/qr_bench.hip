@@ -575,5 +575,9 @@ int main(int argc, char** argv) {
     GROUP(4, 10, 3, 0)
     GROUP(4, 8, 3, 0)
     GROUP(4, 5, 3, 0)
+    GROUP(2, 20, 2, 0)
+    GROUP(2, 20, 1, 0)
+    GROUP(4, 16, 2, 0)
+    GROUP(4, 10, 2, 0)
     return 0;
 }
