@@ -218,6 +218,29 @@ struct GroupLdsRows {
     }
 };
 
+// The group's own rows of Q held in VGPRs (Qr[j] = row L*j + q): the same rotation as
+// GroupLdsRows without the LDS round trip (A/B variant, RSC_EIG_REGROWS; tools/qr_bench sink 2).
+template <int L>
+struct GroupRegRows {
+    static constexpr int RJ = 12 / L;
+    double (&Q)[RJ][12];
+    RSC_HD void operator()(int k, double c, double s, bool apply) {
+        if (__builtin_expect(__any(!apply), 0)) {
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                const double x = Q[j][k], y = Q[j][k + 1];
+                Q[j][k] = apply ? c * x - s * y : x;
+                Q[j][k + 1] = apply ? s * x + c * y : y;
+            }
+        } else {
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                const double x = Q[j][k], y = Q[j][k + 1];
+                Q[j][k] = c * x - s * y;
+                Q[j][k + 1] = s * x + c * y;
+            }
+        }
+    }
+};
+
 // Scale of SelfAdjointEigenSolver = max |lower triangle| over the group's own rows (A: full
 // symmetric own rows, R = L*j + q); a NaN M(0,0) poisons it, as there.
 template <int L>
@@ -476,6 +499,25 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
     // Sweep form: the own rows of Q stay in LDS (T, row-major), so the rotations' read-modify-
     // writes are off the Givens chase's dependency chain.  (The event and split-chase forms of the
     // QR, tools/qr_events.h, are bit-identical and measured slower on gfx950)
+#ifdef RSC_EIG_REGROWS
+    {
+        int perm[12];
+        double Qr[RJ][12];
+        RSC_UNROLL for (int j = 0; j < RJ; ++j)
+            RSC_UNROLL for (int c = 0; c < 12; ++c) Qr[j][c] = T[(L * j + q) * 12 + c];
+        GroupRegRows<L> qapply{Qr};
+        tridiag_qr<double, 12>(diag, sub, qapply, perm);
+        if (active) {
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                RSC_UNROLL for (int c = 0; c < 4; ++c) {
+                    double x = Qr[j][0];
+                    RSC_UNROLL for (int p = 1; p < 12; ++p) x = (perm[c] == p) ? Qr[j][p] : x;
+                    out[kStEv + (L * j + q) * 4 + c] = x;
+                }
+            }
+        }
+    }
+#else
     {
         int perm[12];
         GroupLdsRows<L> qapply{T, q};
@@ -494,6 +536,7 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
             }
         }
     }
+#endif
 }
 
 // Eigenvectors read from the stage record in global memory (stride 1), L + rho in LDS
