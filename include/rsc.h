@@ -61,7 +61,8 @@ int rsc_context_enable_timing(rsc_context* ctx, int enable);
  * (rsc_core.h): 6 sqrt for x in [1,4), 7 1/x for |x| in [1,2), 8 / 9 make_givens(x[i],
  * x[(i+n/2)%n]) c / s; 10 qr_solve_6x4 (PnPsolver.cpp:693-796) on records of 34 doubles
  * (A[6][4] row-major, b[6], previous X[4]) -> X in out[0..3], 1/0 success in out[4] of each record
- * (n a multiple of 34).  Host pointers, n >= 0.  Tests compare with glibc / IEEE numpy / the oracle. */
+ * (n a multiple of 34); 11 pow(x, 1.0/3.0), 12 pow(x, 3.0/2.0) as MLPnP computes them (x >= 0;
+ * MLPnPsolver.cpp:567, :839, :901).  Host pointers, n >= 0.  Tests compare with glibc / IEEE numpy / the oracle. */
 int rsc_selftest_math(rsc_context* ctx, int fn, const double* x, int n, double* out);
 
 /* ---- PnPsolver (include/PnPsolver.hpp:21-138, src/PnPsolver.cpp) ------------------------------ */

@@ -813,6 +813,9 @@ __global__ __launch_bounds__(256) void selftest_math_kernel(int fn, const double
         // make_givens pairs x[i] with x[(i + n/2) % n]
         case 6: r = sqrt_unit(v); break;
         case 7: r = recip_unit(v); break;
+        // MLPnP's pow(x, 1.0/3.0) and pow(t, 3.0/2.0) restatements (rsc_math.h)
+        case 11: r = dm::pow_1_3(v); break;
+        case 12: r = dm::pow_3_2(v); break;
         default: {
             double c, s;
             make_givens(v, x[(i + n / 2) % n], c, s);
@@ -883,7 +886,7 @@ hipError_t launch_upload16(const void* host_src, void* dev_dst, size_t n16, hipS
 }
 
 hipError_t launch_selftest_math(int fn, const double* x, int n, double* out, hipStream_t st) {
-    if (fn < 0 || fn > 10 || n <= 0) return hipErrorInvalidValue;
+    if (fn < 0 || fn > 12 || n <= 0) return hipErrorInvalidValue;
     if (fn == 10) {
         if (n % 34) return hipErrorInvalidValue;
         const int nrec = n / 34;

@@ -1071,7 +1071,7 @@ int rsc_context_enable_timing(rsc_context* C, int enable) {
 }
 
 int rsc_selftest_math(rsc_context* C, int fn, const double* x, int n, double* out) {
-    if (!C || fn < 0 || fn > 10 || n < 0 || (n > 0 && (!x || !out)) || (fn == 10 && n % 34)) return RSC_ERR_ARG;
+    if (!C || fn < 0 || fn > 12 || n < 0 || (n > 0 && (!x || !out)) || (fn == 10 && n % 34)) return RSC_ERR_ARG;
     if (n == 0) return RSC_OK;
     RSC_HIP(hipSetDevice(C->device));
     double* d = nullptr;

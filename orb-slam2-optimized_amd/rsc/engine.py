@@ -447,7 +447,7 @@ class Context:
         _check(load_library().rsc_context_enable_timing(self.h, int(on)), "enable_timing")
 
     MATH_FNS = {"sin": 0, "cos": 1, "acos": 2, "cbrt": 3, "log": 4, "logf": 5, "sqrt_unit": 6, "recip_unit": 7,
-                "givens_c": 8, "givens_s": 9, "qr_solve": 10}
+                "givens_c": 8, "givens_s": 9, "qr_solve": 10, "pow_1_3": 11, "pow_3_2": 12}
 
     def selftest_math(self, fn: str, x):
         """rsc_math.h evaluated on the GPU (f64 array in, f64 array out; logf: float in/out)."""

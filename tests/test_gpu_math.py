@@ -1,5 +1,5 @@
-"""GPU: the device libm restatement (rsc_math.h — fdlibm-style sin/cos/acos/cbrt/log used by the
-Sim3 angles, MLPnP and MapPoint::PredictScale in SearchBySim3) evaluated ON THE GPU through
+"""GPU: the device libm restatement (rsc_math.h — fdlibm-style sin/cos/acos/cbrt/log and the
+correctly rounded pow(x, 1/3) / pow(x, 3/2) used by the Sim3 angles, MLPnP and MapPoint::PredictScale in SearchBySim3) evaluated ON THE GPU through
 rsc_selftest_math, checked (a) bit-for-bit against the same functions compiled for the host (the
 oracle's ora_dm_*: device code generation changes nothing) and (b) within 1 ulp of glibc (Python's
 math module), the CPU test's bar (tests/test_cpu_mlpnp.py), on the ranges the kernels feed them."""
@@ -24,13 +24,15 @@ def _ulp_close(a, b, k):
     return abs(a - b) <= k * math.ulp(b) + 1e-300
 
 
-@pytest.mark.parametrize("name", ["sin", "cos", "acos", "cbrt", "log", "logf"])
+@pytest.mark.parametrize("name", ["sin", "cos", "acos", "cbrt", "log", "logf", "pow_1_3", "pow_3_2"])
 def test_device_libm_matches_host_restatement_and_glibc(name):
     rng = np.random.default_rng(42)
     if name == "acos":
         x = np.concatenate([rng.uniform(-1, 1, 60000), [-1.0, 1.0, 0.0, 0.5, -0.5, 1 - 2**-52, -1 + 2**-52]])
-    elif name == "cbrt":
+    elif name in ("cbrt", "pow_1_3", "pow_3_2"):
         x = np.abs(_inputs(rng)) + 1e-300
+        if name != "cbrt":  # MLPnP's ranges: the scale's |s| and the Jacobian's squared norms
+            x = np.concatenate([x, 10.0 ** rng.uniform(-12, 12, 40000), [0.0, 1.0, 4.0, 8.0, 27.0]])
     elif name in ("log", "logf"):
         # SearchBySim3's PredictScale ratios and a wide sweep
         x = np.concatenate([rng.uniform(0.5, 3.0, 30000), 10.0 ** rng.uniform(-30, 30, 30000), [1.0, 2.0, 1.2]])
@@ -39,7 +41,7 @@ def test_device_libm_matches_host_restatement_and_glibc(name):
     dev = gpu_ctx().selftest_math(name, x)
     L = ol.lib()
     host_fn = {"sin": L.ora_dm_sin, "cos": L.ora_dm_cos, "acos": L.ora_dm_acos, "cbrt": L.ora_dm_cbrt,
-               "log": L.ora_dm_log, "logf": L.ora_dm_log}[name]
+               "log": L.ora_dm_log, "logf": L.ora_dm_log, "pow_1_3": L.ora_dm_pow13, "pow_3_2": L.ora_dm_pow32}[name]
     if name == "logf":
         host = np.array([float(np.float32(host_fn(float(np.float32(v))))) for v in x])
     else:
@@ -47,6 +49,7 @@ def test_device_libm_matches_host_restatement_and_glibc(name):
     assert np.array_equal(dev.view(np.uint64), host.view(np.uint64)), name
     glibc = {"sin": math.sin, "cos": math.cos, "acos": math.acos,
              "cbrt": lambda v: float(np.cbrt(v)), "log": math.log,
+             "pow_1_3": lambda v: math.pow(v, 1.0 / 3.0), "pow_3_2": lambda v: math.pow(v, 3.0 / 2.0),
              "logf": lambda v: float(np.float32(math.log(float(np.float32(v)))))}[name]
     k = 1
     for xi, di in zip(x, dev):
