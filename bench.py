@@ -631,6 +631,34 @@ def latency_event(kind: str, seed: int = 4242):
     return rev.Event("loop", 100001, sizes, ratios, [9 + c for c in range(C)])
 
 
+def eig_rows_ab(ctx, eb, params, seeds, ref, reps):
+    """Interleaved A/B of the eigen-stage form on the single relocalization event: the lane-pair
+    form (default) vs the Refine's rows form (rsc_context_set_eig_rows), same event,
+    alternating calls; the event's outcome must not change.  Off-default variant: reported, not the
+    metric."""
+    keys = ("winner", "round", "hypothesis", "n_inliers")
+    times = {0: [], 1: []}
+    same = True
+    try:
+        for r in range(2 * (reps + 5)):
+            mode = r & 1
+            ctx.set_eig_rows(1 << 20 if mode else 0)
+            t0 = time.perf_counter()
+            eb.batch.reset(seeds)
+            eb.batch.set_ransac_parameters(*params)
+            res = eb.run()
+            t = time.perf_counter() - t0
+            if r >= 10:
+                times[mode].append(t)
+            same = same and all(int(res[0][k]) == int(ref[k]) for k in keys)
+    except Exception as e:  # an A/B variant must never cost the bench line
+        return dict(error=str(e)[:200])
+    finally:
+        ctx.set_eig_rows(0)
+    return dict(pairs_ms=round(1e3 * float(np.median(times[0])), 4), rows_ms=round(1e3 * float(np.median(times[1])), 4),
+                same_result=bool(same), reps=len(times[1]))
+
+
 def run_latency(engine, ctx, args, with_cpu, reps=50):
     """Single-event latency: ONE rsc_reloc_events / rsc_loop_events call on one event (reset +
     SetRansacParameters + the iterate(5) round-robin, result on the host), median over reps calls;
@@ -654,6 +682,8 @@ def run_latency(engine, ctx, args, with_cpu, reps=50):
         sec = dict(candidates=len(ev.sizes), mean_corrs=float(np.mean(ev.sizes)), winner=int(pe["winner"]),
                    round=int(pe["round"]), hypotheses=int(eb.cand["iterations"].sum()),
                    gpu_ms=round(1e3 * float(np.median(times)), 4), reps=reps)
+        if kind == "reloc":
+            sec["eig_rows_ab"] = eig_rows_ab(ctx, eb, params, seeds, pe, reps)
         if with_cpu:
             pk = eo.PackedEvents([ev])
             med, n = median_batches(lambda: pk.run(1), warmup=3, reps=20)

@@ -200,6 +200,18 @@ constexpr int kFoldStride = 65;
 constexpr int kRefineEigLanes = RSC_REFINE_EIG_LANES;
 static_assert(kRefineEigLanes == 2 || kRefineEigLanes == 4, "refine eigen group: pair or quad");
 
+// Eigen stage in the Refine's rows form for small launches (rsc_quad.h pnp_eig_rows_body; A/B
+// variant behind RSC_EIG_ROWS): same workgroup table and stage records as pnp_eig_group_kernel.
+template <int NS>
+__global__ __launch_bounds__(256) void pnp_eig_rows_kernel(const DevPnP* __restrict__ probs,
+                                                           const LaunchProb* __restrict__ lps,
+                                                           const int2* __restrict__ wg_table,
+                                                           const uint32_t* __restrict__ rng_T,
+                                                           double* __restrict__ stage, int32_t* __restrict__ samples) {
+    __shared__ __attribute__((aligned(16))) double smem[kEigHyps * kRowsRegion];
+    pnp_eig_rows_body<NS, kRefineEigLanes>(probs, lps, wg_table, rng_T, stage, samples, smem, [] { wave_lds_sync(); });
+}
+
 // Ordered sums of K columns of per-row terms over rows [0, count), by one wave.  term(i, t[K]).
 // from_zero: s = ((0.0 + t0) + t1) + ... (loops starting from 0.0), else s = (t0 + t1) + ...
 // Returns column k's sum in lane k (k < K); buf holds kFoldStride*K doubles of this wave.
@@ -777,13 +789,16 @@ __global__ void rng_stream_kernel(const uint32_t* __restrict__ T, Window31 w, in
 hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, const int2* wgtB,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
-                                  hipEvent_t eig_begin, hipEvent_t eig_end) {
+                                  hipEvent_t eig_begin, hipEvent_t eig_end, bool eig_rows) {
     if (ns < 4 || ns > 6) return hipErrorInvalidValue;
     if (eig_begin) (void)hipEventRecord(eig_begin, st);
     switch (ns) {
 #define RSC_CASE(N)                                                                                   \
     case N:                                                                                           \
-        pnp_eig_group_kernel<N><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples);            \
+        if (eig_rows)                                                                                 \
+            pnp_eig_rows_kernel<N><<<nwgE, 256, 0, st>>>(probs, lps, wgtE, T, stage, samples);        \
+        else                                                                                          \
+            pnp_eig_group_kernel<N><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples);        \
         if (eig_end) (void)hipEventRecord(eig_end, st);                                               \
         pnp_betas_kernel<N><<<3 * nwgB, 64, 0, st>>>(probs, lps, wgtB, nwgB, stage, samples, poses,   \
                                                      bs.err, bs.pose, bs.ctr, bs.hcap);               \

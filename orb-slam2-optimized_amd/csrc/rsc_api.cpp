@@ -206,6 +206,7 @@ struct rsc_context {
     bool direct_counts = true;  // env RSC_DIRECT_COUNTS=0 restores the HBM buffer + D2H copy
     bool fused_refine = true;   // env RSC_FUSED_REFINE=0: the replay's Refine always as its own launch
     bool dma_upload = false;    // env RSC_DMA_UPLOAD=1: descriptors by hipMemcpyAsync instead of the copy kernel
+    int eig_rows_max_wgs = 0;   // env RSC_EIG_ROWS=W: eigen stage in the rows form when it has <= W workgroups (A/B, off)
     std::chrono::steady_clock::time_point t_entry;
 };
 
@@ -507,7 +508,8 @@ struct HipPnPBackend : PnPBackend {
                                           reinterpret_cast<const int2*>(base + o_quad[g]), (int)solve_wgs[g].size(),
                                           reinterpret_cast<const int2*>(base + o_solve[g]), dprobs, dlps,
                                           C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p, bs, C->stream,
-                                          eb, C->timing ? C->ev[7 + 2 * g] : nullptr));
+                                          eb, C->timing ? C->ev[7 + 2 * g] : nullptr,
+                                          (int)quad_wgs[g].size() <= C->eig_rows_max_wgs));
             first_group = false;
         }
         timing_begin(C, 1);
@@ -1031,6 +1033,7 @@ int rsc_context_create(int device, rsc_context** out) {
     if (const char* m = std::getenv("RSC_DIRECT_COUNTS")) C->direct_counts = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_FUSED_REFINE")) C->fused_refine = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_DMA_UPLOAD")) C->dma_upload = std::strcmp(m, "0") != 0;
+    if (const char* m = std::getenv("RSC_EIG_ROWS")) C->eig_rows_max_wgs = std::max(0, std::atoi(m));
     C->table.build();
     if (int e = C->d_table.ensure(C->table.T.size())) return e;
     RSC_HIP(hipMemcpy(C->d_table.p, C->table.T.data(), C->table.T.size() * 4, hipMemcpyHostToDevice));
@@ -1067,6 +1070,12 @@ int rsc_context_synchronize(rsc_context* C) {
 int rsc_context_enable_timing(rsc_context* C, int enable) {
     if (!C) return RSC_ERR_ARG;
     C->timing = enable != 0;
+    return RSC_OK;
+}
+
+int rsc_context_set_eig_rows(rsc_context* C, int max_workgroups) {
+    if (!C || max_workgroups < 0) return RSC_ERR_ARG;
+    C->eig_rows_max_wgs = max_workgroups;
     return RSC_OK;
 }
 

@@ -539,6 +539,74 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
 #endif
 }
 
+// The eigen stage in the Refine's form, for small (latency-bound) launches (A/B variant, selected
+// by RSC_EIG_ROWS, rsc_api.cpp): a 12-lane group per hypothesis, 5 groups per wave, 4 waves per
+// workgroup of kEigHyps = 20 hypotheses (the pair form's workgroup table).  Phase A as
+// pnp_eig_group_body; phases B-D by rows_eig12_ev4 — Householder phases on the group's first L
+// lanes, then the chase with lane r holding row r of Q in VGPRs, which runs a rotation slot in the
+// Refine's ~685 clocks instead of the pair form's ~1,500.  Bit-identical to the pair
+// form (rows_eig12_ev4 is group_eig12_ev4's arithmetic).  Needs kEigHyps * kRowsRegion doubles.
+constexpr int kRowsGroups = 5;                    // 12-lane groups per wave
+constexpr int kRowsRegion = kQuadT + 90 + 1;      // T, E (rows_eig12_ev4: >= 90 doubles), odd pad
+template <int NS, int L, class Sync>
+__device__ __forceinline__ void pnp_eig_rows_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
+                                                  const int2* __restrict__ wg_table, const uint32_t* __restrict__ rng_T,
+                                                  double* __restrict__ stage, int32_t* __restrict__ samples,
+                                                  double* smem, Sync sync) {
+    static_assert(kEigHyps == 4 * kRowsGroups, "4 waves of 5 twelve-lane groups per workgroup");
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane / 12, r = lane - 12 * g;
+    if (g >= kRowsGroups) return;  // lanes 60..63: whole groups only
+    const int2 wt = wg_table[blockIdx.x];
+    const LaunchProb& lp = lps[wt.x];
+    const int slot = kRowsGroups * wave + g;
+    if (wt.y + kRowsGroups * wave >= lp.H) return;  // a wave without hypotheses (no cross-wave sync below)
+    const bool active = wt.y + slot < lp.H;
+    const int h = active ? wt.y + slot : lp.H - 1;  // idle groups repeat the last hypothesis (no writes)
+    const DevPnP& P = probs[lp.prob];
+    const size_t rec = (size_t)(lp.out0 + h);
+    double* out = stage + rec * kStageDoubles;
+    double* T = smem + slot * kRowsRegion;
+    double* E = T + kQuadT;
+
+    // ---- A: sample, control points, alphas, MtM (every lane of the group, identical values) ----
+    {
+        int idx[NS];
+        uint32_t w[31];
+        RSC_UNROLL for (int j = 0; j < 31; ++j) w[j] = lp.window[j];
+        uint32_t words[NS];
+        RSC_UNROLL for (int d = 0; d < NS; ++d) words[d] = rng_word(rng_T, w, lp.g0 + h * NS + d);
+        swap_remove_sample<NS>(words, NS, P.n, idx);
+        HypStore<NS> st;
+        RSC_UNROLL for (int i = 0; i < NS; ++i) {
+            const float4 p = P.pts[idx[i]];
+            const float2 uv = P.uv[idx[i]];
+            st.pw_[i][0] = p.x; st.pw_[i][1] = p.y; st.pw_[i][2] = p.z;
+            st.u_[i][0] = uv.x; st.u_[i][1] = uv.y;
+        }
+        st.rows_ = P.rows;
+        st.spw = P.pws;
+        st.sal = P.als;
+        const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
+        double cws[4][3];
+        control_points_and_alphas(st, cws);
+        if (r == 0) {
+            build_MtM(st, K, LaneMat{T, 1});
+            if (active) {
+                RSC_UNROLL for (int i = 0; i < NS; ++i)
+                    RSC_UNROLL for (int j = 0; j < 4; ++j) out[kStAl + i * 4 + j] = st.al(i, j);
+                RSC_UNROLL for (int i = 0; i < 4; ++i)
+                    RSC_UNROLL for (int c = 0; c < 3; ++c) out[kStCws + i * 3 + c] = cws[i][c];
+                RSC_UNROLL for (int i = 0; i < NS; ++i) samples[rec * 8 + i] = idx[i];
+            }
+        }
+    }
+    sync();
+    // ---- B-D: 12x12 eigenvectors, row r of the four smallest eigenvalues' columns in lane r ----
+    double ev[4];
+    rows_eig12_ev4<L>(T, E, r, sync, ev);
+    if (active) RSC_UNROLL for (int c = 0; c < 4; ++c) out[kStEv + r * 4 + c] = ev[c];
+}
+
 // Eigenvectors read from the stage record in global memory (stride 1), L + rho in LDS
 // (element-major across the wave).
 struct StageEvView {

@@ -26,6 +26,8 @@ SCRATCH_FREE = [
     # round 4: the NS = 7 / 8 variants too (their phase-1 state is parked as it is produced)
     "mlpnp_quad_kernelILi7ENS_7MlNoCov", "mlpnp_quad_kernelILi7ENS_12MlIndexedCov",
     "mlpnp_quad_kernelILi8ENS_7MlNoCov", "mlpnp_quad_kernelILi8ENS_12MlIndexedCov",
+    # round 4: the rows form of the eigen stage for small launches (RSC_EIG_ROWS A/B variant)
+    "pnp_eig_rows_kernelILi4E", "pnp_eig_rows_kernelILi5E", "pnp_eig_rows_kernelILi6E",
 ]
 
 
