@@ -90,6 +90,8 @@ def parse():
               "rccl-check"):
         p.add_argument(f"--no-{s}", action="store_true")
     p.add_argument("--only-headline", action="store_true", help="config 2 only (PMC passes)")
+    p.add_argument("--eig-rows-ab", action="store_true",
+                   help="single-event A/B of the rows-form eigen stage (off-default variant, DESIGN.md §9)")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="nccl (= RCCL over xGMI, the product path) or gloo (host collectives: lets N ranks "
                         "share fewer GPUs to rehearse the launch and gather on a 1-GPU box)")
@@ -682,7 +684,7 @@ def run_latency(engine, ctx, args, with_cpu, reps=50):
         sec = dict(candidates=len(ev.sizes), mean_corrs=float(np.mean(ev.sizes)), winner=int(pe["winner"]),
                    round=int(pe["round"]), hypotheses=int(eb.cand["iterations"].sum()),
                    gpu_ms=round(1e3 * float(np.median(times)), 4), reps=reps)
-        if kind == "reloc":
+        if kind == "reloc" and getattr(args, "eig_rows_ab", False):
             sec["eig_rows_ab"] = eig_rows_ab(ctx, eb, params, seeds, pe, reps)
         if with_cpu:
             pk = eo.PackedEvents([ev])
