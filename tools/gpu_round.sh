@@ -1,7 +1,8 @@
 #!/bin/bash
 # GPU-box round script: parity tests, headline bench (with CPU baseline), rocprofv3 kernel stats of
 # the same bench command, and (PMC=1) two PMC passes (FETCH_SIZE, WRITE_SIZE) of the PnP section for
-# the HBM traffic per launch.  Outputs under gpurun_out/$TAG/.  Every step has its own time limit and
+# the HBM traffic per launch; VARIANTS=1 / PLANAR=1 the round-4 A/B measurements (build first:
+# make -C tools qr_bench nonan_lib regrows_lib, cp tools/build/qr_bench tools/bin/).  Outputs under gpurun_out/$TAG/.  Every step has its own time limit and
 # the script stops at the first failure.
 set -e
 TAG=${TAG:-run}
@@ -32,6 +33,24 @@ if [ -n "$SQ" ]; then
   # tools/pmc_summary.py summarises them
   timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY -d $OUT/pmc_sqA -o a --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/pmc_sqA.log 2>&1
   timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_VALU_FMA_F64 SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_INSTS_SMEM -d $OUT/pmc_sqB -o b --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/pmc_sqB.log 2>&1
+fi
+if [ -n "$VARIANTS" ]; then
+  # off-default A/B variants: their parity tests, the single-event A/B of the rows-form
+  # eigen stage, the chase-only sink variants, and the VGPR-row chase library on the headline
+  cd $GRAFT_REPO_ROOT
+  RSC_TEST_VARIANTS=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_variants.py -x -v --timeout 180 --timeout-method thread > $OUT/tests_variants.txt 2>&1
+  timeout -k 10 300 python bench.py --no-cpu --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --eig-rows-ab > $OUT/bench_eig_rows_ab.json 2> $OUT/bench_eig_rows_ab.err
+  timeout -k 10 120 tools/bin/qr_bench > $OUT/qr_bench.txt 2>&1
+  for v in a b a b; do
+    if [ $v = a ]; then L=orb-slam2-optimized_amd/lib/librsc.so; else L=tools/bin/librsc_regrows.so; fi
+    RSC_LIBRSC=$L timeout -k 10 200 python bench.py --only-headline --no-cpu >> $OUT/regrows_ab_$v.jsonl 2>> $OUT/regrows_ab.err
+  done
+fi
+if [ -n "$PLANAR" ]; then
+  # planar-content config-2 eigen stage with and without the NaN-block exit
+  cd $GRAFT_REPO_ROOT
+  timeout -k 10 200 python tools/planar_ab.py $OUT/planar_ab_exit.json exit > $OUT/planar_exit.log 2>&1
+  RSC_LIBRSC=tools/bin/librsc_nonanexit.so timeout -k 10 200 python tools/planar_ab.py $OUT/planar_ab_noexit.json noexit > $OUT/planar_noexit.log 2>&1
 fi
 if [ -n "$GPUS2" ]; then
   cd $GRAFT_REPO_ROOT
