@@ -36,7 +36,17 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec)
 FP32_PEAK_TFLOPS = 157.3   # MI355X vector FP32 (spec)
-PROFILE_DIRS = ("profiles/r03", "profiles/r02")  # newest first
+
+
+def _round_dirs():
+    """profiles/rNN directories, newest round first (side files come from the newest round that has
+    them, so a round that re-measures a file supersedes the older one without a code change)."""
+    base = os.path.join(ROOT, "profiles")
+    names = [d for d in os.listdir(base) if d[:1] == "r" and d[1:].isdigit()] if os.path.isdir(base) else []
+    return tuple(os.path.join("profiles", d) for d in sorted(names, key=lambda d: -int(d[1:])))
+
+
+PROFILE_DIRS = _round_dirs()
 
 
 def _profile_json(name):

@@ -786,6 +786,19 @@ __global__ void rng_stream_kernel(const uint32_t* __restrict__ T, Window31 w, in
 // ------------------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------------------
+// The rows-form eigen stage exists only for the 20-hypothesis workgroup (4 waves x 5 twelve-lane
+// groups); builds with another RSC_EIG_HYPS compile without it and refuse the variant.
+template <int N>
+static hipError_t launch_eig_rows(int nwgE, const int2* wgtE, const DevPnP* probs, const LaunchProb* lps,
+                                  const uint32_t* T, double* stage, int32_t* samples, hipStream_t st) {
+    if constexpr (kEigHyps == 4 * kRowsGroups) {
+        pnp_eig_rows_kernel<N><<<nwgE, 256, 0, st>>>(probs, lps, wgtE, T, stage, samples);
+        return hipSuccess;
+    } else {
+        return hipErrorInvalidValue;
+    }
+}
+
 hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, const int2* wgtB,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
@@ -795,9 +808,10 @@ hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, 
     switch (ns) {
 #define RSC_CASE(N)                                                                                   \
     case N:                                                                                           \
-        if (eig_rows)                                                                                 \
-            pnp_eig_rows_kernel<N><<<nwgE, 256, 0, st>>>(probs, lps, wgtE, T, stage, samples);        \
-        else                                                                                          \
+        if (eig_rows) {                                                                               \
+            const hipError_t e = launch_eig_rows<N>(nwgE, wgtE, probs, lps, T, stage, samples, st);   \
+            if (e != hipSuccess) return e;                                                            \
+        } else                                                                                        \
             pnp_eig_group_kernel<N><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples);        \
         if (eig_end) (void)hipEventRecord(eig_end, st);                                               \
         pnp_betas_kernel<N><<<3 * nwgB, 64, 0, st>>>(probs, lps, wgtB, nwgB, stage, samples, poses,   \

@@ -1167,6 +1167,8 @@ int rsc_pnp_iterate_many(rsc_pnp* const* solvers, int count, const int32_t* n_it
     rsc_context* C = solvers[0]->ctx;
     for (int i = 0; i < count; ++i)
         if (!solvers[i] || solvers[i]->ctx != C) return RSC_ERR_ARG;
+    // vbInliers of a call that fails is empty (rsc_pnp_last_inliers returns 0 after it)
+    for (int i = 0; i < count; ++i) solvers[i]->last_kind = 0;
     C->t_entry = std::chrono::steady_clock::now();
     RSC_HIP(hipSetDevice(C->device));
     for (double& v : C->last_ms) v = 0;
@@ -1221,6 +1223,7 @@ int rsc_pnp_last_inliers(rsc_pnp* s, uint8_t* out) {
 int rsc_pnp_reset(rsc_pnp* s, uint32_t seed) {
     if (!s) return RSC_ERR_ARG;
     s->st.reset(seed);
+    s->last_kind = 0;
     return RSC_OK;
 }
 
@@ -2359,6 +2362,7 @@ int rsc_pnp_reset_many(rsc_pnp* const* s, int count, const uint32_t* seeds) {
     for (int i = 0; i < count; ++i) {
         if (!s[i]) return RSC_ERR_ARG;
         s[i]->st.reset(seeds[i]);
+        s[i]->last_kind = 0;
     }
     return RSC_OK;
 }
@@ -2506,6 +2510,7 @@ int rsc_mlpnp_iterate(rsc_mlpnp* s, int n_its, rsc_pnp_result* out, uint8_t* inl
 int rsc_mlpnp_reset(rsc_mlpnp* s, uint32_t seed) {
     if (!s) return RSC_ERR_ARG;
     s->st.reset(seed);
+    s->last_kind = 0;
     return RSC_OK;
 }
 

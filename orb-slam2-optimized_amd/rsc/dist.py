@@ -84,17 +84,35 @@ def all_gather_records(dist, records: np.ndarray, max_per_rank: int, device=None
 
 
 def local_reloc_candidate(records: np.ndarray) -> int:
-    """The only candidate of this rank's contiguous block that can be the relocalization winner:
-    its lowest-index successful one (Tracking.cpp:1241-1265), or -1."""
+    """The candidate of this rank's contiguous block that can be the relocalization winner of the
+    RANSAC stage: its lowest-index successful one (Tracking.cpp:1241-1265), or -1.
+
+    Limitation: the reference moves on to the next successful candidate when PoseOptimization of
+    the winner keeps fewer than 50 inliers (Tracking.cpp:1284-1331).  Only the winner's vbInliers is
+    exchanged, so a caller that needs that fallback gathers the next candidate's mask with
+    successful_candidates() / a second all_gather_records_and_mask."""
     ok = records[records[:, 1] > 0] if len(records) else records
     return int(ok[0, 0]) if len(ok) else -1
 
 
-def local_loop_candidate(records: np.ndarray) -> int:
+def local_loop_candidate(records: np.ndarray, exclude=()) -> int:
     """The loop-closure winner among this rank's candidates: smallest (round, c) with round =
-    (hypothesis of the first success) // 5 (LoopClosing.cpp:271-327), or -1."""
+    (hypothesis of the first success) // 5 (LoopClosing.cpp:271-327), or -1.  ``exclude`` drops
+    candidates already rejected by the OptimizeSim3 gate (< 20 inliers, LoopClosing.cpp:311-324), so
+    a second exchange finds the next one the reference's loop would reach."""
     ok = records[records[:, 1] > 0] if len(records) else records
-    return loop_winner({int(r[0]): int(r[4]) - 1 for r in ok}) if len(ok) else -1
+    hyp = {int(r[0]): int(r[4]) - 1 for r in ok if int(r[0]) not in exclude}
+    return loop_winner(hyp) if hyp else -1
+
+
+def successful_candidates(records: np.ndarray, kind: str = "reloc") -> list:
+    """Every successful candidate of a record block in the order the reference's event loop visits
+    them: index order for relocalization (Tracking.cpp:1241-1331), (round, c) for loop closure
+    (LoopClosing.cpp:271-327).  The fallback order after a rejected winner."""
+    ok = records[records[:, 1] > 0] if len(records) else records
+    if kind == "reloc":
+        return [int(r[0]) for r in ok]
+    return [c for _, c in sorted(((int(r[4]) - 1) // 5, int(r[0])) for r in ok)]
 
 
 def all_gather_records_and_mask(dist, records: np.ndarray, max_per_rank: int, local_cand: int, local_mask,

@@ -494,10 +494,13 @@ class Context:
         return out
 
 
-def _pnp_out(r: PnPResult, mask: np.ndarray) -> dict:
+def _pnp_out(r: PnPResult, mask) -> dict:
+    """Result dict of one PnP / MLPnP iterate().  ``mask`` None = the caller asked for no vbInliers:
+    ``inliers`` is then None (never a zero array that reads like a result)."""
     T = np.array(r.T, dtype=np.float32).reshape(4, 4)
+    inl = None if mask is None else (mask.astype(bool) if r.ok else np.zeros(0, bool))
     return dict(ok=bool(r.ok), no_more=bool(r.no_more), n_inliers=int(r.n_inliers), iterations=int(r.iterations),
-                T=T, inliers=(mask.astype(bool) if r.ok else np.zeros(0, bool)))
+                T=T, inliers=inl)
 
 
 class PnPSolver:
@@ -583,10 +586,10 @@ def pnp_iterate_many(solvers, n_iterations, with_masks: bool = True):
     hs = (C.c_void_p * n)(*[s.h.value for s in solvers])
     its = np.ascontiguousarray(np.broadcast_to(np.asarray(n_iterations, np.int32), (n,)))
     res = (PnPResult * n)()
-    masks = [np.zeros(max(s.n_points, 1), np.uint8) for s in solvers]
-    mp = (C.c_void_p * n)(*[(m.ctypes.data if with_masks else None) for m in masks])
+    masks = [np.zeros(max(s.n_points, 1), np.uint8) if with_masks else None for s in solvers]
+    mp = (C.c_void_p * n)(*[(m.ctypes.data if m is not None else None) for m in masks])
     _check(L.rsc_pnp_iterate_many(hs, n, its, res, mp), "iterate_many")
-    return [_pnp_out(res[i], masks[i][:solvers[i].n_points]) for i in range(n)]
+    return [_pnp_out(res[i], None if masks[i] is None else masks[i][:solvers[i].n_points]) for i in range(n)]
 
 
 def mlpnp_iterate_many(solvers, n_iterations, with_masks: bool = True):
@@ -596,15 +599,17 @@ def mlpnp_iterate_many(solvers, n_iterations, with_masks: bool = True):
     hs = (C.c_void_p * n)(*[s.h.value for s in solvers])
     its = np.ascontiguousarray(np.broadcast_to(np.asarray(n_iterations, np.int32), (n,)))
     res = (PnPResult * n)()
-    masks = [np.zeros(max(s.n_points, 1), np.uint8) for s in solvers]
-    mp = (C.c_void_p * n)(*[(m.ctypes.data if with_masks else None) for m in masks])
+    masks = [np.zeros(max(s.n_points, 1), np.uint8) if with_masks else None for s in solvers]
+    mp = (C.c_void_p * n)(*[(m.ctypes.data if m is not None else None) for m in masks])
     _check(L.rsc_mlpnp_iterate_many(hs, n, its, res, mp), "mlpnp_iterate_many")
-    return [_pnp_out(res[i], masks[i][:solvers[i].n_points]) for i in range(n)]
+    return [_pnp_out(res[i], None if masks[i] is None else masks[i][:solvers[i].n_points]) for i in range(n)]
 
 
-def _sim3_out(r: Sim3Result, mask: np.ndarray) -> dict:
+def _sim3_out(r: Sim3Result, mask) -> dict:
+    """Result dict of one Sim3 iterate(); ``inliers`` None when no vbInliers were requested."""
     return dict(ok=bool(r.ok), no_more=bool(r.no_more), n_inliers=int(r.n_inliers), iterations=int(r.iterations),
-                R=np.array(r.R, np.float32).reshape(3, 3), t=np.array(r.t, np.float32), inliers=mask.astype(bool))
+                R=np.array(r.R, np.float32).reshape(3, 3), t=np.array(r.t, np.float32),
+                inliers=None if mask is None else mask.astype(bool))
 
 
 class Sim3Solver:
@@ -687,10 +692,10 @@ def sim3_iterate_many(solvers, n_iterations, with_masks: bool = True):
     hs = (C.c_void_p * n)(*[s.h.value for s in solvers])
     its = np.ascontiguousarray(np.broadcast_to(np.asarray(n_iterations, np.int32), (n,)))
     res = (Sim3Result * n)()
-    masks = [np.zeros(max(s.n1, 1), np.uint8) for s in solvers]
-    mp = (C.c_void_p * n)(*[(m.ctypes.data if with_masks else None) for m in masks])
+    masks = [np.zeros(max(s.n1, 1), np.uint8) if with_masks else None for s in solvers]
+    mp = (C.c_void_p * n)(*[(m.ctypes.data if m is not None else None) for m in masks])
     _check(L.rsc_sim3_iterate_many(hs, n, its, res, mp), "iterate_many")
-    return [_sim3_out(res[i], masks[i][:solvers[i].n1]) for i in range(n)]
+    return [_sim3_out(res[i], None if masks[i] is None else masks[i][:solvers[i].n1]) for i in range(n)]
 
 
 class MLPnPSolver:
@@ -806,6 +811,7 @@ class SolverBatch:
             _check(L.rsc_sim3_set_ransac_parameters_many(self._h, len(self.solvers), *params), "params_many")
 
     def iterate(self, n_iterations, with_masks=False):
+        """iterate() of every solver; ``inliers`` of each result is None unless with_masks."""
         if self.kind == "pnp":
             return pnp_iterate_many(self.solvers, n_iterations, with_masks)
         if self.kind == "mlpnp":

@@ -228,5 +228,77 @@ def test_mask_exchange_packing_round_trip():
         rec2[:, 1] = 1
         rec2[:, 4] = [12, 4, 9]  # first successes at hypotheses 11, 3, 8 -> rounds 2, 0, 1
         assert rdist.local_loop_candidate(rec2) == 5
+        # the fallback order after a rejected winner (LoopClosing.cpp:311-324, Tracking.cpp:1284-1331)
+        assert rdist.successful_candidates(rec2, "loop") == [5, 6, 4]
+        assert rdist.local_loop_candidate(rec2, exclude={5}) == 6
+        assert rdist.successful_candidates(rec2, "reloc") == [4, 5, 6]
     finally:
         dist.destroy_process_group()
+
+
+N1 = 600  # matches of the current KeyFrame: the common length of every loop candidate's vbInliers
+
+
+def _loop_pairs():
+    from rsc import synth
+    rng = np.random.default_rng(78)
+    return [synth.make_sim3_pair(rng, N1, int(rng.integers(60, 250))) for _ in range(6)]
+
+
+def _solve_sim3(idx, pairs):
+    import oracle_lib as ol
+    out = []
+    for c in idx:
+        o = ol.OracleSim3(pairs[c], 1 + c)
+        o.set_ransac_parameters(0.99, 20, 300)
+        out.append(o.iterate(300))
+    return out
+
+
+def _loop_mask_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "orb-slam2-optimized_amd"))
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import torch.distributed as dist
+    from rsc import dist as rd
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pairs = _loop_pairs()
+    lo, hi = rd.shard_range(len(pairs), world, rank)
+    res = _solve_sim3(range(lo, hi), pairs)
+    rec = rd.pack_sim3(list(range(lo, hi)), res)
+    c = rd.local_loop_candidate(rec)
+    allr, masks = rd.all_gather_records_and_mask(dist, rec, len(pairs), c, res[c - lo]["inliers"] if c >= 0 else None,
+                                                 N1)
+    q.put((rank, c, allr, masks))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_loop_winner_mask_in_the_exchange():
+    """Loop closure (LoopClosing.cpp:271-309): every rank gets the records and the Sim3 winner's
+    vbInliers (mN1 entries) in one all-gather; the global winner by (round, candidate) is one rank's
+    local winner, and its mask equals the single-process run's."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_loop_mask_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=120) for _ in range(2)], key=lambda g: g[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    pairs = _loop_pairs()
+    res = _solve_sim3(range(len(pairs)), pairs)
+    single = rdist.pack_sim3(list(range(len(pairs))), res)
+    win = rdist.local_loop_candidate(single)
+    # every pair succeeds; candidate 1 wins at round 2 ahead of candidate 0 (round 5)
+    assert win == 1 and all(r["ok"] for r in res)
+    for rank, c, allr, masks in got:
+        assert np.array_equal(allr, single)
+        assert rdist.local_loop_candidate(allr) == win
+        assert win in masks and np.array_equal(masks[win], res[win]["inliers"])
+        assert masks[win].sum() == res[win]["n_inliers"]
+    assert all(g[1] >= 0 for g in got)  # both ranks hold a successful pair

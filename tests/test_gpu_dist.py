@@ -43,14 +43,14 @@ def _ml_scenes():
     return [synth.make_pnp_scene(rng, int(rng.integers(100, 900)), float(rng.uniform(0.3, 0.8))) for _ in range(6)]
 
 
-def _run_sim3(ctx, pairs, idx):
+def _run_sim3(ctx, pairs, idx, with_masks=False):
     from rsc import engine
     solvers = [engine.Sim3Solver(ctx, pairs[c], 1 + c) for c in idx]
     if not solvers:
         return []
     b = engine.SolverBatch(solvers)
     b.set_ransac_parameters(0.99, 20, 300)
-    return b.iterate(300)
+    return b.iterate(300, with_masks=with_masks)
 
 
 def _run_mlpnp(ctx, scenes, idx):
@@ -81,7 +81,7 @@ def _mask_scenes():
 def _mask_pairs():
     from rsc import synth
     rng = np.random.default_rng(78)
-    return [synth.make_sim3_pair(rng, N1, int(rng.integers(15, 120))) for _ in range(6)]
+    return [synth.make_sim3_pair(rng, N1, int(rng.integers(60, 250))) for _ in range(6)]
 
 
 def _run_pnp(ctx, scenes, idx):
@@ -150,7 +150,7 @@ def _worker(rank, world, port, q):
                                             sol[c5 - lo5].last_inliers() if c5 >= 0 else None, F_N)
     pp = _mask_pairs()
     lo6, hi6 = rd.shard_range(len(pp), world, rank)
-    res6 = _run_sim3(ctx, pp, range(lo6, hi6))
+    res6 = _run_sim3(ctx, pp, range(lo6, hi6), with_masks=True)
     rec6 = rd.pack_sim3(list(range(lo6, hi6)), res6)
     c6 = rd.local_loop_candidate(rec6)
     r6, k6 = rd.all_gather_records_and_mask(dist, rec6, len(pp), c6,
@@ -239,6 +239,7 @@ def test_world2_librsc_shards_match_single_process_and_oracle():
         assert np.array_equal(k5[w5], ora5[w5]["inliers"]) and np.array_equal(k5[w5], single5[w5]["inliers"])
         assert np.array_equal(r6.view(np.uint32), rec6_ora.view(np.uint32))
         assert rdist.local_loop_candidate(r6) == w6
+        assert w6 in k6 and k6[w6].sum() == ora6[w6]["n_inliers"] > 0
         assert np.array_equal(k6[w6], ora6[w6]["inliers"])
 
 
