@@ -387,6 +387,14 @@ int ora_mlpnp_trace_get(void* h, int cap, int32_t* ints, double* dbls) {
     }
     return n;
 }
+// planar-branch flag of every traced hypothesis (MLPnPsolver.cpp:354-364)
+int ora_mlpnp_trace_planar(void* h, int cap, int32_t* out) {
+    auto* s = static_cast<MLPnPOracle*>(h);
+    if (!s->trace) return 0;
+    const int n = std::min(cap, (int)s->trace->size());
+    for (int i = 0; i < n; ++i) out[i] = (*s->trace)[i].planar;
+    return n;
+}
 void ora_mlpnp_run_batch(int C, const int32_t* n, const int64_t* off, const float* p2d, const float* p3dw,
                          const float* sigma2, float fx, float fy, float cx, float cy, const uint32_t* seeds,
                          double prob, int min_inliers, int max_its, int min_set, float eps, float th2, int n_its,

@@ -518,6 +518,7 @@ void MLPnPOracle::computePose(const int* idx, int n, double Rout[3][3], double t
             PPt[a][b] = s;
         }
     const bool planar = fullpiv_rank3(PPt) == 2;
+    mLastPlanar = planar;
     double eigenRot[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
     if (planar) {
         const SymEig<double, 3> es = sym_eig<double, 3>(PPt);
@@ -733,6 +734,7 @@ bool MLPnPOracle::iterate(int nIterations, bool& bNoMore, std::vector<uint8_t>& 
         CheckInliers();
         if (trace) {
             tr.n_inliers = mnInliersi;
+            tr.planar = mLastPlanar ? 1 : 0;
             for (int r = 0; r < 3; ++r) { tr.t[r] = mti[r]; for (int c = 0; c < 3; ++c) tr.R[3 * r + c] = mRi[r][c]; }
             trace->push_back(tr);
         }

@@ -50,6 +50,7 @@ public:
         int sample[8];
         int n_inliers;
         double R[9], t[3];
+        int planar;  // computePose took the planar branch (MLPnPsolver.cpp:354-364: rank(PP^T) == 2)
     };
     std::vector<Trace>* trace = nullptr;
 
@@ -67,6 +68,7 @@ private:
     std::vector<double> mvCov;     // [N][9] or empty
 
     double mRi[3][3], mti[3];
+    bool mLastPlanar = false;  // branch taken by the last computePose (trace only)
     std::vector<uint8_t> mvbInliersi;
     int mnInliersi = 0;
     int mnIterations = 0;

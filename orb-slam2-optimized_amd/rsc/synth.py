@@ -149,7 +149,12 @@ def make_planar_pnp_scene(rng: np.random.Generator, n: int, inlier_ratio: float,
     plane = "tilted": a random plane through the view, coplanar up to float rounding (ill-conditioned
             but mostly finite samples);
     plane = "duplicates": a frustum scene in which 25 % of the correspondences repeat another one
-            exactly (3D and 2D), so samples with repeated points are rank-deficient.
+            exactly (3D and 2D), so samples with repeated points are rank-deficient;
+    plane = "floor0" / "wall0": the floor / wall moved into a plane THROUGH THE WORLD ORIGIN (world
+            Y = 0 / Z = 0 exactly; the camera pose carries the offset, so the images are the same
+            geometry).  MLPnP's planarity test is rank(points3 * points3^T) == 2 on uncentred world
+            points (MLPnPsolver.cpp:346-364), which only such a plane passes: its samples take the
+            planar branch (9-column A, :404-435; 4-way sign test, :497-558).
     The camera looks at the plane from 1.5-9 m; points outside the image are redrawn."""
     if plane == "duplicates":
         sc = make_pnp_scene(rng, n, inlier_ratio, noise=noise, n_points=n_points)
@@ -160,6 +165,9 @@ def make_planar_pnp_scene(rng: np.random.Generator, n: int, inlier_ratio: float,
             a[dst] = a[src]
         sc.inlier_true[dst] = sc.inlier_true[src]
         return sc
+    origin_off = {"floor0": np.array([0.0, 1.5, 0.0]), "wall0": np.array([0.0, 0.0, 6.0])}.get(plane)
+    if origin_off is not None:
+        plane = plane[:-1]
     R = random_rotation(rng, 0.25)
     t = rng.uniform(-0.5, 0.5, size=3)
     if plane == "tilted":
@@ -190,6 +198,9 @@ def make_planar_pnp_scene(rng: np.random.Generator, n: int, inlier_ratio: float,
         ok = (z > 1.5) & (z < 9.0) & (u >= 0) & (u < WIDTH) & (v >= 0) & (v < HEIGHT)
         pts.append(W[ok])
     Xw = np.concatenate(pts)[:n]
+    if origin_off is not None:  # same camera-frame points: Xc = R (Xw - off) + (t + R off)
+        Xw = Xw - origin_off    # exact: the plane coordinate becomes +0.0
+        t = t + R @ origin_off
     return _observe(rng, R, t, Xw, inlier_ratio, noise, n_points)
 
 

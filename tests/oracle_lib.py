@@ -109,6 +109,7 @@ def lib():
     L.ora_mlpnp_compute_pose.argtypes = [vp, i32p, C.c_int, f64p, f64p]
     L.ora_mlpnp_trace_enable.argtypes = [vp]
     L.ora_mlpnp_trace_get.argtypes = [vp, C.c_int, i32p, f64p]
+    L.ora_mlpnp_trace_planar.argtypes = [vp, C.c_int, i32p]
     L.ora_mlpnp_run_batch.argtypes = [C.c_int, i32p, i64p, f32p, f32p, f32p, C.c_float, C.c_float, C.c_float,
                                       C.c_float, u32p, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
                                       C.c_int, C.c_int, i32p, f32p]
@@ -388,6 +389,12 @@ class OracleMLPnP:
         dbl = np.zeros((cap, 12))
         n = lib().ora_mlpnp_trace_get(self.h, cap, ints, dbl)
         return ints[:n], dbl[:n]
+
+    def trace_planar(self, cap=100000):
+        """bool per traced hypothesis: computePose took the planar branch (rank(PP^T) == 2)."""
+        out = np.zeros(cap, np.int32)
+        n = lib().ora_mlpnp_trace_planar(self.h, cap, out)
+        return out[:n].astype(bool)
 
 
 def pose_optimization(frame):

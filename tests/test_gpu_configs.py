@@ -173,6 +173,33 @@ def test_config4_mlpnp_4096_covariances_every_hypothesis():
         assert np.array_equal(pos.view(np.uint64), dbl.view(np.uint64)), f"cand {i} poses"
 
 
+def test_config4_mlpnp_4096_parity_mode_refine():
+    """Config 4's shape (32 candidates x 4096, the per-GPU share) in parity mode: 60 % inliers, so
+    hypotheses reach minInliers (floor(0.5 N) = 2048) and MLPnP's Refine runs at N = 4096
+    (MLPnPsolver.cpp:257-318: its computePose result is discarded and the current hypothesis
+    re-counted, Q15) and iterate returns at the first success.  Outcome, iterations, pose and
+    vbInliers bit-exact against the oracle; most candidates succeed."""
+    from rsc import engine
+    scenes = wl.config4_scenes(ratio=0.6, seed=79)
+    seeds = wl.step_seeds(0, len(scenes))
+    gs = [engine.MLPnPSolver(ctx(), sc, int(s)) for sc, s in zip(scenes, seeds)]
+    b = engine.SolverBatch(gs)
+    b.set_ransac_parameters(*wl.MLPNP)
+    outs = b.iterate(300, with_masks=True)
+    n_ok = 0
+    for i, (sc, s) in enumerate(zip(scenes, seeds)):
+        o = ol.OracleMLPnP(sc, int(s))
+        o.set_ransac_parameters(*wl.MLPNP)
+        ro = o.iterate(300)
+        g = outs[i]
+        assert (g["ok"], g["no_more"], g["n_inliers"], g["iterations"]) == \
+            (ro["ok"], ro["no_more"], ro["n_inliers"], ro["iterations"]), f"cand {i}"
+        assert np.array_equal(bits(g["T"]), bits(ro["T"])), f"cand {i} T"
+        assert np.array_equal(g["inliers"], ro["inliers"]), f"cand {i} inliers"
+        n_ok += ro["ok"]
+    assert n_ok >= 20
+
+
 def test_config5_full_event_stream():
     """The bench's 150 + 20 event stream (rsc.events.make_event_stream() defaults) through
     rsc_reloc_events / rsc_loop_events against the sequential round-robin replay."""

@@ -11,8 +11,11 @@ repeated points):
   with 25 % repeated correspondences;
 * Sim3 with 40 % collinear matches (Horn on collinear triples, Sim3Solver.cpp:139-151, :196-266) and
   with repeated matches;
-* MLPnP on planar scenes: the planar branch of computePose (FullPivHouseholderQR rank 2, the 9-column
-  system, 4-way sign test, MLPnPsolver.cpp:346-364, :543-601) on the device.
+* MLPnP on planes through the world origin ("floor0" / "wall0"): the planar branch of computePose
+  (FullPivHouseholderQR rank 2 on the uncentred points, the 9-column system, 4-way sign test,
+  MLPnPsolver.cpp:346-364, :404-435, :497-558) on the device, the branch confirmed per hypothesis by
+  the oracle's trace; and on offset planes, which MLPnP's uncentred rank test keeps on the general
+  branch.
 
 Bit-exact as everywhere (samples, counts, masks, poses), with NaN poses compared as NaN (the sign /
 payload of a NaN is not an IEEE-specified result: x86 produces the negative default NaN, gfx950 the
@@ -119,7 +122,10 @@ def test_sim3_degenerate_every_hypothesis(kind):
 
 
 @pytest.mark.parametrize("plane", ["floor", "wall", "tilted"])
-def test_mlpnp_planar_branch_on_device(plane):
+def test_mlpnp_offset_planes_on_device(plane):
+    """Coplanar scenes whose plane misses the world origin: MLPnP's rank test on the UNCENTRED
+    points3 * points3^T (MLPnPsolver.cpp:346-364) gives rank 3, so these stay on the general branch
+    with ill-conditioned samples (the planar branch itself: test_mlpnp_planar_branch_on_device)."""
     from rsc import engine
     rng = np.random.default_rng(900)
     sc = synth.make_planar_pnp_scene(rng, 800, 0.6, plane)
@@ -142,3 +148,73 @@ def test_mlpnp_planar_branch_on_device(plane):
     da, db = pos[:h].astype(np.float64), dbl.astype(np.float64)
     na, nb = np.isnan(da), np.isnan(db)
     assert np.array_equal(na, nb) and np.array_equal(da.view(np.uint64)[~na], db.view(np.uint64)[~nb])
+
+
+def _ml_planar_compare(g, o, n_its, where):
+    rg, ro = g.iterate(n_its), o.iterate(n_its)
+    assert (rg["ok"], rg["n_inliers"], rg["iterations"]) == (ro["ok"], ro["n_inliers"], ro["iterations"]), where
+    assert nan_equal(rg["T"], ro["T"]), where
+    if ro["ok"]:
+        assert np.array_equal(rg["inliers"], ro["inliers"]), where
+    ints, dbl = o.trace()
+    planar = o.trace_planar()
+    smp, pos = g.last_hypotheses()
+    h = len(ints)
+    assert len(smp) >= h and len(planar) == h
+    assert np.array_equal(smp[:h, :6], ints[:, :6]), where
+    da, db = pos[:h].astype(np.float64), dbl.astype(np.float64)
+    na, nb = np.isnan(da), np.isnan(db)
+    assert np.array_equal(na, nb) and np.array_equal(da.view(np.uint64)[~na], db.view(np.uint64)[~nb]), where
+    return ro, planar
+
+
+@pytest.mark.parametrize("plane,ratio,seeds,min_ok", [("floor0", 0.75, (9, 10, 11), 2), ("wall0", 0.6, (9, 10), 0)])
+def test_mlpnp_planar_branch_on_device(plane, ratio, seeds, min_ok):
+    """MLPnP's planar branch on the device: map points on a plane THROUGH THE WORLD ORIGIN (world
+    Y = 0 / Z = 0 exactly, rsc.synth "floor0" / "wall0"), so rank(points3 * points3^T) == 2 for every
+    sample (MLPnPsolver.cpp:346-364) and computePose rotates the points into the plane, solves the
+    9-column system (:404-435) and runs the 4-way sign test (:497-558).  The oracle's trace confirms
+    the branch was taken for EVERY hypothesis; the device's samples and double poses are bit-exact
+    against it (a general-branch solve would give other bits), and on the floor scene the planar
+    hypotheses reach Refine and succeed."""
+    from rsc import engine
+    rng = np.random.default_rng(900)
+    sc = synth.make_planar_pnp_scene(rng, 800, ratio, plane)
+    assert not np.any(sc.p3dw[:, 1 if plane == "floor0" else 2])
+    params = (0.99, 10, 300, 6, 0.5, 5.991)
+    n_ok = 0
+    for seed in seeds:
+        g = engine.MLPnPSolver(ctx(), sc, seed)
+        g.set_ransac_parameters(*params)
+        o = ol.OracleMLPnP(sc, seed)
+        o.set_ransac_parameters(*params)
+        o.enable_trace()
+        ro, planar = _ml_planar_compare(g, o, 60, f"{plane} seed {seed}")
+        assert planar.all() and len(planar) > 0
+        n_ok += ro["ok"]
+    assert n_ok >= min_ok
+
+
+def test_mlpnp_planar_and_general_candidates_in_one_launch():
+    """Planar-branch candidates (origin floor) and general ones in the same mlpnp_iterate_many
+    launches, iterate(5) rounds as the reference's round-robin would call them."""
+    from rsc import engine
+    rng = np.random.default_rng(901)
+    scs = [synth.make_planar_pnp_scene(rng, 600, 0.75, "floor0"), synth.make_pnp_scene(rng, 700, 0.6),
+           synth.make_planar_pnp_scene(rng, 500, 0.7, "wall0"), synth.make_pnp_scene(rng, 400, 0.5)]
+    params = (0.99, 10, 300, 6, 0.5, 5.991)
+    pairs = []
+    for i, sc in enumerate(scs):
+        g = engine.MLPnPSolver(ctx(), sc, 30 + i)
+        g.set_ransac_parameters(*params)
+        o = ol.OracleMLPnP(sc, 30 + i)
+        o.set_ransac_parameters(*params)
+        pairs.append((g, o))
+    for rnd in range(8):
+        outs = engine.mlpnp_iterate_many([p[0] for p in pairs], 5)
+        for i, (g, o) in enumerate(pairs):
+            ro = o.iterate(5)
+            got = outs[i]
+            assert (got["ok"], got["no_more"], got["n_inliers"]) == (ro["ok"], ro["no_more"], ro["n_inliers"]), \
+                f"round {rnd} cand {i}"
+            assert nan_equal(got["T"], ro["T"]) and np.array_equal(got["inliers"], ro["inliers"]), f"round {rnd} cand {i}"
