@@ -376,7 +376,7 @@ void mlpnp_gn(double x[6], int n, const double (*pts)[3], const double (*Ns)[3][
         for (int i = 0; i < n; ++i) {
             double pc[3];
             for (int k = 0; k < 3; ++k)
-                pc[k] = (R[k][0] * pts[i][0] + R[k][1] * pts[i][1] + R[k][2] * pts[i][2]) + x[3 + k];
+                pc[k] = emv3d_row(k, R[k][0] * pts[i][0], R[k][1] * pts[i][1], R[k][2] * pts[i][2]) + x[3 + k];  // :738
             const double nrm = norm3(pc);
             for (int k = 0; k < 3; ++k) pc[k] = pc[k] / nrm;
             const double nr[3] = {Ns[i][0][0], Ns[i][1][0], Ns[i][2][0]};
@@ -527,7 +527,7 @@ void MLPnPOracle::computePose(const int* idx, int n, double Rout[3][3], double t
         for (int i = 0; i < n; ++i) {
             double q[3];
             for (int r = 0; r < 3; ++r)
-                q[r] = eigenRot[r][0] * P[3 * i] + eigenRot[r][1] * P[3 * i + 1] + eigenRot[r][2] * P[3 * i + 2];
+                q[r] = emv3d_row(r, eigenRot[r][0] * P[3 * i], eigenRot[r][1] * P[3 * i + 1], eigenRot[r][2] * P[3 * i + 2]);  // :363
             for (int r = 0; r < 3; ++r) P[3 * i + r] = q[r];
         }
     }
@@ -633,7 +633,8 @@ void MLPnPOracle::computePose(const int* idx, int n, double Rout[3][3], double t
             for (int p = 0; p < 6; ++p) {
                 double v[3];
                 for (int r = 0; r < 3; ++r)
-                    v[r] = (Rc[k][r][0] * P0[3 * p] + Rc[k][r][1] * P0[3 * p + 1] + Rc[k][r][2] * P0[3 * p + 2]) + Tc[k][r];
+                    v[r] = emv3d_row(r, Rc[k][r][0] * P0[3 * p], Rc[k][r][1] * P0[3 * p + 1], Rc[k][r][2] * P0[3 * p + 2]) +
+                           Tc[k][r];  // :548
                 const double nv = norm3(v);
                 for (int r = 0; r < 3; ++r) v[r] = v[r] / nv;
                 norms += (1.0 - dot3(v, &mvBearing[3 * idx[p]]));
@@ -656,7 +657,7 @@ void MLPnPOracle::computePose(const int* idx, int n, double Rout[3][3], double t
         if (det3m(R) < 0) for (auto& row : R) for (double& v : row) v *= -1.0;
         const double ts[3] = {scale * r1[9], scale * r1[10], scale * r1[11]};
         double tv[3];
-        for (int r = 0; r < 3; ++r) tv[r] = R[r][0] * ts[0] + R[r][1] * ts[1] + R[r][2] * ts[2];
+        for (int r = 0; r < 3; ++r) tv[r] = emv3d_row(r, R[r][0] * ts[0], R[r][1] * ts[1], R[r][2] * ts[2]);  // :576
         // 2-way sign test on the first 6 correspondences with the inverted transforms (:570-601)
         double err[2], Ti[2][4][4];
         for (int s = 0; s < 2; ++s) {
@@ -669,7 +670,8 @@ void MLPnPOracle::computePose(const int* idx, int n, double Rout[3][3], double t
             for (int p = 0; p < 6; ++p) {
                 double v[3];
                 for (int r = 0; r < 3; ++r)
-                    v[r] = (Ti[s][r][0] * P0[3 * p] + Ti[s][r][1] * P0[3 * p + 1] + Ti[s][r][2] * P0[3 * p + 2]) + Ti[s][r][3];
+                    v[r] = emv3d_row(r, Ti[s][r][0] * P0[3 * p], Ti[s][r][1] * P0[3 * p + 1], Ti[s][r][2] * P0[3 * p + 2]) +
+                           Ti[s][r][3];  // :591
                 const double nv = norm3(v);
                 for (int r = 0; r < 3; ++r) v[r] = v[r] / nv;
                 err[s] += (1.0 - dot3(v, &mvBearing[3 * idx[p]]));

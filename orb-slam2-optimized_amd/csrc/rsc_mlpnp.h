@@ -576,7 +576,8 @@ RSC_HD bool ml_planarity(const double (&pw)[NS][3], double (&eigenRot)[3][3]) {
 // Point i of the design matrix: pw (general) or eigenRot * pw (planar).
 RSC_HD void ml_design_point(bool planar, const double (&eigenRot)[3][3], const double* pw, double (&P)[3]) {
     double q[3];
-    RSC_UNROLL for (int r = 0; r < 3; ++r) q[r] = eigenRot[r][0] * pw[0] + eigenRot[r][1] * pw[1] + eigenRot[r][2] * pw[2];
+    RSC_UNROLL for (int r = 0; r < 3; ++r)  // Matrix3d * Vector3d (MLPnPsolver.cpp:363): Eigen's row order
+        q[r] = emv3d_row(r, eigenRot[r][0] * pw[0], eigenRot[r][1] * pw[1], eigenRot[r][2] * pw[2]);
     RSC_UNROLL for (int r = 0; r < 3; ++r) P[r] = planar ? q[r] : pw[r];
 }
 
@@ -706,7 +707,7 @@ RSC_HD void mlpnp_finish_pose(const View& in, const JView& jin, const double (&r
             RSC_UNROLL for (int p = 0; p < 6; ++p) {
                 double v[3];
                 RSC_UNROLL for (int r = 0; r < 3; ++r)
-                    v[r] = (Rc[r][0] * in.pw(p, 0) + Rc[r][1] * in.pw(p, 1) + Rc[r][2] * in.pw(p, 2)) + Tc[r];
+                    v[r] = emv3d_row(r, Rc[r][0] * in.pw(p, 0), Rc[r][1] * in.pw(p, 1), Rc[r][2] * in.pw(p, 2)) + Tc[r];
                 const double nv = ml_norm3(v);
                 RSC_UNROLL for (int r = 0; r < 3; ++r) v[r] = v[r] / nv;
                 { const double fp[3] = {in.f(p, 0), in.f(p, 1), in.f(p, 2)}; norms += (1.0 - ml_dot3(v, fp)); }
@@ -727,7 +728,7 @@ RSC_HD void mlpnp_finish_pose(const View& in, const JView& jin, const double (&r
         if (ml_det3(R) < 0) RSC_UNROLL for (int r = 0; r < 3; ++r) RSC_UNROLL for (int c = 0; c < 3; ++c) R[r][c] *= -1.0;
         const double ts[3] = {scale * r1[9], scale * r1[10], scale * r1[11]};
         double tv[3];
-        RSC_UNROLL for (int r = 0; r < 3; ++r) tv[r] = R[r][0] * ts[0] + R[r][1] * ts[1] + R[r][2] * ts[2];
+        RSC_UNROLL for (int r = 0; r < 3; ++r) tv[r] = emv3d_row(r, R[r][0] * ts[0], R[r][1] * ts[1], R[r][2] * ts[2]);
         double err[2], Ti[2][4][4];
         RSC_UNROLL for (int s = 0; s < 2; ++s) {
             const double T4[4][4] = {{R[0][0], R[0][1], R[0][2], s ? -tv[0] : tv[0]},
@@ -739,7 +740,8 @@ RSC_HD void mlpnp_finish_pose(const View& in, const JView& jin, const double (&r
             RSC_UNROLL for (int p = 0; p < 6; ++p) {
                 double v[3];
                 RSC_UNROLL for (int r = 0; r < 3; ++r)
-                    v[r] = (Ti[s][r][0] * in.pw(p, 0) + Ti[s][r][1] * in.pw(p, 1) + Ti[s][r][2] * in.pw(p, 2)) + Ti[s][r][3];
+                    v[r] = emv3d_row(r, Ti[s][r][0] * in.pw(p, 0), Ti[s][r][1] * in.pw(p, 1), Ti[s][r][2] * in.pw(p, 2)) +
+                           Ti[s][r][3];
                 const double nv = ml_norm3(v);
                 RSC_UNROLL for (int r = 0; r < 3; ++r) v[r] = v[r] / nv;
                 { const double fp[3] = {in.f(p, 0), in.f(p, 1), in.f(p, 2)}; err[s] += (1.0 - ml_dot3(v, fp)); }
@@ -779,7 +781,7 @@ RSC_HD void mlpnp_finish_pose(const View& in, const JView& jin, const double (&r
         RSC_UNROLL for (int i = 0; i < NS; ++i) {
             double pc[3];
             RSC_UNROLL for (int k = 0; k < 3; ++k)
-                pc[k] = (Rg[k][0] * jin.pw(i, 0) + Rg[k][1] * jin.pw(i, 1) + Rg[k][2] * jin.pw(i, 2)) + x[3 + k];
+                pc[k] = emv3d_row(k, Rg[k][0] * jin.pw(i, 0), Rg[k][1] * jin.pw(i, 1), Rg[k][2] * jin.pw(i, 2)) + x[3 + k];
             const double nrm = ml_norm3(pc);
             RSC_UNROLL for (int k = 0; k < 3; ++k) pc[k] = pc[k] / nrm;
             const double nr[3] = {jin.ns(i, 0, 0), jin.ns(i, 1, 0), jin.ns(i, 2, 0)};

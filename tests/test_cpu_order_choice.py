@@ -5,7 +5,7 @@ Rounds 1-3 summed every 3-term product left to right.  Eigen 3.3 on the referenc
 evaluates a reduction that cannot use packets (a coefficient of Matrix3f * Vector3f, a dot over a row
 of a column-major matrix, a float 3-vector) with redux_novec_unroller's halving tree a0 + (a1 + a2),
 and a Matrix3d * Vector3d into a Vector3d as one Packet2d chain for rows 0-1 plus the coefficient path
-for row 2 (oracle/ora_linalg.h, sites in profiles/r04/order_choice.json).  The oracle is built both
+for row 2 (oracle/ora_linalg.h, sites in profiles/r05/order_choice.json, MLPnP's included).  The oracle is built both
 ways (librsc_oracle_ltr.so / librsc_oracle.so) and run on the config 2 / 3 / 5 workloads
 (tools/oracle_ab.py).  The outcome agreement is far below 100 % — the minimal 4-point EPnP solve is
 chaotic under last-bit changes (its 4-dimensional null-space basis is fixed by rounding) —
@@ -21,7 +21,7 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-REPORT = os.path.join(ROOT, "profiles", "r04", "order_choice.json")
+REPORT = os.path.join(ROOT, "profiles", "r05", "order_choice.json")
 
 
 @pytest.fixture(scope="module")
@@ -51,3 +51,5 @@ def test_order_changes_outcomes_so_the_eigen_order_is_used(quick):
     # the Sim3 path is well conditioned: poses move by float rounding only, no count changes
     assert rep["c3x"]["count_agreement"] == 1.0 and rep["c3x"]["max_abs_pose_diff"] < 1e-3
     assert quick["c2x"]["pose_bits_changed"] > 0
+    # MLPnP (round 5: the Matrix3d * Vector3d sites of MLPnPsolver.cpp in Eigen's row order too)
+    assert rep["c4x"]["hypotheses"] == 32 * 300 and rep["c4x"]["pose_bits_changed"] > 0

@@ -9,6 +9,7 @@ Workloads (rsc/workloads.py, rsc/events.py):
   c2p  config 2 parity mode (60 % inliers, Refine + early exit): the iterate(300) outcome per candidate;
   c3x  config 3 exhaustive Sim3 (32 x 1000, iterate(300)): every hypothesis' count and pose;
   c3p  config 3 parity (300 true inliers): the outcome per pair;
+  c4x  config 4 MLPnP exhaustive (32 x 4096, iterate(300)): every hypothesis' count and double pose;
   c5   config 5 event stream (150 relocalization + 20 loop-closure events): winner records.
 
 Used for: the Q19 qr_solve change (round-3 oracle vs round-4 oracle) and the arithmetic-order choice
@@ -89,6 +90,19 @@ def dump(out, lib=None, quick=False):
         res[tag + "_poses"] = np.stack(fls)
         res[tag + "_rec"] = np.array(rec, np.int32)
         res[tag + "_masks"] = np.stack(masks)
+    # c4x: config 4 MLPnP exhaustive (per GPU share 32 x 4096): every hypothesis' count and double pose
+    ints, dbls = [], []
+    scenes4 = W.config4_scenes(candidates=4 if quick else W.CONFIG4["candidates_per_gpu"])
+    for sc, s in zip(scenes4, W.step_seeds(0, len(scenes4))):
+        o = ol.OracleMLPnP(sc, int(s))
+        o.set_ransac_parameters(*W.MLPNP)
+        o.enable_trace()
+        o.iterate(300)
+        i, d = o.trace()
+        ints.append(i)
+        dbls.append(d)
+    res["c4x_ints"] = np.stack(ints)
+    res["c4x_poses"] = np.stack(dbls)
     # c5
     evs = rev.make_event_stream(n_reloc=30 if quick else 150, n_loop=6 if quick else 20)
     recs = []
@@ -138,6 +152,18 @@ def compare(a_path, b_path):
             d["max_abs_pose_diff"] = float(dT.max())
             d["median_abs_pose_diff_of_mismatches"] = float(np.median(dT[bad])) if bad.any() else 0.0
         rep[tag] = d
+    if "c4x_ints" in A and "c4x_ints" in B:
+        ia, ib = A["c4x_ints"], B["c4x_ints"]
+        pa, pb = A["c4x_poses"], B["c4x_poses"]
+        same_bits = np.all(pa.view(np.uint64) == pb.view(np.uint64), axis=-1)
+        same_count = ia[..., 8] == ib[..., 8]
+        finite = np.isfinite(pa).all(-1) & np.isfinite(pb).all(-1)
+        dpose = np.abs(pa - pb).max(-1)
+        rep["c4x"] = dict(hypotheses=int(same_bits.size), pose_bits_changed=int((~same_bits).sum()),
+                          count_changed=int((~same_count).sum()), count_agreement=float(np.mean(same_count)),
+                          max_abs_count_diff=int(np.abs(ia[..., 8].astype(np.int64) - ib[..., 8]).max()),
+                          max_abs_pose_diff=float(dpose[finite].max()) if finite.any() else 0.0,
+                          pose_within_1em4=float(np.mean(dpose[finite] <= 1e-4)) if finite.any() else 1.0)
     ea, eb = A["c5_records"], B["c5_records"]
     same = np.all(ea[:, :5] == eb[:, :5], axis=1)
     rep["c5"] = dict(events=int(len(ea)), winner_record_agreement=float(same.mean()),

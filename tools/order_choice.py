@@ -1,13 +1,13 @@
-"""profiles/r04/order_choice.json — how much the association order of the 3-term fixed-size Eigen
+"""profiles/r05/order_choice.json (r04 + the MLPnP sites, config 4) — how much the association order of the 3-term fixed-size Eigen
 reductions matters (VERDICT r3 "Next round" 8).
 
 Two builds of the same oracle sources: librsc_oracle_ltr.so (-DORA_LTR_ORDER: every sum left to
 right, the rounds 1-3 restatement) and librsc_oracle.so (Eigen 3.3's order on the reference's x86-64
 SSE2 build: `ered3` / `emv3d_row`, oracle/ora_linalg.h), run on the config 2 / 3 / 5 workloads by
-tools/oracle_ab.py.  "full" = the bench shapes, "quick" = the reduced shapes that
+tools/oracle_ab.py (config 4 MLPnP since round 5).  "full" = the bench shapes, "quick" = the reduced shapes that
 tests/test_cpu_order_choice.py recomputes and compares with this file.
 
-    python tools/order_choice.py profiles/r04/order_choice.json
+    python tools/order_choice.py profiles/r05/order_choice.json
 """
 import json
 import os
@@ -30,6 +30,11 @@ SITES = {
     "Sim3Solver.cpp:253": "t12 = O1 - R12*O2 (ered3)",
     "Sim3Solver.cpp:264": "T21 = T12.inverse(): -(R21*t12) (ered3)",
     "Sim3Solver.cpp:320": "Project Rcw*P3Dw + tcw (ered3)",
+    "MLPnPsolver.cpp:363": "planar branch eigenRot*points3.col(i) (Matrix3d*Vector3d: emv3d_row)",
+    "MLPnPsolver.cpp:548": "planar sign test Ts[i].block<3,3>*points3v[p] + t (emv3d_row)",
+    "MLPnPsolver.cpp:576": "tout = Rout*(scale*t) (emv3d_row)",
+    "MLPnPsolver.cpp:591": "direction test Ts[s].block<3,3>*points3v[p] + t (emv3d_row)",
+    "MLPnPsolver.cpp:738": "mlpnp_residuals_and_jacs R*pts[i] + T (emv3d_row)",
 }
 
 
