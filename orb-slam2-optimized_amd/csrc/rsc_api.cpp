@@ -2510,7 +2510,6 @@ int rsc_mlpnp_iterate(rsc_mlpnp* s, int n_its, rsc_pnp_result* out, uint8_t* inl
 int rsc_mlpnp_reset(rsc_mlpnp* s, uint32_t seed) {
     if (!s) return RSC_ERR_ARG;
     s->st.reset(seed);
-    s->last_kind = 0;
     return RSC_OK;
 }
 
