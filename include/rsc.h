@@ -7,9 +7,10 @@
  * function); the C++ facade in orb-slam2-optimized_amd/csrc/facade/ re-exposes them with the
  * reference's exact class signatures.  Plain pointers and sizes only; no torch / HIP types.
  *
- * Semantics are the reference's, including its quirks, with one
- * documented contract change (H4): rand() is a per-solver glibc stream seeded with `seed`
- * instead of the process-global stream.
+ * Semantics are the reference's, including its quirks.  rand(): by default
+ * every solver owns a glibc stream seeded with `seed` (H4: identical to srand(seed) right before that
+ * solver runs alone); solvers bound to an rsc_stream (rsc_*_bind_stream) instead draw from ONE shared
+ * stream in call order, the reference's process-global rand() (Q3, Random.cpp:47-50).
  *
  * Status codes: 0 = ok, < 0 = error (see rsc_status_string).  The library fails loudly: when no
  * HIP device is present, rsc_context_create returns RSC_ERR_NODEVICE; there is no CPU fallback.
@@ -34,6 +35,7 @@ typedef struct rsc_context rsc_context;
 typedef struct rsc_pnp rsc_pnp;
 typedef struct rsc_sim3 rsc_sim3;
 typedef struct rsc_mlpnp rsc_mlpnp;
+typedef struct rsc_stream rsc_stream;
 
 /* ---- library / context ------------------------------------------------------------------ */
 int rsc_version(void);
@@ -201,6 +203,28 @@ int rsc_mlpnp_last_poses(rsc_mlpnp* s, double* out, int cap);
 int rsc_mlpnp_last_samples(rsc_mlpnp* s, int32_t* out, int cap);
 int rsc_mlpnp_last_counts(rsc_mlpnp* s, int32_t* counts, int cap);
 
+/* ---- The reference's shared rand() stream (Q3) ---------------------------------------------------
+ * DUtils::Random::RandomInt (Thirdparty/DBoW2/DUtils/Random.cpp:47-50) draws from glibc's process-
+ * global rand(), which the reference never seeds (= srand(1)); every candidate's iterate() of a
+ * relocalization (Tracking.cpp:1239-1262) or loop closure (LoopClosing.cpp:271-286) continues that one
+ * stream where the previous call stopped.  An rsc_stream is that stream: srand(seed) and a position. */
+int rsc_stream_create(rsc_context* ctx, uint32_t seed, rsc_stream** out);
+void rsc_stream_destroy(rsc_stream* s);
+/* Consume n draws (rand() calls made elsewhere in the process between two solver calls). */
+int rsc_stream_skip(rsc_stream* s, int64_t n);
+/* Draws consumed since srand(seed). */
+int rsc_stream_position(const rsc_stream* s, int64_t* out);
+/* The next n rand() outputs, without consuming them (parity hook; computed on the device). */
+int rsc_stream_peek(rsc_stream* s, int n, int32_t* out);
+/* Bind a solver to a shared stream (NULL: back to its own stream, which resumes where it stopped).
+ * Every later iterate()/find() of a bound solver draws its samples from the stream's current position
+ * and advances it by the draws it made (mRansacMinSet per PnP / MLPnP hypothesis, 3 per Sim3
+ * hypothesis), exactly as the reference's call does.  *_iterate_many over bound solvers runs the
+ * calls one after the other in list order (the reference's call order). */
+int rsc_pnp_bind_stream(rsc_pnp* s, rsc_stream* stream);
+int rsc_sim3_bind_stream(rsc_sim3* s, rsc_stream* stream);
+int rsc_mlpnp_bind_stream(rsc_mlpnp* s, rsc_stream* stream);
+
 /* ---- Event drivers (BASELINE config 5) -----------------------------------------------------------
  * One relocalization or loop-closure event = the candidate solvers one Tracking::Relocalization() /
  * LoopClosing::ComputeSim3() call builds (Tracking.cpp:1207-1232, LoopClosing.cpp:238-265), stored
@@ -225,6 +249,18 @@ int rsc_reloc_events(rsc_pnp* const* solvers, const int32_t* event_begin, int n_
  * round = hypothesis / 5 — identical to the reference's round-robin of iterate(5) calls. */
 int rsc_loop_events(rsc_sim3* const* solvers, const int32_t* event_begin, int n_events,
                     rsc_sim3_result* per_candidate, rsc_event_result* per_event);
+/* The same events on the reference's shared rand() stream: event e's calls draw from streams[e]
+ * (one distinct stream per event; its position at the Relocalization / ComputeSim3 call) in the
+ * round-robin's call order — round by round, candidate by candidate, iterate(5) each — and advance it.
+ * All events' rounds still run in the same launches: each call is positioned assuming every earlier
+ * call of its round ran its whole loop, which holds up to the first success (the only early return),
+ * and that success ends the event.  Candidates after the winner in the winning round are calls the
+ * reference never makes: their per_candidate records are left as they were and their solver state
+ * is unspecified.  Solvers must not be bound to a stream (RSC_ERR_ARG). */
+int rsc_reloc_events_shared(rsc_pnp* const* solvers, const int32_t* event_begin, int n_events,
+                            rsc_stream* const* streams, rsc_pnp_result* per_candidate, rsc_event_result* per_event);
+int rsc_loop_events_shared(rsc_sim3* const* solvers, const int32_t* event_begin, int n_events,
+                           rsc_stream* const* streams, rsc_sim3_result* per_candidate, rsc_event_result* per_event);
 
 /* ---- Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) ------------------------------------
  * The pose-only g2o optimisation every tracking step and Tracking::Relocalization()

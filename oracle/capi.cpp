@@ -99,6 +99,12 @@ void* ora_pnp_create(int n, int n_points, const float* p2d, const float* p3dw, c
     return new PnPOracle(n, n_points, p2d, p3dw, sigma2, kp_index, fx, fy, cx, cy, seed);
 }
 void ora_pnp_destroy(void* h) { delete static_cast<PnPOracle*>(h); }
+// Q3 event replays: the solver draws from the process-global libc rand(); ora_libc_srand seeds it.
+void ora_pnp_use_libc_rand(void* h) { static_cast<PnPOracle*>(h)->use_libc_rand(); }
+void ora_sim3_use_libc_rand(void* h) { static_cast<Sim3Oracle*>(h)->use_libc_rand(); }
+void ora_mlpnp_use_libc_rand(void* h) { static_cast<MLPnPOracle*>(h)->use_libc_rand(); }
+void ora_libc_srand(uint32_t seed) { ::srand(seed); }
+int ora_libc_rand(void) { return ::rand(); }
 void ora_pnp_set_params(void* h, double prob, int min_inliers, int max_its, int min_set, float eps, float th2) {
     static_cast<PnPOracle*>(h)->SetRansacParameters(prob, min_inliers, max_its, min_set, eps, th2);
 }

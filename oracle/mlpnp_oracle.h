@@ -54,6 +54,9 @@ public:
     };
     std::vector<Trace>* trace = nullptr;
 
+    // Draw from the process-global libc rand() instead of the own stream: the reference's actual
+    // RandomInt (Random.cpp:47-50), for event replays on one shared stream (Q3).
+    void use_libc_rand() { rng.use_libc = true; }
 private:
     void CheckInliers();
     void computePose(const int* idx, int n, double R[3][3], double t[3]);

@@ -47,6 +47,9 @@ public:
     // qr_solve (PnPsolver.cpp:693-796); false on the singular bail-out (X untouched).
     static bool qr_solve(double A[6][4], double b[6], double X[4]);
 
+    // Draw from the process-global libc rand() instead of the own stream: the reference's actual
+    // RandomInt (Random.cpp:47-50), for event replays on one shared stream (Q3).
+    void use_libc_rand() { rng.use_libc = true; }
 private:
     void CheckInliers();
     bool Refine();

@@ -56,6 +56,9 @@ public:
     void compute_sim3_public(const int idx[3], float R[9], float t[3]);
     int check_inliers_public(const float R[9], const float t[3], std::vector<uint8_t>& inl);
 
+    // Draw from the process-global libc rand() instead of the own stream: the reference's actual
+    // RandomInt (Random.cpp:47-50), for event replays on one shared stream (Q3).
+    void use_libc_rand() { rng.use_libc = true; }
 private:
     void ComputeSim3(const float P1[3][3], const float P2[3][3]);
     void CheckInliers();

@@ -210,6 +210,14 @@ struct rsc_context {
     std::chrono::steady_clock::time_point t_entry;
 };
 
+// The process-global glibc rand() stream the reference draws every sample from (Random.cpp:47-50,
+// Q3): one position shared by all solvers bound to it, advanced by each iterate() call in call order.
+struct rsc_stream {
+    rsc_context* ctx = nullptr;
+    RngStream st;
+    int64_t position = 0;  // draws consumed since srand(seed)
+};
+
 struct rsc_pnp {
     rsc_context* ctx = nullptr;
     PnPState st;
@@ -224,6 +232,7 @@ struct rsc_pnp {
     int last_kind = 0;  // vbInliers of the last iterate(): 0 empty, 1 refined mask, 2 best mask
     // position in the last speculation of its context
     int spec_out0 = -1, spec_H = 0;
+    rsc_stream* stream = nullptr;  // shared rand() stream (rsc_pnp_bind_stream) or null: own stream
     ~rsc_pnp() {
         for (void* p : {(void*)d_pts, (void*)d_uv, (void*)d_pws, (void*)d_us, (void*)d_als, (void*)d_best,
                         (void*)d_refined})
@@ -242,6 +251,7 @@ struct rsc_sim3 {
     float4* d_x2 = nullptr;
     float4* d_pim = nullptr;
     int spec_out0 = -1, spec_H = 0;
+    rsc_stream* stream = nullptr;
     ~rsc_sim3() {
         for (void* p : {(void*)d_x1, (void*)d_x2, (void*)d_pim})
             if (p) (void)hipFree(p);
@@ -260,6 +270,7 @@ struct rsc_mlpnp {
     uint64_t* d_best = nullptr;
     int words = 0;
     int spec_out0 = -1, spec_H = 0;
+    rsc_stream* stream = nullptr;
     ~rsc_mlpnp() {
         for (void* p : {(void*)d_pts, (void*)d_uv, (void*)d_brg, (void*)d_cov, (void*)d_best})
             if (p) (void)hipFree(p);
@@ -1002,6 +1013,116 @@ void to_result(const PnPResult& r, rsc_pnp_result* o) {
 // ================================================================================================
 // C ABI
 // ================================================================================================
+// rand() draws per hypothesis: mRansacMinSet RandomInt calls (PnPsolver.cpp:125-131,
+// MLPnPsolver.cpp:84-92), 3 for Sim3 (Sim3Solver.cpp:140-147).
+static inline int draws_per_hypothesis(const PnPState& s) { return s.mRansacMinSet; }
+static inline int draws_per_hypothesis(const Sim3State&) { return 3; }
+static inline int draws_per_hypothesis(const MLState& s) { return s.mRansacMinSet; }
+
+// iterate() calls of solvers bound to a shared stream draw in call order, so a bound solver's call
+// starts where the previous call ended: the calls run one at a time in list order.
+template <class Solver, class Impl, class Out>
+static int bound_iterate_many(Solver* const* solvers, int count, const int32_t* n_its, Out* out,
+                              uint8_t* const* inliers, Impl impl) {
+    for (int i = 0; i < count; ++i) {
+        Solver* s = solvers[i];
+        if (!s) return RSC_ERR_ARG;
+        const int it0 = s->st.mnIterations;
+        if (s->stream) s->st.rng = s->stream->st;
+        uint8_t* const m[1] = {inliers ? inliers[i] : nullptr};
+        if (int st = impl(&solvers[i], 1, n_its + i, out + i, m)) return st;
+        if (s->stream) {
+            s->stream->st = s->st.rng;
+            s->stream->position += (int64_t)(s->st.mnIterations - it0) * draws_per_hypothesis(s->st);
+        }
+    }
+    return RSC_OK;
+}
+
+namespace {
+template <class Solver, class Res, class IterFn>
+int shared_events(Solver* const* solvers, const int32_t* event_begin, int n_events, rsc_stream* const* streams,
+                  Res* per_candidate, rsc_event_result* per_event, IterFn iter, int (*pred_its)(const Solver*)) {
+    if (n_events <= 0) return RSC_OK;
+    if (!solvers || !event_begin || !streams || !per_candidate || !per_event) return RSC_ERR_ARG;
+    const int total = event_begin[n_events];
+    for (int e = 0; e < n_events; ++e) {
+        if (event_begin[e + 1] < event_begin[e] || !streams[e]) return RSC_ERR_ARG;
+        for (int f = 0; f < e; ++f)
+            if (streams[f] == streams[e]) return RSC_ERR_ARG;  // one stream per event (calls of two events would interleave)
+        per_event[e] = rsc_event_result{-1, -1, -1, 0};
+    }
+    std::vector<char> discarded(total, 0), resolved(n_events, 0);
+    std::vector<int32_t> start_it(total);
+    for (int i = 0; i < total; ++i) {
+        if (!solvers[i] || solvers[i]->ctx != streams[0]->ctx) return RSC_ERR_ARG;
+        start_it[i] = solvers[i]->st.mnIterations;
+    }
+    for (int round = 0;; ++round) {
+        std::vector<Solver*> act;
+        std::vector<int> idx;
+        for (int e = 0; e < n_events; ++e) {
+            if (resolved[e]) continue;
+            RngStream cur = streams[e]->st;  // call positions, assuming every call runs its whole loop
+            for (int i = event_begin[e]; i < event_begin[e + 1]; ++i) {
+                if (discarded[i]) continue;
+                Solver* s = solvers[i];
+                s->st.rng = cur;
+                cur.advance(s->ctx->table, (int64_t)pred_its(s) * draws_per_hypothesis(s->st));
+                act.push_back(s);
+                idx.push_back(i);
+            }
+        }
+        if (act.empty()) break;
+        std::vector<int32_t> its(act.size(), 5), it0(act.size());
+        for (size_t q = 0; q < act.size(); ++q) it0[q] = act[q]->st.mnIterations;
+        std::vector<Res> r(act.size());
+        std::vector<uint8_t*> nomask(act.size(), nullptr);
+        if (int st = iter(act.data(), (int)act.size(), its.data(), r.data(), nomask.data())) return st;
+        std::vector<int> slot(total, -1);
+        for (size_t q = 0; q < act.size(); ++q) slot[idx[q]] = (int)q;
+        for (int e = 0; e < n_events; ++e) {
+            if (resolved[e]) continue;
+            bool any_active = false;
+            int64_t used = 0;
+            for (int i = event_begin[e]; i < event_begin[e + 1]; ++i) {
+                const int q = slot[i];
+                if (q < 0) continue;  // discarded in an earlier round
+                const Solver* s = act[q];
+                used += (int64_t)(s->st.mnIterations - it0[q]) * draws_per_hypothesis(s->st);
+                per_candidate[i] = r[q];
+                if (r[q].no_more) discarded[i] = 1;  // Tracking.cpp:1257-1261, LoopClosing.cpp:292-296
+                if (r[q].ok) {
+                    per_event[e].winner = i - event_begin[e];
+                    per_event[e].round = round;
+                    per_event[e].hypothesis = r[q].iterations - 1 - start_it[i];
+                    per_event[e].n_inliers = r[q].n_inliers;
+                    resolved[e] = 1;
+                    break;
+                }
+                if (!discarded[i]) any_active = true;
+            }
+            streams[e]->st.advance(streams[e]->ctx->table, used);
+            streams[e]->position += used;
+            if (!resolved[e] && !any_active) resolved[e] = 1;
+        }
+    }
+    return RSC_OK;
+}
+
+// hypotheses the next iterate(5) call runs unless it succeeds: PnP's '||' loop (Q1)
+// max(5, maxIts - mnIterations), Sim3's '&&' loop min(5, maxIts - mnIterations); none when N is
+// below minInliers (the call returns at once)
+int pnp_pred_its(const rsc_pnp* s) {
+    const PnPState& t = s->st;
+    return (t.N < t.mRansacMinInliers) ? 0 : std::max(0, std::max(5, t.mRansacMaxIts - t.mnIterations));
+}
+int sim3_pred_its(const rsc_sim3* s) {
+    const Sim3State& t = s->st;
+    return (t.N < t.mRansacMinInliers) ? 0 : std::max(0, std::min(5, t.mRansacMaxIts - t.mnIterations));
+}
+}  // namespace
+
 extern "C" {
 
 int rsc_version(void) { return 1; }
@@ -1160,8 +1281,21 @@ int rsc_pnp_set_ransac_parameters(rsc_pnp* s, double probability, int min_inlier
     return RSC_OK;
 }
 
+static int pnp_iterate_many_impl(rsc_pnp* const* solvers, int count, const int32_t* n_its, rsc_pnp_result* out,
+                                 uint8_t* const* inliers);
+
 int rsc_pnp_iterate_many(rsc_pnp* const* solvers, int count, const int32_t* n_its, rsc_pnp_result* out,
                          uint8_t* const* inliers) {
+    if (count <= 0) return RSC_OK;
+    if (!solvers || !n_its || !out) return RSC_ERR_ARG;
+    for (int i = 0; i < count; ++i)
+        if (solvers[i] && solvers[i]->stream)
+            return bound_iterate_many(solvers, count, n_its, out, inliers, pnp_iterate_many_impl);
+    return pnp_iterate_many_impl(solvers, count, n_its, out, inliers);
+}
+
+static int pnp_iterate_many_impl(rsc_pnp* const* solvers, int count, const int32_t* n_its, rsc_pnp_result* out,
+                                 uint8_t* const* inliers) {
     if (count <= 0) return RSC_OK;
     if (!solvers || !n_its || !out) return RSC_ERR_ARG;
     rsc_context* C = solvers[0]->ctx;
@@ -1333,8 +1467,21 @@ int rsc_sim3_set_ransac_parameters(rsc_sim3* s, double probability, int min_inli
     return RSC_OK;
 }
 
+static int sim3_iterate_many_impl(rsc_sim3* const* solvers, int count, const int32_t* n_its, rsc_sim3_result* out,
+                                  uint8_t* const* inliers);
+
 int rsc_sim3_iterate_many(rsc_sim3* const* solvers, int count, const int32_t* n_its, rsc_sim3_result* out,
                           uint8_t* const* inliers) {
+    if (count <= 0) return RSC_OK;
+    if (!solvers || !n_its || !out) return RSC_ERR_ARG;
+    for (int i = 0; i < count; ++i)
+        if (solvers[i] && solvers[i]->stream)
+            return bound_iterate_many(solvers, count, n_its, out, inliers, sim3_iterate_many_impl);
+    return sim3_iterate_many_impl(solvers, count, n_its, out, inliers);
+}
+
+static int sim3_iterate_many_impl(rsc_sim3* const* solvers, int count, const int32_t* n_its, rsc_sim3_result* out,
+                                  uint8_t* const* inliers) {
     if (count <= 0) return RSC_OK;
     if (!solvers || !n_its || !out) return RSC_ERR_ARG;
     rsc_context* C = solvers[0]->ctx;
@@ -2357,6 +2504,69 @@ int rsc_rand_stream(rsc_context* C, uint32_t seed, int n, int32_t* out) {
 }
 
 // ---- batched state helpers ----
+// ---- Shared rand() stream (Q3) ----
+int rsc_stream_create(rsc_context* C, uint32_t seed, rsc_stream** out) {
+    if (!C || !out) return RSC_ERR_ARG;
+    rsc_stream* s = new rsc_stream();
+    s->ctx = C;
+    s->st.seed(seed);
+    *out = s;
+    return RSC_OK;
+}
+
+void rsc_stream_destroy(rsc_stream* s) { delete s; }
+
+int rsc_stream_skip(rsc_stream* s, int64_t n) {
+    if (!s || n < 0) return RSC_ERR_ARG;
+    s->st.advance(s->ctx->table, n);
+    s->position += n;
+    return RSC_OK;
+}
+
+int rsc_stream_position(const rsc_stream* s, int64_t* out) {
+    if (!s || !out) return RSC_ERR_ARG;
+    *out = s->position;
+    return RSC_OK;
+}
+
+int rsc_stream_peek(rsc_stream* s, int n, int32_t* out) {
+    if (!s || !out || n < 0) return RSC_ERR_ARG;
+    if (n == 0) return RSC_OK;
+    rsc_context* C = s->ctx;
+    RSC_HIP(hipSetDevice(C->device));
+    RngStream r = s->st;
+    DevBuf<int32_t> d;
+    if (int e = d.ensure(std::min(n, 8192))) return e;
+    for (int done = 0; done < n;) {
+        const int chunk = std::min(8192, n - done);
+        r.ensure(C->table, chunk);
+        RSC_HIP(launch_rng_stream(C->d_table.p, r.window, r.g, chunk, d.p, C->stream));
+        RSC_HIP(hipMemcpyAsync(out + done, d.p, (size_t)chunk * 4, hipMemcpyDeviceToHost, C->stream));
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        r.g += chunk;
+        done += chunk;
+    }
+    return RSC_OK;
+}
+
+int rsc_pnp_bind_stream(rsc_pnp* s, rsc_stream* stream) {
+    if (!s || (stream && stream->ctx != s->ctx)) return RSC_ERR_ARG;
+    s->stream = stream;
+    return RSC_OK;
+}
+
+int rsc_sim3_bind_stream(rsc_sim3* s, rsc_stream* stream) {
+    if (!s || (stream && stream->ctx != s->ctx)) return RSC_ERR_ARG;
+    s->stream = stream;
+    return RSC_OK;
+}
+
+int rsc_mlpnp_bind_stream(rsc_mlpnp* s, rsc_stream* stream) {
+    if (!s || (stream && stream->ctx != s->ctx)) return RSC_ERR_ARG;
+    s->stream = stream;
+    return RSC_OK;
+}
+
 int rsc_pnp_reset_many(rsc_pnp* const* s, int count, const uint32_t* seeds) {
     if (count < 0 || (count && (!s || !seeds))) return RSC_ERR_ARG;
     for (int i = 0; i < count; ++i) {
@@ -2475,8 +2685,21 @@ int rsc_mlpnp_set_ransac_parameters_many(rsc_mlpnp* const* s, int count, double 
     return RSC_OK;
 }
 
+static int mlpnp_iterate_many_impl(rsc_mlpnp* const* solvers, int count, const int32_t* n_its, rsc_pnp_result* out,
+                                   uint8_t* const* inliers);
+
 int rsc_mlpnp_iterate_many(rsc_mlpnp* const* solvers, int count, const int32_t* n_its, rsc_pnp_result* out,
                            uint8_t* const* inliers) {
+    if (count <= 0) return RSC_OK;
+    if (!solvers || !n_its || !out) return RSC_ERR_ARG;
+    for (int i = 0; i < count; ++i)
+        if (solvers[i] && solvers[i]->stream)
+            return bound_iterate_many(solvers, count, n_its, out, inliers, mlpnp_iterate_many_impl);
+    return mlpnp_iterate_many_impl(solvers, count, n_its, out, inliers);
+}
+
+static int mlpnp_iterate_many_impl(rsc_mlpnp* const* solvers, int count, const int32_t* n_its, rsc_pnp_result* out,
+                                   uint8_t* const* inliers) {
     if (count <= 0) return RSC_OK;
     if (!solvers || !n_its || !out) return RSC_ERR_ARG;
     rsc_context* C = solvers[0]->ctx;
@@ -2638,5 +2861,29 @@ int rsc_loop_events(rsc_sim3* const* solvers, const int32_t* event_begin, int n_
         }
     }
     return RSC_OK;
+}
+
+// ---- Events on the reference's shared rand() stream (Q3) ----
+// One round of the round-robin: every live candidate of every unresolved event runs iterate(5) in
+// one set of launches.  A candidate's call starts where the previous candidate's call of its event
+// ended, assuming every call runs its whole loop; the only call that ends early is a success, which
+// resolves the event (Tracking.cpp:1284-1331 / LoopClosing.cpp:311-327 with the gate passed), so the
+// candidates after it in that round are calls the reference never makes: their records are
+// discarded (left as they were before the round) and the stream advances by the calls made.
+
+int rsc_reloc_events_shared(rsc_pnp* const* solvers, const int32_t* event_begin, int n_events,
+                            rsc_stream* const* streams, rsc_pnp_result* per_candidate, rsc_event_result* per_event) {
+    for (int i = 0; n_events > 0 && solvers && event_begin && i < event_begin[n_events]; ++i)
+        if (solvers[i] && solvers[i]->stream) return RSC_ERR_ARG;  // events position their own calls
+    return shared_events(solvers, event_begin, n_events, streams, per_candidate, per_event, pnp_iterate_many_impl,
+                         pnp_pred_its);
+}
+
+int rsc_loop_events_shared(rsc_sim3* const* solvers, const int32_t* event_begin, int n_events,
+                           rsc_stream* const* streams, rsc_sim3_result* per_candidate, rsc_event_result* per_event) {
+    for (int i = 0; n_events > 0 && solvers && event_begin && i < event_begin[n_events]; ++i)
+        if (solvers[i] && solvers[i]->stream) return RSC_ERR_ARG;
+    return shared_events(solvers, event_begin, n_events, streams, per_candidate, per_event, sim3_iterate_many_impl,
+                         sim3_pred_its);
 }
 }  // extern "C"

@@ -70,6 +70,9 @@ struct RngStream {
     // new window = r[m+g-31 .. m+g-1], new m = m+g, next draw 0.
     void ensure(const RngTable& tab, int need) {
         if (g + need <= kRngTableRows) return;
+        rebase(tab);
+    }
+    void rebase(const RngTable& tab) {  // requires g <= kRngTableRows
         uint32_t nw[31];
         for (int j = 0; j < 31; ++j) {
             const int x = g - 31 + j;
@@ -77,6 +80,17 @@ struct RngStream {
         }
         std::memcpy(window, nw, sizeof(nw));
         g = 0;
+    }
+    // Skip n draws of the stream (any n >= 0): the window is re-based once per table reach, so a
+    // position millions of draws ahead costs O(n / 16704) re-bases of 31 table rows each.
+    void advance(const RngTable& tab, int64_t n) {
+        while (n > 0) {
+            const int64_t room = (int64_t)kRngTableRows - g;
+            if (n <= room) { g += (int)n; return; }
+            n -= room;
+            g = kRngTableRows;
+            rebase(tab);
+        }
     }
 };
 

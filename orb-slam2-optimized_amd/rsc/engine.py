@@ -49,6 +49,9 @@ EXPORTED = [
     "rsc_optimize_sim3_many",
     "rsc_kfdb_create", "rsc_kfdb_destroy", "rsc_kfdb_add", "rsc_kfdb_erase", "rsc_kfdb_release", "rsc_kfdb_clear",
     "rsc_kfdb_set_covisibility", "rsc_kfdb_set_covisibility_many", "rsc_kfdb_detect_relocalization", "rsc_kfdb_detect_loop", "rsc_kfdb_state",
+    "rsc_stream_create", "rsc_stream_destroy", "rsc_stream_skip", "rsc_stream_position", "rsc_stream_peek",
+    "rsc_pnp_bind_stream", "rsc_sim3_bind_stream", "rsc_mlpnp_bind_stream", "rsc_reloc_events_shared",
+    "rsc_loop_events_shared",
 ]
 
 
@@ -375,6 +378,18 @@ def load_library(path: str = LIB_PATH):
     L.rsc_mlpnp_last_poses.argtypes = [vp, f64p, C.c_int]
     L.rsc_mlpnp_last_samples.argtypes = [vp, i32p, C.c_int]
     L.rsc_reloc_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(PnPResult), C.POINTER(EventResult)]
+    L.rsc_stream_create.argtypes = [vp, C.c_uint32, C.POINTER(vp)]
+    L.rsc_stream_destroy.argtypes = [vp]
+    L.rsc_stream_destroy.restype = None
+    L.rsc_stream_skip.argtypes = [vp, C.c_int64]
+    L.rsc_stream_position.argtypes = [vp, C.POINTER(C.c_int64)]
+    L.rsc_stream_peek.argtypes = [vp, C.c_int, i32p]
+    for f in ("rsc_pnp_bind_stream", "rsc_sim3_bind_stream", "rsc_mlpnp_bind_stream"):
+        getattr(L, f).argtypes = [vp, vp]
+    L.rsc_reloc_events_shared.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(vp), C.POINTER(PnPResult),
+                                          C.POINTER(EventResult)]
+    L.rsc_loop_events_shared.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(vp), C.POINTER(Sim3Result),
+                                         C.POINTER(EventResult)]
     L.rsc_pose_optimization_many.argtypes = [vp, C.POINTER(PoseOptProblem), C.c_int, C.POINTER(PoseOptResult),
                                              C.POINTER(C.c_void_p)]
     L.rsc_optimize_sim3_many.argtypes = [vp, C.POINTER(Sim3OptProblem), C.c_int, C.POINTER(Sim3OptResult),
@@ -494,6 +509,46 @@ class Context:
         return out
 
 
+class Stream:
+    """The reference's process-global rand() stream (Q3): srand(seed) and a position.  Solvers bound
+    to it (``solver.bind_stream(stream)``) draw their samples from it in call order; an event batch
+    run with one stream per event (``EventBatch.run(streams=...)``) draws each event's calls from its
+    stream in the round-robin's order."""
+
+    def __init__(self, ctx: "Context", seed: int = 1):
+        h = C.c_void_p()
+        _check(load_library().rsc_stream_create(ctx.h, seed, C.byref(h)), "rsc_stream_create")
+        self.h = h
+        self.ctx = ctx
+
+    def close(self):
+        if getattr(self, "h", None):
+            load_library().rsc_stream_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def skip(self, n: int):
+        _check(load_library().rsc_stream_skip(self.h, int(n)), "rsc_stream_skip")
+
+    @property
+    def position(self) -> int:
+        v = C.c_int64()
+        _check(load_library().rsc_stream_position(self.h, C.byref(v)), "rsc_stream_position")
+        return int(v.value)
+
+    def peek(self, n: int) -> np.ndarray:
+        out = np.zeros(max(n, 1), np.int32)
+        _check(load_library().rsc_stream_peek(self.h, n, out), "rsc_stream_peek")
+        return out[:n]
+
+
+def _bind(fn, solver, stream):
+    _check(fn(solver.h, stream.h if stream is not None else None), "bind_stream")
+    solver._stream = stream  # keep the stream alive while bound
+
+
 def _pnp_out(r: PnPResult, mask) -> dict:
     """Result dict of one PnP / MLPnP iterate().  ``mask`` None = the caller asked for no vbInliers:
     ``inliers`` is then None (never a zero array that reads like a result)."""
@@ -556,6 +611,10 @@ class PnPSolver:
 
     def reset(self, seed: int):
         _check(load_library().rsc_pnp_reset(self.h, seed), "reset")
+
+    def bind_stream(self, stream):
+        """Draw from a shared Stream (None: back to the own stream) — rsc_pnp_bind_stream."""
+        _bind(load_library().rsc_pnp_bind_stream, self, stream)
 
     def state(self) -> dict:
         out = np.zeros(8, np.int32)
@@ -662,6 +721,9 @@ class Sim3Solver:
     def reset(self, seed: int):
         _check(load_library().rsc_sim3_reset(self.h, seed), "reset")
 
+    def bind_stream(self, stream):
+        _bind(load_library().rsc_sim3_bind_stream, self, stream)
+
     def state(self) -> dict:
         out = np.zeros(6, np.int32)
         _check(load_library().rsc_sim3_get_state(self.h, out), "get_state")
@@ -745,6 +807,9 @@ class MLPnPSolver:
 
     def reset(self, seed: int):
         _check(load_library().rsc_mlpnp_reset(self.h, seed), "reset")
+
+    def bind_stream(self, stream):
+        _bind(load_library().rsc_mlpnp_bind_stream, self, stream)
 
     def state(self) -> dict:
         out = np.zeros(6, np.int32)
@@ -845,10 +910,19 @@ class EventBatch:
         self.cand = np.ctypeslib.as_array(self._cand)
         self.per_event = np.ctypeslib.as_array(self._ev)
 
-    def run(self):
+    def run(self, streams=None):
+        """Run every event.  ``streams``: one Stream per event = the reference's shared rand() stream
+        at that event's call (rsc_reloc_events_shared / rsc_loop_events_shared); None = every
+        candidate on its own stream (H4)."""
         L = load_library()
-        f = L.rsc_loop_events if self.kind == "sim3" else L.rsc_reloc_events
-        _check(f(self.batch._h, self.begin, len(self.events), self._cand, self._ev), "events")
+        if streams is None:
+            f = L.rsc_loop_events if self.kind == "sim3" else L.rsc_reloc_events
+            _check(f(self.batch._h, self.begin, len(self.events), self._cand, self._ev), "events")
+            return self.per_event
+        assert len(streams) == len(self.events)
+        hs = (C.c_void_p * len(streams))(*[st.h.value for st in streams])
+        f = L.rsc_loop_events_shared if self.kind == "sim3" else L.rsc_reloc_events_shared
+        _check(f(self.batch._h, self.begin, len(self.events), hs, self._cand, self._ev), "events_shared")
         return self.per_event
 
     def winner_poses(self) -> np.ndarray:

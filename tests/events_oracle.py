@@ -34,6 +34,42 @@ def run_event(ev, inputs=None):
     return dict(winner=-1, round=-1, hypothesis=-1, n_inliers=0), np.zeros(16, np.float32)
 
 
+def run_event_shared(ev, seed: int = 1, inputs=None):
+    """The event on the reference's ONE process-global rand() stream (Q3, Random.cpp:47-50): srand(seed)
+    (1 = the reference's unseeded state), then the round-robin's iterate(5) calls in order, every
+    candidate drawing from libc's rand() where the previous call stopped.  Returns (record, pose,
+    rand() calls consumed)."""
+    inputs = inputs if inputs is not None else rev.event_inputs(ev)
+    if ev.kind == "reloc":
+        solvers = [ol.OraclePnP(sc, 1) for sc in inputs]
+        for o in solvers:
+            o.set_ransac_parameters(*rev.RELOC_PARAMS)
+    else:
+        solvers = [ol.OracleSim3(p, 1) for p in inputs]
+        for o in solvers:
+            o.set_ransac_parameters(*rev.LOOP_PARAMS)
+    per = (rev.RELOC_PARAMS[3] if ev.kind == "reloc" else 3)
+    for o in solvers:
+        o.use_libc_rand()
+    ol.libc_srand(seed)
+    active = list(range(len(solvers)))
+    rnd, used = 0, 0
+    while active:
+        nxt = []
+        for i in active:
+            before = solvers[i].info()["iterations"]
+            r = solvers[i].iterate(5)
+            used += (solvers[i].info()["iterations"] - before) * per
+            if r["ok"]:
+                pose = np.asarray(r["T"], np.float32).ravel() if ev.kind == "reloc" else rev.sim3_pose16(r["R"], r["t"])
+                return dict(winner=i, round=rnd, hypothesis=r["iterations"] - 1, n_inliers=r["n_inliers"]), pose, used
+            if not r["no_more"]:
+                nxt.append(i)
+        active = nxt
+        rnd += 1
+    return dict(winner=-1, round=-1, hypothesis=-1, n_inliers=0), np.zeros(16, np.float32), used
+
+
 def run_events(evs):
     recs, poses = [], []
     for ev in evs:

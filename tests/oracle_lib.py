@@ -68,6 +68,10 @@ def lib():
     L.ora_pnp_create.argtypes = [C.c_int, C.c_int, f32p, f32p, f32p, i32p, C.c_float, C.c_float, C.c_float,
                                  C.c_float, C.c_uint32]
     L.ora_pnp_destroy.argtypes = [vp]
+    for f in ("ora_pnp_use_libc_rand", "ora_sim3_use_libc_rand", "ora_mlpnp_use_libc_rand"):
+        getattr(L, f).argtypes = [vp]
+    L.ora_libc_srand.argtypes = [C.c_uint32]
+    L.ora_libc_rand.restype = C.c_int
     L.ora_pnp_set_params.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
     L.ora_pnp_iterate.argtypes = [vp, C.c_int, C.POINTER(C.c_int), u8p, C.POINTER(C.c_int), C.POINTER(C.c_int), f32p]
     L.ora_pnp_info.argtypes = [vp, i32p]
@@ -228,6 +232,11 @@ class OraclePnP:
             lib().ora_pnp_destroy(self.h)
             self.h = None
 
+    def use_libc_rand(self):
+        """Draw samples from the process-global libc rand() (the reference's RandomInt source, Q3);
+        seed it with libc_srand."""
+        lib().ora_pnp_use_libc_rand(self.h)
+
     def set_ransac_parameters(self, probability=0.99, min_inliers=8, max_iterations=300, min_set=4,
                               epsilon=0.4, th2=5.991):
         lib().ora_pnp_set_params(self.h, probability, min_inliers, max_iterations, min_set, epsilon, th2)
@@ -289,6 +298,11 @@ class OracleSim3:
             lib().ora_sim3_destroy(self.h)
             self.h = None
 
+    def use_libc_rand(self):
+        """Draw samples from the process-global libc rand() (the reference's RandomInt source, Q3);
+        seed it with libc_srand."""
+        lib().ora_sim3_use_libc_rand(self.h)
+
     @property
     def N(self):
         return lib().ora_sim3_n(self.h)
@@ -347,6 +361,11 @@ class OracleMLPnP:
         if getattr(self, "h", None):
             lib().ora_mlpnp_destroy(self.h)
             self.h = None
+
+    def use_libc_rand(self):
+        """Draw samples from the process-global libc rand() (the reference's RandomInt source, Q3);
+        seed it with libc_srand."""
+        lib().ora_mlpnp_use_libc_rand(self.h)
 
     def set_covariances(self, cov):
         """computePose's covMats ([n, 3, 3]) or None."""
@@ -559,3 +578,12 @@ def optimize_sim3(p):
                                 np.ascontiguousarray(p.uv2, np.float32), np.ascontiguousarray(p.inv1, np.float32),
                                 np.ascontiguousarray(p.inv2, np.float32), p.poses24(), p.K8(), float(p.th2), S, keep, st)
     return r, S, keep[:n], st
+
+
+def libc_srand(seed: int):
+    """srand(seed) of the process-global libc stream the use_libc_rand solvers draw from."""
+    lib().ora_libc_srand(seed)
+
+
+def libc_rand() -> int:
+    return int(lib().ora_libc_rand())
