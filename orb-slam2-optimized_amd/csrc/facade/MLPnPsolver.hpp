@@ -41,6 +41,7 @@ public:
         pb.kp_index = kp.data();
         pb.fx = F.fx; pb.fy = F.fy; pb.cx = F.cx; pb.cy = F.cy;
         check(rsc_mlpnp_create(thread_context(), &pb, seed, &s_), "rsc_mlpnp_create");
+        if (rsc_stream* st = construction_stream()) check(rsc_mlpnp_bind_stream(s_, st), "rsc_mlpnp_bind_stream");
         n_points_ = pb.n_points;
     }
     ~MLPnPsolver() { rsc_mlpnp_destroy(s_); }

@@ -45,6 +45,7 @@ public:
         pb.kp_index = kp.data();
         pb.fx = F.fx; pb.fy = F.fy; pb.cx = F.cx; pb.cy = F.cy;
         check(rsc_pnp_create(thread_context(), &pb, seed, &s_), "rsc_pnp_create");
+        if (rsc_stream* st = construction_stream()) check(rsc_pnp_bind_stream(s_, st), "rsc_pnp_bind_stream");
         n_points_ = pb.n_points;
     }
     ~PnPsolver() { rsc_pnp_destroy(s_); }

@@ -71,6 +71,7 @@ public:
         in.K1[0] = K1(0, 0); in.K1[1] = K1(1, 1); in.K1[2] = K1(0, 2); in.K1[3] = K1(1, 2);
         in.K2[0] = K2(0, 0); in.K2[1] = K2(1, 1); in.K2[2] = K2(0, 2); in.K2[3] = K2(1, 2);
         check(rsc_sim3_create(thread_context(), &in, seed, &s_), "rsc_sim3_create");
+        if (rsc_stream* st = construction_stream()) check(rsc_sim3_bind_stream(s_, st), "rsc_sim3_bind_stream");
         n1_ = n1;
     }
     ~Sim3Solver() { rsc_sim3_destroy(s_); }

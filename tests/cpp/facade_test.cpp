@@ -187,6 +187,54 @@ int main(int argc, char** argv) {
             wr<int32_t>(out, (int32_t)inl.size());
             for (bool v : inl) wr<uint8_t>(out, v ? 1 : 0);
         }
+    } else if (mode == 9) {
+        // Tracking::Relocalization's RANSAC loop (Tracking.cpp:1239-1262) over K candidate Frames with
+        // the facade in reference_rand mode: every solver draws from the thread's one rand() stream
+        // (srand(1), Q3).  Per call: candidate, ok, bNoMore, nInliers, Tcw; ends at the first pose.
+        rsc_orb::reference_rand(true);
+        const int K = rd<int32_t>(in);
+        const double prob = rd<double>(in);
+        const int mi = rd<int32_t>(in), mx = rd<int32_t>(in), ms = rd<int32_t>(in);
+        const float eps = rd<float>(in), th2 = rd<float>(in);
+        std::vector<Frame> frames(K);
+        std::vector<std::vector<std::shared_ptr<MapPoint>>> matches(K);
+        std::vector<std::unique_ptr<rsc_orb::PnPsolver<Frame, MapPoint>>> solvers(K);
+        for (int k = 0; k < K; ++k) {
+            Frame& F = frames[k];
+            const int n = rd<int32_t>(in);
+            F.fx = rd<float>(in); F.fy = rd<float>(in); F.cx = rd<float>(in); F.cy = rd<float>(in);
+            const int nl = rd<int32_t>(in);
+            for (int l = 0; l < nl; ++l) F.mvLevelSigma2.push_back(rd<float>(in));
+            matches[k].resize(n);
+            F.mvKeysUn.resize(n);
+            for (int i = 0; i < n; ++i) {
+                const int present = rd<int32_t>(in);
+                KeyPoint kp; kp.pt.x = rd<float>(in); kp.pt.y = rd<float>(in); kp.octave = rd<int32_t>(in);
+                Vec3 X; X.v[0] = rd<float>(in); X.v[1] = rd<float>(in); X.v[2] = rd<float>(in);
+                F.mvKeysUn[i] = kp;
+                if (present) { auto mp = std::make_shared<MapPoint>(); mp->bad = (present == 2); mp->X = X; matches[k][i] = mp; }
+            }
+            solvers[k].reset(new rsc_orb::PnPsolver<Frame, MapPoint>(F, matches[k], 1000 + k));
+            solvers[k]->SetRansacParameters(prob, mi, mx, ms, eps, th2);
+        }
+        std::vector<bool> discarded(K, false);
+        int nCandidates = K;
+        bool bMatch = false;
+        while (nCandidates > 0 && !bMatch) {
+            for (int i = 0; i < K; ++i) {
+                if (discarded[i]) continue;
+                bool nm = false; std::vector<bool> inl; int ni = -1; Mat4 T; std::memset(&T, 0, sizeof(T));
+                const bool ok = solvers[i]->iterate(5, nm, inl, ni, T);
+                wr<int32_t>(out, i); wr<int32_t>(out, ok); wr<int32_t>(out, nm); wr<int32_t>(out, ni);
+                for (int a = 0; a < 4; ++a) for (int b = 0; b < 4; ++b) wr<float>(out, T.m[a][b]);
+                if (nm) { discarded[i] = true; nCandidates--; }
+                if (ok) { bMatch = true; break; }
+            }
+        }
+        wr<int32_t>(out, -1);
+        int64_t pos = -1;
+        rsc_stream_position(rsc_orb::thread_stream(), &pos);
+        wr<int64_t>(out, pos);
     } else if (mode == 4) {
         // Optimizer::PoseOptimization on a mock Frame: n slots, fx..cy, mbf, Tcw, levels of
         // mvInvLevelSigma2, per slot (present, u, v, octave, X, uR)

@@ -353,3 +353,44 @@ def test_optimize_sim3_facade_matches_oracle():
     assert np.array_equal(S.view(np.uint64), So.view(np.uint64))
     expect = (kind != 0) & (keep == 1)
     assert np.array_equal(still.astype(bool), expect)
+
+
+def test_relocalization_loop_on_the_reference_rand_stream():
+    """The facade in reference_rand mode (csrc/facade/rsc_context.hpp, Q3): Tracking::Relocalization's
+    round-robin (Tracking.cpp:1239-1262) over several candidate Frames, every solver drawing from the
+    thread's one srand(1) stream in call order — every call equals the oracle's call on libc's real
+    rand(), and the stream ends at the oracle's position."""
+    rng = np.random.default_rng(12)
+    s2 = synth.level_sigma2()
+    scenes = [synth.make_pnp_scene(rng, int(rng.integers(150, 600)), r) for r in (0.2, 0.3, 0.05, 0.62, 0.7)]
+    params = (0.99, 10, 300, 4, 0.5, 5.991)
+    buf = struct.pack("<i", 9) + struct.pack("<i", len(scenes)) + struct.pack("<d", params[0])
+    buf += struct.pack("<iii", *params[1:4]) + struct.pack("<ff", *params[4:])
+    for sc in scenes:
+        octaves = np.array([int(np.where(s2 == v)[0][0]) for v in sc.sigma2])
+        buf += struct.pack("<i4f", sc.n, sc.fx, sc.fy, sc.cx, sc.cy) + struct.pack("<i", len(s2))
+        buf += s2.astype("<f4").tobytes()
+        for i in range(sc.n):
+            buf += struct.pack("<i2fi3f", 1, sc.p2d[i, 0], sc.p2d[i, 1], octaves[i], *sc.p3dw[i])
+    out = run(buf)
+    os_ = [ol.OraclePnP(sc, 1) for sc in scenes]
+    for o in os_:
+        o.set_ransac_parameters(*params)
+        o.use_libc_rand()
+    ol.libc_srand(1)
+    off, calls, used = 0, 0, 0
+    while True:
+        (i,) = struct.unpack_from("<i", out, off); off += 4
+        if i < 0:
+            break
+        ok, nm, ni = struct.unpack_from("<3i", out, off); off += 12
+        T = np.frombuffer(out, "<f4", 16, off).reshape(4, 4); off += 64
+        before = os_[i].info()["iterations"]
+        r = os_[i].iterate(5)
+        used += 4 * (os_[i].info()["iterations"] - before)
+        assert (bool(ok), bool(nm), ni) == (r["ok"], r["no_more"], r["n_inliers"]), f"call {calls} cand {i}"
+        if r["ok"]:
+            assert np.array_equal(bits(T), bits(r["T"]))
+        calls += 1
+    (pos,) = struct.unpack_from("<q", out, off)
+    assert calls >= 4 and pos == used
