@@ -367,11 +367,17 @@ def cpu_baseline_pnp(scenes, args, threads):
 # ------------------------------------------------------------------------------------------------
 # config 3 / 4
 # ------------------------------------------------------------------------------------------------
-def run_sharded(engine, ctx, batch, lo, hi, total, params, args, dist, world, steps, pack):
+def run_sharded(engine, ctx, batch, lo, hi, total, params, args, dist, world, steps, pack, winner=None,
+                mask_len=0):
     """One sharded RANSAC section (configs 3 and 4): every rank runs candidates [lo, hi) of the
     section's `total` (seeds by global candidate index, so any world size gives the same records),
     then ONE all-gather of the fixed-size result records (RCCL over xGMI) when world > 1.  Timed
-    like the headline: barrier + sync around K steps, max over ranks, hypotheses summed."""
+    like the headline: barrier + sync around K steps, max over ranks, hypotheses summed.
+
+    winner = "loop" / "reloc": the all-gather also carries the vbInliers (mask_len entries) of the
+    rank's candidate that can win (rsc.dist.all_gather_records_and_mask: the loop-closure winner by
+    (round, candidate), LoopClosing.cpp:271-309; the relocalization winner by index,
+    Tracking.cpp:1241-1284), so every rank holds the winner's mask after the step."""
     from rsc import dist as rdist
     from rsc import workloads as wl
     gather = None  # records per rank of the all-gather: the largest shard
@@ -383,20 +389,30 @@ def run_sharded(engine, ctx, batch, lo, hi, total, params, args, dist, world, st
     ids = list(range(lo, hi))
     state = {"records": None}
 
+    with_mask = gather is not None and winner is not None
+
     def local(s):
         batch.reset(wl.step_seeds(s, total)[lo:hi])
         batch.set_ransac_parameters(*params)
+        if with_mask:  # result dicts with vbInliers of the successful candidates
+            return batch.iterate(args.iters, with_masks=True)
         return batch.iterate_raw(args.iters)
 
     def step(s):
         h = 0
         rec = np.zeros((0, rdist.RECORD), np.float32)
+        outs = None
         if batch is not None:
             outs = local(s)
-            h = int(outs["iterations"].sum())
+            h = int(sum(o["iterations"] for o in outs)) if with_mask else int(outs["iterations"].sum())
             if gather is not None:
                 rec = pack(ids, outs)
-        if gather is not None:
+        if with_mask:
+            c = rdist.local_loop_candidate(rec) if winner == "loop" else rdist.local_reloc_candidate(rec)
+            m = outs[c - lo]["inliers"] if c >= 0 else None
+            rec, state["masks"] = rdist.all_gather_records_and_mask(dist, rec, gather, c, m, mask_len,
+                                                                    device=COLL_DEV)
+        elif gather is not None:
             rec = rdist.all_gather_records(dist, rec, gather, device=COLL_DEV)
         state["records"] = rec
         return h
@@ -419,7 +435,9 @@ def run_sharded(engine, ctx, batch, lo, hi, total, params, args, dist, world, st
     if batch is not None:
         ctx.enable_timing(True)
         for s in range(steps):
-            local(args.warmup + steps + s)
+            batch.reset(wl.step_seeds(args.warmup + steps + s, total)[lo:hi])
+            batch.set_ransac_parameters(*params)
+            batch.iterate_raw(args.iters)
             tm = ctx.last_timing()
             kt["solve_ms"] += tm["solve_ms"]
             kt["scan_ms"] += tm["scan_ms"]
@@ -442,7 +460,8 @@ def run_sim3(engine, ctx, pairs, args, dist=None, rank=0, world=1):
     lo, hi = rdist.shard_range(C, world, rank, [p.n1 for p in pairs])
     solvers = [engine.Sim3Solver(ctx, p, 1) for p in pairs[lo:hi]]
     batch = engine.SolverBatch(solvers) if solvers else None
-    r, rec = run_sharded(engine, ctx, batch, lo, hi, C, wl.LOOP, args, dist, world, args.steps, rdist.pack_sim3)
+    r, rec = run_sharded(engine, ctx, batch, lo, hi, C, wl.LOOP, args, dist, world, args.steps, rdist.pack_sim3,
+                         winner="loop", mask_len=max(p.n1 for p in pairs))
     r.update(pairs=C, pairs_per_rank=hi - lo, correspondences=pairs[0].n1,
              sharding=f"{world} rank(s), contiguous blocks by N, RCCL all-gather of {rdist.RECORD}-float records")
     # config 3 is scan-bound (Horn on 3 points is tiny): FP32 VALU roofline of the scan kernel with
