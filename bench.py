@@ -463,7 +463,8 @@ def run_sim3(engine, ctx, pairs, args, dist=None, rank=0, world=1):
     r, rec = run_sharded(engine, ctx, batch, lo, hi, C, wl.LOOP, args, dist, world, args.steps, rdist.pack_sim3,
                          winner="loop", mask_len=max(p.n1 for p in pairs))
     r.update(pairs=C, pairs_per_rank=hi - lo, correspondences=pairs[0].n1,
-             sharding=f"{world} rank(s), contiguous blocks by N, RCCL all-gather of {rdist.RECORD}-float records")
+             sharding=f"{world} rank(s), contiguous blocks by N, RCCL all-gather of {rdist.RECORD}-float records"
+                      + (" + the loop-closure winner's vbInliers (mN1 bits) in the same collective" if world > 1 else ""))
     # config 3 is scan-bound (Horn on 3 points is tiny): FP32 VALU roofline of the scan kernel with
     # SURVEY §8(d)'s F_h = 62 N flops and B_h = 48 N bytes per hypothesis
     scan_ms = r["kernel_ms_per_launch"]["scan"]
