@@ -135,7 +135,8 @@ constexpr int kBetasHyps = 64;
 hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, const int2* wgtB,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
-                                  hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr, bool eig_rows = false);
+                                  hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr, bool eig_rows = false,
+                                  int betas_hb = kBetasHyps);
 // counts: where the host reads them (pinned memory or HBM); counts_dev (nullable): an HBM copy for
 // pnp_select_refine_kernel.
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,

@@ -6,6 +6,11 @@ path's bits, so each is checked against the oracle exactly like the default path
   latency-bound launches such as one relocalization event: every hypothesis of exhaustive batches
   (min sets 4..6, a planar scene for the NaN path), and a relocalization event stream.
 
+* the beta-approximation stage with one hypothesis per wave (`rsc_context_set_betas_uniform`,
+  pnp_betas_uniform_kernel: the chain wave-uniform), for the same small launches: every hypothesis of
+  exhaustive batches (min sets 4..6, planar NaN path), alone and combined with the rows form, and a
+  relocalization event stream.
+
 Opt-in (RSC_TEST_VARIANTS=1): a variant that has not yet run on hardware is not put in the path of
 the default suite."""
 import os
@@ -27,17 +32,24 @@ def _nan_equal(a, b):
     return np.array_equal(na, nb) and np.array_equal(a.view(np.uint32)[~na], b.view(np.uint32)[~nb])
 
 
-def _rows_ctx():
+def _rows_ctx(rows=True, uniform=False):
     from rsc import engine
     c = engine.Context(0)
-    c.set_eig_rows(1 << 20)  # every launch in the rows form
+    if rows:
+        c.set_eig_rows(1 << 20)  # every launch in the rows form
+    if uniform:
+        c.set_betas_uniform(1 << 20)  # every launch with one hypothesis per betas wave
     return c
 
 
+FORMS = [(True, False), (False, True), (True, True)]
+
+
 @pytest.mark.parametrize("ms", [4, 5, 6])
-def test_eig_rows_every_hypothesis(ms):
+@pytest.mark.parametrize("rows,uniform", FORMS)
+def test_eig_rows_every_hypothesis(ms, rows, uniform):
     from rsc import engine
-    c = _rows_ctx()
+    c = _rows_ctx(rows, uniform)
     rng = np.random.default_rng(900 + ms)
     scenes = [synth.make_pnp_scene(rng, 700, 0.4), synth.make_pnp_scene(rng, 1900, 0.35),
               synth.make_planar_pnp_scene(rng, 500, 0.4, "floor"), synth.make_pnp_scene(rng, 230, 0.45)]
@@ -63,10 +75,11 @@ def test_eig_rows_every_hypothesis(ms):
     c.close()
 
 
-def test_eig_rows_reloc_events():
+@pytest.mark.parametrize("rows,uniform", FORMS)
+def test_eig_rows_reloc_events(rows, uniform):
     from rsc import engine, events as rev
     import events_oracle as eo
-    c = _rows_ctx()
+    c = _rows_ctx(rows, uniform)
     evs = [ev for ev in rev.make_event_stream(seed=23, n_reloc=8, n_loop=0) if ev.kind == "reloc"]
     eb = engine.EventBatch([[engine.PnPSolver(c, x, s) for x, s in zip(rev.event_inputs(ev), ev.seeds)] for ev in evs])
     eb.batch.set_ransac_parameters(*rev.RELOC_PARAMS)

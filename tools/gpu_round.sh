@@ -50,6 +50,12 @@ if [ -n "$VARIANTS" ]; then
     if [ $v = a ]; then L=orb-slam2-optimized_amd/lib/librsc.so; else L=tools/bin/librsc_regrows.so; fi
     RSC_LIBRSC=$L timeout -k 10 200 python bench.py --only-headline --no-cpu >> $OUT/regrows_ab_$v.jsonl 2>> $OUT/regrows_ab.err
   done
+  # the small-launch forms on the whole config-2 batch (rows-form eigen stage; uniform betas is
+  # pointless there: 57,600 waves)
+  for v in a r a r; do
+    if [ $v = a ]; then E=0; else E=1000000; fi
+    RSC_EIG_ROWS=$E timeout -k 10 200 python bench.py --only-headline --no-cpu >> $OUT/rows_headline_ab_$v.jsonl 2>> $OUT/rows_headline_ab.err
+  done
 fi
 if [ -n "$PLANAR" ]; then
   # planar-content config-2 eigen stage with and without the NaN-block exit
