@@ -4,7 +4,7 @@ it by an op-counter build of the CPU restatement and report mean ± σ per confi
 own inputs: the oracle restatements compiled with a counting scalar (tools/opc_*.cpp ->
 tools/build/libopcount.so: +, -, *, /, sqrt and fma count as flops, transcendental calls one each).
 
-    make -C tools opcount_lib && python3 tools/opcount_report.py    # -> profiles/r04/opcount.json
+    make -C tools opcount_lib && python3 tools/opcount_report.py [OUT]   # default profiles/r05/opcount.json
 
 Units: EPnP / MLPnP — one compute_pose on a minimal sample (4 / 6 points); PoseOptimization — one
 Frame's whole call (4 rounds of LM); OptimizeSim3 — one KeyFrame pair's whole call.  Sim3 (config 3)
@@ -98,7 +98,7 @@ def main():
                                    text=True).stdout.strip()
     rep["counting"] = ("op-counter builds of the oracle restatements (tools/opc_*.cpp): +, -, *, /, sqrt = 1 flop, "
                        "fma = 2, sin/cos/acos/pow/log/exp calls = 1; comparisons and fabs not counted")
-    out = os.path.join(ROOT, "profiles", "r04", "opcount.json")
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r05", "opcount.json")
     with open(out, "w") as f:
         json.dump(rep, f, indent=1)
     print(json.dumps(rep, indent=1))
