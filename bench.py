@@ -138,6 +138,7 @@ def launch_ranks(args) -> int:
     return rc
 
 
+DEFAULT_EIG_ROWS = 64  # the library's default rows-form threshold (rsc_kernels.h kEigRowsDefaultWgs)
 COLL_DEV = "cuda"  # device of the collective tensors: cuda for RCCL, cpu for gloo
 RESULT_OUT = sys.stdout  # where rank 0 prints the one JSON line
 RCCL1 = None  # world-1 RCCL process group (torch.distributed) for rccl_check, or the error text
@@ -664,28 +665,21 @@ def latency_event(kind: str, seed: int = 4242):
 
 
 def eig_rows_ab(ctx, eb, params, seeds, ref, reps):
-    """Interleaved A/B of the single relocalization event's small-launch forms: the eigen stage as
-    lane pairs (default) or in the Refine's rows form (rsc_context_set_eig_rows), times the beta
-    stage with 64 hypotheses per wave (default) or one (rsc_context_set_betas_uniform)
-    — same event, the four forms in turn; the event's outcome must not change.  Then one timed pass
-    per form with HIP events (eigen stage, solve pair, Refine).  Off-default variants: reported,
-    not the metric."""
+    """Interleaved A/B of the eigen-stage form on the single relocalization event: lane pairs vs the
+    Refine's rows form (the default for small launches since round 5, rsc_context_set_eig_rows;
+    DESIGN.md §9) — same event, alternating calls; the event's outcome must not change.  Then one
+    timed pass per form with HIP events (eigen stage, solve pair, Refine).  Reported beside the
+    metric, never replaces gpu_ms."""
     keys = ("winner", "round", "hypothesis", "n_inliers")
-    forms = {"pairs": (0, 0), "rows": (1, 0), "pairs_uniform": (0, 1), "rows_uniform": (1, 1)}
+    forms = {"pairs": 0, "rows": 1 << 20}
     names = list(forms)
     times = {k: [] for k in names}
     kern = {}
     same = True
-
-    def use(name):
-        rows, uni = forms[name]
-        ctx.set_eig_rows(1 << 20 if rows else 0)
-        ctx.set_betas_uniform(1 << 20 if uni else 0)
-
     try:
         for r in range(len(names) * (reps + 5)):
             name = names[r % len(names)]
-            use(name)
+            ctx.set_eig_rows(forms[name])
             t0 = time.perf_counter()
             eb.batch.reset(seeds)
             eb.batch.set_ransac_parameters(*params)
@@ -695,7 +689,7 @@ def eig_rows_ab(ctx, eb, params, seeds, ref, reps):
                 times[name].append(t)
             same = same and all(int(res[0][k]) == int(ref[k]) for k in keys)
         for name in names:
-            use(name)
+            ctx.set_eig_rows(forms[name])
             ctx.enable_timing(True)
             acc = np.zeros(3)
             for _ in range(10):
@@ -706,12 +700,11 @@ def eig_rows_ab(ctx, eb, params, seeds, ref, reps):
                 acc += [tm["eig_ms"], tm["solve_ms"], tm["refine_ms"]]
             ctx.enable_timing(False)
             kern[name] = {k: round(float(v) / 10, 4) for k, v in zip(("eig_ms", "solve_ms", "refine_ms"), acc)}
-    except Exception as e:  # an A/B variant must never cost the bench line
+    except Exception as e:  # an A/B must never cost the bench line
         return dict(error=str(e)[:200])
     finally:
         ctx.enable_timing(False)
-        ctx.set_eig_rows(0)
-        ctx.set_betas_uniform(0)
+        ctx.set_eig_rows(DEFAULT_EIG_ROWS)
     out = {f"{k}_ms": round(1e3 * float(np.median(v)), 4) for k, v in times.items()}
     out.update(same_result=bool(same), reps=len(times["pairs"]), kernels=kern)
     return out

@@ -57,16 +57,12 @@ int rsc_context_last_kernel_timing(rsc_context* ctx, double out[6]);
  * [0] first launch, [1] kernels enqueued, [2] results back on the host, [3] return. */
 int rsc_diag_host_timing(rsc_context* ctx, double out[4]);
 int rsc_context_enable_timing(rsc_context* ctx, int enable);
-/* Eigen-stage form of the EPnP hypothesis solve (A/B option, no effect on results): launches whose
- * eigen stage has at most max_workgroups workgroups of 20 hypotheses run it in the Refine's rows
- * form (a 12-lane group per hypothesis, Q rows in VGPRs: lower latency for small, latency-bound
- * launches such as one relocalization event); 0 (default, or env RSC_EIG_ROWS) keeps the lane-pair form. */
+/* Eigen-stage form of the EPnP hypothesis solve (no effect on results): launches whose eigen stage
+ * has at most max_workgroups workgroups of 20 hypotheses run it in the Refine's rows form (a 12-lane
+ * group per hypothesis, Q rows in VGPRs: lower latency for small, latency-bound launches such as one
+ * relocalization event); larger launches use lane pairs.  Default 64 (env RSC_EIG_ROWS overrides);
+ * 0 = lane pairs always. */
 int rsc_context_set_eig_rows(rsc_context* ctx, int max_workgroups);
-/* Beta-approximation stage form (A/B option, no effect on results): rounds of at most max_hypotheses
- * hypotheses run one hypothesis per wave (every lane of the wave on the same chain, so its branches
- * are wave-uniform: lower latency for small launches such as one relocalization event) instead of
- * 64 per wave; 0 (default, or env RSC_BETAS_UNIFORM) keeps 64. */
-int rsc_context_set_betas_uniform(rsc_context* ctx, int max_hypotheses);
 /* Self-test of the device libm restatement (rsc_math.h, used by Sim3 angles, MLPnP, SearchBySim3):
  * out[i] = f(x[i]) computed ON THE GPU, f = 0 sin, 1 cos, 2 acos, 3 cbrt, 4 log, 5 logf
  * ((float)x[i] in, float result widened); and the eigen-solver chase's short-chain forms

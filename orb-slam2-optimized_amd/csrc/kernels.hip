@@ -73,21 +73,6 @@ __global__ __launch_bounds__(64) void pnp_betas_kernel(const DevPnP* __restrict_
     pnp_betas_wave_body<NS>(probs, lps, wg_table, ngroups, kBetasHyps, stage, samples, poses, berr, bpose, bctr, hcap, smem);
 }
 
-// Small launches: one hypothesis per wave (hb = 1), the chain wave-uniform (rsc_quad.h).
-template <int NS>
-__global__ __launch_bounds__(64) void pnp_betas_uniform_kernel(const DevPnP* __restrict__ probs,
-                                                               const LaunchProb* __restrict__ lps,
-                                                               const int2* __restrict__ wg_table, int ngroups,
-                                                               const double* __restrict__ stage,
-                                                               const int32_t* __restrict__ samples,
-                                                               float* __restrict__ poses, double* __restrict__ berr,
-                                                               float* __restrict__ bpose, unsigned* __restrict__ bctr,
-                                                               size_t hcap) {
-    __shared__ __attribute__((aligned(16))) double smem[kBetasUniformSmemDoubles];
-    pnp_betas_wave_body<NS, true>(probs, lps, wg_table, ngroups, 1, stage, samples, poses, berr, bpose, bctr, hcap,
-                                  smem);
-}
-
 // ------------------------------------------------------------------------------------------------
 // PnP inlier scan (CheckInliers) — points-stationary, pose broadcast.
 // ------------------------------------------------------------------------------------------------
@@ -817,8 +802,7 @@ static hipError_t launch_eig_rows(int nwgE, const int2* wgtE, const DevPnP* prob
 hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, const int2* wgtB,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
-                                  hipEvent_t eig_begin, hipEvent_t eig_end, bool eig_rows, int betas_hb) {
-    if (betas_hb != 1 && betas_hb != kBetasHyps) return hipErrorInvalidValue;
+                                  hipEvent_t eig_begin, hipEvent_t eig_end, bool eig_rows) {
     if (ns < 4 || ns > 6) return hipErrorInvalidValue;
     if (eig_begin) (void)hipEventRecord(eig_begin, st);
     switch (ns) {
@@ -830,12 +814,8 @@ hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, 
         } else                                                                                        \
             pnp_eig_group_kernel<N><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples);        \
         if (eig_end) (void)hipEventRecord(eig_end, st);                                               \
-        if (betas_hb == 1)                                                                            \
-            pnp_betas_uniform_kernel<N><<<3 * nwgB, 64, 0, st>>>(probs, lps, wgtB, nwgB, stage, samples,\
-                                                                 poses, bs.err, bs.pose, bs.ctr, bs.hcap);\
-        else                                                                                          \
-            pnp_betas_kernel<N><<<3 * nwgB, 64, 0, st>>>(probs, lps, wgtB, nwgB, stage, samples, poses,\
-                                                         bs.err, bs.pose, bs.ctr, bs.hcap);           \
+        pnp_betas_kernel<N><<<3 * nwgB, 64, 0, st>>>(probs, lps, wgtB, nwgB, stage, samples, poses,   \
+                                                     bs.err, bs.pose, bs.ctr, bs.hcap);               \
         break;
         RSC_CASE(4) RSC_CASE(5) RSC_CASE(6)
 #undef RSC_CASE

@@ -206,8 +206,10 @@ struct rsc_context {
     bool direct_counts = true;  // env RSC_DIRECT_COUNTS=0 restores the HBM buffer + D2H copy
     bool fused_refine = true;   // env RSC_FUSED_REFINE=0: the replay's Refine always as its own launch
     bool dma_upload = false;    // env RSC_DMA_UPLOAD=1: descriptors by hipMemcpyAsync instead of the copy kernel
-    int eig_rows_max_wgs = 0;   // env RSC_EIG_ROWS=W: eigen stage in the rows form when it has <= W workgroups (A/B, off)
-    int betas_uniform_max = 0;  // env RSC_BETAS_UNIFORM=H: one hypothesis per betas wave when a round has <= H hypotheses (A/B, off)
+    // eigen stage in the rows form when it has <= W workgroups (small, latency-bound launches such as
+    // one relocalization event: 125 -> 99 us, profiles/r05/bench_latency_forms_ab_r5b.json); env
+    // RSC_EIG_ROWS=W or rsc_context_set_eig_rows overrides (0: lane pairs always)
+    int eig_rows_max_wgs = kEigRowsDefaultWgs;
     std::chrono::steady_clock::time_point t_entry;
 };
 
@@ -449,12 +451,9 @@ struct HipPnPBackend : PnPBackend {
         std::vector<int>& shape = shape_tl;
         thread_local std::vector<int> key_tl;
         std::vector<int>& key = key_tl;
-        // beta-approximation waves: 64 hypotheses each, or one (wave-uniform chains) for small rounds
-        const int hb = (total <= C->betas_uniform_max) ? 1 : kBetasHyps;
         key.clear();
         key.push_back(count);
         key.push_back(HC);
-        key.push_back(hb);
         for (int i = 0; i < count; ++i) {
             key.push_back(S[i]->mRansacMinSet);
             key.push_back(H[i]);
@@ -464,7 +463,7 @@ struct HipPnPBackend : PnPBackend {
             scan_wgs.clear();
             for (int i = 0; i < count; ++i) {
                 const int g = S[i]->mRansacMinSet - 4;
-                for (int h0 = 0; h0 < H[i]; h0 += hb) solve_wgs[g].push_back(make_int2(i, h0));
+                for (int h0 = 0; h0 < H[i]; h0 += kBetasHyps) solve_wgs[g].push_back(make_int2(i, h0));
                 for (int h0 = 0; h0 < H[i]; h0 += kEigHyps) quad_wgs[g].push_back(make_int2(i, h0));
                 for (int h0 = 0; h0 < H[i]; h0 += HC)
                     scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
@@ -524,7 +523,7 @@ struct HipPnPBackend : PnPBackend {
                                           reinterpret_cast<const int2*>(base + o_solve[g]), dprobs, dlps,
                                           C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p, bs, C->stream,
                                           eb, C->timing ? C->ev[7 + 2 * g] : nullptr,
-                                          (int)quad_wgs[g].size() <= C->eig_rows_max_wgs, hb));
+                                          (int)quad_wgs[g].size() <= C->eig_rows_max_wgs));
             first_group = false;
         }
         timing_begin(C, 1);
@@ -1159,7 +1158,6 @@ int rsc_context_create(int device, rsc_context** out) {
     if (const char* m = std::getenv("RSC_FUSED_REFINE")) C->fused_refine = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_DMA_UPLOAD")) C->dma_upload = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_EIG_ROWS")) C->eig_rows_max_wgs = std::max(0, std::atoi(m));
-    if (const char* m = std::getenv("RSC_BETAS_UNIFORM")) C->betas_uniform_max = std::max(0, std::atoi(m));
     C->table.build();
     if (int e = C->d_table.ensure(C->table.T.size())) return e;
     RSC_HIP(hipMemcpy(C->d_table.p, C->table.T.data(), C->table.T.size() * 4, hipMemcpyHostToDevice));
@@ -1196,12 +1194,6 @@ int rsc_context_synchronize(rsc_context* C) {
 int rsc_context_enable_timing(rsc_context* C, int enable) {
     if (!C) return RSC_ERR_ARG;
     C->timing = enable != 0;
-    return RSC_OK;
-}
-
-int rsc_context_set_betas_uniform(rsc_context* C, int max_hypotheses) {
-    if (!C || max_hypotheses < 0) return RSC_ERR_ARG;
-    C->betas_uniform_max = max_hypotheses;
     return RSC_OK;
 }
 

@@ -132,11 +132,13 @@ struct BetasScratch {
 // case (tools/latency_ab.py, profiles/r03/latency_ab_r3_c.txt): the stage time is not the union of
 // a wave's hypotheses' chains but the per-wave latency, which more, narrower waves do not shorten.
 constexpr int kBetasHyps = 64;
+// Default eigen-stage form switch (rsc_context_set_eig_rows): launches of at most this many 20-hypothesis
+// workgroups run the rows form.
+constexpr int kEigRowsDefaultWgs = 64;
 hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, const int2* wgtB,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
-                                  hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr, bool eig_rows = false,
-                                  int betas_hb = kBetasHyps);
+                                  hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr, bool eig_rows = false);
 // counts: where the host reads them (pinned memory or HBM); counts_dev (nullable): an HBM copy for
 // pnp_select_refine_kernel.
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,

@@ -608,18 +608,14 @@ __device__ __forceinline__ void pnp_eig_rows_body(const DevPnP* __restrict__ pro
 }
 
 // Eigenvectors read from the stage record in global memory (stride 1), L + rho in LDS
-// (element-major across the wave: stride 64; stride 1 for the uniform form, where every lane of
-// the wave holds the same hypothesis and writes the same values).
-template <int ST = 64>
+// (element-major across the wave).
 struct StageEvView {
     const double* evp;
     double* Lp;
     RSC_HD double ev(int r, int c) const { return evp[r * 4 + c]; }
-    RSC_HD double& L(int i, int j) const { return Lp[(i * 10 + j) * ST]; }
-    RSC_HD double& rho(int i) const { return Lp[(60 + i) * ST]; }
+    RSC_HD double& L(int i, int j) const { return Lp[(i * 10 + j) * 64]; }
+    RSC_HD double& rho(int i) const { return Lp[(60 + i) * 64]; }
 };
-// pnp_betas_wave_body LDS of the uniform form (hb = 1): one L + rho.
-constexpr int kBetasUniformSmemDoubles = 66;
 
 // Block -> (64-hypothesis group, approximation) of pnp_betas_kernel: the three waves of a group are
 // blocks b, b+8, b+16 of a run of 24 (one L2: blocks b and b+8 share an XCD), so the group keeps
@@ -646,11 +642,7 @@ RSC_HD void betas_block(int b, int ngroups, int& g, int& apx) {
 // workgroup visibility).  It resets the counter, so every launch starts from zero.
 // hb: hypotheses per wave (64 for large rounds; fewer for small ones, so a wave carries the union
 // of fewer data-dependent chains): lanes >= hb mirror lane % hb (same control flow, no writes).
-// UNIFORM (hb = 1, small launches such as one relocalization event): every lane of the wave runs
-// the same hypothesis' chain — identical values, so every data-dependent branch is wave-uniform and
-// compiles to a scalar branch instead of an exec-mask region holding both sides (the Refine's
-// finding, DESIGN.md §4: about twice as fast per chain), and the L + rho slab shrinks to 66 doubles.
-template <int NS, bool UNIFORM = false>
+template <int NS>
 __device__ __forceinline__ void pnp_betas_wave_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
                                                     const int2* __restrict__ wg_table, int ngroups, int hb,
                                                     const double* __restrict__ stage,
@@ -668,7 +660,7 @@ __device__ __forceinline__ void pnp_betas_wave_body(const DevPnP* __restrict__ p
     const DevPnP& P = probs[lp.prob];
     const size_t rec = (size_t)(lp.out0 + h);
     const double* in = stage + rec * kStageDoubles;
-    const StageEvView<UNIFORM ? 1 : 64> V{in + kStEv, UNIFORM ? smem : smem + lane};
+    const StageEvView V{in + kStEv, smem + lane};
     compute_L_6x10(V);
     {
         double cws[4][3];

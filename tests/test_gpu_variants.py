@@ -1,28 +1,19 @@
-"""GPU parity of the product's A/B variants that are off by default — they must give the default
-path's bits, so each is checked against the oracle exactly like the default path.
+"""GPU parity of the product's alternative kernel forms forced on EVERY launch — each must give the
+default path's bits, so each is checked against the oracle exactly like the default path.
 
 * the eigen stage in the Refine's rows form (`rsc_context_set_eig_rows`, rsc_quad.h
-  pnp_eig_rows_body: a 12-lane group per hypothesis, Q rows in VGPRs), meant for small
-  latency-bound launches such as one relocalization event: every hypothesis of exhaustive batches
-  (min sets 4..6, a planar scene for the NaN path), and a relocalization event stream.
-
-* the beta-approximation stage with one hypothesis per wave (`rsc_context_set_betas_uniform`,
-  pnp_betas_uniform_kernel: the chain wave-uniform), for the same small launches: every hypothesis of
-  exhaustive batches (min sets 4..6, planar NaN path), alone and combined with the rows form, and a
-  relocalization event stream.
-
-Opt-in (RSC_TEST_VARIANTS=1): a variant that has not yet run on hardware is not put in the path of
-the default suite."""
-import os
-
+  pnp_eig_rows_body: a 12-lane group per hypothesis, Q rows in VGPRs) — the default for small
+  launches since round 5 (<= 64 workgroups), forced here onto large ones too: every hypothesis of
+  exhaustive batches (min sets 4..6, a planar scene for the NaN path), and a relocalization event
+  stream; and the lane-pair form forced onto small launches (set_eig_rows(0)).
+First run on hardware in round 5 (profiles/r05/gpu_tests_variants_r5b.txt)."""
 import numpy as np
 import pytest
 
 import oracle_lib as ol
 from rsc import synth
 
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get("RSC_TEST_VARIANTS") != "1", reason="opt-in: RSC_TEST_VARIANTS=1")]
+pytestmark = pytest.mark.gpu
 
 
 def _nan_equal(a, b):
@@ -32,24 +23,17 @@ def _nan_equal(a, b):
     return np.array_equal(na, nb) and np.array_equal(a.view(np.uint32)[~na], b.view(np.uint32)[~nb])
 
 
-def _rows_ctx(rows=True, uniform=False):
+def _rows_ctx(rows=True):
     from rsc import engine
     c = engine.Context(0)
-    if rows:
-        c.set_eig_rows(1 << 20)  # every launch in the rows form
-    if uniform:
-        c.set_betas_uniform(1 << 20)  # every launch with one hypothesis per betas wave
+    c.set_eig_rows(1 << 20 if rows else 0)  # every launch in the rows form / in lane pairs
     return c
 
 
-FORMS = [(True, False), (False, True), (True, True)]
-
-
 @pytest.mark.parametrize("ms", [4, 5, 6])
-@pytest.mark.parametrize("rows,uniform", FORMS)
-def test_eig_rows_every_hypothesis(ms, rows, uniform):
+def test_eig_rows_every_hypothesis(ms):
     from rsc import engine
-    c = _rows_ctx(rows, uniform)
+    c = _rows_ctx()
     rng = np.random.default_rng(900 + ms)
     scenes = [synth.make_pnp_scene(rng, 700, 0.4), synth.make_pnp_scene(rng, 1900, 0.35),
               synth.make_planar_pnp_scene(rng, 500, 0.4, "floor"), synth.make_pnp_scene(rng, 230, 0.45)]
@@ -75,11 +59,11 @@ def test_eig_rows_every_hypothesis(ms, rows, uniform):
     c.close()
 
 
-@pytest.mark.parametrize("rows,uniform", FORMS)
-def test_eig_rows_reloc_events(rows, uniform):
+@pytest.mark.parametrize("rows", [True, False])
+def test_eig_rows_reloc_events(rows):
     from rsc import engine, events as rev
     import events_oracle as eo
-    c = _rows_ctx(rows, uniform)
+    c = _rows_ctx(rows)
     evs = [ev for ev in rev.make_event_stream(seed=23, n_reloc=8, n_loop=0) if ev.kind == "reloc"]
     eb = engine.EventBatch([[engine.PnPSolver(c, x, s) for x, s in zip(rev.event_inputs(ev), ev.seeds)] for ev in evs])
     eb.batch.set_ransac_parameters(*rev.RELOC_PARAMS)
