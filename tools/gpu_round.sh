@@ -43,7 +43,6 @@ if [ -n "$VARIANTS" ]; then
   # off-default A/B variants: their parity tests, the single-event A/B of the rows-form
   # eigen stage, the chase-only sink variants, and the VGPR-row chase library on the headline
   cd $GRAFT_REPO_ROOT
-  RSC_TEST_VARIANTS=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_variants.py -x -v --timeout 180 --timeout-method thread > $OUT/tests_variants.txt 2>&1
   timeout -k 10 300 python bench.py --no-cpu --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --eig-rows-ab > $OUT/bench_eig_rows_ab.json 2> $OUT/bench_eig_rows_ab.err
   timeout -k 10 120 tools/bin/qr_bench > $OUT/qr_bench.txt 2>&1
   for v in a b a b; do
@@ -62,6 +61,11 @@ if [ -n "$PLANAR" ]; then
   cd $GRAFT_REPO_ROOT
   timeout -k 10 200 python tools/planar_ab.py $OUT/planar_ab_exit.json exit > $OUT/planar_exit.log 2>&1
   RSC_LIBRSC=tools/bin/librsc_nonanexit.so timeout -k 10 200 python tools/planar_ab.py $OUT/planar_ab_noexit.json noexit > $OUT/planar_noexit.log 2>&1
+fi
+if [ -n "$PROBE" ]; then
+  # per-phase device clocks of the Refine kernel (stamped build: make -C tools stamps_lib)
+  cd $GRAFT_REPO_ROOT
+  RSC_LIBRSC=tools/bin/librsc_stamps.so timeout -k 10 200 python tools/refine_probe.py > $OUT/refine_probe.txt 2>&1
 fi
 if [ -n "$GPUS2" ]; then
   cd $GRAFT_REPO_ROOT
