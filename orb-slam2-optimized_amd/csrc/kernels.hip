@@ -369,36 +369,47 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
     __threadfence_block();
     __syncthreads();
     refine_stamp(2);
-    // 3. MtM lower triangle, one entry per thread, each folded over the 2*nr rows in order.  The
-    // rows of M are staged through LDS (wbuf, 195 rows x 12 at a time) by all 256 threads, so the
-    // 78 folding threads read operands from LDS instead of recomputing them from global memory.
+    // 3. MtM lower triangle, one entry per folding thread, each folded over the 2*nr rows in order.
+    // The rows of M are staged through LDS in chunks of 195 rows x 12, double-buffered: lanes 0..38
+    // of waves 0 and 1 fold chunk c (the 78 entries) while waves 2 and 3 stage chunk c + 1, so the
+    // fold's dependent additions no longer wait for the staging (one barrier per chunk).
     {
-        double* Mc = &wbuf[0][0];
+        __shared__ __attribute__((aligned(16))) double mtm_stage2[(4 * kFoldStride * 9 / 12) * 12];
+        auto chunk_buf = [&](int c) { return (c & 1) ? mtm_stage2 : &wbuf[0][0]; };
         constexpr int kRows = (4 * kFoldStride * 9) / 12;
-        int a = 0, b = tid;
-        while (b > a) { b -= a + 1; ++a; }  // tid -> (a,b) with b <= a, row-major lower triangle
+        const bool folder = wave < 2 && lane < 39;
+        int a = 0, b = wave * 39 + lane;
+        while (b > a) { b -= a + 1; ++a; }  // fold id -> (a,b) with b <= a, row-major lower triangle
+        const int nchunks = (2 * nr + kRows - 1) / kRows;
+        auto stage = [&](int c, int t0, int nt) {
+            const int r0 = c * kRows, m = min(kRows, 2 * nr - r0);
+            double* dst = chunk_buf(c);
+            for (int e = t0; e < m * 12; e += nt) dst[e] = M_entry(st, K, r0 + e / 12, e % 12);
+        };
+        if (nchunks > 0) stage(0, tid, 256);
+        __syncthreads();
         double s = 0.0;
-        for (int r0 = 0; r0 < 2 * nr; r0 += kRows) {
-            const int m = min(kRows, 2 * nr - r0);
-            __syncthreads();  // the previous chunk has been folded
-            for (int e = tid; e < m * 12; e += 256) Mc[e] = M_entry(st, K, r0 + e / 12, e % 12);
-            __syncthreads();
-            if (tid < 78) {
+        for (int c = 0; c < nchunks; ++c) {
+            if (wave >= 2 && c + 1 < nchunks) stage(c + 1, tid - 128, 128);
+            if (folder) {
+                const double* M = chunk_buf(c);
+                const int m = min(kRows, 2 * nr - c * kRows);
                 int r = 0;
-                if (r0 == 0) {
-                    s = Mc[a] * Mc[b];
+                if (c == 0) {
+                    s = M[a] * M[b];
                     r = 1;
                 }
                 // 8 rows' operands loaded before their products and ordered additions
                 for (; r + 8 <= m; r += 8) {
                     double x[8], y[8];
-                    RSC_UNROLL for (int k = 0; k < 8; ++k) { x[k] = Mc[(r + k) * 12 + a]; y[k] = Mc[(r + k) * 12 + b]; }
+                    RSC_UNROLL for (int k = 0; k < 8; ++k) { x[k] = M[(r + k) * 12 + a]; y[k] = M[(r + k) * 12 + b]; }
                     RSC_UNROLL for (int k = 0; k < 8; ++k) s = s + x[k] * y[k];
                 }
-                for (; r < m; ++r) s = s + Mc[r * 12 + a] * Mc[r * 12 + b];
+                for (; r < m; ++r) s = s + M[r * 12 + a] * M[r * 12 + b];
             }
+            __syncthreads();  // chunk c folded, chunk c + 1 staged
         }
-        if (tid < 78) S.at(a, b) = s;
+        if (folder) S.at(a, b) = s;
     }
     __syncthreads();
     refine_stamp(3);
