@@ -219,7 +219,8 @@ struct GroupLdsRows {
 };
 
 // The group's own rows of Q held in VGPRs (Qr[j] = row L*j + q): the same rotation as
-// GroupLdsRows without the LDS round trip (A/B variant, RSC_EIG_REGROWS; tools/qr_bench sink 2).
+// GroupLdsRows without the LDS round trip (the hypothesis eigen stage's sink since round 5;
+// tools/qr_bench sink 2).
 template <int L>
 struct GroupRegRows {
     static constexpr int RJ = 12 / L;
@@ -496,10 +497,12 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
     }
 
     // ---- D: implicit symmetric QR, rotations applied to the own rows ----
-    // Sweep form: the own rows of Q stay in LDS (T, row-major), so the rotations' read-modify-
-    // writes are off the Givens chase's dependency chain.  (The event and split-chase forms of the
-    // QR, tools/qr_events.h, are bit-identical and measured slower on gfx950)
-#ifdef RSC_EIG_REGROWS
+    // Sweep form with the own rows of Q in VGPRs (round 5: eigen stage 132 -> 119-122 us per config-2
+    // launch against the rows in LDS, profiles/r05/regrows_ab_r5c.json; 256 VGPRs + AGPRs, no
+    // scratch).  RSC_EIG_LDSROWS builds the LDS-row form for A/B (tools/Makefile ldsrows_lib).  (The
+    // event and split-chase forms of the QR, tools/qr_events.h, are bit-identical and measured slower
+    // on gfx950)
+#ifndef RSC_EIG_LDSROWS
     {
         int perm[12];
         double Qr[RJ][12];

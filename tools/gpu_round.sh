@@ -2,7 +2,7 @@
 # GPU-box round script: parity tests, headline bench (with CPU baseline), rocprofv3 kernel stats of
 # the same bench command, and (PMC=1) two PMC passes (FETCH_SIZE, WRITE_SIZE) of the PnP section for
 # the HBM traffic per launch; VARIANTS=1 / PLANAR=1 the round-4 A/B measurements (build first:
-# make -C tools qr_bench nonan_lib regrows_lib, cp tools/build/qr_bench tools/bin/).  Outputs under gpurun_out/$TAG/.  Every step has its own time limit and
+# make -C tools qr_bench nonan_lib ldsrows_lib stamps_lib, cp tools/build/qr_bench tools/bin/).  Outputs under gpurun_out/$TAG/.  Every step has its own time limit and
 # the script stops at the first failure.
 set -e
 TAG=${TAG:-run}
@@ -46,8 +46,8 @@ if [ -n "$VARIANTS" ]; then
   timeout -k 10 300 python bench.py --no-cpu --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --eig-rows-ab > $OUT/bench_eig_rows_ab.json 2> $OUT/bench_eig_rows_ab.err
   timeout -k 10 120 tools/bin/qr_bench > $OUT/qr_bench.txt 2>&1
   for v in a b a b; do
-    if [ $v = a ]; then L=orb-slam2-optimized_amd/lib/librsc.so; else L=tools/bin/librsc_regrows.so; fi
-    RSC_LIBRSC=$L timeout -k 10 200 python bench.py --only-headline --no-cpu >> $OUT/regrows_ab_$v.jsonl 2>> $OUT/regrows_ab.err
+    if [ $v = a ]; then L=orb-slam2-optimized_amd/lib/librsc.so; else L=tools/bin/librsc_ldsrows.so; fi
+    RSC_LIBRSC=$L timeout -k 10 200 python bench.py --only-headline --no-cpu >> $OUT/ldsrows_ab_$v.jsonl 2>> $OUT/ldsrows_ab.err
   done
   # the small-launch forms on the whole config-2 batch (rows-form eigen stage; uniform betas is
   # pointless there: 57,600 waves)
