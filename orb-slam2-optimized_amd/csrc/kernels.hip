@@ -212,20 +212,25 @@ __global__ __launch_bounds__(256) void pnp_eig_rows_kernel(const DevPnP* __restr
     pnp_eig_rows_body<NS, kRefineEigLanes>(probs, lps, wg_table, rng_T, stage, samples, smem, [] { wave_lds_sync(); });
 }
 
-// Ordered sums of K columns of per-row terms over rows [0, count), by one wave.  term(i, t[K]).
+// Ordered sums of K columns of per-row terms over rows [0, count), by one wave: row i's operands are
+// v = load(i) (global loads only), its terms term(i, v, t[K]).  The next block's loads are issued
+// before the current block is folded, so their latency overlaps the fold's dependent additions.
 // from_zero: s = ((0.0 + t0) + t1) + ... (loops starting from 0.0), else s = (t0 + t1) + ...
 // Returns column k's sum in lane k (k < K); buf holds kFoldStride*K doubles of this wave.
-template <int K, class Term>
-__device__ __forceinline__ double wave_ordered_sum(int count, double* buf, bool from_zero, Term&& term) {
+template <int K, class Load, class Term>
+__device__ __forceinline__ double wave_ordered_sum(int count, double* buf, bool from_zero, Load&& load, Term&& term) {
     const int lane = threadIdx.x & 63;
     double s = 0.0;
+    auto next = load(min(lane, max(count - 1, 0)));
     for (int base = 0; base < count; base += 64) {
         const int i = base + lane;
+        const auto v = next;
         if (i < count) {
             double t[K];
-            term(i, t);
+            term(i, v, t);
             RSC_UNROLL for (int k = 0; k < K; ++k) buf[k * kFoldStride + lane] = t[k];
         }
+        if (base + 64 < count) next = load(min(i + 64, count - 1));  // in flight during the fold
         wave_lds_sync();
         if (lane < K) {
             const int m = min(64, count - base);
@@ -238,6 +243,11 @@ __device__ __forceinline__ double wave_ordered_sum(int count, double* buf, bool 
     }
     return s;
 }
+
+// Operands of one EPnP row for the Refine's ordered sums (global loads; the unused ones are dead).
+struct RefRow {
+    double a[4], p[3], u[2];
+};
 
 __device__ __forceinline__ void refine_stamp(int slot) {
     if (RSC_REFINE_STAMPS && blockIdx.x < 64 && threadIdx.x == 0) g_refine_stamps[blockIdx.x][slot] = wall_clock64();
@@ -319,15 +329,16 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
     LaneMat S{slab, 1};
     // 2. choose_control_points + barycentric coordinates (PnPsolver.cpp:296-343), wave 0
     if (wave == 0) {
-        const double cs = wave_ordered_sum<3>(rows, buf, false, [&](int i, double (&t)[3]) {
-            t[0] = pws[3 * i]; t[1] = pws[3 * i + 1]; t[2] = pws[3 * i + 2];
+        auto ld_p = [&](int i) { return RefRow{{0, 0, 0, 0}, {pws[3 * i], pws[3 * i + 1], pws[3 * i + 2]}, {0, 0}}; };
+        const double cs = wave_ordered_sum<3>(rows, buf, false, ld_p, [&](int, const RefRow& v, double (&t)[3]) {
+            t[0] = v.p[0]; t[1] = v.p[1]; t[2] = v.p[2];
         });
         if (lane < 3) cen_sh[lane] = cs / nr;
         wave_lds_sync();
         const double c0 = cen_sh[0], c1 = cen_sh[1], c2 = cen_sh[2];
         // A[a][b], (a,b) in (00 01 02 11 12 22); A[b][a] is the same sum of the same products
-        const double as = wave_ordered_sum<6>(nr, buf, false, [&](int i, double (&t)[6]) {
-            const double d0 = pws[3 * i] - c0, d1 = pws[3 * i + 1] - c1, d2 = pws[3 * i + 2] - c2;
+        const double as = wave_ordered_sum<6>(nr, buf, false, ld_p, [&](int, const RefRow& v, double (&t)[6]) {
+            const double d0 = v.p[0] - c0, d1 = v.p[1] - c1, d2 = v.p[2] - c2;
             t[0] = d0 * d0; t[1] = d0 * d1; t[2] = d0 * d2; t[3] = d1 * d1; t[4] = d1 * d2; t[5] = d2 * d2;
         });
         if (lane < 6) buf[lane] = as;
@@ -458,19 +469,24 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
             RSC_UNROLL for (int c = 0; c < 3; ++c) ccs[i][c] = ccs_sh[wave][3 * i + c];
         const double pw0[3] = {cws_sh[0], cws_sh[1], cws_sh[2]};
         // pc0 over all allocated rows (stale rows use their stale alphas, Q6)
-        const double ps = wave_ordered_sum<3>(rows, buf, false, [&](int i, double (&t)[3]) {
-            const double a[4] = {als[4 * i], als[4 * i + 1], als[4 * i + 2], als[4 * i + 3]};
-            RSC_UNROLL for (int c = 0; c < 3; ++c) t[c] = pcs_of(a, ccs, c);
+        auto ld_a = [&](int i) {
+            return RefRow{{als[4 * i], als[4 * i + 1], als[4 * i + 2], als[4 * i + 3]}, {0, 0, 0}, {0, 0}};
+        };
+        const double ps = wave_ordered_sum<3>(rows, buf, false, ld_a, [&](int, const RefRow& v, double (&t)[3]) {
+            RSC_UNROLL for (int c = 0; c < 3; ++c) t[c] = pcs_of(v.a, ccs, c);
         });
         __shared__ double pc0_sh[3][3];
         if (lane < 3) pc0_sh[wave][lane] = ps / nr;
         wave_lds_sync();
         refine_wave_stamp(wave, 1);
         const double pc0[3] = {pc0_sh[wave][0], pc0_sh[wave][1], pc0_sh[wave][2]};
-        const double ms = wave_ordered_sum<9>(nr, buf, true, [&](int i, double (&t)[9]) {
-            const double al4[4] = {als[4 * i], als[4 * i + 1], als[4 * i + 2], als[4 * i + 3]};
+        auto ld_ap = [&](int i) {
+            return RefRow{{als[4 * i], als[4 * i + 1], als[4 * i + 2], als[4 * i + 3]},
+                          {pws[3 * i], pws[3 * i + 1], pws[3 * i + 2]}, {0, 0}};
+        };
+        const double ms = wave_ordered_sum<9>(nr, buf, true, ld_ap, [&](int, const RefRow& v, double (&t)[9]) {
             double a[3], b[3];
-            RSC_UNROLL for (int c = 0; c < 3; ++c) { a[c] = pcs_of(al4, ccs, c) - pc0[c]; b[c] = pws[3 * i + c] - pw0[c]; }
+            RSC_UNROLL for (int c = 0; c < 3; ++c) { a[c] = pcs_of(v.a, ccs, c) - pc0[c]; b[c] = v.p[c] - pw0[c]; }
             RSC_UNROLL for (int r = 0; r < 3; ++r)
                 RSC_UNROLL for (int c = 0; c < 3; ++c) t[3 * r + c] = a[r] * b[c];
         });
@@ -491,8 +507,11 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
         double R[3][3], t[3];
         RSC_UNROLL for (int k = 0; k < 9; ++k) R[k / 3][k % 3] = rt_sh[wave][k];
         RSC_UNROLL for (int k = 0; k < 3; ++k) t[k] = rt_sh[wave][9 + k];
-        const double es = wave_ordered_sum<1>(nr, buf, true, [&](int i, double (&tt)[1]) {
-            tt[0] = reproj_term(R, t, K, pws[3 * i], pws[3 * i + 1], pws[3 * i + 2], us[2 * i], us[2 * i + 1]);
+        auto ld_pu = [&](int i) {
+            return RefRow{{0, 0, 0, 0}, {pws[3 * i], pws[3 * i + 1], pws[3 * i + 2]}, {us[2 * i], us[2 * i + 1]}};
+        };
+        const double es = wave_ordered_sum<1>(nr, buf, true, ld_pu, [&](int, const RefRow& v, double (&tt)[1]) {
+            tt[0] = reproj_term(R, t, K, v.p[0], v.p[1], v.p[2], v.u[0], v.u[1]);
         });
         if (lane == 0) {
             RSC_UNROLL for (int k = 0; k < 12; ++k) res_sh[wave][k] = rt_sh[wave][k];

@@ -65,7 +65,7 @@ fi
 if [ -n "$PROBE" ]; then
   # per-phase device clocks of the Refine kernel (stamped build: make -C tools stamps_lib)
   cd $GRAFT_REPO_ROOT
-  RSC_LIBRSC=tools/bin/librsc_stamps.so timeout -k 10 200 python tools/refine_probe.py > $OUT/refine_probe.txt 2>&1
+  RSC_LIBRSC=tools/bin/librsc_stamps.so timeout -k 10 200 python tools/refine_probe.py event > $OUT/refine_probe_event.txt 2>&1
 fi
 if [ -n "$GPUS2" ]; then
   cd $GRAFT_REPO_ROOT

@@ -11,7 +11,18 @@ import numpy as np  # noqa: E402
 from rsc import engine, events as rev  # noqa: E402
 
 ctx = engine.Context(0)
-evs = [ev for ev in rev.make_event_stream() if ev.kind == "reloc"]
+if len(sys.argv) > 1 and sys.argv[1] == "event":
+    # the bench's single relocalization event (bench.py latency_event: C = 15, N ~ U[300, 900]): the
+    # Refine jobs of ONE Tracking::Relocalization call, the latency case
+    rng = np.random.default_rng(4242)
+    C = 15
+    sizes = [int(x) for x in rng.integers(300, 901, size=C)]
+    ratios = [float(x) for x in rng.choice([0.05, 0.2, 0.6, 0.8], size=C, p=[0.5, 0.2, 0.15, 0.15])]
+    evs = [rev.Event("reloc", 100000, sizes, ratios, [7 + c for c in range(C)])]
+    print("single relocalization event (bench latency_event)")
+else:
+    evs = [ev for ev in rev.make_event_stream() if ev.kind == "reloc"]
+    print("config-5 stream, the launch with the most Refine jobs")
 solvers = [[engine.PnPSolver(ctx, x, s) for x, s in zip(rev.event_inputs(ev), ev.seeds)] for ev in evs]
 eb = engine.EventBatch(solvers)
 seeds = np.array([s for ev in evs for s in ev.seeds], np.uint32)
@@ -33,3 +44,9 @@ if (st[ok, 8] > 0).all():  # eigen sub-phases (RSC_REFINE_STAMPS builds)
     e = np.diff(np.concatenate([st[ok][:, 3:4], st[ok][:, 8:12], st[ok][:, 4:5]], axis=1), axis=1) / 100.0
     for i, n in enumerate(["tridiag", "accumulate", "QR chase", "eigvecs", "L + rho"]):
         print(f"    eigen/{n:10s} mean {e[:, i].mean():8.1f} us  max {e[:, i].max():8.1f} us")
+if (st[ok, 12] > 0).all():  # beta-approximation waves (refine_wave_stamp: slots 12 + 4 * wave + j)
+    for w in range(3):
+        b = st[ok][:, 12 + 4 * w: 16 + 4 * w]
+        seg = np.diff(np.concatenate([st[ok][:, 4:5], b], axis=1), axis=1) / 100.0
+        print(f"  betas wave {w}: betas+GN+ccs {seg[:, 0].mean():6.1f}  pc0 {seg[:, 1].mean():5.1f}  "
+              f"M+Horn {seg[:, 2].mean():5.1f}  err {seg[:, 3].mean():5.1f} us")
