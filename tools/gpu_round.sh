@@ -62,6 +62,19 @@ if [ -n "$PLANAR" ]; then
   timeout -k 10 200 python tools/planar_ab.py $OUT/planar_ab_exit.json exit > $OUT/planar_exit.log 2>&1
   RSC_LIBRSC=tools/bin/librsc_nonanexit.so timeout -k 10 200 python tools/planar_ab.py $OUT/planar_ab_noexit.json noexit > $OUT/planar_noexit.log 2>&1
 fi
+if [ -n "$LDSAB" ]; then
+  # the eigen chase's own Q rows in VGPRs (product) vs in LDS (RSC_EIG_LDSROWS build), headline only
+  cd $GRAFT_REPO_ROOT
+  for v in a b a b; do
+    if [ $v = a ]; then L=orb-slam2-optimized_amd/lib/librsc.so; else L=tools/bin/librsc_ldsrows.so; fi
+    RSC_LIBRSC=$L timeout -k 10 200 python bench.py --only-headline --no-cpu >> $OUT/ldsrows_ab_$v.jsonl 2>> $OUT/ldsrows_ab.err
+  done
+fi
+if [ -n "$LAT" ]; then
+  # single-event latency with the eigen-form A/B (pairs vs rows)
+  cd $GRAFT_REPO_ROOT
+  timeout -k 10 300 python bench.py --no-cpu --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --eig-rows-ab > $OUT/bench_eig_rows_ab.json 2> $OUT/bench_eig_rows_ab.err
+fi
 if [ -n "$PROBE" ]; then
   # per-phase device clocks of the Refine kernel (stamped build: make -C tools stamps_lib)
   cd $GRAFT_REPO_ROOT
