@@ -381,21 +381,36 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
     __syncthreads();
     refine_stamp(2);
     // 3. MtM lower triangle, one entry per folding thread, each folded over the 2*nr rows in order.
-    // The rows of M are staged through LDS in chunks of 195 rows x 12, double-buffered: lanes 0..38
-    // of waves 0 and 1 fold chunk c (the 78 entries) while waves 2 and 3 stage chunk c + 1, so the
-    // fold's dependent additions no longer wait for the staging (one barrier per chunk).
+    // The rows of M are staged through LDS in chunks of 97 correspondences (194 rows x 12),
+    // double-buffered: lanes 0..38 of waves 0 and 1 fold chunk c (the 78 entries) while waves 2 and 3
+    // stage chunk c + 1, one correspondence (its two rows of M, PnPsolver.cpp:365-377, the values of
+    // M_entry) per thread, so the chunk's operand loads are one round trip (one barrier per chunk).
     {
-        __shared__ __attribute__((aligned(16))) double mtm_stage2[(4 * kFoldStride * 9 / 12) * 12];
+        constexpr int kPairs = (4 * kFoldStride * 9) / 24;  // 97 correspondences per chunk
+        __shared__ __attribute__((aligned(16))) double mtm_stage2[kPairs * 24];
         auto chunk_buf = [&](int c) { return (c & 1) ? mtm_stage2 : &wbuf[0][0]; };
-        constexpr int kRows = (4 * kFoldStride * 9) / 12;
         const bool folder = wave < 2 && lane < 39;
         int a = 0, b = wave * 39 + lane;
         while (b > a) { b -= a + 1; ++a; }  // fold id -> (a,b) with b <= a, row-major lower triangle
-        const int nchunks = (2 * nr + kRows - 1) / kRows;
+        const int nchunks = (nr + kPairs - 1) / kPairs;
         auto stage = [&](int c, int t0, int nt) {
-            const int r0 = c * kRows, m = min(kRows, 2 * nr - r0);
+            const int i0 = c * kPairs, m = min(kPairs, nr - i0);
             double* dst = chunk_buf(c);
-            for (int e = t0; e < m * 12; e += nt) dst[e] = M_entry(st, K, r0 + e / 12, e % 12);
+            for (int t = t0; t < m; t += nt) {
+                const int i = i0 + t;
+                const double al4[4] = {als[4 * i], als[4 * i + 1], als[4 * i + 2], als[4 * i + 3]};
+                const double u0 = us[2 * i], u1 = us[2 * i + 1];
+                double* ev = dst + 24 * t;  // row 2i
+                double* od = ev + 12;       // row 2i + 1
+                RSC_UNROLL for (int j = 0; j < 4; ++j) {
+                    ev[3 * j] = al4[j] * K.fx;
+                    ev[3 * j + 1] = 0.0;
+                    ev[3 * j + 2] = al4[j] * (K.cx - u0);
+                    od[3 * j] = 0.0;
+                    od[3 * j + 1] = al4[j] * K.fy;
+                    od[3 * j + 2] = al4[j] * (K.cy - u1);
+                }
+            }
         };
         if (nchunks > 0) stage(0, tid, 256);
         __syncthreads();
@@ -404,7 +419,7 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
             if (wave >= 2 && c + 1 < nchunks) stage(c + 1, tid - 128, 128);
             if (folder) {
                 const double* M = chunk_buf(c);
-                const int m = min(kRows, 2 * nr - c * kRows);
+                const int m = 2 * min(kPairs, nr - c * kPairs);
                 int r = 0;
                 if (c == 0) {
                     s = M[a] * M[b];
