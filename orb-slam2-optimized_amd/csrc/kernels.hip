@@ -952,6 +952,18 @@ hipError_t launch_copy_bytes(const void* src, void* dst, size_t n, hipStream_t s
     return hipGetLastError();
 }
 
+// Completion flag of a speculation round for the host's spin wait (rsc_api.cpp stream_wait): one
+// lane stores the round's sequence number to pinned host memory with a system-scope release once
+// every earlier operation of the stream has finished (a vector store; no scalar-cache writes).
+__global__ __launch_bounds__(64) void signal_kernel(uint32_t* flag, uint32_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_signal(uint32_t* host_flag, uint32_t value, hipStream_t st) {
+    signal_kernel<<<1, 64, 0, st>>>(host_flag, value);
+    return hipGetLastError();
+}
+
 hipError_t launch_upload16(const void* host_src, void* dev_dst, size_t n16, hipStream_t st) {
     if (n16 == 0) return hipSuccess;
     const unsigned blocks = (unsigned)((n16 + 255) / 256);

@@ -210,6 +210,12 @@ struct rsc_context {
     // one relocalization event: 125 -> 99 us, profiles/r05/bench_latency_forms_ab_r5b.json); env
     // RSC_EIG_ROWS=W or rsc_context_set_eig_rows overrides (0: lane pairs always)
     int eig_rows_max_wgs = kEigRowsDefaultWgs;
+    // host wait for a speculation round's results: spin on a completion flag in pinned host memory
+    // (written by signal_kernel after the round) instead of hipStreamSynchronize's wake-up; env
+    // RSC_SPIN_WAIT=0/1 (stream_wait)
+    bool spin_wait = false;
+    uint32_t* h_flag = nullptr;
+    uint32_t flag_seq = 0;
     std::chrono::steady_clock::time_point t_entry;
 };
 
@@ -343,6 +349,28 @@ int counts_target(rsc_context* C, int total, int32_t** dst) {
     }
     if (int e = C->d_counts.ensure((size_t)total)) return e;
     *dst = C->d_counts.p;
+    return 0;
+}
+
+// Wait until everything enqueued on the context stream has finished.  With spin_wait a one-lane
+// kernel stores a sequence number into pinned host memory behind the round and the host polls it
+// (results written to pinned memory by the round's kernels are visible once the flag is: stream
+// order + the flag's system-scope release); after 20 ms of polling it falls back to
+// hipStreamSynchronize, which also reports a failed kernel.
+int stream_wait(rsc_context* C) {
+    if (!C->spin_wait || !C->h_flag || C->timing) {  // the timing pass reads events: a full sync
+        RSC_HIP(hipStreamSynchronize(C->stream));
+        return 0;
+    }
+    const uint32_t want = ++C->flag_seq;
+    RSC_HIP(launch_signal(C->h_flag, want, C->stream));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 1;; ++it) {
+        if (__atomic_load_n(C->h_flag, __ATOMIC_ACQUIRE) == want) return 0;
+        __builtin_ia32_pause();
+        if ((it & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+    }
+    RSC_HIP(hipStreamSynchronize(C->stream));
     return 0;
 }
 
@@ -542,7 +570,7 @@ struct HipPnPBackend : PnPBackend {
         if (!C->direct_counts)
             RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
         host_mark(C, 1);
-        RSC_HIP(hipStreamSynchronize(C->stream));
+        if (int e = stream_wait(C)) return e;
         host_mark(C, 2);
         if (C->timing) {
             float a = 0, s = 0;
@@ -794,7 +822,7 @@ struct HipSim3Backend : Sim3Backend {
         }
         if (!C->direct_counts)
             RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
-        RSC_HIP(hipStreamSynchronize(C->stream));
+        if (int e = stream_wait(C)) return e;
         if (C->timing) {
             float a = 0, s = 0;
             (void)hipEventElapsedTime(&a, C->ev[0], C->ev[1]);
@@ -939,7 +967,7 @@ struct HipMLBackend : MLBackend {
         timing_begin(C, 2);
         if (!C->direct_counts)
             RSC_HIP(hipMemcpyAsync(C->h_counts.p, C->d_counts.p, (size_t)total * 4, hipMemcpyDeviceToHost, C->stream));
-        RSC_HIP(hipStreamSynchronize(C->stream));
+        if (int e = stream_wait(C)) return e;
         if (C->timing) {
             float a = 0, sc = 0;
             (void)hipEventElapsedTime(&a, C->ev[0], C->ev[1]);
@@ -1158,6 +1186,13 @@ int rsc_context_create(int device, rsc_context** out) {
     if (const char* m = std::getenv("RSC_FUSED_REFINE")) C->fused_refine = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_DMA_UPLOAD")) C->dma_upload = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_EIG_ROWS")) C->eig_rows_max_wgs = std::max(0, std::atoi(m));
+    if (const char* m = std::getenv("RSC_SPIN_WAIT")) C->spin_wait = std::strcmp(m, "0") != 0;
+    {
+        void* f = nullptr;
+        RSC_HIP(hipHostMalloc(&f, 64, hipHostMallocCoherent));
+        C->h_flag = static_cast<uint32_t*>(f);
+        *C->h_flag = 0;
+    }
     C->table.build();
     if (int e = C->d_table.ensure(C->table.T.size())) return e;
     RSC_HIP(hipMemcpy(C->d_table.p, C->table.T.data(), C->table.T.size() * 4, hipMemcpyHostToDevice));
@@ -1170,6 +1205,7 @@ void rsc_context_destroy(rsc_context* C) {
     if (!C) return;
     (void)hipSetDevice(C->device);
     if (C->stream) (void)hipStreamSynchronize(C->stream);
+    if (C->h_flag) (void)hipHostFree(C->h_flag);
     for (auto& e : C->ev)
         if (e) (void)hipEventDestroy(e);
     if (C->own_stream && C->stream) (void)hipStreamDestroy(C->stream);

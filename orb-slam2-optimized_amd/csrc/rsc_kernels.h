@@ -102,6 +102,7 @@ hipError_t launch_selftest_math(int fn, const double* x, int n, double* out, hip
 // Descriptor upload of a round: n16 16-byte words from pinned host memory (read over PCIe by the
 // kernel) into device memory, in stream order with the launches that read them.
 hipError_t launch_upload16(const void* host_src, void* dev_dst, size_t n16, hipStream_t st);
+hipError_t launch_signal(uint32_t* host_flag, uint32_t value, hipStream_t st);
 // Any-size copy between pinned host memory and HBM by a kernel (latency-bound small transfers of
 // the KeyFrameDatabase queries: no DMA start-up or engine hand-off).
 hipError_t launch_copy_bytes(const void* src, void* dst, size_t n, hipStream_t st);
