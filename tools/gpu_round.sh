@@ -75,6 +75,15 @@ if [ -n "$LAT" ]; then
   cd $GRAFT_REPO_ROOT
   timeout -k 10 300 python bench.py --no-cpu --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --eig-rows-ab > $OUT/bench_eig_rows_ab.json 2> $OUT/bench_eig_rows_ab.err
 fi
+if [ -n "$SPINAB" ]; then
+  # host wait for a round: hipStreamSynchronize (0) vs spin on a pinned completion flag (1)
+  cd $GRAFT_REPO_ROOT
+  for v in 0 1 0 1; do
+    RSC_SPIN_WAIT=$v timeout -k 10 200 python bench.py --only-headline --no-cpu >> $OUT/spin_ab_$v.jsonl 2>> $OUT/spin_ab.err
+    RSC_SPIN_WAIT=$v TIMING=0 timeout -k 10 120 python tools/host_overhead.py >> $OUT/host_overhead_spin$v.txt 2>&1
+    RSC_SPIN_WAIT=$v timeout -k 10 300 python bench.py --no-cpu --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --no-mlpnp --no-events --no-sim3 >> $OUT/spin_ab_lat_$v.jsonl 2>> $OUT/spin_ab.err
+  done
+fi
 if [ -n "$PROBE" ]; then
   # per-phase device clocks of the Refine kernel (stamped build: make -C tools stamps_lib)
   cd $GRAFT_REPO_ROOT
