@@ -76,6 +76,37 @@ __global__ __launch_bounds__(64) void pnp_betas_kernel(const DevPnP* __restrict_
 // ------------------------------------------------------------------------------------------------
 // PnP inlier scan (CheckInliers) — points-stationary, pose broadcast.
 // ------------------------------------------------------------------------------------------------
+// pnp_inlier (rsc_core.h) for two correspondences at once, in the scan's fast form:
+//   * the float rotation, the error and its squared norm run as packed FP32 (v_pk_mul_f32 /
+//     v_pk_add_f32: two IEEE operations per instruction, the same roundings as two scalar ones;
+//     no contraction, -ffp-contract=off);
+//   * invZc = 1/Zc is v_rcp_f32 + one FMA Newton step, which is the correctly rounded reciprocal
+//     for every float with 2^-126 <= |z| <= 2^125 (all 2^32 patterns against IEEE 1.0f / z:
+//     tools/rcp_exhaustive.hip); the compiler's IEEE division is the same core wrapped in range
+//     scaling and special-value fix-ups (10 instructions per point instead of 2).  `ok` is cleared
+//     for a point outside that range (0, denormals, huge, inf, NaN), and the caller then redoes the
+//     hypothesis with pnp_inlier.
+// The projection stays scalar double as the reference's (:253).
+typedef float rsc_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void pnp_inlier2(const float (&R)[9], const float (&t)[3], double fx, double fy, double cx,
+                                            double cy, rsc_f2 X, rsc_f2 Y, rsc_f2 Z, rsc_f2 u, rsc_f2 v, rsc_f2 maxErr,
+                                            bool& in0, bool& in1, bool& ok) {
+    const rsc_f2 Xc = (R[0] * X + (R[1] * Y + R[2] * Z)) + t[0];  // ered3, then + mti
+    const rsc_f2 Yc = (R[3] * X + (R[4] * Y + R[5] * Z)) + t[1];
+    const rsc_f2 Zc = (R[6] * X + (R[7] * Y + R[8] * Z)) + t[2];
+    const rsc_f2 r0 = {__builtin_amdgcn_rcpf(Zc.x), __builtin_amdgcn_rcpf(Zc.y)};
+    const rsc_f2 e = __builtin_elementwise_fma(-Zc, r0, (rsc_f2){1.0f, 1.0f});
+    const rsc_f2 iz = __builtin_elementwise_fma(e, r0, r0);
+    const float a0 = fabsf(Zc.x), a1 = fabsf(Zc.y);
+    ok = ok & (a0 >= 0x1p-126f) & (a0 <= 0x1p125f) & (a1 >= 0x1p-126f) & (a1 <= 0x1p125f);
+    const rsc_f2 ue = {(float)(cx + fx * (double)Xc.x * (double)iz.x), (float)(cx + fx * (double)Xc.y * (double)iz.y)};
+    const rsc_f2 ve = {(float)(cy + fy * (double)Yc.x * (double)iz.x), (float)(cy + fy * (double)Yc.y * (double)iz.y)};
+    const rsc_f2 du = ue - u, dv = ve - v;
+    const rsc_f2 e2 = du * du + dv * dv;
+    in0 = e2.x < maxErr.x;
+    in1 = e2.y < maxErr.y;
+}
+
 template <int PPT>
 __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict__ probs,
                                                        const LaunchProb* __restrict__ lps,
@@ -83,7 +114,8 @@ __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict_
                                                        const float* __restrict__ poses,
                                                        int32_t* __restrict__ counts,
                                                        int32_t* __restrict__ counts_dev,
-                                                       uint64_t* __restrict__ masks, int mask_words) {
+                                                       uint64_t* __restrict__ masks, int mask_words,
+                                                       int32_t* __restrict__ qual) {
     // Hypotheses per flush: the 4 waves' mask words of a batch wait in LDS (16 KB) until the batch's
     // counts are summed; only hypotheses reaching mRansacMinInliers — the only ones whose inlier
     // mask the host ever adopts (PnPsolver.cpp:176-195) — are stored.  In exhaustive
@@ -126,8 +158,26 @@ __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict_
             RSC_UNROLL for (int k = 0; k < 3; ++k) tn[k] = pp[9 + k];
         }
         uint64_t b[PPT];
-        RSC_UNROLL for (int s = 0; s < PPT; ++s)
-            b[s] = __ballot(pnp_inlier(R, t, fx, fy, cx, cy, X[s], Y[s], Z[s], U[s], V[s], E[s]));
+        if constexpr (PPT >= 2) {
+            bool ok = true;
+            RSC_UNROLL for (int s = 0; s < PPT; s += 2) {
+                bool i0, i1;
+                pnp_inlier2(R, t, fx, fy, cx, cy, (rsc_f2){X[s], X[s + 1]}, (rsc_f2){Y[s], Y[s + 1]},
+                            (rsc_f2){Z[s], Z[s + 1]}, (rsc_f2){U[s], U[s + 1]}, (rsc_f2){V[s], V[s + 1]},
+                            (rsc_f2){E[s], E[s + 1]}, i0, i1, ok);
+                b[s] = __ballot(i0);
+                b[s + 1] = __ballot(i1);
+            }
+            // a depth outside the fast reciprocal's range on any lane (a point on the camera
+            // plane, a degenerate pose): the whole hypothesis again with the IEEE division
+            if (__builtin_expect(__any(!ok), 0)) {
+                RSC_UNROLL for (int s = 0; s < PPT; ++s)
+                    b[s] = __ballot(pnp_inlier(R, t, fx, fy, cx, cy, X[s], Y[s], Z[s], U[s], V[s], E[s]));
+            }
+        } else {
+            RSC_UNROLL for (int s = 0; s < PPT; ++s)
+                b[s] = __ballot(pnp_inlier(R, t, fx, fy, cx, cy, X[s], Y[s], Z[s], U[s], V[s], E[s]));
+        }
         int cnt = 0;
         uint64_t mine = 0;
         RSC_UNROLL for (int s = 0; s < PPT; ++s) {
@@ -144,6 +194,9 @@ __global__ __launch_bounds__(256) void pnp_scan_kernel(const DevPnP* __restrict_
                 const int c = wave_cnt[0][tid] + wave_cnt[1][tid] + wave_cnt[2][tid] + wave_cnt[3][tid];
                 counts[lp.out0 + wt.y + base + tid] = c;
                 if (counts_dev) counts_dev[lp.out0 + wt.y + base + tid] = c;  // pnp_select_refine_kernel
+                // the problem has a hypothesis reaching mRansacMinInliers: the host replay reads its
+                // counts (it skips the counts of a problem without one, rsc_engine.h)
+                if (c >= lp.min_inliers) qual[wt.x] = 1;
                 wave_cnt[0][tid] = c;  // the batch's totals, for the mask stores below
             }
             __syncthreads();
@@ -985,9 +1038,9 @@ hipError_t launch_selftest_math(int fn, const double* x, int n, double* out, hip
 
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,
                            const float* poses, int32_t* counts, int32_t* counts_dev, uint64_t* masks, int mask_words,
-                           hipStream_t st) {
+                           int32_t* qual, hipStream_t st) {
     switch (ppt) {
-#define RSC_CASE(P) case P: pnp_scan_kernel<P><<<nwg, 256, 0, st>>>(probs, lps, wgt, poses, counts, counts_dev, masks, mask_words); break;
+#define RSC_CASE(P) case P: pnp_scan_kernel<P><<<nwg, 256, 0, st>>>(probs, lps, wgt, poses, counts, counts_dev, masks, mask_words, qual); break;
         RSC_CASE(1) RSC_CASE(2) RSC_CASE(4) RSC_CASE(8) RSC_CASE(16) RSC_CASE(32)
 #undef RSC_CASE
         default: return hipErrorInvalidValue;

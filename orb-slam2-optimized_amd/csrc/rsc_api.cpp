@@ -135,9 +135,14 @@ void xcd_order(std::vector<T>& wgs, Prob prob_of) {
 
 // Hypotheses per scan workgroup: enough workgroups for ~8 waves per SIMD (256 CUs x 4 SIMDs,
 // 4 waves per workgroup) without going below 8 hypotheses per point load.
+// RSC_SCAN_WGS overrides the workgroup target (A/B of the chunk size).
 int scan_chunk(int total_hyps) {
+    static const int target = [] {
+        const char* m = std::getenv("RSC_SCAN_WGS");
+        return m ? std::max(1, std::atoi(m)) : 2048;
+    }();
     int hc = 32;
-    while (hc > 8 && (total_hyps + hc - 1) / hc < 2048) hc >>= 1;
+    while (hc > 8 && (total_hyps + hc - 1) / hc < target) hc >>= 1;
     return hc;
 }
 
@@ -170,6 +175,12 @@ struct rsc_context {
     DevBuf<char> d_desc;
     PinBuf<char> h_desc;
     PinBuf<int32_t> h_counts;
+    PinBuf<int32_t> h_qual;  // PnP rounds: 1 when a problem has a hypothesis reaching min_inliers
+    // PnP work tables (eigen / betas / scan workgroups) on the device, uploaded when the round's shape
+    // (pnp_tab_key) changes instead of with every round's descriptors
+    DevBuf<char> d_pnp_tab;
+    std::vector<int> pnp_tab_key;
+    size_t pnp_tab_quad[3] = {0, 0, 0}, pnp_tab_solve[3] = {0, 0, 0}, pnp_tab_scan = 0;
     PinBuf<float> h_small;
     PinBuf<float> h_pick;  // Sim3 pick records of the last round, [solver][16]
     DevBuf<char> d_refine;
@@ -503,19 +514,38 @@ struct HipPnPBackend : PnPBackend {
             xcd_order(scan_wgs, [](const int4& w) { return w.x; });
             shape.assign(key.begin(), key.end());
         }
+        // The work tables (≈50 KB for config 2) live in the context's d_pnp_tab while the round's shape
+        // repeats; only the per-round descriptors (problems, launch records, selections) travel in the
+        // blob (the host copies and the upload kernel's PCIe reads shrink accordingly).
+        if (C->pnp_tab_key != key || !C->d_pnp_tab.p) {
+            std::vector<char> tab;
+            auto put = [&](const void* p, size_t n) {
+                const size_t o = tab.size();
+                tab.resize(o + ((n + 15) & ~(size_t)15));
+                if (n) std::memcpy(tab.data() + o, p, n);
+                return o;
+            };
+            for (int g = 0; g < 3; ++g) C->pnp_tab_solve[g] = put(solve_wgs[g].data(), solve_wgs[g].size() * sizeof(int2));
+            for (int g = 0; g < 3; ++g) C->pnp_tab_quad[g] = put(quad_wgs[g].data(), quad_wgs[g].size() * sizeof(int2));
+            C->pnp_tab_scan = put(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
+            C->pnp_tab_key.clear();  // invalid until the copy below has landed
+            if (int e = C->d_pnp_tab.ensure(std::max(tab.size(), (size_t)16))) return e;
+            // the previous round (the tables' last reader) has finished: every round ends synchronized
+            RSC_HIP(hipMemcpyAsync(C->d_pnp_tab.p, tab.data(), tab.size(), hipMemcpyHostToDevice, C->stream));
+            RSC_HIP(hipStreamSynchronize(C->stream));
+            C->pnp_tab_key = key;
+        }
         Blob b;
         const size_t o_probs = b.add(probs.data(), probs.size() * sizeof(DevPnP));
         const size_t o_lps = b.add(lps.data(), lps.size() * sizeof(LaunchProb));
-        size_t o_solve[3];
-        size_t o_quad[3];
-        for (int g = 0; g < 3; ++g) o_solve[g] = b.add(solve_wgs[g].data(), solve_wgs[g].size() * sizeof(int2));
-        for (int g = 0; g < 3; ++g) o_quad[g] = b.add(quad_wgs[g].data(), quad_wgs[g].size() * sizeof(int2));
-        const size_t o_scan = b.add(scan_wgs.data(), scan_wgs.size() * sizeof(int4));
         const size_t o_sel = fused ? b.add(sels.data(), sels.size() * sizeof(RefineSel)) : 0;
         if (int e = upload_blob(C, b)) return e;
+        const char* tab = C->d_pnp_tab.p;
         if (int e = C->d_poses.ensure((size_t)total * 12)) return e;
         int32_t* cnt_dst = nullptr;
         if (int e = counts_target(C, total, &cnt_dst)) return e;
+        if (int e = C->h_qual.ensure((size_t)count)) return e;
+        std::memset(C->h_qual.p, 0, (size_t)count * sizeof(int32_t));  // the previous round has finished
         int32_t* cnt_dev = nullptr;  // HBM copy of the counts for the device-side selection
         if (fused) {
             if (C->direct_counts) {
@@ -547,16 +577,16 @@ struct HipPnPBackend : PnPBackend {
             // the first group's eigen stage starts at ev[0]: no extra event in the queue
             hipEvent_t eb = (C->timing && !first_group) ? C->ev[6 + 2 * g] : nullptr;
             RSC_HIP(launch_pnp_solve_split(4 + g, (int)quad_wgs[g].size(),
-                                          reinterpret_cast<const int2*>(base + o_quad[g]), (int)solve_wgs[g].size(),
-                                          reinterpret_cast<const int2*>(base + o_solve[g]), dprobs, dlps,
+                                          reinterpret_cast<const int2*>(tab + C->pnp_tab_quad[g]), (int)solve_wgs[g].size(),
+                                          reinterpret_cast<const int2*>(tab + C->pnp_tab_solve[g]), dprobs, dlps,
                                           C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p, bs, C->stream,
                                           eb, C->timing ? C->ev[7 + 2 * g] : nullptr,
                                           (int)quad_wgs[g].size() <= C->eig_rows_max_wgs));
             first_group = false;
         }
         timing_begin(C, 1);
-        RSC_HIP(launch_pnp_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(base + o_scan),
-                                C->d_poses.p, cnt_dst, cnt_dev, C->d_masks.p, mw, C->stream));
+        RSC_HIP(launch_pnp_scan(ppt, (int)scan_wgs.size(), dprobs, dlps, reinterpret_cast<const int4*>(tab + C->pnp_tab_scan),
+                                C->d_poses.p, cnt_dst, cnt_dev, C->d_masks.p, mw, C->h_qual.p, C->stream));
         timing_begin(C, 2);
         if (fused) {
             timing_begin(C, 3);
@@ -594,9 +624,15 @@ struct HipPnPBackend : PnPBackend {
                 C->last_ms[2] += r;
             }
         }
+        // a problem none of whose hypotheses reaches min_inliers hands back no counts: the replay only
+        // advances its counters (the GPU-written counts are not read back through the host caches)
         counts.resize(count);  // keeps the inner vectors' capacity
-        for (int i = 0; i < count; ++i)
-            counts[i].assign(C->h_counts.p + lps[i].out0, C->h_counts.p + lps[i].out0 + H[i]);
+        for (int i = 0; i < count; ++i) {
+            if (C->h_qual.p[i])
+                counts[i].assign(C->h_counts.p + lps[i].out0, C->h_counts.p + lps[i].out0 + H[i]);
+            else
+                counts[i].clear();
+        }
         if (fused) fused_count = count;
         return 0;
     }

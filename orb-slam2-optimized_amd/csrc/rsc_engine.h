@@ -168,7 +168,8 @@ struct PnPResult {
 // Backend contract for the PnP replay.
 struct PnPBackend {
     // Speculate hypotheses [0, H[i]) for solver states[i] (from their current rng position and
-    // EPnP buffer rows).  Fills counts[i][0..H[i]).
+    // EPnP buffer rows).  Fills counts[i][0..H[i]), or leaves counts[i] empty when none of those
+    // counts reaches states[i]->mRansacMinInliers (the replay then only advances the counters).
     virtual int speculate(PnPState* const* states, int count, const int* H, std::vector<std::vector<int32_t>>& counts) = 0;
     // Refine() for each listed solver, paused at hypothesis pause_k[q] of speculation slot
     // spec_j[q], preceded (adopt_k[q] >= 0) by the new-best bookkeeping of PnPsolver.cpp:147-156:
@@ -240,9 +241,10 @@ inline int pnp_iterate_many(PnPBackend& be, PnPState* const* S, int count, const
             PnPState& s = *spec[j];
             const int i = who[j];
             // hypotheses [0, k) are below minInliers: they only advance the counters
+            // (a backend may hand back no counts for a slot none of whose hypotheses reaches mi)
             const int32_t* cj = counts[j].data();
             const int hj = H[j], mi = s.mRansacMinInliers;
-            int k = 0;
+            int k = counts[j].empty() ? hj : 0;
             while (k < hj && cj[k] < mi) ++k;
             const int ran = (k < hj) ? k + 1 : hj;
             ncur[i] += ran;

@@ -141,10 +141,11 @@ hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, 
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
                                   hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr, bool eig_rows = false);
 // counts: where the host reads them (pinned memory or HBM); counts_dev (nullable): an HBM copy for
-// pnp_select_refine_kernel.
+// pnp_select_refine_kernel; qual[lp] (pinned, zeroed by the host) is set to 1 when a hypothesis of
+// launch problem lp reaches its min_inliers.
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,
                            const float* poses, int32_t* counts, int32_t* counts_dev, uint64_t* masks, int mask_words,
-                           hipStream_t st);
+                           int32_t* qual, hipStream_t st);
 hipError_t launch_pnp_select_refine(int nsel, const DevPnP* probs, const RefineSel* sels, const int32_t* counts,
                                     uint64_t* masks, int mask_words, const float* poses, RefineSelOut* out,
                                     hipStream_t st);
