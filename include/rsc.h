@@ -70,7 +70,8 @@ int rsc_context_set_eig_rows(rsc_context* ctx, int max_workgroups);
  * x[(i+n/2)%n]) c / s; 10 qr_solve_6x4 (PnPsolver.cpp:693-796) on records of 34 doubles
  * (A[6][4] row-major, b[6], previous X[4]) -> X in out[0..3], 1/0 success in out[4] of each record
  * (n a multiple of 34); 11 pow(x, 1.0/3.0), 12 pow(x, 3.0/2.0) as MLPnP computes them (x >= 0;
- * MLPnPsolver.cpp:567, :839, :901).  Host pointers, n >= 0.  Tests compare with glibc / IEEE numpy / the oracle. */
+ * MLPnPsolver.cpp:567, :839, :901); 13 the PnP scan's float reciprocal of (float)x (v_rcp_f32 + one
+ * Newton step, PnPsolver.cpp:251).  Host pointers, n >= 0.  Tests compare with glibc / IEEE numpy / the oracle. */
 int rsc_selftest_math(rsc_context* ctx, int fn, const double* x, int n, double* out);
 
 /* ---- PnPsolver (include/PnPsolver.hpp:21-138, src/PnPsolver.cpp) ------------------------------ */
@@ -467,6 +468,11 @@ int rsc_kfdb_state(rsc_kfdb* db, int kf, uint64_t* q, int32_t* w, float* s);
  * wave w: betas + Gauss-Newton, pc0 sum, M sum + Horn, error sum (zeros unless built with
  * RSC_REFINE_STAMPS=1). */
 int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
+/* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP hypothesis solve, [2][wg < 4096][8]:
+ * [0] eigen stage per workgroup (entry, sample + MtM, tridiagonal, Q, chase + store), [1] betas stage
+ * per wave (entry, L + rho, find_betas, Gauss-Newton, row loads, R and t, hand-off; [7] = the
+ * approximation | 256 * group) (zeros unless built with RSC_SOLVE_STAMPS=1; cap >= 65536). */
+int rsc_diag_solve_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
 /* Diagnostic: wall-clock (100 MHz) ticks of the last PoseOptimization launch, [frame < 64][8]:
  * fused passes (ticks), number of passes + (their active edges << 24), re-classification, whole kernel,
  * 4 unused. */

@@ -31,6 +31,22 @@
 namespace rsc {
 __device__ uint64_t g_refine_stamps[64][24];
 }
+// Diagnostic phase stamps of the hypothesis solve (rsc_diag_solve_phase_stamps), compiled in only
+// with RSC_SOLVE_STAMPS=1: [0][wg][k] eigen stage (entry, sample + MtM, tridiagonal, Q, chase + store),
+// [1][wg][k] betas stage (entry, L + rho, find_betas, Gauss-Newton, row loads, R and t, hand-off,
+// exit); slot 7 = the approximation (betas) | 256 * launch-table index.
+#ifndef RSC_SOLVE_STAMPS
+#define RSC_SOLVE_STAMPS 0
+#endif
+namespace rsc {
+__device__ uint64_t g_solve_stamps[2][4096][8];
+}
+#if RSC_SOLVE_STAMPS
+#define RSC_SOLVE_STAMP(st, k)                                                                         \
+    do {                                                                                               \
+        if (blockIdx.x < 4096 && (threadIdx.x & 63) == 0) ::rsc::g_solve_stamps[st][blockIdx.x][k] = wall_clock64(); \
+    } while (0)
+#endif
 #if RSC_REFINE_STAMPS
 #define RSC_EIG_PHASE(k)                                                                               \
     do {                                                                                               \
@@ -58,6 +74,18 @@ __global__ __launch_bounds__(64) void pnp_eig_group_kernel(const DevPnP* __restr
                                                           double* __restrict__ stage, int32_t* __restrict__ samples) {
     __shared__ __attribute__((aligned(16))) double smem[kEigHyps * kQuadRegion];
     pnp_eig_group_body<NS, 99, kEigLanes, kEigHyps>(probs, lps, wg_table, rng_T, stage, samples, smem);
+}
+
+// split form (rsc_quad.h pnp_eig_split_body): wave 0 chases, wave 1 rotates Q
+// (<= 256 registers: two waves per SIMD, so a SIMD holds a chase wave and its row wave)
+template <int NS>
+__global__ __launch_bounds__(128 * kSplitUnits) __attribute__((amdgpu_waves_per_eu(2))) void pnp_eig_split_kernel(
+    const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps, const int2* __restrict__ wg_table,
+    int nwg_table, const uint32_t* __restrict__ rng_T, double* __restrict__ stage, int32_t* __restrict__ samples) {
+    __shared__ __attribute__((aligned(16))) double smem[kSplitHyps * kQuadRegion];
+    __shared__ __attribute__((aligned(16))) double dsub[kSplitHyps * kSplitDsub];
+    __shared__ int pub[kSplitUnits], ack[kSplitUnits];
+    pnp_eig_split_body<NS>(probs, lps, wg_table, nwg_table, rng_T, stage, samples, smem, dsub, pub, ack);
 }
 
 template <int NS>
@@ -900,7 +928,7 @@ static hipError_t launch_eig_rows(int nwgE, const int2* wgtE, const DevPnP* prob
 hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, const int2* wgtB,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
-                                  hipEvent_t eig_begin, hipEvent_t eig_end, bool eig_rows) {
+                                  hipEvent_t eig_begin, hipEvent_t eig_end, bool eig_rows, bool eig_split) {
     if (ns < 4 || ns > 6) return hipErrorInvalidValue;
     if (eig_begin) (void)hipEventRecord(eig_begin, st);
     switch (ns) {
@@ -909,7 +937,10 @@ hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, 
         if (eig_rows) {                                                                               \
             const hipError_t e = launch_eig_rows<N>(nwgE, wgtE, probs, lps, T, stage, samples, st);   \
             if (e != hipSuccess) return e;                                                            \
-        } else                                                                                        \
+        } else if (eig_split)                                                                         \
+            pnp_eig_split_kernel<N><<<(nwgE + kSplitUnits - 1) / kSplitUnits, 128 * kSplitUnits, 0, st>>>( \
+                probs, lps, wgtE, nwgE, T, stage, samples);                                           \
+        else                                                                                          \
             pnp_eig_group_kernel<N><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples);        \
         if (eig_end) (void)hipEventRecord(eig_end, st);                                               \
         pnp_betas_kernel<N><<<3 * nwgB, 64, 0, st>>>(probs, lps, wgtB, nwgB, stage, samples, poses,   \
@@ -943,6 +974,14 @@ __global__ __launch_bounds__(256) void selftest_math_kernel(int fn, const double
         // MLPnP's pow(x, 1.0/3.0) and pow(t, 3.0/2.0) restatements (rsc_math.h)
         case 11: r = dm::pow_1_3(v); break;
         case 12: r = dm::pow_3_2(v); break;
+        // the PnP scan's reciprocal (pnp_inlier2, one element) of (float)v; rcp_fast_ok is not
+        // applied, so the caller sees the fast form on every argument
+        case 13: {
+            const float z = (float)v;
+            const float r0 = __builtin_amdgcn_rcpf(z);
+            r = (double)__builtin_fmaf(__builtin_fmaf(-z, r0, 1.0f), r0, r0);
+            break;
+        }
         default: {
             double c, s;
             make_givens(v, x[(i + n / 2) % n], c, s);
@@ -1025,7 +1064,7 @@ hipError_t launch_upload16(const void* host_src, void* dev_dst, size_t n16, hipS
 }
 
 hipError_t launch_selftest_math(int fn, const double* x, int n, double* out, hipStream_t st) {
-    if (fn < 0 || fn > 12 || n <= 0) return hipErrorInvalidValue;
+    if (fn < 0 || fn > 13 || n <= 0) return hipErrorInvalidValue;
     if (fn == 10) {
         if (n % 34) return hipErrorInvalidValue;
         const int nrec = n / 34;
@@ -1046,6 +1085,10 @@ hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchPr
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+hipError_t read_solve_stamps(uint64_t* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solve_stamps), sizeof(uint64_t) * 2 * 4096 * 8, 0, hipMemcpyDeviceToHost);
 }
 
 hipError_t read_refine_stamps(uint64_t* out) {

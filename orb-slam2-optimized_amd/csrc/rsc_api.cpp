@@ -221,6 +221,9 @@ struct rsc_context {
     // one relocalization event: 125 -> 99 us, profiles/r05/bench_latency_forms_ab_r5b.json); env
     // RSC_EIG_ROWS=W or rsc_context_set_eig_rows overrides (0: lane pairs always)
     int eig_rows_max_wgs = kEigRowsDefaultWgs;
+    // eigen stages beyond the rows form's range: split form (chase and Q rotations on two waves,
+    // pnp_eig_split_kernel) or the pair form (env RSC_EIG_SPLIT=0/1)
+    bool eig_split = false;
     // host wait for a speculation round's results: spin on a completion flag in pinned host memory
     // (written by signal_kernel after the round) instead of hipStreamSynchronize's wake-up; env
     // RSC_SPIN_WAIT=0/1 (stream_wait)
@@ -581,7 +584,7 @@ struct HipPnPBackend : PnPBackend {
                                           reinterpret_cast<const int2*>(tab + C->pnp_tab_solve[g]), dprobs, dlps,
                                           C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p, bs, C->stream,
                                           eb, C->timing ? C->ev[7 + 2 * g] : nullptr,
-                                          (int)quad_wgs[g].size() <= C->eig_rows_max_wgs));
+                                          (int)quad_wgs[g].size() <= C->eig_rows_max_wgs, C->eig_split));
             first_group = false;
         }
         timing_begin(C, 1);
@@ -1222,6 +1225,7 @@ int rsc_context_create(int device, rsc_context** out) {
     if (const char* m = std::getenv("RSC_FUSED_REFINE")) C->fused_refine = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_DMA_UPLOAD")) C->dma_upload = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_EIG_ROWS")) C->eig_rows_max_wgs = std::max(0, std::atoi(m));
+    if (const char* m = std::getenv("RSC_EIG_SPLIT")) C->eig_split = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_SPIN_WAIT")) C->spin_wait = std::strcmp(m, "0") != 0;
     {
         void* f = nullptr;
@@ -1276,7 +1280,7 @@ int rsc_context_set_eig_rows(rsc_context* C, int max_workgroups) {
 }
 
 int rsc_selftest_math(rsc_context* C, int fn, const double* x, int n, double* out) {
-    if (!C || fn < 0 || fn > 12 || n < 0 || (n > 0 && (!x || !out)) || (fn == 10 && n % 34)) return RSC_ERR_ARG;
+    if (!C || fn < 0 || fn > 13 || n < 0 || (n > 0 && (!x || !out)) || (fn == 10 && n % 34)) return RSC_ERR_ARG;
     if (n == 0) return RSC_OK;
     RSC_HIP(hipSetDevice(C->device));
     double* d = nullptr;
@@ -2531,6 +2535,13 @@ int rsc_diag_refine_phase_stamps(rsc_context* C, uint64_t* out, int cap) {
     if (!C || !out || cap < 64 * 24) return RSC_ERR_ARG;
     RSC_HIP(hipStreamSynchronize(C->stream));
     RSC_HIP(read_refine_stamps(out));
+    return RSC_OK;
+}
+
+int rsc_diag_solve_phase_stamps(rsc_context* C, uint64_t* out, int cap) {
+    if (!C || !out || cap < 2 * 4096 * 8) return RSC_ERR_ARG;
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    RSC_HIP(read_solve_stamps(out));
     return RSC_OK;
 }
 

@@ -181,6 +181,12 @@ template <typename Q, typename = void>
 struct qr_has_prefetch { static constexpr bool value = false; };
 template <typename Q>
 struct qr_has_prefetch<Q, decltype((void)std::declval<Q&>().prefetch(0))> { static constexpr bool value = true; };
+// Optional hook `q.sweep_end()`: called after every implicit-QR step (once per loop iteration that
+// ran a step, on the lanes that ran it), e.g. to publish the step's rotations to other waves.
+template <typename Q, typename = void>
+struct qr_has_sweep_end { static constexpr bool value = false; };
+template <typename Q>
+struct qr_has_sweep_end<Q, decltype((void)std::declval<Q&>().sweep_end())> { static constexpr bool value = true; };
 
 // Implicit symmetric QR iterations on (diag, sub) with the rotations handed to
 // `qapply(k, c, s, apply)` (which must perform Q = Q * G on columns k,k+1 when `apply`, and leave
@@ -289,6 +295,7 @@ RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, int (&per
                 qapply(k, c, s, !(c == S(1) && s == S(0)));
             }
         }
+        if constexpr (qr_has_sweep_end<QApply>::value) qapply.sweep_end();
         RSC_LOOP_FENCE();
     }
     const bool ok = (iter <= maxIterations * n);

@@ -132,14 +132,18 @@ struct BetasScratch {
 // waves of quads x 4 or quads x 1 instead of pairs x 20, were measured slower on the single-event
 // case (tools/latency_ab.py, profiles/r03/latency_ab_r3_c.txt): the stage time is not the union of
 // a wave's hypotheses' chains but the per-wave latency, which more, narrower waves do not shorten.
-constexpr int kBetasHyps = 64;
+#ifndef RSC_BETAS_HYPS
+#define RSC_BETAS_HYPS 64  // build-time override for A/B runs (tools/Makefile betas32_lib)
+#endif
+constexpr int kBetasHyps = RSC_BETAS_HYPS;
 // Default eigen-stage form switch (rsc_context_set_eig_rows): launches of at most this many 20-hypothesis
 // workgroups run the rows form.
 constexpr int kEigRowsDefaultWgs = 64;
 hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, const int2* wgtB,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
-                                  hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr, bool eig_rows = false);
+                                  hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr, bool eig_rows = false,
+                                  bool eig_split = false);
 // counts: where the host reads them (pinned memory or HBM); counts_dev (nullable): an HBM copy for
 // pnp_select_refine_kernel; qual[lp] (pinned, zeroed by the host) is set to 1 when a hypothesis of
 // launch problem lp reaches its min_inliers.
@@ -154,6 +158,7 @@ hipError_t launch_pnp_select_refine(int nsel, const DevPnP* probs, const RefineS
 // rounds (config 2), where no hypothesis qualifies, keep their launch set unchanged.
 constexpr int kFusedRefineMaxHyps = 4096;
 hipError_t read_refine_stamps(uint64_t* out);  // diagnostic, [64][24]
+hipError_t read_solve_stamps(uint64_t* out);   // diagnostic, [2][4096][8]
 hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, hipStream_t st);
 hipError_t launch_sim3_solve(int nwg, const DevSim3* probs, const LaunchProb* lps, const int2* wgt,
                              const uint32_t* T, float* poses, int32_t* samples, hipStream_t st);

@@ -26,6 +26,11 @@
     do {                 \
     } while (0)
 #endif
+#ifndef RSC_SOLVE_STAMP
+#define RSC_SOLVE_STAMP(st, k) \
+    do {                       \
+    } while (0)
+#endif
 
 namespace rsc {
 
@@ -34,8 +39,8 @@ constexpr int kQuadE = 55;   // Householder essential vectors
 constexpr int kQuadRegion = kQuadT + kQuadE + 1;  // 200 doubles per hypothesis
 // stage record offsets (rsc_kernels.h kStageDoubles)
 constexpr int kStEv = 0, kStAl = 48, kStCws = 72;
-// pnp_betas_wave_body LDS: L + rho [66][64].
-constexpr int kBetasWaveSmemDoubles = 66 * 64;
+// pnp_betas_wave_body LDS: L + rho [66][kBetasHyps].
+constexpr int kBetasWaveSmemDoubles = 66 * kBetasHyps;
 
 // Offset of step i's essential Householder vector (entries v[1..10-i]) in the E region.
 RSC_HD constexpr int quad_eoff(int i) { return 10 * i - (i * (i - 1)) / 2; }
@@ -415,6 +420,7 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
     double* out = stage + rec * kStageDoubles;
     double* T = smem + g * kQuadRegion;
     double* E = T + kQuadT;
+    RSC_SOLVE_STAMP(0, 0);
 
     // ---- A: sample, control points, alphas, MtM (every lane of the group, identical values) ----
     {
@@ -449,6 +455,7 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
         }
     }
     __syncthreads();
+    RSC_SOLVE_STAMP(0, 1);
     if (STOP == 1) {
         if (active && q == 0) out[0] = T[0] + T[143];
         return;
@@ -468,6 +475,7 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
         group_tridiag<L>(A, q, E, diag, sub, hC);
     }
     __syncthreads();
+    RSC_SOLVE_STAMP(0, 2);
     if (STOP == 2) {
         if (active && q == 0) {
             double acc = 0.0;
@@ -486,6 +494,7 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
             RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + L * j + q] = Qc[j][r];
     }
     __syncthreads();
+    RSC_SOLVE_STAMP(0, 3);
     if (STOP == 3) {
         if (active) {
             double acc = 0.0;
@@ -508,7 +517,14 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
         double Qr[RJ][12];
         RSC_UNROLL for (int j = 0; j < RJ; ++j)
             RSC_UNROLL for (int c = 0; c < 12; ++c) Qr[j][c] = T[(L * j + q) * 12 + c];
+#ifndef RSC_EIG_NULLSINK
         GroupRegRows<L> qapply{Qr};
+#else
+        // timing diagnostic only (tools/Makefile nullsink_lib): the chase without the Q rotations
+        struct {
+            RSC_HD void operator()(int, double, double, bool) {}
+        } qapply;
+#endif
         tridiag_qr<double, 12>(diag, sub, qapply, perm);
         if (active) {
             RSC_UNROLL for (int j = 0; j < RJ; ++j) {
@@ -519,6 +535,7 @@ __device__ __forceinline__ void pnp_eig_group_body(const DevPnP* __restrict__ pr
                 }
             }
         }
+        RSC_SOLVE_STAMP(0, 4);
     }
 #else
     {
@@ -610,14 +627,263 @@ __device__ __forceinline__ void pnp_eig_rows_body(const DevPnP* __restrict__ pro
     if (active) RSC_UNROLL for (int c = 0; c < 4; ++c) out[kStEv + r * 4 + c] = ev[c];
 }
 
+// ---- The eigen stage with the QR chase and the Q rotations on different waves (split form) ----
+// A workgroup of 2 * kSplitUnits waves serves kSplitUnits units of kEigHyps = 20 hypotheses (one
+// entry of the eigen-stage work table each); unit c owns chase wave c and row wave kSplitUnits + c,
+// which the dispatcher places on the same SIMD (waves go round-robin over the CU's four SIMDs):
+//   A    chase wave c, lane pairs as pnp_eig_group_body: sample, control points, alphas, MtM into T;
+//   B-C  lane quads over the unit's two waves (hypotheses 0-15 in the chase wave, 16-19 in the row
+//        wave): scale, Householder tridiagonalisation and Q accumulation exactly as group_eig12_ev4
+//        (the Refine's quad form, bit-identical to the pair form), Q row-major into T, (diag, sub)
+//        into a slab of their own;
+//   D    the chase wave, one lane per hypothesis, runs the implicit-QR chase on (diag, sub) alone:
+//        each QR step's rotations — (c, s) per slot and a bit per slot that rotated — go into the
+//        hypothesis' E region (two parities; E is free after phase C) and the step number into the
+//        unit's `pub` word (tridiag_qr's sweep_end hook); the row wave holds Q in VGPRs, lane 3h + m
+//        owning rows m, m+3, m+6, m+9 of hypothesis h, waits for each step on `pub`, applies it,
+//        slots in order — GroupRegRows' operations in its order, so the eigenvectors are
+//        bit-identical — and acknowledges it in `ack`; before step s + 1 overwrites the parity of
+//        step s - 1 the chase wave waits for that acknowledgement.
+// The chase wave issues only the scalar chain (no Q rows in its registers), the row updates issue
+// from the other wave of the SIMD (<= 256 registers: two waves per SIMD), and the units run
+// independently (LDS flags, not workgroup barriers, between a chase wave and its row wave).  A step
+// is valid for a hypothesis when its step number matches (a converged hypothesis publishes nothing
+// and keeps an older number in its ring slot); the chase wave's last `pub` carries kSplitDone.
+constexpr int kSplitUnits = 4;     // chase / row wave pairs per workgroup (one per SIMD)
+constexpr int kSplitRowLanes = 3;  // row-wave lanes per hypothesis (4 rows of Q each)
+constexpr int kRingPar = 24;       // doubles per parity in E: (c, s) of slots 0..10, then the step word
+constexpr int kRingPerm = 48;      // E[48..49]: the four sorted column indices (int32)
+constexpr int kSplitDsub = 24;     // doubles per hypothesis of the (diag, sub) slab
+constexpr int kSplitHyps = kSplitUnits * 20;
+
+constexpr int kSplitDone = 1 << 30;    // `pub` flag: the chase has ended (low bits: its steps)
+constexpr int kSplitSpinLimit = 1 << 24;  // polls before a wait gives up (never reached; no hang)
+
+// Wait (wave-uniformly) until pred(value of *flag) holds; returns the value seen.
+template <class Pred>
+__device__ __forceinline__ int split_wait(int* flag, Pred pred) {
+    int v = 0;
+    for (int it = 0; it < kSplitSpinLimit; ++it) {
+        v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (pred(v)) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return v;
+}
+
+struct SplitRing {
+    double* E;          // this hypothesis' E region (55 doubles)
+    int* pub;           // this unit's published step count
+    int* ack;           // this unit's applied step count (row wave)
+    uint32_t mask = 0;  // slots of the step being built that rotated
+    uint32_t seq = 0;   // steps published
+    RSC_HD void operator()(int k, double c, double s, bool apply) {
+        double* r = E + kRingPar * ((seq + 1) & 1) + 2 * k;
+        r[0] = c;
+        r[1] = s;
+        mask |= apply ? (1u << k) : 0u;
+    }
+    RSC_HD void sweep_end() {
+        ++seq;
+        *reinterpret_cast<uint64_t*>(E + kRingPar * (seq & 1) + 22) = (uint64_t)seq | ((uint64_t)mask << 32);
+        mask = 0;
+        // every lane still iterating is at the same step: the ring stores above, then the count
+        __hip_atomic_store(pub, (int)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // step seq + 1 overwrites the parity of step seq - 1: it must have been applied
+        const int need = (int)seq - 1;
+        split_wait(ack, [need](int v) { return v >= need; });
+    }
+};
+
+template <int NS>
+__device__ __forceinline__ void pnp_eig_split_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
+                                                   const int2* __restrict__ wg_table, int nwg_table,
+                                                   const uint32_t* __restrict__ rng_T, double* __restrict__ stage,
+                                                   int32_t* __restrict__ samples, double* smem, double* dsub,
+                                                   int* pub, int* ack) {
+    constexpr int HPW = kEigHyps, U = kSplitUnits;
+    static_assert(HPW == 20 && 2 * HPW <= 64 && 4 * HPW <= 128 && HPW * kSplitRowLanes <= 64, "unit layout");
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int unit = wave % U;
+    const bool row_wave = wave >= U;
+    const int entry = blockIdx.x * U + unit;
+    const bool unit_ok = entry < nwg_table;  // the last workgroup may hold fewer units
+    const int2 wt = wg_table[unit_ok ? entry : 0];
+    const LaunchProb& lp = lps[wt.x];
+    const DevPnP& P = probs[lp.prob];
+    double* Tu = smem + unit * HPW * kQuadRegion;  // the unit's 20 regions
+    double* Du = dsub + unit * HPW * kSplitDsub;
+#if RSC_SOLVE_STAMPS
+#define RSC_SPLIT_STAMP(k) \
+    do { if (tid == 0 && blockIdx.x < 4096) g_solve_stamps[0][blockIdx.x][k] = wall_clock64(); } while (0)
+#else
+#define RSC_SPLIT_STAMP(k) do {} while (0)
+#endif
+    RSC_SPLIT_STAMP(0);
+    if (tid < U) {
+        pub[tid] = 0;
+        ack[tid] = 0;
+    }
+    // ---- A: chase waves, lane pairs ----
+    if (!row_wave && unit_ok && lane < 2 * HPW) {
+        const int g = lane >> 1, q = lane & 1;
+        const bool active = wt.y + g < lp.H;
+        const int h = active ? wt.y + g : lp.H - 1;
+        const size_t rec = (size_t)(lp.out0 + h);
+        double* out = stage + rec * kStageDoubles;
+        double* T = Tu + g * kQuadRegion;
+        int idx[NS];
+        uint32_t w[31];
+        RSC_UNROLL for (int j = 0; j < 31; ++j) w[j] = lp.window[j];
+        uint32_t words[NS];
+        RSC_UNROLL for (int d = 0; d < NS; ++d) words[d] = rng_word(rng_T, w, lp.g0 + h * NS + d);
+        swap_remove_sample<NS>(words, NS, P.n, idx);
+        HypStore<NS> st;
+        RSC_UNROLL for (int i = 0; i < NS; ++i) {
+            const float4 p = P.pts[idx[i]];
+            const float2 uv = P.uv[idx[i]];
+            st.pw_[i][0] = p.x; st.pw_[i][1] = p.y; st.pw_[i][2] = p.z;
+            st.u_[i][0] = uv.x; st.u_[i][1] = uv.y;
+        }
+        st.rows_ = P.rows;
+        st.spw = P.pws;
+        st.sal = P.als;
+        const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
+        double cws[4][3];
+        control_points_and_alphas(st, cws);
+        if (q == 0) {
+            build_MtM(st, K, LaneMat{T, 1});
+            if (active) {
+                RSC_UNROLL for (int i = 0; i < NS; ++i)
+                    RSC_UNROLL for (int j = 0; j < 4; ++j) out[kStAl + i * 4 + j] = st.al(i, j);
+                RSC_UNROLL for (int i = 0; i < 4; ++i)
+                    RSC_UNROLL for (int c = 0; c < 3; ++c) out[kStCws + i * 3 + c] = cws[i][c];
+                RSC_UNROLL for (int i = 0; i < NS; ++i) samples[rec * 8 + i] = idx[i];
+            }
+        }
+    }
+    __syncthreads();  // A: MtM (lower triangle) in T
+    RSC_SPLIT_STAMP(1);
+    // ---- B-C: the unit's two waves, lane quads ----
+    const int g4 = (row_wave ? 16 : 0) + (lane >> 2), q4 = lane & 3;
+    const bool quad = unit_ok && g4 < HPW;
+    double* T4 = Tu + (quad ? g4 : 0) * kQuadRegion;
+    double* E4 = T4 + kQuadT;
+    double hC[11];
+    if (quad) {
+        double diag[12], sub[11];
+        double A[3][12];
+        RSC_UNROLL for (int j = 0; j < 3; ++j) {
+            const int R = 4 * j + q4;
+            RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = T4[(R >= c) ? R * 12 + c : c * 12 + R];
+        }
+        const double scale = group_scale<4>(A, q4);
+        RSC_UNROLL for (int j = 0; j < 3; ++j)
+            RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = A[j][c] / scale;
+        __builtin_amdgcn_wave_barrier();
+        group_tridiag<4>(A, q4, E4, diag, sub, hC);
+        if (q4 == 0) {
+            double* ds = Du + g4 * kSplitDsub;
+            RSC_UNROLL for (int i = 0; i < 12; ++i) ds[i] = diag[i];
+            RSC_UNROLL for (int i = 0; i < 11; ++i) ds[12 + i] = sub[i];
+        }
+    }
+    __syncthreads();  // B: every lane of a quad has read T; E holds the Householder vectors
+    RSC_SPLIT_STAMP(2);
+    if (quad) {
+        double Qc[3][12];
+        group_accumulate<4>(Qc, q4, E4, hC);
+        RSC_UNROLL for (int j = 0; j < 3; ++j)
+            RSC_UNROLL for (int r = 0; r < 12; ++r) T4[r * 12 + 4 * j + q4] = Qc[j][r];
+    }
+    __syncthreads();  // C: Q row-major in T, (diag, sub) in the slab; E is read by no one any more
+    RSC_SPLIT_STAMP(3);
+    // (no workgroup barrier below: a unit's two waves synchronise through pub / ack)
+    if (row_wave) {
+        // ---- D, row wave: Q rows ----
+        const int g = lane / kSplitRowLanes, m = lane - kSplitRowLanes * g;
+        const bool lane_ok = unit_ok && g < HPW;
+        const bool active = lane_ok && wt.y + g < lp.H;
+        const int h = active ? wt.y + g : lp.H - 1;
+        const double* T = Tu + (lane_ok ? g : 0) * kQuadRegion;
+        const double* E = T + kQuadT;
+        double Q[4][12];
+        RSC_UNROLL for (int j = 0; j < 4; ++j)
+            RSC_UNROLL for (int c = 0; c < 12; ++c) Q[j][c] = T[(kSplitRowLanes * j + m) * 12 + c];
+        for (int s = 1;; ++s) {
+            // step s published, or the chase ended before it
+            const int v = split_wait(pub + unit, [s](int x) { return (x & (kSplitDone - 1)) >= s || (x & kSplitDone); });
+            if ((v & (kSplitDone - 1)) < s) break;
+            const double* ring = E + kRingPar * (s & 1);
+            const uint64_t word = *reinterpret_cast<const uint64_t*>(ring + 22);
+            const uint32_t bits = (lane_ok && (uint32_t)word == (uint32_t)s) ? (uint32_t)(word >> 32) : 0u;
+            RSC_UNROLL for (int k = 0; k < 11; ++k) {
+                if ((bits >> k) & 1u) {
+                    const double c = ring[2 * k], sn = ring[2 * k + 1];
+                    RSC_UNROLL for (int j = 0; j < 4; ++j) {
+                        const double x = Q[j][k], y = Q[j][k + 1];
+                        Q[j][k] = c * x - sn * y;
+                        Q[j][k + 1] = sn * x + c * y;
+                    }
+                }
+            }
+            __hip_atomic_store(ack + unit, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (active) {
+            const int32_t* pm = reinterpret_cast<const int32_t*>(E + kRingPerm);
+            int perm4[4];
+            RSC_UNROLL for (int c = 0; c < 4; ++c) perm4[c] = pm[c];
+            double* out = stage + (size_t)(lp.out0 + h) * kStageDoubles;
+            RSC_UNROLL for (int j = 0; j < 4; ++j) {
+                RSC_UNROLL for (int c = 0; c < 4; ++c) {
+                    double x = Q[j][0];
+                    RSC_UNROLL for (int p = 1; p < 12; ++p) x = (perm4[c] == p) ? Q[j][p] : x;
+                    out[kStEv + (kSplitRowLanes * j + m) * 4 + c] = x;
+                }
+            }
+        }
+        return;
+    }
+    // ---- D, chase wave: one lane per hypothesis ----
+    // the chain's instructions win the SIMD's issue arbitration against the row wave's
+#ifndef RSC_SPLIT_PRIO
+#define RSC_SPLIT_PRIO 3
+#endif
+    __builtin_amdgcn_s_setprio(RSC_SPLIT_PRIO);
+    if (unit_ok && lane < HPW) {
+        double* E = Tu + lane * kQuadRegion + kQuadT;
+        // the ring's step words start below step 1 (E held the Householder vectors)
+        *reinterpret_cast<uint64_t*>(E + 22) = 0;
+        *reinterpret_cast<uint64_t*>(E + kRingPar + 22) = 0;
+        double diag[12], sub[11];
+        const double* ds = Du + lane * kSplitDsub;
+        RSC_UNROLL for (int i = 0; i < 12; ++i) diag[i] = ds[i];
+        RSC_UNROLL for (int i = 0; i < 11; ++i) sub[i] = ds[12 + i];
+        int perm[12];
+        SplitRing ring{E, pub + unit, ack + unit};
+        tridiag_qr<double, 12>(diag, sub, ring, perm);
+        int32_t* pm = reinterpret_cast<int32_t*>(E + kRingPerm);
+        RSC_UNROLL for (int c = 0; c < 4; ++c) pm[c] = perm[c];
+    }
+    RSC_SPLIT_STAMP(6);
+    // the chase has ended (the permutation above, then the flag; a unit without hypotheses publishes
+    // zero steps)
+    if (lane == 0) {
+        const int steps = __hip_atomic_load(pub + unit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(pub + unit, steps | kSplitDone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    RSC_SPLIT_STAMP(4);
+#undef RSC_SPLIT_STAMP
+}
+
 // Eigenvectors read from the stage record in global memory (stride 1), L + rho in LDS
 // (element-major across the wave).
 struct StageEvView {
     const double* evp;
     double* Lp;
     RSC_HD double ev(int r, int c) const { return evp[r * 4 + c]; }
-    RSC_HD double& L(int i, int j) const { return Lp[(i * 10 + j) * 64]; }
-    RSC_HD double& rho(int i) const { return Lp[(60 + i) * 64]; }
+    RSC_HD double& L(int i, int j) const { return Lp[(i * 10 + j) * kBetasHyps]; }
+    RSC_HD double& rho(int i) const { return Lp[(60 + i) * kBetasHyps]; }
 };
 
 // Block -> (64-hypothesis group, approximation) of pnp_betas_kernel: the three waves of a group are
@@ -663,7 +929,10 @@ __device__ __forceinline__ void pnp_betas_wave_body(const DevPnP* __restrict__ p
     const DevPnP& P = probs[lp.prob];
     const size_t rec = (size_t)(lp.out0 + h);
     const double* in = stage + rec * kStageDoubles;
-    const StageEvView V{in + kStEv, smem + lane};
+    // lanes >= kBetasHyps (a build with fewer hypotheses per wave) mirror lane % kBetasHyps and
+    // write the same values into the same LDS column
+    const StageEvView V{in + kStEv, smem + lane % kBetasHyps};
+    RSC_SOLVE_STAMP(1, 0);
     compute_L_6x10(V);
     {
         double cws[4][3];
@@ -677,10 +946,13 @@ __device__ __forceinline__ void pnp_betas_wave_body(const DevPnP* __restrict__ p
         V.rho(3) = d2(1, 2); V.rho(4) = d2(1, 3); V.rho(5) = d2(2, 3);
     }
     double betas[4] = {0.0, 0.0, 0.0, 0.0};
+    RSC_SOLVE_STAMP(1, 1);
     if (apx == 0) find_betas<1>(V, betas);
     else if (apx == 1) find_betas<2>(V, betas);
     else find_betas<3>(V, betas);
+    RSC_SOLVE_STAMP(1, 2);
     gauss_newton(V, betas);
+    RSC_SOLVE_STAMP(1, 3);
     // the hypothesis' points and alphas are read only now (live across the solves above they pushed
     // the wave past 256 VGPRs: scratch spills, round 1)
     HypStore<NS> st;
@@ -698,7 +970,9 @@ __device__ __forceinline__ void pnp_betas_wave_body(const DevPnP* __restrict__ p
     const Intrinsics K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy};
     const double pw0[3] = {in[kStCws + 0], in[kStCws + 1], in[kStCws + 2]};
     double R[3][3], t[3];
+    RSC_SOLVE_STAMP(1, 4);
     const double err = compute_R_and_t(st, K, V, betas, pw0, R, t);
+    RSC_SOLVE_STAMP(1, 5);
     float pz[12];
     RSC_UNROLL for (int r = 0; r < 3; ++r)
         RSC_UNROLL for (int c = 0; c < 3; ++c) pz[3 * r + c] = (float)R[r][c];
@@ -713,6 +987,10 @@ __device__ __forceinline__ void pnp_betas_wave_body(const DevPnP* __restrict__ p
     unsigned prev = 0;
     if (lane == 0) prev = __hip_atomic_fetch_add(bctr + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     prev = __builtin_amdgcn_readlane(prev, 0);
+    RSC_SOLVE_STAMP(1, 6);
+#if RSC_SOLVE_STAMPS
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) g_solve_stamps[1][blockIdx.x][7] = (uint64_t)apx | ((uint64_t)g << 8);
+#endif
     if (prev != 2) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -129,3 +129,23 @@ def test_device_qr_solve_q19_matches_oracle():
         assert np.array_equal(X[i].view(np.uint64), want.view(np.uint64)), (i, X[i], want)
         n_singular += not ok_want
     assert n_singular >= 4
+
+
+def test_scan_reciprocal_is_ieee_in_its_range():
+    """The PnP scan's invZc = 1/Zc (PnPsolver.cpp:251) is v_rcp_f32 + one FMA Newton step
+    (kernels.hip pnp_inlier2), used only for 2^-126 <= |z| <= 2^125 (the scan redoes a hypothesis
+    with the IEEE division when a depth falls outside).  Here: every significand of one binade in
+    both signs, both ends of the range, and random floats across the range, against IEEE float32
+    1/z (numpy) bit for bit.  The whole 2^32 sweep is tools/rcp_exhaustive.hip
+    (profiles/r05/rcp_exhaustive_r5f.txt: 0 mismatches for exponent fields 1..252)."""
+    rng = np.random.default_rng(5)
+    mant = np.arange(1 << 23, dtype=np.uint32)
+    pats = [mant | np.uint32(127 << 23), mant[::7] | np.uint32(1 << 23), mant[::7] | np.uint32(252 << 23),
+            rng.integers(1 << 23, 253 << 23, 2_000_000, dtype=np.uint32)]
+    bits = np.concatenate(pats)
+    bits = np.concatenate([bits, bits[: 1 << 23] | np.uint32(0x80000000)])
+    z = bits.view(np.float32)
+    dev = gpu_ctx().selftest_math("rcp_scan", z.astype(np.float64)).astype(np.float32)
+    ref = np.float32(1.0) / z
+    bad = np.flatnonzero(dev.view(np.uint32) != ref.view(np.uint32))
+    assert bad.size == 0, (bad.size, z[bad[:5]], dev[bad[:5]], ref[bad[:5]])

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase wall clock of the config-2 hypothesis solve across all workgroups, from
+rsc_diag_solve_phase_stamps (a library built with RSC_SOLVE_STAMPS=1: make -C tools solve_stamps_lib,
+RSC_LIBRSC=tools/bin/librsc_solvestamps.so).  Eigen stage: per workgroup (20 hypotheses) the
+phases sample + MtM / tridiagonal / Q / chase + store; betas stage: per wave (64 hypotheses, one
+approximation) L + rho / find_betas / Gauss-Newton / row loads / R and t / hand-off, by
+approximation.  Times in us (10 ns ticks), median / 90th percentile / max over workgroups, and
+the spread of the workgroups' start and end times within the launch."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "orb-slam2-optimized_amd"), ROOT]
+import numpy as np  # noqa: E402
+from rsc import engine, workloads as wl  # noqa: E402
+
+scenes = wl.config2_scenes()
+ctx = engine.Context(0)
+batch = engine.SolverBatch([engine.PnPSolver(ctx, sc, 1) for sc in scenes])
+for s in range(3):
+    batch.reset(wl.config2_seeds(s))
+    batch.set_ransac_parameters(*wl.RELOC)
+    batch.iterate_raw(300)
+st = np.zeros(2 * 4096 * 8, np.uint64)
+engine._check(engine.load_library().rsc_diag_solve_phase_stamps(ctx.h, st, st.size), "solve stamps")
+st = st.reshape(2, 4096, 8).astype(np.int64)
+
+
+def stats(x):
+    return f"med {np.median(x):7.2f}  p90 {np.percentile(x, 90):7.2f}  max {x.max():7.2f}"
+
+
+e = st[0][st[0][:, 0] > 0]
+t0 = min(e[:, 0].min(), st[1][st[1][:, 0] > 0][:, 0].min() if (st[1][:, 0] > 0).any() else e[:, 0].min())
+print(f"eigen stage: {len(e)} workgroups; start spread {(e[:, 0].max() - e[:, 0].min()) / 100:.2f} us, "
+      f"launch span {(e[:, 4].max() - e[:, 0].min()) / 100:.2f} us")
+for k, name in enumerate(["sample + MtM", "tridiagonal", "Q accumulate", "chase + store"]):
+    print(f"  {name:14s} {stats(np.diff(e[:, k:k + 2], axis=1)[:, 0] / 100)}")
+print(f"  {'total':14s} {stats((e[:, 4] - e[:, 0]) / 100)}")
+b = st[1][st[1][:, 0] > 0]
+apx = b[:, 7] & 255
+print(f"betas stage: {len(b)} waves; start spread {(b[:, 0].max() - b[:, 0].min()) / 100:.2f} us, "
+      f"launch span {(b[:, 6].max() - b[:, 0].min()) / 100:.2f} us (first eig start -> last betas hand-off "
+      f"{(b[:, 6].max() - t0) / 100:.2f} us)")
+for a in range(3):
+    ba = b[apx == a]
+    print(f" approximation {a + 1}: {len(ba)} waves")
+    for k, name in enumerate(["L + rho", "find_betas", "Gauss-Newton", "row loads", "R and t", "hand-off"]):
+        print(f"  {name:14s} {stats(np.diff(ba[:, k:k + 2], axis=1)[:, 0] / 100)}")
+    print(f"  {'total':14s} {stats((ba[:, 6] - ba[:, 0]) / 100)}")
