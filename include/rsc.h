@@ -468,10 +468,12 @@ int rsc_kfdb_state(rsc_kfdb* db, int kf, uint64_t* q, int32_t* w, float* s);
  * wave w: betas + Gauss-Newton, pc0 sum, M sum + Horn, error sum (zeros unless built with
  * RSC_REFINE_STAMPS=1). */
 int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
-/* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP hypothesis solve, [2][wg < 4096][8]:
+/* Diagnostic: wall-clock (100 MHz) phase stamps of the last PnP hypothesis solve, [3][wg < 4096][8]:
  * [0] eigen stage per workgroup (entry, sample + MtM, tridiagonal, Q, chase + store), [1] betas stage
  * per wave (entry, L + rho, find_betas, Gauss-Newton, row loads, R and t, hand-off; [7] = the
- * approximation | 256 * group) (zeros unless built with RSC_SOLVE_STAMPS=1; cap >= 65536). */
+ * approximation | 256 * group), [2] inside find_betas' Jacobi SVD per betas wave (QR preconditioner,
+ * U formed, sweeps done, then k = the SVD's columns) (zeros unless built with RSC_SOLVE_STAMPS=1;
+ * cap >= 98304). */
 int rsc_diag_solve_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
 /* Diagnostic: wall-clock (100 MHz) ticks of the last PoseOptimization launch, [frame < 64][8]:
  * fused passes (ticks), number of passes + (their active edges << 24), re-classification, whole kernel,

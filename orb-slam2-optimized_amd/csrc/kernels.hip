@@ -16,9 +16,6 @@
 // Reference: src/PnPsolver.cpp, src/Sim3Solver.cpp (see rsc_core.h for the arithmetic contract).
 #include <hip/hip_runtime.h>
 #include <climits>
-#include "rsc_core.h"
-#include "rsc_epnp.h"
-#include "rsc_sim3.h"
 
 // Diagnostic phase stamps of the refine kernel (rsc_diag_refine_phase_stamps), compiled in only with
 // RSC_REFINE_STAMPS=1: [job][0..7] = entry, compaction, control points, MtM, eigen, betas, check,
@@ -39,14 +36,27 @@ __device__ uint64_t g_refine_stamps[64][24];
 #define RSC_SOLVE_STAMPS 0
 #endif
 namespace rsc {
-__device__ uint64_t g_solve_stamps[2][4096][8];
+__device__ uint64_t g_solve_stamps[3][4096][8];
 }
 #if RSC_SOLVE_STAMPS
+// inside jacobi_svd_solve_6xk (find_betas): plane 2, [wave][j], j = QR done, U formed, sweeps done,
+// [wave][3] = k (only the betas kernel's single-wave workgroups, blockIdx.x < 4096)
+#define RSC_JSVD_STAMP(k, j)                                                                           \
+    do {                                                                                               \
+        if (blockIdx.x < 4096 && (threadIdx.x & 63) == 0 && blockDim.x == 64) {                       \
+            ::rsc::g_solve_stamps[2][blockIdx.x][j] = wall_clock64();                                  \
+            ::rsc::g_solve_stamps[2][blockIdx.x][3] = (k);                                             \
+        }                                                                                              \
+    } while (0)
 #define RSC_SOLVE_STAMP(st, k)                                                                         \
     do {                                                                                               \
         if (blockIdx.x < 4096 && (threadIdx.x & 63) == 0) ::rsc::g_solve_stamps[st][blockIdx.x][k] = wall_clock64(); \
     } while (0)
 #endif
+// (the stamp macros above are defined before the headers that expand them)
+#include "rsc_core.h"
+#include "rsc_epnp.h"
+#include "rsc_sim3.h"
 #if RSC_REFINE_STAMPS
 #define RSC_EIG_PHASE(k)                                                                               \
     do {                                                                                               \
@@ -1088,7 +1098,7 @@ hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchPr
 }
 
 hipError_t read_solve_stamps(uint64_t* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solve_stamps), sizeof(uint64_t) * 2 * 4096 * 8, 0, hipMemcpyDeviceToHost);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solve_stamps), sizeof(uint64_t) * 3 * 4096 * 8, 0, hipMemcpyDeviceToHost);
 }
 
 hipError_t read_refine_stamps(uint64_t* out) {

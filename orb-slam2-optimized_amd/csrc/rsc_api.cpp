@@ -222,8 +222,9 @@ struct rsc_context {
     // RSC_EIG_ROWS=W or rsc_context_set_eig_rows overrides (0: lane pairs always)
     int eig_rows_max_wgs = kEigRowsDefaultWgs;
     // eigen stages beyond the rows form's range: split form (chase and Q rotations on two waves,
-    // pnp_eig_split_kernel) or the pair form (env RSC_EIG_SPLIT=0/1)
-    bool eig_split = false;
+    // pnp_eig_split_kernel; config-2 eigen stage 119 -> 114 us, profiles/r05/split_ab_r5q.jsonl) or
+    // the pair form (env RSC_EIG_SPLIT=0)
+    bool eig_split = true;
     // host wait for a speculation round's results: spin on a completion flag in pinned host memory
     // (written by signal_kernel after the round) instead of hipStreamSynchronize's wake-up; env
     // RSC_SPIN_WAIT=0/1 (stream_wait)
@@ -2539,7 +2540,7 @@ int rsc_diag_refine_phase_stamps(rsc_context* C, uint64_t* out, int cap) {
 }
 
 int rsc_diag_solve_phase_stamps(rsc_context* C, uint64_t* out, int cap) {
-    if (!C || !out || cap < 2 * 4096 * 8) return RSC_ERR_ARG;
+    if (!C || !out || cap < 3 * 4096 * 8) return RSC_ERR_ARG;
     RSC_HIP(hipStreamSynchronize(C->stream));
     RSC_HIP(read_solve_stamps(out));
     return RSC_OK;

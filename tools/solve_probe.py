@@ -21,9 +21,9 @@ for s in range(3):
     batch.reset(wl.config2_seeds(s))
     batch.set_ransac_parameters(*wl.RELOC)
     batch.iterate_raw(300)
-st = np.zeros(2 * 4096 * 8, np.uint64)
+st = np.zeros(3 * 4096 * 8, np.uint64)
 engine._check(engine.load_library().rsc_diag_solve_phase_stamps(ctx.h, st, st.size), "solve stamps")
-st = st.reshape(2, 4096, 8).astype(np.int64)
+st = st.reshape(3, 4096, 8).astype(np.int64)
 
 
 def stats(x):
@@ -48,3 +48,17 @@ for a in range(3):
     for k, name in enumerate(["L + rho", "find_betas", "Gauss-Newton", "row loads", "R and t", "hand-off"]):
         print(f"  {name:14s} {stats(np.diff(ba[:, k:k + 2], axis=1)[:, 0] / 100)}")
     print(f"  {'total':14s} {stats((ba[:, 6] - ba[:, 0]) / 100)}")
+j = st[2][st[2][:, 0] > 0]
+if len(j):
+    print("find_betas' Jacobi SVD (from the L + rho stamp of the same wave):")
+    for k in (4, 3, 5):
+        jj = j[j[:, 3] == k]
+        if not len(jj):
+            continue
+        idx = np.flatnonzero((st[2][:, 0] > 0) & (st[2][:, 3] == k))
+        fb0 = st[1][idx, 1]  # find_betas entry
+        print(f" k = {k}: {len(jj)} waves")
+        for name, x in [("QR precond.", jj[:, 0] - fb0), ("U formed", jj[:, 1] - jj[:, 0]),
+                        ("Jacobi sweeps", jj[:, 2] - jj[:, 1]), ("solve + betas", st[1][idx, 2] - jj[:, 2])]:
+            print(f"  {name:14s} {stats(x / 100)}")
+

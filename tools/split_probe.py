@@ -17,9 +17,9 @@ for s in range(3):
     batch.reset(wl.config2_seeds(s))
     batch.set_ransac_parameters(*wl.RELOC)
     batch.iterate_raw(300)
-st = np.zeros(2 * 4096 * 8, np.uint64)
+st = np.zeros(3 * 4096 * 8, np.uint64)
 engine._check(engine.load_library().rsc_diag_solve_phase_stamps(ctx.h, st, st.size), "solve stamps")
-e = st.reshape(2, 4096, 8)[0].astype(np.int64)
+e = st.reshape(3, 4096, 8)[0].astype(np.int64)
 e = e[e[:, 0] > 0]
 
 
