@@ -1207,12 +1207,15 @@ def headline_roofline(args, r):
     S_h = op_count("pnp")
     tf = per_launch_hyps * S_h / (solve_ms * 1e-3) / 1e12 if (S_h and solve_ms > 0) else None
     meas = traffic["epnp_launch_set_bytes"] if traffic else None
+    # the eigen-stage form the library runs on launches of this size (rsc_api.cpp: split form unless
+    # RSC_EIG_SPLIT=0; the rows form only for <= 64 workgroups)
+    eig_kernel = "pnp_eig_group_kernel" if os.environ.get("RSC_EIG_SPLIT", "1") == "0" else "pnp_eig_split_kernel"
     roof = {"bound": "fp64-latency",
             "achieved": round(tf, 4) if tf else None, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / FP64_PEAK_TFLOPS, 5) if tf else None,
             "traffic": round(meas) if meas else None,
-            "kernel": "EPnP hypothesis solve: pnp_eig_group_kernel<4> + pnp_betas_kernel<4> "
-                      f"({per_launch_hyps} hypotheses per launch)",
+            "kernel": (f"EPnP hypothesis solve: {eig_kernel}<4> + pnp_betas_kernel<4> "
+                       f"({per_launch_hyps} hypotheses per launch)"),
             "algorithmic_flops_per_launch": round(per_launch_hyps * S_h) if S_h else None,
             "S_h_fp64_flops_per_hypothesis": S_h,
             "ms_per_launch": {"eig": round(eig_ms, 4), "betas": round(solve_ms - eig_ms, 4),

@@ -97,31 +97,6 @@ RSC_HD double recip_unit(double u) {
     return 1.0 / u;
 #endif
 }
-// IEEE n / d: the compiler's division without its range scaling (v_div_scale, v_div_fmas) and its
-// special-value fix-up (v_div_fixup) — the same core instructions, so the same bits whenever those
-// steps are the identity, which holds for normal n and d with |n|, |d| in [2^-500, 2^500] (mid_mag:
-// no operand near the exponent limits, a normal quotient).  Callers check mid_mag and fall back to
-// the IEEE form otherwise (jacobi_svd_solve_6xk_fast).  sqrt_unit and recip_unit above are the
-// same cores for x in [1, 2^1000] and u in [1, 2^500] (no scaling below 2^-767 or fix-up of 0 / inf
-// is reached there).
-RSC_HD double div_core(double n, double d) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    double r = __builtin_amdgcn_rcp(d);
-    double e = __builtin_fma(-d, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    e = __builtin_fma(-d, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    const double q = n * r;
-    const double rem = __builtin_fma(-d, q, n);
-    return __builtin_fma(rem, r, q);
-#else
-    return n / d;
-#endif
-}
-RSC_HD bool mid_mag(double x) {
-    const double a = fabs(x);
-    return (a >= 0x1p-500) & (a <= 0x1p500);
-}
 RSC_HD float sqrt_unit(float x) { return sqrtf(x); }
 RSC_HD float recip_unit(float u) { return 1.0f / u; }
 RSC_HD float rsqrt_(float x) { return sqrtf(x); }
@@ -665,12 +640,8 @@ RSC_HD bool sym_eig12(const LaneMat& M) {
     do {                     \
     } while (0)
 #endif
-// FAST: the Jacobi sweeps' 2x2 SVD divides and takes roots with the short cores (div_core, sqrt_unit,
-// recip_unit), each operand checked with mid_mag; *bad is set for a lane that had one outside, and
-// the solve is redone in the IEEE form (jacobi_svd_solve_6xk_fast below).  Same bits either way for
-// every lane with *bad clear.
-template <int k, bool FAST = false>
-RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6], double (&x)[k], bool* bad = nullptr) {
+template <int k>
+RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6], double (&x)[k]) {
     constexpr int rows = 6;
     const double eps = lim<double>::eps();
     const double precision = 2.0 * eps;
@@ -825,21 +796,10 @@ RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6]
                     const double t = m00 + m11;
                     const double d = m10 - m01;
                     const bool dz = rabs(d) < considerAsZero;
-                    double u, tmp, s1, c1;
-                    if (FAST) {
-                        // dz: the quotients are selected away; otherwise t, d, u in range make
-                        // 1 + u^2 in [1, 2^1000] and tmp in [1, 2^500]
-                        u = div_core(t, d);
-                        *bad |= !dz & !(mid_mag(t) & mid_mag(d) & mid_mag(u));
-                        tmp = sqrt_unit(1.0 + u * u);
-                        s1 = dz ? 0.0 : div_core(1.0, tmp);
-                        c1 = dz ? 1.0 : div_core(u, tmp);
-                    } else {
-                        u = t / d;
-                        tmp = sqrt(1.0 + u * u);
-                        s1 = dz ? 0.0 : 1.0 / tmp;
-                        c1 = dz ? 1.0 : u / tmp;
-                    }
+                    const double u = t / d;
+                    const double tmp = sqrt(1.0 + u * u);
+                    const double s1 = dz ? 0.0 : 1.0 / tmp;
+                    const double c1 = dz ? 1.0 : u / tmp;
                     {
                         const bool rot = !((c1 == 1.0) & (s1 == 0.0));
                         const double x0 = m00, y0 = m10, x1 = m01, y1 = m11;
@@ -852,20 +812,9 @@ RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6]
                     {
                         const double deno = 2.0 * rabs(m01);
                         const bool nz = deno < considerAsZero;
-                        double tau, w, tt;
-                        if (FAST) {
-                            // nz: selected away; otherwise tau in range makes tau^2 + 1 in
-                            // [1, 2^1000] and |tau +- w| in [1, 2^501]
-                            const double dm = m00 - m11;
-                            tau = div_core(dm, deno);
-                            *bad |= !nz & !(mid_mag(dm) & mid_mag(deno) & mid_mag(tau));
-                            w = sqrt_unit(tau * tau + 1.0);
-                            tt = div_core(1.0, tau > 0.0 ? tau + w : tau - w);
-                        } else {
-                            tau = (m00 - m11) / deno;
-                            w = sqrt(tau * tau + 1.0);
-                            tt = 1.0 / (tau > 0.0 ? tau + w : tau - w);
-                        }
+                        const double tau = (m00 - m11) / deno;
+                        const double w = sqrt(tau * tau + 1.0);
+                        const double tt = 1.0 / (tau > 0.0 ? tau + w : tau - w);
                         const double sign_t = tt > 0.0 ? 1.0 : -1.0;
                         const double nn = recip_unit(sqrt_unit(tt * tt + 1.0));
                         sr = nz ? 0.0 : -sign_t * (m01 / rabs(m01)) * rabs(tt) * nn;
@@ -959,20 +908,6 @@ RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6]
     }
 }
 
-// find_betas' solve (PnPsolver.cpp:520-602): the short-core Jacobi sweeps, redone in the IEEE form
-// when a lane of the wave met an operand outside their range (never on the config-2 workloads;
-// degenerate inputs such as exact cancellations take it).  Bit-identical to jacobi_svd_solve_6xk.
-template <int k>
-RSC_HD void jacobi_svd_solve_6xk_fast(const double (&A)[6][k], const double (&b)[6], double (&x)[k]) {
-    bool bad = false;
-    jacobi_svd_solve_6xk<k, true>(A, b, x, &bad);
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (__builtin_expect(__any(bad), 0))
-#else
-    if (bad)
-#endif
-        jacobi_svd_solve_6xk<k, false>(A, b, x);
-}
 
 // Matrix3d::inverse (cofactors); result(r,c) = cofactor(c,r) * invdet.
 RSC_HD void inverse3(const double (&m)[3][3], double (&o)[3][3]) {

@@ -289,7 +289,7 @@ RSC_HD void find_betas(const SV& S, double (&betas)[4]) {
         RSC_UNROLL for (int r = 0; r < 6; ++r) {
             A[r][0] = S.L(r, 0); A[r][1] = S.L(r, 1); A[r][2] = S.L(r, 3); A[r][3] = S.L(r, 6);
         }
-        jacobi_svd_solve_6xk_fast<4>(A, rho, b4);
+        jacobi_svd_solve_6xk<4>(A, rho, b4);
         if (b4[0] < 0) {
             betas[0] = sqrt(-b4[0]);
             betas[1] = -b4[1] / betas[0];
@@ -304,7 +304,7 @@ RSC_HD void find_betas(const SV& S, double (&betas)[4]) {
     } else if (which == 2) {
         double A[6][3], b3[3];
         RSC_UNROLL for (int r = 0; r < 6; ++r) { A[r][0] = S.L(r, 0); A[r][1] = S.L(r, 1); A[r][2] = S.L(r, 2); }
-        jacobi_svd_solve_6xk_fast<3>(A, rho, b3);
+        jacobi_svd_solve_6xk<3>(A, rho, b3);
         if (b3[0] < 0) {
             betas[0] = sqrt(-b3[0]);
             betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
@@ -319,7 +319,7 @@ RSC_HD void find_betas(const SV& S, double (&betas)[4]) {
         double A[6][5], b5[5];
         RSC_UNROLL for (int r = 0; r < 6; ++r)
             RSC_UNROLL for (int c = 0; c < 5; ++c) A[r][c] = S.L(r, c);
-        jacobi_svd_solve_6xk_fast<5>(A, rho, b5);
+        jacobi_svd_solve_6xk<5>(A, rho, b5);
         if (b5[0] < 0) {
             betas[0] = sqrt(-b5[0]);
             betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;

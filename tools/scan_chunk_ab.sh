@@ -1,5 +1,5 @@
 set -e
-OUT=$GRAFT_REPO_ROOT/gpurun_out/r5g
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-scanab}
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 for v in 2048 1000 500 2048 1000 500; do
