@@ -31,7 +31,7 @@ for k in sorted(set(fetch) | set(write)):
     rd = 2.0 * fetch.get(k, 0.0) * 1024.0
     wr = write.get(k, 0.0) * 1024.0
     kernels[k] = {"read_bytes": rd, "write_bytes": wr, "bytes": rd + wr, "dispatches": nf.get(k, nw.get(k, 0))}
-path = [k for k in kernels if k.replace("rsc::", "").startswith(("pnp_eig_group_kernel", "pnp_eig_quad_kernel", "pnp_betas_kernel", "pnp_scan_kernel"))]
+path = [k for k in kernels if k.replace("rsc::", "").startswith(("pnp_eig_group_kernel", "pnp_eig_split_kernel", "pnp_eig_quad_kernel", "pnp_betas_kernel", "pnp_scan_kernel"))]
 out = {"kernels": kernels, "epnp_launch_set": path,
        "epnp_launch_set_bytes": sum(kernels[k]["bytes"] for k in path),
        "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB",
