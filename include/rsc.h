@@ -60,9 +60,13 @@ int rsc_context_enable_timing(rsc_context* ctx, int enable);
 /* Eigen-stage form of the EPnP hypothesis solve (no effect on results): launches whose eigen stage
  * has at most max_workgroups workgroups of 20 hypotheses run it in the Refine's rows form (a 12-lane
  * group per hypothesis, Q rows in VGPRs: lower latency for small, latency-bound launches such as one
- * relocalization event); larger launches use lane pairs.  Default 64 (env RSC_EIG_ROWS overrides);
- * 0 = lane pairs always. */
+ * relocalization event); larger launches use the split form (below).  Default 64 (env RSC_EIG_ROWS
+ * overrides); 0 = never the rows form. */
 int rsc_context_set_eig_rows(rsc_context* ctx, int max_workgroups);
+/* Eigen-stage form of the launches the rows form does not take: 1 (default; env RSC_EIG_SPLIT) the
+ * split form — the QR chase and the Q rotations on two waves of one SIMD (pnp_eig_split_kernel) — or
+ * 0 the lane-pair form (pnp_eig_group_kernel).  Both are bit-identical. */
+int rsc_context_set_eig_split(rsc_context* ctx, int on);
 /* Self-test of the device libm restatement (rsc_math.h, used by Sim3 angles, MLPnP, SearchBySim3):
  * out[i] = f(x[i]) computed ON THE GPU, f = 0 sin, 1 cos, 2 acos, 3 cbrt, 4 log, 5 logf
  * ((float)x[i] in, float result widened); and the eigen-solver chase's short-chain forms

@@ -1280,6 +1280,12 @@ int rsc_context_set_eig_rows(rsc_context* C, int max_workgroups) {
     return RSC_OK;
 }
 
+int rsc_context_set_eig_split(rsc_context* C, int on) {
+    if (!C) return RSC_ERR_ARG;
+    C->eig_split = on != 0;
+    return RSC_OK;
+}
+
 int rsc_selftest_math(rsc_context* C, int fn, const double* x, int n, double* out) {
     if (!C || fn < 0 || fn > 13 || n < 0 || (n > 0 && (!x || !out)) || (fn == 10 && n % 34)) return RSC_ERR_ARG;
     if (n == 0) return RSC_OK;

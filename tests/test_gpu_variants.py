@@ -5,7 +5,10 @@ default path's bits, so each is checked against the oracle exactly like the defa
   pnp_eig_rows_body: a 12-lane group per hypothesis, Q rows in VGPRs) — the default for small
   launches since round 5 (<= 64 workgroups), forced here onto large ones too: every hypothesis of
   exhaustive batches (min sets 4..6, a planar scene for the NaN path), and a relocalization event
-  stream; and the lane-pair form forced onto small launches (set_eig_rows(0)).
+  stream;
+* the split form (`rsc_context_set_eig_split`, pnp_eig_split_body: chase wave + row wave per unit,
+  the default beyond the rows form's range) and the lane-pair form, each forced onto every launch,
+  small ones included (set_eig_rows(0)): the same batches and event stream.
 First run on hardware in round 5 (profiles/r05/gpu_tests_variants_r5b.txt)."""
 import numpy as np
 import pytest
@@ -23,17 +26,19 @@ def _nan_equal(a, b):
     return np.array_equal(na, nb) and np.array_equal(a.view(np.uint32)[~na], b.view(np.uint32)[~nb])
 
 
-def _rows_ctx(rows=True):
+def _rows_ctx(rows=True, split=True):
     from rsc import engine
     c = engine.Context(0)
-    c.set_eig_rows(1 << 20 if rows else 0)  # every launch in the rows form / in lane pairs
+    c.set_eig_rows(1 << 20 if rows else 0)  # every launch in the rows form / in the split or pair form
+    c.set_eig_split(split)
     return c
 
 
+@pytest.mark.parametrize("form", ["rows", "split", "pairs"])
 @pytest.mark.parametrize("ms", [4, 5, 6])
-def test_eig_rows_every_hypothesis(ms):
+def test_eig_rows_every_hypothesis(ms, form):
     from rsc import engine
-    c = _rows_ctx()
+    c = _rows_ctx(form == "rows", form == "split")
     rng = np.random.default_rng(900 + ms)
     scenes = [synth.make_pnp_scene(rng, 700, 0.4), synth.make_pnp_scene(rng, 1900, 0.35),
               synth.make_planar_pnp_scene(rng, 500, 0.4, "floor"), synth.make_pnp_scene(rng, 230, 0.45)]
@@ -59,11 +64,11 @@ def test_eig_rows_every_hypothesis(ms):
     c.close()
 
 
-@pytest.mark.parametrize("rows", [True, False])
-def test_eig_rows_reloc_events(rows):
+@pytest.mark.parametrize("form", ["rows", "split", "pairs"])
+def test_eig_rows_reloc_events(form):
     from rsc import engine, events as rev
     import events_oracle as eo
-    c = _rows_ctx(rows)
+    c = _rows_ctx(form == "rows", form == "split")
     evs = [ev for ev in rev.make_event_stream(seed=23, n_reloc=8, n_loop=0) if ev.kind == "reloc"]
     eb = engine.EventBatch([[engine.PnPSolver(c, x, s) for x, s in zip(rev.event_inputs(ev), ev.seeds)] for ev in evs])
     eb.batch.set_ransac_parameters(*rev.RELOC_PARAMS)
