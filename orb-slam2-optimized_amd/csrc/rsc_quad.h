@@ -764,37 +764,47 @@ __device__ __forceinline__ void pnp_eig_split_body(const DevPnP* __restrict__ pr
     }
     __syncthreads();  // A: MtM (lower triangle) in T
     RSC_SPLIT_STAMP(1);
-    // ---- B-C: the unit's two waves, lane quads ----
-    const int g4 = (row_wave ? 16 : 0) + (lane >> 2), q4 = lane & 3;
-    const bool quad = unit_ok && g4 < HPW;
-    double* T4 = Tu + (quad ? g4 : 0) * kQuadRegion;
-    double* E4 = T4 + kQuadT;
+    // ---- B-C: scale, Householder tridiagonalisation, Q accumulation ----
+    // RSC_SPLIT_BC_LANES 4: lane quads over the unit's two waves (hypotheses 0-15 in the chase wave,
+    // 16-19 in the row wave); 2: lane pairs in the chase wave alone (lanes 0-39; the row wave only
+    // passes the barriers, so the chase wave has the SIMD's issue to itself).  Same values either way
+    // (group_eig12_ev4's forms are bit-identical).
+#ifndef RSC_SPLIT_BC_LANES
+#define RSC_SPLIT_BC_LANES 4
+#endif
+    constexpr int LB = RSC_SPLIT_BC_LANES, RB = 12 / LB;
+    static_assert(LB == 2 || LB == 4, "B-C in lane pairs or quads");
+    const int gB = (LB == 4) ? (row_wave ? 16 : 0) + (lane >> 2) : (row_wave ? HPW : lane >> 1);
+    const int qB = lane & (LB - 1);
+    const bool grp = unit_ok && gB < HPW;
+    double* TB = Tu + (grp ? gB : 0) * kQuadRegion;
+    double* EB = TB + kQuadT;
     double hC[11];
-    if (quad) {
+    if (grp) {
         double diag[12], sub[11];
-        double A[3][12];
-        RSC_UNROLL for (int j = 0; j < 3; ++j) {
-            const int R = 4 * j + q4;
-            RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = T4[(R >= c) ? R * 12 + c : c * 12 + R];
+        double A[RB][12];
+        RSC_UNROLL for (int j = 0; j < RB; ++j) {
+            const int R = LB * j + qB;
+            RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = TB[(R >= c) ? R * 12 + c : c * 12 + R];
         }
-        const double scale = group_scale<4>(A, q4);
-        RSC_UNROLL for (int j = 0; j < 3; ++j)
+        const double scale = group_scale<LB>(A, qB);
+        RSC_UNROLL for (int j = 0; j < RB; ++j)
             RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = A[j][c] / scale;
         __builtin_amdgcn_wave_barrier();
-        group_tridiag<4>(A, q4, E4, diag, sub, hC);
-        if (q4 == 0) {
-            double* ds = Du + g4 * kSplitDsub;
+        group_tridiag<LB>(A, qB, EB, diag, sub, hC);
+        if (qB == 0) {
+            double* ds = Du + gB * kSplitDsub;
             RSC_UNROLL for (int i = 0; i < 12; ++i) ds[i] = diag[i];
             RSC_UNROLL for (int i = 0; i < 11; ++i) ds[12 + i] = sub[i];
         }
     }
-    __syncthreads();  // B: every lane of a quad has read T; E holds the Householder vectors
+    __syncthreads();  // B: every lane of a group has read T; E holds the Householder vectors
     RSC_SPLIT_STAMP(2);
-    if (quad) {
-        double Qc[3][12];
-        group_accumulate<4>(Qc, q4, E4, hC);
-        RSC_UNROLL for (int j = 0; j < 3; ++j)
-            RSC_UNROLL for (int r = 0; r < 12; ++r) T4[r * 12 + 4 * j + q4] = Qc[j][r];
+    if (grp) {
+        double Qc[RB][12];
+        group_accumulate<LB>(Qc, qB, EB, hC);
+        RSC_UNROLL for (int j = 0; j < RB; ++j)
+            RSC_UNROLL for (int r = 0; r < 12; ++r) TB[r * 12 + LB * j + qB] = Qc[j][r];
     }
     __syncthreads();  // C: Q row-major in T, (diag, sub) in the slab; E is read by no one any more
     RSC_SPLIT_STAMP(3);
