@@ -656,6 +656,10 @@ constexpr int kRingPerm = 48;      // E[48..49]: the four sorted column indices 
 constexpr int kSplitDsub = 24;     // doubles per hypothesis of the (diag, sub) slab
 constexpr int kSplitHyps = kSplitUnits * 20;
 
+// s_sleep argument between polls of a pub / ack flag (0: poll back to back)
+#ifndef RSC_SPLIT_SLEEP
+#define RSC_SPLIT_SLEEP 1
+#endif
 constexpr int kSplitDone = 1 << 30;    // `pub` flag: the chase has ended (low bits: its steps)
 constexpr int kSplitSpinLimit = 1 << 24;  // polls before a wait gives up (never reached; no hang)
 
@@ -666,7 +670,9 @@ __device__ __forceinline__ int split_wait(int* flag, Pred pred) {
     for (int it = 0; it < kSplitSpinLimit; ++it) {
         v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (pred(v)) break;
-        __builtin_amdgcn_s_sleep(1);
+#if RSC_SPLIT_SLEEP
+        __builtin_amdgcn_s_sleep(RSC_SPLIT_SLEEP);
+#endif
     }
     return v;
 }
