@@ -193,6 +193,10 @@ struct qr_has_sweep_end<Q, decltype((void)std::declval<Q&>().sweep_end())> { sta
 // Q bit-identical otherwise).  computeFromTridiagonal_impl + sort.
 // Returns Eigen's "Success".  perm: the sort's column permutation (identity when not converged,
 // as Eigen skips the sort then); the caller applies it to its eigenvector storage.
+// How often tridiag_qr tests for a non-finite block (steps; 1 = every step).
+#ifndef RSC_NAN_CHECK_EVERY
+#define RSC_NAN_CHECK_EVERY 8
+#endif
 template <typename S, int n, typename QApply>
 RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, int (&perm)[n]) {
     const int maxIterations = 30;
@@ -239,13 +243,18 @@ RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, int (&per
         // turns Q's columns start..end into NaN; every later sweep maps that state onto itself
         // (NaN in, NaN out; the block cannot change: its sub-diagonal never reads 0).  Ending after
         // this sweep with Eigen's NoConvergence (no sort) therefore returns Eigen's final state.
-        unsigned dnan = 0u, snan = 0u;
-        RSC_UNROLL for (int i = 0; i < n; ++i) dnan |= (diag[i] != diag[i]) ? (1u << i) : 0u;
-        RSC_UNROLL for (int i = 0; i < n - 1; ++i) snan |= (sub[i] != sub[i]) ? (1u << i) : 0u;
-        const unsigned lo = (1u << start) - 1u;
-        const unsigned blk_d = ((2u << end) - 1u) & ~lo, blk_s = ((1u << end) - 1u) & ~lo;
-        const bool dead = ((dnan & blk_d) == blk_d) & ((snan & blk_s) == blk_s);
-        iter = dead ? maxIterations * n : iter;  // the next loop test ends it, not converged
+        // The test runs on the first step and then every RSC_NAN_CHECK_EVERY-th: a dead block is a
+        // fixed point of the sweep, so the sweeps it runs before the next test leave the state
+        // as Eigen's (all running lanes are at the same step, so the branch is wave-uniform).
+        if ((unsigned)(iter - 1) % (unsigned)RSC_NAN_CHECK_EVERY == 0u) {
+            unsigned dnan = 0u, snan = 0u;
+            RSC_UNROLL for (int i = 0; i < n; ++i) dnan |= (diag[i] != diag[i]) ? (1u << i) : 0u;
+            RSC_UNROLL for (int i = 0; i < n - 1; ++i) snan |= (sub[i] != sub[i]) ? (1u << i) : 0u;
+            const unsigned lo = (1u << start) - 1u;
+            const unsigned blk_d = ((2u << end) - 1u) & ~lo, blk_s = ((1u << end) - 1u) & ~lo;
+            const bool dead = ((dnan & blk_d) == blk_d) & ((snan & blk_s) == blk_s);
+            iter = dead ? maxIterations * n : iter;  // the next loop test ends it, not converged
+        }
 #endif
         // ---- tridiagonal_qr_step(diag, sub, start, end) ----
         S dEm1 = S(0), dE = S(0), eE = S(0), dS = S(0), zS = S(0);
