@@ -276,9 +276,12 @@ RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, int (&per
         const S e2 = eE * eE;
         const S h = eig_hypot(td, e);
         const S mu_z = dE - rabs(e);
-        const S mu_u = dE - (e / (td + (td > S(0) ? S(1) : S(-1)))) * (e / h);
         const S mu_n = dE - e2 / (td + (td > S(0) ? h : -h));
-        const S mu = (td == S(0)) ? mu_z : ((e2 == S(0)) ? mu_u : mu_n);
+        S mu = (td == S(0)) ? mu_z : mu_n;
+        // e^2 underflowed (td != 0): the two-quotient form, behind a branch that a wave skips when
+        // none of its lanes needs it (its two divisions are otherwise wasted on every step)
+        if (__builtin_expect((td != S(0)) & (e2 == S(0)), 0))
+            mu = dE - (e / (td + (td > S(0) ? S(1) : S(-1)))) * (e / h);
         S x = dS - mu;
         S z = zS;
         RSC_UNROLL for (int k = 0; k < n - 1; ++k) {
