@@ -193,6 +193,10 @@ struct qr_has_sweep_end<Q, decltype((void)std::declval<Q&>().sweep_end())> { sta
 // Q bit-identical otherwise).  computeFromTridiagonal_impl + sort.
 // Returns Eigen's "Success".  perm: the sort's column permutation (identity when not converged,
 // as Eigen skips the sort then); the caller applies it to its eigenvector storage.
+// tridiag_qr reads diag[start], sub[start] by a select chain only when start > 0 (0: always).
+#ifndef RSC_QR_START0
+#define RSC_QR_START0 1
+#endif
 // How often tridiag_qr tests for a non-finite block (steps; 1 = every step).
 #ifndef RSC_NAN_CHECK_EVERY
 #define RSC_NAN_CHECK_EVERY 8
@@ -264,11 +268,25 @@ RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, int (&per
             dE = m ? diag[j] : dE;
             eE = m ? sub[j - 1] : eE;
         }
+#if RSC_QR_START0
+        // start is 0 until a sub-diagonal entry above the bottom block deflates: the select chain
+        // runs behind a branch that a wave skips while none of its lanes has start > 0
+        dS = diag[0];
+        zS = sub[0];
+        if (__builtin_expect(start != 0, 0)) {
+            RSC_UNROLL for (int j = 1; j < n - 1; ++j) {
+                const bool m = j == start;
+                dS = m ? diag[j] : dS;
+                zS = m ? sub[j] : zS;
+            }
+        }
+#else
         RSC_UNROLL for (int j = 0; j < n - 1; ++j) {
             const bool m = j == start;
             dS = m ? diag[j] : dS;
             zS = m ? sub[j] : zS;
         }
+#endif
         // Wilkinson shift; the three cases of Eigen are evaluated side by side and selected
         // (td == 0: mu - |e|; e^2 underflows: the two-quotient form; otherwise e^2/(td +- h))
         const S td = (dEm1 - dE) * S(0.5);
