@@ -9,7 +9,7 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fa
            -fno-gpu-flush-denormals-to-zero -Wall -Wno-unused-function -Wno-unused-variable
 HDRS = include/rsc.h $(wildcard $(CSRC)/*.h)
 
-all: $(LIBDIR)/librsc.so oracle hostemu facade_test
+all: $(LIBDIR)/librsc.so $(LIBDIR)/librsc_spin1.so oracle hostemu facade_test
 
 $(LIBDIR)/kernels.o: $(CSRC)/kernels.hip $(HDRS)
 	mkdir -p $(LIBDIR)
@@ -44,6 +44,15 @@ $(LIBDIR)/rsc_api.o: $(CSRC)/rsc_api.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(LIBDIR)/librsc.so: $(LIBDIR)/kernels.o $(LIBDIR)/mlpnp.o $(LIBDIR)/poseopt.o $(LIBDIR)/sim3opt.o $(LIBDIR)/orbmatch.o $(LIBDIR)/sim3match.o $(LIBDIR)/kfdb.o $(LIBDIR)/rsc_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
+
+# TEST-ONLY variant: the split eigen stage's hand-off waits give up after one poll, so the fault path
+# (split_wait -> fault word -> RSC_ERR_INTERNAL) runs on the device (tests/test_gpu_fault.py)
+$(LIBDIR)/kernels_spin1.o: $(CSRC)/kernels.hip $(HDRS)
+	mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -DRSC_SPLIT_SPIN_LIMIT=1 -c $< -o $@
+
+$(LIBDIR)/librsc_spin1.so: $(LIBDIR)/kernels_spin1.o $(LIBDIR)/mlpnp.o $(LIBDIR)/poseopt.o $(LIBDIR)/sim3opt.o $(LIBDIR)/orbmatch.o $(LIBDIR)/sim3match.o $(LIBDIR)/kfdb.o $(LIBDIR)/rsc_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 facade_test: $(LIBDIR)/facade_test

@@ -1350,9 +1350,13 @@ def main():
             dist.destroy_process_group()
         return
     value = hyps_total / dt
-    par = (f"{'strong' if args.strong else 'weak'}: candidates sharded over {world} rank(s) "
-           f"({'64 total' if args.strong else f'{args.candidates} per GPU'}), RCCL all-gather of "
-           f"{rdist.RECORD}-float result records per step")
+    if world > 1:
+        par = (f"{'strong' if args.strong else 'weak'}: candidates sharded over {world} ranks "
+               f"({'64 total' if args.strong else f'{args.candidates} per GPU'}), {args.dist_backend} "
+               f"all-gather of {rdist.RECORD}-float result records per step")
+    else:
+        par = ("single GPU, one rank: no exchange in the step (the all-gather of result records runs "
+               "only at N > 1; the world-1 RCCL check is outside the timed region)")
     out = {
         "metric": "RANSAC hypotheses/sec (EPnP relocalization batch, 2k corrs x 64 candidates)",
         "value": round(value, 1),

@@ -100,9 +100,9 @@ void* ora_pnp_create(int n, int n_points, const float* p2d, const float* p3dw, c
 }
 void ora_pnp_destroy(void* h) { delete static_cast<PnPOracle*>(h); }
 // Q3 event replays: the solver draws from the process-global libc rand(); ora_libc_srand seeds it.
-void ora_pnp_use_libc_rand(void* h) { static_cast<PnPOracle*>(h)->use_libc_rand(); }
-void ora_sim3_use_libc_rand(void* h) { static_cast<Sim3Oracle*>(h)->use_libc_rand(); }
-void ora_mlpnp_use_libc_rand(void* h) { static_cast<MLPnPOracle*>(h)->use_libc_rand(); }
+void ora_pnp_use_libc_rand(void* h, int on) { static_cast<PnPOracle*>(h)->use_libc_rand(on != 0); }
+void ora_sim3_use_libc_rand(void* h, int on) { static_cast<Sim3Oracle*>(h)->use_libc_rand(on != 0); }
+void ora_mlpnp_use_libc_rand(void* h, int on) { static_cast<MLPnPOracle*>(h)->use_libc_rand(on != 0); }
 void ora_libc_srand(uint32_t seed) { ::srand(seed); }
 int ora_libc_rand(void) { return ::rand(); }
 void ora_pnp_set_params(void* h, double prob, int min_inliers, int max_its, int min_set, float eps, float th2) {

@@ -56,7 +56,7 @@ public:
 
     // Draw from the process-global libc rand() instead of the own stream: the reference's actual
     // RandomInt (Random.cpp:47-50), for event replays on one shared stream (Q3).
-    void use_libc_rand() { rng.use_libc = true; }
+    void use_libc_rand(bool on = true) { rng.use_libc = on; }  // off: the own stream resumes
 private:
     void CheckInliers();
     void computePose(const int* idx, int n, double R[3][3], double t[3]);

@@ -17,8 +17,9 @@ namespace rsc_orb {
 template <class FrameT, class MapPointT>
 class PnPsolver {
 public:
-    // PnPsolver::PnPsolver (PnPsolver.cpp:11-55).  `seed` is the per-solver rand() stream (H4); the
-    // reference's unseeded global stream behaves as seed 1.
+    // PnPsolver::PnPsolver (PnPsolver.cpp:11-55).  By default the solver draws from its thread's one
+    // rand() stream (the reference's, rsc_context.hpp); `seed` is the per-solver stream srand(seed)
+    // after the opt-in reference_rand(false) (H4).
     PnPsolver(const FrameT& F, const std::vector<std::shared_ptr<MapPointT>>& vpMapPointMatches, uint32_t seed = 1) {
         std::vector<float> p2d, p3d, s2;
         std::vector<int32_t> kp;

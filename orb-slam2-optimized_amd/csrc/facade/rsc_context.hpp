@@ -16,20 +16,24 @@ inline void check(int status, const char* what) {
 }
 
 // rand() (Q3): the reference draws every RANSAC sample from glibc's process-global, never seeded
-// rand() (Random.cpp:47-50).  By default each facade solver owns a stream seeded with its
-// constructor's `seed` (H4).  With reference_rand(true) — or RSC_REFERENCE_RAND=1 in the environment —
-// every solver constructed afterwards on this thread is bound to the thread's ONE stream (srand(1) on
-// first use), so the calls of a single-threaded Relocalization() / ComputeSim3() draw exactly the
-// samples the reference binary draws (other rand() users in between: rsc_stream_skip).
+// rand() (Random.cpp:47-50).  By default (round 6) every solver constructed on a thread is bound to
+// the thread's ONE stream (srand(1) on first use), so the calls of a single-threaded Relocalization()
+// / ComputeSim3() draw exactly the samples the reference binary draws (other rand() users in between:
+// rsc_stream_skip); the constructor's `seed` is then unused.  The stream is per host thread, not
+// process-global: the reference's Tracking and LoopClosing threads race on one rand(), which no
+// replay can reproduce.  reference_rand(false) — or RSC_REFERENCE_RAND=0 in the environment — is the
+// opt-in to per-solver streams srand(seed) (H4) for solvers constructed afterwards on this thread.
+// Lifetime: facade solvers use their thread's context (and stream); they must not outlive the thread
+// that constructed them.
 struct ThreadContext {
     rsc_context* ctx = nullptr;
     rsc_stream* stream = nullptr;
-    bool reference_rand = false;
+    bool reference_rand = true;
     ThreadContext() {
         const char* d = std::getenv("RSC_DEVICE");
         check(rsc_context_create(d ? std::atoi(d) : 0, &ctx), "rsc_context_create");
         const char* r = std::getenv("RSC_REFERENCE_RAND");
-        reference_rand = r && std::atoi(r) != 0;
+        if (r) reference_rand = std::atoi(r) != 0;
     }
     ~ThreadContext() {
         if (stream) rsc_stream_destroy(stream);

@@ -91,11 +91,12 @@ __global__ __launch_bounds__(64) void pnp_eig_group_kernel(const DevPnP* __restr
 template <int NS>
 __global__ __launch_bounds__(128 * kSplitUnits) __attribute__((amdgpu_waves_per_eu(2))) void pnp_eig_split_kernel(
     const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps, const int2* __restrict__ wg_table,
-    int nwg_table, const uint32_t* __restrict__ rng_T, double* __restrict__ stage, int32_t* __restrict__ samples) {
+    int nwg_table, const uint32_t* __restrict__ rng_T, double* __restrict__ stage, int32_t* __restrict__ samples,
+    unsigned* fault) {
     __shared__ __attribute__((aligned(16))) double smem[kSplitHyps * kQuadRegion];
     __shared__ __attribute__((aligned(16))) double dsub[kSplitHyps * kSplitDsub];
     __shared__ int pub[kSplitUnits], ack[kSplitUnits];
-    pnp_eig_split_body<NS>(probs, lps, wg_table, nwg_table, rng_T, stage, samples, smem, dsub, pub, ack);
+    pnp_eig_split_body<NS>(probs, lps, wg_table, nwg_table, rng_T, stage, samples, smem, dsub, pub, ack, fault);
 }
 
 template <int NS>
@@ -938,8 +939,10 @@ static hipError_t launch_eig_rows(int nwgE, const int2* wgtE, const DevPnP* prob
 hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, const int2* wgtB,
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
-                                  hipEvent_t eig_begin, hipEvent_t eig_end, bool eig_rows, bool eig_split) {
+                                  hipEvent_t eig_begin, hipEvent_t eig_end, bool eig_rows, bool eig_split,
+                                  unsigned* fault) {
     if (ns < 4 || ns > 6) return hipErrorInvalidValue;
+    if (eig_split && !eig_rows && !fault) return hipErrorInvalidValue;
     if (eig_begin) (void)hipEventRecord(eig_begin, st);
     switch (ns) {
 #define RSC_CASE(N)                                                                                   \
@@ -949,7 +952,7 @@ hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, 
             if (e != hipSuccess) return e;                                                            \
         } else if (eig_split)                                                                         \
             pnp_eig_split_kernel<N><<<(nwgE + kSplitUnits - 1) / kSplitUnits, 128 * kSplitUnits, 0, st>>>( \
-                probs, lps, wgtE, nwgE, T, stage, samples);                                           \
+                probs, lps, wgtE, nwgE, T, stage, samples, fault);                                    \
         else                                                                                          \
             pnp_eig_group_kernel<N><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples);        \
         if (eig_end) (void)hipEventRecord(eig_end, st);                                               \

@@ -155,6 +155,8 @@ int ppt_for(int n) {
 
 }  // namespace
 
+constexpr int kFaultWord = 4;  // rsc_context::h_flag[4]: the split eigen stage's fault word
+
 struct rsc_context {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -229,7 +231,7 @@ struct rsc_context {
     // (written by signal_kernel after the round) instead of hipStreamSynchronize's wake-up; env
     // RSC_SPIN_WAIT=0/1 (stream_wait)
     bool spin_wait = false;
-    uint32_t* h_flag = nullptr;
+    uint32_t* h_flag = nullptr;  // [0] stream_wait's sequence flag, [kFaultWord] the eigen stage's fault word
     uint32_t flag_seq = 0;
     std::chrono::steady_clock::time_point t_entry;
 };
@@ -257,6 +259,7 @@ struct rsc_pnp {
     // position in the last speculation of its context
     int spec_out0 = -1, spec_H = 0;
     rsc_stream* stream = nullptr;  // shared rand() stream (rsc_pnp_bind_stream) or null: own stream
+    RngStream own_rng;             // the own stream, parked while bound (st.rng follows the shared one)
     ~rsc_pnp() {
         for (void* p : {(void*)d_pts, (void*)d_uv, (void*)d_pws, (void*)d_us, (void*)d_als, (void*)d_best,
                         (void*)d_refined})
@@ -276,6 +279,7 @@ struct rsc_sim3 {
     float4* d_pim = nullptr;
     int spec_out0 = -1, spec_H = 0;
     rsc_stream* stream = nullptr;
+    RngStream own_rng;
     ~rsc_sim3() {
         for (void* p : {(void*)d_x1, (void*)d_x2, (void*)d_pim})
             if (p) (void)hipFree(p);
@@ -295,6 +299,7 @@ struct rsc_mlpnp {
     int words = 0;
     int spec_out0 = -1, spec_H = 0;
     rsc_stream* stream = nullptr;
+    RngStream own_rng;
     ~rsc_mlpnp() {
         for (void* p : {(void*)d_pts, (void*)d_uv, (void*)d_brg, (void*)d_cov, (void*)d_best})
             if (p) (void)hipFree(p);
@@ -387,6 +392,15 @@ int stream_wait(rsc_context* C) {
     }
     RSC_HIP(hipStreamSynchronize(C->stream));
     return 0;
+}
+
+// The eigen stage's fault word (h_flag[kFaultWord], set by split_wait when a hand-off gives up):
+// read after the round's wait, cleared, and returned as an error instead of the round's results.
+int take_fault(rsc_context* C) {
+    if (__atomic_load_n(C->h_flag + kFaultWord, __ATOMIC_ACQUIRE) == 0) return 0;
+    __atomic_store_n(C->h_flag + kFaultWord, 0u, __ATOMIC_RELEASE);
+    g_last_error = "eigen stage: a chase / row-wave hand-off timed out (split_wait); results discarded";
+    return RSC_ERR_INTERNAL;
 }
 
 void host_mark(rsc_context* C, int k) {
@@ -585,7 +599,8 @@ struct HipPnPBackend : PnPBackend {
                                           reinterpret_cast<const int2*>(tab + C->pnp_tab_solve[g]), dprobs, dlps,
                                           C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p, bs, C->stream,
                                           eb, C->timing ? C->ev[7 + 2 * g] : nullptr,
-                                          (int)quad_wgs[g].size() <= C->eig_rows_max_wgs, C->eig_split));
+                                          (int)quad_wgs[g].size() <= C->eig_rows_max_wgs, C->eig_split,
+                                          C->h_flag + kFaultWord));
             first_group = false;
         }
         timing_begin(C, 1);
@@ -606,6 +621,7 @@ struct HipPnPBackend : PnPBackend {
         host_mark(C, 1);
         if (int e = stream_wait(C)) return e;
         host_mark(C, 2);
+        if (int e = take_fault(C)) return e;
         if (C->timing) {
             float a = 0, s = 0;
             (void)hipEventElapsedTime(&a, C->ev[0], C->ev[1]);
@@ -1090,6 +1106,24 @@ static inline int draws_per_hypothesis(const PnPState& s) { return s.mRansacMinS
 static inline int draws_per_hypothesis(const Sim3State&) { return 3; }
 static inline int draws_per_hypothesis(const MLState& s) { return s.mRansacMinSet; }
 
+// srand(seed) on a solver's own stream: while the solver is bound, that stream is the parked one
+template <class Solver>
+static void reset_solver(Solver* s, uint32_t seed) {
+    s->st.reset(seed);
+    if (s->stream) s->own_rng = s->st.rng;
+}
+
+// rsc_*_bind_stream: binding parks the own stream, unbinding resumes it where it stopped (a bound
+// call overwrites st.rng with the shared stream's position); rebinding keeps the parked one
+template <class Solver>
+static int bind_stream(Solver* s, rsc_stream* stream) {
+    if (!s || (stream && stream->ctx != s->ctx)) return RSC_ERR_ARG;
+    if (!s->stream && stream) s->own_rng = s->st.rng;
+    if (s->stream && !stream) s->st.rng = s->own_rng;
+    s->stream = stream;
+    return RSC_OK;
+}
+
 // iterate() calls of solvers bound to a shared stream draw in call order, so a bound solver's call
 // starts where the previous call ended: the calls run one at a time in list order.
 template <class Solver, class Impl, class Out>
@@ -1118,16 +1152,20 @@ int shared_events(Solver* const* solvers, const int32_t* event_begin, int n_even
     if (!solvers || !event_begin || !streams || !per_candidate || !per_event) return RSC_ERR_ARG;
     const int total = event_begin[n_events];
     for (int e = 0; e < n_events; ++e) {
-        if (event_begin[e + 1] < event_begin[e] || !streams[e]) return RSC_ERR_ARG;
+        if (event_begin[e + 1] < event_begin[e] || !streams[e] || streams[e]->ctx != streams[0]->ctx)
+            return RSC_ERR_ARG;
         for (int f = 0; f < e; ++f)
             if (streams[f] == streams[e]) return RSC_ERR_ARG;  // one stream per event (calls of two events would interleave)
         per_event[e] = rsc_event_result{-1, -1, -1, 0};
     }
     std::vector<char> discarded(total, 0), resolved(n_events, 0);
     std::vector<int32_t> start_it(total);
+    std::vector<RngStream> own(total);  // the calls draw from the event's stream; a solver's own
+                                        // stream (st.rng of an unbound one) resumes afterwards
     for (int i = 0; i < total; ++i) {
         if (!solvers[i] || solvers[i]->ctx != streams[0]->ctx) return RSC_ERR_ARG;
         start_it[i] = solvers[i]->st.mnIterations;
+        own[i] = solvers[i]->st.rng;
     }
     for (int round = 0;; ++round) {
         std::vector<Solver*> act;
@@ -1178,6 +1216,7 @@ int shared_events(Solver* const* solvers, const int32_t* event_begin, int n_even
             if (!resolved[e] && !any_active) resolved[e] = 1;
         }
     }
+    for (int i = 0; i < total; ++i) solvers[i]->st.rng = own[i];
     return RSC_OK;
 }
 
@@ -1232,7 +1271,7 @@ int rsc_context_create(int device, rsc_context** out) {
         void* f = nullptr;
         RSC_HIP(hipHostMalloc(&f, 64, hipHostMallocCoherent));
         C->h_flag = static_cast<uint32_t*>(f);
-        *C->h_flag = 0;
+        std::memset(C->h_flag, 0, 64);
     }
     C->table.build();
     if (int e = C->d_table.ensure(C->table.T.size())) return e;
@@ -1442,7 +1481,7 @@ int rsc_pnp_last_inliers(rsc_pnp* s, uint8_t* out) {
 
 int rsc_pnp_reset(rsc_pnp* s, uint32_t seed) {
     if (!s) return RSC_ERR_ARG;
-    s->st.reset(seed);
+    reset_solver(s, seed);
     s->last_kind = 0;
     return RSC_OK;
 }
@@ -1610,7 +1649,7 @@ int rsc_sim3_reset(rsc_sim3* s, uint32_t seed) {
     if (!s) return RSC_ERR_ARG;
     const int mi = s->st.mRansacMinInliers, mx = s->st.mRansacMaxIts;
     (void)mi; (void)mx;
-    s->st.reset(seed);
+    reset_solver(s, seed);
     return RSC_OK;
 }
 
@@ -2642,29 +2681,17 @@ int rsc_stream_peek(rsc_stream* s, int n, int32_t* out) {
     return RSC_OK;
 }
 
-int rsc_pnp_bind_stream(rsc_pnp* s, rsc_stream* stream) {
-    if (!s || (stream && stream->ctx != s->ctx)) return RSC_ERR_ARG;
-    s->stream = stream;
-    return RSC_OK;
-}
+int rsc_pnp_bind_stream(rsc_pnp* s, rsc_stream* stream) { return bind_stream(s, stream); }
 
-int rsc_sim3_bind_stream(rsc_sim3* s, rsc_stream* stream) {
-    if (!s || (stream && stream->ctx != s->ctx)) return RSC_ERR_ARG;
-    s->stream = stream;
-    return RSC_OK;
-}
+int rsc_sim3_bind_stream(rsc_sim3* s, rsc_stream* stream) { return bind_stream(s, stream); }
 
-int rsc_mlpnp_bind_stream(rsc_mlpnp* s, rsc_stream* stream) {
-    if (!s || (stream && stream->ctx != s->ctx)) return RSC_ERR_ARG;
-    s->stream = stream;
-    return RSC_OK;
-}
+int rsc_mlpnp_bind_stream(rsc_mlpnp* s, rsc_stream* stream) { return bind_stream(s, stream); }
 
 int rsc_pnp_reset_many(rsc_pnp* const* s, int count, const uint32_t* seeds) {
     if (count < 0 || (count && (!s || !seeds))) return RSC_ERR_ARG;
     for (int i = 0; i < count; ++i) {
         if (!s[i]) return RSC_ERR_ARG;
-        s[i]->st.reset(seeds[i]);
+        reset_solver(s[i], seeds[i]);
         s[i]->last_kind = 0;
     }
     return RSC_OK;
@@ -2684,7 +2711,7 @@ int rsc_sim3_reset_many(rsc_sim3* const* s, int count, const uint32_t* seeds) {
     if (count < 0 || (count && (!s || !seeds))) return RSC_ERR_ARG;
     for (int i = 0; i < count; ++i) {
         if (!s[i]) return RSC_ERR_ARG;
-        s[i]->st.reset(seeds[i]);
+        reset_solver(s[i], seeds[i]);
     }
     return RSC_OK;
 }
@@ -2825,7 +2852,7 @@ int rsc_mlpnp_iterate(rsc_mlpnp* s, int n_its, rsc_pnp_result* out, uint8_t* inl
 
 int rsc_mlpnp_reset(rsc_mlpnp* s, uint32_t seed) {
     if (!s) return RSC_ERR_ARG;
-    s->st.reset(seed);
+    reset_solver(s, seed);
     return RSC_OK;
 }
 
@@ -2833,7 +2860,7 @@ int rsc_mlpnp_reset_many(rsc_mlpnp* const* s, int count, const uint32_t* seeds) 
     if (count > 0 && (!s || !seeds)) return RSC_ERR_ARG;
     for (int i = 0; i < count; ++i) {
         if (!s[i]) return RSC_ERR_ARG;
-        s[i]->st.reset(seeds[i]);
+        reset_solver(s[i], seeds[i]);
     }
     return RSC_OK;
 }

@@ -41,6 +41,20 @@
 
 namespace rsc {
 
+// Bounded poll of a hand-off flag (the split eigen stage's pub / ack words): v = load() until pred(v)
+// holds, pause() between polls, at most `limit` polls.  Returns false when it gave up — the caller
+// then raises the launch's fault word, so a lost hand-off is an error status, never a silently
+// wrong eigenvector.  Compiled for the host too (tests/hostemu: the give-up path at limit 1).
+template <class Load, class Pause, class Pred>
+RSC_HD bool poll_until(int limit, Load load, Pause pause, Pred pred, int& v) {
+    for (int it = 0; it < limit; ++it) {
+        v = load();
+        if (pred(v)) return true;
+        pause();
+    }
+    return false;
+}
+
 template <typename S> struct lim;
 template <> struct lim<double> {
     RSC_HD static double eps() { return 2.220446049250313080847e-16; }

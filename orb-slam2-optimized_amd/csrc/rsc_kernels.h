@@ -143,7 +143,9 @@ hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, 
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
                                   hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr, bool eig_rows = false,
-                                  bool eig_split = false);
+                                  bool eig_split = false, unsigned* fault = nullptr);
+// fault (required by the split form): a word in pinned host memory that the split eigen stage sets to
+// 1 when a chase / row-wave hand-off gives up (split_wait); the host turns it into RSC_ERR_INTERNAL.
 // counts: where the host reads them (pinned memory or HBM); counts_dev (nullable): an HBM copy for
 // pnp_select_refine_kernel; qual[lp] (pinned, zeroed by the host) is set to 1 when a hypothesis of
 // launch problem lp reaches its min_inliers.

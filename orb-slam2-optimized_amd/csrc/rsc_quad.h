@@ -661,19 +661,27 @@ constexpr int kSplitHyps = kSplitUnits * 20;
 #define RSC_SPLIT_SLEEP 1
 #endif
 constexpr int kSplitDone = 1 << 30;    // `pub` flag: the chase has ended (low bits: its steps)
-constexpr int kSplitSpinLimit = 1 << 24;  // polls before a wait gives up (never reached; no hang)
-
-// Wait (wave-uniformly) until pred(value of *flag) holds; returns the value seen.
-template <class Pred>
-__device__ __forceinline__ int split_wait(int* flag, Pred pred) {
-    int v = 0;
-    for (int it = 0; it < kSplitSpinLimit; ++it) {
-        v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (pred(v)) break;
-#if RSC_SPLIT_SLEEP
-        __builtin_amdgcn_s_sleep(RSC_SPLIT_SLEEP);
+// polls before a wait gives up (a stall of seconds: never reached by a working hand-off); giving up
+// raises the launch's fault word, which the host returns as RSC_ERR_INTERNAL
+#ifndef RSC_SPLIT_SPIN_LIMIT
+#define RSC_SPLIT_SPIN_LIMIT (1 << 24)
 #endif
-    }
+constexpr int kSplitSpinLimit = RSC_SPLIT_SPIN_LIMIT;
+
+// Wait (wave-uniformly) until pred(value of *flag) holds; returns the value seen.  On give-up the
+// fault word (pinned host memory, rsc_context::h_flag) is set.
+template <class Pred>
+__device__ __forceinline__ int split_wait(int* flag, unsigned* fault, Pred pred) {
+    int v = 0;
+    const bool ok = poll_until(
+        kSplitSpinLimit, [flag]() { return __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); },
+        []() {
+#if RSC_SPLIT_SLEEP
+            __builtin_amdgcn_s_sleep(RSC_SPLIT_SLEEP);
+#endif
+        },
+        pred, v);
+    if (!ok) __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return v;
 }
 
@@ -681,6 +689,7 @@ struct SplitRing {
     double* E;          // this hypothesis' E region (55 doubles)
     int* pub;           // this unit's published step count
     int* ack;           // this unit's applied step count (row wave)
+    unsigned* fault;    // the launch's fault word (split_wait)
     uint32_t mask = 0;  // slots of the step being built that rotated
     uint32_t seq = 0;   // steps published
     RSC_HD void operator()(int k, double c, double s, bool apply) {
@@ -697,7 +706,7 @@ struct SplitRing {
         __hip_atomic_store(pub, (int)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         // step seq + 1 overwrites the parity of step seq - 1: it must have been applied
         const int need = (int)seq - 1;
-        split_wait(ack, [need](int v) { return v >= need; });
+        split_wait(ack, fault, [need](int v) { return v >= need; });
     }
 };
 
@@ -706,7 +715,7 @@ __device__ __forceinline__ void pnp_eig_split_body(const DevPnP* __restrict__ pr
                                                    const int2* __restrict__ wg_table, int nwg_table,
                                                    const uint32_t* __restrict__ rng_T, double* __restrict__ stage,
                                                    int32_t* __restrict__ samples, double* smem, double* dsub,
-                                                   int* pub, int* ack) {
+                                                   int* pub, int* ack, unsigned* fault) {
     constexpr int HPW = kEigHyps, U = kSplitUnits;
     static_assert(HPW == 20 && 2 * HPW <= 64 && 4 * HPW <= 128 && HPW * kSplitRowLanes <= 64, "unit layout");
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -828,7 +837,7 @@ __device__ __forceinline__ void pnp_eig_split_body(const DevPnP* __restrict__ pr
             RSC_UNROLL for (int c = 0; c < 12; ++c) Q[j][c] = T[(kSplitRowLanes * j + m) * 12 + c];
         for (int s = 1;; ++s) {
             // step s published, or the chase ended before it
-            const int v = split_wait(pub + unit, [s](int x) { return (x & (kSplitDone - 1)) >= s || (x & kSplitDone); });
+            const int v = split_wait(pub + unit, fault, [s](int x) { return (x & (kSplitDone - 1)) >= s || (x & kSplitDone); });
             if ((v & (kSplitDone - 1)) < s) break;
             const double* ring = E + kRingPar * (s & 1);
             const uint64_t word = *reinterpret_cast<const uint64_t*>(ring + 22);
@@ -876,7 +885,7 @@ __device__ __forceinline__ void pnp_eig_split_body(const DevPnP* __restrict__ pr
         RSC_UNROLL for (int i = 0; i < 12; ++i) diag[i] = ds[i];
         RSC_UNROLL for (int i = 0; i < 11; ++i) sub[i] = ds[12 + i];
         int perm[12];
-        SplitRing ring{E, pub + unit, ack + unit};
+        SplitRing ring{E, pub + unit, ack + unit, fault};
         tridiag_qr<double, 12>(diag, sub, ring, perm);
         int32_t* pm = reinterpret_cast<int32_t*>(E + kRingPerm);
         RSC_UNROLL for (int c = 0; c < 4; ++c) pm[c] = perm[c];

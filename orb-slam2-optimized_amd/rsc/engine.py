@@ -832,7 +832,10 @@ class MLPnPSolver:
         L = load_library()
         n = L.rsc_mlpnp_last_samples(self.h, smp.reshape(-1), cap)
         m = L.rsc_mlpnp_last_poses(self.h, pos.reshape(-1), cap)
-        assert n == m
+        if n < 0 or m < 0:
+            _check(min(n, m), "last_hypotheses")
+        if n != m:
+            raise RuntimeError(f"last_hypotheses: {n} samples vs {m} poses")
         return smp[:n], pos[:n]
 
     def last_counts(self, cap=4096):
@@ -927,7 +930,8 @@ class EventBatch:
             f = L.rsc_loop_events if self.kind == "sim3" else L.rsc_reloc_events
             _check(f(self.batch._h, self.begin, len(self.events), self._cand, self._ev), "events")
             return self.per_event
-        assert len(streams) == len(self.events)
+        if len(streams) != len(self.events) or any(st is None for st in streams):
+            raise ValueError(f"one Stream per event: {len(self.events)} events, {len(streams)} streams")
         hs = (C.c_void_p * len(streams))(*[st.h.value for st in streams])
         f = L.rsc_loop_events_shared if self.kind == "sim3" else L.rsc_reloc_events_shared
         _check(f(self.batch._h, self.begin, len(self.events), hs, self._cand, self._ev), "events_shared")

@@ -148,6 +148,9 @@ int main(int argc, char** argv) {
     FILE* out = fopen(argv[2], "wb");
     if (!in || !out) return 2;
     const int mode = rd<int32_t>(in);
+    // modes 1-3 compare solvers on their own srand(seed) streams (the opt-in); mode 9 runs on the
+    // facade's default, the thread's one reference rand() stream
+    if (mode != 9) rsc_orb::reference_rand(false);
     if (mode == 1 || mode == 3) {
         Frame F;
         const int n = rd<int32_t>(in);
@@ -189,9 +192,9 @@ int main(int argc, char** argv) {
         }
     } else if (mode == 9) {
         // Tracking::Relocalization's RANSAC loop (Tracking.cpp:1239-1262) over K candidate Frames with
-        // the facade in reference_rand mode: every solver draws from the thread's one rand() stream
-        // (srand(1), Q3).  Per call: candidate, ok, bNoMore, nInliers, Tcw; ends at the first pose.
-        rsc_orb::reference_rand(true);
+        // the facade's default (no reference_rand call, no environment variable): every solver draws
+        // from the thread's one rand() stream (srand(1), Q3).  Per call: candidate, ok, bNoMore,
+        // nInliers, Tcw; ends at the first pose.
         const int K = rd<int32_t>(in);
         const double prob = rd<double>(in);
         const int mi = rd<int32_t>(in), mx = rd<int32_t>(in), ms = rd<int32_t>(in);

@@ -140,6 +140,18 @@ int he_sim3_count(const float* pose24, const float* K1, const float* K2, int n, 
     return c;
 }
 
+// split_wait's bounded poll (rsc_core.h poll_until) on a flag that becomes ready at the
+// `ready_after`-th load: 1 when it held within `limit` polls, 0 when the wait gave up (the device
+// raises the fault word then); *loads = flag loads made, *pauses = pauses between them
+int he_poll_until(int limit, int ready_after, int* loads, int* pauses) {
+    int n = 0, p = 0, v = -1;
+    const bool ok = rsc::poll_until(limit, [&]() { return ++n; }, [&]() { ++p; },
+                                    [ready_after](int x) { return x >= ready_after; }, v);
+    *loads = n;
+    *pauses = p;
+    return ok ? 1 : 0;
+}
+
 }  // extern "C"
 
 // ------------------------------------------------------------------------------------------------

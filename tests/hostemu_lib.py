@@ -39,8 +39,16 @@ def lib():
         L.he_qr_compare.argtypes = [f64p, f64p, i32p, f64p, i32p, f64p, i32p, f64p, i32p]
         L.he_qr_split.argtypes = [f64p, C.c_int, f64p, i32p, f64p, i32p]
         L.he_optimize_sim3.argtypes = [C.c_int, f32p, f32p, f32p, f32p, C.c_float, f64p, u8p, i32p]
+        L.he_poll_until.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         _lib = L
     return _lib
+
+
+def poll_until(limit, ready_after):
+    """(held, loads, pauses) of rsc_core.h poll_until on a flag ready at load `ready_after`."""
+    n, p = C.c_int(), C.c_int()
+    ok = lib().he_poll_until(limit, ready_after, C.byref(n), C.byref(p))
+    return bool(ok), n.value, p.value
 
 
 def rand_stream(seed, n):

@@ -69,7 +69,7 @@ def lib():
                                  C.c_float, C.c_uint32]
     L.ora_pnp_destroy.argtypes = [vp]
     for f in ("ora_pnp_use_libc_rand", "ora_sim3_use_libc_rand", "ora_mlpnp_use_libc_rand"):
-        getattr(L, f).argtypes = [vp]
+        getattr(L, f).argtypes = [vp, C.c_int]
     L.ora_libc_srand.argtypes = [C.c_uint32]
     L.ora_libc_rand.restype = C.c_int
     L.ora_pnp_set_params.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
@@ -232,10 +232,10 @@ class OraclePnP:
             lib().ora_pnp_destroy(self.h)
             self.h = None
 
-    def use_libc_rand(self):
+    def use_libc_rand(self, on=True):
         """Draw samples from the process-global libc rand() (the reference's RandomInt source, Q3);
-        seed it with libc_srand."""
-        lib().ora_pnp_use_libc_rand(self.h)
+        seed it with libc_srand.  on=False: back to the own srand(seed) stream where it stopped."""
+        lib().ora_pnp_use_libc_rand(self.h, int(on))
 
     def set_ransac_parameters(self, probability=0.99, min_inliers=8, max_iterations=300, min_set=4,
                               epsilon=0.4, th2=5.991):
@@ -298,10 +298,10 @@ class OracleSim3:
             lib().ora_sim3_destroy(self.h)
             self.h = None
 
-    def use_libc_rand(self):
+    def use_libc_rand(self, on=True):
         """Draw samples from the process-global libc rand() (the reference's RandomInt source, Q3);
-        seed it with libc_srand."""
-        lib().ora_sim3_use_libc_rand(self.h)
+        seed it with libc_srand.  on=False: back to the own srand(seed) stream where it stopped."""
+        lib().ora_sim3_use_libc_rand(self.h, int(on))
 
     @property
     def N(self):
@@ -362,10 +362,10 @@ class OracleMLPnP:
             lib().ora_mlpnp_destroy(self.h)
             self.h = None
 
-    def use_libc_rand(self):
+    def use_libc_rand(self, on=True):
         """Draw samples from the process-global libc rand() (the reference's RandomInt source, Q3);
-        seed it with libc_srand."""
-        lib().ora_mlpnp_use_libc_rand(self.h)
+        seed it with libc_srand.  on=False: back to the own srand(seed) stream where it stopped."""
+        lib().ora_mlpnp_use_libc_rand(self.h, int(on))
 
     def set_covariances(self, cov):
         """computePose's covMats ([n, 3, 3]) or None."""

@@ -183,3 +183,15 @@ def test_replay_emulation_refine_failures(case):
         assert e.state()["max_rows"] == o.info()["max_rows"]
     ints, _ = o.trace()
     assert ((ints[:, 9] == 1) & (ints[:, 11] == 0)).any(), "case must contain a failed Refine"
+
+
+def test_split_wait_gives_up_after_its_limit():
+    """rsc_core.h poll_until, the split eigen stage's bounded hand-off wait (split_wait), compiled for
+    the host: it returns as soon as the flag is ready, and at a spin limit of 1 a flag that is not yet
+    ready makes it give up after one load (the device then raises the launch's fault word, which the
+    host returns as RSC_ERR_INTERNAL — tests/test_gpu_fault.py runs that path on the device)."""
+    assert he.poll_until(1, 1) == (True, 1, 0)
+    assert he.poll_until(1, 2) == (False, 1, 1)  # the give-up path at limit 1
+    assert he.poll_until(1 << 24, 5) == (True, 5, 4)
+    assert he.poll_until(3, 5) == (False, 3, 3)
+    assert he.poll_until(0, 1) == (False, 0, 0)

@@ -113,10 +113,13 @@ def test_config3_parity_batch_first_success():
     assert n_ok >= 24
 
 
-def test_config4_mlpnp_4096_batch_every_hypothesis():
-    """MLPnP at N = 4096: mlpnp_scan_kernel<16> and the 4096-row LDS slab of the solve."""
+@pytest.mark.parametrize("candidates", [32, 128])
+def test_config4_mlpnp_4096_batch_every_hypothesis(candidates):
+    """MLPnP at N = 4096: mlpnp_scan_kernel<16> and the 4096-row LDS slab of the solve, at the per-GPU
+    share of 4 GPUs (32 candidates) and at the bench's single-GPU launch shape (all 128 candidates of
+    config 4 in one launch: 38,400 hypotheses, bench.py's mlpnp section at N = 1)."""
     from rsc import engine
-    scenes = wl.config4_scenes()
+    scenes = wl.config4_scenes(candidates=candidates)
     seeds = wl.step_seeds(0, len(scenes))
     gs = [engine.MLPnPSolver(ctx(), sc, int(s)) for sc, s in zip(scenes, seeds)]
     b = engine.SolverBatch(gs)

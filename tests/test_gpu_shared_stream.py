@@ -143,3 +143,55 @@ def test_events_on_the_shared_stream(kind):
         assert streams[e].peek(1)[0] == ol.libc_rand(), f"event {ev.eid}"
         n_win += rec["winner"] >= 0
     assert n_win >= 2
+
+
+@pytest.mark.parametrize("kind", ["pnp", "sim3", "mlpnp"])
+def test_unbind_resumes_the_own_stream(kind):
+    """include/rsc.h rsc_*_bind_stream: unbinding (NULL) returns a solver to its own srand(seed) stream
+    where it stopped: own calls, bound calls on the shared stream, own calls again, a reset
+    while bound (reseeds the parked stream), unbind — every call equals the oracle that switches between
+    its own stream and libc's rand() at the same points."""
+    from rsc import engine
+    rng = np.random.default_rng(43)
+    if kind == "sim3":
+        x = synth.make_sim3_pair(rng, 500, 60)
+        g, o = engine.Sim3Solver(ctx(), x, 77), ol.OracleSim3(x, 77)
+        args = (0.99, 20, 300)
+    else:
+        x = synth.make_pnp_scene(rng, 500, 0.3)
+        cls, ocls = (engine.PnPSolver, ol.OraclePnP) if kind == "pnp" else (engine.MLPnPSolver, ol.OracleMLPnP)
+        g, o = cls(ctx(), x, 77), ocls(x, 77)
+        args = (0.99, 10, 300, 4 if kind == "pnp" else 6, 0.5, 5.991)
+    for s in (g, o):
+        s.set_ransac_parameters(*args)
+    st = engine.Stream(ctx(), 1)
+    ol.libc_srand(1)
+
+    def step(tag):
+        a, b = g.iterate(5), o.iterate(5)
+        assert (a["ok"], a["no_more"], a["n_inliers"], a["iterations"]) == \
+            (b["ok"], b["no_more"], b["n_inliers"], b["iterations"]), tag
+        key = "R" if kind == "sim3" else "T"
+        if b["ok"] or kind == "sim3":
+            assert np.array_equal(bits(a[key]), bits(b[key])), tag
+
+    step("own 1")
+    g.bind_stream(st)
+    o.use_libc_rand(True)
+    step("bound 1")
+    step("bound 2")
+    g.bind_stream(None)
+    o.use_libc_rand(False)
+    step("own 2")
+    step("own 3")
+    assert st.peek(1)[0] == ol.libc_rand()  # the unbound calls did not touch the shared stream
+    # reset while bound reseeds the parked own stream
+    g.bind_stream(st)
+    g.reset(91)
+    o2 = type(o)(x, 91)
+    o2.set_ransac_parameters(*args)
+    o = o2
+    for s in (g, o):
+        s.set_ransac_parameters(*args)
+    g.bind_stream(None)
+    step("own after reset")
