@@ -268,6 +268,72 @@ int rsc_reloc_events_shared(rsc_pnp* const* solvers, const int32_t* event_begin,
 int rsc_loop_events_shared(rsc_sim3* const* solvers, const int32_t* event_begin, int n_events,
                            rsc_stream* const* streams, rsc_sim3_result* per_candidate, rsc_event_result* per_event);
 
+/* ---- Gated events (round 6): the reference's post-RANSAC acceptance test inside the event loop ----
+ * The drivers above end an event at the first candidate whose iterate() returns a pose.  The
+ * reference then checks that pose with the next stages and, on rejection, continues the round-robin
+ * (the next candidate of the same round, then later rounds, the rejected candidate included).  The
+ * gated drivers run those stages on the device (PoseOptimization / SearchBySim3 + OptimizeSim3, the
+ * kernels of rsc_pose_optimization_many / rsc_search_by_sim3_many / rsc_optimize_sim3_many) for every
+ * success in the reference's order, batched across events, until a success passes.  Solvers draw
+ * from their own streams (bound solvers: RSC_ERR_UNSUPPORTED).  per_candidate: each candidate's last
+ * iterate() record. */
+#define RSC_GATE_NONE 0    /* every candidate discarded without an accepted pose (bMatch false) */
+#define RSC_GATE_MATCH 1   /* a success passed the gate (bMatch = true) */
+#define RSC_GATE_HANDOFF 2 /* relocalization: 10 <= nGood < 50 after PoseOptimization; the reference runs
+                              SearchByProjection next (Tracking.cpp:1294-1323, outside this engine) —
+                              the event stops here and the host continues it (the records of the
+                              candidates after the winner in its round are already those calls' results) */
+/* Tracking::Relocalization (Tracking.cpp:1239-1335).  The current Frame's data PoseOptimization reads
+ * beyond what the solvers hold (their compacted p2d / p3dw / sigma2 are Frame::mvKeysUn, the MapPoint
+ * positions and mvLevelSigma2; mvInvLevelSigma2 = 1.0f / mvLevelSigma2 as ORBextractor sets it). */
+typedef struct {
+    const float* u_right;  /* [n_points] Frame::mvuRight (>= 0: stereo edge), NULL for a monocular Frame */
+    float bf;              /* Frame::mbf */
+} rsc_reloc_frame;
+typedef struct {
+    int32_t status;       /* RSC_GATE_* */
+    int32_t winner;       /* candidate of the accepted (MATCH) or handed-off success, -1 for NONE */
+    int32_t round;        /* its round of iterate(5) calls */
+    int32_t hypothesis;   /* index of the returning hypothesis in that candidate's stream */
+    int32_t n_inliers;    /* RANSAC nInliers of that success */
+    int32_t n_good;       /* PoseOptimization's return value on it (Tracking.cpp:1284) */
+    int32_t rejected;     /* successes rejected before it (nGood < 10, Tracking.cpp:1286-1287) */
+    int32_t gates;        /* PoseOptimization runs of the event */
+    float Tcw[16];        /* row-major pose after PoseOptimization (mCurrentFrame.mTcw) */
+} rsc_reloc_gate_result;
+/* frames[e]: event e's current Frame (its solvers' n_points = Frame::N).  outlier[e] (may be NULL, or
+ * NULL entries): [n_points] mvbOutlier of the winner's PoseOptimization for the slots with a map point
+ * (others 0); inliers[e] (may be NULL / NULL entries): [n_points] the winner's vbInliers. */
+int rsc_reloc_events_gated(rsc_pnp* const* solvers, const int32_t* event_begin, int n_events,
+                           const rsc_reloc_frame* frames, rsc_pnp_result* per_candidate,
+                           rsc_reloc_gate_result* per_event, uint8_t* const* outlier, uint8_t* const* inliers);
+
+/* LoopClosing::ComputeSim3 (LoopClosing.cpp:268-329).  A candidate's Sim3 solver was built from
+ * (kf1 = mpCurrentKF, kf2 = the candidate KeyFrame, vvpMapPointMatches[i]); the gate needs those
+ * views and matches: SearchBySim3(kf1, kf2, vpMapPointMatches = the RANSAC inliers of matches12, R,
+ * t, 7.5) then OptimizeSim3(kf1, kf2, vpMapPointMatches, gScm = Sim3(R, t, 1), 10) with
+ * mvInvLevelSigma2 = 1 / (scale_factors[l]^2) (float, as ORBextractor); accepted when nInliers >= 20. */
+struct rsc_kfview;
+typedef struct {
+    struct rsc_kfview* kf1;    /* mpCurrentKF's view (rsc_kfview_create) */
+    struct rsc_kfview* kf2;    /* the candidate KeyFrame's view */
+    const int32_t* matches12;  /* [kf1 n] vvpMapPointMatches[i]: KF2 keypoint index of the matched
+                                  MapPoint, -1 NULL, -2 a MapPoint not in KF2 (the solver's input) */
+} rsc_loop_candidate;
+typedef struct {
+    int32_t status;         /* RSC_GATE_NONE or RSC_GATE_MATCH */
+    int32_t winner, round, hypothesis, n_inliers;  /* the accepted success (as rsc_event_result) */
+    int32_t n_found;        /* SearchBySim3's return value on it */
+    int32_t n_opt_inliers;  /* OptimizeSim3's return value (>= 20 on MATCH) */
+    int32_t rejected;       /* successes rejected before it (nInliers < 20) */
+    double S[8];            /* gScm after OptimizeSim3: q (x, y, z, w), t, s */
+} rsc_loop_gate_result;
+/* matches_out[e] (may be NULL / NULL entries): [kf1 n] mvpCurrentMatchedPoints of the accepted
+ * candidate as KF2 keypoint indices (-1 NULL, -2 a MapPoint not in KF2). */
+int rsc_loop_events_gated(rsc_sim3* const* solvers, const rsc_loop_candidate* candidates,
+                          const int32_t* event_begin, int n_events, rsc_sim3_result* per_candidate,
+                          rsc_loop_gate_result* per_event, int32_t* const* matches_out);
+
 /* ---- Optimizer::PoseOptimization (src/Optimizer.cpp:205-424) ------------------------------------
  * The pose-only g2o optimisation every tracking step and Tracking::Relocalization()
  * (Tracking.cpp:1284,1300,1315) run on the RANSAC pose: Levenberg-Marquardt of one VertexSE3Expmap

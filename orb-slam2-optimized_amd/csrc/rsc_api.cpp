@@ -260,6 +260,7 @@ struct rsc_pnp {
     int spec_out0 = -1, spec_H = 0;
     rsc_stream* stream = nullptr;  // shared rand() stream (rsc_pnp_bind_stream) or null: own stream
     RngStream own_rng;             // the own stream, parked while bound (st.rng follows the shared one)
+    std::vector<float> h_p2d, h_p3d;  // host copies (the gated events' PoseOptimization problems)
     ~rsc_pnp() {
         for (void* p : {(void*)d_pts, (void*)d_uv, (void*)d_pws, (void*)d_us, (void*)d_als, (void*)d_best,
                         (void*)d_refined})
@@ -1367,6 +1368,8 @@ int rsc_pnp_create(rsc_context* C, const rsc_pnp_problem* pb, uint32_t seed, rsc
     for (int i = 0; i < pb->n; ++i) s.kp_index[i] = pb->kp_index ? pb->kp_index[i] : i;
     s.sigma2.assign(pb->sigma2, pb->sigma2 + pb->n);
     s.reset(seed);
+    S->h_p2d.assign(pb->p2d, pb->p2d + 2 * (size_t)pb->n);
+    S->h_p3d.assign(pb->p3dw, pb->p3dw + 3 * (size_t)pb->n);
     const int n = std::max(pb->n, 1);
     S->words = (n + 63) / 64;
     std::vector<float4> pts(n);
@@ -2127,6 +2130,11 @@ struct rsc_kfview {
     int n = 0;
     DevBuf<char> mem;  // DevSim3KF header | kp | octave | desc | grid | scales | MapPoints
     const DevSim3KF* hdr = nullptr;
+    // host copies of what OptimizeSim3 reads (the gated loop events build its problem from them)
+    std::vector<float> kp, mp_pos, inv_level_sigma2;
+    std::vector<int32_t> octave;
+    std::vector<uint8_t> mp_state;
+    float R[9], t[3], K[4];
 };
 
 int rsc_kfview_create(rsc_context* C, const rsc_sim3_kf* k, rsc_kfview** out) {
@@ -2172,6 +2180,20 @@ int rsc_kfview_create(rsc_context* C, const rsc_sim3_kf* k, rsc_kfview** out) {
     std::memcpy(b.h.data() + o_hdr, &h, sizeof(h));
     RSC_HIP(hipMemcpy(d, b.h.data(), b.h.size(), hipMemcpyHostToDevice));
     v->hdr = reinterpret_cast<const DevSim3KF*>(d + o_hdr);
+    v->kp.assign(k->kp, k->kp + 2 * n);
+    v->octave.assign(k->octave, k->octave + n);
+    v->mp_state.assign(k->mp_state, k->mp_state + n);
+    v->mp_pos.assign(k->mp_pos, k->mp_pos + 3 * n);
+    // mvLevelSigma2[l] = mvScaleFactor[l]^2, mvInvLevelSigma2[l] = 1.0f / mvLevelSigma2[l] (float,
+    // ORBextractor's constructor; KeyFrame copies them from the Frame)
+    v->inv_level_sigma2.resize((size_t)k->n_levels);
+    for (int l = 0; l < k->n_levels; ++l) {
+        const float s2 = k->scale_factors[l] * k->scale_factors[l];
+        v->inv_level_sigma2[l] = 1.0f / s2;
+    }
+    std::memcpy(v->R, k->Rcw, sizeof(v->R));
+    std::memcpy(v->t, k->tcw, sizeof(v->t));
+    v->K[0] = k->fx; v->K[1] = k->fy; v->K[2] = k->cx; v->K[3] = k->cy;
     *out = v.release();
     return RSC_OK;
 }
@@ -3005,5 +3027,364 @@ int rsc_loop_events_shared(rsc_sim3* const* solvers, const int32_t* event_begin,
         if (solvers[i] && solvers[i]->stream) return RSC_ERR_ARG;
     return shared_events(solvers, event_begin, n_events, streams, per_candidate, per_event, sim3_iterate_many_impl,
                          sim3_pred_its);
+}
+
+// ---- Gated events (round 6) ----
+// Tracking::Relocalization (Tracking.cpp:1239-1335): each round runs iterate(5) on every live
+// candidate of every unresolved event in one set of launches (own streams: the results are the
+// reference's calls whatever happens before them in the round), then walks each event's successes in
+// candidate order: PoseOptimization on the success (mCurrentFrame.mvpMapPoints = the inlier matches,
+// mTcw = the RANSAC pose, :1268-1284), nGood < 10 -> the next success of the round (:1286-1287),
+// nGood >= 50 -> match (:1327-1331), otherwise SearchByProjection's turn (handed off).  The gate
+// passes of all events run as one rsc_pose_optimization_many each.
+int rsc_reloc_events_gated(rsc_pnp* const* solvers, const int32_t* event_begin, int n_events,
+                           const rsc_reloc_frame* frames, rsc_pnp_result* per_candidate,
+                           rsc_reloc_gate_result* per_event, uint8_t* const* outlier, uint8_t* const* inliers) {
+    if (n_events <= 0) return RSC_OK;
+    if (!solvers || !event_begin || !frames || !per_candidate || !per_event) return RSC_ERR_ARG;
+    const int total = event_begin[n_events];
+    rsc_context* C = nullptr;
+    for (int e = 0; e < n_events; ++e) {
+        if (event_begin[e + 1] < event_begin[e] || event_begin[e] < 0) return RSC_ERR_ARG;
+        rsc_reloc_gate_result& r = per_event[e];
+        std::memset(&r, 0, sizeof(r));
+        r.status = RSC_GATE_NONE;
+        r.winner = r.round = r.hypothesis = -1;
+        for (int i = event_begin[e]; i < event_begin[e + 1]; ++i) {
+            if (!solvers[i]) return RSC_ERR_ARG;
+            if (solvers[i]->stream) return RSC_ERR_UNSUPPORTED;  // gating moves later calls' stream positions
+            if (!C) C = solvers[i]->ctx;
+            // one Frame per event: every candidate's vbInliers indexes the same mCurrentFrame slots
+            if (solvers[i]->ctx != C || solvers[i]->st.N_points != solvers[event_begin[e]]->st.N_points)
+                return RSC_ERR_ARG;
+        }
+    }
+    if (!C) return RSC_OK;
+    std::vector<char> discarded(total, 0), resolved(n_events, 0);
+    std::vector<int32_t> start_it(total);
+    std::vector<std::vector<uint8_t>> mask(total);
+    for (int i = 0; i < total; ++i) {
+        start_it[i] = solvers[i]->st.mnIterations;
+        mask[i].assign((size_t)std::max(solvers[i]->st.N_points, 1), 0);
+    }
+    // per gate job: the PoseOptimization problem's slot arrays (Frame::N slots)
+    struct Job {
+        int e, i;
+        std::vector<uint8_t> has_mp, outl;
+        std::vector<float> uv, Xw, inv;
+    };
+    for (int round = 0;; ++round) {
+        std::vector<rsc_pnp*> act;
+        std::vector<int> idx;
+        for (int e = 0; e < n_events; ++e) {
+            if (resolved[e]) continue;
+            for (int i = event_begin[e]; i < event_begin[e + 1]; ++i)
+                if (!discarded[i]) { act.push_back(solvers[i]); idx.push_back(i); }
+        }
+        if (act.empty()) break;
+        std::vector<int32_t> its(act.size(), 5);
+        std::vector<rsc_pnp_result> r(act.size());
+        std::vector<uint8_t*> mp(act.size());
+        for (size_t q = 0; q < act.size(); ++q) mp[q] = mask[idx[q]].data();
+        if (int st = rsc_pnp_iterate_many(act.data(), (int)act.size(), its.data(), r.data(), mp.data())) return st;
+        std::vector<char> iterated(total, 0);
+        for (size_t q = 0; q < act.size(); ++q) {
+            iterated[idx[q]] = 1;
+            per_candidate[idx[q]] = r[q];
+            if (r[q].no_more) discarded[idx[q]] = 1;  // Tracking.cpp:1257-1261
+        }
+        // gate passes: each unresolved event's next success of this round, in candidate order
+        std::vector<int> cursor(n_events);
+        for (int e = 0; e < n_events; ++e) cursor[e] = event_begin[e];
+        for (;;) {
+            std::vector<Job> jobs;
+            for (int e = 0; e < n_events; ++e) {
+                if (resolved[e]) continue;
+                int i = cursor[e];
+                while (i < event_begin[e + 1] && !(iterated[i] && per_candidate[i].ok)) ++i;
+                cursor[e] = i + 1;
+                if (i >= event_begin[e + 1]) continue;
+                const rsc_pnp* s = solvers[i];
+                const PnPState& st = s->st;
+                const int nf = st.N_points;
+                Job j;
+                j.e = e;
+                j.i = i;
+                j.has_mp.assign((size_t)nf, 0);
+                j.outl.assign((size_t)nf, 0);
+                j.uv.assign(2 * (size_t)nf, 0.f);
+                j.Xw.assign(3 * (size_t)nf, 0.f);
+                j.inv.assign((size_t)nf, 0.f);
+                for (int c = 0; c < st.N; ++c) {
+                    const int slot = st.kp_index[c];
+                    if (!mask[i][slot]) continue;  // mvpMapPoints[j] = inlier ? match : NULL (:1276-1282)
+                    j.has_mp[slot] = 1;
+                    j.uv[2 * slot] = s->h_p2d[2 * c];
+                    j.uv[2 * slot + 1] = s->h_p2d[2 * c + 1];
+                    for (int k = 0; k < 3; ++k) j.Xw[3 * slot + k] = s->h_p3d[3 * c + k];
+                    j.inv[slot] = 1.0f / st.sigma2[c];  // mvInvLevelSigma2 = 1.0f / mvLevelSigma2
+                }
+                jobs.push_back(std::move(j));
+            }
+            if (jobs.empty()) break;
+            std::vector<rsc_poseopt_problem> pr(jobs.size());
+            std::vector<rsc_poseopt_result> res(jobs.size());
+            std::vector<uint8_t*> op(jobs.size());
+            for (size_t q = 0; q < jobs.size(); ++q) {
+                const Job& j = jobs[q];
+                const PnPState& st = solvers[j.i]->st;
+                rsc_poseopt_problem& P = pr[q];
+                P.n = st.N_points;
+                P.has_mp = j.has_mp.data();
+                P.uv = j.uv.data();
+                P.Xw = j.Xw.data();
+                P.inv_sigma2 = j.inv.data();
+                P.u_right = frames[j.e].u_right;
+                P.fx = st.fx; P.fy = st.fy; P.cx = st.cx; P.cy = st.cy;
+                std::memcpy(P.Tcw, per_candidate[j.i].T, sizeof(P.Tcw));
+                P.bf = frames[j.e].bf;
+                op[q] = jobs[q].outl.data();
+            }
+            if (int st = rsc_pose_optimization_many(C, pr.data(), (int)pr.size(), res.data(), op.data())) return st;
+            for (size_t q = 0; q < jobs.size(); ++q) {
+                const Job& j = jobs[q];
+                rsc_reloc_gate_result& g = per_event[j.e];
+                g.gates++;
+                const int nGood = res[q].n_good;
+                if (nGood < 10) {  // Tracking.cpp:1286-1287: continue with the next candidate
+                    g.rejected++;
+                    continue;
+                }
+                g.status = nGood >= 50 ? RSC_GATE_MATCH : RSC_GATE_HANDOFF;
+                g.winner = j.i - event_begin[j.e];
+                g.round = round;
+                g.hypothesis = per_candidate[j.i].iterations - 1 - start_it[j.i];
+                g.n_inliers = per_candidate[j.i].n_inliers;
+                g.n_good = nGood;
+                std::memcpy(g.Tcw, res[q].Tcw, sizeof(g.Tcw));
+                const int nf = solvers[j.i]->st.N_points;
+                if (outlier && outlier[j.e]) std::memcpy(outlier[j.e], j.outl.data(), (size_t)nf);
+                if (inliers && inliers[j.e]) std::memcpy(inliers[j.e], mask[j.i].data(), (size_t)nf);
+                resolved[j.e] = 1;
+            }
+        }
+        for (int e = 0; e < n_events; ++e) {  // nCandidates == 0: the while loop ends (:1239)
+            if (resolved[e]) continue;
+            bool any_active = false;
+            for (int i = event_begin[e]; i < event_begin[e + 1]; ++i) any_active |= !discarded[i];
+            if (!any_active) resolved[e] = 1;
+        }
+    }
+    return RSC_OK;
+}
+
+// LoopClosing::ComputeSim3 (LoopClosing.cpp:268-329): a candidate's k-th success comes back from the
+// call that reaches it (Sim3Solver::iterate returns at the first hypothesis with more than
+// mRansacMinInliers inliers, Sim3Solver.cpp:155-163), so with its own stream each candidate's
+// successes are computed one at a time, each with the whole remaining budget in one call, and placed
+// in the round-robin: a call starting at hypothesis p in round c covers p..p+4, so the success at
+// hypothesis s is returned in round c + (s - p) / 5 and the next call starts at s + 1 in the round
+// after.  The event takes its successes in (round, candidate) order: SearchBySim3(7.5) on the inliers
+// (:296-309), OptimizeSim3(gScm = Sim3(R, t, 1), 10) (:310-311), accepted when nInliers >= 20
+// (:314-325); a rejected candidate's next success is computed and the walk goes on.  Each pass gates
+// one success per unresolved event (one launch of each stage over all of them).
+int rsc_loop_events_gated(rsc_sim3* const* solvers, const rsc_loop_candidate* cands, const int32_t* event_begin,
+                          int n_events, rsc_sim3_result* per_candidate, rsc_loop_gate_result* per_event,
+                          int32_t* const* matches_out) {
+    if (n_events <= 0) return RSC_OK;
+    if (!solvers || !cands || !event_begin || !per_candidate || !per_event) return RSC_ERR_ARG;
+    const int total = event_begin[n_events];
+    rsc_context* C = nullptr;
+    for (int e = 0; e < n_events; ++e) {
+        if (event_begin[e + 1] < event_begin[e] || event_begin[e] < 0) return RSC_ERR_ARG;
+        rsc_loop_gate_result& r = per_event[e];
+        std::memset(&r, 0, sizeof(r));
+        r.status = RSC_GATE_NONE;
+        r.winner = r.round = r.hypothesis = -1;
+        for (int i = event_begin[e]; i < event_begin[e + 1]; ++i) {
+            const rsc_loop_candidate& k = cands[i];
+            if (!solvers[i] || !k.kf1 || !k.kf2) return RSC_ERR_ARG;
+            if (solvers[i]->stream) return RSC_ERR_UNSUPPORTED;
+            if (!C) C = solvers[i]->ctx;
+            if (solvers[i]->ctx != C || k.kf1->ctx != C || k.kf2->ctx != C) return RSC_ERR_ARG;
+            if (solvers[i]->st.mN1 != k.kf1->n || (k.kf1->n > 0 && !k.matches12)) return RSC_ERR_ARG;
+            if (k.kf1 != cands[event_begin[e]].kf1) return RSC_ERR_ARG;  // one mpCurrentKF per event
+            for (int a = 0; a < k.kf1->n; ++a)
+                if (k.matches12[a] < -2 || k.matches12[a] >= k.kf2->n) return RSC_ERR_ARG;
+        }
+    }
+    if (!C) return RSC_OK;
+    std::vector<int32_t> start_it(total), pos(total), calls(total, 0), s_round(total, -1);
+    std::vector<std::vector<uint8_t>> mask(total);
+    for (int i = 0; i < total; ++i) {
+        start_it[i] = pos[i] = solvers[i]->st.mnIterations;
+        mask[i].assign((size_t)std::max(solvers[i]->st.mN1, 1), 0);
+    }
+    // the next success of each listed candidate (s_round = its round, -1: none left)
+    auto refill = [&](const std::vector<int>& list) -> int {
+        if (list.empty()) return RSC_OK;
+        std::vector<rsc_sim3*> act;
+        std::vector<int32_t> its;
+        std::vector<uint8_t*> mp;
+        for (int i : list) {
+            act.push_back(solvers[i]);
+            its.push_back(std::max(1, solvers[i]->st.mRansacMaxIts - solvers[i]->st.mnIterations));
+            mp.push_back(mask[i].data());
+        }
+        std::vector<rsc_sim3_result> r(act.size());
+        if (int st = rsc_sim3_iterate_many(act.data(), (int)act.size(), its.data(), r.data(), mp.data())) return st;
+        for (size_t q = 0; q < list.size(); ++q) {
+            const int i = list[q];
+            per_candidate[i] = r[q];
+            if (!r[q].ok) {
+                s_round[i] = -1;
+                continue;
+            }
+            const int s = r[q].iterations - 1;
+            s_round[i] = calls[i] + (s - pos[i]) / 5;
+            pos[i] = s + 1;
+            calls[i] = s_round[i] + 1;
+        }
+        return RSC_OK;
+    };
+    {
+        std::vector<int> all(total);
+        for (int i = 0; i < total; ++i) all[i] = i;
+        if (int st = refill(all)) return st;
+    }
+    std::vector<char> resolved(n_events, 0);
+    for (;;) {
+        std::vector<int> ev, ci;  // one gate job per unresolved event: its smallest (round, candidate)
+        for (int e = 0; e < n_events; ++e) {
+            if (resolved[e]) continue;
+            int best = -1;
+            for (int i = event_begin[e]; i < event_begin[e + 1]; ++i)
+                if (s_round[i] >= 0 && (best < 0 || s_round[i] < s_round[best])) best = i;
+            if (best < 0) {
+                resolved[e] = 1;  // every candidate discarded: bMatch stays false
+                continue;
+            }
+            ev.push_back(e);
+            ci.push_back(best);
+        }
+        const int J = (int)ev.size();
+        if (J == 0) break;
+        // SearchBySim3 over the RANSAC inliers (vpMapPointMatches[j] = inlier ? match : NULL)
+        std::vector<rsc_kfview*> k1(J), k2(J);
+        std::vector<float> R12(9 * (size_t)J), t12(3 * (size_t)J);
+        std::vector<std::vector<int32_t>> m12(J), o12(J);
+        std::vector<const int32_t*> m12p(J);
+        std::vector<int32_t*> o12p(J);
+        std::vector<int32_t> nfound(J, 0);
+        for (int q = 0; q < J; ++q) {
+            const int i = ci[q];
+            const rsc_loop_candidate& k = cands[i];
+            k1[q] = k.kf1;
+            k2[q] = k.kf2;
+            std::memcpy(&R12[9 * (size_t)q], per_candidate[i].R, 9 * sizeof(float));
+            std::memcpy(&t12[3 * (size_t)q], per_candidate[i].t, 3 * sizeof(float));
+            const int n1 = k.kf1->n;
+            m12[q].assign((size_t)std::max(n1, 1), -1);
+            o12[q].assign((size_t)std::max(n1, 1), -1);
+            for (int a = 0; a < n1; ++a) m12[q][a] = mask[i][a] ? k.matches12[a] : -1;
+            m12p[q] = m12[q].data();
+            o12p[q] = o12[q].data();
+        }
+        if (int st = rsc_search_by_sim3_many(C, k1.data(), k2.data(), J, R12.data(), t12.data(), 7.5f, m12p.data(),
+                                             o12p.data(), nfound.data()))
+            return st;
+        // OptimizeSim3 on vpMapPointMatches after the search (Optimizer.cpp:1108-1171 slot rules)
+        std::vector<rsc_sim3opt_problem> pr(J);
+        std::vector<rsc_sim3opt_result> res(J);
+        std::vector<std::vector<uint8_t>> valid(J), keep(J);
+        std::vector<std::vector<float>> X1(J), X2(J), u1(J), u2(J), i1(J), i2(J);
+        std::vector<uint8_t*> keepp(J);
+        for (int q = 0; q < J; ++q) {
+            const int i = ci[q];
+            const rsc_kfview& a = *cands[i].kf1;
+            const rsc_kfview& b = *cands[i].kf2;
+            const int n1 = a.n;
+            for (int x = 0; x < n1; ++x)
+                if (o12[q][x] >= 0) m12[q][x] = o12[q][x];  // vpMatches12[i1] = vpMapPoints2[idx2]
+            valid[q].assign((size_t)std::max(n1, 1), 0);
+            keep[q].assign((size_t)std::max(n1, 1), 1);
+            X1[q].assign(3 * (size_t)std::max(n1, 1), 0.f);
+            X2[q].assign(3 * (size_t)std::max(n1, 1), 0.f);
+            u1[q].assign(2 * (size_t)std::max(n1, 1), 0.f);
+            u2[q].assign(2 * (size_t)std::max(n1, 1), 0.f);
+            i1[q].assign((size_t)std::max(n1, 1), 0.f);
+            i2[q].assign((size_t)std::max(n1, 1), 0.f);
+            for (int x = 0; x < n1; ++x) {
+                const int y = m12[q][x];
+                // vpMatches1[i] set, pMP1 set, neither bad, i2 = GetIndexInKeyFrame(pKF2) >= 0
+                if (y < 0 || a.mp_state[x] != 1 || b.mp_state[y] != 1) continue;
+                valid[q][x] = 1;
+                for (int c = 0; c < 3; ++c) {
+                    X1[q][3 * x + c] = a.mp_pos[3 * x + c];
+                    X2[q][3 * x + c] = b.mp_pos[3 * (size_t)y + c];
+                }
+                u1[q][2 * x] = a.kp[2 * x];
+                u1[q][2 * x + 1] = a.kp[2 * x + 1];
+                u2[q][2 * x] = b.kp[2 * (size_t)y];
+                u2[q][2 * x + 1] = b.kp[2 * (size_t)y + 1];
+                const int o1 = a.octave[x], o2 = b.octave[y];
+                if (o1 < 0 || o1 >= (int)a.inv_level_sigma2.size() || o2 < 0 || o2 >= (int)b.inv_level_sigma2.size())
+                    return RSC_ERR_ARG;
+                i1[q][x] = a.inv_level_sigma2[o1];
+                i2[q][x] = b.inv_level_sigma2[o2];
+            }
+            rsc_sim3opt_problem& P = pr[q];
+            P.n = n1;
+            P.valid = valid[q].data();
+            P.X1w = X1[q].data();
+            P.X2w = X2[q].data();
+            P.uv1 = u1[q].data();
+            P.uv2 = u2[q].data();
+            P.inv1 = i1[q].data();
+            P.inv2 = i2[q].data();
+            std::memcpy(P.R1w, a.R, sizeof(P.R1w));
+            std::memcpy(P.t1w, a.t, sizeof(P.t1w));
+            std::memcpy(P.R2w, b.R, sizeof(P.R2w));
+            std::memcpy(P.t2w, b.t, sizeof(P.t2w));
+            std::memcpy(P.K1, a.K, sizeof(P.K1));
+            std::memcpy(P.K2, b.K, sizeof(P.K2));
+            // g2o::Sim3 gScm(R.cast<double>(), t.cast<double>(), 1.0): Quaterniond(R), no normalisation
+            double Rd[3][3];
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) Rd[r][c] = (double)per_candidate[i].R[3 * r + c];
+            const PoQuat qq = po_quat_from_R(Rd);
+            P.S[0] = qq.x; P.S[1] = qq.y; P.S[2] = qq.z; P.S[3] = qq.w;
+            for (int c = 0; c < 3; ++c) P.S[4 + c] = (double)per_candidate[i].t[c];
+            P.S[7] = 1.0;
+            P.th2 = 10.0f;
+            keepp[q] = keep[q].data();
+        }
+        if (int st = rsc_optimize_sim3_many(C, pr.data(), J, res.data(), keepp.data())) return st;
+        std::vector<int> again;
+        for (int q = 0; q < J; ++q) {
+            const int e = ev[q], i = ci[q];
+            rsc_loop_gate_result& g = per_event[e];
+            if (res[q].n_inliers < 20) {  // LoopClosing.cpp:314: not accepted, the round-robin goes on
+                g.rejected++;
+                again.push_back(i);
+                continue;
+            }
+            g.status = RSC_GATE_MATCH;
+            g.winner = i - event_begin[e];
+            g.round = s_round[i];
+            g.hypothesis = per_candidate[i].iterations - 1 - start_it[i];
+            g.n_inliers = per_candidate[i].n_inliers;
+            g.n_found = nfound[q];
+            g.n_opt_inliers = res[q].n_inliers;
+            std::memcpy(g.S, res[q].S, sizeof(g.S));
+            if (matches_out && matches_out[e]) {
+                const int n1 = cands[i].kf1->n;
+                for (int x = 0; x < n1; ++x) matches_out[e][x] = keep[q][x] ? m12[q][x] : -1;  // outliers NULLed
+            }
+            resolved[e] = 1;
+        }
+        if (int st = refill(again)) return st;
+    }
+    return RSC_OK;
 }
 }  // extern "C"

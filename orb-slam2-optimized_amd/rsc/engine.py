@@ -51,12 +51,35 @@ EXPORTED = [
     "rsc_kfdb_set_covisibility", "rsc_kfdb_set_covisibility_many", "rsc_kfdb_detect_relocalization", "rsc_kfdb_detect_loop", "rsc_kfdb_state",
     "rsc_stream_create", "rsc_stream_destroy", "rsc_stream_skip", "rsc_stream_position", "rsc_stream_peek",
     "rsc_pnp_bind_stream", "rsc_sim3_bind_stream", "rsc_mlpnp_bind_stream", "rsc_reloc_events_shared",
-    "rsc_loop_events_shared",
+    "rsc_loop_events_shared", "rsc_reloc_events_gated", "rsc_loop_events_gated",
 ]
+
+# include/rsc.h RSC_GATE_*
+GATE_NONE, GATE_MATCH, GATE_HANDOFF = 0, 1, 2
 
 
 class EventResult(C.Structure):
     _fields_ = [("winner", C.c_int32), ("round", C.c_int32), ("hypothesis", C.c_int32), ("n_inliers", C.c_int32)]
+
+
+class RelocFrame(C.Structure):
+    _fields_ = [("u_right", C.c_void_p), ("bf", C.c_float)]
+
+
+class RelocGateResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("winner", C.c_int32), ("round", C.c_int32), ("hypothesis", C.c_int32),
+                ("n_inliers", C.c_int32), ("n_good", C.c_int32), ("rejected", C.c_int32), ("gates", C.c_int32),
+                ("Tcw", C.c_float * 16)]
+
+
+class LoopCandidate(C.Structure):
+    _fields_ = [("kf1", C.c_void_p), ("kf2", C.c_void_p), ("matches12", C.c_void_p)]
+
+
+class LoopGateResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("winner", C.c_int32), ("round", C.c_int32), ("hypothesis", C.c_int32),
+                ("n_inliers", C.c_int32), ("n_found", C.c_int32), ("n_opt_inliers", C.c_int32),
+                ("rejected", C.c_int32), ("S", C.c_double * 8)]
 
 
 class PnPProblem(C.Structure):
@@ -430,6 +453,10 @@ def load_library(path: str = LIB_PATH):
     L.rsc_kfdb_detect_loop.argtypes = [vp, C.c_uint64, C.c_int, u32p_, f64p_, C.c_int, i32p, C.c_float, i32p, i32p]
     L.rsc_kfdb_state.argtypes = [vp, C.c_int, u64p_, i32p, f32p_]
     L.rsc_loop_events.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(Sim3Result), C.POINTER(EventResult)]
+    L.rsc_reloc_events_gated.argtypes = [C.POINTER(vp), i32p, C.c_int, C.POINTER(RelocFrame), C.POINTER(PnPResult),
+                                         C.POINTER(RelocGateResult), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+    L.rsc_loop_events_gated.argtypes = [C.POINTER(vp), C.POINTER(LoopCandidate), i32p, C.c_int,
+                                        C.POINTER(Sim3Result), C.POINTER(LoopGateResult), C.POINTER(C.c_void_p)]
     _lib = L
     return L
 
@@ -936,6 +963,58 @@ class EventBatch:
         f = L.rsc_loop_events_shared if self.kind == "sim3" else L.rsc_reloc_events_shared
         _check(f(self.batch._h, self.begin, len(self.events), hs, self._cand, self._ev), "events_shared")
         return self.per_event
+
+    def run_reloc_gated(self, frames):
+        """Relocalization events with the reference's PoseOptimization gate (rsc_reloc_events_gated,
+        Tracking.cpp:1239-1335).  frames[e] = (u_right [n_points] float32 or None, bf).  Returns
+        (per-event RelocGateResult records, winner outlier masks, winner vbInliers) — the masks are
+        [n_points] uint8 arrays per event (zeros without a winner)."""
+        assert self.kind == "pnp"
+        if len(frames) != len(self.events):
+            raise ValueError(f"one frame per event: {len(self.events)} events, {len(frames)} frames")
+        L = load_library()
+        fr = (RelocFrame * len(self.events))()
+        keep = []
+        for e, (ur, bf) in enumerate(frames):
+            if ur is not None:
+                a = np.ascontiguousarray(ur, np.float32)
+                keep.append(a)
+                fr[e].u_right = a.ctypes.data
+            fr[e].bf = float(bf)
+        res = (RelocGateResult * len(self.events))()
+        npts = [ev[0].n_points if ev else 0 for ev in self.events]
+        outl = [np.zeros(max(n, 1), np.uint8) for n in npts]
+        inl = [np.zeros(max(n, 1), np.uint8) for n in npts]
+        po = (C.c_void_p * len(self.events))(*[a.ctypes.data for a in outl])
+        pi = (C.c_void_p * len(self.events))(*[a.ctypes.data for a in inl])
+        _check(L.rsc_reloc_events_gated(self.batch._h, self.begin, len(self.events), fr, self._cand, res, po, pi),
+               "reloc_events_gated")
+        return np.ctypeslib.as_array(res).copy(), [o[:n] for o, n in zip(outl, npts)], \
+            [m[:n] for m, n in zip(inl, npts)]
+
+    def run_loop_gated(self, candidates):
+        """Loop-closure events with the reference's SearchBySim3 + OptimizeSim3 gate
+        (rsc_loop_events_gated, LoopClosing.cpp:268-329).  candidates[e][c] = (KFView of mpCurrentKF,
+        KFView of the candidate, matches12 int32 [kf1 n]).  Returns (per-event LoopGateResult records,
+        the accepted candidate's mvpCurrentMatchedPoints per event as KF2 indices)."""
+        assert self.kind == "sim3"
+        if len(candidates) != len(self.events) or any(len(c) != len(ev) for c, ev in zip(candidates, self.events)):
+            raise ValueError("one (kf1, kf2, matches12) per candidate of every event")
+        L = load_library()
+        flat = [c for cs in candidates for c in cs]
+        lc = (LoopCandidate * max(len(flat), 1))()
+        keep = []
+        for k, (v1, v2, m) in enumerate(flat):
+            a = np.ascontiguousarray(m, np.int32)
+            keep.append(a)
+            lc[k].kf1, lc[k].kf2, lc[k].matches12 = v1.h.value, v2.h.value, a.ctypes.data
+        res = (LoopGateResult * len(self.events))()
+        n1 = [cs[0][0].n if cs else 0 for cs in candidates]
+        mo = [np.full(max(n, 1), -1, np.int32) for n in n1]
+        pm = (C.c_void_p * len(self.events))(*[a.ctypes.data for a in mo])
+        _check(L.rsc_loop_events_gated(self.batch._h, lc, self.begin, len(self.events), self._cand, res, pm),
+               "loop_events_gated")
+        return np.ctypeslib.as_array(res).copy(), [m[:n] for m, n in zip(mo, n1)]
 
     def winner_poses(self) -> np.ndarray:
         """[n_events, 16] float32 pose of each event's winning candidate (PnP Tcw row-major, Sim3

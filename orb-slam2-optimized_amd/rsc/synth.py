@@ -715,3 +715,116 @@ def make_kfdb_scene(rng: np.random.Generator, n_kfs: int, words_per_kf: int = 60
 def make_kfdb_query(rng: np.random.Generator, sc: KFDBScene, pos: float, words: int = 600):
     """A Frame's (or new KeyFrame's) BowVector observed at trajectory position pos."""
     return _bow_from(rng, _place_words(rng, sc, pos, words))
+
+
+# ---- Gated events (rsc_reloc_events_gated / rsc_loop_events_gated) -------------------------------
+def make_reloc_gate_event(rng: np.random.Generator, n_frame: int, cands, poisoned=(), stereo_frac: float = 0.0):
+    """One Tracking::Relocalization() call: candidate scenes (n, inlier ratio) whose matches are subsets
+    of one current Frame's n_frame keypoint slots (kp_index), and the Frame's mvuRight / mbf.
+    Candidates listed in `poisoned` have a right-image coordinate on every slot they match that
+    disagrees with their pose by 100+ px (a wrong stereo match), so PoseOptimization classifies those
+    stereo edges as outliers (chi2 > 7.815) and the RANSAC pose is rejected (nGood < 10); with
+    stereo_frac > 0 that share of the other candidates' slots carries a consistent mvuRight.
+    Returns (scenes, u_right float32 [n_frame] (-1 = monocular slot), bf)."""
+    scenes = [make_pnp_scene(rng, int(n), float(r), n_points=n_frame) for n, r in cands]
+    ur = np.full(n_frame, -1.0, np.float32)
+    for c, sc in enumerate(scenes):
+        if c in poisoned:
+            continue
+        pc = sc.p3dw.astype(np.float64) @ sc.R_true.T + sc.t_true
+        u = sc.p2d[:, 0].astype(np.float64) - float(EUROC_BF) / np.maximum(pc[:, 2], 1e-3)
+        st = (rng.random(sc.n) < stereo_frac) & (u >= 0.0) & sc.inlier_true
+        ur[sc.kp_index[st]] = u[st].astype(np.float32)
+    for c in poisoned:
+        sc = scenes[c]
+        ur[sc.kp_index] = (sc.p2d[:, 0] + rng.uniform(100.0, 200.0, sc.n)).astype(np.float32)
+    return scenes, ur, EUROC_BF
+
+
+def _make_kf(rng, P, mp_desc, R, t, n_extra, bad_frac, noise_px):
+    """A KeyFrame (Sim3KF) observing the world points P from pose (R, t): keypoints of the visible points
+    (+ pixel noise) and n_extra unmatched ones in a random order, octaves, descriptors, MapPoints."""
+    sf = scale_factors()
+    Xc = P @ R.T + t
+    uv = np.stack([FX * Xc[:, 0] / Xc[:, 2] + CX, FY * Xc[:, 1] / Xc[:, 2] + CY], 1)
+    vis = (Xc[:, 2] > 0.1) & (uv[:, 0] >= 0) & (uv[:, 0] < WIDTH) & (uv[:, 1] >= 0) & (uv[:, 1] < HEIGHT)
+    ids = np.nonzero(vis)[0]
+    m = len(ids) + n_extra
+    kp = np.zeros((m, 2), np.float32)
+    kp[:len(ids)] = uv[ids] + rng.normal(0, noise_px, (len(ids), 2))
+    kp[len(ids):] = np.stack([rng.uniform(0, WIDTH, n_extra), rng.uniform(0, HEIGHT, n_extra)], 1)
+    kp = np.clip(kp, 0, [WIDTH - 1e-3, HEIGHT - 1e-3]).astype(np.float32)
+    octave = rng.choice(N_LEVELS, size=m, p=level_probabilities()).astype(np.int32)
+    desc = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+    desc[:len(ids)] = _flip(rng, mp_desc[ids], 8.0)
+    perm = rng.permutation(m)
+    kp, octave, desc = kp[perm], octave[perm], desc[perm]
+    mp_id = np.concatenate([ids, np.full(n_extra, -1)])[perm].astype(np.int64)
+    has = mp_id >= 0
+    state = np.where(has, 1, 0).astype(np.uint8)
+    state[has & (rng.random(m) < bad_frac)] = 2
+    pos = np.zeros((m, 3), np.float32)
+    pos[has] = P[mp_id[has]]
+    dist = np.linalg.norm(P[np.maximum(mp_id, 0)] - (-R.T @ t), axis=1)
+    dmax = np.where(has, dist * sf[octave], 0).astype(np.float32)
+    dmin = (dmax / sf[N_LEVELS - 1]).astype(np.float32)
+    mdesc = np.zeros((m, 32), np.uint8)
+    mdesc[has] = mp_desc[mp_id[has]]
+    begin, feat = build_grid(kp)
+    return Sim3KF(m, kp, octave, desc, begin, feat, R.astype(np.float32), t.astype(np.float32), state, pos, dmax,
+                  dmin, mdesc, mp_id)
+
+
+def sim3_pair_from_kfs(kf1: Sim3KF, kf2: Sim3KF, matches12: np.ndarray) -> Sim3Pair:
+    """Sim3Solver(pKF1, pKF2, vpMatched12) constructor inputs (Sim3Solver.cpp:6-85) from two KeyFrame
+    views and the BoW matches (KF2 keypoint index per KF1 slot, -1 none): a slot is usable when both
+    MapPoints exist and neither is bad; sigma^2 from the keypoints' octaves."""
+    s2 = level_sigma2()
+    n1 = kf1.n
+    m = np.asarray(matches12)
+    y = np.maximum(m, 0)
+    valid = (m >= 0) & (kf1.mp_state == 1) & (kf2.mp_state[y] == 1)
+    K = np.array([kf1.fx, kf1.fy, kf1.cx, kf1.cy], np.float32)
+    return Sim3Pair(valid=valid.astype(np.uint8), Xw1=np.ascontiguousarray(kf1.mp_pos, np.float32),
+                    Xw2=np.ascontiguousarray(kf2.mp_pos[y], np.float32),
+                    sigma2_1=s2[kf1.octave].astype(np.float32), sigma2_2=s2[kf2.octave[y]].astype(np.float32),
+                    R1=kf1.Rcw, t1=kf1.tcw, R2=kf2.Rcw, t2=kf2.tcw, K1=K, K2=K.copy(),
+                    inlier_true=np.zeros(n1, bool))
+
+
+def make_loop_gate_event(rng: np.random.Generator, cands, n_points: int = 700, n_extra: int = 150,
+                         match_frac: float = 0.6, poisoned=()):
+    """One LoopClosing::ComputeSim3() call: the current KeyFrame and candidate KeyFrames observing a
+    shared world (no map drift, scale 1), with BoW-style matches12 per candidate: cands = [right-match
+    share, ...] of the matched KF1 MapPoints (the rest matched to a random KF2 MapPoint).  Candidates in
+    `poisoned` carry keypoints displaced by 30-60 px from their MapPoints' projections (their Sim3
+    RANSAC, which projects 3D points and never reads keypoints, still succeeds; OptimizeSim3's
+    KF2-side reprojection edges all exceed th2, so the gate rejects it).
+    Returns (kf1, [(kf2, matches12, Sim3Pair)])."""
+    P = np.stack([rng.uniform(-3, 3, n_points), rng.uniform(-2, 2, n_points), rng.uniform(2, 9, n_points)], 1)
+    mp_desc = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    R1 = random_rotation(rng, 0.2)
+    t1 = np.zeros(3)
+    kf1 = _make_kf(rng, P, mp_desc, R1, t1, n_extra, 0.02, 1.0)
+    out = []
+    for c, good in enumerate(cands):
+        R2 = random_rotation(rng, 0.12) @ R1
+        t2 = -R2 @ rng.normal(0, 0.25, 3)
+        kf2 = _make_kf(rng, P, mp_desc, R2, t2, n_extra, 0.02, 1.0)
+        if c in poisoned:
+            has = kf2.mp_id >= 0
+            k = int(has.sum())
+            off = rng.choice([-1.0, 1.0], (k, 2)) * rng.uniform(30.0, 60.0, (k, 2))
+            kp = kf2.kp.copy()
+            kp[has] = np.clip(kp[has] + off, 0, [WIDTH - 1e-3, HEIGHT - 1e-3])
+            kf2.kp = kp.astype(np.float32)
+            kf2.cell_begin, kf2.cell_feat = build_grid(kf2.kp)
+        where2 = {int(i): j for j, i in enumerate(kf2.mp_id) if i >= 0}
+        with_mp2 = np.nonzero(kf2.mp_id >= 0)[0]
+        m12 = np.full(kf1.n, -1, np.int32)
+        for i, mid in enumerate(kf1.mp_id):
+            if mid < 0 or int(mid) not in where2 or rng.random() >= match_frac:
+                continue
+            m12[i] = where2[int(mid)] if rng.random() < good else int(rng.choice(with_mp2))
+        out.append((kf2, m12, sim3_pair_from_kfs(kf1, kf2, m12)))
+    return kf1, out
