@@ -290,6 +290,15 @@ constexpr int kFoldStride = 65;
 #define RSC_REFINE_EIG_LANES 4
 #endif
 constexpr int kRefineEigLanes = RSC_REFINE_EIG_LANES;
+// Refine beta waves: the Jacobi SVD's U / V rows distributed over the (uniform) wave's lanes
+#ifndef RSC_REFINE_LANE_ROWS
+#define RSC_REFINE_LANE_ROWS 1
+#endif
+constexpr bool kRefineLaneRows = RSC_REFINE_LANE_ROWS != 0;
+// Refine MtM fold with the LDS reads of the next 8 rows issued ahead of the current 8 rows' adds
+#ifndef RSC_MTM_PIPELINE
+#define RSC_MTM_PIPELINE 1
+#endif
 static_assert(kRefineEigLanes == 2 || kRefineEigLanes == 4, "refine eigen group: pair or quad");
 
 // Eigen stage in the Refine's rows form for small launches (rsc_quad.h pnp_eig_rows_body; A/B
@@ -473,6 +482,80 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
     __syncthreads();
     refine_stamp(2);
     // 3. MtM lower triangle, one entry per folding thread, each folded over the 2*nr rows in order.
+#if RSC_MTM_PIPELINE
+    // The rows of M are staged through LDS in chunks of 128 correspondences (256 rows), column-major
+    // (column j of the chunk at j * kMtmRS, rows contiguous; kMtmRS = 258 doubles puts the 12 columns
+    // on different LDS banks) and double-buffered: lanes 0..38 of waves 0 and 1 fold chunk c (the 78
+    // entries) while waves 2 and 3 stage chunk c + 1, one correspondence (its two rows of M,
+    // PnPsolver.cpp:365-377, the values of M_entry) per thread, one 16-byte store per column.  A
+    // folder reads two rows of each of its columns per 16-byte load and issues the next 8 rows' loads
+    // before adding the current 8 products, so the LDS round trip stays off the ordered add chain.
+    {
+        constexpr int kPairs = 128, kMtmRS = 2 * kPairs + 2;
+        __shared__ __attribute__((aligned(16))) double mtm_buf[2][12 * kMtmRS];
+        const bool folder = wave < 2 && lane < 39;
+        int a = 0, b = wave * 39 + lane;
+        while (b > a) { b -= a + 1; ++a; }  // fold id -> (a,b) with b <= a, row-major lower triangle
+        const int nchunks = (nr + kPairs - 1) / kPairs;
+        auto stage = [&](int c, int t0, int nt) {
+            const int i0 = c * kPairs, m = min(kPairs, nr - i0);
+            double* dst = mtm_buf[c & 1];
+            for (int t = t0; t < m; t += nt) {
+                const int i = i0 + t;
+                const double al4[4] = {als[4 * i], als[4 * i + 1], als[4 * i + 2], als[4 * i + 3]};
+                const double u0 = us[2 * i], u1 = us[2 * i + 1];
+                RSC_UNROLL for (int j = 0; j < 4; ++j) {  // (row 2i, row 2i + 1) of columns 3j .. 3j + 2
+                    *reinterpret_cast<double2*>(dst + (3 * j) * kMtmRS + 2 * t) = double2{al4[j] * K.fx, 0.0};
+                    *reinterpret_cast<double2*>(dst + (3 * j + 1) * kMtmRS + 2 * t) = double2{0.0, al4[j] * K.fy};
+                    *reinterpret_cast<double2*>(dst + (3 * j + 2) * kMtmRS + 2 * t) =
+                        double2{al4[j] * (K.cx - u0), al4[j] * (K.cy - u1)};
+                }
+            }
+        };
+        if (nchunks > 0) stage(0, tid, 256);
+        __syncthreads();
+        double s = 0.0;
+        for (int c = 0; c < nchunks; ++c) {
+            if (wave >= 2 && c + 1 < nchunks) stage(c + 1, tid - 128, 128);
+            if (folder) {
+                const double* Ma = mtm_buf[c & 1] + a * kMtmRS;
+                const double* Mb = mtm_buf[c & 1] + b * kMtmRS;
+                const int m = 2 * min(kPairs, nr - c * kPairs);  // even, >= 2
+                int r = 0;
+                if (c == 0) {
+                    s = Ma[0] * Mb[0];
+                    s = s + Ma[1] * Mb[1];
+                    r = 2;
+                }
+                if (r + 8 <= m) {
+                    double p[8];
+                    RSC_UNROLL for (int k = 0; k < 4; ++k) {
+                        const double2 x = *reinterpret_cast<const double2*>(Ma + r + 2 * k);
+                        const double2 y = *reinterpret_cast<const double2*>(Mb + r + 2 * k);
+                        p[2 * k] = x.x * y.x;
+                        p[2 * k + 1] = x.y * y.y;
+                    }
+                    for (r += 8; r + 8 <= m; r += 8) {
+                        double2 x[4], y[4];
+                        RSC_UNROLL for (int k = 0; k < 4; ++k) {
+                            x[k] = *reinterpret_cast<const double2*>(Ma + r + 2 * k);
+                            y[k] = *reinterpret_cast<const double2*>(Mb + r + 2 * k);
+                        }
+                        RSC_UNROLL for (int k = 0; k < 8; ++k) s = s + p[k];
+                        RSC_UNROLL for (int k = 0; k < 4; ++k) {
+                            p[2 * k] = x[k].x * y[k].x;
+                            p[2 * k + 1] = x[k].y * y[k].y;
+                        }
+                    }
+                    RSC_UNROLL for (int k = 0; k < 8; ++k) s = s + p[k];
+                }
+                for (; r < m; ++r) s = s + Ma[r] * Mb[r];
+            }
+            __syncthreads();  // chunk c folded, chunk c + 1 staged
+        }
+        if (folder) S.at(a, b) = s;
+    }
+#else
     // The rows of M are staged through LDS in chunks of 97 correspondences (194 rows x 12),
     // double-buffered: lanes 0..38 of waves 0 and 1 fold chunk c (the 78 entries) while waves 2 and 3
     // stage chunk c + 1, one correspondence (its two rows of M, PnPsolver.cpp:365-377, the values of
@@ -529,6 +612,7 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
         }
         if (folder) S.at(a, b) = s;
     }
+#endif
     __syncthreads();
     refine_stamp(3);
     // 4. 12x12 eigenvectors (rows_eig12_ev4: Householder phases on lanes 0..kRefineEigLanes-1 of
@@ -560,9 +644,9 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
         __shared__ double ccs_sh[3][12];
         {  // every lane of the wave (identical values and writes; see the control points above)
             double betas[4] = {0.0, 0.0, 0.0, 0.0};
-            if (wave == 0) find_betas<1>(SV, betas);
-            else if (wave == 1) find_betas<2>(SV, betas);
-            else find_betas<3>(SV, betas);
+            if (wave == 0) find_betas<1, SlabView, kRefineLaneRows>(SV, betas);
+            else if (wave == 1) find_betas<2, SlabView, kRefineLaneRows>(SV, betas);
+            else find_betas<3, SlabView, kRefineLaneRows>(SV, betas);
             gauss_newton(SV, betas);
             double ccs[4][3];
             ccs_with_sign(st, SV, betas, ccs);

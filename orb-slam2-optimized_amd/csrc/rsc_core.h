@@ -684,7 +684,19 @@ RSC_HD bool sym_eig12(const LaneMat& M) {
     do {                     \
     } while (0)
 #endif
-template <int k>
+// LaneRows (device, a wave whose lanes all hold the same problem — the Refine's beta waves): U and V
+// are not replicated; lane r keeps row r of U (r < 6) and of V (r < k) and applies each Jacobi
+// rotation to its own row (2 products + 1 sum per matrix instead of 6 + 5 rows per lane), the rows
+// gathered with readlane for the final solve.  Same operations on the same operands per entry, so
+// the result is bit-identical to the replicated form.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ double lane_read(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+#endif
+template <int k, bool LaneRows = false>
 RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6], double (&x)[k]) {
     constexpr int rows = 6;
     const double eps = lim<double>::eps();
@@ -819,6 +831,20 @@ RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6]
     }
     RSC_UNROLL for (int r = 0; r < k; ++r)
         RSC_UNROLL for (int c = 0; c < k; ++c) V[r][c] = (perm[c] == r) ? 1.0 : 0.0;
+    // LaneRows: this lane's rows of U and V (lanes beyond 6 / k carry rows nobody reads)
+    double Ur[k], Vr[k];
+    if constexpr (LaneRows) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const int ln = (int)(threadIdx.x & 63u);
+        RSC_UNROLL for (int c = 0; c < k; ++c) {
+            double u = U[0][c], v = V[0][c];
+            RSC_UNROLL for (int r = 1; r < rows; ++r) u = (ln == r) ? U[r][c] : u;
+            RSC_UNROLL for (int r = 1; r < k; ++r) v = (ln == r) ? V[r][c] : v;
+            Ur[c] = u;
+            Vr[c] = v;
+        }
+#endif
+    }
 
     RSC_JSVD_STAMP(k, 1);  // U formed
     double maxDiag = rabs(W[0][0]);
@@ -873,10 +899,16 @@ RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6]
                             W[p][c] = cl * xi + sl * yi;
                             W[q][c] = -sl * xi + cl * yi;
                         }
-                        RSC_UNROLL for (int r = 0; r < rows; ++r) {
-                            double xi = U[r][p], yi = U[r][q];
-                            U[r][p] = cl * xi + sl * yi;
-                            U[r][q] = -sl * xi + cl * yi;
+                        if constexpr (LaneRows) {
+                            const double xi = Ur[p], yi = Ur[q];
+                            Ur[p] = cl * xi + sl * yi;
+                            Ur[q] = -sl * xi + cl * yi;
+                        } else {
+                            RSC_UNROLL for (int r = 0; r < rows; ++r) {
+                                double xi = U[r][p], yi = U[r][q];
+                                U[r][p] = cl * xi + sl * yi;
+                                U[r][q] = -sl * xi + cl * yi;
+                            }
                         }
                     }
                     if (!(cr == 1.0 && sr == 0.0)) {
@@ -885,10 +917,16 @@ RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6]
                             W[r][p] = cr * xi - sr * yi;
                             W[r][q] = sr * xi + cr * yi;
                         }
-                        RSC_UNROLL for (int r = 0; r < k; ++r) {
-                            double xi = V[r][p], yi = V[r][q];
-                            V[r][p] = cr * xi - sr * yi;
-                            V[r][q] = sr * xi + cr * yi;
+                        if constexpr (LaneRows) {
+                            const double xi = Vr[p], yi = Vr[q];
+                            Vr[p] = cr * xi - sr * yi;
+                            Vr[q] = sr * xi + cr * yi;
+                        } else {
+                            RSC_UNROLL for (int r = 0; r < k; ++r) {
+                                double xi = V[r][p], yi = V[r][q];
+                                V[r][p] = cr * xi - sr * yi;
+                                V[r][q] = sr * xi + cr * yi;
+                            }
                         }
                     }
                     double a = rabs(W[p][p]), bq = rabs(W[q][q]);
@@ -900,6 +938,14 @@ RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6]
         RSC_LOOP_FENCE();
     }
     RSC_JSVD_STAMP(k, 2);  // Jacobi sweeps done
+    if constexpr (LaneRows) {  // rows back from their lanes (uniform values) for the sort and solve
+#if defined(__HIP_DEVICE_COMPILE__)
+        RSC_UNROLL for (int c = 0; c < k; ++c) {
+            RSC_UNROLL for (int r = 0; r < rows; ++r) U[r][c] = lane_read(Ur[c], r);
+            RSC_UNROLL for (int r = 0; r < k; ++r) V[r][c] = lane_read(Vr[c], r);
+        }
+#endif
+    }
     double sv[k];
     RSC_UNROLL for (int i = 0; i < k; ++i) {
         double a = W[i][i];

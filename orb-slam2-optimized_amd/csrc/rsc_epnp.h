@@ -280,7 +280,8 @@ RSC_HD void gauss_newton(const SV& S, double (&betas)[4]) {
 }
 
 // find_betas_approx_{1,2,3} (PnPsolver.cpp:520-602).
-template <int which, class SV>
+// LaneRows: the wave's lanes hold the same problem (jacobi_svd_solve_6xk's lane-row form).
+template <int which, class SV, bool LaneRows = false>
 RSC_HD void find_betas(const SV& S, double (&betas)[4]) {
     double rho[6];
     RSC_UNROLL for (int r = 0; r < 6; ++r) rho[r] = S.rho(r);
@@ -289,7 +290,7 @@ RSC_HD void find_betas(const SV& S, double (&betas)[4]) {
         RSC_UNROLL for (int r = 0; r < 6; ++r) {
             A[r][0] = S.L(r, 0); A[r][1] = S.L(r, 1); A[r][2] = S.L(r, 3); A[r][3] = S.L(r, 6);
         }
-        jacobi_svd_solve_6xk<4>(A, rho, b4);
+        jacobi_svd_solve_6xk<4, LaneRows>(A, rho, b4);
         if (b4[0] < 0) {
             betas[0] = sqrt(-b4[0]);
             betas[1] = -b4[1] / betas[0];
@@ -304,7 +305,7 @@ RSC_HD void find_betas(const SV& S, double (&betas)[4]) {
     } else if (which == 2) {
         double A[6][3], b3[3];
         RSC_UNROLL for (int r = 0; r < 6; ++r) { A[r][0] = S.L(r, 0); A[r][1] = S.L(r, 1); A[r][2] = S.L(r, 2); }
-        jacobi_svd_solve_6xk<3>(A, rho, b3);
+        jacobi_svd_solve_6xk<3, LaneRows>(A, rho, b3);
         if (b3[0] < 0) {
             betas[0] = sqrt(-b3[0]);
             betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
@@ -319,7 +320,7 @@ RSC_HD void find_betas(const SV& S, double (&betas)[4]) {
         double A[6][5], b5[5];
         RSC_UNROLL for (int r = 0; r < 6; ++r)
             RSC_UNROLL for (int c = 0; c < 5; ++c) A[r][c] = S.L(r, c);
-        jacobi_svd_solve_6xk<5>(A, rho, b5);
+        jacobi_svd_solve_6xk<5, LaneRows>(A, rho, b5);
         if (b5[0] < 0) {
             betas[0] = sqrt(-b5[0]);
             betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;

@@ -94,4 +94,25 @@ if [ -n "$GPUS2" ]; then
   timeout -k 10 300 python bench.py --gpus 2 --dist-backend gloo --no-cpu --no-latency --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --steps 8 --warmup 2 > $OUT/bench_gpus2_gloo.json 2> $OUT/bench_gpus2_gloo.err
   timeout -k 10 300 python bench.py --gpus 4 --dist-backend gloo --no-cpu --no-latency --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --steps 8 --warmup 2 > $OUT/bench_gpus4_gloo.json 2> $OUT/bench_gpus4_gloo.err
 fi
+if [ -n "$REFAB" ]; then
+  # Refine phase stamps of the single relocalization event for stamped builds of the libraries named
+  # in REFAB (tools/bin/librsc_<name>.so: make -C tools variant NAME=<name> DEFS=...), interleaved
+  cd $GRAFT_REPO_ROOT
+  for rep in 1 2; do
+    for v in $REFAB; do
+      echo "== $v rep $rep" >> $OUT/refine_probe_$v.txt
+      RSC_LIBRSC=tools/bin/librsc_$v.so timeout -k 10 120 python tools/refine_probe.py event >> $OUT/refine_probe_$v.txt 2>&1
+    done
+  done
+fi
+if [ -n "$LIBAB" ]; then
+  # headline + single-event latency per library (product = "product"), interleaved twice
+  cd $GRAFT_REPO_ROOT
+  for rep in 1 2; do
+    for v in $LIBAB; do
+      if [ $v = product ]; then L=orb-slam2-optimized_amd/lib/librsc.so; else L=tools/bin/librsc_$v.so; fi
+      RSC_LIBRSC=$L timeout -k 10 300 python bench.py --no-cpu --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --no-mlpnp --no-events --no-sim3 >> $OUT/libab_$v.jsonl 2>> $OUT/libab.err
+    done
+  done
+fi
 echo done > $OUT/done
