@@ -36,6 +36,7 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6    # MI355X vector FP64 (spec)
 FP32_PEAK_TFLOPS = 157.3   # MI355X vector FP32 (spec)
+LDS_PEAK_TBS = 78.6        # 256 CU x 128 B/clk x 2.4 GHz
 
 
 def _round_dirs():
@@ -1232,6 +1233,40 @@ def headline_roofline(args, r):
             "sources": {"S_h": f"{opc_src} (tools/opcount_report.py)",
                         "traffic": (f"{traffic_src} (2 x FETCH_SIZE + WRITE_SIZE, commit "
                                     f"{traffic.get('commit')})") if traffic else None}}
+    # SURVEY.md section 8(d) "also report": the scan's FP32 fraction (F_h = 31 N FP32-equivalent flops per
+    # hypothesis) over the scan kernel's time, and the achieved LDS bandwidth fraction of the launch
+    # set (upper estimate: PMC SQ_INSTS_LDS x 64 lanes x 8 B, 256 CU x 128 B/clk x 2.4 GHz peak)
+    F_h = 31 * args.corrs
+    if scan_ms > 0:
+        tf32 = per_launch_hyps * F_h / (scan_ms * 1e-3) / 1e12
+        roof["scan_fp32"] = {"kernel": "pnp_scan_kernel", "achieved": round(tf32, 4), "peak": FP32_PEAK_TFLOPS,
+                             "unit": "TFLOP/s", "frac": round(tf32 / FP32_PEAK_TFLOPS, 5),
+                             "F_h_flops_per_hypothesis": F_h}
+    lds, lds_src = _profile_json("pmc_lds.json")
+    if lds and set_ms > 0:
+        b = lds["lds_bytes_upper_per_launch_set"]
+        roof["lds"] = {"bytes_per_launch_set_upper": round(b), "achieved_TBs": round(b / (set_ms * 1e-3) / 1e12, 4),
+                       "peak_TBs": LDS_PEAK_TBS, "frac": round(b / (set_ms * 1e-3) / 1e12 / LDS_PEAK_TBS, 5),
+                       "source": f"{lds_src} (SQ_INSTS_LDS x 64 lanes x 8 B, commit {lds.get('commit')})"}
+    # latency roofline of the chain that bounds the eigen stage: measured clocks
+    # per union QR slot of a unit's chase against the dependency-chain bound per slot
+    lat, lat_src = _profile_json("latency_model.json")
+    if lat:
+        p = lat["probe"]
+        slots = lat["union_slots_per_unit"]
+        bound = lat["bound_clocks_per_unit"] / slots
+        probe_clk = p["chase_us_median"] * 1e3 * p["clock_GHz"] / slots
+        live_chase_us = eig_ms * 1e3 - (p["phase_A_us"] + p["phase_B_us"] + p["phase_C_us"])
+        live_clk = live_chase_us * 1e3 * p["clock_GHz"] / slots
+        roof["latency"] = {"kernel": f"{eig_kernel}<4> QR chase", "unit": "clocks per union QR slot",
+                           "bound": round(bound, 1), "achieved_probe": round(probe_clk, 1),
+                           "frac_probe": round(bound / probe_clk, 4),
+                           "achieved_live": round(live_clk, 1) if live_chase_us > 0 else None,
+                           "frac_live": round(bound / live_clk, 4) if live_chase_us > 0 else None,
+                           "note": ("bound = make_givens chain + 2 mul-add levels per slot + the shift chain per "
+                                    "sweep, spread over the slots; achieved_probe = the stamped chase median; "
+                                    "achieved_live = this run's eigen-kernel time minus the probe's phases A-C"),
+                           "source": lat_src}
     return roof
 
 
