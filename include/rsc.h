@@ -545,6 +545,10 @@ int rsc_diag_refine_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
  * U formed, sweeps done, then k = the SVD's columns) (zeros unless built with RSC_SOLVE_STAMPS=1;
  * cap >= 98304). */
 int rsc_diag_solve_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
+/* Diagnostic wall-clock (100 MHz) stamps of mlpnp_quad_kernel's phases, [8192 workgroups][8]: entry,
+ * sample, design + normal matrix, JacobiSVD, pose recovery, Gauss-Newton (zeros unless the library is
+ * built with RSC_ML_STAMPS=1; tools/mlpnp_probe.py). cap >= 8192 * 8. */
+int rsc_diag_mlpnp_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
 /* Diagnostic: wall-clock (100 MHz) ticks of the last PoseOptimization launch, [frame < 64][8]:
  * fused passes (ticks), number of passes + (their active edges << 24), re-classification, whole kernel,
  * 4 unused. */

@@ -4,6 +4,23 @@
 //                               Cov = MlIndexedCov: the covMats branch (bearing covariances given)
 //   mlpnp_scan_kernel<PPT>      MLPnPsolver::CheckInliers, points-stationary, double pose broadcast.
 #include <hip/hip_runtime.h>
+#include <cstdint>
+// Diagnostic phase stamps of mlpnp_quad_kernel (rsc_diag_mlpnp_phase_stamps, tools/mlpnp_probe.py),
+// compiled in only with RSC_ML_STAMPS=1 (a stamp is a wall-clock read and a store per phase):
+// [workgroup][k] = 0 entry, 1 sample drawn, 2 design matrix + normal matrix, 3 JacobiSVD, 4 pose
+// recovery (sign tests), 5 Gauss-Newton done; first 8192 workgroups.
+#ifndef RSC_ML_STAMPS
+#define RSC_ML_STAMPS 0
+#endif
+namespace rsc {
+__device__ uint64_t g_ml_stamps[8192][8];
+}
+#if RSC_ML_STAMPS
+#define RSC_ML_STAMP(k)                                                                       \
+    do {                                                                                      \
+        if (blockIdx.x < 8192 && threadIdx.x == 0) ::rsc::g_ml_stamps[blockIdx.x][k] = wall_clock64(); \
+    } while (0)
+#endif
 #include "rsc_core.h"
 #include "rsc_math.h"
 #include "rsc_mlpnp.h"
@@ -30,6 +47,7 @@ __global__ __launch_bounds__(64) void mlpnp_quad_kernel(const DevML* __restrict_
     const bool active = wt.y + g < lp.H;
     const int h = active ? wt.y + g : lp.H - 1;  // idle quads repeat the last hypothesis (no writes)
     const DevML& P = probs[lp.prob];
+    RSC_ML_STAMP(0);
     int idx[NS];
     {
         uint32_t w[31];
@@ -38,6 +56,7 @@ __global__ __launch_bounds__(64) void mlpnp_quad_kernel(const DevML* __restrict_
         RSC_UNROLL for (int d = 0; d < NS; ++d) words[d] = rng_word(rng_T, w, lp.g0 + h * NS + d);
         swap_remove_sample<NS>(words, NS, P.n, idx);
     }
+    RSC_ML_STAMP(1);
     double R[3][3], t[3];
     double* region = smem + g * kRegion;
     if constexpr (Cov::on) {  // covariances supplied: the covMats branch of computePose
@@ -45,6 +64,7 @@ __global__ __launch_bounds__(64) void mlpnp_quad_kernel(const DevML* __restrict_
     } else {
         mlpnp_quad_hypothesis<NS>(P, idx, MlNoCov{}, q, region, R, t);
     }
+    RSC_ML_STAMP(5);
     if (active && q == 0) {
         const size_t rec = (size_t)(lp.out0 + h);
         double* out = poses + rec * 12;
@@ -119,6 +139,10 @@ hipError_t launch_mlpnp_solve(int ns, bool cov, int nwg, const DevML* probs, con
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+hipError_t read_ml_stamps(uint64_t* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ml_stamps), sizeof(uint64_t) * 8192 * 8, 0, hipMemcpyDeviceToHost);
 }
 
 hipError_t launch_mlpnp_scan(int ppt, int nwg, const DevML* probs, const LaunchProb* lps, const int4* wgt,

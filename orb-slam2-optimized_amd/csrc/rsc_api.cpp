@@ -2613,6 +2613,13 @@ int rsc_diag_solve_phase_stamps(rsc_context* C, uint64_t* out, int cap) {
     return RSC_OK;
 }
 
+int rsc_diag_mlpnp_phase_stamps(rsc_context* C, uint64_t* out, int cap) {
+    if (!C || !out || cap < 8192 * 8) return RSC_ERR_ARG;
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    RSC_HIP(read_ml_stamps(out));
+    return RSC_OK;
+}
+
 int rsc_diag_bow_phase_stamps(rsc_context* C, uint64_t* out, int cap) {
     if (!C || !out || cap < 0) return RSC_ERR_ARG;
     RSC_HIP(hipStreamSynchronize(C->stream));

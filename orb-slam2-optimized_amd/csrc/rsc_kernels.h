@@ -160,7 +160,8 @@ hipError_t launch_pnp_select_refine(int nsel, const DevPnP* probs, const RefineS
 // rounds (config 2), where no hypothesis qualifies, keep their launch set unchanged.
 constexpr int kFusedRefineMaxHyps = 4096;
 hipError_t read_refine_stamps(uint64_t* out);  // diagnostic, [64][24]
-hipError_t read_solve_stamps(uint64_t* out);   // diagnostic, [3][4096][8]
+hipError_t read_solve_stamps(uint64_t* out);
+hipError_t read_ml_stamps(uint64_t* out);     // diagnostic, [8192][8] (mlpnp.hip)   // diagnostic, [3][4096][8]
 hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, hipStream_t st);
 hipError_t launch_sim3_solve(int nwg, const DevSim3* probs, const LaunchProb* lps, const int2* wgt,
                              const uint32_t* T, float* poses, int32_t* samples, hipStream_t st);

@@ -8,6 +8,12 @@
 // and its V accumulate in a per-lane LDS slab (LaneMat, element-major across the wave, 288 doubles
 // per lane); during Gauss-Newton the W region holds the 2n x 6 Jacobian and the LDLT factor.
 #pragma once
+// phase stamp hook (mlpnp.hip defines it for its RSC_ML_STAMPS=1 diagnostic build)
+#ifndef RSC_ML_STAMP
+#define RSC_ML_STAMP(k) \
+    do {                \
+    } while (0)
+#endif
 #include "rsc_core.h"
 #include "rsc_math.h"
 #include "rsc_mlpnp_jac.h"
@@ -753,6 +759,7 @@ RSC_HD void mlpnp_finish_pose(const View& in, const JView& jin, const double (&r
             RSC_UNROLL for (int c = 0; c < 3; ++c) R[r][c] = Ti[0][r][c];
         }
     }
+    RSC_ML_STAMP(4);
     // Gauss-Newton (mlpnp_gn); J rows in the W region, A = J^T J (or J^T Kll J) in the V region
     double x[6];
     {

@@ -347,9 +347,11 @@ __device__ __forceinline__ void mlpnp_quad_hypothesis(const DevML& P, const int 
             }
         }
     }
+    RSC_ML_STAMP(2);
     double r1[12];
     if (planar) ml_quad_jacobi_svd<9>(Wc, Vc, q, r1);
     else ml_quad_jacobi_svd<12>(Wc, Vc, q, r1);
+    RSC_ML_STAMP(3);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

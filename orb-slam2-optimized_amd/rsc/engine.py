@@ -52,6 +52,7 @@ EXPORTED = [
     "rsc_stream_create", "rsc_stream_destroy", "rsc_stream_skip", "rsc_stream_position", "rsc_stream_peek",
     "rsc_pnp_bind_stream", "rsc_sim3_bind_stream", "rsc_mlpnp_bind_stream", "rsc_reloc_events_shared",
     "rsc_loop_events_shared", "rsc_reloc_events_gated", "rsc_loop_events_gated",
+    "rsc_diag_mlpnp_phase_stamps",
 ]
 
 # include/rsc.h RSC_GATE_*
@@ -430,6 +431,8 @@ def load_library(path: str = LIB_PATH):
     L.rsc_diag_refine_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"),
                                                C.c_int]
     L.rsc_diag_solve_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"),
+                                              C.c_int]
+    L.rsc_diag_mlpnp_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"),
                                               C.c_int]
     L.rsc_diag_poseopt_phases.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"), C.c_int]
     L.rsc_diag_kfdb_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"), C.c_int]
