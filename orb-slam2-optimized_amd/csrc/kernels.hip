@@ -290,6 +290,10 @@ constexpr int kFoldStride = 65;
 #define RSC_REFINE_EIG_LANES 4
 #endif
 constexpr int kRefineEigLanes = RSC_REFINE_EIG_LANES;
+// Refine 12x12 eigen phase in the split form (chase wave + row wave, rsc_quad.h refine_eig12_*)
+#ifndef RSC_REFINE_SPLIT
+#define RSC_REFINE_SPLIT 0
+#endif
 // Refine beta waves: the Jacobi SVD's U / V rows distributed over the (uniform) wave's lanes
 #ifndef RSC_REFINE_LANE_ROWS
 #define RSC_REFINE_LANE_ROWS 1
@@ -358,7 +362,7 @@ __device__ __forceinline__ void refine_wave_stamp(int wave, int j) {
         g_refine_stamps[blockIdx.x][12 + 4 * wave + j] = wall_clock64();
 }
 
-__device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs, const RefineJob& J) {
+__device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs, const RefineJob& J, unsigned* fault) {
     __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles];
     __shared__ __attribute__((aligned(16))) double wbuf[4][kFoldStride * 9];
     __shared__ int prefix[129];
@@ -619,12 +623,35 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
     // wave 0 as one lane group, the QR chase on lanes 0..11 with one row of Q in each lane's VGPRs),
     // then L_6x10 and rho (single lane).  The MtM lower triangle in the slab is the group's T region;
     // wbuf the E scratch.  The eigenvector columns 0..3 go back to slab columns 0..3 (SlabView::ev).
+#if RSC_REFINE_SPLIT
+    // split form (rsc_quad.h refine_eig12_*): phases B-C on wave 0, then the chase on lane 0 of wave 0
+    // and the Q rows on lanes 0..11 of wave 1, hand-off through a SplitRing in wbuf[1]
+    {
+        __shared__ int rpub, rack;
+        if (tid == 0) { rpub = 0; rack = 0; }
+        if (wave == 0) refine_eig12_bc<kRefineEigLanes>(slab, &wbuf[0][0], lane, [] { wave_lds_sync(); });
+        __syncthreads();
+        if (RSC_REFINE_STAMPS && blockIdx.x < 64 && tid == 0)
+            g_refine_stamps[blockIdx.x][8] = g_refine_stamps[blockIdx.x][9] = wall_clock64();
+        if (wave == 0) {
+            if (lane == 0) refine_eig12_chase(&wbuf[0][0], &wbuf[1][0], &rpub, &rack, fault);
+            if (RSC_REFINE_STAMPS && blockIdx.x < 64 && tid == 0) g_refine_stamps[blockIdx.x][10] = wall_clock64();
+        } else if (wave == 1 && lane < 12) {
+            double ev[4];
+            refine_eig12_rows(slab, &wbuf[1][0], &rpub, &rack, fault, lane, ev);
+            RSC_UNROLL for (int c = 0; c < 4; ++c) slab[lane * 12 + c] = ev[c];
+        }
+        __syncthreads();
+        if (RSC_REFINE_STAMPS && blockIdx.x < 64 && tid == 0) g_refine_stamps[blockIdx.x][11] = wall_clock64();
+    }
+#else
     if (wave == 0) {
         double ev[4];
         rows_eig12_ev4<kRefineEigLanes>(slab, &wbuf[0][0], lane, [] { wave_lds_sync(); }, ev);
         if (lane < 12) RSC_UNROLL for (int c = 0; c < 4; ++c) slab[lane * 12 + c] = ev[c];
     }
     __syncthreads();
+#endif
     if (wave == 0) {  // every lane of wave 0, identical values and writes
         compute_L_6x10(SlabView{S});
         auto d2 = [&](int a, int b) {
@@ -750,9 +777,9 @@ __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs
 }
 
 __global__ __launch_bounds__(256) void pnp_refine_kernel(const DevPnP* __restrict__ probs,
-                                                         const RefineJob* __restrict__ jobs) {
+                                                         const RefineJob* __restrict__ jobs, unsigned* fault) {
     const RefineJob J = jobs[blockIdx.x];
-    pnp_refine_body(probs, J);
+    pnp_refine_body(probs, J, fault);
 }
 
 // The host replay's first pause of a speculation round, evaluated on the device right after the scan
@@ -768,7 +795,7 @@ __global__ __launch_bounds__(256) void pnp_select_refine_kernel(const DevPnP* __
                                                                 const int32_t* __restrict__ counts,
                                                                 uint64_t* __restrict__ masks, int mask_words,
                                                                 const float* __restrict__ poses,
-                                                                RefineSelOut* __restrict__ out) {
+                                                                RefineSelOut* __restrict__ out, unsigned* fault) {
     __shared__ int k_sh;
     const RefineSel S = sels[blockIdx.x];
     const int tid = threadIdx.x;
@@ -809,7 +836,7 @@ __global__ __launch_bounds__(256) void pnp_select_refine_kernel(const DevPnP* __
         o.adopt = adopt ? 1 : 0;
         o.rows_after = J.rows_after;
     }
-    pnp_refine_body(probs, J);
+    pnp_refine_body(probs, J, fault);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1192,16 +1219,18 @@ hipError_t read_refine_stamps(uint64_t* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_refine_stamps), sizeof(uint64_t) * 64 * 24, 0, hipMemcpyDeviceToHost);
 }
 
-hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, hipStream_t st) {
-    pnp_refine_kernel<<<njobs, 256, 0, st>>>(probs, jobs);
+hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, unsigned* fault, hipStream_t st) {
+    if (!fault) return hipErrorInvalidValue;
+    pnp_refine_kernel<<<njobs, 256, 0, st>>>(probs, jobs, fault);
     return hipGetLastError();
 }
 
 hipError_t launch_pnp_select_refine(int nsel, const DevPnP* probs, const RefineSel* sels, const int32_t* counts,
                                     uint64_t* masks, int mask_words, const float* poses, RefineSelOut* out,
-                                    hipStream_t st) {
+                                    unsigned* fault, hipStream_t st) {
     if (nsel <= 0) return hipSuccess;
-    pnp_select_refine_kernel<<<nsel, 256, 0, st>>>(probs, sels, counts, masks, mask_words, poses, out);
+    if (!fault) return hipErrorInvalidValue;
+    pnp_select_refine_kernel<<<nsel, 256, 0, st>>>(probs, sels, counts, masks, mask_words, poses, out, fault);
     return hipGetLastError();
 }
 

@@ -32,6 +32,12 @@ namespace {
 #define RSC_POSE_PHASES 0
 #endif
 constexpr bool kPosePhases = RSC_POSE_PHASES;
+// Timing diagnostics only (wrong results): 1 = the edge waves store placeholder terms instead of
+// evaluating the edges (the pass is then the folds + barriers), 2 = wave 0 skips the folds (the pass
+// is then the edge evaluation + barriers).  tools/Makefile povariant.
+#ifndef RSC_PO_DIAG
+#define RSC_PO_DIAG 0
+#endif
 
 constexpr int kPoseThreads = 256;                 // one wave per SIMD of a CU
 constexpr int kPoseFoldLanes = 64;                // wave 0 folds
@@ -173,14 +179,19 @@ __device__ void po_pass(const DevPoseProb& P, const PoseLds& S, int m, const PoS
                 if (pos + kPoseSlab < m) nx = po_load(P, S.list[pos + kPoseSlab]);
                 const bool st = in.ur >= 0.0f;
                 const double X[3] = {(double)in.xw.x, (double)in.xw.y, (double)in.xw.z};
-                double e0, e1, e2;
-                po_error(est, K, X, (double)in.uv.x, (double)in.uv.y, st ? (double)in.ur : 0.0, st, e0, e1, e2);
-                po_st(P.err, in.e, e0, e1);
-                if (st) po_g(P.err_r)[in.e] = e2;
-                const double delta = st ? hk.ds : hk.dm, dsqr = st ? hk.ds2 : hk.dm2;
-                double t[kPoseTerms];
-                po_quad_terms(est, K, X, (double)in.xw.w, e0, e1, e2, st, robust, delta, dsqr, t);
-                const double tc = po_chi_term(robust, st, (double)in.xw.w, e0, e1, e2, delta, dsqr);
+                double t[kPoseTerms], tc;
+                if constexpr (RSC_PO_DIAG == 1) {
+                    RSC_UNROLL for (int q = 0; q < kPoseTerms; ++q) t[q] = X[q % 3] * 1e-30;
+                    tc = X[0] * 1e-30;
+                } else {
+                    double e0, e1, e2;
+                    po_error(est, K, X, (double)in.uv.x, (double)in.uv.y, st ? (double)in.ur : 0.0, st, e0, e1, e2);
+                    po_st(P.err, in.e, e0, e1);
+                    if (st) po_g(P.err_r)[in.e] = e2;
+                    const double delta = st ? hk.ds : hk.dm, dsqr = st ? hk.ds2 : hk.dm2;
+                    po_quad_terms(est, K, X, (double)in.xw.w, e0, e1, e2, st, robust, delta, dsqr, t);
+                    tc = po_chi_term(robust, st, (double)in.xw.w, e0, e1, e2, delta, dsqr);
+                }
                 double* buf = S.terms + (k & 1) * kPoseBuf + j;
                 RSC_UNROLL for (int q = 0; q < 21; ++q) buf[q * kPoseCol] = t[q];
                 RSC_UNROLL for (int q = 21; q < kPoseTerms; ++q) buf[q * kPoseCol] = -t[q];
@@ -192,7 +203,7 @@ __device__ void po_pass(const DevPoseProb& P, const PoseLds& S, int m, const PoS
                 RSC_UNROLL for (int q = 0; q < kPoseCols; ++q) buf[q * kPoseCol] = 0.0;
             }
         } else if (k > 0 && tid < kPoseCols) {
-            acc = fold_fixed<kPoseSlab>(acc, S.terms + ((k - 1) & 1) * kPoseBuf + tid * kPoseCol);
+            if constexpr (RSC_PO_DIAG != 2) acc = fold_fixed<kPoseSlab>(acc, S.terms + ((k - 1) & 1) * kPoseBuf + tid * kPoseCol);
         }
         __syncthreads();
     }

@@ -612,7 +612,7 @@ struct HipPnPBackend : PnPBackend {
             timing_begin(C, 3);
             RSC_HIP(launch_pnp_select_refine(count, dprobs, reinterpret_cast<const RefineSel*>(base + o_sel),
                                              cnt_dev ? cnt_dev : cnt_dst, C->d_masks.p, mw, C->d_poses.p,
-                                             C->d_selout.p, C->stream));
+                                             C->d_selout.p, C->h_flag + kFaultWord, C->stream));
             timing_begin(C, 4);
             RSC_HIP(hipMemcpyAsync(C->h_selout.p, C->d_selout.p, sizeof(RefineSelOut) * count, hipMemcpyDeviceToHost,
                                    C->stream));
@@ -732,11 +732,13 @@ struct HipPnPBackend : PnPBackend {
         if (int e = upload_blob(C, b)) return e;
         timing_begin(C, 3);
         RSC_HIP(launch_pnp_refine(count, reinterpret_cast<const DevPnP*>(C->d_desc.p + o_probs),
-                                  reinterpret_cast<const RefineJob*>(C->d_desc.p + o_jobs), C->stream));
+                                  reinterpret_cast<const RefineJob*>(C->d_desc.p + o_jobs), C->h_flag + kFaultWord,
+                                  C->stream));
         timing_begin(C, 4);
         if (int e = C->h_small.ensure((size_t)count * 25)) return e;
         RSC_HIP(hipMemcpyAsync(C->h_small.p, C->d_refine.p, (size_t)count * 100, hipMemcpyDeviceToHost, C->stream));
         RSC_HIP(hipStreamSynchronize(C->stream));
+        if (int e = take_fault(C)) return e;
         if (C->timing) {
             float r = 0;
             (void)hipEventElapsedTime(&r, C->ev[3], C->ev[4]);

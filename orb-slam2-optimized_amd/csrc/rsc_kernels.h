@@ -152,17 +152,18 @@ hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, 
 hipError_t launch_pnp_scan(int ppt, int nwg, const DevPnP* probs, const LaunchProb* lps, const int4* wgt,
                            const float* poses, int32_t* counts, int32_t* counts_dev, uint64_t* masks, int mask_words,
                            int32_t* qual, hipStream_t st);
+// fault: the context's fault word (the Refine's split-form eigen hand-off, RSC_REFINE_SPLIT)
 hipError_t launch_pnp_select_refine(int nsel, const DevPnP* probs, const RefineSel* sels, const int32_t* counts,
                                     uint64_t* masks, int mask_words, const float* poses, RefineSelOut* out,
-                                    hipStream_t st);
+                                    unsigned* fault, hipStream_t st);
 // Rounds up to this many hypotheses run the replay's first Refine on the device right after the
 // scan (pnp_select_refine_kernel): latency-bound rounds lose a host round trip; large exhaustive
 // rounds (config 2), where no hypothesis qualifies, keep their launch set unchanged.
 constexpr int kFusedRefineMaxHyps = 4096;
 hipError_t read_refine_stamps(uint64_t* out);  // diagnostic, [64][24]
-hipError_t read_solve_stamps(uint64_t* out);
-hipError_t read_ml_stamps(uint64_t* out);     // diagnostic, [8192][8] (mlpnp.hip)   // diagnostic, [3][4096][8]
-hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, hipStream_t st);
+hipError_t read_solve_stamps(uint64_t* out);  // diagnostic, [3][4096][8]
+hipError_t read_ml_stamps(uint64_t* out);     // diagnostic, [8192][8] (mlpnp.hip)
+hipError_t launch_pnp_refine(int njobs, const DevPnP* probs, const RefineJob* jobs, unsigned* fault, hipStream_t st);
 hipError_t launch_sim3_solve(int nwg, const DevSim3* probs, const LaunchProb* lps, const int2* wgt,
                              const uint32_t* T, float* poses, int32_t* samples, hipStream_t st);
 // counts: where the host reads them (pinned memory or HBM); counts_dev (nullable): an HBM copy for

@@ -710,6 +710,91 @@ struct SplitRing {
     }
 };
 
+// ---- The Refine's 12x12 eigenvectors in the split form (one problem, two waves) ----
+// Phases B-C as rows_eig12_ev4 on lanes 0..L-1 of the chase wave (Q row-major into T, (diag, sub)
+// into E[64..87]); after a workgroup barrier, lane 0 of the chase wave runs the implicit-QR chase on
+// (diag, sub) alone and publishes every step's rotations through the SplitRing in `ring` (two
+// parities, then the sorted column indices at kRingPerm), while lanes 0..11 of the row wave hold the
+// rows of Q in VGPRs, apply each published step in slot order (RegRowQ's operations, so the
+// eigenvectors are bit-identical) and acknowledge it.  The chase wave issues the scalar chain alone.
+template <int L, class Sync>
+__device__ __forceinline__ void refine_eig12_bc(double* T, double* E, int lane, Sync sync) {
+    constexpr int RJ = 12 / L;
+    constexpr int kDiag = 64, kSub = 76;
+    if (lane < L) {
+        double diag[12], sub[11], hC[11];
+        {
+            double A[RJ][12];
+            RSC_UNROLL for (int j = 0; j < RJ; ++j) {
+                const int R = L * j + lane;
+                RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = T[(R >= c) ? R * 12 + c : c * 12 + R];
+            }
+            const double scale = group_scale<L>(A, lane);
+            RSC_UNROLL for (int j = 0; j < RJ; ++j)
+                RSC_UNROLL for (int c = 0; c < 12; ++c) A[j][c] = A[j][c] / scale;
+            sync();
+            group_tridiag<L>(A, lane, E, diag, sub, hC);
+        }
+        sync();
+        double Qc[RJ][12];
+        group_accumulate<L>(Qc, lane, E, hC);
+        RSC_UNROLL for (int j = 0; j < RJ; ++j)
+            RSC_UNROLL for (int r = 0; r < 12; ++r) T[r * 12 + L * j + lane] = Qc[j][r];
+        if (lane == 0) {
+            RSC_UNROLL for (int i = 0; i < 12; ++i) E[kDiag + i] = diag[i];
+            RSC_UNROLL for (int i = 0; i < 11; ++i) E[kSub + i] = sub[i];
+        }
+    }
+}
+
+// Chase wave, lane 0 (after refine_eig12_bc and a workgroup barrier; pub / ack zeroed before it).
+__device__ __forceinline__ void refine_eig12_chase(const double* E, double* ring, int* pub, int* ack, unsigned* fault) {
+    constexpr int kDiag = 64, kSub = 76;
+    *reinterpret_cast<uint64_t*>(ring + 22) = 0;
+    *reinterpret_cast<uint64_t*>(ring + kRingPar + 22) = 0;
+    double diag[12], sub[11];
+    RSC_UNROLL for (int i = 0; i < 12; ++i) diag[i] = E[kDiag + i];
+    RSC_UNROLL for (int i = 0; i < 11; ++i) sub[i] = E[kSub + i];
+    int perm[12];
+    SplitRing rg{ring, pub, ack, fault};
+    tridiag_qr<double, 12>(diag, sub, rg, perm);
+    int32_t* pm = reinterpret_cast<int32_t*>(ring + kRingPerm);
+    RSC_UNROLL for (int c = 0; c < 4; ++c) pm[c] = perm[c];
+    const int steps = __hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(pub, steps | kSplitDone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Row wave, lanes 0..11: row `lane` of Q from T, the published steps applied in order; returns the
+// row's entries of the four sorted eigenvector columns.
+__device__ __forceinline__ void refine_eig12_rows(const double* T, const double* ring, int* pub, int* ack,
+                                                  unsigned* fault, int lane, double (&ev)[4]) {
+    double row[12];
+    RSC_UNROLL for (int c = 0; c < 12; ++c) row[c] = T[lane * 12 + c];
+    for (int s = 1;; ++s) {
+        const int v = split_wait(pub, fault, [s](int x) { return (x & (kSplitDone - 1)) >= s || (x & kSplitDone); });
+        if ((v & (kSplitDone - 1)) < s) break;
+        const double* r = ring + kRingPar * (s & 1);
+        const uint64_t word = *reinterpret_cast<const uint64_t*>(r + 22);
+        const uint32_t bits = ((uint32_t)word == (uint32_t)s) ? (uint32_t)(word >> 32) : 0u;
+        RSC_UNROLL for (int k = 0; k < 11; ++k) {
+            if ((bits >> k) & 1u) {
+                const double c = r[2 * k], sn = r[2 * k + 1];
+                const double x = row[k], y = row[k + 1];
+                row[k] = c * x - sn * y;
+                row[k + 1] = sn * x + c * y;
+            }
+        }
+        __hip_atomic_store(ack, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    const int32_t* pm = reinterpret_cast<const int32_t*>(ring + kRingPerm);
+    RSC_UNROLL for (int c = 0; c < 4; ++c) {
+        const int pc = pm[c];
+        double x = row[0];
+        RSC_UNROLL for (int p = 1; p < 12; ++p) x = (pc == p) ? row[p] : x;
+        ev[c] = x;
+    }
+}
+
 template <int NS>
 __device__ __forceinline__ void pnp_eig_split_body(const DevPnP* __restrict__ probs, const LaunchProb* __restrict__ lps,
                                                    const int2* __restrict__ wg_table, int nwg_table,

@@ -115,4 +115,32 @@ if [ -n "$LIBAB" ]; then
     done
   done
 fi
+if [ -n "$ML" ]; then
+  # config-4 MLPnP kernel: phase stamps (stamped build), kernel trace, two SQ
+  # passes and the HBM traffic passes of the bench's 128 x 4096 launch (tools/mlpnp_probe.py)
+  cd $GRAFT_REPO_ROOT
+  RSC_LIBRSC=tools/bin/librsc_mlstamps.so timeout -k 10 200 python tools/mlpnp_probe.py 128 stamps > $OUT/mlpnp_probe.txt 2>&1
+  cd /tmp
+  P="python3 $GRAFT_REPO_ROOT/tools/mlpnp_probe.py 128 run 4"
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/ml_prof -o ml --output-format csv -- $P > $OUT/ml_prof.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY -d $OUT/ml_sqA -o a --output-format csv -- $P > $OUT/ml_sqA.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_VALU_FMA_F64 SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_INSTS_SMEM -d $OUT/ml_sqB -o b --output-format csv -- $P > $OUT/ml_sqB.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/ml_fetch -o f --output-format csv -- $P > $OUT/ml_fetch.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/ml_write -o w --output-format csv -- $P > $OUT/ml_write.log 2>&1
+fi
+if [ -n "$VARTEST" ]; then
+  # the Refine / event parity tests against an A/B library (tools/bin/librsc_<name>.so)
+  cd $GRAFT_REPO_ROOT
+  for v in $VARTEST; do
+    RSC_LIBRSC=tools/bin/librsc_$v.so timeout -k 10 400 python -u -m pytest tests/test_gpu_pnp.py tests/test_gpu_events.py tests/test_gpu_degenerate.py tests/test_gpu_gated.py "tests/test_gpu_configs.py::test_config2_parity_batch_with_refine" "tests/test_gpu_configs.py::test_config5_full_event_stream" -m gpu -q --timeout 180 --timeout-method thread > $OUT/vartest_$v.txt 2>&1 || echo "rc=$?" >> $OUT/vartest_$v.txt
+  done
+fi
+if [ -n "$POAB" ]; then
+  # PoseOptimization pass timing per library (tools/poseopt_probe.py; RSC_POSE_PHASES builds)
+  cd $GRAFT_REPO_ROOT
+  for v in $POAB; do
+    echo "== $v" >> $OUT/poseopt_probe.txt
+    RSC_LIBRSC=tools/bin/librsc_$v.so timeout -k 10 200 python tools/poseopt_probe.py >> $OUT/poseopt_probe.txt 2>&1
+  done
+fi
 echo done > $OUT/done
