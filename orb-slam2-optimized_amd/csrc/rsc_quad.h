@@ -587,6 +587,21 @@ __device__ __forceinline__ void pnp_eig_rows_body(const DevPnP* __restrict__ pro
     double* out = stage + rec * kStageDoubles;
     double* T = smem + slot * kRowsRegion;
     double* E = T + kQuadT;
+#if RSC_SOLVE_STAMPS
+    // per wave (its 5 hypotheses run independently of the other waves): [0][4 * block + wave][k],
+    // k = 0 entry, 1-3 phase A done, 4 eigenvectors stored (tools/solve_probe.py event)
+    const int stamp_row = 4 * (int)blockIdx.x + wave;
+#define RSC_ROWS_STAMP(k0, k1)                                                   \
+    do {                                                                         \
+        if (lane == 0 && stamp_row < 4096) {                                     \
+            const uint64_t t_ = wall_clock64();                                  \
+            for (int k_ = (k0); k_ <= (k1); ++k_) g_solve_stamps[0][stamp_row][k_] = t_; \
+        }                                                                        \
+    } while (0)
+#else
+#define RSC_ROWS_STAMP(k0, k1) do {} while (0)
+#endif
+    RSC_ROWS_STAMP(0, 0);
 
     // ---- A: sample, control points, alphas, MtM (every lane of the group, identical values) ----
     {
@@ -621,10 +636,13 @@ __device__ __forceinline__ void pnp_eig_rows_body(const DevPnP* __restrict__ pro
         }
     }
     sync();
+    RSC_ROWS_STAMP(1, 3);
     // ---- B-D: 12x12 eigenvectors, row r of the four smallest eigenvalues' columns in lane r ----
     double ev[4];
     rows_eig12_ev4<L>(T, E, r, sync, ev);
     if (active) RSC_UNROLL for (int c = 0; c < 4; ++c) out[kStEv + r * 4 + c] = ev[c];
+    RSC_ROWS_STAMP(4, 4);
+#undef RSC_ROWS_STAMP
 }
 
 // ---- The eigen stage with the QR chase and the Q rotations on different waves (split form) ----
@@ -649,6 +667,15 @@ __device__ __forceinline__ void pnp_eig_rows_body(const DevPnP* __restrict__ pro
 // independently (LDS flags, not workgroup barriers, between a chase wave and its row wave).  A step
 // is valid for a hypothesis when its step number matches (a converged hypothesis publishes nothing
 // and keeps an older number in its ring slot); the chase wave's last `pub` carries kSplitDone.
+// Traffic diagnostics of the split eigen stage (wrong results; tools/Makefile variants, the PMC
+// FETCH_SIZE / WRITE_SIZE attribution of DESIGN.md section 9): no stage-record stores, samples from a
+// hash instead of the rand() jump table.
+#ifndef RSC_DIAG_NO_STAGE
+#define RSC_DIAG_NO_STAGE 0
+#endif
+#ifndef RSC_DIAG_NO_RNG
+#define RSC_DIAG_NO_RNG 0
+#endif
 constexpr int kSplitUnits = 4;     // chase / row wave pairs per workgroup (one per SIMD)
 constexpr int kSplitRowLanes = 3;  // row-wave lanes per hypothesis (4 rows of Q each)
 constexpr int kRingPar = 24;       // doubles per parity in E: (c, s) of slots 0..10, then the step word
@@ -836,7 +863,7 @@ __device__ __forceinline__ void pnp_eig_split_body(const DevPnP* __restrict__ pr
         uint32_t w[31];
         RSC_UNROLL for (int j = 0; j < 31; ++j) w[j] = lp.window[j];
         uint32_t words[NS];
-        RSC_UNROLL for (int d = 0; d < NS; ++d) words[d] = rng_word(rng_T, w, lp.g0 + h * NS + d);
+        RSC_UNROLL for (int d = 0; d < NS; ++d) words[d] = RSC_DIAG_NO_RNG ? (uint32_t)(2654435761u * (uint32_t)(h * NS + d + 1)) : rng_word(rng_T, w, lp.g0 + h * NS + d);
         swap_remove_sample<NS>(words, NS, P.n, idx);
         HypStore<NS> st;
         RSC_UNROLL for (int i = 0; i < NS; ++i) {
@@ -853,7 +880,7 @@ __device__ __forceinline__ void pnp_eig_split_body(const DevPnP* __restrict__ pr
         control_points_and_alphas(st, cws);
         if (q == 0) {
             build_MtM(st, K, LaneMat{T, 1});
-            if (active) {
+            if (active && !RSC_DIAG_NO_STAGE) {
                 RSC_UNROLL for (int i = 0; i < NS; ++i)
                     RSC_UNROLL for (int j = 0; j < 4; ++j) out[kStAl + i * 4 + j] = st.al(i, j);
                 RSC_UNROLL for (int i = 0; i < 4; ++i)
@@ -939,7 +966,7 @@ __device__ __forceinline__ void pnp_eig_split_body(const DevPnP* __restrict__ pr
             }
             __hip_atomic_store(ack + unit, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        if (active) {
+        if (active && !RSC_DIAG_NO_STAGE) {
             const int32_t* pm = reinterpret_cast<const int32_t*>(E + kRingPerm);
             int perm4[4];
             RSC_UNROLL for (int c = 0; c < 4; ++c) perm4[c] = pm[c];

@@ -143,4 +143,18 @@ if [ -n "$POAB" ]; then
     RSC_LIBRSC=tools/bin/librsc_$v.so timeout -k 10 200 python tools/poseopt_probe.py >> $OUT/poseopt_probe.txt 2>&1
   done
 fi
+if [ -n "$TRAFAB" ]; then
+  # HBM traffic attribution of the headline launch set: FETCH_SIZE / WRITE_SIZE passes per library
+  # (product = "product", else tools/bin/librsc_<name>.so)
+  cd /tmp
+  for v in $TRAFAB; do
+    if [ $v = product ]; then L=$GRAFT_REPO_ROOT/orb-slam2-optimized_amd/lib/librsc.so; else L=$GRAFT_REPO_ROOT/tools/bin/librsc_$v.so; fi
+    RSC_LIBRSC=$L timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $OUT/traf_fetch_$v -o f --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/traf_fetch_$v.log 2>&1
+    RSC_LIBRSC=$L timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $OUT/traf_write_$v -o w --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/traf_write_$v.log 2>&1
+  done
+fi
+if [ -n "$SOLVEPROBE" ]; then
+  cd $GRAFT_REPO_ROOT
+  RSC_LIBRSC=tools/bin/librsc_solvestamps.so timeout -k 10 120 python tools/solve_probe.py event > $OUT/solve_probe_event.txt 2>&1
+fi
 echo done > $OUT/done

@@ -14,13 +14,29 @@ sys.path[:0] = [os.path.join(ROOT, "orb-slam2-optimized_amd"), ROOT]
 import numpy as np  # noqa: E402
 from rsc import engine, workloads as wl  # noqa: E402
 
-scenes = wl.config2_scenes()
 ctx = engine.Context(0)
-batch = engine.SolverBatch([engine.PnPSolver(ctx, sc, 1) for sc in scenes])
-for s in range(3):
-    batch.reset(wl.config2_seeds(s))
-    batch.set_ransac_parameters(*wl.RELOC)
-    batch.iterate_raw(300)
+if len(sys.argv) > 1 and sys.argv[1] == "event":
+    # the bench's single relocalization event (bench.py latency_event: C = 15, N ~ U[300, 900]): its
+    # first round is the launch whose stamps remain (rows-form eigen stage)
+    from rsc import events as rev
+    rng = np.random.default_rng(4242)
+    C = 15
+    sizes = [int(x) for x in rng.integers(300, 901, size=C)]
+    ratios = [float(x) for x in rng.choice([0.05, 0.2, 0.6, 0.8], size=C, p=[0.5, 0.2, 0.15, 0.15])]
+    ev = rev.Event("reloc", 100000, sizes, ratios, [7 + c for c in range(C)])
+    eb = engine.EventBatch([[engine.PnPSolver(ctx, x, s) for x, s in zip(rev.event_inputs(ev), ev.seeds)]])
+    for _ in range(3):
+        eb.batch.reset(np.array(ev.seeds, np.uint32))
+        eb.batch.set_ransac_parameters(*rev.RELOC_PARAMS)
+        eb.batch.iterate_raw(5)  # round 0 of the event: every candidate's first iterate(5)
+    print("single relocalization event, round 0 (rows-form eigen stage)")
+else:
+    scenes = wl.config2_scenes()
+    batch = engine.SolverBatch([engine.PnPSolver(ctx, sc, 1) for sc in scenes])
+    for s in range(3):
+        batch.reset(wl.config2_seeds(s))
+        batch.set_ransac_parameters(*wl.RELOC)
+        batch.iterate_raw(300)
 st = np.zeros(3 * 4096 * 8, np.uint64)
 engine._check(engine.load_library().rsc_diag_solve_phase_stamps(ctx.h, st, st.size), "solve stamps")
 st = st.reshape(3, 4096, 8).astype(np.int64)
