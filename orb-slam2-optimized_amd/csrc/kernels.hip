@@ -107,9 +107,9 @@ __global__ __launch_bounds__(64) void pnp_betas_kernel(const DevPnP* __restrict_
                                                        const int32_t* __restrict__ samples,
                                                        float* __restrict__ poses, double* __restrict__ berr,
                                                        float* __restrict__ bpose, unsigned* __restrict__ bctr,
-                                                       size_t hcap) {
+                                                       size_t hcap, int hb) {
     __shared__ __attribute__((aligned(16))) double smem[kBetasWaveSmemDoubles];
-    pnp_betas_wave_body<NS>(probs, lps, wg_table, ngroups, kBetasHyps, stage, samples, poses, berr, bpose, bctr, hcap, smem);
+    pnp_betas_wave_body<NS>(probs, lps, wg_table, ngroups, hb, stage, samples, poses, berr, bpose, bctr, hcap, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1051,8 +1051,8 @@ hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, 
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
                                   hipEvent_t eig_begin, hipEvent_t eig_end, bool eig_rows, bool eig_split,
-                                  unsigned* fault) {
-    if (ns < 4 || ns > 6) return hipErrorInvalidValue;
+                                  unsigned* fault, int betas_hb) {
+    if (ns < 4 || ns > 6 || betas_hb < 1 || betas_hb > kBetasHyps) return hipErrorInvalidValue;
     if (eig_split && !eig_rows && !fault) return hipErrorInvalidValue;
     if (eig_begin) (void)hipEventRecord(eig_begin, st);
     switch (ns) {
@@ -1068,7 +1068,7 @@ hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, 
             pnp_eig_group_kernel<N><<<nwgE, 64, 0, st>>>(probs, lps, wgtE, T, stage, samples);        \
         if (eig_end) (void)hipEventRecord(eig_end, st);                                               \
         pnp_betas_kernel<N><<<3 * nwgB, 64, 0, st>>>(probs, lps, wgtB, nwgB, stage, samples, poses,   \
-                                                     bs.err, bs.pose, bs.ctr, bs.hcap);               \
+                                                     bs.err, bs.pose, bs.ctr, bs.hcap, betas_hb);     \
         break;
         RSC_CASE(4) RSC_CASE(5) RSC_CASE(6)
 #undef RSC_CASE

@@ -223,6 +223,9 @@ struct rsc_context {
     // one relocalization event: 125 -> 99 us, profiles/r05/bench_latency_forms_ab_r5b.json); env
     // RSC_EIG_ROWS=W or rsc_context_set_eig_rows overrides (0: lane pairs always)
     int eig_rows_max_wgs = kEigRowsDefaultWgs;
+    // hypotheses per betas wave for launches small enough for the rows-form eigen stage (a wave runs
+    // the union of its hypotheses' data-dependent chains; env RSC_BETAS_HB)
+    int betas_small_hb = kBetasHyps;
     // eigen stages beyond the rows form's range: split form (chase and Q rotations on two waves,
     // pnp_eig_split_kernel; config-2 eigen stage 119 -> 114 us, profiles/r05/split_ab_r5q.jsonl) or
     // the pair form (env RSC_EIG_SPLIT=0)
@@ -501,6 +504,7 @@ struct HipPnPBackend : PnPBackend {
         std::vector<int2>* quad_wgs = quad_wgs_tl;
         std::vector<int4>& scan_wgs = scan_wgs_tl;
         const int HC = scan_chunk(total);  // hypotheses per scan workgroup
+        const int hb = (total <= kEigHyps * C->eig_rows_max_wgs) ? C->betas_small_hb : kBetasHyps;
 
         // The tables depend only on the round's shape (count, sample size and H per problem, HC):
         // a round with the shape of the previous one on this thread reuses them (building and
@@ -512,6 +516,7 @@ struct HipPnPBackend : PnPBackend {
         key.clear();
         key.push_back(count);
         key.push_back(HC);
+        key.push_back(hb);
         for (int i = 0; i < count; ++i) {
             key.push_back(S[i]->mRansacMinSet);
             key.push_back(H[i]);
@@ -521,7 +526,7 @@ struct HipPnPBackend : PnPBackend {
             scan_wgs.clear();
             for (int i = 0; i < count; ++i) {
                 const int g = S[i]->mRansacMinSet - 4;
-                for (int h0 = 0; h0 < H[i]; h0 += kBetasHyps) solve_wgs[g].push_back(make_int2(i, h0));
+                for (int h0 = 0; h0 < H[i]; h0 += hb) solve_wgs[g].push_back(make_int2(i, h0));
                 for (int h0 = 0; h0 < H[i]; h0 += kEigHyps) quad_wgs[g].push_back(make_int2(i, h0));
                 for (int h0 = 0; h0 < H[i]; h0 += HC)
                     scan_wgs.push_back(make_int4(i, h0, std::min(HC, H[i] - h0), 0));
@@ -601,7 +606,7 @@ struct HipPnPBackend : PnPBackend {
                                           C->d_table.p, C->d_stage.p, C->d_poses.p, C->d_samples.p, bs, C->stream,
                                           eb, C->timing ? C->ev[7 + 2 * g] : nullptr,
                                           (int)quad_wgs[g].size() <= C->eig_rows_max_wgs, C->eig_split,
-                                          C->h_flag + kFaultWord));
+                                          C->h_flag + kFaultWord, hb));
             first_group = false;
         }
         timing_begin(C, 1);
@@ -1269,6 +1274,7 @@ int rsc_context_create(int device, rsc_context** out) {
     if (const char* m = std::getenv("RSC_DMA_UPLOAD")) C->dma_upload = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_EIG_ROWS")) C->eig_rows_max_wgs = std::max(0, std::atoi(m));
     if (const char* m = std::getenv("RSC_EIG_SPLIT")) C->eig_split = std::strcmp(m, "0") != 0;
+    if (const char* m = std::getenv("RSC_BETAS_HB")) C->betas_small_hb = std::min(kBetasHyps, std::max(1, std::atoi(m)));
     if (const char* m = std::getenv("RSC_SPIN_WAIT")) C->spin_wait = std::strcmp(m, "0") != 0;
     {
         void* f = nullptr;

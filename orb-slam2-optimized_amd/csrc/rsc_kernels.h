@@ -143,7 +143,8 @@ hipError_t launch_pnp_solve_split(int ns, int nwgE, const int2* wgtE, int nwgB, 
                                   const DevPnP* probs, const LaunchProb* lps, const uint32_t* T, double* stage,
                                   float* poses, int32_t* samples, const BetasScratch& bs, hipStream_t st,
                                   hipEvent_t eig_begin = nullptr, hipEvent_t eig_end = nullptr, bool eig_rows = false,
-                                  bool eig_split = false, unsigned* fault = nullptr);
+                                  bool eig_split = false, unsigned* fault = nullptr, int betas_hb = kBetasHyps);
+// betas_hb: hypotheses per betas wave (<= kBetasHyps; the wg_table's groups step by it).
 // fault (required by the split form): a word in pinned host memory that the split eigen stage sets to
 // 1 when a chase / row-wave hand-off gives up (split_wait); the host turns it into RSC_ERR_INTERNAL.
 // counts: where the host reads them (pinned memory or HBM); counts_dev (nullable): an HBM copy for

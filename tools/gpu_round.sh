@@ -6,6 +6,15 @@
 # the script stops at the first failure.
 set -e
 TAG=${TAG:-run}
+# a diagnostic step that fails (a Python error) is recorded and the script goes on; a time limit, an
+# abort or a crash ends it (nothing more runs on the GPU after those)
+step() {
+  local rc=0
+  "$@" || rc=$?
+  if [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "fatal rc=$rc: $*" >> $OUT/fatal.txt; exit $rc; fi
+  [ $rc -eq 0 ] || echo "step rc=$rc: $*" >> $OUT/step_errors.txt
+  return 0
+}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
@@ -101,7 +110,7 @@ if [ -n "$REFAB" ]; then
   for rep in 1 2; do
     for v in $REFAB; do
       echo "== $v rep $rep" >> $OUT/refine_probe_$v.txt
-      RSC_LIBRSC=tools/bin/librsc_$v.so timeout -k 10 120 python tools/refine_probe.py event >> $OUT/refine_probe_$v.txt 2>&1
+      step env RSC_LIBRSC=tools/bin/librsc_$v.so timeout -k 10 120 python tools/refine_probe.py event >> $OUT/refine_probe_$v.txt 2>&1
     done
   done
 fi
@@ -111,7 +120,7 @@ if [ -n "$LIBAB" ]; then
   for rep in 1 2; do
     for v in $LIBAB; do
       if [ $v = product ]; then L=orb-slam2-optimized_amd/lib/librsc.so; else L=tools/bin/librsc_$v.so; fi
-      RSC_LIBRSC=$L timeout -k 10 300 python bench.py --no-cpu --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --no-mlpnp --no-events --no-sim3 >> $OUT/libab_$v.jsonl 2>> $OUT/libab.err
+      step env RSC_LIBRSC=$L timeout -k 10 300 python bench.py --no-cpu --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --no-mlpnp --no-events --no-sim3 >> $OUT/libab_$v.jsonl 2>> $OUT/libab.err
     done
   done
 fi
@@ -119,20 +128,20 @@ if [ -n "$ML" ]; then
   # config-4 MLPnP kernel: phase stamps (stamped build), kernel trace, two SQ
   # passes and the HBM traffic passes of the bench's 128 x 4096 launch (tools/mlpnp_probe.py)
   cd $GRAFT_REPO_ROOT
-  RSC_LIBRSC=tools/bin/librsc_mlstamps.so timeout -k 10 200 python tools/mlpnp_probe.py 128 stamps > $OUT/mlpnp_probe.txt 2>&1
+  step env RSC_LIBRSC=tools/bin/librsc_mlstamps.so timeout -k 10 200 python tools/mlpnp_probe.py 128 stamps > $OUT/mlpnp_probe.txt 2>&1
   cd /tmp
   P="python3 $GRAFT_REPO_ROOT/tools/mlpnp_probe.py 128 run 4"
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/ml_prof -o ml --output-format csv -- $P > $OUT/ml_prof.log 2>&1
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY -d $OUT/ml_sqA -o a --output-format csv -- $P > $OUT/ml_sqA.log 2>&1
-  timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_VALU_FMA_F64 SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_INSTS_SMEM -d $OUT/ml_sqB -o b --output-format csv -- $P > $OUT/ml_sqB.log 2>&1
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/ml_fetch -o f --output-format csv -- $P > $OUT/ml_fetch.log 2>&1
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/ml_write -o w --output-format csv -- $P > $OUT/ml_write.log 2>&1
+  step env timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/ml_prof -o ml --output-format csv -- $P > $OUT/ml_prof.log 2>&1
+  step env timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY -d $OUT/ml_sqA -o a --output-format csv -- $P > $OUT/ml_sqA.log 2>&1
+  step env timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_VALU_FMA_F64 SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_INSTS_SMEM -d $OUT/ml_sqB -o b --output-format csv -- $P > $OUT/ml_sqB.log 2>&1
+  step env timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/ml_fetch -o f --output-format csv -- $P > $OUT/ml_fetch.log 2>&1
+  step env timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/ml_write -o w --output-format csv -- $P > $OUT/ml_write.log 2>&1
 fi
 if [ -n "$VARTEST" ]; then
   # the Refine / event parity tests against an A/B library (tools/bin/librsc_<name>.so)
   cd $GRAFT_REPO_ROOT
   for v in $VARTEST; do
-    RSC_LIBRSC=tools/bin/librsc_$v.so timeout -k 10 400 python -u -m pytest tests/test_gpu_pnp.py tests/test_gpu_events.py tests/test_gpu_degenerate.py tests/test_gpu_gated.py "tests/test_gpu_configs.py::test_config2_parity_batch_with_refine" "tests/test_gpu_configs.py::test_config5_full_event_stream" -m gpu -q --timeout 180 --timeout-method thread > $OUT/vartest_$v.txt 2>&1 || echo "rc=$?" >> $OUT/vartest_$v.txt
+    step env RSC_LIBRSC=tools/bin/librsc_$v.so timeout -k 10 400 python -u -m pytest tests/test_gpu_pnp.py tests/test_gpu_events.py tests/test_gpu_degenerate.py tests/test_gpu_gated.py "tests/test_gpu_configs.py::test_config2_parity_batch_with_refine" "tests/test_gpu_configs.py::test_config5_full_event_stream" -m gpu -q --timeout 180 --timeout-method thread > $OUT/vartest_$v.txt 2>&1 || echo "rc=$?" >> $OUT/vartest_$v.txt
   done
 fi
 if [ -n "$POAB" ]; then
@@ -140,7 +149,7 @@ if [ -n "$POAB" ]; then
   cd $GRAFT_REPO_ROOT
   for v in $POAB; do
     echo "== $v" >> $OUT/poseopt_probe.txt
-    RSC_LIBRSC=tools/bin/librsc_$v.so timeout -k 10 200 python tools/poseopt_probe.py >> $OUT/poseopt_probe.txt 2>&1
+    step env RSC_LIBRSC=tools/bin/librsc_$v.so timeout -k 10 200 python tools/poseopt_probe.py >> $OUT/poseopt_probe.txt 2>&1
   done
 fi
 if [ -n "$TRAFAB" ]; then
@@ -149,12 +158,28 @@ if [ -n "$TRAFAB" ]; then
   cd /tmp
   for v in $TRAFAB; do
     if [ $v = product ]; then L=$GRAFT_REPO_ROOT/orb-slam2-optimized_amd/lib/librsc.so; else L=$GRAFT_REPO_ROOT/tools/bin/librsc_$v.so; fi
-    RSC_LIBRSC=$L timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $OUT/traf_fetch_$v -o f --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/traf_fetch_$v.log 2>&1
-    RSC_LIBRSC=$L timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $OUT/traf_write_$v -o w --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/traf_write_$v.log 2>&1
+    step env RSC_LIBRSC=$L timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $OUT/traf_fetch_$v -o f --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/traf_fetch_$v.log 2>&1
+    step env RSC_LIBRSC=$L timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $OUT/traf_write_$v -o w --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py $PMCARGS > $OUT/traf_write_$v.log 2>&1
   done
 fi
 if [ -n "$SOLVEPROBE" ]; then
   cd $GRAFT_REPO_ROOT
-  RSC_LIBRSC=tools/bin/librsc_solvestamps.so timeout -k 10 120 python tools/solve_probe.py event > $OUT/solve_probe_event.txt 2>&1
+  step env RSC_LIBRSC=tools/bin/librsc_solvestamps.so timeout -k 10 120 python tools/solve_probe.py event > $OUT/solve_probe_event.txt 2>&1
+fi
+if [ -n "$ENVAB" ]; then
+  # headline + single-event latency per environment setting (e.g. "RSC_BETAS_HB=64 RSC_BETAS_HB=16"), interleaved twice
+  cd $GRAFT_REPO_ROOT
+  for rep in 1 2; do
+    for v in $ENVAB; do
+      step env $v timeout -k 10 300 python bench.py --no-cpu --no-poseopt --no-bow --no-sim3match --no-sim3opt --no-kfdb --no-config1 --no-mlpnp --no-events --no-sim3 >> $OUT/envab_$v.jsonl 2>> $OUT/envab.err
+    done
+  done
+fi
+if [ -n "$ENVTEST" ]; then
+  # the Refine / event parity tests under an environment setting of the product library
+  cd $GRAFT_REPO_ROOT
+  for v in $ENVTEST; do
+    step env $v timeout -k 10 400 python -u -m pytest tests/test_gpu_pnp.py tests/test_gpu_events.py tests/test_gpu_degenerate.py tests/test_gpu_gated.py "tests/test_gpu_configs.py::test_config2_parity_batch_with_refine" "tests/test_gpu_configs.py::test_config5_full_event_stream" -m gpu -q --timeout 180 --timeout-method thread > $OUT/envtest_$v.txt 2>&1
+  done
 fi
 echo done > $OUT/done
