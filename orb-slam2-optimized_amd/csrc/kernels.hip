@@ -299,6 +299,10 @@ constexpr int kRefineEigLanes = RSC_REFINE_EIG_LANES;
 #define RSC_REFINE_LANE_ROWS 1
 #endif
 constexpr bool kRefineLaneRows = RSC_REFINE_LANE_ROWS != 0;
+// Refine ordered sums (control points, pc0, M, error) pipelined over double-buffered blocks
+#ifndef RSC_FOLD_PIPE
+#define RSC_FOLD_PIPE 0
+#endif
 // Refine MtM fold with the LDS reads of the next 8 rows issued ahead of the current 8 rows' adds
 #ifndef RSC_MTM_PIPELINE
 #define RSC_MTM_PIPELINE 1
@@ -317,6 +321,70 @@ __global__ __launch_bounds__(256) void pnp_eig_rows_kernel(const DevPnP* __restr
     pnp_eig_rows_body<NS, kRefineEigLanes>(probs, lps, wg_table, rng_T, stage, samples, smem, [] { wave_lds_sync(); });
 }
 
+#if RSC_FOLD_PIPE
+// Ordered sums of K columns of per-row terms over rows [0, count), by one wave: row i's operands are
+// v = load(i) (global loads only), its terms term(i, v, t[K]).  Software-pipelined over blocks of 64
+// rows with two LDS buffers: while lanes 0..K-1 add block b's terms in order, the wave evaluates block
+// b + 1's terms into the other buffer (in the same straight-line block for full blocks, so the term
+// arithmetic fills the dependent additions' latency) and block b + 2's loads are in flight; one wave
+// barrier per block.  Lanes >= K fold a copy of column K - 1 (discarded), so no exec-mask region
+// splits the block.  from_zero: s = ((0.0 + t0) + t1) + ..., else s = (t0 + t1) + ...
+// Returns column k's sum in lane k (k < K); buf holds 2 * K * kFoldStride2 doubles of this wave.
+constexpr int kFoldStride2 = 66;  // even (16-byte column starts), 132 words: K <= 16 columns on distinct banks
+template <int K, class Load, class Term>
+__device__ __forceinline__ double wave_ordered_sum(int count, double* buf, bool from_zero, Load&& load, Term&& term) {
+    constexpr int CS = kFoldStride2;
+    const int lane = threadIdx.x & 63;
+    const int colk = lane < K ? lane : K - 1;
+    double s = 0.0;
+    if (count <= 0) return s;
+    const int nb = (count + 63) / 64;
+    auto put = [&](int b, const auto& v) {
+        double t[K];
+        term(min(b * 64 + lane, count - 1), v, t);
+        double* dst = buf + (b & 1) * (K * CS) + lane;
+        RSC_UNROLL for (int k = 0; k < K; ++k) dst[k * CS] = t[k];
+    };
+    auto v = load(min(lane, count - 1));
+    put(0, v);
+    v = load(min(64 + lane, count - 1));  // clamped: a block past the end reloads the last row
+    wave_lds_sync();
+    for (int b = 0; b < nb; ++b) {
+        const double* c = buf + (b & 1) * (K * CS) + colk * CS;
+        const bool steady = (b + 1 < nb) & (b * 64 + 64 <= count) & ((b > 0) | from_zero);
+        if (steady) {
+            // block b + 1's terms and block b's 64 ordered additions in one basic block
+            const auto vn = v;
+            v = load(min((b + 2) * 64 + lane, count - 1));
+            put(b + 1, vn);
+            const double2* c2 = reinterpret_cast<const double2*>(c);
+            RSC_UNROLL for (int g = 0; g < 4; ++g) {
+                double2 x[8];
+                RSC_UNROLL for (int q = 0; q < 8; ++q) x[q] = c2[8 * g + q];
+                RSC_UNROLL for (int q = 0; q < 8; ++q) {
+                    s = s + x[q].x;
+                    s = s + x[q].y;
+                }
+            }
+        } else {
+            if (b + 1 < nb) {
+                const auto vn = v;
+                v = load(min((b + 2) * 64 + lane, count - 1));
+                put(b + 1, vn);
+            }
+            const int m = min(64, count - b * 64);
+            int r = 0;
+            if (b == 0 && !from_zero) {
+                s = c[0];
+                r = 1;
+            }
+            s = fold_col(s, c, r, m);
+        }
+        wave_lds_sync();
+    }
+    return s;
+}
+#else
 // Ordered sums of K columns of per-row terms over rows [0, count), by one wave: row i's operands are
 // v = load(i) (global loads only), its terms term(i, v, t[K]).  The next block's loads are issued
 // before the current block is folded, so their latency overlaps the fold's dependent additions.
@@ -349,6 +417,8 @@ __device__ __forceinline__ double wave_ordered_sum(int count, double* buf, bool 
     return s;
 }
 
+#endif
+
 // Operands of one EPnP row for the Refine's ordered sums (global loads; the unused ones are dead).
 struct RefRow {
     double a[4], p[3], u[2];
@@ -364,7 +434,11 @@ __device__ __forceinline__ void refine_wave_stamp(int wave, int j) {
 
 __device__ __forceinline__ void pnp_refine_body(const DevPnP* __restrict__ probs, const RefineJob& J, unsigned* fault) {
     __shared__ __attribute__((aligned(16))) double slab[kSlabDoubles];
+#if RSC_FOLD_PIPE
+    __shared__ __attribute__((aligned(16))) double wbuf[4][2 * 9 * kFoldStride2];
+#else
     __shared__ __attribute__((aligned(16))) double wbuf[4][kFoldStride * 9];
+#endif
     __shared__ int prefix[129];
     __shared__ double cen_sh[3], cws_sh[12], cci_sh[9];
     __shared__ double res_sh[3][13];  // per approximation: R[9], t[3], error
