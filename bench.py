@@ -1228,6 +1228,9 @@ def headline_roofline(args, r):
                     "peak_GBs": HBM_PEAK_GBS},
             "effective_scan_bw_frac": round(scan_bytes / (set_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if set_ms else None,
             "scan_algorithmic_bytes_per_launch": scan_bytes,
+            "effective_scan_bw_note": ("the scan's algorithmic bytes (every hypothesis re-reads its candidate's "
+                                       "N correspondences, 24 B each; served from L2 / registers, not HBM) over "
+                                       "the whole launch set's time, as a fraction of HBM peak"),
             "timing": "HIP events on the context stream, second pass of the same K steps "
                       f"({1e3 * r['seconds_instrumented'] / args.steps:.4f} ms/step with events)",
             "sources": {"S_h": f"{opc_src} (tools/opcount_report.py)",

@@ -549,9 +549,11 @@ int rsc_diag_solve_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
  * sample, design + normal matrix, JacobiSVD, pose recovery, Gauss-Newton (zeros unless the library is
  * built with RSC_ML_STAMPS=1; tools/mlpnp_probe.py). cap >= 8192 * 8. */
 int rsc_diag_mlpnp_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
-/* Diagnostic: wall-clock (100 MHz) ticks of the last PoseOptimization launch, [frame < 64][8]:
- * fused passes (ticks), number of passes + (their active edges << 24), re-classification, whole kernel,
- * 4 unused. */
+/* Diagnostic: wall-clock (100 MHz) ticks of the last PoseOptimization launch (built with
+ * RSC_POSE_PHASES=1), [frame < 64][8]: fused passes (ticks), number of passes + (their active edges
+ * << 24), re-classification, whole kernel, the LM solves, wave 1's slab phases (to the errors, to the
+ * terms) and its slab count.  cap >= 64 * 24 returns [frame][24]: columns 8..15 = the HW_ID register
+ * of waves 0..7 (SIMD in bits 5:4, CU in 11:8), 16 / 17 = wave 0's folding ticks and fold count. */
 int rsc_diag_poseopt_phases(rsc_context* ctx, uint64_t* out, int cap);
 /* Diagnostic: wall clock (100 MHz) of KeyFrameDatabase slots 0..4095 in the last count launch,
  * [slot][4] = entry, staged, counted, exit (zeros unless built with RSC_KFDB_STAMPS=1). */

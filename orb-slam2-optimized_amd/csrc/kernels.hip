@@ -300,8 +300,10 @@ constexpr int kRefineEigLanes = RSC_REFINE_EIG_LANES;
 #endif
 constexpr bool kRefineLaneRows = RSC_REFINE_LANE_ROWS != 0;
 // Refine ordered sums (control points, pc0, M, error) pipelined over double-buffered blocks
+// (profiles/r06/refine_probe_foldstamps_s6f.txt: control points 13.9 -> 12.4 us, pc0 + M/Horn + error
+// 24.9 -> 22.6 us on the approximation-3 wave; single event 0.385-0.390 -> 0.382-0.383 ms)
 #ifndef RSC_FOLD_PIPE
-#define RSC_FOLD_PIPE 0
+#define RSC_FOLD_PIPE 1
 #endif
 // Refine MtM fold with the LDS reads of the next 8 rows issued ahead of the current 8 rows' adds
 #ifndef RSC_MTM_PIPELINE

@@ -9,6 +9,11 @@
 // runs the same additions: a - t == a + (-t) in IEEE arithmetic).  Only the active (level-0) edges
 // are listed, in edge order, so the folds add exactly the reference's terms.
 //
+// The per-edge _error of a pass is not stored: re-classification needs only the last pass's errors
+// of the level-0 edges, and recomputes them at that pass's estimate (po_error is a pure function of
+// the estimate and the edge, so the values are the ones the pass computed).  Global stores in the
+// slab loop would count in vmcnt with the next slab's prefetch loads and be waited for at every slab.
+//
 // Every pass is the fused computeActiveErrors + activeRobustChi2 + buildSystem at one estimate: the
 // LM trial's chi2 pass (optimization_algorithm_levenberg.cpp:108-112) also builds the system at the
 // trial estimate, which is the next iteration's buildSystem when the trial is accepted
@@ -39,21 +44,58 @@ constexpr bool kPosePhases = RSC_POSE_PHASES;
 #define RSC_PO_DIAG 0
 #endif
 
-constexpr int kPoseThreads = 256;                 // one wave per SIMD of a CU
+// Pass form.  0 (default): wave 0 folds and RSC_PO_EDGE_WAVES waves (3: 256 threads, slabs of 192; 4: 320 threads, slabs of 256, the fourth edge wave beside the
+// fold on SIMD 0 — the older fold wave issues first) evaluate the edges into double-buffered slabs.
+// 1 (wide): 512 threads, two waves per SIMD, seven edge waves (RSC_PO_IDLE = w leaves wave w out),
+// slabs of 448 into a single buffer (two do not fit in LDS beside the active list): a slab's terms
+// wait in VGPRs for the previous slab's fold and are stored between two barriers.  Measured
+// (profiles/r06/poseopt_probe_s6l.txt): the edge evaluation is issue-bound (about 380 VALU
+// instructions per edge) and two waves per SIMD only share the issue; 192-edge slabs 13.7 us per pass
+// of 1,494 edges, 448-edge slabs 14.1, 384 with an idle wave 14.4.
+#ifndef RSC_PO_WIDE
+#define RSC_PO_WIDE 0
+#endif
+#ifndef RSC_PO_EDGE_WAVES
+#define RSC_PO_EDGE_WAVES 4
+#endif
+constexpr bool kPoseWide = RSC_PO_WIDE != 0;
+// the wide form's idle wave (0: none): waves w and w + 4 of a workgroup land on one SIMD
+// (profiles/r06/poseopt_probe_s6j.txt), so wave 4 shares the fold wave's SIMD
+#ifndef RSC_PO_IDLE
+#define RSC_PO_IDLE 0
+#endif
+static_assert(RSC_PO_IDLE >= 0 && RSC_PO_IDLE <= 7, "idle wave");
+static_assert(RSC_PO_EDGE_WAVES == 3 || RSC_PO_EDGE_WAVES == 4, "edge waves of the default form");
+constexpr int kPoseEdgeWaves = kPoseWide ? (RSC_PO_IDLE ? 6 : 7) : RSC_PO_EDGE_WAVES;
+constexpr int kPoseThreads = kPoseWide ? 512 : 64 * (1 + kPoseEdgeWaves);
 constexpr int kPoseFoldLanes = 64;                // wave 0 folds
-constexpr int kPoseSlab = kPoseThreads - kPoseFoldLanes;  // active edges per slab (waves 1..3)
+constexpr int kPoseSlab = 64 * kPoseEdgeWaves;   // active edges per slab
+constexpr int kPoseBufs = kPoseWide ? 1 : 2;
 constexpr int kPoseCol = kPoseSlab + 2;           // padded column stride (doubles): 16 B bank shift per column
 constexpr int kPoseCols = kPoseTerms + 1;         // 27 H/b columns + the chi2 column
 constexpr int kPoseBuf = kPoseCols * kPoseCol;    // one slab buffer
-constexpr size_t kPoseLds = sizeof(double) * 2 * kPoseBuf + sizeof(uint16_t) * kPoseMaxEdges + kPoseMaxEdges;
+constexpr size_t kPoseLds =
+    sizeof(double) * kPoseBufs * kPoseBuf + sizeof(uint16_t) * kPoseMaxEdges + kPoseMaxEdges;
 static_assert(kPoseCol % 2 == 0, "fold_run reads 16-byte aligned columns");
+static_assert(kPoseSlab % 16 == 0, "fold_fixed folds whole 16-term groups");
 static_assert(kPoseMaxEdges <= 65536, "active list is uint16");
+static_assert(kPoseLds <= 160 * 1024 - 1024, "LDS");
+
+// Slab position of this thread's edge (-1: the fold wave, and the idle wave of the wide form).
+__device__ __forceinline__ int po_slot(int tid) {
+    const int w = tid >> 6, lane = tid & 63;
+    if constexpr (kPoseWide && RSC_PO_IDLE != 0)
+        return (w == 0 || w == RSC_PO_IDLE) ? -1 : (w - (w > RSC_PO_IDLE ? 2 : 1)) * 64 + lane;
+    else if constexpr (kPoseWide) return w == 0 ? -1 : (w - 1) * 64 + lane;
+    else return tid - kPoseFoldLanes;
+}
 
 struct PoseLds {
-    double* terms;   // [2][kPoseCols][kPoseCol] slab buffers
+    double* terms;   // [kPoseBufs][kPoseCols][kPoseCol] slab buffers
     uint16_t* list;  // [kPoseMaxEdges] active edges of the round, in edge order
     uint8_t* lvl;    // [kPoseMaxEdges] edge level: 0 active, 1 outlier (g2o setLevel)
-    double* red;     // [32] folded sums
+    double* red;     // [32] a pass's folded sums (H lower triangle row-major, b, chi2)
+    double* cur;     // [32] the LM's current system (a copy of an adopted pass's red)
     int* scan;       // [kPoseThreads / 64] wave totals
     int* nbad;
 };
@@ -82,12 +124,17 @@ __device__ __forceinline__ double2 po_ld(const double2* p, int e) {
     const V v = po_g(reinterpret_cast<const V*>(p))[e];
     return make_double2(v.x, v.y);
 }
-__device__ __forceinline__ void po_st(double2* p, int e, double a, double b) {
-    using V = double __attribute__((ext_vector_type(2)));
-    V v;
-    v.x = a;
-    v.y = b;
-    po_g(reinterpret_cast<V*>(p))[e] = v;
+
+// An estimate in LDS (quaternion x, y, z, w, then t).
+__device__ __forceinline__ void po_put(double* d, const PoSE3& e) {
+    d[0] = e.r.x; d[1] = e.r.y; d[2] = e.r.z; d[3] = e.r.w;
+    d[4] = e.t[0]; d[5] = e.t[1]; d[6] = e.t[2];
+}
+__device__ __forceinline__ PoSE3 po_get(const double* d) {
+    PoSE3 e;
+    e.r.x = d[0]; e.r.y = d[1]; e.r.z = d[2]; e.r.w = d[3];
+    e.t[0] = d[4]; e.t[1] = d[5]; e.t[2] = d[6];
+    return e;
 }
 
 // Huber kernels of the two edge types (Optimizer.cpp:240-241: float deltas, setDelta(double)).
@@ -97,7 +144,7 @@ struct PoKernels {
 
 __device__ __forceinline__ bool po_is_stereo(const DevPoseProb& P, int e) { return P.ur && po_g(P.ur)[e] >= 0.0f; }
 
-// Error of edge e at `est` (computeError of its edge type), stored as _error.
+// Error of edge e at `est` (computeError of its edge type).
 __device__ __forceinline__ double3 po_edge_error(const DevPoseProb& P, int e, const PoSE3& est, const PoCam& K) {
     const float4 xw = po_ld(P.xw, e);
     const float2 uv = po_ld(P.uv, e);
@@ -105,14 +152,7 @@ __device__ __forceinline__ double3 po_edge_error(const DevPoseProb& P, int e, co
     const double X[3] = {(double)xw.x, (double)xw.y, (double)xw.z};
     double e0, e1, e2;
     po_error(est, K, X, (double)uv.x, (double)uv.y, st ? (double)po_g(P.ur)[e] : 0.0, st, e0, e1, e2);
-    po_st(P.err, e, e0, e1);
-    if (st) po_g(P.err_r)[e] = e2;
     return make_double3(e0, e1, e2);
-}
-
-__device__ __forceinline__ double3 po_stored_error(const DevPoseProb& P, int e) {
-    const double2 er = po_ld(P.err, e);
-    return make_double3(er.x, er.y, po_is_stereo(P, e) ? po_g(P.err_r)[e] : 0.0);
 }
 
 // Inputs of one edge, loaded a slab ahead of their use in a pass.
@@ -135,7 +175,11 @@ __device__ __forceinline__ PoEdgeIn po_load(const DevPoseProb& P, int e) {
 // The level-0 edges in edge order (SparseOptimizer::initializeOptimization(0) keeps the edges of
 // level 0 in the order they were added, sparse_optimizer.cpp:174-182); returns their count.
 __device__ int po_list_active(const PoseLds& S, int n) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // tid laundered: the scan's shuffle addresses are recomputed per call instead of being hoisted
+    // out of the round loop and held (spilled) across the passes
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, w = tid >> 6;
     const int per = (n + kPoseThreads - 1) / kPoseThreads;
     const int lo = min(n, tid * per), hi = min(n, lo + per);
     int c = 0;
@@ -159,82 +203,129 @@ __device__ int po_list_active(const PoseLds& S, int n) {
     return total;
 }
 
-// One pass at `est` over the m active edges: computeActiveErrors (errors stored),
-// activeRobustChi2 (sparse_optimizer.cpp:61-114) and BlockSolver::buildSystem
-// (block_solver.hpp:502-560: H lower triangle added, b subtracted, both from 0.0), every sum
-// folded in edge order.
-__device__ void po_pass(const DevPoseProb& P, const PoseLds& S, int m, const PoSE3& est, const PoCam& K, bool robust,
-                        const PoKernels& hk, double (&H)[6][6], double (&b)[6], double& chi) {
+// The first slab's inputs of this lane (edge list position po_slot), kept in registers
+// for the round's passes: a pass then starts on its first slab without a load round trip.
+__device__ __forceinline__ PoEdgeIn po_first(const DevPoseProb& P, const PoseLds& S, int m) {
+    const int j = po_slot(threadIdx.x);
+    PoEdgeIn f{};
+    if (j >= 0 && j < m) f = po_load(P, S.list[j]);
+    return f;
+}
+
+// One pass at `est` over the m active edges: computeActiveErrors, activeRobustChi2
+// (sparse_optimizer.cpp:61-114) and BlockSolver::buildSystem (block_solver.hpp:502-560: H lower
+// triangle added, b subtracted, both from 0.0), every sum folded in edge order; the folded sums are
+// left in S.red (returns chi2).  `first` = the inputs of the lane's edge in the first slab, loaded
+// once per round (po_first).
+__device__ double po_pass(const DevPoseProb& P, const PoseLds& S, int m, const PoEdgeIn& first, const PoSE3& est,
+                          const PoCam& K, bool robust, const PoKernels& hk, uint64_t (&ps)[6]) {
     const int tid = threadIdx.x;
     const int nslab = (m + kPoseSlab - 1) / kPoseSlab;
-    const int j = tid - kPoseFoldLanes;
-    PoEdgeIn nx{};
-    if (j >= 0 && j < m) nx = po_load(P, S.list[j]);
+    const int j = po_slot(tid);
+    PoEdgeIn nx = first;
     double acc = 0.0;
     for (int k = 0; k <= nslab; ++k) {
-        if (j >= 0) {
-            const int pos = k * kPoseSlab + j;
-            if (k < nslab && pos < m) {
+        double t[kPoseTerms], tc = 0.0;
+        const int pos = k * kPoseSlab + j;
+        if (j >= 0 && k < nslab) {
+            if (pos < m) {
+                // phase clocks of wave 1 (lane 0): [0] slab start -> error, [1] error -> terms
+                const bool pclk = kPosePhases && tid == kPoseFoldLanes;
+                uint64_t c0 = pclk ? wall_clock64() : 0;
                 const PoEdgeIn in = nx;
                 if (pos + kPoseSlab < m) nx = po_load(P, S.list[pos + kPoseSlab]);
                 const bool st = in.ur >= 0.0f;
                 const double X[3] = {(double)in.xw.x, (double)in.xw.y, (double)in.xw.z};
-                double t[kPoseTerms], tc;
                 if constexpr (RSC_PO_DIAG == 1) {
                     RSC_UNROLL for (int q = 0; q < kPoseTerms; ++q) t[q] = X[q % 3] * 1e-30;
                     tc = X[0] * 1e-30;
                 } else {
                     double e0, e1, e2;
                     po_error(est, K, X, (double)in.uv.x, (double)in.uv.y, st ? (double)in.ur : 0.0, st, e0, e1, e2);
-                    po_st(P.err, in.e, e0, e1);
-                    if (st) po_g(P.err_r)[in.e] = e2;
+                    if (pclk) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        const uint64_t c1 = wall_clock64() + (uint64_t)(e0 != e0) + (uint64_t)(e2 != e2);
+                        ps[0] += c1 - c0;
+                        c0 = c1;
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                     const double delta = st ? hk.ds : hk.dm, dsqr = st ? hk.ds2 : hk.dm2;
-                    po_quad_terms(est, K, X, (double)in.xw.w, e0, e1, e2, st, robust, delta, dsqr, t);
+                    // the zero-product-free form, and the full one for an edge outside its precondition
+                    if (!po_quad_terms_finite(est, K, X, (double)in.xw.w, e0, e1, e2, st, robust, delta, dsqr, t))
+                        po_quad_terms(est, K, X, (double)in.xw.w, e0, e1, e2, st, robust, delta, dsqr, t);
                     tc = po_chi_term(robust, st, (double)in.xw.w, e0, e1, e2, delta, dsqr);
                 }
-                double* buf = S.terms + (k & 1) * kPoseBuf + j;
-                RSC_UNROLL for (int q = 0; q < 21; ++q) buf[q * kPoseCol] = t[q];
-                RSC_UNROLL for (int q = 21; q < kPoseTerms; ++q) buf[q * kPoseCol] = -t[q];
-                buf[kPoseTerms * kPoseCol] = tc;
-            } else if (k < nslab) {
+                RSC_UNROLL for (int q = 21; q < kPoseTerms; ++q) t[q] = -t[q];
+                if (pclk) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    ps[1] += wall_clock64() - c0 + (uint64_t)(t[0] != t[0]);
+                    ps[2] += 1;
+                }
+            } else {
                 // padding of the last slab: +0.0 terms are exact identities of these folds (an
                 // accumulator that starts at +0.0 never becomes -0.0 under round-to-nearest)
-                double* buf = S.terms + (k & 1) * kPoseBuf + j;
-                RSC_UNROLL for (int q = 0; q < kPoseCols; ++q) buf[q * kPoseCol] = 0.0;
+                RSC_UNROLL for (int q = 0; q < kPoseTerms; ++q) t[q] = 0.0;
             }
-        } else if (k > 0 && tid < kPoseCols) {
-            if constexpr (RSC_PO_DIAG != 2) acc = fold_fixed<kPoseSlab>(acc, S.terms + ((k - 1) & 1) * kPoseBuf + tid * kPoseCol);
+            if constexpr (!kPoseWide) {
+                double* buf = S.terms + (k & 1) * kPoseBuf + j;
+                RSC_UNROLL for (int q = 0; q < kPoseTerms; ++q) buf[q * kPoseCol] = t[q];
+                buf[kPoseTerms * kPoseCol] = tc;
+            }
+        } else if (tid < kPoseCols && k > 0) {
+            // fold clocks of lane 0: [3] folding, [4] folds
+            const bool fclk = kPosePhases && tid == 0;
+            const uint64_t f0 = fclk ? wall_clock64() : 0;
+            if constexpr (RSC_PO_DIAG != 2)
+                acc = fold_fixed<kPoseSlab>(acc, S.terms + (kPoseWide ? 0 : ((k - 1) & 1) * kPoseBuf) + tid * kPoseCol);
+            if (fclk) {
+                __builtin_amdgcn_sched_barrier(0);
+                ps[3] += wall_clock64() - f0 + (uint64_t)(acc != acc);
+                ps[4] += 1;
+            }
         }
         __syncthreads();
+        if constexpr (kPoseWide) {
+            // the fold of slab k - 1 is done: slab k's terms go into the buffer
+            if (k < nslab) {
+                if (j >= 0) {
+                    double* buf = S.terms + j;
+                    RSC_UNROLL for (int q = 0; q < kPoseTerms; ++q) buf[q * kPoseCol] = t[q];
+                    buf[kPoseTerms * kPoseCol] = tc;
+                }
+                __syncthreads();
+            }
+        }
     }
     if (tid < kPoseCols) S.red[tid] = acc;
     __syncthreads();
-    int q = 0;
-    RSC_UNROLL for (int i = 0; i < 6; ++i)
-        RSC_UNROLL for (int j = 0; j <= i; ++j) {
-            H[i][j] = S.red[q++];
-            H[j][i] = H[i][j];
-        }
-    RSC_UNROLL for (int i = 0; i < 6; ++i) b[i] = S.red[21 + i];
-    chi = S.red[kPoseTerms];
+    return S.red[kPoseTerms];
     // S.red is next written after the next pass's slab barriers, by which time every thread has read it
+}
+
+// S.cur = S.red (the LM adopts the last pass's system); every thread reads S.cur after the barrier.
+__device__ __forceinline__ void po_adopt(const PoseLds& S) {
+    if (threadIdx.x < kPoseCols) S.cur[threadIdx.x] = S.red[threadIdx.x];
+    __syncthreads();
 }
 
 }  // namespace
 
 // Diagnostic phase clock (wall clock, 100 MHz ticks) of the last launch, frames 0..63: [0] passes,
 // [1] number of passes + (sum of their active edges << 24), [2] re-classification, [3] whole kernel
-// (thread 0); [4..7] unused.
-__device__ uint64_t g_po_phase[64][8];
+// (thread 0); [4] the LM trials' solve (LDLT + exp + product, thread 0); [5] / [6] wave 1's slab time
+// up to the edges' errors / from there to the terms stored, [7] its slab count; [8 + w] the HW_ID
+// register of wave w (which SIMD each wave of the workgroup landed on); [16] / [17] wave 0's folding
+// time and fold count.
+__device__ uint64_t g_po_phase[64][24];
 
 __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb* __restrict__ probs) {
     extern __shared__ __attribute__((aligned(16))) double po_lds[];
-    __shared__ double red_sh[32];
+    __shared__ double red_sh[32], cur_sh[32];
     __shared__ int scan_sh[kPoseThreads / 64];
     __shared__ int nbad_sh;
-    const PoseLds S{po_lds, reinterpret_cast<uint16_t*>(po_lds + 2 * kPoseBuf),
-                    reinterpret_cast<uint8_t*>(po_lds + 2 * kPoseBuf) + sizeof(uint16_t) * kPoseMaxEdges, red_sh,
-                    scan_sh, &nbad_sh};
+    const PoseLds S{po_lds, reinterpret_cast<uint16_t*>(po_lds + kPoseBufs * kPoseBuf),
+                    reinterpret_cast<uint8_t*>(po_lds + kPoseBufs * kPoseBuf) + sizeof(uint16_t) * kPoseMaxEdges,
+                    red_sh, cur_sh, scan_sh, &nbad_sh};
     const DevPoseProb& P = probs[blockIdx.x];
     const int tid = threadIdx.x, n = P.n;
     const PoCam K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy, (double)P.bf};
@@ -251,31 +342,45 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
         RSC_UNROLL for (int c = 0; c < 3; ++c) R0[r][c] = (double)P.T[4 * r + c];
         t0[r] = (double)P.T[4 * r + 3];
     }
-    const PoSE3 init = po_from_Rt(R0, t0);  // Converter::toSE3Quat (rotation() = linear(), Q14)
+    // Converter::toSE3Quat (rotation() = linear(), Q14), parked in LDS and read back per round rather
+    // than held in VGPRs across the passes (read after the barrier below)
+    __shared__ double init_sh[8];
+    if (tid == 0) po_put(init_sh, po_from_Rt(R0, t0));
+    auto init = [&]() { return po_get(init_sh); };
     const bool clk = kPosePhases && blockIdx.x < 64 && tid == 0;
-    uint64_t ph_pass = 0, n_pass = 0, ph_cls = 0, t_start = clk ? wall_clock64() : 0;
+    uint64_t ph_pass = 0, n_pass = 0, ph_cls = 0, ph_solve = 0, t_start = clk ? wall_clock64() : 0;
+    uint64_t ps[6] = {0, 0, 0, 0, 0, 0};  // wave 1's slab and wave 0's fold clocks (po_pass)
     for (int e = tid; e < n; e += kPoseThreads) {
         S.lvl[e] = 0;
         po_g(P.outlier)[e] = 0;
     }
     if (tid == 0) *S.nbad = 0;
+    if (kPosePhases && blockIdx.x < 64 && (tid & 63) == 0) {
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        g_po_phase[blockIdx.x][8 + (tid >> 6)] = hw;
+    }
     __syncthreads();
 
     double x[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // BlockSolver::_x persists across rounds
     double lambda = -1.0, ni = 2.0;
     int nBadLM = 0, rounds = 0, lm_its = 0, lm_trials = 0, nBad = 0;
     bool robust = true;
-    PoSE3 est = init;
+    PoSE3 est = init();
+    // the estimate of the round's last pass (the level-0 edges' _error is evaluated there), in LDS
+    __shared__ double last_sh[8];
     for (int it = 0; it < 4; ++it) {
         rounds++;
-        est = init;
+        est = init();
+        if (tid == 0) po_put(last_sh, est);  // read after the round's barriers
         const int m = po_list_active(S, n);
         if (m > 0) {
-            // the system at est and the chi2 solve() computes there
-            double H[6][6], b[6], chiEst;
+            const PoEdgeIn first = po_first(P, S, m);
+            // the system at est (S.cur) and the chi2 solve() computes there
             uint64_t tp = clk ? wall_clock64() : 0;
-            po_pass(P, S, m, est, K, robust, hk, H, b, chiEst);
+            double chiEst = po_pass(P, S, m, first, est, K, robust, hk, ps);
             if (clk) { ph_pass += wall_clock64() - tp; n_pass += 1 + ((uint64_t)m << 24); }
+            po_adopt(S);
             bool ok = true;
             for (int i = 0; i < 10 && ok; ++i) {
                 lm_its++;
@@ -284,7 +389,7 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
                 if (i == 0) {
                     double maxDiagonal = 0.;
                     RSC_UNROLL for (int j = 0; j < 6; ++j) {  // std::max(fabs(H(j,j)), maxDiagonal)
-                        const double a = rabs(H[j][j]);
+                        const double a = rabs(S.cur[j * (j + 1) / 2 + j]);
                         maxDiagonal = (a < maxDiagonal) ? maxDiagonal : a;
                     }
                     lambda = 1e-5 * maxDiagonal;
@@ -295,17 +400,22 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
                 int qmax = 0;
                 do {
                     lm_trials++;
-                    double Hd[6][6];
-                    RSC_UNROLL for (int r = 0; r < 6; ++r)
-                        RSC_UNROLL for (int c = 0; c < 6; ++c) Hd[r][c] = H[r][c];
+                    const uint64_t ts = clk ? wall_clock64() : 0;
+                    double Hd[6][6], b[6];
+                    RSC_UNROLL for (int r = 0; r < 6; ++r) {
+                        RSC_UNROLL for (int c = 0; c < 6; ++c)
+                            Hd[r][c] = r >= c ? S.cur[r * (r + 1) / 2 + c] : S.cur[c * (c + 1) / 2 + r];
+                        b[r] = S.cur[21 + r];
+                    }
                     RSC_UNROLL for (int r = 0; r < 6; ++r) Hd[r][r] += lambda;
                     double xs[6];
                     const bool ok2 = po_ldlt_solve6(Hd, b, xs);
                     if (ok2) RSC_UNROLL for (int j = 0; j < 6; ++j) x[j] = xs[j];
                     const PoSE3 trial = po_mul(po_exp(x), est);
-                    double Ht[6][6], bt[6], chiT;
                     tp = clk ? wall_clock64() : 0;
-                    po_pass(P, S, m, trial, K, robust, hk, Ht, bt, chiT);
+                    if (clk) ph_solve += tp - ts;
+                    const double chiT = po_pass(P, S, m, first, trial, K, robust, hk, ps);
+                    if (tid == 0) po_put(last_sh, trial);  // read after this pass's barriers
                     if (clk) { ph_pass += wall_clock64() - tp; n_pass += 1 + ((uint64_t)m << 24); }
                     const double tempChi = ok2 ? chiT : DBL_MAX;
                     rho = (currentChi - tempChi);
@@ -321,10 +431,7 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
                         ni = 2;
                         currentChi = tempChi;
                         est = trial;
-                        RSC_UNROLL for (int r = 0; r < 6; ++r) {
-                            RSC_UNROLL for (int c = 0; c < 6; ++c) H[r][c] = Ht[r][c];
-                            b[r] = bt[r];
-                        }
+                        po_adopt(S);  // the trial's system (a uniform branch: every thread decides alike)
                         chiEst = chiT;
                     } else {
                         lambda *= ni;
@@ -346,7 +453,7 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
         const uint64_t tr0 = clk ? wall_clock64() : 0;
         int cnt = 0;
         for (int e = tid; e < n; e += kPoseThreads) {
-            const double3 er = S.lvl[e] ? po_edge_error(P, e, est, K) : po_stored_error(P, e);
+            const double3 er = po_edge_error(P, e, S.lvl[e] ? est : po_get(last_sh), K);
             const bool st = po_is_stereo(P, e);
             const float c2 = (float)po_chi2((double)po_ld(P.xw, e).w, st, er.x, er.y, er.z);
             const bool bad = c2 > (st ? chi2Stereo : chi2Mono);
@@ -380,11 +487,24 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
         g_po_phase[blockIdx.x][1] = n_pass;
         g_po_phase[blockIdx.x][2] = ph_cls;
         g_po_phase[blockIdx.x][3] = wall_clock64() - t_start;
+        g_po_phase[blockIdx.x][4] = ph_solve;
+        g_po_phase[blockIdx.x][16] = ps[3];
+        g_po_phase[blockIdx.x][17] = ps[4];
+    }
+    if (kPosePhases && blockIdx.x < 64 && tid == kPoseFoldLanes) {
+        g_po_phase[blockIdx.x][5] = ps[0];
+        g_po_phase[blockIdx.x][6] = ps[1];
+        g_po_phase[blockIdx.x][7] = ps[2];
     }
 }
 
-hipError_t read_poseopt_phases(uint64_t* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_po_phase), sizeof(uint64_t) * 64 * 8, 0, hipMemcpyDeviceToHost);
+hipError_t read_poseopt_phases(uint64_t* out, bool wide) {
+    uint64_t all[64][24];
+    if (hipError_t e = hipMemcpyFromSymbol(all, HIP_SYMBOL(g_po_phase), sizeof(all), 0, hipMemcpyDeviceToHost)) return e;
+    const int w = wide ? 24 : 8;
+    for (int f = 0; f < 64; ++f)
+        for (int k = 0; k < w; ++k) out[f * w + k] = all[f][k];
+    return hipSuccess;
 }
 
 hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st) {

@@ -190,12 +190,9 @@ struct rsc_context {
     PinBuf<RefineSelOut> h_selout;
     // PoseOptimization: packed inputs (problems | xw | uv), edge error scratch, results (outliers | poses)
     DevBuf<char> d_po_in;
-    DevBuf<double2> d_po_err;
-    DevBuf<double> d_po_err_r;  // third error component of the stereo edges
     // OptimizeSim3: packed inputs (problems | e12 | e21 | uv), edge errors, results (out | keep)
     DevBuf<char> d_so_in;
     PinBuf<char> h_so_in;
-    DevBuf<double2> d_so_err;
     DevBuf<char> d_so_res;
     PinBuf<char> h_so_res;
     DevBuf<char> d_po_res;
@@ -1738,8 +1735,6 @@ int rsc_pose_optimization_many(rsc_context* C, const rsc_poseopt_problem* P, int
     if (int e = C->d_po_in.ensure(in_bytes)) return e;
     if (int e = C->h_po_res.ensure(res_bytes)) return e;
     if (int e = C->d_po_res.ensure(res_bytes)) return e;
-    if (int e = C->d_po_err.ensure(E)) return e;
-    if (int e = C->d_po_err_r.ensure(E)) return e;
     // the previous call's copies out of the pinned staging must be complete
     RSC_HIP(hipStreamSynchronize(C->stream));
     char* h = C->h_po_in.p;
@@ -1764,8 +1759,6 @@ int rsc_pose_optimization_many(rsc_context* C, const rsc_poseopt_problem* P, int
         dp.xw = reinterpret_cast<const float4*>(d + o_xw) + eoff[k];
         dp.uv = reinterpret_cast<const float2*>(d + o_uv) + eoff[k];
         dp.ur = stereo ? reinterpret_cast<const float*>(d + o_ur) + eoff[k] : nullptr;
-        dp.err = C->d_po_err.p + eoff[k];
-        dp.err_r = C->d_po_err_r.p + eoff[k];
         dp.outlier = reinterpret_cast<uint8_t*>(C->d_po_res.p + r_flags) + eoff[k];
         dp.out = reinterpret_cast<float*>(C->d_po_res.p + r_out) + 16 * k;
         dp.n = (int)(eoff[k + 1] - eoff[k]);
@@ -1848,7 +1841,6 @@ int rsc_optimize_sim3_many(rsc_context* C, const rsc_sim3opt_problem* P, int cou
     if (int e = C->d_so_in.ensure(in_bytes)) return e;
     if (int e = C->h_so_res.ensure(res_bytes)) return e;
     if (int e = C->d_so_res.ensure(res_bytes)) return e;
-    if (int e = C->d_so_err.ensure(2 * M)) return e;
     RSC_HIP(hipStreamSynchronize(C->stream));  // the previous call's copies out of the staging are done
     char* h = C->h_so_in.p;
     char* d = C->d_so_in.p;
@@ -1878,7 +1870,6 @@ int rsc_optimize_sim3_many(rsc_context* C, const rsc_sim3opt_problem* P, int cou
         dp.e12 = reinterpret_cast<const float4*>(d + o_e12) + moff[k];
         dp.e21 = reinterpret_cast<const float4*>(d + o_e21) + moff[k];
         dp.uv = reinterpret_cast<const float4*>(d + o_uv) + moff[k];
-        dp.err = C->d_so_err.p + 2 * moff[k];
         dp.keep = reinterpret_cast<uint8_t*>(C->d_so_res.p + r_keep) + moff[k];
         dp.out = reinterpret_cast<double*>(C->d_so_res.p) + 16 * k;
         dp.m = (int)(moff[k + 1] - moff[k]);
@@ -2603,7 +2594,7 @@ int rsc_diag_poseopt_phases(rsc_context* C, uint64_t* out, int cap) {
     if (!C || !out || cap < 64 * 8) return RSC_ERR_ARG;
     RSC_HIP(hipSetDevice(C->device));
     RSC_HIP(hipStreamSynchronize(C->stream));
-    RSC_HIP(read_poseopt_phases(out));
+    RSC_HIP(read_poseopt_phases(out, cap >= 64 * 24));
     return RSC_OK;
 }
 

@@ -38,6 +38,14 @@
 #else
 #define RSC_LOOP_FENCE() ((void)0)
 #endif
+// A scheduling fence (no instruction): the scheduler keeps every instruction on its side, so a
+// straight-line sequence of independent blocks does not have all their loads hoisted to the top
+// (the register live ranges stay one block long).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RSC_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define RSC_SCHED_FENCE() ((void)0)
+#endif
 
 namespace rsc {
 
@@ -236,7 +244,7 @@ RSC_HD bool tridiag_qr(S (&diag)[n], S (&sub)[n - 1], QApply&& qapply, int (&per
         // for (i = start; i < end; ++i): |sub| < considerAsZero, or (sub/eps)^2 <= |d_i| + |d_i+1|
         RSC_UNROLL for (int i = 0; i < n - 1; ++i) {
             const S scaled = precision_inv * sub[i];
-            const bool z = (rabs(sub[i]) < considerAsZero) | (scaled * scaled <= (rabs(diag[i]) + rabs(diag[i + 1])));
+            const bool z = (int)(rabs(sub[i]) < considerAsZero) | (int)(scaled * scaled <= (rabs(diag[i]) + rabs(diag[i + 1])));
             sub[i] = (z & (i >= start) & (i < end)) ? S(0) : sub[i];
         }
         // The two searches on a bit mask of the nonzero sub-diagonal entries (a find-last-set instead
@@ -856,7 +864,7 @@ RSC_HD void jacobi_svd_solve_6xk(const double (&Ain)[6][k], const double (&b)[6]
             RSC_UNROLL for (int q = 0; q < p; ++q) {
                 double pt = precision * maxDiag;
                 double threshold = (considerAsZero < pt) ? pt : considerAsZero;
-                if ((rabs(W[p][q]) > threshold) | (rabs(W[q][p]) > threshold)) {
+                if ((int)(rabs(W[p][q]) > threshold) | (int)(rabs(W[q][p]) > threshold)) {
                     finished = false;
                     // real_2x2_jacobi_svd.  Its inner ifs are value selects on the same operands
                     // (a divergent if is an exec-mask region, a uniform one a scalar branch; both cost

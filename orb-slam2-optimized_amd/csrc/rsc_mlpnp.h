@@ -143,39 +143,35 @@ RSC_HD int ml_fullpiv_rank3(const double (&A)[3][3]) {
 // threshold (no rotation).
 RSC_HD void ml_jacobi_2x2(double m00, double m01, double m10, double m11, double& cl, double& sl, double& cr,
                           double& sr) {
+    // real_2x2_jacobi_svd with its ifs as value selects on the same operands (a divergent if is an
+    // exec-mask region; the selects keep the 16 hypotheses of a wave on one instruction stream), and
+    // 1 / sqrt(tt^2 + 1) in the short-chain unit forms: |tt| <= 1 (|tau +- w| >= 1), so tt^2 + 1 is
+    // in [1, 2] and its root in [1, sqrt 2] (rsc_core.h sqrt_unit / recip_unit, correctly rounded).
     const double considerAsZero = lim<double>::min();
-    double c1, s1;
     const double t = m00 + m11;
     const double d = m10 - m01;
-    if (rabs(d) < considerAsZero) {
-        s1 = 0.0;
-        c1 = 1.0;
-    } else {
-        const double u = t / d;
-        const double tmp = sqrt(1.0 + u * u);
-        s1 = 1.0 / tmp;
-        c1 = u / tmp;
-    }
-    if (!(c1 == 1.0 && s1 == 0.0)) {
+    const bool dz = rabs(d) < considerAsZero;
+    const double u = t / d;
+    const double tmp = sqrt(1.0 + u * u);
+    const double s1 = dz ? 0.0 : 1.0 / tmp;
+    const double c1 = dz ? 1.0 : u / tmp;
+    {
+        const bool rot = !((int)(c1 == 1.0) & (int)(s1 == 0.0));
         const double x0 = m00, y0 = m10, x1 = m01, y1 = m11;
-        m00 = c1 * x0 + s1 * y0;
-        m10 = -s1 * x0 + c1 * y0;
-        m01 = c1 * x1 + s1 * y1;
-        m11 = -s1 * x1 + c1 * y1;
+        m00 = rot ? c1 * x0 + s1 * y0 : x0;
+        m10 = rot ? -s1 * x0 + c1 * y0 : y0;
+        m01 = rot ? c1 * x1 + s1 * y1 : x1;
+        m11 = rot ? -s1 * x1 + c1 * y1 : y1;
     }
     const double deno = 2.0 * rabs(m01);
-    if (deno < considerAsZero) {
-        cr = 1.0;
-        sr = 0.0;
-    } else {
-        const double tau = (m00 - m11) / deno;
-        const double w = sqrt(tau * tau + 1.0);
-        const double tt = (tau > 0.0) ? 1.0 / (tau + w) : 1.0 / (tau - w);
-        const double sign_t = tt > 0.0 ? 1.0 : -1.0;
-        const double nn = 1.0 / sqrt(tt * tt + 1.0);
-        sr = -sign_t * (m01 / rabs(m01)) * rabs(tt) * nn;
-        cr = nn;
-    }
+    const bool nz = deno < considerAsZero;
+    const double tau = (m00 - m11) / deno;
+    const double w = sqrt(tau * tau + 1.0);
+    const double tt = 1.0 / (tau > 0.0 ? tau + w : tau - w);
+    const double sign_t = tt > 0.0 ? 1.0 : -1.0;
+    const double nn = recip_unit(sqrt_unit(tt * tt + 1.0));
+    sr = nz ? 0.0 : -sign_t * (m01 / rabs(m01)) * rabs(tt) * nn;
+    cr = nz ? 1.0 : nn;
     const double crt = cr, srt = -sr;
     cl = c1 * crt - s1 * srt;
     sl = c1 * srt + s1 * crt;

@@ -101,12 +101,11 @@ __device__ __forceinline__ void ml_quad_jacobi_step(double (&Wc)[3][12], double 
         finished = false;
         double cl, sl, cr, sr;
         ml_jacobi_2x2(qm_get<P, P>(Wc), wps, wsp, qm_get<S, S>(Wc), cl, sl, cr, sr);
-        if (!(cl == 1.0 && sl == 0.0)) {
-            RSC_UNROLL for (int j = 0; j < 3; ++j) {  // rows P, S over the own columns
-                const double xi = Wc[j][P], yi = Wc[j][S];
-                Wc[j][P] = cl * xi + sl * yi;
-                Wc[j][S] = -sl * xi + cl * yi;
-            }
+        const bool lrot = !((int)(cl == 1.0) & (int)(sl == 0.0));  // a select: 6 products per lane
+        RSC_UNROLL for (int j = 0; j < 3; ++j) {  // rows P, S over the own columns
+            const double xi = Wc[j][P], yi = Wc[j][S];
+            Wc[j][P] = lrot ? cl * xi + sl * yi : xi;
+            Wc[j][S] = lrot ? -sl * xi + cl * yi : yi;
         }
         if (!(cr == 1.0 && sr == 0.0)) {
             qm_rotate_cols<n, P, S>(Wc, q, cr, sr);

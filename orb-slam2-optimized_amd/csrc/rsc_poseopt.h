@@ -32,8 +32,6 @@ struct DevPoseProb {
     const float4* xw;    // [n] Xw (x, y, z), w = invSigma2 (information = I * invSigma2)
     const float2* uv;    // [n] observation mvKeysUn[i].pt
     const float* ur;     // [n] mvuRight (>= 0: stereo edge), or nullptr: every edge monocular
-    double2* err;        // [n] scratch: the edges' _error (u, v components)
-    double* err_r;       // [n] scratch: third _error component of the stereo edges
     uint8_t* outlier;    // [n] out: mvbOutlier of each edge
     float* out;          // out: [0..11] Tcw rows 0..2 (float), [12] nGood (as float bits of int), [13..15] stats
     int n;               // edges (slots with a map point), >= 3
@@ -336,10 +334,104 @@ RSC_HD void po_quad_terms(const PoSE3& est, const PoCam& K, const double (&Xw)[3
     }
 }
 
+// po_quad_terms without its multiplications by the information matrix's zero off-diagonal entries
+// (Wo = rho1 * 0.0, the 0.0 of omega): when every Jacobian entry, rho1 and inv are finite, each such
+// product is a signed zero, and x + (+-0) is x for x != 0 and a zero otherwise — so every term equals
+// po_quad_terms' up to the sign of a zero term.  The folds cannot tell those apart: every H / b / chi2
+// accumulator starts at +0.0 and adds (b: subtracts) the terms, and under round-to-nearest a sum is
+// -0 only when both operands are -0, so an accumulator that starts at +0.0 never holds -0 and
+// acc + (+0) == acc + (-0) for every acc it can hold.  The errors are in the precondition too (a zero
+// term times an infinite error would be a NaN whose bits the folds carry).  Returns false (t
+// unspecified) when the finite precondition fails; the caller then evaluates po_quad_terms.  Products
+// by zero make up about a third of po_quad_terms' multiply-adds.
+RSC_HD bool po_quad_terms_finite(const PoSE3& est, const PoCam& K, const double (&Xw)[3], double inv, double e0,
+                                 double e1, double e2, bool stereo, bool robust, double delta, double dsqr,
+                                 double (&t)[kPoseTerms]) {
+    double p[3];
+    po_map(est, Xw, p);
+    const double x = p[0], y = p[1];
+    const double invz = 1.0 / p[2];
+    const double invz_2 = invz * invz;
+    double A[3][6];
+    A[0][0] = x * y * invz_2 * K.fx;
+    A[0][1] = -(1 + (x * x * invz_2)) * K.fx;
+    A[0][2] = y * invz * K.fx;
+    A[0][3] = -invz * K.fx;
+    A[0][4] = 0;
+    A[0][5] = x * invz_2 * K.fx;
+    A[1][0] = (1 + y * y * invz_2) * K.fy;
+    A[1][1] = -x * y * invz_2 * K.fy;
+    A[1][2] = -x * invz * K.fy;
+    A[1][3] = 0;
+    A[1][4] = -invz * K.fy;
+    A[1][5] = y * invz_2 * K.fy;
+    A[2][0] = A[0][0] - K.bf * y * invz_2;
+    A[2][1] = A[0][1] + K.bf * x * invz_2;
+    A[2][2] = A[0][2];
+    A[2][3] = A[0][3];
+    A[2][4] = 0;
+    A[2][5] = A[0][5] - K.bf * invz_2;
+    double Wd = inv, rho1 = 1.0;
+    if (robust) {
+        double r0;
+        po_huber(po_chi2(inv, stereo, e0, e1, e2), delta, dsqr, r0, rho1);
+        Wd = rho1 * inv;
+    }
+    // finite precondition (a sum of magnitudes: an overflow only sends the edge to the full form)
+    double mag = ((rabs(rho1) + rabs(inv)) + (rabs(e0) + rabs(e1))) + rabs(e2);
+    RSC_UNROLL for (int i = 0; i < 6; ++i) mag = mag + ((rabs(A[0][i]) + rabs(A[1][i])) + rabs(A[2][i]));
+    // The Jacobian's constant zeros A[0][4] = A[1][3] = A[2][4] = 0 make every product through them a
+    // signed zero too (finite precondition), so those products are dropped from the sums the same way
+    // (z0 / z1 / z2 below: static after unrolling).
+    double tm[6][3];  // A^T W
+    RSC_UNROLL for (int i = 0; i < 6; ++i) {
+        tm[i][0] = A[0][i] * Wd;
+        tm[i][1] = A[1][i] * Wd;
+        tm[i][2] = A[2][i] * Wd;
+    }
+    int k = 0;
+    RSC_UNROLL for (int i = 0; i < 6; ++i)
+        RSC_UNROLL for (int j = 0; j <= i; ++j) {
+            const bool z0 = (i == 4) | (j == 4), z1 = (i == 3) | (j == 3), z2 = (i == 4) | (j == 4);
+            double h;
+            if (!z0 && !z1) h = tm[i][0] * A[0][j] + tm[i][1] * A[1][j];
+            else if (!z0) h = tm[i][0] * A[0][j];
+            else if (!z1) h = tm[i][1] * A[1][j];
+            else h = 0.0;
+            t[k++] = (stereo && !z2) ? h + tm[i][2] * A[2][j] : h;
+        }
+    RSC_UNROLL for (int i = 0; i < 6; ++i) {
+        double a0 = A[0][i], a1 = A[1][i], a2 = A[2][i];
+        if (robust) {
+            a0 = rho1 * a0;
+            a1 = rho1 * a1;
+            a2 = rho1 * a2;
+        }
+        double gb;
+        if (i == 3) gb = (a0 * inv) * e0;       // a1 = rho1 A[1][3] = 0
+        else if (i == 4) gb = (a1 * inv) * e1;  // a0 = a2 = 0
+        else gb = (a0 * inv) * e0 + (a1 * inv) * e1;
+        t[21 + i] = (stereo && i != 4) ? gb + (a2 * inv) * e2 : gb;
+    }
+    return mag <= 1.7976931348623157e308;  // finite (a NaN compares false)
+}
+
+// A pivot index every lane of the wave holds (device: read from the first lane into an SGPR, so the
+// branches on it are scalar and only the taken transposition runs; host: itself).
+RSC_HD int po_uniform(int v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_readfirstlane(v);
+#else
+    return v;
+#endif
+}
+
 // Eigen::LDLT<MatrixXd> on the lower triangle of the n x n (ldlt_inplace<Lower>::unblocked) and
 // _solve_impl; returns isPositive() (x untouched otherwise, as LinearSolverDense::solve).
-// Register arrays with static indices only: the diagonal pivot search and the symmetric
-// transposition are written as value selects.  n = 6 (PoseOptimization), 7 (OptimizeSim3).
+// Register arrays with static indices only: the diagonal pivot search is a select chain, the pivot
+// it finds is made wave-uniform (po_uniform) and the symmetric transposition and the solve's
+// permutation steps branch on it.  Precondition: every lane of the wave solves the same system (the
+// callers' LM steps run redundantly on identical data).  n = 6 (PoseOptimization), 7 (OptimizeSim3).
 template <int n>
 RSC_HD bool po_ldlt_solve(double (&A)[n][n], const double (&b)[n], double (&x)[n]) {
     int sign = 0;  // 0 zero, 1 positive semidef, 2 negative semidef, 3 indefinite
@@ -352,6 +444,7 @@ RSC_HD bool po_ldlt_solve(double (&A)[n][n], const double (&b)[n], double (&x)[n
             double bv = rabs(A[k][k]);
             RSC_UNROLL for (int i = k + 1; i < n; ++i)
                 if (rabs(A[i][i]) > bv) { bv = rabs(A[i][i]); big = i; }
+            big = po_uniform(big);
             tr[k] = big;
             // symmetric swap of k and big on the lower triangle (Eigen's four-step exchange)
             RSC_UNROLL for (int bb = k + 1; bb < n; ++bb) {
@@ -375,7 +468,7 @@ RSC_HD bool po_ldlt_solve(double (&A)[n][n], const double (&b)[n], double (&x)[n
                 }
             }
             const double akk = A[k][k];
-            const bool valid = rabs(akk) > 0.0;
+            const bool valid = po_uniform(rabs(akk) > 0.0);
             if (k == 0 && !valid) {
                 sign = 0;
                 stop = true;
@@ -397,12 +490,8 @@ RSC_HD bool po_ldlt_solve(double (&A)[n][n], const double (&b)[n], double (&x)[n
     double y[n];
     RSC_UNROLL for (int i = 0; i < n; ++i) y[i] = b[i];
     RSC_UNROLL for (int k = 0; k < n; ++k)
-        RSC_UNROLL for (int j = k + 1; j < n; ++j) {
-            const bool sw = (tr[k] == j);
-            const double a = y[k], c = y[j];
-            y[k] = sw ? c : a;
-            y[j] = sw ? a : c;
-        }
+        RSC_UNROLL for (int j = k + 1; j < n; ++j)
+            if (tr[k] == j) rswap(y[k], y[j]);
     RSC_UNROLL for (int i = 1; i < n; ++i) {
         double acc = A[i][0] * y[0];
         RSC_UNROLL for (int j = 1; j < i; ++j) acc = acc + A[i][j] * y[j];
@@ -416,12 +505,8 @@ RSC_HD bool po_ldlt_solve(double (&A)[n][n], const double (&b)[n], double (&x)[n
         y[i] -= acc;
     }
     RSC_UNROLL for (int k = n - 1; k >= 0; --k)
-        RSC_UNROLL for (int j = k + 1; j < n; ++j) {
-            const bool sw = (tr[k] == j);
-            const double a = y[k], c = y[j];
-            y[k] = sw ? c : a;
-            y[j] = sw ? a : c;
-        }
+        RSC_UNROLL for (int j = k + 1; j < n; ++j)
+            if (tr[k] == j) rswap(y[k], y[j]);
     RSC_UNROLL for (int i = 0; i < n; ++i) x[i] = y[i];
     return true;
 }
@@ -429,7 +514,7 @@ RSC_HD bool po_ldlt_solve(double (&A)[n][n], const double (&b)[n], double (&x)[n
 RSC_HD bool po_ldlt_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[6]) { return po_ldlt_solve<6>(A, b, x); }
 
 #if defined(__HIPCC__)
-hipError_t read_poseopt_phases(uint64_t* out);  // diagnostic, [64][8] (poseopt.hip)
+hipError_t read_poseopt_phases(uint64_t* out, bool wide);  // diagnostic, [64][8] or [64][24] (poseopt.hip)
 hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st);
 #endif
 

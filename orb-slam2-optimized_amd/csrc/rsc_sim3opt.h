@@ -33,7 +33,6 @@ struct DevSim3OptProb {
     const float4* e12;   // [m] (P3D2c, invSigma2 of KF1's keypoint)   — edge x1 = S12 * X2
     const float4* e21;   // [m] (P3D1c, invSigma2 of KF2's keypoint)   — edge x2 = S21 * X1
     const float4* uv;    // [m] (kpUn1.pt, kpUn2.pt)
-    double2* err;        // [2m] scratch: _error of e12 (2c) and e21 (2c + 1)
     uint8_t* keep;       // [m] in/out: 1 while the correspondence's edges are in the graph / inliers
     double* out;         // out [16]: q (x, y, z, w), t, s of g2oS12; then nIn, nBad, LM its, LM trials (int bits)
     int m;               // correspondences (>= 1)

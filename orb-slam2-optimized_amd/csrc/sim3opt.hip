@@ -10,6 +10,9 @@
 // H/b terms) into one of two LDS slab buffers while lanes 0..35 of wave 0 fold the previous slab.
 // The 14 perturbed estimates of a pass (and their inverses) are built once, one per lane, into LDS
 // and read from there by every edge.  The 7x7 LDLT and the LM control run redundantly in every lane.
+// The edges' _error is not stored by the passes: the inlier checks recompute it at the estimate of the
+// last pass (SoLM::last), which is what g2o's edges hold then (a pure function of the estimate and the
+// edge, so the same bits); global stores in the slab loop would be waited for at every slab.
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <cfloat>
@@ -20,15 +23,35 @@ namespace rsc {
 
 namespace {
 
-constexpr int kSoThreads = 256;                  // one wave per SIMD of a CU
+// Pass form, as poseopt.hip's: 1 (wide) = 512 threads, wave 0 folds, the wave sharing its SIMD
+// (RSC_SO_IDLE) idles in the passes, six waves evaluate 384 edges per slab into a single buffer;
+// 0 = 256 threads, three edge waves, double-buffered slabs of 192.
+#ifndef RSC_SO_WIDE
+#define RSC_SO_WIDE 0
+#endif
+#ifndef RSC_SO_IDLE
+#define RSC_SO_IDLE 4
+#endif
+constexpr bool kSoWide = RSC_SO_WIDE != 0;
+constexpr int kSoThreads = kSoWide ? 512 : 256;
 constexpr int kSoFoldLanes = 64;                 // wave 0 folds
-constexpr int kSoSlab = kSoThreads - kSoFoldLanes;  // active edges per slab (waves 1..3)
+constexpr int kSoSlab = kSoWide ? 384 : 192;     // active edges per slab
+constexpr int kSoBufs = kSoWide ? 1 : 2;
 constexpr int kSoCol = kSoSlab + 2;              // padded column stride (doubles)
 constexpr int kSoCols = kSim3OptTerms + 1;       // 35 H/b columns + the chi2 column
 constexpr int kSoBuf = kSoCols * kSoCol;         // one slab buffer
 constexpr size_t kSoPt = sizeof(SoPerturbed);
-constexpr size_t kSoLds = sizeof(double) * 2 * kSoBuf + kSoPt + sizeof(uint16_t) * kSim3OptMaxCorr;
+constexpr size_t kSoLds = sizeof(double) * kSoBufs * kSoBuf + kSoPt + sizeof(uint16_t) * kSim3OptMaxCorr;
 static_assert(kSoCol % 2 == 0, "fold_fixed reads 16-byte aligned columns");
+static_assert(kSoLds <= 160 * 1024 - 1024, "LDS");
+static_assert(RSC_SO_IDLE >= 1 && RSC_SO_IDLE <= 7, "idle wave");
+
+// Slab position of this thread's edge (-1: the fold wave, and the idle wave of the wide form).
+__device__ __forceinline__ int so_slot(int tid) {
+    const int w = tid >> 6, lane = tid & 63;
+    if constexpr (kSoWide) return (w == 0 || w == RSC_SO_IDLE) ? -1 : (w - (w > RSC_SO_IDLE ? 2 : 1)) * 64 + lane;
+    else return tid - kSoFoldLanes;
+}
 static_assert(kSoPt % 16 == 0, "the active list follows the perturbed estimates");
 static_assert(kSim3OptMaxCorr <= 65536, "active list is uint16");
 
@@ -48,17 +71,10 @@ __device__ __forceinline__ double2 so_ld(const double2* p, int e) {
     const V v = so_g(reinterpret_cast<const V*>(p))[e];
     return make_double2(v.x, v.y);
 }
-__device__ __forceinline__ void so_st(double2* p, int e, double a, double b) {
-    using V = double __attribute__((ext_vector_type(2)));
-    V v;
-    v.x = a;
-    v.y = b;
-    so_g(reinterpret_cast<V*>(p))[e] = v;
-}
 
 struct SoCtx {
     const DevSim3OptProb& P;
-    double* terms;       // [2][kSoCols][kSoCol] slab buffers
+    double* terms;       // [kSoBufs][kSoCols][kSoCol] slab buffers
     SoPerturbed* pt;     // the pass's perturbed estimates
     uint16_t* list;      // kept correspondences in order
     double* red;         // [36] a pass's folded sums
@@ -129,7 +145,7 @@ __device__ void so_build_perturbed(const SoCtx& C, const SoSim3& S) {
     __syncthreads();
 }
 
-// One pass at S over the 2 mk active edges: computeActiveErrors (errors stored),
+// One pass at S over the 2 mk active edges: computeActiveErrors,
 // activeRobustChi2 (sparse_optimizer.cpp:61-114) and BlockSolverX::buildSystem
 // (block_solver.hpp:502-560: H lower triangle and b added from 0.0), every sum folded in edge order.
 // The folded sums are left in C.red (H lower triangle row-major, b, chi2); C.red is next written at
@@ -138,16 +154,16 @@ __device__ double so_pass(const SoCtx& C, int mk, const SoSim3& S) {
     so_build_perturbed(C, S);
     const int tid = threadIdx.x, me = 2 * mk;
     const int nslab = (me + kSoSlab - 1) / kSoSlab;
-    const int j = tid - kSoFoldLanes;
+    const int j = so_slot(tid);
     const SoSim3 Si = so_inverse(S);
     SoEdgeIn nx{};
     if (j >= 0 && j < me) nx = so_load_edge(C, j);
     double acc = 0.0;
     for (int k = 0; k <= nslab; ++k) {
-        if (j >= 0) {
+        double t[kSim3OptTerms], tc = 0.0;
+        if (j >= 0 && k < nslab) {
             const int pos = k * kSoSlab + j;
-            double* buf = C.terms + (k & 1) * kSoBuf + j;
-            if (k < nslab && pos < me) {
+            if (pos < me) {
                 const SoEdgeIn in = nx;
                 if (pos + kSoSlab < me) nx = so_load_edge(C, pos + kSoSlab);
                 const bool inv_edge = in.side == 1;
@@ -157,22 +173,39 @@ __device__ double so_pass(const SoCtx& C, int mk, const SoSim3& S) {
                 const SoCam& K = inv_edge ? C.K2 : C.K1;
                 double e0, e1;
                 so_edge_error(inv_edge ? Si : S, K, X, u, v, e0, e1);
-                so_st(C.P.err, 2 * in.c + in.side, e0, e1);
-                double tc, r1;
+                double r1;
                 po_huber(po_chi2(inv, false, e0, e1, 0.0), C.delta, C.dsqr, tc, r1);
-                double t[kSim3OptTerms];
-                so_quad_terms(*C.pt, inv_edge, K, X, u, v, inv, e0, e1, C.delta, C.dsqr, t);
-                RSC_UNROLL for (int q = 0; q < kSim3OptTerms; ++q) buf[q * kSoCol] = t[q];
-                buf[kSim3OptTerms * kSoCol] = tc;
-            } else if (k < nslab) {
+                // the perturbed estimates are read from LDS per edge: laundering the pointer keeps the
+                // compiler from hoisting all 28 of them out of the slab loop into VGPRs
+                int z = 0;
+                asm volatile("" : "+v"(z));
+                const SoPerturbed* pt = C.pt + z;
+                so_quad_terms(*pt, inv_edge, K, X, u, v, inv, e0, e1, C.delta, C.dsqr, t);
+            } else {
                 // padding of the last slab: +0.0 terms are exact identities of these folds (an
                 // accumulator that starts at +0.0 never becomes -0.0 under round-to-nearest)
-                RSC_UNROLL for (int q = 0; q < kSoCols; ++q) buf[q * kSoCol] = 0.0;
+                RSC_UNROLL for (int q = 0; q < kSim3OptTerms; ++q) t[q] = 0.0;
+            }
+            if constexpr (!kSoWide) {
+                double* buf = C.terms + (k & 1) * kSoBuf + j;
+                RSC_UNROLL for (int q = 0; q < kSim3OptTerms; ++q) buf[q * kSoCol] = t[q];
+                buf[kSim3OptTerms * kSoCol] = tc;
             }
         } else if (k > 0 && tid < kSoCols) {
-            acc = fold_fixed<kSoSlab>(acc, C.terms + ((k - 1) & 1) * kSoBuf + tid * kSoCol);
+            acc = fold_fixed<kSoSlab>(acc, C.terms + (kSoWide ? 0 : ((k - 1) & 1) * kSoBuf) + tid * kSoCol);
         }
         __syncthreads();
+        if constexpr (kSoWide) {
+            // the fold of slab k - 1 is done: slab k's terms go into the buffer
+            if (k < nslab) {
+                if (j >= 0) {
+                    double* buf = C.terms + j;
+                    RSC_UNROLL for (int q = 0; q < kSim3OptTerms; ++q) buf[q * kSoCol] = t[q];
+                    buf[kSim3OptTerms * kSoCol] = tc;
+                }
+                __syncthreads();
+            }
+        }
     }
     if (tid < kSoCols) C.red[tid] = acc;
     __syncthreads();
@@ -183,6 +216,7 @@ struct SoLM {
     double x[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // BlockSolver::_x persists across optimize() calls
     double lambda = -1.0, ni = 2.0;
     int nBadLM = 0, its = 0, trials = 0;
+    SoSim3 last;  // estimate of the last pass (the edges' _error is evaluated there)
 };
 
 // initializeOptimization() + optimize(iterations) (sparse_optimizer.cpp:354-414) with
@@ -192,6 +226,7 @@ __device__ void so_optimize(const SoCtx& C, SoLM& L, SoSim3& S, int iterations) 
     if (mk == 0) return;
     // the system at S (C.cur: lower triangle row-major, then b) and the chi2 solve() computes there
     double chiS = so_pass(C, mk, S);
+    L.last = S;
     auto adopt = [&]() {  // C.cur = the last pass's system
         if (threadIdx.x < kSim3OptTerms) C.cur[threadIdx.x] = C.red[threadIdx.x];
         __syncthreads();
@@ -229,6 +264,7 @@ __device__ void so_optimize(const SoCtx& C, SoLM& L, SoSim3& S, int iterations) 
             if (ok2) RSC_UNROLL for (int j = 0; j < 7; ++j) L.x[j] = xs[j];
             const SoSim3 trial = so_oplus(L.x, S);
             const double chiT = so_pass(C, mk, trial);
+            L.last = trial;
             const double tempChi = ok2 ? chiT : DBL_MAX;
             rho = (currentChi - tempChi);
             double scale = 0.;
@@ -262,11 +298,14 @@ __device__ void so_optimize(const SoCtx& C, SoLM& L, SoSim3& S, int iterations) 
     }
 }
 
-// chi2 > th2 test of correspondence c on its stored errors (Optimizer.cpp:1184, :1216).
-__device__ __forceinline__ bool so_outlier(const SoCtx& C, int c) {
-    const double2 a = so_ld(C.P.err, 2 * c), b = so_ld(C.P.err, 2 * c + 1);
-    const float4 p = so_ld(C.P.e12, c), q = so_ld(C.P.e21, c);
-    return po_chi2((double)p.w, false, a.x, a.y, 0.0) > C.th2 || po_chi2((double)q.w, false, b.x, b.y, 0.0) > C.th2;
+// chi2 > th2 test of correspondence c (Optimizer.cpp:1184, :1216) on the errors of the last pass:
+// e12 at S, e21 at S^-1 (Sl, Sli), as so_pass evaluated them.
+__device__ __forceinline__ bool so_outlier(const SoCtx& C, int c, const SoSim3& Sl, const SoSim3& Sli) {
+    const float4 p = so_ld(C.P.e12, c), q = so_ld(C.P.e21, c), o = so_ld(C.P.uv, c);
+    double a0, a1, b0, b1;
+    so_edge_error(Sl, C.K1, {(double)p.x, (double)p.y, (double)p.z}, o.x, o.y, a0, a1);
+    so_edge_error(Sli, C.K2, {(double)q.x, (double)q.y, (double)q.z}, o.z, o.w, b0, b1);
+    return po_chi2((double)p.w, false, a0, a1, 0.0) > C.th2 || po_chi2((double)q.w, false, b0, b1, 0.0) > C.th2;
 }
 
 __device__ void so_write(const DevSim3OptProb& P, const SoSim3& S, int nIn, int nBad, const SoLM& L) {
@@ -288,7 +327,7 @@ __global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptPro
     __shared__ int tot_sh;
     const DevSim3OptProb& P = probs[blockIdx.x];
     const int tid = threadIdx.x;
-    SoPerturbed* pt = reinterpret_cast<SoPerturbed*>(so_lds + 2 * kSoBuf);
+    SoPerturbed* pt = reinterpret_cast<SoPerturbed*>(so_lds + kSoBufs * kSoBuf);
     uint16_t* list = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(pt) + kSoPt);
     SoCtx C{P, so_lds, pt, list, red_sh, cur_sh, cnt_sh, {}, {}, 0.0, 0.0, (double)P.th2};
     C.K1 = SoCam{(double)P.K1[0], (double)P.K1[1], (double)P.K1[2], (double)P.K1[3]};
@@ -304,11 +343,13 @@ __global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptPro
     if (tid == 0) tot_sh = 0;
     __syncthreads();
     SoLM L;
+    L.last = S;
     so_optimize(C, L, S, 5);
     // Check inliers (Optimizer.cpp:1176-1194): remove both edges of a failing correspondence
     int bad = 0;
+    SoSim3 Sli = so_inverse(L.last);
     for (int c = tid; c < P.m; c += kSoThreads) {
-        if (so_outlier(C, c)) {
+        if (so_outlier(C, c, L.last, Sli)) {
             so_g(P.keep)[c] = 0;
             ++bad;
         }
@@ -324,9 +365,10 @@ __global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptPro
     if (tid == 0) tot_sh = 0;
     so_optimize(C, L, S, nBad > 0 ? 10 : 5);
     int in = 0;
+    Sli = so_inverse(L.last);
     for (int c = tid; c < P.m; c += kSoThreads) {
         if (!so_g(P.keep)[c]) continue;
-        if (so_outlier(C, c)) so_g(P.keep)[c] = 0;
+        if (so_outlier(C, c, L.last, Sli)) so_g(P.keep)[c] = 0;
         else ++in;
     }
     if (in) atomicAdd(&tot_sh, in);

@@ -398,8 +398,10 @@ void he_pose_optimization(int n, const float* xw4, const float* uv, const float*
             const double X[3] = {xw4[4 * e], xw4[4 * e + 1], xw4[4 * e + 2]};
             const bool st = stereo(e);
             double t[kPoseTerms];
-            po_quad_terms(est, K, X, xw4[4 * e + 3], err[3 * e], err[3 * e + 1], err[3 * e + 2], st, robust,
-                          st ? ds : dm, st ? ds2 : dm2, t);
+            if (!po_quad_terms_finite(est, K, X, xw4[4 * e + 3], err[3 * e], err[3 * e + 1], err[3 * e + 2], st, robust,
+                                      st ? ds : dm, st ? ds2 : dm2, t))
+                po_quad_terms(est, K, X, xw4[4 * e + 3], err[3 * e], err[3 * e + 1], err[3 * e + 2], st, robust,
+                              st ? ds : dm, st ? ds2 : dm2, t);
             const double tc = po_chi_term(robust, st, xw4[4 * e + 3], err[3 * e], err[3 * e + 1], err[3 * e + 2],
                                           st ? ds : dm, st ? ds2 : dm2);
             for (int k = 0; k < kPoseTerms; ++k) acc[k] = acc[k] + ((k >= 21) ? -t[k] : t[k]);
@@ -499,6 +501,44 @@ void he_pose_optimization(int n, const float* xw4, const float* uv, const float*
     }
     const int ints[4] = {n - nBad, rounds, lm_its, lm_trials};
     std::memcpy(out + 12, ints, 16);
+}
+
+// The PoseOptimization folds of n edges at one estimate, with the full po_quad_terms (out[0..27]) and
+// with the kernel's form (po_quad_terms_finite, po_quad_terms for an edge outside its precondition;
+// out[28..55]); flags[e] bit 0 = stereo, bit 1 = robust; pose7 = quaternion (x, y, z, w), t; K5 =
+// fx, fy, cx, cy, bf.  Returns the number of edges that took the full form in the kernel's.
+int he_po_fold_compare(int n, const double* X3, const double* e3, const double* inv, const int32_t* flags,
+                       const double* pose7, const double* K5, double* out) {
+    using namespace rsc;
+    PoSE3 est;
+    est.r.x = pose7[0]; est.r.y = pose7[1]; est.r.z = pose7[2]; est.r.w = pose7[3];
+    for (int i = 0; i < 3; ++i) est.t[i] = pose7[4 + i];
+    const PoCam K{K5[0], K5[1], K5[2], K5[3], K5[4]};
+    const double dm = (double)std::sqrt(5.991f), ds = (double)std::sqrt(7.815f);
+    double a[kPoseTerms], b[kPoseTerms];
+    for (int k = 0; k < kPoseTerms; ++k) a[k] = b[k] = 0.0;
+    int full = 0;
+    for (int e = 0; e < n; ++e) {
+        const double X[3] = {X3[3 * e], X3[3 * e + 1], X3[3 * e + 2]};
+        const bool st = flags[e] & 1, rb = flags[e] & 2;
+        const double delta = st ? ds : dm, dsqr = delta * delta;
+        double t[kPoseTerms], f[kPoseTerms];
+        po_quad_terms(est, K, X, inv[e], e3[3 * e], e3[3 * e + 1], e3[3 * e + 2], st, rb, delta, dsqr, t);
+        if (!po_quad_terms_finite(est, K, X, inv[e], e3[3 * e], e3[3 * e + 1], e3[3 * e + 2], st, rb, delta, dsqr, f)) {
+            po_quad_terms(est, K, X, inv[e], e3[3 * e], e3[3 * e + 1], e3[3 * e + 2], st, rb, delta, dsqr, f);
+            ++full;
+        }
+        for (int k = 0; k < kPoseTerms; ++k) {
+            a[k] = (k >= 21) ? a[k] + (-t[k]) : a[k] + t[k];
+            b[k] = (k >= 21) ? b[k] + (-f[k]) : b[k] + f[k];
+        }
+    }
+    for (int k = 0; k < kPoseTerms; ++k) {
+        out[k] = a[k];
+        out[kPoseTerms + 1 + k] = b[k];
+    }
+    out[kPoseTerms] = out[2 * kPoseTerms + 1] = 0.0;
+    return full;
 }
 
 // OptimizeSim3 in the device orchestration (sim3opt.hip), run sequentially: the same per-edge

@@ -40,6 +40,7 @@ def lib():
         L.he_qr_split.argtypes = [f64p, C.c_int, f64p, i32p, f64p, i32p]
         L.he_optimize_sim3.argtypes = [C.c_int, f32p, f32p, f32p, f32p, C.c_float, f64p, u8p, i32p]
         L.he_poll_until.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.he_po_fold_compare.argtypes = [C.c_int, f64p, f64p, f64p, i32p, f64p, f64p, f64p]
         _lib = L
     return _lib
 
@@ -232,3 +233,15 @@ def optimize_sim3(p):
     keep = np.ones(p.n, np.uint8)
     keep[sel] = keep_c[:m]
     return int(st[0]), S, keep, st
+
+
+def po_fold_compare(X, e, inv, flags, pose7, K5):
+    """PoseOptimization folds over the edges with the full and with the kernel's term form
+    (hostemu he_po_fold_compare): returns (full [28], kernel [28], edges that took the full form)."""
+    n = len(inv)
+    out = np.zeros(56, np.float64)
+    full = lib().he_po_fold_compare(n, np.ascontiguousarray(X, np.float64).reshape(-1),
+                                    np.ascontiguousarray(e, np.float64).reshape(-1),
+                                    np.ascontiguousarray(inv, np.float64), np.ascontiguousarray(flags, np.int32),
+                                    np.ascontiguousarray(pose7, np.float64), np.ascontiguousarray(K5, np.float64), out)
+    return out[:28], out[28:], full

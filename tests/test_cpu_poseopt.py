@@ -153,3 +153,41 @@ def test_golden_regression():
         assert r == g["n_good"][k]
         assert np.array_equal(T.reshape(16).view(np.uint32), g["T"][k].view(np.uint32))
         assert np.array_equal(st, g["stats"][k])
+
+
+def test_zero_product_free_terms_fold_identically():
+    """The kernel's per-edge terms skip the products by the information matrix's zero entries
+    (po_quad_terms_finite): the folded H / b must equal the full form's bit for bit, on edges chosen to
+    make signed zeros (coordinates and errors of exactly +-0, points on the optical axis), on edges
+    whose Jacobian overflows or is not finite (those take the full form), and on ordinary edges."""
+    rng = np.random.default_rng(4242)
+    K5 = np.array([458.654, 457.296, 367.215, 248.375, 47.9], np.float64)
+    q = rng.normal(size=4)
+    q /= np.linalg.norm(q)
+    pose = np.concatenate([q, rng.normal(size=3) * 0.3])
+    ident = np.array([0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0])
+    n = 600
+    X = rng.normal(size=(n, 3)) * [2.0, 1.5, 1.0] + [0.0, 0.0, 5.0]
+    e = rng.normal(size=(n, 3)) * 3.0
+    inv = rng.choice([1.0, 0.694, 0.482, 0.335], n)
+    flags = rng.integers(0, 4, n).astype(np.int32)
+    zero = rng.random(n) < 0.3          # signed zeros in the inputs
+    X[zero, 0] = np.where(rng.random(int(zero.sum())) < 0.5, 0.0, -0.0)
+    X[zero[::-1], 1] = -0.0
+    e[rng.random(n) < 0.2, 0] = -0.0
+    e[rng.random(n) < 0.2, 1] = 0.0
+    e[rng.random(n) < 0.2, 2] = -0.0
+    for pz in (pose, ident):
+        a, b, full = hl.po_fold_compare(X, e, inv, flags, pz, K5)
+        assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), np.nonzero(a.view(np.uint64) != b.view(np.uint64))
+        assert full == 0
+    # an axis point of the identity pose (x = y = 0: exact zero Jacobian entries everywhere)
+    Xa = np.array([[0.0, 0.0, 4.0], [-0.0, 0.0, 3.0], [0.0, -0.0, 2.0]])
+    ea = np.array([[0.0, -0.0, 0.0], [-0.0, -0.0, -0.0], [1.0, -0.0, 0.0]])
+    a, b, full = hl.po_fold_compare(Xa, ea, np.ones(3), np.array([3, 1, 0], np.int32), ident, K5)
+    assert np.array_equal(a.view(np.uint64), b.view(np.uint64)) and full == 0
+    # non-finite and overflowing edges: full form, same bits (NaN payloads included)
+    Xb = np.array([[1.0, 2.0, 0.0], [1e200, 1e200, 1e-200], [1.0, 1.0, 3.0], [1.0, 1.0, 3.0]])
+    eb = np.array([[1.0, 1.0, 1.0], [1.0, 1.0, 1.0], [np.inf, 0.0, 0.0], [np.nan, 1.0, 0.0]])
+    a, b, full = hl.po_fold_compare(Xb, eb, np.ones(4), np.array([3, 3, 3, 1], np.int32), ident, K5)
+    assert np.array_equal(a.view(np.uint64), b.view(np.uint64)) and full == 4

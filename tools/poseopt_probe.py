@@ -18,9 +18,11 @@ for sf in (0.8, 0.0):
     b = engine.PoseOptBatch(ctx, frames)
     for _ in range(5):
         b.run()
-    ph = np.zeros(64 * 8, np.uint64)
+    ph = np.zeros(64 * 24, np.uint64)
     engine._check(engine.load_library().rsc_diag_poseopt_phases(ctx.h, ph, ph.size), "poseopt phases")
-    ph = ph.reshape(64, 8).astype(np.float64)
+    hw = ph.reshape(64, 24)[:, 8:16].astype(np.int64)
+    fold = ph.reshape(64, 24)[:, 16:18].astype(np.float64)
+    ph = ph.reshape(64, 24)[:, :8].astype(np.float64)
     npass = (ph[:, 1].astype(np.uint64) & np.uint64(0xFFFFFF)).astype(np.float64)
     summ = (ph[:, 1].astype(np.uint64) >> np.uint64(24)).astype(np.float64)
     ph /= 100.0  # us
@@ -41,4 +43,16 @@ for sf in (0.8, 0.0):
           f"(max {ph[:, 3].max():.1f}); passes {ph[:, 0].mean():.1f} us = {npass.mean():.1f} x "
           f"{(ph[:, 0] / npass).mean():.2f} (active edges per pass {(summ / npass).mean():.0f}: "
           f"{(ph[:, 0] / summ).mean() * 1e3:.2f} ns per edge); LM iterations {its:.1f}, trials {trials:.1f}; re-classification "
-          f"{ph[:, 2].mean():.1f}; rest {(ph[:, 3] - ph[:, 0] - ph[:, 2]).mean():.1f}")
+          f"{ph[:, 2].mean():.1f}; LM solves {ph[:, 4].mean():.1f}; rest {(ph[:, 3] - ph[:, 0] - ph[:, 2] - ph[:, 4]).mean():.1f}")
+    if hw.any():
+        simd = (hw >> 4) & 3
+        cu = (hw >> 8) & 15
+        print("    SIMD of waves 0..7, frames 0-3: " + "; ".join(" ".join(str(int(v)) for v in simd[f]) for f in range(4))
+              + f"  (CU ids {sorted(set(cu[:4, 0].tolist()))})")
+    if fold[:, 1].any():
+        print(f"    wave-0 folds: {(fold[:, 0] / fold[:, 1]).mean() * 10:.0f} ns per fold of a slab, "
+              f"{fold[:, 0].mean() / 100:.1f} us per frame ({fold[:, 1].mean():.0f} folds)")
+    nsl = ph[:, 7] * 100.0  # slab count (undo the us scaling)
+    if nsl.any():
+        print(f"    wave-1 slab phases: to the errors {(ph[:, 5] / nsl).mean() * 1e3:.0f} ns, errors -> terms stored "
+              f"{(ph[:, 6] / nsl).mean() * 1e3:.0f} ns per slab ({nsl.mean():.0f} slabs per frame)")
