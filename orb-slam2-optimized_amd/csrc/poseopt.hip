@@ -315,7 +315,7 @@ __device__ __forceinline__ void po_adopt(const PoseLds& S) {
 // (thread 0); [4] the LM trials' solve (LDLT + exp + product, thread 0); [5] / [6] wave 1's slab time
 // up to the edges' errors / from there to the terms stored, [7] its slab count; [8 + w] the HW_ID
 // register of wave w (which SIMD each wave of the workgroup landed on); [16] / [17] wave 0's folding
-// time and fold count.
+// time and fold count; [18] the LDLT part of [4].
 __device__ uint64_t g_po_phase[64][24];
 
 __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb* __restrict__ probs) {
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
     if (tid == 0) po_put(init_sh, po_from_Rt(R0, t0));
     auto init = [&]() { return po_get(init_sh); };
     const bool clk = kPosePhases && blockIdx.x < 64 && tid == 0;
-    uint64_t ph_pass = 0, n_pass = 0, ph_cls = 0, ph_solve = 0, t_start = clk ? wall_clock64() : 0;
+    uint64_t ph_pass = 0, n_pass = 0, ph_cls = 0, ph_solve = 0, ph_ldlt = 0, t_start = clk ? wall_clock64() : 0;
     uint64_t ps[6] = {0, 0, 0, 0, 0, 0};  // wave 1's slab and wave 0's fold clocks (po_pass)
     for (int e = tid; e < n; e += kPoseThreads) {
         S.lvl[e] = 0;
@@ -411,8 +411,13 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
                     double xs[6];
                     const bool ok2 = po_ldlt_solve6(Hd, b, xs);
                     if (ok2) RSC_UNROLL for (int j = 0; j < 6; ++j) x[j] = xs[j];
+                    if (clk) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        ph_ldlt += wall_clock64() - ts + (uint64_t)(x[0] != x[0]);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                     const PoSE3 trial = po_mul(po_exp(x), est);
-                    tp = clk ? wall_clock64() : 0;
+                    tp = clk ? wall_clock64() + (uint64_t)(trial.t[0] != trial.t[0]) : 0;
                     if (clk) ph_solve += tp - ts;
                     const double chiT = po_pass(P, S, m, first, trial, K, robust, hk, ps);
                     if (tid == 0) po_put(last_sh, trial);  // read after this pass's barriers
@@ -490,6 +495,7 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
         g_po_phase[blockIdx.x][4] = ph_solve;
         g_po_phase[blockIdx.x][16] = ps[3];
         g_po_phase[blockIdx.x][17] = ps[4];
+        g_po_phase[blockIdx.x][18] = ph_ldlt;
     }
     if (kPosePhases && blockIdx.x < 64 && tid == kPoseFoldLanes) {
         g_po_phase[blockIdx.x][5] = ps[0];
