@@ -75,7 +75,9 @@ int rsc_context_set_eig_split(rsc_context* ctx, int on);
  * (A[6][4] row-major, b[6], previous X[4]) -> X in out[0..3], 1/0 success in out[4] of each record
  * (n a multiple of 34); 11 pow(x, 1.0/3.0), 12 pow(x, 3.0/2.0) as MLPnP computes them (x >= 0;
  * MLPnPsolver.cpp:567, :839, :901); 13 the PnP scan's float reciprocal of (float)x (v_rcp_f32 + one
- * Newton step, PnPsolver.cpp:251).  Host pointers, n >= 0.  Tests compare with glibc / IEEE numpy / the oracle. */
+ * Newton step, PnPsolver.cpp:251); (14, 15 unused); 16 the LM steps' 6 x 6 LDLT solve in its scalar and row-per-lane forms
+ * (records of 42: matrix row-major + b in, x / ok of each form out; n a multiple of 42).  Host
+ * pointers, n >= 0.  Tests compare with glibc / IEEE numpy / the oracle. */
 int rsc_selftest_math(rsc_context* ctx, int fn, const double* x, int n, double* out);
 
 /* ---- PnPsolver (include/PnPsolver.hpp:21-138, src/PnPsolver.cpp) ------------------------------ */
@@ -555,6 +557,10 @@ int rsc_diag_mlpnp_phase_stamps(rsc_context* ctx, uint64_t* out, int cap);
  * terms) and its slab count.  cap >= 64 * 24 returns [frame][24]: columns 8..15 = the HW_ID register
  * of waves 0..7 (SIMD in bits 5:4, CU in 11:8), 16 / 17 = wave 0's folding ticks and fold count. */
 int rsc_diag_poseopt_phases(rsc_context* ctx, uint64_t* out, int cap);
+/* Diagnostic: wall-clock (100 MHz) ticks of the last OptimizeSim3 launch (built with RSC_SO_PHASES=1),
+ * [pair < 64][8]: passes, pass count, perturbed-estimate builds, LM solves, wave 1's edge evaluation
+ * and its slab count, wave 0's folds, whole kernel.  cap >= 64 * 8. */
+int rsc_diag_sim3opt_phases(rsc_context* ctx, uint64_t* out, int cap);
 /* Diagnostic: wall clock (100 MHz) of KeyFrameDatabase slots 0..4095 in the last count launch,
  * [slot][4] = entry, staged, counted, exit (zeros unless built with RSC_KFDB_STAMPS=1). */
 int rsc_diag_kfdb_stamps(rsc_context* ctx, uint64_t* out, int cap);

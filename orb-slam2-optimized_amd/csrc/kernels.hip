@@ -1182,6 +1182,7 @@ __global__ __launch_bounds__(256) void selftest_math_kernel(int fn, const double
             r = (double)__builtin_fmaf(__builtin_fmaf(-z, r0, 1.0f), r0, r0);
             break;
         }
+
         default: {
             double c, s;
             make_givens(v, x[(i + n / 2) % n], c, s);

@@ -26,6 +26,7 @@
 #include "rsc_poseopt.h"
 #include "rsc_kernels.h"
 #include "rsc_fold.h"
+#include "rsc_quad.h"  // split_wait (bounded hand-off waits, fault word)
 
 namespace rsc {
 
@@ -44,32 +45,61 @@ constexpr bool kPosePhases = RSC_POSE_PHASES;
 #define RSC_PO_DIAG 0
 #endif
 
-// Pass form.  0 (default): wave 0 folds and RSC_PO_EDGE_WAVES waves (3: 256 threads, slabs of 192; 4: 320 threads, slabs of 256, the fourth edge wave beside the
-// fold on SIMD 0 — the older fold wave issues first) evaluate the edges into double-buffered slabs.
-// 1 (wide): 512 threads, two waves per SIMD, seven edge waves (RSC_PO_IDLE = w leaves wave w out),
-// slabs of 448 into a single buffer (two do not fit in LDS beside the active list): a slab's terms
-// wait in VGPRs for the previous slab's fold and are stored between two barriers.  Measured
-// (profiles/r06/poseopt_probe_s6l.txt): the edge evaluation is issue-bound (about 380 VALU
-// instructions per edge) and two waves per SIMD only share the issue; 192-edge slabs 13.7 us per pass
-// of 1,494 edges, 448-edge slabs 14.1, 384 with an idle wave 14.4.
+// Pass form.
+// RSC_PO_STREAM = 1: a streamed pass.  Wave 0 folds; RSC_PO_STREAM_WAVES edge waves take
+// 64-edge chunks from an LDS counter (the next chunk's inputs loaded while the current one is
+// evaluated), write a chunk's terms into its slab's slot of a two-slot ring (256 edges per slab) once
+// the fold has released that slot, and count it in; the fold wave folds a slab as soon as its four
+// chunks are in and releases the slot.  No workgroup barrier per slab: an edge wave that is ahead
+// keeps evaluating, a slower one (the one beside the fold on SIMD 0) takes fewer chunks, and the
+// fold never waits on the slowest wave of a tick.  Every wait is bounded (split_wait: on give-up
+// the launch's fault word is raised and the host returns an error).  Measured no faster
+// (profiles/r06/poseopt_probe_s6n/s6o/s6p.txt: 12.9-13.7 us per pass of 1,494 edges against 13.0 for
+// the ticked form): the fold waits 4.7 us per pass, 2 of them for the first slab, while the edge
+// waves wait 3 us for free slots — a two-slot ring behind per-wave queues of three chunks blocks at
+// the head of the line; kept as an option (its parity tests pass, gpu_tests_lm_s6n.txt).
+// RSC_PO_STREAM = 0 (default): barrier-ticked slabs — RSC_PO_WIDE = 0: RSC_PO_EDGE_WAVES (3 or 4) edge waves,
+// double-buffered slabs of 64 x that; RSC_PO_WIDE = 1: 512 threads, seven edge waves (RSC_PO_IDLE = w
+// leaves wave w out), slabs of 448 into a single buffer, a slab's terms held in VGPRs until the
+// previous slab's fold is done.  Measured (profiles/r06/poseopt_probe_s6l.txt, s6m): the edge
+// evaluation is issue-bound (about 380 VALU instructions per edge); per pass of 1,494 edges 13.7 us
+// with 3 edge waves, 12.9 with 4, 14.1 wide (448), 14.4 wide with an idle wave.
+#ifndef RSC_PO_STREAM
+#define RSC_PO_STREAM 0
+#endif
+#ifndef RSC_PO_STREAM_WAVES
+#define RSC_PO_STREAM_WAVES 7
+#endif
 #ifndef RSC_PO_WIDE
 #define RSC_PO_WIDE 0
 #endif
 #ifndef RSC_PO_EDGE_WAVES
 #define RSC_PO_EDGE_WAVES 4
 #endif
-constexpr bool kPoseWide = RSC_PO_WIDE != 0;
+constexpr bool kPoseStream = RSC_PO_STREAM != 0;
+// the LM trials' LDLT with one matrix row per lane (rsc_poseopt.h po_ldlt_solve_lanes): measured
+// slower than the scalar form (profiles/r06/poseopt_probe_s6t.txt: 118 vs 107 us of LDLT per stereo
+// Frame; sim3opt_probe_s6t.txt: 47.8 vs 42.7 us of LM solves per pair) — the factorization is a
+// latency chain and the lane form adds a v_readlane round trip to every link; off
+#ifndef RSC_LM_LDLT_LANES
+#define RSC_LM_LDLT_LANES 0
+#endif
+constexpr bool kLdltLanes = RSC_LM_LDLT_LANES != 0;
+constexpr bool kPoseWide = !kPoseStream && RSC_PO_WIDE != 0;
 // the wide form's idle wave (0: none): waves w and w + 4 of a workgroup land on one SIMD
 // (profiles/r06/poseopt_probe_s6j.txt), so wave 4 shares the fold wave's SIMD
 #ifndef RSC_PO_IDLE
 #define RSC_PO_IDLE 0
 #endif
 static_assert(RSC_PO_IDLE >= 0 && RSC_PO_IDLE <= 7, "idle wave");
-static_assert(RSC_PO_EDGE_WAVES == 3 || RSC_PO_EDGE_WAVES == 4, "edge waves of the default form");
-constexpr int kPoseEdgeWaves = kPoseWide ? (RSC_PO_IDLE ? 6 : 7) : RSC_PO_EDGE_WAVES;
+static_assert(RSC_PO_EDGE_WAVES == 3 || RSC_PO_EDGE_WAVES == 4, "edge waves of the ticked form");
+static_assert(RSC_PO_STREAM_WAVES >= 1 && RSC_PO_STREAM_WAVES <= 7, "edge waves of the streamed form");
+constexpr int kPoseEdgeWaves =
+    kPoseStream ? RSC_PO_STREAM_WAVES : (kPoseWide ? (RSC_PO_IDLE ? 6 : 7) : RSC_PO_EDGE_WAVES);
 constexpr int kPoseThreads = kPoseWide ? 512 : 64 * (1 + kPoseEdgeWaves);
+constexpr int kPoseChunks = 4;  // 64-edge chunks per slab of the streamed form
 constexpr int kPoseFoldLanes = 64;                // wave 0 folds
-constexpr int kPoseSlab = 64 * kPoseEdgeWaves;   // active edges per slab
+constexpr int kPoseSlab = kPoseStream ? 64 * kPoseChunks : 64 * kPoseEdgeWaves;  // active edges per slab
 constexpr int kPoseBufs = kPoseWide ? 1 : 2;
 constexpr int kPoseCol = kPoseSlab + 2;           // padded column stride (doubles): 16 B bank shift per column
 constexpr int kPoseCols = kPoseTerms + 1;         // 27 H/b columns + the chi2 column
@@ -98,6 +128,8 @@ struct PoseLds {
     double* cur;     // [32] the LM's current system (a copy of an adopted pass's red)
     int* scan;       // [kPoseThreads / 64] wave totals
     int* nbad;
+    int* ctl;        // streamed pass: [0] next chunk, [1 + s] chunks stored in slot s, [3] slabs folded,
+                     // [4] a wait gave up
 };
 
 // The problem's arrays as global-address-space pointers: accessed through them the compiler issues
@@ -212,13 +244,37 @@ __device__ __forceinline__ PoEdgeIn po_first(const DevPoseProb& P, const PoseLds
     return f;
 }
 
+// The streamed pass's first two chunks of edge wave w (chunks w - 1 and w - 1 + E, E edge waves),
+// loaded once per round and kept in VGPRs: a pass starts evaluating at once instead of after a
+// global-load round trip (measured 3.1 us from pass start to the first slab when they were loaded
+// per pass, profiles/r06/poseopt_probe_s6o.txt).
+struct PoFirst2 {
+    PoEdgeIn a, b;
+};
+__device__ __forceinline__ PoEdgeIn po_chunk_load(const DevPoseProb& P, const PoseLds& S, int m, int c) {
+    const int lane = threadIdx.x & 63;
+    const int pos = (c / kPoseChunks) * kPoseSlab + (c % kPoseChunks) * 64 + lane;
+    PoEdgeIn in{};
+    if (pos < m) in = po_load(P, S.list[pos]);
+    return in;
+}
+__device__ __forceinline__ PoFirst2 po_first_stream(const DevPoseProb& P, const PoseLds& S, int m) {
+    const int w = threadIdx.x >> 6;
+    PoFirst2 f{};
+    if (w > 0) {
+        f.a = po_chunk_load(P, S, m, w - 1);
+        f.b = po_chunk_load(P, S, m, w - 1 + kPoseEdgeWaves);
+    }
+    return f;
+}
+
 // One pass at `est` over the m active edges: computeActiveErrors, activeRobustChi2
 // (sparse_optimizer.cpp:61-114) and BlockSolver::buildSystem (block_solver.hpp:502-560: H lower
 // triangle added, b subtracted, both from 0.0), every sum folded in edge order; the folded sums are
 // left in S.red (returns chi2).  `first` = the inputs of the lane's edge in the first slab, loaded
 // once per round (po_first).
 __device__ double po_pass(const DevPoseProb& P, const PoseLds& S, int m, const PoEdgeIn& first, const PoSE3& est,
-                          const PoCam& K, bool robust, const PoKernels& hk, uint64_t (&ps)[6]) {
+                          const PoCam& K, bool robust, const PoKernels& hk, uint64_t (&ps)[9]) {
     const int tid = threadIdx.x;
     const int nslab = (m + kPoseSlab - 1) / kPoseSlab;
     const int j = po_slot(tid);
@@ -302,6 +358,119 @@ __device__ double po_pass(const DevPoseProb& P, const PoseLds& S, int m, const P
     // S.red is next written after the next pass's slab barriers, by which time every thread has read it
 }
 
+// The streamed pass (RSC_PO_STREAM): the same sums as po_pass, folded in the same edge order (a
+// slab's chunks land at their edge positions, so fold_fixed reads exactly po_pass's columns).
+__device__ double po_pass_stream(const DevPoseProb& P, const PoseLds& S, int m, const PoFirst2& first,
+                                 const PoSE3& est, const PoCam& K, bool robust, const PoKernels& hk, unsigned* fault,
+                                 uint64_t (&ps)[9]) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nslab = (m + kPoseSlab - 1) / kPoseSlab;
+    const int nchunks = nslab * kPoseChunks;
+    int* const ctl = S.ctl;
+    if (tid < 5) ctl[tid] = tid == 0 ? 2 * kPoseEdgeWaves : 0;  // chunks 0 .. 2E - 1 are dealt statically
+    __syncthreads();
+    // a wait that gives up raises the fault word and ctl[4]: every later wait of the launch's
+    // workgroup returns at once, so a broken hand-off ends the kernel after one time-out per wave
+    auto wait_for = [ctl, fault](int* flag, int need) {
+        if (__hip_atomic_load(ctl + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
+        const int v = split_wait(flag, fault, [need](int x) { return x >= need; });
+        if (v < need) __hip_atomic_store(ctl + 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    double acc = 0.0;
+    if (w == 0) {
+        const bool fclk = kPosePhases && tid == 0;
+        const uint64_t p0 = fclk ? wall_clock64() : 0;
+        for (int k = 0; k < nslab; ++k) {
+            const uint64_t wt0 = fclk ? wall_clock64() : 0;
+            wait_for(ctl + 1 + (k & 1), kPoseChunks * ((k >> 1) + 1));  // slot k & 1 holds slab k
+            const uint64_t f0 = fclk ? wall_clock64() : 0;
+            if (fclk) {  // [5] the fold's waits, [7] pass start -> first slab in
+                ps[5] += f0 - wt0;
+                if (k == 0) ps[7] += f0 - p0;
+            }
+            if (lane < kPoseCols) {
+                if constexpr (RSC_PO_DIAG != 2) acc = fold_fixed<kPoseSlab>(acc, S.terms + (k & 1) * kPoseBuf + lane * kPoseCol);
+            }
+            if (fclk) {
+                __builtin_amdgcn_sched_barrier(0);
+                ps[3] += wall_clock64() - f0 + (uint64_t)(acc != acc);
+                ps[4] += 1;
+            }
+            // the slot's reads are complete (release): slab k + 2 may overwrite it
+            if (lane == 0) __hip_atomic_store(ctl + 3, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    } else {
+        auto grab = [&]() {
+            int c = 0;
+            if (lane == 0) c = __hip_atomic_fetch_add(ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return __builtin_amdgcn_readfirstlane(c);
+        };
+        auto edge_pos = [&](int c) { return (c / kPoseChunks) * kPoseSlab + (c % kPoseChunks) * 64 + lane; };
+        // the wave's chunks in increasing order: two dealt statically (inputs in VGPRs since the round
+        // began), then grabbed ones, each loaded two chunks ahead of its evaluation
+        int c = w - 1, cn = w - 1 + kPoseEdgeWaves;
+        PoEdgeIn in_c = first.a, in_n = first.b;
+        while (c < nchunks) {
+            const int cnn = grab();
+            PoEdgeIn in_nn{};
+            if (cnn < nchunks) in_nn = po_chunk_load(P, S, m, cnn);
+            const PoEdgeIn in = in_c;
+            in_c = in_n;
+            in_n = in_nn;
+            const int k = c / kPoseChunks, pos = edge_pos(c);
+            // phase clocks of wave 1 (lane 0): [0] chunk start -> error, [1] error -> terms
+            const bool pclk = kPosePhases && tid == kPoseFoldLanes;
+            uint64_t c0 = pclk ? wall_clock64() : 0;
+            double t[kPoseTerms], tc = 0.0;
+            if (pos < m) {
+                const bool st = in.ur >= 0.0f;
+                const double X[3] = {(double)in.xw.x, (double)in.xw.y, (double)in.xw.z};
+                if constexpr (RSC_PO_DIAG == 1) {
+                    RSC_UNROLL for (int q = 0; q < kPoseTerms; ++q) t[q] = X[q % 3] * 1e-30;
+                    tc = X[0] * 1e-30;
+                } else {
+                    double e0, e1, e2;
+                    po_error(est, K, X, (double)in.uv.x, (double)in.uv.y, st ? (double)in.ur : 0.0, st, e0, e1, e2);
+                    if (pclk) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        const uint64_t c1 = wall_clock64() + (uint64_t)(e0 != e0) + (uint64_t)(e2 != e2);
+                        ps[0] += c1 - c0;
+                        c0 = c1;
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    const double delta = st ? hk.ds : hk.dm, dsqr = st ? hk.ds2 : hk.dm2;
+                    if (!po_quad_terms_finite(est, K, X, (double)in.xw.w, e0, e1, e2, st, robust, delta, dsqr, t))
+                        po_quad_terms(est, K, X, (double)in.xw.w, e0, e1, e2, st, robust, delta, dsqr, t);
+                    tc = po_chi_term(robust, st, (double)in.xw.w, e0, e1, e2, delta, dsqr);
+                }
+                RSC_UNROLL for (int q = 21; q < kPoseTerms; ++q) t[q] = -t[q];
+            } else {
+                // padding of the last slab: +0.0 terms are exact identities of these folds
+                RSC_UNROLL for (int q = 0; q < kPoseTerms; ++q) t[q] = 0.0;
+            }
+            if (pclk) {
+                __builtin_amdgcn_sched_barrier(0);
+                ps[1] += wall_clock64() - c0 + (uint64_t)(t[0] != t[0]);
+                ps[2] += 1;
+            }
+            // slot k & 1 held slab k - 2: it is free once the fold has passed slab k - 2
+            const uint64_t ws = pclk ? wall_clock64() : 0;
+            wait_for(ctl + 3, k - 1);
+            if (pclk) ps[6] += wall_clock64() - ws;  // [6] wave 1's slot waits
+            double* buf = S.terms + (k & 1) * kPoseBuf + (c % kPoseChunks) * 64 + lane;
+            RSC_UNROLL for (int q = 0; q < kPoseTerms; ++q) buf[q * kPoseCol] = t[q];
+            buf[kPoseTerms * kPoseCol] = tc;
+            // count the chunk in (release: the wave's stores above complete first)
+            if (lane == 0) __hip_atomic_fetch_add(ctl + 1 + (k & 1), 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            c = cn;
+            cn = cnn;
+        }
+    }
+    if (tid < kPoseCols) S.red[tid] = acc;
+    __syncthreads();
+    return S.red[kPoseTerms];
+}
+
 // S.cur = S.red (the LM adopts the last pass's system); every thread reads S.cur after the barrier.
 __device__ __forceinline__ void po_adopt(const PoseLds& S) {
     if (threadIdx.x < kPoseCols) S.cur[threadIdx.x] = S.red[threadIdx.x];
@@ -315,17 +484,19 @@ __device__ __forceinline__ void po_adopt(const PoseLds& S) {
 // (thread 0); [4] the LM trials' solve (LDLT + exp + product, thread 0); [5] / [6] wave 1's slab time
 // up to the edges' errors / from there to the terms stored, [7] its slab count; [8 + w] the HW_ID
 // register of wave w (which SIMD each wave of the workgroup landed on); [16] / [17] wave 0's folding
-// time and fold count; [18] the LDLT part of [4].
+// time and fold count; [18] the LDLT part of [4]; streamed pass: [19] the fold wave's waits for
+// chunks, [20] wave 1's waits for a free slot, [21] pass start to the first slab in.
 __device__ uint64_t g_po_phase[64][24];
 
-__global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb* __restrict__ probs) {
+__global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb* __restrict__ probs, unsigned* fault) {
     extern __shared__ __attribute__((aligned(16))) double po_lds[];
     __shared__ double red_sh[32], cur_sh[32];
     __shared__ int scan_sh[kPoseThreads / 64];
     __shared__ int nbad_sh;
+    __shared__ int ctl_sh[5];
     const PoseLds S{po_lds, reinterpret_cast<uint16_t*>(po_lds + kPoseBufs * kPoseBuf),
                     reinterpret_cast<uint8_t*>(po_lds + kPoseBufs * kPoseBuf) + sizeof(uint16_t) * kPoseMaxEdges,
-                    red_sh, cur_sh, scan_sh, &nbad_sh};
+                    red_sh, cur_sh, scan_sh, &nbad_sh, ctl_sh};
     const DevPoseProb& P = probs[blockIdx.x];
     const int tid = threadIdx.x, n = P.n;
     const PoCam K{(double)P.fx, (double)P.fy, (double)P.cx, (double)P.cy, (double)P.bf};
@@ -349,7 +520,7 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
     auto init = [&]() { return po_get(init_sh); };
     const bool clk = kPosePhases && blockIdx.x < 64 && tid == 0;
     uint64_t ph_pass = 0, n_pass = 0, ph_cls = 0, ph_solve = 0, ph_ldlt = 0, t_start = clk ? wall_clock64() : 0;
-    uint64_t ps[6] = {0, 0, 0, 0, 0, 0};  // wave 1's slab and wave 0's fold clocks (po_pass)
+    uint64_t ps[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // wave 1's slab and wave 0's fold clocks (po_pass)
     for (int e = tid; e < n; e += kPoseThreads) {
         S.lvl[e] = 0;
         po_g(P.outlier)[e] = 0;
@@ -375,10 +546,12 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
         if (tid == 0) po_put(last_sh, est);  // read after the round's barriers
         const int m = po_list_active(S, n);
         if (m > 0) {
-            const PoEdgeIn first = po_first(P, S, m);
+            const PoEdgeIn first = kPoseStream ? PoEdgeIn{} : po_first(P, S, m);
+            const PoFirst2 first2 = kPoseStream ? po_first_stream(P, S, m) : PoFirst2{};
             // the system at est (S.cur) and the chi2 solve() computes there
             uint64_t tp = clk ? wall_clock64() : 0;
-            double chiEst = po_pass(P, S, m, first, est, K, robust, hk, ps);
+            double chiEst = kPoseStream ? po_pass_stream(P, S, m, first2, est, K, robust, hk, fault, ps)
+                                        : po_pass(P, S, m, first, est, K, robust, hk, ps);
             if (clk) { ph_pass += wall_clock64() - tp; n_pass += 1 + ((uint64_t)m << 24); }
             po_adopt(S);
             bool ok = true;
@@ -401,15 +574,25 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
                 do {
                     lm_trials++;
                     const uint64_t ts = clk ? wall_clock64() : 0;
-                    double Hd[6][6], b[6];
-                    RSC_UNROLL for (int r = 0; r < 6; ++r) {
+                    double b[6], xs[6];
+                    RSC_UNROLL for (int r = 0; r < 6; ++r) b[r] = S.cur[21 + r];
+                    bool ok2;
+                    if constexpr (kLdltLanes) {
+                        // this lane's row of H + lambda I (rows 0..5 on lanes 0..5)
+                        const int lr = min((int)(tid & 63), 5);
+                        double row[6];
                         RSC_UNROLL for (int c = 0; c < 6; ++c)
-                            Hd[r][c] = r >= c ? S.cur[r * (r + 1) / 2 + c] : S.cur[c * (c + 1) / 2 + r];
-                        b[r] = S.cur[21 + r];
+                            row[c] = lr >= c ? S.cur[lr * (lr + 1) / 2 + c] : S.cur[c * (c + 1) / 2 + lr];
+                        RSC_UNROLL for (int c = 0; c < 6; ++c) row[c] = (c == lr) ? row[c] + lambda : row[c];
+                        ok2 = po_ldlt_solve_lanes<6>(row, b, xs);
+                    } else {
+                        double Hd[6][6];
+                        RSC_UNROLL for (int r = 0; r < 6; ++r)
+                            RSC_UNROLL for (int c = 0; c < 6; ++c)
+                                Hd[r][c] = r >= c ? S.cur[r * (r + 1) / 2 + c] : S.cur[c * (c + 1) / 2 + r];
+                        RSC_UNROLL for (int r = 0; r < 6; ++r) Hd[r][r] += lambda;
+                        ok2 = po_ldlt_solve6(Hd, b, xs);
                     }
-                    RSC_UNROLL for (int r = 0; r < 6; ++r) Hd[r][r] += lambda;
-                    double xs[6];
-                    const bool ok2 = po_ldlt_solve6(Hd, b, xs);
                     if (ok2) RSC_UNROLL for (int j = 0; j < 6; ++j) x[j] = xs[j];
                     if (clk) {
                         __builtin_amdgcn_sched_barrier(0);
@@ -419,7 +602,8 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
                     const PoSE3 trial = po_mul(po_exp(x), est);
                     tp = clk ? wall_clock64() + (uint64_t)(trial.t[0] != trial.t[0]) : 0;
                     if (clk) ph_solve += tp - ts;
-                    const double chiT = po_pass(P, S, m, first, trial, K, robust, hk, ps);
+                    const double chiT = kPoseStream ? po_pass_stream(P, S, m, first2, trial, K, robust, hk, fault, ps)
+                                                    : po_pass(P, S, m, first, trial, K, robust, hk, ps);
                     if (tid == 0) po_put(last_sh, trial);  // read after this pass's barriers
                     if (clk) { ph_pass += wall_clock64() - tp; n_pass += 1 + ((uint64_t)m << 24); }
                     const double tempChi = ok2 ? chiT : DBL_MAX;
@@ -496,11 +680,14 @@ __global__ __launch_bounds__(kPoseThreads) void poseopt_kernel(const DevPoseProb
         g_po_phase[blockIdx.x][16] = ps[3];
         g_po_phase[blockIdx.x][17] = ps[4];
         g_po_phase[blockIdx.x][18] = ph_ldlt;
+        g_po_phase[blockIdx.x][19] = ps[5];
+        g_po_phase[blockIdx.x][21] = ps[7];
     }
     if (kPosePhases && blockIdx.x < 64 && tid == kPoseFoldLanes) {
         g_po_phase[blockIdx.x][5] = ps[0];
         g_po_phase[blockIdx.x][6] = ps[1];
         g_po_phase[blockIdx.x][7] = ps[2];
+        g_po_phase[blockIdx.x][20] = ps[6];
     }
 }
 
@@ -513,7 +700,35 @@ hipError_t read_poseopt_phases(uint64_t* out, bool wide) {
     return hipSuccess;
 }
 
-hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st) {
+__global__ __launch_bounds__(64) void selftest_ldlt_kernel(const double* __restrict__ x, double* __restrict__ out) {
+    const double* rec = x + 42 * (size_t)blockIdx.x;
+    double* o = out + 42 * (size_t)blockIdx.x;
+    const int lane = threadIdx.x, r = lane < 6 ? lane : 5;
+    double A[6][6], b[6], xs[6] = {0, 0, 0, 0, 0, 0}, xl[6] = {0, 0, 0, 0, 0, 0}, row[6];
+    RSC_UNROLL for (int i = 0; i < 6; ++i) {
+        RSC_UNROLL for (int j = 0; j < 6; ++j) A[i][j] = rec[6 * i + j];
+        b[i] = rec[36 + i];
+    }
+    RSC_UNROLL for (int c = 0; c < 6; ++c) row[c] = rec[6 * r + c];
+    const bool oks = po_ldlt_solve<6>(A, b, xs);
+    const bool okl = po_ldlt_solve_lanes<6>(row, b, xl);
+    if (lane == 0) {
+        RSC_UNROLL for (int i = 0; i < 6; ++i) {
+            o[i] = xs[i];
+            o[7 + i] = xl[i];
+        }
+        o[6] = oks ? 1.0 : 0.0;
+        o[13] = okl ? 1.0 : 0.0;
+        for (int i = 14; i < 42; ++i) o[i] = 0.0;
+    }
+}
+
+hipError_t launch_selftest_ldlt(const double* x, int nrec, double* out, hipStream_t st) {
+    if (nrec > 0) selftest_ldlt_kernel<<<nrec, 64, 0, st>>>(x, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_poseopt(int count, const DevPoseProb* probs, unsigned* fault, hipStream_t st) {
     // the dynamic-LDS size above 64 KB needs the per-device function attribute: raised lazily at
     // this kernel's first launch on each device, so only callers of this path depend on it
     static std::atomic<unsigned long long> raised{0};
@@ -526,7 +741,7 @@ hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st) {
             return e;
         raised.fetch_or(1ull << dev, std::memory_order_acq_rel);
     }
-    poseopt_kernel<<<count, kPoseThreads, kPoseLds, st>>>(probs);
+    poseopt_kernel<<<count, kPoseThreads, kPoseLds, st>>>(probs, fault);
     return hipGetLastError();
 }
 

@@ -400,7 +400,8 @@ int stream_wait(rsc_context* C) {
 int take_fault(rsc_context* C) {
     if (__atomic_load_n(C->h_flag + kFaultWord, __ATOMIC_ACQUIRE) == 0) return 0;
     __atomic_store_n(C->h_flag + kFaultWord, 0u, __ATOMIC_RELEASE);
-    g_last_error = "eigen stage: a chase / row-wave hand-off timed out (split_wait); results discarded";
+    g_last_error = "a device hand-off wait timed out (split_wait: eigen stage chase / row wave, or a streamed "
+                   "PoseOptimization pass); results discarded";
     return RSC_ERR_INTERNAL;
 }
 
@@ -1332,14 +1333,17 @@ int rsc_context_set_eig_split(rsc_context* C, int on) {
 }
 
 int rsc_selftest_math(rsc_context* C, int fn, const double* x, int n, double* out) {
-    if (!C || fn < 0 || fn > 13 || n < 0 || (n > 0 && (!x || !out)) || (fn == 10 && n % 34)) return RSC_ERR_ARG;
+    if (!C || fn < 0 || fn > 16 || fn == 14 || fn == 15 || n < 0 || (n > 0 && (!x || !out)) || (fn == 10 && n % 34) ||
+        (fn == 16 && n % 42))
+        return RSC_ERR_ARG;
     if (n == 0) return RSC_OK;
     RSC_HIP(hipSetDevice(C->device));
     double* d = nullptr;
     RSC_HIP(hipMalloc(&d, (size_t)n * 16));
     std::unique_ptr<double, void (*)(double*)> hold(d, [](double* p) { (void)hipFree(p); });
     RSC_HIP(hipMemcpyAsync(d, x, (size_t)n * 8, hipMemcpyHostToDevice, C->stream));
-    RSC_HIP(launch_selftest_math(fn, d, n, d + n, C->stream));
+    if (fn == 16) RSC_HIP(launch_selftest_ldlt(d, n / 42, d + n, C->stream));
+    else RSC_HIP(launch_selftest_math(fn, d, n, d + n, C->stream));
     RSC_HIP(hipMemcpyAsync(out, d + n, (size_t)n * 8, hipMemcpyDeviceToHost, C->stream));
     RSC_HIP(hipStreamSynchronize(C->stream));
     return RSC_OK;
@@ -1767,10 +1771,11 @@ int rsc_pose_optimization_many(rsc_context* C, const rsc_poseopt_problem* P, int
     }
     RSC_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, C->stream));
     timing_begin(C, 3);
-    RSC_HIP(launch_poseopt(R, reinterpret_cast<const DevPoseProb*>(d + o_probs), C->stream));
+    RSC_HIP(launch_poseopt(R, reinterpret_cast<const DevPoseProb*>(d + o_probs), C->h_flag + kFaultWord, C->stream));
     timing_begin(C, 4);
     RSC_HIP(hipMemcpyAsync(C->h_po_res.p, C->d_po_res.p, res_bytes, hipMemcpyDeviceToHost, C->stream));
     RSC_HIP(hipStreamSynchronize(C->stream));
+    if (int e = take_fault(C)) return e;
     if (C->timing) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, C->ev[3], C->ev[4]);
@@ -2595,6 +2600,14 @@ int rsc_diag_poseopt_phases(rsc_context* C, uint64_t* out, int cap) {
     RSC_HIP(hipSetDevice(C->device));
     RSC_HIP(hipStreamSynchronize(C->stream));
     RSC_HIP(read_poseopt_phases(out, cap >= 64 * 24));
+    return RSC_OK;
+}
+
+int rsc_diag_sim3opt_phases(rsc_context* C, uint64_t* out, int cap) {
+    if (!C || !out || cap < 64 * 8) return RSC_ERR_ARG;
+    RSC_HIP(hipSetDevice(C->device));
+    RSC_HIP(hipStreamSynchronize(C->stream));
+    RSC_HIP(read_sim3opt_phases(out));
     return RSC_OK;
 }
 

@@ -513,9 +513,111 @@ RSC_HD bool po_ldlt_solve(double (&A)[n][n], const double (&b)[n], double (&x)[n
 
 RSC_HD bool po_ldlt_solve6(double (&A)[6][6], const double (&b)[6], double (&x)[6]) { return po_ldlt_solve<6>(A, b, x); }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// po_ldlt_solve with the matrix distributed one ROW PER LANE (lane r < n holds row r of the full
+// symmetric matrix in VGPRs; lanes >= n mirror row n - 1 and are never read).  Same operations on
+// the same operands, so the same bits: the pivot search reads the diagonal with v_readlane; the
+// symmetric transposition of k and big is the permutation P A P of the full storage — rows k and big
+// exchanged across lanes, columns k and big inside every lane — which equals Eigen's four-step
+// lower-triangle exchange because the trailing block (rows and columns >= k) is never written before
+// its own step and so is still symmetric; a step's column update and division run on the n - k
+// lanes at once (one IEEE division per lane instead of n - k in sequence).  The solve reads L and D
+// back with v_readlane and runs wave-uniformly as po_ldlt_solve's.  `row` = this lane's row of
+// H (lambda added to its diagonal by the caller), `b` wave-uniform.  Every lane of the wave must
+// call it (wave-uniform control).
+template <int n>
+__device__ bool po_ldlt_solve_lanes(const double (&row)[n], const double (&b)[n], double (&x)[n]) {
+    const int lane = (int)(threadIdx.x & 63);
+    double a[n];
+    RSC_UNROLL for (int c = 0; c < n; ++c) a[c] = row[c];
+    int sign = 0;
+    int tr[n];
+    bool stop = false;
+    RSC_UNROLL for (int k = 0; k < n; ++k) {
+        tr[k] = k;
+        if (!stop) {
+            int big = k;
+            double bv = rabs(lane_read(a[k], k));
+            RSC_UNROLL for (int i = k + 1; i < n; ++i) {
+                const double d = rabs(lane_read(a[i], i));
+                if (d > bv) { bv = d; big = i; }
+            }
+            big = po_uniform(big);
+            tr[k] = big;
+            if (big != k) {
+                RSC_UNROLL for (int c = 0; c < n; ++c) {  // rows k and big
+                    const double vb = lane_read(a[c], big), vk = lane_read(a[c], k);
+                    a[c] = (lane == k) ? vb : ((lane == big) ? vk : a[c]);
+                }
+                RSC_UNROLL for (int c = k + 1; c < n; ++c)  // columns k and big
+                    if (c == big) rswap(a[k], a[c]);
+            }
+            if (k > 0) {
+                double temp[n];
+                RSC_UNROLL for (int j = 0; j < k; ++j) temp[j] = lane_read(a[j], j) * lane_read(a[j], k);
+                double acc = a[0] * temp[0];
+                RSC_UNROLL for (int j = 1; j < k; ++j) acc = acc + a[j] * temp[j];
+                if (lane >= k) a[k] -= acc;  // A[k][k] on lane k, A[r][k] on lanes r > k
+            }
+            const double akk = lane_read(a[k], k);
+            const bool valid = po_uniform(rabs(akk) > 0.0);
+            if (k == 0 && !valid) {
+                sign = 0;
+                stop = true;
+                tr[0] = 0;
+            } else {
+                if (valid && lane > k) a[k] /= akk;
+                if (sign == 1) {
+                    if (akk < 0.0) sign = 3;
+                } else if (sign == 2) {
+                    if (akk > 0.0) sign = 3;
+                } else if (sign == 0) {
+                    if (akk > 0.0) sign = 1;
+                    else if (akk < 0.0) sign = 2;
+                }
+            }
+        }
+    }
+    if (!(sign == 1 || sign == 0)) return false;
+    double L[n][n];  // the factor read back, wave-uniform (lower triangle and diagonal)
+    RSC_UNROLL for (int i = 0; i < n; ++i)
+        RSC_UNROLL for (int j = 0; j <= i; ++j) L[i][j] = lane_read(a[j], i);
+    double y[n];
+    RSC_UNROLL for (int i = 0; i < n; ++i) y[i] = b[i];
+    RSC_UNROLL for (int k = 0; k < n; ++k)
+        RSC_UNROLL for (int j = k + 1; j < n; ++j)
+            if (tr[k] == j) rswap(y[k], y[j]);
+    RSC_UNROLL for (int i = 1; i < n; ++i) {
+        double acc = L[i][0] * y[0];
+        RSC_UNROLL for (int j = 1; j < i; ++j) acc = acc + L[i][j] * y[j];
+        y[i] -= acc;
+    }
+    const double tol = lim<double>::min();
+    RSC_UNROLL for (int i = 0; i < n; ++i) y[i] = (rabs(L[i][i]) > tol) ? y[i] / L[i][i] : 0.0;
+    RSC_UNROLL for (int i = n - 2; i >= 0; --i) {
+        double acc = L[i + 1][i] * y[i + 1];
+        RSC_UNROLL for (int j = i + 2; j < n; ++j) acc = acc + L[j][i] * y[j];
+        y[i] -= acc;
+    }
+    RSC_UNROLL for (int k = n - 1; k >= 0; --k)
+        RSC_UNROLL for (int j = k + 1; j < n; ++j)
+            if (tr[k] == j) rswap(y[k], y[j]);
+    RSC_UNROLL for (int i = 0; i < n; ++i) x[i] = y[i];
+    return true;
+}
+#elif defined(__HIPCC__)
+// host pass of a .hip file: declared for the kernels' parse, defined for the device only
+template <int n>
+__device__ bool po_ldlt_solve_lanes(const double (&row)[n], const double (&b)[n], double (&x)[n]);
+#endif
+
 #if defined(__HIPCC__)
 hipError_t read_poseopt_phases(uint64_t* out, bool wide);  // diagnostic, [64][8] or [64][24] (poseopt.hip)
-hipError_t launch_poseopt(int count, const DevPoseProb* probs, hipStream_t st);
+// rsc_selftest_math fn 16: record r = x[42 r ..] holds a 6 x 6 matrix (row-major, symmetric) and b[6];
+// out[42 r + 0..5] / [6] = po_ldlt_solve's x / ok, [7..12] / [13] = po_ldlt_solve_lanes' (one wave per record)
+hipError_t launch_selftest_ldlt(const double* x, int nrec, double* out, hipStream_t st);
+// fault: the launch's fault word (pinned host memory; raised when a streamed pass's hand-off wait gives up)
+hipError_t launch_poseopt(int count, const DevPoseProb* probs, unsigned* fault, hipStream_t st);
 #endif
 
 }  // namespace rsc

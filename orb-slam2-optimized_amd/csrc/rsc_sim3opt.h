@@ -192,6 +192,7 @@ RSC_HD void so_quad_terms(const SoPerturbed& P, bool inverse, const SoCam& K, co
 
 #if defined(__HIPCC__)
 hipError_t launch_sim3opt(int count, const DevSim3OptProb* probs, hipStream_t st);
+hipError_t read_sim3opt_phases(uint64_t* out);  // diagnostic, [64][8] (sim3opt.hip)
 #endif
 
 }  // namespace rsc

@@ -23,6 +23,19 @@ namespace rsc {
 
 namespace {
 
+// Diagnostic phase clocks (rsc_diag_sim3opt_phases) only with RSC_SO_PHASES=1 (an outstanding
+// s_memrealtime turns the folds' LDS waits into full lgkmcnt(0) waits).
+#ifndef RSC_SO_PHASES
+#define RSC_SO_PHASES 0
+#endif
+constexpr bool kSoPhases = RSC_SO_PHASES;
+// the LM trials' LDLT with one matrix row per lane (rsc_poseopt.h po_ldlt_solve_lanes; measured
+// slower, poseopt.hip): off
+#ifndef RSC_LM_LDLT_LANES
+#define RSC_LM_LDLT_LANES 0
+#endif
+
+
 // Pass form, as poseopt.hip's: 1 (wide) = 512 threads, wave 0 folds, the wave sharing its SIMD
 // (RSC_SO_IDLE) idles in the passes, six waves evaluate 384 edges per slab into a single buffer;
 // 0 = 256 threads, three edge waves, double-buffered slabs of 192.
@@ -82,6 +95,7 @@ struct SoCtx {
     int* cnt;            // scan / count scratch
     SoCam K1, K2;
     double delta, dsqr, th2;
+    uint64_t* clk;       // [8] phase clocks (RSC_SO_PHASES): written by threads 0 and 64 only
 };
 
 // Inputs of one edge (side 0: e12 of correspondence c, side 1: e21), loaded a slab ahead.
@@ -151,19 +165,25 @@ __device__ void so_build_perturbed(const SoCtx& C, const SoSim3& S) {
 // The folded sums are left in C.red (H lower triangle row-major, b, chi2); C.red is next written at
 // the end of the next pass, so they can be read until then.
 __device__ double so_pass(const SoCtx& C, int mk, const SoSim3& S) {
-    so_build_perturbed(C, S);
     const int tid = threadIdx.x, me = 2 * mk;
     const int nslab = (me + kSoSlab - 1) / kSoSlab;
     const int j = so_slot(tid);
-    const SoSim3 Si = so_inverse(S);
+    // the first slab's inputs are loaded before the perturbed estimates are built, so their global
+    // round trip overlaps that build instead of delaying the first slab
     SoEdgeIn nx{};
     if (j >= 0 && j < me) nx = so_load_edge(C, j);
+    const bool clk0 = kSoPhases && blockIdx.x < 64 && tid == 0, clk1 = kSoPhases && blockIdx.x < 64 && tid == 64;
+    const uint64_t tp0 = clk0 ? wall_clock64() : 0;
+    so_build_perturbed(C, S);
+    if (clk0) C.clk[2] += wall_clock64() - tp0;  // [2] perturbed estimates (incl. the barrier)
+    const SoSim3 Si = so_inverse(S);
     double acc = 0.0;
     for (int k = 0; k <= nslab; ++k) {
         double t[kSim3OptTerms], tc = 0.0;
         if (j >= 0 && k < nslab) {
             const int pos = k * kSoSlab + j;
             if (pos < me) {
+                const uint64_t c0 = clk1 ? wall_clock64() : 0;
                 const SoEdgeIn in = nx;
                 if (pos + kSoSlab < me) nx = so_load_edge(C, pos + kSoSlab);
                 const bool inv_edge = in.side == 1;
@@ -181,6 +201,11 @@ __device__ double so_pass(const SoCtx& C, int mk, const SoSim3& S) {
                 asm volatile("" : "+v"(z));
                 const SoPerturbed* pt = C.pt + z;
                 so_quad_terms(*pt, inv_edge, K, X, u, v, inv, e0, e1, C.delta, C.dsqr, t);
+                if (clk1) {  // [4] / [5] wave 1's edge evaluation per slab
+                    __builtin_amdgcn_sched_barrier(0);
+                    C.clk[4] += wall_clock64() - c0 + (uint64_t)(t[0] != t[0]);
+                    C.clk[5] += 1;
+                }
             } else {
                 // padding of the last slab: +0.0 terms are exact identities of these folds (an
                 // accumulator that starts at +0.0 never becomes -0.0 under round-to-nearest)
@@ -192,7 +217,12 @@ __device__ double so_pass(const SoCtx& C, int mk, const SoSim3& S) {
                 buf[kSim3OptTerms * kSoCol] = tc;
             }
         } else if (k > 0 && tid < kSoCols) {
+            const uint64_t f0 = clk0 ? wall_clock64() : 0;
             acc = fold_fixed<kSoSlab>(acc, C.terms + (kSoWide ? 0 : ((k - 1) & 1) * kSoBuf) + tid * kSoCol);
+            if (clk0) {  // [6] wave 0's folds
+                __builtin_amdgcn_sched_barrier(0);
+                C.clk[6] += wall_clock64() - f0 + (uint64_t)(acc != acc);
+            }
         }
         __syncthreads();
         if constexpr (kSoWide) {
@@ -209,6 +239,10 @@ __device__ double so_pass(const SoCtx& C, int mk, const SoSim3& S) {
     }
     if (tid < kSoCols) C.red[tid] = acc;
     __syncthreads();
+    if (clk0) {  // [0] / [1] whole passes
+        C.clk[0] += wall_clock64() - tp0;
+        C.clk[1] += 1;
+    }
     return C.red[kSim3OptTerms];
 }
 
@@ -251,18 +285,30 @@ __device__ void so_optimize(const SoCtx& C, SoLM& L, SoSim3& S, int iterations) 
         int qmax = 0;
         do {
             L.trials++;
-            double Hd[7][7];
-            double b[7];
-            RSC_UNROLL for (int r = 0; r < 7; ++r) {
+            const bool sclk = kSoPhases && blockIdx.x < 64 && threadIdx.x == 0;
+            const uint64_t ts = sclk ? wall_clock64() : 0;
+            double b[7], xs[7];
+            RSC_UNROLL for (int r = 0; r < 7; ++r) b[r] = C.cur[28 + r];
+            bool ok2;
+            if constexpr (RSC_LM_LDLT_LANES) {
+                // this lane's row of H + lambda I (rows 0..6 on lanes 0..6; rsc_poseopt.h)
+                const int lr = min((int)(threadIdx.x & 63), 6);
+                double row[7];
                 RSC_UNROLL for (int c = 0; c < 7; ++c)
-                    Hd[r][c] = r >= c ? C.cur[r * (r + 1) / 2 + c] : C.cur[c * (c + 1) / 2 + r];
-                b[r] = C.cur[28 + r];
+                    row[c] = lr >= c ? C.cur[lr * (lr + 1) / 2 + c] : C.cur[c * (c + 1) / 2 + lr];
+                RSC_UNROLL for (int c = 0; c < 7; ++c) row[c] = (c == lr) ? row[c] + L.lambda : row[c];
+                ok2 = po_ldlt_solve_lanes<7>(row, b, xs);
+            } else {
+                double Hd[7][7];
+                RSC_UNROLL for (int r = 0; r < 7; ++r)
+                    RSC_UNROLL for (int c = 0; c < 7; ++c)
+                        Hd[r][c] = r >= c ? C.cur[r * (r + 1) / 2 + c] : C.cur[c * (c + 1) / 2 + r];
+                RSC_UNROLL for (int r = 0; r < 7; ++r) Hd[r][r] += L.lambda;
+                ok2 = po_ldlt_solve<7>(Hd, b, xs);
             }
-            RSC_UNROLL for (int r = 0; r < 7; ++r) Hd[r][r] += L.lambda;
-            double xs[7];
-            const bool ok2 = po_ldlt_solve<7>(Hd, b, xs);
             if (ok2) RSC_UNROLL for (int j = 0; j < 7; ++j) L.x[j] = xs[j];
             const SoSim3 trial = so_oplus(L.x, S);
+            if (sclk) C.clk[3] += wall_clock64() - ts + (uint64_t)(trial.t[0] != trial.t[0]);  // [3] LM solves
             const double chiT = so_pass(C, mk, trial);
             L.last = trial;
             const double tempChi = ok2 ? chiT : DBL_MAX;
@@ -319,17 +365,25 @@ __device__ void so_write(const DevSim3OptProb& P, const SoSim3& S, int nIn, int 
 
 }  // namespace
 
+// Diagnostic phase clocks of the last launch (RSC_SO_PHASES=1; wall clock, 100 MHz ticks), pairs
+// 0..63: [0] passes, [1] pass count, [2] perturbed-estimate builds, [3] LM solves (LDLT + oplus),
+// [4] / [5] wave 1's edge evaluation time / slabs, [6] wave 0's folds, [7] whole kernel.
+__device__ uint64_t g_so_phase[64][8];
+
 __global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptProb* __restrict__ probs) {
     extern __shared__ __attribute__((aligned(16))) double so_lds[];
     __shared__ double red_sh[kSoCols];
     __shared__ double cur_sh[kSim3OptTerms];
     __shared__ int cnt_sh[kSoThreads / 64];
     __shared__ int tot_sh;
+    __shared__ uint64_t clk_sh[8];
     const DevSim3OptProb& P = probs[blockIdx.x];
     const int tid = threadIdx.x;
     SoPerturbed* pt = reinterpret_cast<SoPerturbed*>(so_lds + kSoBufs * kSoBuf);
     uint16_t* list = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(pt) + kSoPt);
-    SoCtx C{P, so_lds, pt, list, red_sh, cur_sh, cnt_sh, {}, {}, 0.0, 0.0, (double)P.th2};
+    SoCtx C{P, so_lds, pt, list, red_sh, cur_sh, cnt_sh, {}, {}, 0.0, 0.0, (double)P.th2, clk_sh};
+    if (kSoPhases && tid < 8) clk_sh[tid] = 0;
+    const uint64_t t_start = kSoPhases ? wall_clock64() : 0;
     C.K1 = SoCam{(double)P.K1[0], (double)P.K1[1], (double)P.K1[2], (double)P.K1[3]};
     C.K2 = SoCam{(double)P.K2[0], (double)P.K2[1], (double)P.K2[2], (double)P.K2[3]};
     C.delta = P.delta;
@@ -374,6 +428,16 @@ __global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptPro
     if (in) atomicAdd(&tot_sh, in);
     __syncthreads();
     if (tid == 0) so_write(P, S, tot_sh, nBad, L);
+    if (kSoPhases && blockIdx.x < 64) {
+        __syncthreads();
+        if (tid == 0) clk_sh[7] = wall_clock64() - t_start;  // [7] whole kernel
+        __syncthreads();
+        if (tid < 8) g_so_phase[blockIdx.x][tid] = clk_sh[tid];
+    }
+}
+
+hipError_t read_sim3opt_phases(uint64_t* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_so_phase), sizeof(uint64_t) * 64 * 8, 0, hipMemcpyDeviceToHost);
 }
 
 hipError_t launch_sim3opt(int count, const DevSim3OptProb* probs, hipStream_t st) {

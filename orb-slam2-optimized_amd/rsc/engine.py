@@ -44,7 +44,7 @@ EXPORTED = [
     "rsc_mlpnp_reset_many", "rsc_mlpnp_get_state", "rsc_mlpnp_last_poses", "rsc_mlpnp_last_samples",
     "rsc_reloc_events", "rsc_loop_events", "rsc_pose_optimization_many",
     "rsc_bow_create", "rsc_bow_destroy", "rsc_bow_set_valid", "rsc_search_by_bow_frame_many",
-    "rsc_search_by_bow_kf_many", "rsc_diag_bow_phase_stamps", "rsc_diag_refine_phase_stamps", "rsc_diag_solve_phase_stamps", "rsc_diag_poseopt_phases", "rsc_diag_kfdb_stamps",
+    "rsc_search_by_bow_kf_many", "rsc_diag_bow_phase_stamps", "rsc_diag_refine_phase_stamps", "rsc_diag_solve_phase_stamps", "rsc_diag_poseopt_phases", "rsc_diag_sim3opt_phases", "rsc_diag_kfdb_stamps",
     "rsc_search_by_sim3_many", "rsc_kfview_create", "rsc_kfview_destroy",
     "rsc_optimize_sim3_many",
     "rsc_kfdb_create", "rsc_kfdb_destroy", "rsc_kfdb_add", "rsc_kfdb_erase", "rsc_kfdb_release", "rsc_kfdb_clear",
@@ -435,6 +435,7 @@ def load_library(path: str = LIB_PATH):
     L.rsc_diag_mlpnp_phase_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"),
                                               C.c_int]
     L.rsc_diag_poseopt_phases.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"), C.c_int]
+    L.rsc_diag_sim3opt_phases.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"), C.c_int]
     L.rsc_diag_kfdb_stamps.argtypes = [vp, np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS"), C.c_int]
     f32p_ = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
     L.rsc_kfview_create.argtypes = [vp, C.POINTER(Sim3KFStruct), C.POINTER(vp)]
@@ -506,7 +507,8 @@ class Context:
         _check(load_library().rsc_context_set_eig_split(self.h, int(bool(on))), "set_eig_split")
 
     MATH_FNS = {"sin": 0, "cos": 1, "acos": 2, "cbrt": 3, "log": 4, "logf": 5, "sqrt_unit": 6, "recip_unit": 7,
-                "givens_c": 8, "givens_s": 9, "qr_solve": 10, "pow_1_3": 11, "pow_3_2": 12, "rcp_scan": 13}
+                "givens_c": 8, "givens_s": 9, "qr_solve": 10, "pow_1_3": 11, "pow_3_2": 12, "rcp_scan": 13,
+                "ldlt_lanes": 16}
 
     def selftest_math(self, fn: str, x):
         """rsc_math.h evaluated on the GPU (f64 array in, f64 array out; logf: float in/out)."""

@@ -149,3 +149,48 @@ def test_scan_reciprocal_is_ieee_in_its_range():
     ref = np.float32(1.0) / z
     bad = np.flatnonzero(dev.view(np.uint32) != ref.view(np.uint32))
     assert bad.size == 0, (bad.size, z[bad[:5]], dev[bad[:5]], ref[bad[:5]])
+
+
+def test_ldlt_row_per_lane_matches_scalar():
+    """The LM steps' LDLT (rsc_poseopt.h): the row-per-lane form the PoseOptimization / OptimizeSim3
+    kernels run equals the scalar restatement bit for bit — solution and isPositive() — on SPD systems
+    like H + lambda I, on matrices whose pivoting exchanges rows, with ties on the diagonal, indefinite
+    and singular ones (zero first pivot: Eigen's early stop) and non-finite entries."""
+    rng = np.random.default_rng(1616)
+    recs = []
+    for t in range(3000):
+        kind = t % 6
+        if kind == 0:      # SPD, LM-like scales
+            J = rng.standard_normal((12, 6)) * 10.0 ** rng.uniform(-3, 3, 6)
+            A = J.T @ J + np.eye(6) * 10.0 ** rng.uniform(-6, 2)
+        elif kind == 1:    # random symmetric (indefinite)
+            M = rng.standard_normal((6, 6))
+            A = M + M.T
+        elif kind == 2:    # diagonal ties
+            M = rng.standard_normal((6, 6)) * 0.1
+            A = M + M.T + np.diag(np.repeat(rng.uniform(1, 3), 6))
+        elif kind == 3:    # singular / zero pivot
+            M = rng.standard_normal((6, 3))
+            A = M @ M.T
+            A[:, rng.integers(6)] = 0.0
+            A[rng.integers(6), :] = 0.0
+            A = 0.5 * (A + A.T)
+            if t % 12 == 3:
+                A[:] = 0.0
+        elif kind == 4:    # large dynamic range
+            d = 10.0 ** rng.uniform(-150, 150, 6)
+            A = np.diag(d) + np.outer(d, d) ** 0.5 * 1e-3
+        else:              # non-finite entries
+            M = rng.standard_normal((6, 6))
+            A = M + M.T
+            i, j = rng.integers(6, size=2)
+            A[i, j] = A[j, i] = [np.inf, np.nan, -np.inf][t % 3]
+        b = rng.standard_normal(6) * 10.0 ** rng.uniform(-3, 3)
+        recs.append(np.concatenate([A.reshape(-1), b]))
+    x = np.concatenate(recs)
+    out = gpu_ctx().selftest_math("ldlt_lanes", x).reshape(-1, 42)
+    assert np.array_equal(out[:, 6], out[:, 13])
+    ok = out[:, 6] == 1.0
+    assert ok.sum() > 1000 and (~ok).sum() > 100
+    same = _same_bits(out[ok, 0:6], out[ok, 7:13]).all(axis=1)
+    assert same.all(), np.flatnonzero(ok)[~same][:8]

@@ -21,7 +21,7 @@ for sf in (0.8, 0.0):
     ph = np.zeros(64 * 24, np.uint64)
     engine._check(engine.load_library().rsc_diag_poseopt_phases(ctx.h, ph, ph.size), "poseopt phases")
     hw = ph.reshape(64, 24)[:, 8:16].astype(np.int64)
-    fold = ph.reshape(64, 24)[:, 16:19].astype(np.float64)
+    fold = ph.reshape(64, 24)[:, 16:22].astype(np.float64)
     ph = ph.reshape(64, 24)[:, :8].astype(np.float64)
     npass = (ph[:, 1].astype(np.uint64) & np.uint64(0xFFFFFF)).astype(np.float64)
     summ = (ph[:, 1].astype(np.uint64) >> np.uint64(24)).astype(np.float64)
@@ -53,6 +53,9 @@ for sf in (0.8, 0.0):
         print(f"    wave-0 folds: {(fold[:, 0] / fold[:, 1]).mean() * 10:.0f} ns per fold of a slab, "
               f"{fold[:, 0].mean() / 100:.1f} us per frame ({fold[:, 1].mean():.0f} folds); LDLT part of the LM "
               f"solves {fold[:, 2].mean() / 100:.1f} us per frame")
+        if fold[:, 3].any() or fold[:, 5].any():
+            print(f"    streamed pass: fold waits {fold[:, 3].mean() / 100:.1f} us per frame, wave-1 slot waits "
+                  f"{fold[:, 4].mean() / 100:.1f} us, pass start -> first slab in {fold[:, 5].mean() / 100:.1f} us")
     nsl = ph[:, 7] * 100.0  # slab count (undo the us scaling)
     if nsl.any():
         print(f"    wave-1 slab phases: to the errors {(ph[:, 5] / nsl).mean() * 1e3:.0f} ns, errors -> terms stored "
