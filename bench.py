@@ -745,6 +745,100 @@ def run_latency(engine, ctx, args, with_cpu, reps=50):
                                        sample=f"the same event, 3 warm-up + median of {n}, oracle replay, 1 thread")
             sec["speedup_vs_cpu_1core"] = round(med / float(np.median(times)), 2)
         out[kind] = sec
+    out.update(run_latency_gated(engine, ctx, with_cpu, reps))
+    return out
+
+
+def run_latency_gated(engine, ctx, with_cpu, reps=50):
+    """Single-event latency of the GATED events (rsc_reloc_events_gated / rsc_loop_events_gated): the
+    RANSAC round-robin plus the reference's acceptance test on the device — PoseOptimization after
+    every success (Tracking.cpp:1268-1331) / SearchBySim3 + OptimizeSim3 with nInliers >= 20
+    (LoopClosing.cpp:268-329) — one call per event, result on the host, median over reps calls.  The
+    events are built so the first success is rejected by its gate (a candidate with wrong stereo
+    matches / keypoints off their MapPoints), as in tests/test_gpu_gated.py.  CPU: the oracle replay
+    of the same gated event on one core; both must agree on status, winner, round and rejections."""
+    from rsc import events as rev
+    from rsc import synth
+    import events_oracle as eo
+    out = {}
+    keys = ("status", "winner", "round", "hypothesis", "rejected")
+    # relocalization: C = 15 candidates sized as latency_event("reloc"), the best one poisoned
+    rng = np.random.default_rng(4343)
+    C = 15
+    sizes = [int(x) for x in rng.integers(300, 901, size=C)]
+    ratios = [float(x) for x in rng.choice([0.05, 0.2, 0.6, 0.8], size=C, p=[0.5, 0.2, 0.15, 0.15])]
+    ratios[0] = 0.9
+    scenes, ur, bf = synth.make_reloc_gate_event(rng, 1000, list(zip(sizes, ratios)), (0,), 0.5)
+    seeds = [int(x) for x in rng.integers(1, 1 << 30, len(scenes))]
+    eb = engine.EventBatch([[engine.PnPSolver(ctx, sc, s) for sc, s in zip(scenes, seeds)]])
+    sd = np.array(seeds, np.uint32)
+    times = []
+    for r in range(reps + 5):
+        t0 = time.perf_counter()
+        eb.batch.reset(sd)
+        eb.batch.set_ransac_parameters(*rev.RELOC_PARAMS)
+        res, _, _ = eb.run_reloc_gated([(ur, bf)])
+        t = time.perf_counter() - t0
+        if r >= 5:
+            times.append(t)
+    g = res[0]
+    sec = dict(candidates=C, mean_corrs=float(np.mean(sizes)), status=int(g["status"]), winner=int(g["winner"]),
+               round=int(g["round"]), rejected=int(g["rejected"]), gates=int(g["gates"]),
+               gpu_ms=round(1e3 * float(np.median(times)), 4), reps=reps,
+               note="RANSAC round-robin + PoseOptimization gate on the device (status 1 match, 2 hand-off)")
+    if with_cpu:
+        o = None
+        ct = []
+        for r in range(3 + 10):
+            t0 = time.perf_counter()
+            o = eo.run_reloc_gated(scenes, seeds, ur, bf)
+            if r >= 3:
+                ct.append(time.perf_counter() - t0)
+        assert all(int(o[k]) == int(g[k]) for k in keys), ({k: int(o[k]) for k in keys}, {k: int(g[k]) for k in keys})
+        med = float(np.median(ct))
+        sec["cpu_baseline"] = dict(value=round(1e3 * med, 4), unit="ms/event", cores=1, kind="port",
+                                   sample=f"the same gated event, 3 warm-up + median of {len(ct)}, oracle replay, 1 thread")
+        sec["speedup_vs_cpu_1core"] = round(med / float(np.median(times)), 2)
+    out["reloc_gated"] = sec
+    # loop closure: 3 candidate KeyFrames, the first poisoned (its Sim3 RANSAC succeeds, OptimizeSim3 fails)
+    rng = np.random.default_rng(4444)
+    kf1, cands = synth.make_loop_gate_event(rng, [0.9, 0.85, 0.8], poisoned=(0,))
+    seeds = [int(x) for x in rng.integers(1, 1 << 30, len(cands))]
+    v1 = engine.KFView(ctx, kf1)
+    views, solvers, row = [v1], [], []
+    for (kf2, m12, pair), s in zip(cands, seeds):
+        v2 = engine.KFView(ctx, kf2)
+        views.append(v2)
+        solvers.append(engine.Sim3Solver(ctx, pair, s))
+        row.append((v1, v2, m12))
+    eb = engine.EventBatch([solvers])
+    sd = np.array(seeds, np.uint32)
+    times = []
+    for r in range(reps + 5):
+        t0 = time.perf_counter()
+        eb.batch.reset(sd)
+        eb.batch.set_ransac_parameters(*rev.LOOP_PARAMS)
+        res, _ = eb.run_loop_gated([row])
+        t = time.perf_counter() - t0
+        if r >= 5:
+            times.append(t)
+    g = res[0]
+    sec = dict(candidates=len(cands), status=int(g["status"]), winner=int(g["winner"]), round=int(g["round"]),
+               rejected=int(g["rejected"]), gpu_ms=round(1e3 * float(np.median(times)), 4), reps=reps,
+               note="Sim3 RANSAC round-robin + SearchBySim3(7.5) + OptimizeSim3(10), nInliers >= 20, on the device")
+    if with_cpu:
+        ct = []
+        for r in range(3 + 10):
+            t0 = time.perf_counter()
+            o = eo.run_loop_gated(kf1, cands, seeds)
+            if r >= 3:
+                ct.append(time.perf_counter() - t0)
+        assert all(int(o[k]) == int(g[k]) for k in keys), ({k: int(o[k]) for k in keys}, {k: int(g[k]) for k in keys})
+        med = float(np.median(ct))
+        sec["cpu_baseline"] = dict(value=round(1e3 * med, 4), unit="ms/event", cores=1, kind="port",
+                                   sample=f"the same gated event, 3 warm-up + median of {len(ct)}, oracle replay, 1 thread")
+        sec["speedup_vs_cpu_1core"] = round(med / float(np.median(times)), 2)
+    out["loop_gated"] = sec
     return out
 
 
