@@ -67,6 +67,11 @@ int rsc_context_set_eig_rows(rsc_context* ctx, int max_workgroups);
  * split form — the QR chase and the Q rotations on two waves of one SIMD (pnp_eig_split_kernel) — or
  * 0 the lane-pair form (pnp_eig_group_kernel).  Both are bit-identical. */
 int rsc_context_set_eig_split(rsc_context* ctx, int on);
+/* Form of rsc_optimize_sim3_many (no effect on results): helpers > 0 runs each pair on one master
+ * workgroup plus that many helper workgroups that evaluate the edges' numeric Jacobians in chunks
+ * (the cooperative form); 0 one workgroup per pair; -1 (default; env RSC_SO_HELPERS) as many helpers
+ * as fit one workgroup per CU, at most 7 per pair.  Bit-identical results. */
+int rsc_context_set_sim3opt_helpers(rsc_context* ctx, int helpers);
 /* Self-test of the device libm restatement (rsc_math.h, used by Sim3 angles, MLPnP, SearchBySim3):
  * out[i] = f(x[i]) computed ON THE GPU, f = 0 sin, 1 cos, 2 acos, 3 cbrt, 4 log, 5 logf
  * ((float)x[i] in, float result widened); and the eigen-solver chase's short-chain forms

@@ -155,6 +155,7 @@ int ppt_for(int n) {
 
 }  // namespace
 
+constexpr int kSoCoopCUs = 256;  // OptimizeSim3's cooperative form: workgroups per launch at most (MI355X CUs)
 constexpr int kFaultWord = 4;  // rsc_context::h_flag[4]: the split eigen stage's fault word
 
 struct rsc_context {
@@ -231,6 +232,10 @@ struct rsc_context {
     // (written by signal_kernel after the round) instead of hipStreamSynchronize's wake-up; env
     // RSC_SPIN_WAIT=0/1 (stream_wait)
     bool spin_wait = false;
+    // OptimizeSim3's helper workgroups per pair (the cooperative form; -1: as many as fit one per CU,
+    // at most 7; 0: one workgroup per pair)
+    int so_helpers = -1;
+    DevBuf<char> d_so_coop;  // the cooperative form's hand-off: polled words | publications | lists | chunks
     uint32_t* h_flag = nullptr;  // [0] stream_wait's sequence flag, [kFaultWord] the eigen stage's fault word
     uint32_t flag_seq = 0;
     std::chrono::steady_clock::time_point t_entry;
@@ -401,7 +406,7 @@ int take_fault(rsc_context* C) {
     if (__atomic_load_n(C->h_flag + kFaultWord, __ATOMIC_ACQUIRE) == 0) return 0;
     __atomic_store_n(C->h_flag + kFaultWord, 0u, __ATOMIC_RELEASE);
     g_last_error = "a device hand-off wait timed out (split_wait: eigen stage chase / row wave, or a streamed "
-                   "PoseOptimization pass); results discarded";
+                   "PoseOptimization pass, or an OptimizeSim3 chunk of the cooperative form); results discarded";
     return RSC_ERR_INTERNAL;
 }
 
@@ -1274,6 +1279,7 @@ int rsc_context_create(int device, rsc_context** out) {
     if (const char* m = std::getenv("RSC_EIG_SPLIT")) C->eig_split = std::strcmp(m, "0") != 0;
     if (const char* m = std::getenv("RSC_BETAS_HB")) C->betas_small_hb = std::min(kBetasHyps, std::max(1, std::atoi(m)));
     if (const char* m = std::getenv("RSC_SPIN_WAIT")) C->spin_wait = std::strcmp(m, "0") != 0;
+    if (const char* m = std::getenv("RSC_SO_HELPERS")) C->so_helpers = std::max(-1, std::atoi(m));
     {
         void* f = nullptr;
         RSC_HIP(hipHostMalloc(&f, 64, hipHostMallocCoherent));
@@ -1329,6 +1335,12 @@ int rsc_context_set_eig_rows(rsc_context* C, int max_workgroups) {
 int rsc_context_set_eig_split(rsc_context* C, int on) {
     if (!C) return RSC_ERR_ARG;
     C->eig_split = on != 0;
+    return RSC_OK;
+}
+
+int rsc_context_set_sim3opt_helpers(rsc_context* C, int helpers) {
+    if (!C || helpers < -1) return RSC_ERR_ARG;
+    C->so_helpers = helpers;
     return RSC_OK;
 }
 
@@ -1885,12 +1897,42 @@ int rsc_optimize_sim3_many(rsc_context* C, const rsc_sim3opt_problem* P, int cou
         std::memcpy(dp.K2, q.K2, sizeof(dp.K2));
         std::memcpy(dp.S0, q.S, sizeof(dp.S0));
     }
+    // the cooperative form: helper workgroups per pair, one workgroup per CU at most (its LDS)
+    const int rpad = (R + 7) / 8 * 8;
+    int helpers = C->so_helpers >= 0 ? C->so_helpers : std::min(7, kSoCoopCUs / rpad - 1);
+    helpers = std::max(0, helpers);
+    for (int k = 0; k < R; ++k) {
+        hp[k].cf = nullptr;
+        hp[k].cpub = hp[k].cstore = nullptr;
+        hp[k].clist = nullptr;
+    }
+    if (helpers > 0) {
+        const size_t o_pub = al(sizeof(SoCoopFlags) * R), o_list = o_pub + al(sizeof(double) * kSoCoopPub * R);
+        size_t o_store = o_list + al(sizeof(int) * M), store = 0;
+        for (int k = 0; k < R; ++k) {
+            const size_t nch = (2 * (moff[k + 1] - moff[k]) + kSoCoopChunk - 1) / kSoCoopChunk;
+            store += nch * kSoCoopJd * kSoCoopChunk;
+        }
+        if (int e = C->d_so_coop.ensure(o_store + sizeof(double) * store)) return e;
+        char* w = C->d_so_coop.p;
+        size_t so = 0;
+        for (int k = 0; k < R; ++k) {
+            DevSim3OptProb& dp = hp[k];
+            dp.cf = reinterpret_cast<SoCoopFlags*>(w) + k;
+            dp.cpub = reinterpret_cast<double*>(w + o_pub) + (size_t)kSoCoopPub * k;
+            dp.clist = reinterpret_cast<int*>(w + o_list) + moff[k];
+            dp.cstore = reinterpret_cast<double*>(w + o_store) + so;
+            so += (2 * (moff[k + 1] - moff[k]) + kSoCoopChunk - 1) / kSoCoopChunk * kSoCoopJd * kSoCoopChunk;
+        }
+    }
     RSC_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, C->stream));
+    if (helpers > 0) RSC_HIP(hipMemsetAsync(C->d_so_coop.p, 0, sizeof(SoCoopFlags) * R, C->stream));
     timing_begin(C, 3);
-    RSC_HIP(launch_sim3opt(R, reinterpret_cast<const DevSim3OptProb*>(d), C->stream));
+    RSC_HIP(launch_sim3opt(R, reinterpret_cast<const DevSim3OptProb*>(d), helpers, C->h_flag + kFaultWord, C->stream));
     timing_begin(C, 4);
     RSC_HIP(hipMemcpyAsync(C->h_so_res.p, C->d_so_res.p, res_bytes, hipMemcpyDeviceToHost, C->stream));
     RSC_HIP(hipStreamSynchronize(C->stream));
+    if (int e = take_fault(C)) return e;
     if (C->timing) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, C->ev[3], C->ev[4]);

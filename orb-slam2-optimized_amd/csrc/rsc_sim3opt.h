@@ -28,6 +28,25 @@ namespace rsc {
 constexpr int kSim3OptMaxCorr = 8192;  // correspondences per pair
 constexpr int kSim3OptTerms = 35;      // 28 lower-triangle H entries + 7 b entries
 
+// The cooperative form (sim3opt.hip, RSC_SO_COOP): per pair one master workgroup (the LM control and
+// the ordered folds) and helper workgroups that evaluate the edges' numeric Jacobians in chunks of 64
+// active edges and hand them to the master through global memory (write-through, drained, flagged).
+constexpr int kSoCoopChunk = 64;                                   // active edges per chunk
+constexpr int kSoCoopJd = 17;                                      // doubles per edge: J (14), e0, e1, inv
+constexpr int kSoCoopMaxChunks = 2 * kSim3OptMaxCorr / kSoCoopChunk;
+constexpr int kSoCoopPub = 256;                                    // doubles per pair: S, S^-1, perturbed, me
+
+// The polled words of one pair (zeroed before every launch).  Pass ids count from 1 within a launch;
+// kSoCoopDone ends the helpers.
+struct SoCoopFlags {
+    unsigned long long claim;          // (pass << 32) | next unclaimed chunk
+    unsigned pass;                     // the pass the master published last
+    unsigned pad[13];
+    unsigned ready[kSoCoopMaxChunks];  // pass id once chunk k of that pass is in the store
+};
+static_assert(sizeof(SoCoopFlags) % 16 == 0, "memset block");
+constexpr unsigned kSoCoopDone = 0xffffffffu;
+
 #if defined(__HIPCC__)
 struct DevSim3OptProb {
     const float4* e12;   // [m] (P3D2c, invSigma2 of KF1's keypoint)   — edge x1 = S12 * X2
@@ -40,6 +59,11 @@ struct DevSim3OptProb {
     double delta;        // Huber delta: (double) of the float sqrt(th2) (Optimizer.cpp:1104)
     float K1[4], K2[4];  // fx, fy, cx, cy
     double S0[8];        // g2oS12 on entry
+    // the cooperative form's per-pair hand-off (unused by the one-workgroup form)
+    SoCoopFlags* cf;     // polled words
+    double* cpub;        // [kSoCoopPub] the pass's estimate, its inverse, the perturbed estimates, me
+    int* clist;          // [m] the kept correspondences of the current optimize()
+    double* cstore;      // [ceil(2m / 64)][kSoCoopJd][64] the chunks' edge hand-offs
 };
 #endif
 
@@ -159,14 +183,11 @@ RSC_HD void so_perturb(const SoSim3& S, SoPerturbed& P) {
     }
 }
 
-// linearizeOplus (numeric, the point vertex fixed) + constructQuadraticForm (robust branch) of one
-// edge whose _error is (e0, e1): t[0..27] = lower triangle of B^T (rho1 omega) B (row-major i >= j),
-// t[28..34] = B^T omega_r added to b (omega_r = -omega * error * rho1).
-RSC_HD void so_quad_terms(const SoPerturbed& P, bool inverse, const SoCam& K, const double (&X)[3], double u,
-                          double v, double inv, double e0, double e1, double delta, double dsqr,
-                          double (&t)[kSim3OptTerms]) {
+// linearizeOplus (numeric, the point vertex fixed): central differences of the edge error over the
+// 14 perturbed estimates.
+RSC_HD void so_jacobian(const SoPerturbed& P, bool inverse, const SoCam& K, const double (&X)[3], double u, double v,
+                        double (&J)[2][7]) {
     const double scalar = 1.0 / (2 * 1e-9);
-    double J[2][7];
     RSC_UNROLL for (int d = 0; d < 7; ++d) {
         double a0, a1, b0, b1;
         so_edge_error(inverse ? P.pi[d] : P.p[d], K, X, u, v, a0, a1);
@@ -174,6 +195,13 @@ RSC_HD void so_quad_terms(const SoPerturbed& P, bool inverse, const SoCam& K, co
         J[0][d] = scalar * (a0 - b0);
         J[1][d] = scalar * (a1 - b1);
     }
+}
+
+// constructQuadraticForm (robust branch) of an edge with Jacobian J and _error (e0, e1):
+// t[0..27] = lower triangle of B^T (rho1 omega) B (row-major i >= j), t[28..34] = B^T omega_r added to
+// b (omega_r = -omega * error * rho1).
+RSC_HD void so_quad_tail(const double (&J)[2][7], double inv, double e0, double e1, double delta, double dsqr,
+                         double (&t)[kSim3OptTerms]) {
     double r0, rho1;
     po_huber(po_chi2(inv, false, e0, e1, 0.0), delta, dsqr, r0, rho1);
     double omr0 = (-inv) * e0 + (-0.0) * e1;
@@ -190,8 +218,19 @@ RSC_HD void so_quad_terms(const SoPerturbed& P, bool inverse, const SoCam& K, co
     RSC_UNROLL for (int i = 0; i < 7; ++i) t[28 + i] = J[0][i] * omr0 + J[1][i] * omr1;
 }
 
+// Both: linearizeOplus + constructQuadraticForm of one edge.
+RSC_HD void so_quad_terms(const SoPerturbed& P, bool inverse, const SoCam& K, const double (&X)[3], double u,
+                          double v, double inv, double e0, double e1, double delta, double dsqr,
+                          double (&t)[kSim3OptTerms]) {
+    double J[2][7];
+    so_jacobian(P, inverse, K, X, u, v, J);
+    so_quad_tail(J, inv, e0, e1, delta, dsqr, t);
+}
+
 #if defined(__HIPCC__)
-hipError_t launch_sim3opt(int count, const DevSim3OptProb* probs, hipStream_t st);
+// helpers = 0: one workgroup per pair; helpers > 0: the cooperative form with that many helper
+// workgroups per pair (fault: the launch's fault word, raised when a bounded hand-off wait gives up).
+hipError_t launch_sim3opt(int count, const DevSim3OptProb* probs, int helpers, unsigned* fault, hipStream_t st);
 hipError_t read_sim3opt_phases(uint64_t* out);  // diagnostic, [64][8] (sim3opt.hip)
 #endif
 

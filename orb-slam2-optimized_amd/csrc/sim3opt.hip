@@ -96,6 +96,13 @@ struct SoCtx {
     SoCam K1, K2;
     double delta, dsqr, th2;
     uint64_t* clk;       // [8] phase clocks (RSC_SO_PHASES): written by threads 0 and 64 only
+    // the cooperative form (so_pass_coop)
+    double* ring = nullptr;     // [kSoRing][kSoCols][kSoRCol] the fold's chunk ring
+    int* rf = nullptr;          // [kSoRing] chunk index + 1 whose terms fill the slot
+    int* rd = nullptr;          // [kSoRing] chunk index + 1 the fold consumed last from the slot
+    unsigned* pid = nullptr;    // the last pass id published (every lane's copy)
+    unsigned* fault = nullptr;  // the launch's fault word
+    int* cflt = nullptr;        // LDS: a wait of this workgroup gave up (later waits return at once)
 };
 
 // Inputs of one edge (side 0: e12 of correspondence c, side 1: e21), loaded a slab ahead.
@@ -246,6 +253,317 @@ __device__ double so_pass(const SoCtx& C, int mk, const SoSim3& S) {
     return C.red[kSim3OptTerms];
 }
 
+// Diagnostic phase clocks of the last launch (RSC_SO_PHASES=1; wall clock, 100 MHz ticks), pairs
+// 0..63: [0] passes, [1] pass count, [2] perturbed-estimate builds, [3] LM solves (LDLT + oplus),
+// [4] / [5] wave 1's edge evaluation time / slabs, [6] wave 0's folds, [7] whole kernel.
+__device__ uint64_t g_so_phase[64][8];
+
+// ---- The cooperative form (RSC_SO_COOP; rsc_sim3opt.h) ----
+// A pass of the one-workgroup form spends two thirds of its time evaluating the numeric Jacobians
+// (14 projections per edge) on three waves; the ordered folds need one.  Here the master workgroup
+// of a pair publishes each pass's estimate (S, S^-1 and the 14 perturbed estimates) and the helper
+// workgroups of the pair claim chunks of 64 active edges with a pass-tagged compare-and-swap (an
+// atomic add could take a chunk of the next pass), evaluate J and the error per edge and hand the 17
+// doubles per edge to the master: write-through (sc1) stores, drained (vmcnt(0)), then the chunk's
+// ready word = the pass id (sc1).  The master's waves 1..3 load the chunks in edge order (sc1 loads,
+// no stale L1), expand them into the 35 H/b terms and the chi2 term (so_quad_tail: the same
+// operations as so_quad_terms, so the same bits) into an LDS ring, and wave 0 folds the ring in
+// chunk order exactly as so_pass folds its slabs.  Progress never depends on the helpers being
+// resident: a master wave waiting for a chunk nobody claimed claims and evaluates it itself, and a
+// helper that sees no new pass within its bound just ends.  Every master wait is bounded: on give-up
+// the fault word is raised (an error status), never a silently wrong sum.
+#ifndef RSC_SO_RING
+#define RSC_SO_RING 6
+#endif
+constexpr int kSoRing = RSC_SO_RING;            // LDS ring slots (chunks)
+constexpr int kSoRCol = kSoCoopChunk + 2;       // padded column stride (doubles)
+constexpr int kSoRBuf = kSoCols * kSoRCol;      // one slot
+constexpr size_t kSoCoopLds = sizeof(double) * kSoRing * kSoRBuf + kSoPt + sizeof(uint16_t) * kSim3OptMaxCorr;
+constexpr int kSoSpin = 1 << 22;                // polls before a master wait gives up
+constexpr int kSoHelperSpin = 1 << 20;          // polls before an idle helper ends
+static_assert(kSoRing >= 3, "one slot per loader wave at least");
+static_assert((kSoRBuf * 8) % 16 == 0 && (kSoRCol * 8) % 16 == 0, "fold_fixed reads 16-byte aligned columns");
+static_assert(kSoCoopLds <= 160 * 1024 - 1024, "LDS");
+static_assert(16 + 224 + 1 <= kSoCoopPub && sizeof(SoPerturbed) == 224 * sizeof(double), "publication layout");
+
+using so_gu32 = __attribute__((address_space(1))) unsigned;
+using so_gu64 = __attribute__((address_space(1))) unsigned long long;
+using so_gi32 = __attribute__((address_space(1))) int;
+using so_gf64 = __attribute__((address_space(1))) double;
+
+__device__ __forceinline__ unsigned co_ld(const unsigned* p) {
+    return __hip_atomic_load((so_gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double co_ldd(const double* p) {
+    return __hip_atomic_load((so_gf64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void co_std(double* p, double v) {
+    __hip_atomic_store((so_gf64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void co_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// S's components in so_write's order (r.x, r.y, r.z, r.w, t, s), to the publication and back.
+__device__ __forceinline__ void so_put(double* p, const SoSim3& a) {
+    co_std(p + 0, a.r.x); co_std(p + 1, a.r.y); co_std(p + 2, a.r.z); co_std(p + 3, a.r.w);
+    co_std(p + 4, a.t[0]); co_std(p + 5, a.t[1]); co_std(p + 6, a.t[2]);
+    co_std(p + 7, a.s);
+}
+__device__ __forceinline__ SoSim3 so_from(const double* p) {
+    SoSim3 a;
+    a.r.x = p[0]; a.r.y = p[1]; a.r.z = p[2]; a.r.w = p[3];
+    a.t[0] = p[4]; a.t[1] = p[5]; a.t[2] = p[6];
+    a.s = p[7];
+    return a;
+}
+
+__device__ __forceinline__ unsigned long long co_first(unsigned long long v) {
+    return ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
+           (unsigned)__builtin_amdgcn_readfirstlane((unsigned)v);
+}
+
+// Chunk claims of a pass: the claim word is (pass << 32) | (front << 16) | back — the master's waves
+// take chunks 0, 1, ... from the front (evaluated straight into its fold ring), the helpers take
+// nch - 1, nch - 2, ... from the back (handed off through global memory; the fold reaches them
+// last, so their hand-off latency is covered).  Returns the claimed chunk or -1 when front and back
+// have met (*boundary = the first back chunk then) or the pass is over.  The loop is wave-uniform
+// (lane 0's atomics broadcast after each step): a lane-0-only retry loop lets the compiler give the
+// lanes separate loop exits, and the chunk loops around it then diverge.
+template <bool Front>
+__device__ __forceinline__ int co_claim(SoCoopFlags* cf, unsigned pid, int nch, int* boundary) {
+    so_gu64* cw = (so_gu64*)&cf->claim;
+    const bool l0 = (threadIdx.x & 63) == 0;
+    unsigned long long v = 0;
+    if (l0) v = __hip_atomic_load(cw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v = co_first(v);
+    for (;;) {
+        const int front = (int)((v >> 16) & 0xffff), back = (int)(v & 0xffff);
+        if ((unsigned)(v >> 32) != pid || front + back >= nch) {
+            if (boundary) *boundary = front;
+            return -1;
+        }
+        unsigned long long e = v;
+        if (l0)
+            __hip_atomic_compare_exchange_strong(cw, &e, v + (Front ? 0x10000ull : 1ull), __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        e = co_first(e);
+        if (e == v) return Front ? front : nch - 1 - back;
+        v = e;
+    }
+}
+
+// The hand-off of edge j * 64 + lane (< me): J (14), e0, e1, inv.
+__device__ __forceinline__ void co_eval(const DevSim3OptProb& P, const SoPerturbed* pt, const SoSim3& S,
+                                        const SoSim3& Si, const SoCam& K1, const SoCam& K2, int pos,
+                                        double (&h)[kSoCoopJd]) {
+    const int c = __hip_atomic_load((so_gi32*)(P.clist + (pos >> 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool inv_edge = (pos & 1) != 0;
+    const float4 a = so_ld(inv_edge ? P.e21 : P.e12, c), o = so_ld(P.uv, c);
+    const double X[3] = {(double)a.x, (double)a.y, (double)a.z};
+    const double u = inv_edge ? o.z : o.x, v = inv_edge ? o.w : o.y;
+    const SoCam& K = inv_edge ? K2 : K1;
+    double e0, e1, J[2][7];
+    so_edge_error(inv_edge ? Si : S, K, X, u, v, e0, e1);
+    int z = 0;  // the perturbed estimates stay in LDS (as so_pass)
+    asm volatile("" : "+v"(z));
+    so_jacobian(*(pt + z), inv_edge, K, X, u, v, J);
+    RSC_UNROLL for (int k = 0; k < 14; ++k) h[k] = J[k / 7][k % 7];
+    h[14] = e0;
+    h[15] = e1;
+    h[16] = a.w;
+}
+
+// One wave evaluates chunk j of pass pid (edge j * 64 + lane of the kept list) and hands it off.
+__device__ __forceinline__ void co_chunk(const DevSim3OptProb& P, const SoPerturbed* pt, const SoSim3& S,
+                                         const SoSim3& Si, const SoCam& K1, const SoCam& K2, int me, int j,
+                                         unsigned pid) {
+    const int lane = threadIdx.x & 63, pos = j * kSoCoopChunk + lane;
+    if (pos < me) {
+        double h[kSoCoopJd];
+        co_eval(P, pt, S, Si, K1, K2, pos, h);
+        double* dst = P.cstore + (size_t)j * kSoCoopJd * kSoCoopChunk + lane;
+        RSC_UNROLL for (int k = 0; k < kSoCoopJd; ++k) co_std(dst + k * kSoCoopChunk, h[k]);
+    }
+    co_drain();
+    if (lane == 0) __hip_atomic_store((so_gu32*)&P.cf->ready[j], pid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void co_fail(const SoCtx& C) {
+    __hip_atomic_store(C.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(C.cflt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Bounded wait for an LDS ring word to reach `need` (returns at once after a give-up of this
+// workgroup).
+__device__ __forceinline__ void co_wait_lds(const SoCtx& C, int* f, int need) {
+    int v = 0;
+    const bool ok = poll_until(
+        kSoSpin,
+        [&]() {
+            if (__hip_atomic_load(C.cflt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return need;
+            return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        },
+        []() { __builtin_amdgcn_s_sleep(1); }, [need](int x) { return x >= need; }, v);
+    if (!ok) co_fail(C);
+}
+
+// One pass at S (so_pass's contract, the cooperative form).
+__device__ double so_pass_coop(const SoCtx& C, int mk, const SoSim3& S) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, me = 2 * mk;
+    const int nch = (me + kSoCoopChunk - 1) / kSoCoopChunk;
+    SoCoopFlags* cf = C.P.cf;
+    const bool clk0 = kSoPhases && blockIdx.x < 64 && tid == 0, clk1 = kSoPhases && blockIdx.x < 64 && tid == 64;
+    const uint64_t tp0 = clk0 ? wall_clock64() : 0;
+    so_build_perturbed(C, S);
+    const SoSim3 Si = so_inverse(S);
+    const unsigned pid = ++*C.pid;
+    // publish the pass: S, S^-1, the perturbed estimates, me and the claim word; then the pass id
+    if (tid == 0) {
+        so_put(C.P.cpub, S);
+        so_put(C.P.cpub + 8, Si);
+        // the claim word before the barrier: the master's waves claim right after it
+        __hip_atomic_store((so_gu64*)&cf->claim, (unsigned long long)pid << 32, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else if (tid >= 16 && tid < 16 + 224 + 1) {
+        co_std(C.P.cpub + tid, tid < 240 ? reinterpret_cast<const double*>(C.pt)[tid - 16] : (double)me);
+    }
+    if (tid < kSoRing) {
+        C.rf[tid] = 0;
+        C.rd[tid] = 0;
+    }
+    co_drain();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store((so_gu32*)&cf->pass, pid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t tp1 = clk0 ? wall_clock64() : 0;
+    if (clk0) C.clk[2] += tp1 - tp0;  // [2] perturbed estimates + publication
+    double acc = 0.0;
+    if (w == 0) {
+        // the folds, chunk by chunk in edge order (lanes 0..35: one accumulator each)
+        if (lane < kSoCols) {
+            for (int i = 0; i < nch; ++i) {
+                const int sl = i % kSoRing;
+                co_wait_lds(C, C.rf + sl, i + 1);
+                if (clk0 && i == 0) C.clk[4] += wall_clock64() - tp1;  // [4] publication -> first chunk in the ring
+                acc = fold_fixed<kSoCoopChunk>(acc, C.ring + sl * kSoRBuf + lane * kSoRCol);
+                // every lane's reads of the slot are done before it is handed back
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_store(C.rd + sl, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (clk0) C.clk[6] += wall_clock64() - tp1;  // [6] publication -> last fold done
+        }
+    } else {
+        // waves 1..3: front chunks, evaluated here straight into the ring, until front and back meet;
+        // then the helpers' chunks [b, nch), chunk c = b + w - 1 (mod 3), from the store into the
+        // ring, the hand-off of the wave's next chunk loaded (when it is ready) before this one is
+        // expanded
+        auto put = [&](int c, const double (&h)[kSoCoopJd]) {
+            const int pos = c * kSoCoopChunk + lane;
+            double t[kSim3OptTerms], tc = 0.0;
+            if (pos < me) {
+                double J[2][7];
+                RSC_UNROLL for (int k = 0; k < 14; ++k) J[k / 7][k % 7] = h[k];
+                const double e0 = h[14], e1 = h[15], inv = h[16];
+                double r1;
+                po_huber(po_chi2(inv, false, e0, e1, 0.0), C.delta, C.dsqr, tc, r1);
+                so_quad_tail(J, inv, e0, e1, C.delta, C.dsqr, t);
+            } else {
+                // padding of the last chunk: +0.0 terms (so_pass's argument)
+                RSC_UNROLL for (int q = 0; q < kSim3OptTerms; ++q) t[q] = 0.0;
+            }
+            const int sl = c % kSoRing;
+            if (c >= kSoRing) co_wait_lds(C, C.rd + sl, c - kSoRing + 1);
+            double* slot = C.ring + sl * kSoRBuf + lane;
+            RSC_UNROLL for (int q = 0; q < kSim3OptTerms; ++q) slot[q * kSoRCol] = t[q];
+            slot[kSim3OptTerms * kSoRCol] = tc;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(C.rf + sl, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        };
+        int b = nch;
+        for (;;) {
+            const int j = co_claim<true>(cf, pid, nch, &b);
+            if (j < 0) break;
+            double h[kSoCoopJd];
+            const int pos = j * kSoCoopChunk + lane;
+            if (pos < me) co_eval(C.P, C.pt, S, Si, C.K1, C.K2, pos, h);
+            put(j, h);
+            if (clk1) C.clk[5] += 1;  // [5] front chunks of wave 1
+        }
+        auto ready = [&](int c) { return __builtin_amdgcn_readfirstlane(co_ld(&cf->ready[c])) == pid; };
+        auto wait_ready = [&](int c) {  // the helper that claimed it is running: a bounded wait
+            int v = 0;
+            if (!poll_until(
+                    kSoSpin,
+                    [&]() {
+                        if (__hip_atomic_load(C.cflt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return 1;
+                        return ready(c) ? 1 : 0;
+                    },
+                    []() { __builtin_amdgcn_s_sleep(1); }, [](int x) { return x != 0; }, v))
+                co_fail(C);
+        };
+        auto load = [&](int c, double (&h)[kSoCoopJd]) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the loads stay after the poll
+            const double* src = C.P.cstore + (size_t)c * kSoCoopJd * kSoCoopChunk + lane;
+            RSC_UNROLL for (int k = 0; k < kSoCoopJd; ++k) h[k] = co_ldd(src + k * kSoCoopChunk);
+        };
+        double hc[kSoCoopJd];
+        bool have = false;
+        for (int i = b + w - 1; i < nch; i += 3) {
+            if (!have) {
+                wait_ready(i);
+                load(i, hc);
+            }
+            const int n = i + 3;
+            have = n < nch && ready(n);
+            double hn[kSoCoopJd];
+            load(have ? n : i, hn);  // issued either way (straight-line waits); used when have
+            put(i, hc);
+            RSC_UNROLL for (int k = 0; k < kSoCoopJd; ++k) hc[k] = hn[k];
+        }
+    }
+    __syncthreads();
+    if (tid < kSoCols) C.red[tid] = acc;
+    __syncthreads();
+    if (clk0) {  // [0] / [1] whole passes
+        C.clk[0] += wall_clock64() - tp0;
+        C.clk[1] += 1;
+    }
+    return C.red[kSim3OptTerms];
+}
+
+// A helper workgroup of pair P: every pass the master publishes, claim and evaluate chunks until
+// none is left; end at kSoCoopDone (or when no new pass comes within the bound).
+__device__ __forceinline__ void so_helper(const DevSim3OptProb& P, double* pub, unsigned* pid_sh) {
+    const int tid = threadIdx.x;
+    const SoCam K1{(double)P.K1[0], (double)P.K1[1], (double)P.K1[2], (double)P.K1[3]};
+    const SoCam K2{(double)P.K2[0], (double)P.K2[1], (double)P.K2[2], (double)P.K2[3]};
+    const SoPerturbed* pt = reinterpret_cast<const SoPerturbed*>(pub + 16);
+    unsigned last = 0;
+    for (;;) {
+        if (tid == 0) {
+            int v = 0;
+            const bool ok = poll_until(
+                kSoHelperSpin, [&]() { return (int)co_ld(&P.cf->pass); }, []() { __builtin_amdgcn_s_sleep(2); },
+                [last](int x) { return (unsigned)x != last; }, v);
+            *pid_sh = ok ? (unsigned)v : kSoCoopDone;
+        }
+        __syncthreads();
+        const unsigned pid = *pid_sh;
+        if (pid == kSoCoopDone) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (tid < 16 + 224 + 1) pub[tid] = co_ldd(P.cpub + tid);
+        __syncthreads();
+        const SoSim3 S = so_from(pub), Si = so_from(pub + 8);
+        const int me = (int)pub[240];
+        const int nch = (me + kSoCoopChunk - 1) / kSoCoopChunk;
+        for (;;) {
+            const int j = co_claim<false>(P.cf, pid, nch, nullptr);
+            if (j < 0) break;
+            co_chunk(P, pt, S, Si, K1, K2, me, j, pid);
+        }
+        __syncthreads();  // every wave is done with this pass's publication in LDS
+        last = pid;
+    }
+}
+
 struct SoLM {
     double x[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // BlockSolver::_x persists across optimize() calls
     double lambda = -1.0, ni = 2.0;
@@ -255,11 +573,22 @@ struct SoLM {
 
 // initializeOptimization() + optimize(iterations) (sparse_optimizer.cpp:354-414) with
 // OptimizationAlgorithmLevenberg::solve (optimization_algorithm_levenberg.cpp:59-151).
+template <bool Coop>
+__device__ __forceinline__ double so_pass_any(const SoCtx& C, int mk, const SoSim3& S) {
+    if constexpr (Coop) return so_pass_coop(C, mk, S);
+    else return so_pass(C, mk, S);
+}
+
+template <bool Coop>
 __device__ void so_optimize(const SoCtx& C, SoLM& L, SoSim3& S, int iterations) {
     const int mk = so_list_kept(C);
     if (mk == 0) return;
+    if constexpr (Coop) {  // the helpers read the kept list from global memory
+        for (int i = threadIdx.x; i < mk; i += kSoThreads)
+            __hip_atomic_store((so_gi32*)(C.P.clist + i), (int)C.list[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // the system at S (C.cur: lower triangle row-major, then b) and the chi2 solve() computes there
-    double chiS = so_pass(C, mk, S);
+    double chiS = so_pass_any<Coop>(C, mk, S);
     L.last = S;
     auto adopt = [&]() {  // C.cur = the last pass's system
         if (threadIdx.x < kSim3OptTerms) C.cur[threadIdx.x] = C.red[threadIdx.x];
@@ -309,7 +638,7 @@ __device__ void so_optimize(const SoCtx& C, SoLM& L, SoSim3& S, int iterations) 
             if (ok2) RSC_UNROLL for (int j = 0; j < 7; ++j) L.x[j] = xs[j];
             const SoSim3 trial = so_oplus(L.x, S);
             if (sclk) C.clk[3] += wall_clock64() - ts + (uint64_t)(trial.t[0] != trial.t[0]);  // [3] LM solves
-            const double chiT = so_pass(C, mk, trial);
+            const double chiT = so_pass_any<Coop>(C, mk, trial);
             L.last = trial;
             const double tempChi = ok2 ? chiT : DBL_MAX;
             rho = (currentChi - tempChi);
@@ -365,23 +694,45 @@ __device__ void so_write(const DevSim3OptProb& P, const SoSim3& S, int nIn, int 
 
 }  // namespace
 
-// Diagnostic phase clocks of the last launch (RSC_SO_PHASES=1; wall clock, 100 MHz ticks), pairs
-// 0..63: [0] passes, [1] pass count, [2] perturbed-estimate builds, [3] LM solves (LDLT + oplus),
-// [4] / [5] wave 1's edge evaluation time / slabs, [6] wave 0's folds, [7] whole kernel.
-__device__ uint64_t g_so_phase[64][8];
 
-__global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptProb* __restrict__ probs) {
+
+// One pair (master workgroup) or, in the cooperative form, one helper workgroup: blocks [0, npairs)
+// are the masters, blocks rpad + h * rpad + p (p < npairs) the helpers of pair p — the same block index
+// modulo 8 as the master, so the dispatch order puts them on its XCD (a speed matter only: the
+// hand-off is write-through and read past L1).
+template <bool Coop>
+__global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptProb* __restrict__ probs, int npairs,
+                                                            int rpad, unsigned* fault) {
     extern __shared__ __attribute__((aligned(16))) double so_lds[];
     __shared__ double red_sh[kSoCols];
     __shared__ double cur_sh[kSim3OptTerms];
     __shared__ int cnt_sh[kSoThreads / 64];
     __shared__ int tot_sh;
     __shared__ uint64_t clk_sh[8];
-    const DevSim3OptProb& P = probs[blockIdx.x];
+    __shared__ int rf_sh[Coop ? kSoRing : 1], rd_sh[Coop ? kSoRing : 1], cflt_sh;
+    __shared__ unsigned hpid_sh;
     const int tid = threadIdx.x;
-    SoPerturbed* pt = reinterpret_cast<SoPerturbed*>(so_lds + kSoBufs * kSoBuf);
+    if (Coop && (int)blockIdx.x >= rpad) {
+        const int p = ((int)blockIdx.x - rpad) % rpad;
+        if (p < npairs) so_helper(probs[p], so_lds, &hpid_sh);
+        return;
+    }
+    if ((int)blockIdx.x >= npairs) return;
+    const DevSim3OptProb& P = probs[blockIdx.x];
+    constexpr size_t kTermBytes = Coop ? sizeof(double) * kSoRing * kSoRBuf : sizeof(double) * kSoBufs * kSoBuf;
+    SoPerturbed* pt = reinterpret_cast<SoPerturbed*>(reinterpret_cast<unsigned char*>(so_lds) + kTermBytes);
     uint16_t* list = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(pt) + kSoPt);
+    unsigned pid = 0;
     SoCtx C{P, so_lds, pt, list, red_sh, cur_sh, cnt_sh, {}, {}, 0.0, 0.0, (double)P.th2, clk_sh};
+    if constexpr (Coop) {
+        C.ring = so_lds;
+        C.rf = rf_sh;
+        C.rd = rd_sh;
+        C.pid = &pid;
+        C.fault = fault;
+        C.cflt = &cflt_sh;
+        if (tid == 0) cflt_sh = 0;
+    }
     if (kSoPhases && tid < 8) clk_sh[tid] = 0;
     const uint64_t t_start = kSoPhases ? wall_clock64() : 0;
     C.K1 = SoCam{(double)P.K1[0], (double)P.K1[1], (double)P.K1[2], (double)P.K1[3]};
@@ -398,7 +749,13 @@ __global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptPro
     __syncthreads();
     SoLM L;
     L.last = S;
-    so_optimize(C, L, S, 5);
+    // the helpers end when this workgroup does, whichever way it returns
+    auto done = [&]() {
+        if constexpr (Coop) {
+            if (tid == 0) __hip_atomic_store((so_gu32*)&P.cf->pass, kSoCoopDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    so_optimize<Coop>(C, L, S, 5);
     // Check inliers (Optimizer.cpp:1176-1194): remove both edges of a failing correspondence
     int bad = 0;
     SoSim3 Sli = so_inverse(L.last);
@@ -414,10 +771,12 @@ __global__ __launch_bounds__(kSoThreads) void sim3opt_kernel(const DevSim3OptPro
     __syncthreads();
     if (P.m - nBad < 10) {  // return 0, g2oS12 untouched (:1201-1202)
         if (tid == 0) so_write(P, S_in, 0, nBad, L);
+        done();
         return;
     }
     if (tid == 0) tot_sh = 0;
-    so_optimize(C, L, S, nBad > 0 ? 10 : 5);
+    so_optimize<Coop>(C, L, S, nBad > 0 ? 10 : 5);
+    done();
     int in = 0;
     Sli = so_inverse(L.last);
     for (int c = tid; c < P.m; c += kSoThreads) {
@@ -440,20 +799,29 @@ hipError_t read_sim3opt_phases(uint64_t* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_so_phase), sizeof(uint64_t) * 64 * 8, 0, hipMemcpyDeviceToHost);
 }
 
-hipError_t launch_sim3opt(int count, const DevSim3OptProb* probs, hipStream_t st) {
+hipError_t launch_sim3opt(int count, const DevSim3OptProb* probs, int helpers, unsigned* fault, hipStream_t st) {
     // the dynamic-LDS size above 64 KB needs the per-device function attribute: raised lazily at
     // this kernel's first launch on each device, so only callers of this path depend on it
     static std::atomic<unsigned long long> raised{0};
     int dev = 0;
     if (hipError_t e = hipGetDevice(&dev)) return e;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (helpers < 0 || (helpers > 0 && !fault)) return hipErrorInvalidValue;
     if (!((raised.load(std::memory_order_acquire) >> dev) & 1ull)) {
-        if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sim3opt_kernel),
+        if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sim3opt_kernel<false>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSoLds))
+            return e;
+        if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sim3opt_kernel<true>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSoCoopLds))
             return e;
         raised.fetch_or(1ull << dev, std::memory_order_acq_rel);
     }
-    sim3opt_kernel<<<count, kSoThreads, kSoLds, st>>>(probs);
+    if (helpers == 0) {
+        sim3opt_kernel<false><<<count, kSoThreads, kSoLds, st>>>(probs, count, count, fault);
+    } else {
+        const int rpad = (count + 7) / 8 * 8;  // helpers share their master's block index modulo 8
+        sim3opt_kernel<true><<<rpad * (1 + helpers), kSoThreads, kSoCoopLds, st>>>(probs, count, rpad, fault);
+    }
     return hipGetLastError();
 }
 

@@ -30,7 +30,7 @@ u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
 EXPORTED = [
     "rsc_version", "rsc_status_string", "rsc_context_create", "rsc_context_destroy", "rsc_context_set_stream",
     "rsc_context_synchronize", "rsc_context_last_timing", "rsc_context_last_kernel_timing", "rsc_diag_host_timing", "rsc_context_enable_timing", "rsc_selftest_math",
-    "rsc_context_set_eig_rows", "rsc_context_set_eig_split",
+    "rsc_context_set_eig_rows", "rsc_context_set_eig_split", "rsc_context_set_sim3opt_helpers",
     "rsc_pnp_create", "rsc_pnp_destroy", "rsc_pnp_set_ransac_parameters", "rsc_pnp_iterate", "rsc_pnp_find",
     "rsc_pnp_last_inliers",
     "rsc_pnp_iterate_many", "rsc_pnp_reset", "rsc_pnp_get_state", "rsc_pnp_last_samples", "rsc_pnp_last_hypotheses",
@@ -358,6 +358,7 @@ def load_library(path: str = LIB_PATH):
     L.rsc_context_enable_timing.argtypes = [vp, C.c_int]
     L.rsc_context_set_eig_rows.argtypes = [vp, C.c_int]
     L.rsc_context_set_eig_split.argtypes = [vp, C.c_int]
+    L.rsc_context_set_sim3opt_helpers.argtypes = [vp, C.c_int]
     L.rsc_pnp_create.argtypes = [vp, C.POINTER(PnPProblem), C.c_uint32, C.POINTER(vp)]
     L.rsc_pnp_destroy.argtypes = [vp]
     L.rsc_pnp_set_ransac_parameters.argtypes = [vp, C.c_double, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float]
@@ -505,6 +506,11 @@ class Context:
         """Split-form eigen stage (chase and Q rotations on two waves) for the launches the rows form
         does not take (default on); off: the lane-pair form."""
         _check(load_library().rsc_context_set_eig_split(self.h, int(bool(on))), "set_eig_split")
+
+    def set_sim3opt_helpers(self, helpers: int):
+        """OptimizeSim3's form: helper workgroups per pair (the cooperative form), 0 = one workgroup
+        per pair, -1 = automatic (default)."""
+        _check(load_library().rsc_context_set_sim3opt_helpers(self.h, int(helpers)), "set_sim3opt_helpers")
 
     MATH_FNS = {"sin": 0, "cos": 1, "acos": 2, "cbrt": 3, "log": 4, "logf": 5, "sqrt_unit": 6, "recip_unit": 7,
                 "givens_c": 8, "givens_s": 9, "qr_solve": 10, "pow_1_3": 11, "pow_3_2": 12, "rcp_scan": 13,

@@ -1,6 +1,7 @@
 """GPU: rsc_optimize_sim3_many (Optimizer::OptimizeSim3 on the MI355X) == the oracle, bit for bit
 (nIn, g2oS12 quaternion / translation / scale bits, the NULLed vpMatches1 entries, LM iteration and
-trial counts), across sizes, outlier ratios, the < 10 rule, empty problems and a 32-pair batch."""
+trial counts), across sizes, outlier ratios, the < 10 rule, empty problems and a 32-pair batch, in
+both forms (one workgroup per pair; the cooperative form with helper workgroups, the default)."""
 import numpy as np
 import pytest
 
@@ -11,8 +12,8 @@ from rsc import engine, synth
 pytestmark = pytest.mark.gpu
 
 
-def check(problems):
-    res = engine.optimize_sim3_many(ctx(), problems)
+def check(problems, c=None):
+    res = engine.optimize_sim3_many(c or ctx(), problems)
     for k, (p, g) in enumerate(zip(problems, res)):
         r, S, keep, st = ol.optimize_sim3(p)
         assert g["n_inliers"] == r, f"pair {k}: nIn {g['n_inliers']} vs {r}"
@@ -46,3 +47,41 @@ def test_loop_closure_batch_32_pairs():
     """The bench shape: 32 KeyFrame pairs x ~1000 correspondences (config-3 pairs)."""
     rng = np.random.default_rng(93)
     check([synth.make_sim3opt_problem(rng, 1000, outlier_frac=0.25) for _ in range(32)])
+
+
+@pytest.fixture
+def form_ctx():
+    """The shared context in a given OptimizeSim3 form, restored to automatic afterwards."""
+    c = ctx()
+    yield c
+    c.set_sim3opt_helpers(-1)
+
+
+@pytest.mark.parametrize("helpers", [0, 1, 3, 7])
+def test_forms_bitexact(form_ctx, helpers):
+    """The one-workgroup form and the cooperative form at 1, 3 and 7 helpers per pair: every chunk
+    claimed by a helper or by the master, the same bits."""
+    form_ctx.set_sim3opt_helpers(helpers)
+    rng = np.random.default_rng(94 + helpers)
+    probs = [synth.make_sim3opt_problem(rng, int(rng.integers(5, 2500)), valid_frac=float(rng.uniform(0.5, 1.0)),
+                                        outlier_frac=float(rng.uniform(0.0, 0.5)), noise=True,
+                                        pose_noise=float(rng.uniform(0.0, 0.05))) for _ in range(12)]
+    check(probs, form_ctx)
+
+
+def test_cooperative_maximum_pair(form_ctx):
+    """8192 correspondences (16,384 edges, the 256-chunk maximum of the hand-off) and a single pair
+    (the loop-closure event's launch: 7 helpers), with the automatic form."""
+    rng = np.random.default_rng(98)
+    check([synth.make_sim3opt_problem(rng, 8192, outlier_frac=0.2)], form_ctx)
+    check([synth.make_sim3opt_problem(rng, 8192, outlier_frac=0.2, valid_frac=1.0),
+           synth.make_sim3opt_problem(rng, 33, outlier_frac=0.0)], form_ctx)
+
+
+def test_cooperative_many_pairs(form_ctx):
+    """72 pairs: 72 master blocks leave room for 2 helpers each; 160 pairs: none (the
+    one-workgroup form)."""
+    rng = np.random.default_rng(99)
+    check([synth.make_sim3opt_problem(rng, int(rng.integers(20, 600)), outlier_frac=0.2) for _ in range(72)], form_ctx)
+    check([synth.make_sim3opt_problem(rng, int(rng.integers(20, 200)), outlier_frac=0.2) for _ in range(160)],
+          form_ctx)
